@@ -1,0 +1,137 @@
+#!/usr/bin/env python
+"""Headline benchmark: MNIST 2-layer CNN, sync all-reduce data parallel, bf16,
+images/sec for the whole job (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Weak scaling: every rank trains --batch_size images per step (global batch =
+batch_size * N).  Synthetic MNIST-shaped data resident in HBM, random-init
+weights.  The timed region is exactly K full training steps (device-side batch
+sampling, forward, backward, RCCL gradient all-reduce, fused Adam), bracketed
+by barrier + device synchronize on both sides; the reported time is the MAX
+over ranks.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import dtfe  # noqa: E402,F401
+from dtfe.models.mnist_cnn import MnistCnnTrainer, num_params  # noqa: E402
+from dtfe.parallel.allreduce import BucketAllReduce  # noqa: E402
+from dtfe.utils.graphs import StepGraph, graphs_enabled  # noqa: E402
+
+DEFAULT_BATCH = 1024  # per GPU
+
+
+def _baseline(n_gpus, batch):
+    """Stock-PyTorch (DDP + MIOpen/hipBLASLt, bf16) images/sec measured on the same MI355X
+    box and config by bench/stock_torch_cnn.py; see BASELINE.md."""
+    p = os.path.join(ROOT, "bench", "stock_baseline.json")
+    try:
+        with open(p) as f:
+            tab = json.load(f)
+        return tab.get(f"{n_gpus}x{batch}")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch_size", type=int, default=DEFAULT_BATCH, help="per-GPU batch")
+    ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
+    ap.add_argument("--no_graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+
+    allreduce = None
+    trainer = MnistCnnTrainer(args.batch_size, device, seed=0, world_size=world)
+    if world > 1:
+        allreduce = BucketAllReduce(trainer.P.grad, trainer.buckets,
+                                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+        trainer.allreduce = allreduce
+
+    if allreduce is not None and allreduce.grad16 is not None:
+        def step():
+            trainer.forward_backward()
+            trainer.opt.step(grad16=allreduce.grad16, gscale=1.0 / world)
+    else:
+        step = trainer.step
+    # world == 1: the whole step is one hipGraph replay
+    runner = StepGraph(step, warmup=2, enabled=(world == 1 and not args.no_graph and graphs_enabled()))
+
+    for _ in range(args.warmup):
+        runner()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    loss = float(trainer.loss_sum.item()) / args.batch_size
+    global_batch = args.batch_size * world
+    value = global_batch * args.steps / elapsed
+    base = _baseline(world, args.batch_size)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node), MNIST CNN sync all-reduce",
+            "value": round(value, 1),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": "bf16",
+            "data": "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)",
+            "config": {
+                "model": "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(),
+                "global_batch": global_batch,
+                "seq_len": None,
+                "parallelism": "dp%d" % world,
+                "per_gpu_batch": args.batch_size,
+                "optimizer": "adam (TF1)",
+                "grad_allreduce": ("rccl bucketed %s" % args.comm_dtype) if world > 1 else "none (1 rank)",
+                "hip_graph": runner.graph is not None,
+                "last_loss": round(loss, 4),
+            },
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,386 @@
+// torch.ops.dtfe.* bindings for the gfx950 kernel library.
+//
+// Every op writes into caller-provided (pre-allocated) tensors and launches on
+// the current HIP stream, so a whole training step built from these ops can be
+// captured into a hipGraph (torch.cuda.CUDAGraph) with zero allocations.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <torch/library.h>
+#include <vector>
+
+#include "../kernels/conv.h"
+#include "../kernels/elementwise.h"
+#include "../kernels/gemm_dense.h"
+#include "../kernels/head.h"
+#include "../kernels/optim.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+template <typename T>
+T* ptr_or_null(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "dtfe: tensor '", name, "' must be on the GPU (HIP) device");
+}
+
+int dtype_code(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return 0;
+  if (t.scalar_type() == at::kFloat) return 1;
+  TORCH_CHECK(false, "dtfe: unsupported dtype ", t.scalar_type());
+}
+
+// ------------------------------------------------------------------- gemm
+void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t bmode, int64_t ldb, int64_t M,
+          int64_t N, int64_t K, const Tensor& out, int64_t ldc, const optional<Tensor>& bias, int64_t bias_axis,
+          int64_t act, double alpha, double beta, bool atomic, int64_t splits, int64_t tile,
+          const optional<Tensor>& aux, int64_t ld_aux, int64_t aux_act, int64_t b_ones_row, double keep, int64_t seed,
+          const optional<Tensor>& counter, const optional<Tensor>& pooled, const optional<Tensor>& argmax,
+          int64_t PH, int64_t PW, int64_t PC, const optional<Tensor>& out2, int64_t ldc2, bool out2_trans) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  check_cuda(out, "out");
+  TORCH_CHECK(A.scalar_type() == B.scalar_type(), "gemm: A and B dtypes differ");
+  const int dt = dtype_code(A);
+  dtfe::DenseGemmArgs a{};
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.A = A.data_ptr(); a.lda = lda;
+  a.B = B.data_ptr(); a.ldb = ldb;
+  a.b_ones_row = (int)b_ones_row;
+  if (splits < 1) splits = 1;
+  int chunk = (int)((K + splits - 1) / splits);
+  chunk = ((chunk + dtfe::BK - 1) / dtfe::BK) * dtfe::BK;
+  if (chunk < dtfe::BK) chunk = dtfe::BK;
+  const int real_splits = (int)((K + chunk - 1) / chunk);
+  a.k_chunk = chunk;
+  a.out = out.data_ptr(); a.ldc = ldc; a.out_f32 = out.scalar_type() == at::kFloat;
+  a.bias = ptr_or_null<float>(bias); a.bias_axis = (int)bias_axis;
+  a.act = (int)act; a.alpha = (float)alpha; a.beta = (float)beta; a.atomic = atomic;
+  TORCH_CHECK(!(real_splits > 1 && !atomic), "gemm: split-K needs atomic accumulation");
+  TORCH_CHECK(!atomic || a.out_f32, "gemm: atomic accumulation needs an fp32 output");
+  a.out2 = ptr_or_null<void>(out2); a.ldc2 = ldc2;
+  a.out2_f32 = (out2.has_value() && out2->defined()) ? out2->scalar_type() == at::kFloat : 0;
+  a.out2_trans = out2_trans;
+  a.aux = ptr_or_null<void>(aux); a.ld_aux = ld_aux;
+  a.aux_f32 = (aux.has_value() && aux->defined()) ? aux->scalar_type() == at::kFloat : 0;
+  a.aux_act = (int)aux_act;
+  a.unpool = (pooled.has_value() && pooled->defined()) ? 1 : 0;
+  if (a.unpool) {
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16, "gemm: unpool epilogue writes bf16");
+    a.up.pooled = reinterpret_cast<const dtfe::bf16*>(pooled->data_ptr());
+    a.up.argmax = reinterpret_cast<const uint8_t*>(argmax->data_ptr());
+    a.up.PH = (int)PH; a.up.PW = (int)PW; a.up.C = (int)PC;
+  }
+  a.keep = (float)keep; a.seed = (uint64_t)seed; a.counter = ptr_or_null<int64_t>(counter);
+  dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
+}
+
+// ------------------------------------------------------------------- conv
+dtfe::ConvGeom geom(int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, int64_t OH, int64_t OW, int64_t KH,
+                    int64_t KW, int64_t stride, int64_t pad, int64_t pool) {
+  dtfe::ConvGeom g;
+  g.B = (int)B; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.Cout = (int)Cout; g.OH = (int)OH; g.OW = (int)OW;
+  g.KH = (int)KH; g.KW = (int)KW; g.stride = (int)stride; g.pad = (int)pad; g.pool_order = (int)pool;
+  return g;
+}
+
+void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
+              const optional<Tensor>& argmax, int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, int64_t OH,
+              int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool pool, int64_t act) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv_fwd: bf16 only");
+  dtfe::ConvFwdArgs a{};
+  a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, pool);
+  a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
+  a.bias = ptr_or_null<float>(bias);
+  a.y = reinterpret_cast<dtfe::bf16*>(y.data_ptr());
+  a.argmax = ptr_or_null<uint8_t>(argmax);
+  a.act = (int)act;
+  dtfe::launch_conv_fwd(a, cur_stream());
+}
+
+void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B, int64_t H, int64_t W, int64_t C,
+                int64_t Cout, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                const optional<Tensor>& pooled, const optional<Tensor>& argmax) {
+  check_cuda(dy, "dy");
+  dtfe::ConvDgradArgs a{};
+  a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
+  a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
+  a.wt = reinterpret_cast<const dtfe::bf16*>(wt.data_ptr());
+  a.dx = reinterpret_cast<dtfe::bf16*>(dx.data_ptr());
+  a.unpool = (pooled.has_value() && pooled->defined()) ? 1 : 0;
+  if (a.unpool) {
+    a.up.pooled = reinterpret_cast<const dtfe::bf16*>(pooled->data_ptr());
+    a.up.argmax = reinterpret_cast<const uint8_t*>(argmax->data_ptr());
+    a.up.PH = (int)H; a.up.PW = (int)W; a.up.C = (int)C;
+  }
+  dtfe::launch_conv_dgrad(a, cur_stream());
+}
+
+void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t H,
+                int64_t W, int64_t C, int64_t Cout, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t stride,
+                int64_t pad, double scale) {
+  check_cuda(dz, "dz");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat, "conv_wgrad: fp32 grad buffer");
+  dtfe::ConvWgradArgs a{};
+  a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
+  a.dz = reinterpret_cast<const dtfe::bf16*>(dz.data_ptr());
+  a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  a.dw = dw.data_ptr<float>();
+  a.db = ptr_or_null<float>(db);
+  a.scale = (float)scale;
+  dtfe::launch_conv_wgrad(a, cur_stream());
+}
+
+// ------------------------------------------------------------------- head
+void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, const Tensor& labels, const Tensor& dz,
+               const Tensor& dw, const optional<Tensor>& db, const optional<Tensor>& dbh,
+               const optional<Tensor>& loss_sum, const optional<Tensor>& correct, const optional<Tensor>& logits,
+               double scale, double inv_keep) {
+  check_cuda(h, "h");
+  dtfe::HeadArgs a{};
+  a.B = (int)h.size(0); a.K = (int)h.size(1); a.NC = (int)(w.numel() / a.K);
+  a.h = reinterpret_cast<const dtfe::bf16*>(h.data_ptr());
+  a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
+  a.b = ptr_or_null<float>(b);
+  a.labels = labels.data_ptr<int32_t>();
+  a.scale = (float)scale; a.inv_keep = (float)inv_keep;
+  a.dz = reinterpret_cast<dtfe::bf16*>(dz.data_ptr());
+  a.dw = dw.data_ptr<float>();
+  a.db = ptr_or_null<float>(db); a.dbh = ptr_or_null<float>(dbh);
+  a.loss_sum = ptr_or_null<float>(loss_sum); a.correct = ptr_or_null<int32_t>(correct);
+  a.logits_out = ptr_or_null<float>(logits);
+  dtfe::launch_head_xent(a, cur_stream());
+}
+
+// -------------------------------------------------------------- optimizer
+// segs: int64 [nseg, 6] = (off, R, T, C, w16_ptr, wt16_ptr)
+// work: int64 [nwork, 7] = (kind, seg, t, r0, c0, start, count)
+// returns a device blob holding both struct arrays
+Tensor opt_pack(const Tensor& segs, const Tensor& work, const Tensor& device_like) {
+  TORCH_CHECK(segs.device().is_cpu() && work.device().is_cpu(), "opt_pack: CPU int64 tables");
+  auto S = segs.contiguous(), Wk = work.contiguous();
+  const int64_t ns = S.size(0), nw = Wk.size(0);
+  std::vector<dtfe::OptSeg> vs(ns);
+  std::vector<dtfe::OptWork> vw(nw);
+  const int64_t* s = S.data_ptr<int64_t>();
+  const int64_t* w = Wk.data_ptr<int64_t>();
+  for (int64_t i = 0; i < ns; ++i) {
+    vs[i].off = s[i * 6 + 0];
+    vs[i].R = (int)s[i * 6 + 1]; vs[i].T = (int)s[i * 6 + 2]; vs[i].C = (int)s[i * 6 + 3];
+    vs[i].w16 = reinterpret_cast<dtfe::bf16*>(s[i * 6 + 4]);
+    vs[i].wt16 = reinterpret_cast<dtfe::bf16*>(s[i * 6 + 5]);
+  }
+  for (int64_t i = 0; i < nw; ++i) {
+    vw[i].kind = (int)w[i * 7 + 0]; vw[i].seg = (int)w[i * 7 + 1]; vw[i].t = (int)w[i * 7 + 2];
+    vw[i].r0 = (int)w[i * 7 + 3]; vw[i].c0 = (int)w[i * 7 + 4];
+    vw[i].start = w[i * 7 + 5]; vw[i].count = w[i * 7 + 6];
+  }
+  const size_t bs = ns * sizeof(dtfe::OptSeg), bw = nw * sizeof(dtfe::OptWork);
+  const size_t off_w = (bs + 255) / 256 * 256;
+  Tensor host = at::empty({(int64_t)(off_w + bw)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(host.data_ptr(), vs.data(), bs);
+  std::memcpy((char*)host.data_ptr() + off_w, vw.data(), bw);
+  return host.to(device_like.device());
+}
+
+void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, const optional<Tensor>& g16,
+                     double gscale, const optional<Tensor>& s1, const optional<Tensor>& s2, double lr, double beta1,
+                     double beta2, double eps, double momentum, double rho, const optional<Tensor>& beta_pow,
+                     const optional<Tensor>& global_step, int64_t gs_inc, const Tensor& done, const Tensor& blob,
+                     int64_t nseg, int64_t nwork) {
+  check_cuda(p, "p");
+  dtfe::OptArgs a{};
+  a.kind = (int)kind;
+  a.p = p.data_ptr<float>();
+  a.g = ptr_or_null<float>(g);
+  a.g16 = ptr_or_null<dtfe::bf16>(g16);
+  TORCH_CHECK((a.g != nullptr) != (a.g16 != nullptr), "apply_gradients: exactly one of g / g16");
+  a.gscale = (float)gscale;
+  a.s1 = ptr_or_null<float>(s1); a.s2 = ptr_or_null<float>(s2);
+  a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.momentum = (float)momentum; a.rho = (float)rho;
+  a.beta_pow = ptr_or_null<float>(beta_pow);
+  a.global_step = ptr_or_null<int32_t>(global_step);
+  a.gs_inc = (int)gs_inc;
+  a.done_counter = reinterpret_cast<uint32_t*>(done.data_ptr());
+  const size_t bs = nseg * sizeof(dtfe::OptSeg);
+  const size_t off_w = (bs + 255) / 256 * 256;
+  a.segs = reinterpret_cast<const dtfe::OptSeg*>(blob.data_ptr());
+  a.work = reinterpret_cast<const dtfe::OptWork*>((const char*)blob.data_ptr() + off_w);
+  a.nwork = (int)nwork;
+  if (kind == dtfe::OPT_ADAM) TORCH_CHECK(a.beta_pow && a.s1 && a.s2, "adam needs slots and beta powers");
+  if (kind == dtfe::OPT_RMSPROP) TORCH_CHECK(a.s1 && a.s2, "rmsprop needs slots");
+  if (kind == dtfe::OPT_MOMENTUM) TORCH_CHECK(a.s1, "momentum needs a slot");
+  dtfe::launch_apply_gradients(a, cur_stream());
+}
+
+// ---------------------------------------------------------- elementwise
+int data_code(const Tensor& t) {
+  if (t.scalar_type() == at::kByte) return 0;
+  if (t.scalar_type() == at::kFloat) return 1;
+  if (t.scalar_type() == at::kBFloat16) return 2;
+  TORCH_CHECK(false, "gather_rows: unsupported dtype");
+}
+
+void gather_rows(const Tensor& src, const Tensor& dst, const optional<Tensor>& idx, const optional<Tensor>& labels_src,
+                 const optional<Tensor>& labels_dst, int64_t seed, const optional<Tensor>& counter,
+                 const optional<Tensor>& done) {
+  check_cuda(src, "src");
+  dtfe::GatherArgs a{};
+  a.src = src.data_ptr(); a.src_dtype = data_code(src); a.n_rows = src.size(0); a.D = (int)(src.numel() / src.size(0));
+  a.dst = dst.data_ptr(); a.dst_dtype = data_code(dst); a.B = (int)dst.size(0);
+  TORCH_CHECK(a.dst_dtype != 0, "gather_rows: dst must be f32 or bf16");
+  a.idx = ptr_or_null<int32_t>(idx);
+  a.labels_src = ptr_or_null<int32_t>(labels_src); a.labels_dst = ptr_or_null<int32_t>(labels_dst);
+  a.seed = (uint64_t)seed; a.counter = ptr_or_null<int64_t>(counter); a.done = ptr_or_null<uint32_t>(done);
+  dtfe::launch_gather_rows(a, cur_stream());
+}
+
+void uniform_fill(const Tensor& out, double lo, double hi, int64_t seed, const optional<Tensor>& counter,
+                  const optional<Tensor>& done) {
+  check_cuda(out, "out");
+  dtfe::launch_uniform_fill(out.data_ptr<float>(), out.numel(), (float)lo, (float)hi, (uint64_t)seed,
+                            ptr_or_null<int64_t>(counter), ptr_or_null<uint32_t>(done), cur_stream());
+}
+
+void cast_(const Tensor& src, const Tensor& dst) {
+  check_cuda(src, "src");
+  TORCH_CHECK(src.numel() == dst.numel(), "cast: size mismatch");
+  if (src.scalar_type() == at::kFloat && dst.scalar_type() == at::kBFloat16)
+    dtfe::launch_cast_f32_bf16(src.data_ptr<float>(), reinterpret_cast<dtfe::bf16*>(dst.data_ptr()), src.numel(),
+                               cur_stream());
+  else if (src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kFloat)
+    dtfe::launch_cast_bf16_f32(reinterpret_cast<const dtfe::bf16*>(src.data_ptr()), dst.data_ptr<float>(),
+                               src.numel(), cur_stream());
+  else
+    TORCH_CHECK(false, "cast: f32<->bf16 only");
+}
+
+void softmax_xent(const Tensor& logits, const optional<Tensor>& labels_i, const optional<Tensor>& labels_oh,
+                  double scale, const optional<Tensor>& dlogits, const optional<Tensor>& loss_rows,
+                  const optional<Tensor>& loss_sum, const optional<Tensor>& correct, const optional<Tensor>& probs) {
+  check_cuda(logits, "logits");
+  dtfe::XentArgs a{};
+  a.B = (int)logits.size(0); a.NC = (int)logits.size(1);
+  a.logits = logits.data_ptr<float>();
+  a.labels_i = ptr_or_null<int32_t>(labels_i); a.labels_oh = ptr_or_null<float>(labels_oh);
+  TORCH_CHECK(a.labels_i || a.labels_oh, "softmax_xent: labels required");
+  a.scale = (float)scale;
+  a.dlogits = ptr_or_null<float>(dlogits); a.loss_rows = ptr_or_null<float>(loss_rows);
+  a.loss_sum = ptr_or_null<float>(loss_sum); a.correct = ptr_or_null<int32_t>(correct);
+  a.probs = ptr_or_null<float>(probs);
+  dtfe::launch_softmax_xent(a, cur_stream());
+}
+
+void gan_loss(const Tensor& d_real, const Tensor& d_fake, const Tensor& gen_loss, const Tensor& disc_loss,
+              const Tensor& dz_real_disc, const Tensor& dz_fake_disc, const Tensor& dz_fake_gen, double clamp_eps) {
+  check_cuda(d_real, "d_real");
+  dtfe::GanLossArgs a{};
+  a.B = (int)d_real.numel();
+  a.d_real = d_real.data_ptr<float>(); a.d_fake = d_fake.data_ptr<float>();
+  a.gen_loss = gen_loss.data_ptr<float>(); a.disc_loss = disc_loss.data_ptr<float>();
+  a.dz_real_disc = dz_real_disc.data_ptr<float>(); a.dz_fake_disc = dz_fake_disc.data_ptr<float>();
+  a.dz_fake_gen = dz_fake_gen.data_ptr<float>();
+  a.clamp_eps = (float)clamp_eps;
+  dtfe::launch_gan_loss(a, cur_stream());
+}
+
+void mse_sigmoid(const Tensor& y, const Tensor& t, const Tensor& loss, const Tensor& dz) {
+  check_cuda(y, "y");
+  dtfe::launch_mse_sigmoid(y.data_ptr<float>(), t.data_ptr<float>(), y.numel(), loss.data_ptr<float>(),
+                           dz.data_ptr<float>(), cur_stream());
+}
+
+void colsum(const Tensor& x, int64_t M, int64_t N, int64_t ld, const Tensor& db, double scale) {
+  check_cuda(x, "x");
+  dtfe::launch_colsum(x.data_ptr(), x.scalar_type() == at::kFloat, (int)M, (int)N, ld, db.data_ptr<float>(),
+                      (float)scale, cur_stream());
+}
+
+void act_grad(const Tensor& dy, const Tensor& y, const Tensor& dz, int64_t act) {
+  check_cuda(dy, "dy");
+  dtfe::launch_act_grad(dy.data_ptr<float>(), y.data_ptr<float>(), dz.data_ptr<float>(), dy.numel(), (int)act,
+                        cur_stream());
+}
+
+void bias_act(const Tensor& x, const optional<Tensor>& bias, const Tensor& out, int64_t act, double keep,
+              int64_t seed, const optional<Tensor>& counter) {
+  check_cuda(x, "x");
+  dtfe::BiasActArgs a{};
+  a.x = x.data_ptr<float>(); a.bias = ptr_or_null<float>(bias);
+  a.M = (int)x.size(0); a.N = (int)(x.numel() / x.size(0)); a.act = (int)act;
+  a.keep = (float)keep; a.seed = (uint64_t)seed; a.counter = ptr_or_null<int64_t>(counter);
+  a.out = out.data_ptr(); a.out_f32 = out.scalar_type() == at::kFloat;
+  dtfe::launch_bias_act(a, cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dtfe, m) {
+  m.def(
+      "gemm(Tensor A, int amode, int lda, Tensor B, int bmode, int ldb, int M, int N, int K, Tensor(a!) out, int ldc,"
+      " Tensor? bias, int bias_axis, int act, float alpha, float beta, bool atomic, int splits, int tile,"
+      " Tensor? aux, int ld_aux, int aux_act, int b_ones_row, float keep, int seed, Tensor? counter,"
+      " Tensor? pooled, Tensor? argmax, int PH, int PW, int PC, Tensor(b!)? out2, int ldc2, bool out2_trans) -> ()");
+  m.def(
+      "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
+      " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");
+  m.def(
+      "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
+      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax) -> ()");
+  m.def(
+      "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
+      " int OW, int KH, int KW, int stride, int pad, float scale) -> ()");
+  m.def(
+      "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!)? db,"
+      " Tensor(d!)? dbh, Tensor(e!)? loss_sum, Tensor(f!)? correct, Tensor(g!)? logits, float scale,"
+      " float inv_keep) -> ()");
+  m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
+  m.def(
+      "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
+      " float lr, float beta1, float beta2, float eps, float momentum, float rho, Tensor(d!)? beta_pow,"
+      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork) -> ()");
+  m.def(
+      "gather_rows(Tensor src, Tensor(a!) dst, Tensor? idx, Tensor? labels_src, Tensor(b!)? labels_dst, int seed,"
+      " Tensor(c!)? counter, Tensor(d!)? done) -> ()");
+  m.def("uniform_fill(Tensor(a!) out, float lo, float hi, int seed, Tensor(b!)? counter, Tensor(c!)? done) -> ()");
+  m.def("cast_(Tensor src, Tensor(a!) dst) -> ()");
+  m.def(
+      "softmax_xent(Tensor logits, Tensor? labels_i, Tensor? labels_oh, float scale, Tensor(a!)? dlogits,"
+      " Tensor(b!)? loss_rows, Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? probs) -> ()");
+  m.def(
+      "gan_loss(Tensor d_real, Tensor d_fake, Tensor(a!) gen_loss, Tensor(b!) disc_loss, Tensor(c!) dz_real_disc,"
+      " Tensor(d!) dz_fake_disc, Tensor(e!) dz_fake_gen, float clamp_eps) -> ()");
+  m.def("mse_sigmoid(Tensor y, Tensor t, Tensor(a!) loss, Tensor(b!) dz) -> ()");
+  m.def("colsum(Tensor x, int M, int N, int ld, Tensor(a!) db, float scale) -> ()");
+  m.def("act_grad(Tensor dy, Tensor y, Tensor(a!) dz, int act) -> ()");
+  m.def("bias_act(Tensor x, Tensor? bias, Tensor(a!) out, int act, float keep, int seed, Tensor? counter) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
+  m.impl("gemm", &gemm);
+  m.impl("conv_fwd", &conv_fwd);
+  m.impl("conv_dgrad", &conv_dgrad);
+  m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("head_xent", &head_xent);
+  m.impl("apply_gradients", &apply_gradients);
+  m.impl("gather_rows", &gather_rows);
+  m.impl("uniform_fill", &uniform_fill);
+  m.impl("cast_", &cast_);
+  m.impl("softmax_xent", &softmax_xent);
+  m.impl("gan_loss", &gan_loss);
+  m.impl("mse_sigmoid", &mse_sigmoid);
+  m.impl("colsum", &colsum);
+  m.impl("act_grad", &act_grad);
+  m.impl("bias_act", &bias_act);
+}
+
+TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) { m.impl("opt_pack", &opt_pack); }

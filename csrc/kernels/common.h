@@ -1,0 +1,97 @@
+// Common device helpers for the dtfe CDNA4 (gfx950) kernel library.
+//
+// Everything here is written for MI355X directly: 64-lane wavefronts, MFMA
+// fragments, LDS address-space casts for the gfx950 transpose read.  No CUDA
+// shims, no dual paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dtfe {
+
+typedef uint16_t bf16;  // storage type for bfloat16
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ float bf2f(bf16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even fp32 -> bf16 (NaN preserved as quiet NaN)
+__device__ __forceinline__ bf16 f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16)0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// Activation codes shared with the host side (ops/_lib.py mirrors these).
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ float apply_act(float x, int act) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_SIGMOID: return sigmoidf_(x);
+    case ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+
+// derivative of the activation expressed through its OUTPUT y = act(z)
+__device__ __forceinline__ float act_grad_from_out(float y, int act) {
+  switch (act) {
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_SIGMOID: return y * (1.f - y);
+    case ACT_TANH: return 1.f - y * y;
+    default: return 1.f;
+  }
+}
+
+// 64-lane wave reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based hash RNG (deterministic, stateless): used for dropout masks,
+// on-device batch sampling and synthetic data.  splitmix/murmur finaliser.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)z;
+}
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
+  return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);  // [0,1)
+}
+
+// XCD-aware bijective remap of a flat workgroup id (cdna_hip_programming T1):
+// consecutive logical tiles land on the same XCD so they share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int nxcd = 8;
+  if (nwg <= nxcd) return orig;
+  int q = nwg / nxcd, r = nwg % nxcd;
+  int xcd = orig % nxcd;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / nxcd;
+}
+
+}  // namespace dtfe

@@ -1,0 +1,61 @@
+// Convolution / pooling argument blocks shared by the kernels and the bindings.
+#pragma once
+#include "common.h"
+
+namespace dtfe {
+
+struct ConvGeom {
+  int B, H, W, C;          // input NHWC
+  int Cout, OH, OW;        // output
+  int KH, KW, stride, pad;
+  int pool_order;          // forward rows enumerated by 2x2 pool window (fused max-pool)
+};
+
+// Un-pool description: the GEMM output element at flat index pidx of a pooled
+// tensor [B, PH, PW, C] is a gradient w.r.t. pooled value P[pidx]; it is routed
+// to position argmax[pidx] of its 2x2 window in the full-resolution tensor
+// [B, 2PH, 2PW, C] (zeros elsewhere) and masked by ReLU'(P) (P > 0).
+struct UnpoolArgs {
+  const bf16* pooled;
+  const uint8_t* argmax;
+  int PH, PW, C;
+};
+
+__device__ __forceinline__ void unpool_store(const UnpoolArgs& u, long pidx, float g, bf16* dz) {
+  const int c = (int)(pidx % u.C);
+  long t = pidx / u.C;
+  const int pw = (int)(t % u.PW);
+  t /= u.PW;
+  const int ph = (int)(t % u.PH);
+  const long b = t / u.PH;
+  const int am = u.argmax[pidx];
+  const float gv = bf2f(u.pooled[pidx]) > 0.f ? g : 0.f;
+  const int W2 = 2 * u.PW, H2 = 2 * u.PH;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long o = ((b * H2 + 2 * ph + (q >> 1)) * W2 + 2 * pw + (q & 1)) * u.C + c;
+    dz[o] = f2bf(q == am ? gv : 0.f);
+  }
+}
+
+struct ConvFwdArgs {
+  ConvGeom g;
+  const bf16* x; const bf16* w; const float* bias;
+  bf16* y; uint8_t* argmax; int act;
+};
+struct ConvDgradArgs {
+  ConvGeom g;
+  const bf16* dy; const bf16* wt;   // wt: [C][KH][KW][Cout]
+  bf16* dx; int unpool; UnpoolArgs up;
+};
+struct ConvWgradArgs {
+  ConvGeom g;
+  const bf16* dz; const bf16* x;    // dz: [B*OH*OW][Cout] (full resolution)
+  float* dw; float* db; float scale; int k_chunk;
+};
+
+void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
+void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s);
+void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);
+
+}  // namespace dtfe

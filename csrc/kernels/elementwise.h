@@ -1,0 +1,69 @@
+#pragma once
+#include "common.h"
+
+namespace dtfe {
+
+// ---- data path: HBM-resident dataset -> batch
+// src dtype: 0 = uint8 (raw pixels, scaled by 1/255), 1 = f32, 2 = bf16
+// dst dtype: 1 = f32, 2 = bf16
+// idx == nullptr: indices sampled on device from (seed, *counter) and the
+// counter advanced by the last workgroup, so a replayed graph draws a new batch.
+struct GatherArgs {
+  const void* src; int src_dtype; long n_rows; int D;
+  void* dst; int dst_dtype; int B;
+  const int32_t* idx;
+  const int32_t* labels_src; int32_t* labels_dst;
+  uint64_t seed; int64_t* counter; uint32_t* done;
+};
+void launch_gather_rows(const GatherArgs& a, hipStream_t s);
+
+// uniform noise U(lo, hi) from a counter-based hash; *counter advanced per call
+void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, int64_t* counter,
+                         uint32_t* done, hipStream_t s);
+
+// dtype casts
+void launch_cast_f32_bf16(const float* src, bf16* dst, long n, hipStream_t s);
+void launch_cast_bf16_f32(const bf16* src, float* dst, long n, hipStream_t s);
+
+// softmax cross-entropy fwd+bwd on fp32 logits [B][NC]
+// labels: int32 class ids (labels_i) or one-hot fp32 rows (labels_oh).
+// dlogits = (softmax - y) * scale; loss_rows[b] = per-row loss; correct += argmax hits
+struct XentArgs {
+  int B, NC;
+  const float* logits; const int32_t* labels_i; const float* labels_oh;
+  float scale;
+  float* dlogits; float* loss_rows; float* loss_sum; int32_t* correct; float* probs;
+};
+void launch_softmax_xent(const XentArgs& a, hipStream_t s);
+
+// GAN losses on the sigmoid outputs of D, with grads w.r.t. the
+// pre-sigmoid logits.  No epsilon inside log, as in the reference (GAN:142-143),
+// unless clamp_eps > 0.
+struct GanLossArgs {
+  int B;
+  const float* d_real; const float* d_fake;   // sigmoid outputs [B]
+  float* gen_loss; float* disc_loss;          // scalars (overwritten)
+  float* dz_real_disc; float* dz_fake_disc;   // d disc_loss / d logit
+  float* dz_fake_gen;                         // d gen_loss / d logit_fake
+  float clamp_eps;
+};
+void launch_gan_loss(const GanLossArgs& a, hipStream_t s);
+
+// mean((t - y)^2) with the gradient w.r.t. the pre-sigmoid logit of y
+void launch_mse_sigmoid(const float* y, const float* t, long n, float* loss, float* dz, hipStream_t s);
+
+// db[n] += scale * sum_m x[m][n]   (x f32 or bf16)
+void launch_colsum(const void* x, int x_f32, int M, int N, long ld, float* db, float scale, hipStream_t s);
+
+// dz = dy * act'(y)   (y = forward output of the activation)
+void launch_act_grad(const float* dy, const float* y, float* dz, long n, int act, hipStream_t s);
+
+// out = act(x + bias[col]) ; optional dropout (keep prob, hash RNG) ; bf16 or f32 out
+struct BiasActArgs {
+  const float* x; const float* bias; int M, N; int act;
+  float keep; uint64_t seed; const int64_t* counter;
+  void* out; int out_f32;
+};
+void launch_bias_act(const BiasActArgs& a, hipStream_t s);
+
+}  // namespace dtfe

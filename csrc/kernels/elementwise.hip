@@ -1,0 +1,250 @@
+// Memory-bound helper kernels: batch gather from HBM-resident data, noise,
+// casts, the small losses of the reference models and bias/activation passes.
+// All vectorised where the data layout allows (CDNA guide G13).
+#include "elementwise.h"
+
+namespace dtfe {
+
+// last-workgroup counter advance (see optim.hip): every workgroup has read
+// *counter before it arrives, so the bump is invisible to this launch.
+__device__ __forceinline__ void advance_counter_last_block(int64_t* counter, uint32_t* done, int64_t by) {
+  if (!counter || !done) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x * gridDim.y - 1) {
+      atomicAdd((unsigned long long*)counter, (unsigned long long)by);
+      atomicExch(done, 0u);
+      __threadfence();
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
+  const int64_t step = a.counter ? *a.counter : 0;
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    long r;
+    if (a.idx) r = a.idx[b];
+    else r = (long)(hash_u32(a.seed, (uint64_t)step * a.B + b) % (uint32_t)a.n_rows);
+    if (a.labels_dst && threadIdx.x == 0) a.labels_dst[b] = a.labels_src[r];
+    for (int d = threadIdx.x; d < a.D; d += 256) {
+      float v;
+      if (a.src_dtype == 0) v = reinterpret_cast<const uint8_t*>(a.src)[r * a.D + d] * (1.f / 255.f);
+      else if (a.src_dtype == 1) v = reinterpret_cast<const float*>(a.src)[r * a.D + d];
+      else v = bf2f(reinterpret_cast<const bf16*>(a.src)[r * a.D + d]);
+      if (a.dst_dtype == 1) reinterpret_cast<float*>(a.dst)[(long)b * a.D + d] = v;
+      else reinterpret_cast<bf16*>(a.dst)[(long)b * a.D + d] = f2bf(v);
+    }
+  }
+  advance_counter_last_block(a.counter, a.done, 1);
+}
+
+void launch_gather_rows(const GatherArgs& a, hipStream_t s) {
+  int blocks = a.B < 1024 ? a.B : 1024;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void uniform_fill_kernel(float* out, long n, float lo, float hi, uint64_t seed,
+                                                          int64_t* counter, uint32_t* done) {
+  const int64_t step = counter ? *counter : 0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    out[i] = lo + (hi - lo) * hash_uniform(seed ^ 0xA5A5A5A5ull, (uint64_t)step * n + i);
+  advance_counter_last_block(counter, done, 1);
+}
+
+void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, int64_t* counter, uint32_t* done,
+                         hipStream_t s) {
+  long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(uniform_fill_kernel, dim3(blocks), dim3(256), 0, s, out, n, lo, hi, seed, counter, done);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* src, bf16* dst, long n) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const f32x4_t v = reinterpret_cast<const f32x4_t*>(src)[i];
+    u32x2_t o = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+    reinterpret_cast<u32x2_t*>(dst)[i] = o;
+  }
+  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = f2bf(src[i]);
+}
+void launch_cast_f32_bf16(const float* src, bf16* dst, long n, hipStream_t s) {
+  long blocks = (n / 4 + 255) / 256 + 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(blocks), dim3(256), 0, s, src, dst, n);
+}
+__global__ void cast_bf16_f32_kernel(const bf16* src, float* dst, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = bf2f(src[i]);
+}
+void launch_cast_bf16_f32(const bf16* src, float* dst, long n, hipStream_t s) {
+  long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(blocks), dim3(256), 0, s, src, dst, n);
+}
+
+// one wave per row
+__global__ __launch_bounds__(256) void softmax_xent_kernel(XentArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.B) return;
+  const float* lg = a.logits + (long)row * a.NC;
+  float mx = -INFINITY;
+  int am = 0;
+  for (int n = lane; n < a.NC; n += 64) if (lg[n] > mx) { mx = lg[n]; am = n; }
+  // wave argmax (first max)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+  }
+  float se = 0.f;
+  for (int n = lane; n < a.NC; n += 64) se += __expf(lg[n] - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  float loss = 0.f;
+  int label = -1;
+  if (a.labels_i) label = a.labels_i[row];
+  float ymax = -1.f;
+  int yarg = 0;
+  for (int n = lane; n < a.NC; n += 64) {
+    const float y = a.labels_i ? (n == label ? 1.f : 0.f) : a.labels_oh[(long)row * a.NC + n];
+    const float p = __expf(lg[n] - lse);
+    loss += y * (lse - lg[n]);
+    if (a.dlogits) a.dlogits[(long)row * a.NC + n] = (p - y) * a.scale;
+    if (a.probs) a.probs[(long)row * a.NC + n] = p;
+    if (y > ymax) { ymax = y; yarg = n; }
+  }
+  loss = wave_sum(loss);
+  if (!a.labels_i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(ymax, o, 64);
+      const int oa = __shfl_xor(yarg, o, 64);
+      if (om > ymax || (om == ymax && oa < yarg)) { ymax = om; yarg = oa; }
+    }
+    label = yarg;
+  }
+  if (lane == 0) {
+    if (a.loss_rows) a.loss_rows[row] = loss;
+    if (a.loss_sum) atomicAdd(a.loss_sum, loss);
+    if (a.correct) atomicAdd(a.correct, (int)(am == label));
+  }
+}
+void launch_softmax_xent(const XentArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3((a.B + 3) / 4), dim3(256), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void gan_loss_kernel(GanLossArgs a) {
+  __shared__ float sg[4], sd[4];
+  float gl = 0.f, dl = 0.f;
+  const float invB = 1.f / a.B;
+  for (int i = threadIdx.x; i < a.B; i += 256) {
+    float pr = a.d_real[i], pf = a.d_fake[i];
+    float pr_c = pr, pf_c = pf, qf_c = 1.f - pf;
+    if (a.clamp_eps > 0.f) {
+      pr_c = fmaxf(pr, a.clamp_eps);
+      pf_c = fmaxf(pf, a.clamp_eps);
+      qf_c = fmaxf(1.f - pf, a.clamp_eps);
+    }
+    gl += -logf(pf_c);
+    dl += -(logf(pr_c) + logf(qf_c));
+    // d/dz of -log(sigmoid(z)) = -(1 - s);  d/dz of -log(1 - sigmoid(z)) = s
+    a.dz_real_disc[i] = -(1.f - pr) * invB;
+    a.dz_fake_disc[i] = pf * invB;
+    a.dz_fake_gen[i] = -(1.f - pf) * invB;
+  }
+  gl = wave_sum(gl);
+  dl = wave_sum(dl);
+  if ((threadIdx.x & 63) == 0) { sg[threadIdx.x >> 6] = gl; sd[threadIdx.x >> 6] = dl; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *a.gen_loss = (sg[0] + sg[1] + sg[2] + sg[3]) * invB;
+    *a.disc_loss = (sd[0] + sd[1] + sd[2] + sd[3]) * invB;
+  }
+}
+void launch_gan_loss(const GanLossArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(gan_loss_kernel, dim3(1), dim3(256), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void mse_sigmoid_kernel(const float* y, const float* t, long n, float* loss,
+                                                          float* dz) {
+  __shared__ float part[4];
+  float acc = 0.f;
+  const float inv = 1.f / (float)n;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float d = y[i] - t[i];
+    acc += d * d;
+    dz[i] = 2.f * d * inv * y[i] * (1.f - y[i]);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, (part[0] + part[1] + part[2] + part[3]) * inv);
+}
+void launch_mse_sigmoid(const float* y, const float* t, long n, float* loss, float* dz, hipStream_t s) {
+  long blocks = (n + 255) / 256;
+  if (blocks > 512) blocks = 512;
+  hipMemsetAsync(loss, 0, sizeof(float), s);
+  hipLaunchKernelGGL(mse_sigmoid_kernel, dim3(blocks), dim3(256), 0, s, y, t, n, loss, dz);
+}
+
+// column sums: block = 64 columns x 4 row-groups
+__global__ __launch_bounds__(256) void colsum_kernel(const void* x, int x_f32, int M, int N, long ld, float* db,
+                                                     float scale) {
+  __shared__ float part[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < N) {
+    for (int m = blockIdx.y * 4 + rg; m < M; m += gridDim.y * 4) {
+      acc += x_f32 ? reinterpret_cast<const float*>(x)[(long)m * ld + c]
+                   : bf2f(reinterpret_cast<const bf16*>(x)[(long)m * ld + c]);
+    }
+  }
+  part[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    const float s = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    atomicAdd(db + c, s * scale);
+  }
+}
+void launch_colsum(const void* x, int x_f32, int M, int N, long ld, float* db, float scale, hipStream_t s) {
+  int gx = (N + 63) / 64;
+  int gy = (M + 255) / 256;
+  if (gy > 64) gy = 64;
+  if (gy < 1) gy = 1;
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, s, x, x_f32, M, N, ld, db, scale);
+}
+
+__global__ void act_grad_kernel(const float* dy, const float* y, float* dz, long n, int act) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    dz[i] = dy[i] * act_grad_from_out(y[i], act);
+}
+void launch_act_grad(const float* dy, const float* y, float* dz, long n, int act, hipStream_t s) {
+  long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(act_grad_kernel, dim3(blocks), dim3(256), 0, s, dy, y, dz, n, act);
+}
+
+__global__ void bias_act_kernel(BiasActArgs a) {
+  const long n = (long)a.M * a.N;
+  const int64_t step = a.counter ? *a.counter : 0;
+  const float inv_keep = 1.f / a.keep;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float v = a.x[i] + (a.bias ? a.bias[i % a.N] : 0.f);
+    v = apply_act(v, a.act);
+    if (a.keep < 1.f) v = hash_uniform(a.seed, (uint64_t)step * n + i) < a.keep ? v * inv_keep : 0.f;
+    if (a.out_f32) reinterpret_cast<float*>(a.out)[i] = v;
+    else reinterpret_cast<bf16*>(a.out)[i] = f2bf(v);
+  }
+}
+void launch_bias_act(const BiasActArgs& a, hipStream_t s) {
+  long n = (long)a.M * a.N;
+  long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(bias_act_kernel, dim3(blocks), dim3(256), 0, s, a);
+}
+
+}  // namespace dtfe

@@ -1,0 +1,212 @@
+"""MNIST 2-layer CNN - the north-star headline workload (BASELINE.json config 2/4).
+
+Architecture (TensorFlow-Examples ``convolutional_network``, the notebook
+family the reference scripts come from, ENC:14):
+
+    x[B,28,28,1] -> conv5x5 1->32 SAME + ReLU -> maxpool 2x2
+                 -> conv5x5 32->64 SAME + ReLU -> maxpool 2x2
+                 -> fc 3136->1024 + ReLU -> dropout(keep 0.75) -> fc 1024->10
+                 -> softmax cross-entropy                     (3,274,634 params)
+
+MI355X design: the step is an explicit program of 10 fused HIP kernels over
+pre-allocated NHWC bf16 buffers (fp32 master weights / grads / Adam slots in
+one flat buffer), captured into one hipGraph:
+
+  gather      batch from the HBM-resident dataset (device RNG, no host feed)
+  conv1/pool  implicit-GEMM MFMA, bias+ReLU+2x2 max-pool+argmax in registers
+  conv2/pool  same
+  fc1         MFMA GEMM, bias+ReLU+dropout epilogue
+  head        fc2 + softmax-xent + fc2 backward + dropout/ReLU grad (+ fc1 bias grad)
+  fc1 dgrad   MFMA GEMM with the un-pool(argmax2)+ReLU' epilogue -> dZ2 full-res
+  fc1 wgrad   MFMA GEMM (both operands via ds_read_b64_tr_b16)
+  conv2 dgrad implicit-GEMM with the un-pool(argmax1)+ReLU' epilogue -> dZ1
+  conv2/conv1 wgrad  split-K implicit GEMM, bias grad as an extra ones column
+  Adam        one fused TF1 Adam launch, writes bf16 + transposed bf16 copies
+
+In data-parallel mode the fc/head gradient bucket (98% of the bytes) is
+all-reduced over RCCL while the conv backward kernels still run.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..optim import FlatParams, Optimizer, OptimizerConfig, VarSpec
+
+IMG, C1, C2, FC, NCLS = 28, 32, 64, 1024, 10
+KS = 5
+
+
+def _normal(std):
+    return lambda shape, g: torch.randn(*shape, generator=g) * std
+
+
+def _zeros(shape, g):
+    return torch.zeros(*shape)
+
+
+def _conv_to_tf(t):   # ours [Cout][KH][KW][Cin] -> TF [KH][KW][Cin][Cout]
+    return t.permute(1, 2, 3, 0).contiguous()
+
+
+def _conv_from_tf(t):
+    return t.permute(3, 0, 1, 2).contiguous()
+
+
+def _fc_to_tf(t):     # ours [out][in] -> TF [in][out]
+    return t.t().contiguous()
+
+
+def _fc_from_tf(t):
+    return t.t().contiguous()
+
+
+def var_specs():
+    """Variables in TF creation order (weights dict then biases dict, as in the
+    TensorFlow-Examples notebook) -> TF auto names Variable, Variable_1, ...
+
+    Flat-buffer order is the backward-completion order (head first, conv1
+    last) so gradient buckets fill front to back.
+    """
+    tf_order = [
+        ("wc1", (C1, KS, KS, 1), _normal(0.1), "conv"),
+        ("wc2", (C2, KS, KS, C1), _normal(0.05), "conv"),
+        ("wd1", (FC, 7 * 7 * C2), _normal(0.02), "fc"),
+        ("out", (NCLS, FC), _normal(0.05), "fc"),
+        ("bc1", (C1,), _zeros, None),
+        ("bc2", (C2,), _zeros, None),
+        ("bd1", (FC,), _zeros, None),
+        ("bout", (NCLS,), _zeros, None),
+    ]
+    names = {}
+    for i, (k, *_rest) in enumerate(tf_order):
+        names[k] = "Variable" if i == 0 else f"Variable_{i}"
+    spec = {}
+    for k, shape, init, kind in tf_order:
+        kw = dict(name=names[k], shape=shape, init=init)
+        if kind == "conv":
+            kw.update(bf16=True, to_tf=_conv_to_tf, from_tf=_conv_from_tf,
+                      tf_shape=(shape[1], shape[2], shape[3], shape[0]))
+        elif kind == "fc":
+            kw.update(bf16=True, to_tf=_fc_to_tf, from_tf=_fc_from_tf, tf_shape=(shape[1], shape[0]))
+        spec[k] = VarSpec(**kw)
+    # transposed bf16 copies needed by the backward GEMMs
+    spec["wc2"].transpose = (C2, KS * KS, C1)    # -> Wt[C1][25][C2] for conv2 dgrad
+    spec["wd1"].transpose = (FC, 1, 7 * 7 * C2)  # -> Wt[3136][1024] for fc1 dgrad
+    flat_order = ["out", "bout", "bd1", "wd1", "wc2", "bc2", "wc1", "bc1"]
+    return [spec[k] for k in flat_order], names
+
+
+def num_params():
+    specs, _ = var_specs()
+    return sum(s.numel for s in specs)
+
+
+class SyntheticMnist:
+    """HBM-resident MNIST-shaped dataset (uint8 pixels + int32 labels)."""
+
+    def __init__(self, n: int, device, seed: int = 1234, images=None, labels=None):
+        if images is None:
+            g = torch.Generator().manual_seed(seed)
+            images = torch.randint(0, 256, (n, IMG * IMG), generator=g, dtype=torch.uint8)
+            labels = torch.randint(0, NCLS, (n,), generator=g, dtype=torch.int32)
+        self.images = images.to(device).contiguous()
+        self.labels = labels.to(device=device, dtype=torch.int32).contiguous()
+        self.n = self.images.shape[0]
+
+
+class MnistCnnTrainer:
+    """Per-rank training-step program for the MNIST CNN."""
+
+    def __init__(self, batch: int, device, lr: float = 1e-3, keep_prob: float = 0.75, seed: int = 0,
+                 data: SyntheticMnist | None = None, allreduce=None, world_size: int = 1):
+        self.B = batch
+        self.device = torch.device(device)
+        assert self.device.type == "cuda", "MnistCnnTrainer runs on the MI355X kernel path"
+        ops.require()
+        self.keep = keep_prob
+        self.seed = seed
+        self.world = world_size
+        self.allreduce = allreduce
+        specs, self.names = var_specs()
+        self.P = FlatParams(specs, self.device, seed=seed)
+        self.global_step = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.opt = Optimizer(OptimizerConfig(kind="adam", lr=lr), self.P, global_step=self.global_step)
+        self.data = data or SyntheticMnist(60000, self.device, seed=seed + 17)
+        d = self.device
+        B = batch
+        bf = torch.bfloat16
+        self.x = torch.empty(B, IMG, IMG, 1, device=d, dtype=bf)
+        self.labels = torch.empty(B, dtype=torch.int32, device=d)
+        self.p1 = torch.empty(B, 14, 14, C1, device=d, dtype=bf)
+        self.a1 = torch.empty(B, 14, 14, C1, device=d, dtype=torch.uint8)
+        self.p2 = torch.empty(B, 7, 7, C2, device=d, dtype=bf)
+        self.a2 = torch.empty(B, 7, 7, C2, device=d, dtype=torch.uint8)
+        self.h = torch.empty(B, FC, device=d, dtype=bf)
+        self.dzf = torch.empty(B, FC, device=d, dtype=bf)
+        self.dz2 = torch.empty(B, 14, 14, C2, device=d, dtype=bf)
+        self.dz1 = torch.empty(B, IMG, IMG, C1, device=d, dtype=bf)
+        self.loss_sum = torch.zeros(1, device=d)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=d)
+        self.data_ctr = torch.zeros(1, dtype=torch.int64, device=d)
+        self.data_done = torch.zeros(1, dtype=torch.int32, device=d)
+        self.g1 = dict(B=B, H=IMG, W=IMG, C=1, Cout=C1, OH=IMG, OW=IMG, KH=KS, KW=KS, stride=1, pad=2)
+        self.g2 = dict(B=B, H=14, W=14, C=C1, Cout=C2, OH=14, OW=14, KH=KS, KW=KS, stride=1, pad=2)
+        n = self.names
+        P = self.P
+        self.w = {k: P.w16[n[k]] for k in ("wc1", "wc2", "wd1", "out")}
+        self.wt = {k: P.wt16[n[k]] for k in ("wc2", "wd1")}
+        self.b = {k: P.view(n[k]) for k in ("bc1", "bc2", "bd1", "bout")}
+        self.gw = {k: P.gview(n[k]) for k in ("wc1", "wc2", "wd1", "out", "bc1", "bc2", "bd1", "bout")}
+        # gradient buckets in flat order: [head + fc1] then [conv2 + conv1]
+        lo1, hi1 = P.range_of([n["out"], n["bout"], n["bd1"], n["wd1"]])
+        lo2, hi2 = P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
+        self.buckets = [(lo1, hi1), (lo2, hi2)]
+
+    # ------------------------------------------------------------------
+    def forward_backward(self):
+        B = self.B
+        P = self.P
+        P.grad.zero_()
+        self.loss_sum.zero_()
+        self.correct.zero_()
+        ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
+                        seed=self.seed + 1, counter=self.data_ctr, done=self.data_done)
+        ops.conv_fwd(self.x, self.w["wc1"], self.b["bc1"], self.p1, self.a1, self.g1, pool=True, act=ops.ACT_RELU)
+        ops.conv_fwd(self.p1, self.w["wc2"], self.b["bc2"], self.p2, self.a2, self.g2, pool=True, act=ops.ACT_RELU)
+        K1 = 7 * 7 * C2
+        ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
+                 keep=self.keep, seed=self.seed + 2, counter=self.data_ctr)
+        ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.gw["out"], self.gw["bout"],
+                      self.gw["bd1"], self.loss_sum, self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
+        # fc1 dgrad -> dZ2 (full resolution, un-pooled through argmax2, ReLU-masked)
+        ops.gemm(self.dzf, self.wt["wd1"], self.dz2, M=B, N=K1, K=FC, pooled=self.p2, argmax=self.a2, PH=7, PW=7,
+                 PC=C2)
+        # fc1 wgrad: dW[1024][3136] = dZf^T . P2
+        ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
+                 ldb=K1)
+        if self.allreduce is not None:
+            self.allreduce.launch(0)
+        ops.conv_dgrad(self.dz2, self.wt["wc2"], self.dz1, self.g2, pooled=self.p1, argmax=self.a1)
+        ops.conv_wgrad(self.dz2, self.p1, self.gw["wc2"], self.gw["bc2"], self.g2)
+        ops.conv_wgrad(self.dz1, self.x, self.gw["wc1"], self.gw["bc1"], self.g1)
+        if self.allreduce is not None:
+            self.allreduce.launch(1)
+            self.allreduce.wait()
+
+    def apply(self):
+        self.opt.step(gscale=1.0 / self.world)
+
+    def step(self):
+        self.forward_backward()
+        self.apply()
+
+    def flops_per_image(self) -> float:
+        """Training FLOPs per image (fwd + dgrad + wgrad of every GEMM-shaped op)."""
+        c1 = 2 * IMG * IMG * C1 * KS * KS
+        c2 = 2 * 14 * 14 * C2 * KS * KS * C1
+        f1 = 2 * 7 * 7 * C2 * FC
+        f2 = 2 * FC * NCLS
+        return c1 * 2 + c2 * 3 + f1 * 3 + f2 * 3  # conv1 has no dgrad

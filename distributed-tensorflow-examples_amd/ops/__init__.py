@@ -1,0 +1,351 @@
+"""Op layer: thin wrappers over ``torch.ops.dtfe`` (gfx950 HIP kernels).
+
+Every op writes into caller-provided tensors (no allocation inside a step, so
+steps are hipGraph-capturable).  GPU tensors always go to the HIP kernels -
+if the native library is missing that is an error, never a silent fallback.
+CPU tensors take a plain-PyTorch reference path: it exists for the CPU/gloo
+plumbing configuration (BASELINE.json config 1), for CPU tests of the
+distributed machinery, and as the fp32 oracle the kernel tests compare to.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import (ACT_CODES, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, KMAJ, OPT_ADAM, OPT_MOMENTUM,
+                   OPT_RMSPROP, OPT_SGD, RMAJ, available, load, require)
+
+__all__ = [
+    "gemm", "linear_fwd", "conv_fwd", "conv_dgrad", "conv_wgrad", "head_xent", "apply_gradients", "opt_pack",
+    "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
+    "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
+    "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile",
+]
+
+_TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
+
+
+def pick_tile(M: int, N: int) -> int:
+    """Largest MFMA tile that still yields >= one workgroup per CU (256 CUs)."""
+    if M <= 32 and N <= 32:
+        return 4
+    for tid, bm, bn in _TILES:
+        if math.ceil(M / bm) * math.ceil(N / bn) >= 256:
+            return tid
+    return 0
+
+
+# --------------------------------------------------------------- references
+def _act_ref(x, act):
+    if act == ACT_RELU:
+        return torch.relu(x)
+    if act == ACT_SIGMOID:
+        return torch.sigmoid(x)
+    if act == ACT_TANH:
+        return torch.tanh(x)
+    return x
+
+
+def _act_grad_from_out_ref(y, act):
+    if act == ACT_RELU:
+        return (y > 0).to(y.dtype)
+    if act == ACT_SIGMOID:
+        return y * (1 - y)
+    if act == ACT_TANH:
+        return 1 - y * y
+    return torch.ones_like(y)
+
+
+def _mat(t, mode, rows, K, ld):
+    """Logical [rows, K] fp32 view of an operand given its mode/leading dim."""
+    flat = t.reshape(-1).float()
+    if mode == KMAJ:
+        idx = torch.arange(rows).unsqueeze(1) * ld + torch.arange(K).unsqueeze(0)
+    else:
+        idx = torch.arange(K).unsqueeze(0) * ld + torch.arange(rows).unsqueeze(1)
+    return flat[idx]
+
+
+# --------------------------------------------------------------------- GEMM
+def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=None, bias=None, bias_axis=0,
+         act=ACT_NONE, alpha=1.0, beta=0.0, atomic=False, splits=1, tile=None, aux=None, ld_aux=None, aux_act=0,
+         b_ones_row=-1, keep=1.0, seed=0, counter=None, pooled=None, argmax=None, PH=0, PW=0, PC=0, out2=None,
+         ldc2=0, out2_trans=False):
+    """out[M,N] = epilogue( A(m,k) . B(n,k) ).
+
+    A(m,k) = A[m*lda+k] (KMAJ) or A[k*lda+m] (RMAJ); likewise B(n,k).
+    Epilogue order: alpha*acc, +bias, act, dropout(keep), *act'(aux), [unpool | +beta*out], store.
+    """
+    if lda is None:
+        lda = K if amode == KMAJ else M
+    if ldb is None:
+        ldb = K if bmode == KMAJ else N
+    if ldc is None:
+        ldc = N
+    if ld_aux is None:
+        ld_aux = ldc
+    if out.is_cuda:
+        if tile is None:
+            tile = pick_tile(M, N)
+        require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
+                       splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
+                       PC, out2, ldc2, out2_trans)
+        return out
+    # CPU reference
+    a = _mat(A, amode, M, K, lda)
+    b = _mat(B, bmode, N, K, ldb)
+    if b_ones_row >= 0:
+        b[b_ones_row, :] = 1.0
+    acc = a @ b.t()
+    oflat = out.view(-1)
+    oidx = torch.arange(M).unsqueeze(1) * ldc + torch.arange(N).unsqueeze(0)
+    if atomic:
+        oflat[oidx] += (alpha * acc).to(out.dtype)
+        return out
+    x = alpha * acc
+    if bias is not None:
+        x = x + (bias.float().view(1, -1) if bias_axis == 0 else bias.float().view(-1, 1))
+    x = _act_ref(x, act)
+    if keep < 1.0:
+        raise NotImplementedError("dropout reference path: use the GPU kernels")
+    if aux is not None:
+        aidx = torch.arange(M).unsqueeze(1) * ld_aux + torch.arange(N).unsqueeze(0)
+        x = x * _act_grad_from_out_ref(aux.reshape(-1).float()[aidx], aux_act)
+    if pooled is not None:
+        _unpool_ref(x.reshape(-1), pooled, argmax, PH, PW, PC, out)
+        return out
+    if beta != 0.0:
+        x = x + beta * oflat[oidx].float()
+    oflat[oidx] = x.to(out.dtype)
+    if out2 is not None:
+        o2 = out2.view(-1)
+        idx2 = (torch.arange(N).unsqueeze(0) * ldc2 + torch.arange(M).unsqueeze(1)) if out2_trans else \
+            (torch.arange(M).unsqueeze(1) * ldc2 + torch.arange(N).unsqueeze(0))
+        o2[idx2] = x.to(out2.dtype)
+    return out
+
+
+def _unpool_ref(g, pooled, argmax, PH, PW, C, dz):
+    """Route pooled-grad g (flat [B*PH*PW*C]) to argmax positions, ReLU-masked by pooled>0."""
+    Bn = g.numel() // (PH * PW * C)
+    g = g.view(Bn, PH, PW, C) * (pooled.view(Bn, PH, PW, C).float() > 0)
+    am = argmax.view(Bn, PH, PW, C).long()
+    full = torch.zeros(Bn, PH, 2, PW, 2, C)
+    for q in range(4):
+        full[:, :, q >> 1, :, q & 1, :] = torch.where(am == q, g, torch.zeros_like(g))
+    dz.view(-1)[:] = full.reshape(-1).to(dz.dtype)
+
+
+def linear_fwd(x, w_kn, b, out, act=ACT_NONE):
+    """TF-layout dense layer: out = act(x[M,K] . W[K,N] + b)."""
+    M, K = x.shape[0], x.shape[-1]
+    N = w_kn.shape[1]
+    return gemm(x, w_kn, out, M=M, N=N, K=K, amode=KMAJ, bmode=RMAJ, ldb=N, bias=b, act=act)
+
+
+# -------------------------------------------------------------------- conv
+def _conv_geom_args(g):
+    return (g["B"], g["H"], g["W"], g["C"], g["Cout"], g["OH"], g["OW"], g["KH"], g["KW"], g["stride"], g["pad"])
+
+
+def conv_fwd(x, w, bias, y, argmax, g, pool=False, act=ACT_RELU):
+    """NHWC conv (+bias, act, optional fused 2x2 max-pool writing argmax)."""
+    if y.is_cuda:
+        require().conv_fwd(x, w, bias, y, argmax, *_conv_geom_args(g), pool, act)
+        return y
+    xt = x.float().view(g["B"], g["H"], g["W"], g["C"]).permute(0, 3, 1, 2)
+    wt = w.float().view(g["Cout"], g["KH"], g["KW"], g["C"]).permute(0, 3, 1, 2)
+    z = torch.nn.functional.conv2d(xt, wt, bias.float() if bias is not None else None, stride=g["stride"],
+                                   padding=g["pad"])
+    z = _act_ref(z, act)
+    if pool:
+        p, idx = _pool_ref(z)
+        y.view(-1)[:] = p.permute(0, 2, 3, 1).reshape(-1).to(y.dtype)
+        if argmax is not None:
+            argmax.view(-1)[:] = idx.permute(0, 2, 3, 1).reshape(-1).to(argmax.dtype)
+    else:
+        y.view(-1)[:] = z.permute(0, 2, 3, 1).reshape(-1).to(y.dtype)
+    return y
+
+
+def _pool_ref(z):
+    """2x2/2 max pool of NCHW z; returns (pooled, argmax in 0..3 = dy*2+dx, first max wins)."""
+    Bn, C, H, W = z.shape
+    win = z.view(Bn, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(Bn, C, H // 2, W // 2, 4)
+    p, idx = win.max(dim=-1)
+    # torch.max returns the first maximal index on ties
+    return p, idx
+
+
+def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None):
+    """dX of an NHWC conv (wt = W laid out [C][KH][KW][Cout]); optional un-pool epilogue."""
+    if dx.is_cuda:
+        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax)
+        return dx
+    dyt = dy.float().view(g["B"], g["OH"], g["OW"], g["Cout"]).permute(0, 3, 1, 2)
+    w = wt.float().view(g["C"], g["KH"], g["KW"], g["Cout"]).permute(3, 0, 1, 2)
+    dxt = torch.nn.grad.conv2d_input((g["B"], g["C"], g["H"], g["W"]), w, dyt, stride=g["stride"], padding=g["pad"])
+    flat = dxt.permute(0, 2, 3, 1).reshape(-1)
+    if pooled is not None:
+        _unpool_ref(flat, pooled, argmax, g["H"], g["W"], g["C"], dx)
+    else:
+        dx.view(-1)[:] = flat.to(dx.dtype)
+    return dx
+
+
+def conv_wgrad(dz, x, dw, db, g, scale=1.0):
+    """dW[Cout][KH][KW][C] += scale * sum dz (x) im2col(x);  db += scale * sum dz."""
+    if dw.is_cuda:
+        require().conv_wgrad(dz, x, dw, db, *_conv_geom_args(g), scale)
+        return dw
+    xt = x.float().view(g["B"], g["H"], g["W"], g["C"]).permute(0, 3, 1, 2)
+    dzt = dz.float().view(g["B"], g["OH"], g["OW"], g["Cout"]).permute(0, 3, 1, 2)
+    gw = torch.nn.grad.conv2d_weight(xt, (g["Cout"], g["C"], g["KH"], g["KW"]), dzt, stride=g["stride"],
+                                     padding=g["pad"])
+    dw.view(-1)[:] += scale * gw.permute(0, 2, 3, 1).reshape(-1)
+    if db is not None:
+        db += scale * dzt.sum(dim=(0, 2, 3))
+    return dw
+
+
+# -------------------------------------------------------------------- head
+def head_xent(h, w, b, labels, dz, dw, db, dbh, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0):
+    if h.is_cuda:
+        require().head_xent(h, w, b, labels, dz, dw, db, dbh, loss_sum, correct, logits, scale, inv_keep)
+        return
+    hf, wf = h.float(), w.float()
+    lg = hf @ wf.t() + (b.float() if b is not None else 0)
+    if logits is not None:
+        logits.copy_(lg)
+    lse = torch.logsumexp(lg, dim=1)
+    lab = labels.long()
+    if loss_sum is not None:
+        loss_sum += (lse - lg.gather(1, lab[:, None])[:, 0]).sum()
+    if correct is not None:
+        correct += (lg.argmax(1) == lab).sum().to(correct.dtype)
+    p = torch.softmax(lg, dim=1)
+    p[torch.arange(len(lab)), lab] -= 1
+    dl = p * scale
+    dw += dl.t() @ hf
+    if db is not None:
+        db += dl.sum(0)
+    g = (dl @ wf) * (hf > 0).float() * inv_keep
+    dz.copy_(g.to(dz.dtype))
+    if dbh is not None:
+        dbh += g.sum(0)
+
+
+# --------------------------------------------------------------- optimizer
+def opt_pack(segs, work, device_like):
+    return require().opt_pack(segs, work, device_like)
+
+
+def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow, global_step,
+                    gs_inc, done, blob, nseg, nwork):
+    require().apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow,
+                              global_step, gs_inc, done, blob, nseg, nwork)
+
+
+# ------------------------------------------------------------- elementwise
+def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, counter=None, done=None):
+    if dst.is_cuda:
+        require().gather_rows(src, dst, idx, labels_src, labels_dst, seed, counter, done)
+        return dst
+    assert idx is not None, "CPU gather needs explicit indices"
+    rows = src[idx.long()]
+    if src.dtype == torch.uint8:
+        rows = rows.float() / 255.0
+    dst.copy_(rows.reshape(dst.shape).to(dst.dtype))
+    if labels_dst is not None:
+        labels_dst.copy_(labels_src[idx.long()])
+    return dst
+
+
+def uniform_fill(out, lo, hi, seed=0, counter=None, done=None):
+    if out.is_cuda:
+        require().uniform_fill(out, lo, hi, seed, counter, done)
+        return out
+    out.uniform_(lo, hi)
+    return out
+
+
+def cast_(src, dst):
+    if dst.is_cuda:
+        require().cast_(src, dst)
+    else:
+        dst.copy_(src.to(dst.dtype))
+    return dst
+
+
+def softmax_xent(logits, labels_i=None, labels_oh=None, scale=1.0, dlogits=None, loss_rows=None, loss_sum=None,
+                 correct=None, probs=None):
+    if logits.is_cuda:
+        require().softmax_xent(logits, labels_i, labels_oh, scale, dlogits, loss_rows, loss_sum, correct, probs)
+        return
+    y = labels_oh.float() if labels_oh is not None else \
+        torch.nn.functional.one_hot(labels_i.long(), logits.shape[1]).float()
+    lse = torch.logsumexp(logits, 1, keepdim=True)
+    p = torch.exp(logits - lse)
+    rows = (y * (lse - logits)).sum(1)
+    if dlogits is not None:
+        dlogits.copy_((p - y) * scale)
+    if loss_rows is not None:
+        loss_rows.copy_(rows)
+    if loss_sum is not None:
+        loss_sum += rows.sum()
+    if correct is not None:
+        correct += (logits.argmax(1) == y.argmax(1)).sum().to(correct.dtype)
+    if probs is not None:
+        probs.copy_(p)
+
+
+def gan_loss(d_real, d_fake, gen_loss, disc_loss, dz_real_disc, dz_fake_disc, dz_fake_gen, clamp_eps=0.0):
+    if d_real.is_cuda:
+        require().gan_loss(d_real, d_fake, gen_loss, disc_loss, dz_real_disc, dz_fake_disc, dz_fake_gen, clamp_eps)
+        return
+    B = d_real.numel()
+    pr, pf = d_real.view(-1), d_fake.view(-1)
+    if clamp_eps > 0:
+        lr_, lf, lq = torch.log(pr.clamp_min(clamp_eps)), torch.log(pf.clamp_min(clamp_eps)), \
+            torch.log((1 - pf).clamp_min(clamp_eps))
+    else:
+        lr_, lf, lq = torch.log(pr), torch.log(pf), torch.log(1 - pf)
+    gen_loss.fill_(-lf.mean().item())
+    disc_loss.fill_(-(lr_ + lq).mean().item())
+    dz_real_disc.view(-1).copy_(-(1 - pr) / B)
+    dz_fake_disc.view(-1).copy_(pf / B)
+    dz_fake_gen.view(-1).copy_(-(1 - pf) / B)
+
+
+def mse_sigmoid(y, t, loss, dz):
+    if y.is_cuda:
+        require().mse_sigmoid(y, t, loss, dz)
+        return
+    n = y.numel()
+    d = y - t
+    loss.fill_((d * d).mean().item())
+    dz.copy_(2 * d / n * y * (1 - y))
+
+
+def colsum(x, M, N, ld, db, scale=1.0):
+    if x.is_cuda:
+        require().colsum(x, M, N, ld, db, scale)
+        return
+    idx = torch.arange(M).unsqueeze(1) * ld + torch.arange(N).unsqueeze(0)
+    db += scale * x.reshape(-1).float()[idx].sum(0)
+
+
+def act_grad(dy, y, dz, act):
+    if dy.is_cuda:
+        require().act_grad(dy, y, dz, act)
+        return
+    dz.copy_(dy * _act_grad_from_out_ref(y, act))
+
+
+def bias_act(x, bias, out, act, keep=1.0, seed=0, counter=None):
+    if x.is_cuda:
+        require().bias_act(x, bias, out, act, keep, seed, counter)
+        return
+    v = x.float() + (bias.float() if bias is not None else 0)
+    out.copy_(_act_ref(v, act).to(out.dtype))

@@ -1,0 +1,53 @@
+"""Bucketed gradient all-reduce over RCCL (BASELINE.json "ring all-reduce mode").
+
+Gradients live in one flat fp32 buffer ordered by backward completion, so a
+bucket is a contiguous slice.  ``launch(i)`` is called from the step program
+the moment bucket i's last gradient kernel has been *enqueued*: the RCCL
+all-reduce is issued asynchronously (ProcessGroupNCCL runs it on its own HIP
+stream, ordered after the producer kernels by an event), so it overlaps the
+backward kernels that follow on the compute stream.  ``wait()`` joins the
+compute stream to every outstanding bucket before the optimizer.
+
+Optionally the wire format is bf16 (half the xGMI bytes): a cast kernel packs
+the bucket into a bf16 shadow buffer, the all-reduce runs on it, and the fused
+optimizer consumes the bf16 sums directly (``grad16``) with 1/world folded in.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+
+class BucketAllReduce:
+    def __init__(self, flat_grad: torch.Tensor, buckets, group=None, comm_dtype=torch.float32):
+        self.flat = flat_grad
+        self.buckets = list(buckets)
+        self.group = group
+        self.comm_dtype = comm_dtype
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.shadow = None
+        if comm_dtype == torch.bfloat16:
+            self.shadow = torch.empty(flat_grad.numel(), dtype=torch.bfloat16, device=flat_grad.device)
+        self._works = []
+
+    @property
+    def grad16(self):
+        return self.shadow
+
+    def launch(self, i: int):
+        lo, hi = self.buckets[i]
+        if self.shadow is not None:
+            ops.cast_(self.flat[lo:hi], self.shadow[lo:hi])
+            buf = self.shadow[lo:hi]
+        else:
+            buf = self.flat[lo:hi]
+        if self.world == 1:
+            return
+        self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def wait(self):
+        for w in self._works:
+            w.wait()
+        self._works.clear()

@@ -1,0 +1,329 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp32 reference (T3).
+
+Asymmetric operands everywhere (A=I checks with asymmetric B catch C-write
+transposes), odd sizes for masked tails, all operand layouts.
+"""
+import itertools
+
+import pytest
+import torch
+
+import dtfe.ops as ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+def _operand(mat, mode, dtype):
+    """Store logical [rows, K] matrix in the requested mode; return (tensor, ld)."""
+    if mode == ops.KMAJ:
+        t = mat.contiguous()
+        return t.to(DEV, dtype), mat.shape[1]
+    t = mat.t().contiguous()
+    return t.to(DEV, dtype), mat.shape[0]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("amode,bmode", list(itertools.product([0, 1], [0, 1])))
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+def test_gemm_modes_tiles(dtype, amode, bmode, tile):
+    torch.manual_seed(0)
+    M, N, K = 200, 136, 264
+    A = torch.randn(M, K)
+    B = torch.randn(N, K)
+    At, lda = _operand(A, amode, dtype)
+    Bt, ldb = _operand(B, bmode, dtype)
+    out = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+    ops.gemm(At, Bt, out, M=M, N=N, K=K, amode=amode, lda=lda, bmode=bmode, ldb=ldb, tile=tile)
+    ref = At.float().cpu() if amode == 0 else At.float().cpu().t()
+    refb = Bt.float().cpu() if bmode == 0 else Bt.float().cpu().t()
+    exp = ref @ refb.t()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(out.cpu(), exp) < tol
+
+
+def test_gemm_identity_asymmetric():
+    M = N = K = 64
+    A = torch.eye(M)
+    B = torch.arange(N * K, dtype=torch.float32).view(N, K) / 1000.0  # asymmetric
+    out = torch.zeros(M, N, device=DEV)
+    ops.gemm(A.to(DEV), B.to(DEV), out, M=M, N=N, K=K)
+    assert torch.allclose(out.cpu(), B.t(), atol=1e-5)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_gemm_epilogue_bias_act_bf16_out(act):
+    torch.manual_seed(1)
+    M, N, K = 130, 70, 100
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.gemm(A, B, out, M=M, N=N, K=K, bias=bias, act=act)
+    z = A.cpu() @ B.cpu().t() + bias.cpu()
+    exp = [z, torch.relu(z), torch.sigmoid(z), torch.tanh(z)][act]
+    assert _rel(out.cpu(), exp) < 1e-5
+
+
+def test_gemm_split_k_atomic_and_aux():
+    torch.manual_seed(2)
+    M, N, K = 96, 160, 1000
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    out = torch.zeros(M, N, device=DEV)
+    ops.gemm(A, B, out, M=M, N=N, K=K, atomic=True, splits=7)
+    assert _rel(out.cpu(), A.cpu() @ B.cpu().t()) < 1e-5
+    # activation-gradient prologue: x * sigmoid'(y)
+    y = torch.rand(M, N, device=DEV)
+    out2 = torch.empty(M, N, device=DEV)
+    ops.gemm(A, B, out2, M=M, N=N, K=K, aux=y, aux_act=ops.ACT_SIGMOID)
+    exp = (A.cpu() @ B.cpu().t()) * y.cpu() * (1 - y.cpu())
+    assert _rel(out2.cpu(), exp) < 1e-5
+
+
+def test_gemm_ones_row_bias_column():
+    M, N, K = 48, 33, 80
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    out = torch.zeros(M, N, device=DEV)
+    ops.gemm(A, B, out, M=M, N=N, K=K, b_ones_row=N - 1)
+    exp = A.cpu() @ B.cpu().t()
+    exp[:, N - 1] = A.cpu().sum(1)
+    assert _rel(out.cpu(), exp) < 1e-5
+
+
+def _geom(B, H, W, C, Cout, KH, KW, stride, pad):
+    OH = (H + 2 * pad - KH) // stride + 1
+    OW = (W + 2 * pad - KW) // stride + 1
+    return dict(B=B, H=H, W=W, C=C, Cout=Cout, OH=OH, OW=OW, KH=KH, KW=KW, stride=stride, pad=pad)
+
+
+CONV_CASES = [
+    _geom(4, 28, 28, 1, 32, 5, 5, 1, 2),     # MNIST conv1
+    _geom(4, 14, 14, 32, 64, 5, 5, 1, 2),    # MNIST conv2
+    _geom(2, 16, 16, 16, 32, 3, 3, 2, 1),    # ResNet downsample
+    _geom(2, 8, 8, 64, 128, 1, 1, 1, 0),     # 1x1
+]
+
+
+@pytest.mark.parametrize("g", CONV_CASES)
+@pytest.mark.parametrize("pool", [False, True])
+def test_conv_fwd(g, pool):
+    if pool and (g["OH"] % 2 or g["OW"] % 2):
+        pytest.skip("odd output")
+    torch.manual_seed(3)
+    x = torch.randn(g["B"], g["H"], g["W"], g["C"]).to(DEV, torch.bfloat16)
+    w = (torch.randn(g["Cout"], g["KH"], g["KW"], g["C"]) * 0.2).to(DEV, torch.bfloat16)
+    b = torch.randn(g["Cout"], device=DEV)
+    OHp, OWp = (g["OH"] // 2, g["OW"] // 2) if pool else (g["OH"], g["OW"])
+    y = torch.empty(g["B"], OHp, OWp, g["Cout"], device=DEV, dtype=torch.bfloat16)
+    am = torch.empty(g["B"], OHp, OWp, g["Cout"], device=DEV, dtype=torch.uint8) if pool else None
+    ops.conv_fwd(x, w, b, y, am, g, pool=pool, act=ops.ACT_RELU)
+    yr = torch.empty(y.shape, dtype=torch.float32)
+    amr = torch.empty(y.shape, dtype=torch.uint8) if pool else None
+    ops.conv_fwd(x.cpu(), w.cpu(), b.cpu(), yr, amr, g, pool=pool, act=ops.ACT_RELU)
+    assert _rel(y.cpu(), yr) < 2e-2
+    if pool:
+        # argmax only matters where the pooled value is > 0 (ReLU ties at 0 are irrelevant)
+        pos = yr > 0.05
+        agree = (am.cpu()[pos] == amr[pos]).float().mean().item()
+        assert agree > 0.97
+
+
+@pytest.mark.parametrize("g", CONV_CASES[1:])
+def test_conv_dgrad(g):
+    torch.manual_seed(4)
+    dy = torch.randn(g["B"], g["OH"], g["OW"], g["Cout"]).to(DEV, torch.bfloat16)
+    w = (torch.randn(g["Cout"], g["KH"], g["KW"], g["C"]) * 0.2)
+    wt = w.permute(3, 1, 2, 0).contiguous().to(DEV, torch.bfloat16)  # [C][KH][KW][Cout]
+    dx = torch.empty(g["B"], g["H"], g["W"], g["C"], device=DEV, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, wt, dx, g)
+    ref = torch.empty(dx.shape)
+    ops.conv_dgrad(dy.cpu(), wt.cpu(), ref, g)
+    assert _rel(dx.cpu(), ref) < 2e-2
+
+
+def test_conv_dgrad_unpool():
+    g = CONV_CASES[1]
+    torch.manual_seed(5)
+    dy = torch.randn(g["B"], g["OH"], g["OW"], g["Cout"]).to(DEV, torch.bfloat16)
+    wt = (torch.randn(g["C"], g["KH"], g["KW"], g["Cout"]) * 0.2).to(DEV, torch.bfloat16)
+    pooled = torch.randn(g["B"], g["H"], g["W"], g["C"]).to(DEV, torch.bfloat16)
+    am = torch.randint(0, 4, pooled.shape, dtype=torch.uint8).to(DEV)
+    dz = torch.empty(g["B"], 2 * g["H"], 2 * g["W"], g["C"], device=DEV, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, wt, dz, g, pooled=pooled, argmax=am)
+    ref = torch.empty(dz.shape)
+    ops.conv_dgrad(dy.cpu(), wt.cpu(), ref, g, pooled=pooled.cpu(), argmax=am.cpu())
+    assert _rel(dz.cpu(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("g", CONV_CASES)
+def test_conv_wgrad(g):
+    torch.manual_seed(6)
+    x = torch.randn(g["B"], g["H"], g["W"], g["C"]).to(DEV, torch.bfloat16)
+    dz = torch.randn(g["B"], g["OH"], g["OW"], g["Cout"]).to(DEV, torch.bfloat16)
+    dw = torch.zeros(g["Cout"], g["KH"], g["KW"], g["C"], device=DEV)
+    db = torch.zeros(g["Cout"], device=DEV)
+    ops.conv_wgrad(dz, x, dw, db, g, scale=0.5)
+    dwr = torch.zeros(dw.shape)
+    dbr = torch.zeros(g["Cout"])
+    ops.conv_wgrad(dz.cpu(), x.cpu(), dwr, dbr, g, scale=0.5)
+    assert _rel(dw.cpu(), dwr) < 1e-2
+    assert _rel(db.cpu(), dbr) < 1e-2
+
+
+def test_head_xent():
+    torch.manual_seed(7)
+    B, K, NC = 300, 1024, 10
+    h = torch.relu(torch.randn(B, K)).to(DEV, torch.bfloat16)
+    w = (torch.randn(NC, K) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(NC, device=DEV)
+    labels = torch.randint(0, NC, (B,), dtype=torch.int32, device=DEV)
+
+    def run(dev):
+        dz = torch.empty(B, K, device=dev, dtype=torch.bfloat16 if dev == DEV else torch.float32)
+        dw = torch.zeros(NC, K, device=dev)
+        db = torch.zeros(NC, device=dev)
+        dbh = torch.zeros(K, device=dev)
+        loss = torch.zeros(1, device=dev)
+        corr = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.head_xent(h.to(dev), w.to(dev), b.to(dev), labels.to(dev), dz, dw, db, dbh, loss, corr,
+                      scale=1.0 / B, inv_keep=1.25)
+        return [t.cpu() for t in (dz, dw, db, dbh, loss, corr)]
+
+    got, exp = run(DEV), run("cpu")
+    for gt, ex in zip(got[:5], exp[:5]):
+        assert _rel(gt, ex) < 2e-2
+    assert abs(int(got[5]) - int(exp[5])) <= 2
+
+
+def _plan(n, dev):
+    segs = torch.tensor([[0, n, 1, 1, 0, 0]], dtype=torch.int64)
+    work = torch.tensor([[0, 0, 0, 0, 0, 0, n]], dtype=torch.int64)
+    return ops.opt_pack(segs, work, torch.empty(1, device=dev)), 1, 1
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_optimizers_tf1_math(kind):
+    torch.manual_seed(8)
+    n = 5000
+    p0 = torch.randn(n)
+    g = torch.randn(n)
+    p = p0.clone().to(DEV)
+    s1 = (torch.ones(n) if kind == ops.OPT_RMSPROP else torch.zeros(n)).to(DEV)
+    s2 = torch.zeros(n, device=DEV)
+    bp = torch.tensor([0.9, 0.999], device=DEV)
+    gs = torch.zeros(1, dtype=torch.int32, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    blob, ns, nw = _plan(n, DEV)
+    lr, b1, b2, eps, mom, rho = 0.01, 0.9, 0.999, 1e-8, 0.5, 0.9
+    reps = 3
+    for _ in range(reps):
+        ops.apply_gradients(kind, p, g.to(DEV), None, 1.0, s1, s2, lr, b1, b2, eps if kind == 2 else 1e-10, mom, rho,
+                            bp, gs, 1, done, blob, ns, nw)
+    # closed form
+    v = p0.clone()
+    a1 = torch.ones(n) if kind == 3 else torch.zeros(n)
+    a2 = torch.zeros(n)
+    b1p, b2p = 0.9, 0.999
+    for _ in range(reps):
+        if kind == 0:
+            v -= lr * g
+        elif kind == 1:
+            a1 = a1 * mom + g
+            v -= lr * a1
+        elif kind == 2:
+            lr_t = lr * (1 - b2p) ** 0.5 / (1 - b1p)
+            a1 = b1 * a1 + (1 - b1) * g
+            a2 = b2 * a2 + (1 - b2) * g * g
+            v -= lr_t * a1 / (a2.sqrt() + eps)
+            b1p *= b1
+            b2p *= b2
+        else:
+            a1 = rho * a1 + (1 - rho) * g * g
+            a2 = mom * a2 + lr * g / (a1 + 1e-10).sqrt()
+            v -= a2
+    assert torch.allclose(p.cpu(), v, atol=1e-5, rtol=1e-5)
+    assert int(gs.item()) == reps
+    if kind == 2:
+        assert abs(bp[0].item() - 0.9 ** (reps + 1)) < 1e-6
+
+
+def test_optimizer_transposed_copies():
+    R, T, C = 70, 3, 50
+    n = R * T * C
+    p = torch.randn(n, device=DEV)
+    g = torch.zeros(n, device=DEV)
+    w16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    wt16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    segs = torch.tensor([[0, R, T, C, w16.data_ptr(), wt16.data_ptr()]], dtype=torch.int64)
+    work = []
+    for t in range(T):
+        for r0 in range(0, R, 64):
+            for c0 in range(0, C, 64):
+                work.append([1, 0, t, r0, c0, 0, 0])
+    blob = ops.opt_pack(segs, torch.tensor(work, dtype=torch.int64), p)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.apply_gradients(0, p, g, None, 1.0, None, None, 0.1, 0, 0, 0, 0, 0, None, None, 0, done, blob, 1, len(work))
+    torch.cuda.synchronize()
+    assert torch.equal(w16.cpu(), p.cpu().to(torch.bfloat16))
+    exp_t = p.cpu().view(R, T, C).permute(2, 1, 0).reshape(-1).to(torch.bfloat16)
+    assert torch.equal(wt16.cpu(), exp_t)
+
+
+def test_gather_and_noise():
+    src = torch.randint(0, 256, (1000, 784), dtype=torch.uint8, device=DEV)
+    labels = torch.randint(0, 10, (1000,), dtype=torch.int32, device=DEV)
+    idx = torch.randint(0, 1000, (64,), dtype=torch.int32, device=DEV)
+    dst = torch.empty(64, 784, device=DEV, dtype=torch.bfloat16)
+    ld = torch.empty(64, dtype=torch.int32, device=DEV)
+    ops.gather_rows(src, dst, idx, labels, ld)
+    exp = src.cpu()[idx.cpu().long()].float() / 255
+    assert _rel(dst.cpu(), exp) < 1e-2
+    assert torch.equal(ld.cpu(), labels.cpu()[idx.cpu().long()])
+    # device sampling: counter advances once per call
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.gather_rows(src, dst, None, labels, ld, seed=5, counter=ctr, done=done)
+    ops.gather_rows(src, dst, None, labels, ld, seed=5, counter=ctr, done=done)
+    assert int(ctr.item()) == 2
+    z = torch.empty(128, 100, device=DEV)
+    ops.uniform_fill(z, -1.0, 1.0, seed=3, counter=ctr, done=done)
+    assert -1.0 <= z.min().item() and z.max().item() < 1.0 and abs(z.mean().item()) < 0.05
+
+
+def test_softmax_xent_and_losses():
+    torch.manual_seed(9)
+    B, NC = 77, 10
+    lg = torch.randn(B, NC, device=DEV)
+    lab = torch.randint(0, NC, (B,), dtype=torch.int32, device=DEV)
+    outs = {}
+    for dev in (DEV, "cpu"):
+        d = torch.empty(B, NC, device=dev)
+        rows = torch.empty(B, device=dev)
+        s = torch.zeros(1, device=dev)
+        c = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.softmax_xent(lg.to(dev), labels_i=lab.to(dev), scale=1.0 / B, dlogits=d, loss_rows=rows, loss_sum=s,
+                         correct=c)
+        outs[dev] = [t.cpu() for t in (d, rows, s, c)]
+    for a, b in zip(outs[DEV], outs["cpu"]):
+        assert _rel(a, b) < 1e-4
+    # gan + mse
+    pr, pf = torch.rand(128, device=DEV) * 0.9 + 0.05, torch.rand(128, device=DEV) * 0.9 + 0.05
+    res = {}
+    for dev in (DEV, "cpu"):
+        t = [torch.empty(1, device=dev), torch.empty(1, device=dev)] + [torch.empty(128, device=dev) for _ in range(3)]
+        ops.gan_loss(pr.to(dev), pf.to(dev), *t)
+        res[dev] = [x.cpu() for x in t]
+    for a, b in zip(res[DEV], res["cpu"]):
+        assert _rel(a, b) < 1e-4
+    y, tt = torch.rand(256, 784, device=DEV), torch.rand(256, 784, device=DEV)
+    l1, d1 = torch.empty(1, device=DEV), torch.empty_like(y)
+    ops.mse_sigmoid(y, tt, l1, d1)
+    l2, d2 = torch.empty(1), torch.empty(256, 784)
+    ops.mse_sigmoid(y.cpu(), tt.cpu(), l2, d2)
+    assert _rel(l1.cpu(), l2) < 1e-4 and _rel(d1.cpu(), d2) < 1e-4

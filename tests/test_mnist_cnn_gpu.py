@@ -1,0 +1,87 @@
+"""End-to-end numerics of the fused MNIST-CNN step program vs torch autograd (fp32)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+class _Bf16Point(torch.autograd.Function):
+    """Round to bf16 in forward AND backward: mirrors where the kernels store bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+q = _Bf16Point.apply
+
+
+def _reference_grads(trainer):
+    P, n = trainer.P, trainer.names
+    x = trainer.x.float().permute(0, 3, 1, 2).cpu()            # what the kernels consumed
+    y = trainer.labels.long().cpu()
+
+    def w(k):
+        return P.view(n[k]).detach().cpu().to(torch.bfloat16).float().requires_grad_(True)
+
+    def b(k):
+        return P.view(n[k]).detach().cpu().float().requires_grad_(True)
+
+    wc1, wc2, wd1, wo = w("wc1"), w("wc2"), w("wd1"), w("out")
+    bc1, bc2, bd1, bo = b("bc1"), b("bc2"), b("bd1"), b("bout")
+    z = q(F.conv2d(x, wc1.permute(0, 3, 1, 2), bc1, padding=2))
+    z = F.max_pool2d(F.relu(z), 2)
+    z = q(F.conv2d(z, wc2.permute(0, 3, 1, 2), bc2, padding=2))
+    z = F.max_pool2d(F.relu(z), 2)
+    z = z.permute(0, 2, 3, 1).reshape(x.shape[0], -1)           # NHWC flatten, as the kernels
+    h = F.relu(q(z @ wd1.t() + bd1))
+    logits = h @ wo.t() + bo
+    loss = F.cross_entropy(logits, y)
+    loss.backward()
+    return loss.item(), {"wc1": wc1.grad, "wc2": wc2.grad, "wd1": wd1.grad, "out": wo.grad,
+                         "bc1": bc1.grad, "bc2": bc2.grad, "bd1": bd1.grad, "bout": bo.grad}
+
+
+def test_cnn_step_matches_autograd():
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    torch.manual_seed(0)
+    tr = MnistCnnTrainer(64, "cuda", keep_prob=1.0, seed=3)
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    loss_ref, grads = _reference_grads(tr)
+    loss = tr.loss_sum.item() / tr.B
+    assert abs(loss - loss_ref) < 2e-2 * max(1.0, abs(loss_ref))
+    errs = {}
+    for k, gref in grads.items():
+        got = tr.gw[k].detach().cpu()
+        errs[k] = ((got - gref).norm() / (gref.norm() + 1e-12)).item()
+    assert all(e < 3e-2 for e in errs.values()), errs
+
+
+def test_cnn_trains_and_graph_replays():
+    from dtfe.models.mnist_cnn import MnistCnnTrainer, SyntheticMnist
+    from dtfe.utils.graphs import StepGraph
+
+    # a learnable synthetic task: label = brightest of 10 pixel bands
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 64, (4096, 784), generator=g, dtype=torch.uint8)
+    lab = torch.randint(0, 10, (4096,), generator=g, dtype=torch.int32)
+    for i in range(4096):
+        band = int(lab[i])
+        imgs[i, band * 78:(band + 1) * 78] = 255
+    data = SyntheticMnist(0, "cuda", images=imgs, labels=lab)
+    tr = MnistCnnTrainer(128, "cuda", data=data, lr=1e-3)
+    run = StepGraph(tr.step, warmup=2)
+    losses = []
+    for _ in range(60):
+        run()
+        losses.append(tr.loss_sum.item() / tr.B)
+    assert run.graph is not None, run.capture_error
+    assert losses[-1] < 0.5 * losses[0]
+    assert int(tr.global_step.item()) == 60
