@@ -42,7 +42,8 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
           int64_t act, double alpha, double beta, bool atomic, int64_t splits, int64_t tile,
           const optional<Tensor>& aux, int64_t ld_aux, int64_t aux_act, int64_t b_ones_row, double keep, int64_t seed,
           const optional<Tensor>& counter, const optional<Tensor>& pooled, const optional<Tensor>& argmax,
-          int64_t PH, int64_t PW, int64_t PC, const optional<Tensor>& out2, int64_t ldc2, bool out2_trans) {
+          int64_t PH, int64_t PW, int64_t PC, const optional<Tensor>& out2, int64_t ldc2, bool out2_trans,
+          const optional<Tensor>& bias_out) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(out, "out");
@@ -78,6 +79,8 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
     a.up.PH = (int)PH; a.up.PW = (int)PW; a.up.C = (int)PC;
   }
   a.keep = (float)keep; a.seed = (uint64_t)seed; a.counter = ptr_or_null<int64_t>(counter);
+  a.bias_out = ptr_or_null<float>(bias_out);
+  TORCH_CHECK(!a.bias_out || b_ones_row >= 0, "gemm: bias_out needs b_ones_row");
   dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
 }
 
@@ -141,20 +144,20 @@ void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optio
 
 // ------------------------------------------------------------------- head
 void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, const Tensor& labels, const Tensor& dz,
-               const Tensor& dw, const optional<Tensor>& db, const optional<Tensor>& dbh,
-               const optional<Tensor>& loss_sum, const optional<Tensor>& correct, const optional<Tensor>& logits,
-               double scale, double inv_keep) {
+               const Tensor& dl, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
+               const optional<Tensor>& logits, double scale, double inv_keep) {
   check_cuda(h, "h");
+  TORCH_CHECK(dl.scalar_type() == at::kBFloat16 && dl.dim() == 2, "head_xent: dl must be bf16 [B][ld]");
   dtfe::HeadArgs a{};
   a.B = (int)h.size(0); a.K = (int)h.size(1); a.NC = (int)(w.numel() / a.K);
+  TORCH_CHECK(dl.size(1) >= a.NC && dl.size(1) <= 64, "head_xent: dl row must hold NC classes");
   a.h = reinterpret_cast<const dtfe::bf16*>(h.data_ptr());
   a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
   a.b = ptr_or_null<float>(b);
   a.labels = labels.data_ptr<int32_t>();
   a.scale = (float)scale; a.inv_keep = (float)inv_keep;
   a.dz = reinterpret_cast<dtfe::bf16*>(dz.data_ptr());
-  a.dw = dw.data_ptr<float>();
-  a.db = ptr_or_null<float>(db); a.dbh = ptr_or_null<float>(dbh);
+  a.dl = reinterpret_cast<dtfe::bf16*>(dl.data_ptr()); a.ld_dl = (int)dl.size(1);
   a.loss_sum = ptr_or_null<float>(loss_sum); a.correct = ptr_or_null<int32_t>(correct);
   a.logits_out = ptr_or_null<float>(logits);
   dtfe::launch_head_xent(a, cur_stream());
@@ -322,14 +325,42 @@ void bias_act(const Tensor& x, const optional<Tensor>& bias, const Tensor& out, 
   dtfe::launch_bias_act(a, cur_stream());
 }
 
+void lstm_cell_fwd(const Tensor& gates, const Tensor& act, const optional<Tensor>& c_prev, const Tensor& c,
+                   const Tensor& h_out, int64_t ld_h, double forget_bias) {
+  check_cuda(gates, "gates");
+  dtfe::LstmCellArgs a{};
+  a.B = (int)c.size(0); a.H = (int)c.size(1);
+  a.gates = gates.data_ptr<float>(); a.act = act.data_ptr<float>(); a.c_prev = ptr_or_null<float>(c_prev);
+  a.c = c.data_ptr<float>(); a.h_out = h_out.data_ptr<float>(); a.ld_h = ld_h;
+  a.forget_bias = (float)forget_bias;
+  dtfe::launch_lstm_cell_fwd(a, cur_stream());
+}
+
+void lstm_cell_bwd(const Tensor& act, const optional<Tensor>& c_prev, const Tensor& c, const optional<Tensor>& dh,
+                   const optional<Tensor>& dh2, const optional<Tensor>& dc_next, const Tensor& dgates,
+                   const Tensor& dc_prev) {
+  check_cuda(act, "act");
+  dtfe::LstmCellArgs a{};
+  a.B = (int)c.size(0); a.H = (int)c.size(1);
+  a.act = act.data_ptr<float>(); a.c_prev = ptr_or_null<float>(c_prev); a.c = c.data_ptr<float>();
+  a.dh = ptr_or_null<float>(dh); a.dh2 = ptr_or_null<float>(dh2); a.dc_next = ptr_or_null<float>(dc_next);
+  a.dgates = dgates.data_ptr<float>(); a.dc_prev = dc_prev.data_ptr<float>();
+  dtfe::launch_lstm_cell_bwd(a, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dtfe, m) {
+  m.def("lstm_cell_fwd(Tensor gates, Tensor(a!) act, Tensor? c_prev, Tensor(b!) c, Tensor(c!) h_out, int ld_h,"
+        " float forget_bias) -> ()");
+  m.def("lstm_cell_bwd(Tensor act, Tensor? c_prev, Tensor c, Tensor? dh, Tensor? dh2, Tensor? dc_next,"
+        " Tensor(a!) dgates, Tensor(b!) dc_prev) -> ()");
   m.def(
       "gemm(Tensor A, int amode, int lda, Tensor B, int bmode, int ldb, int M, int N, int K, Tensor(a!) out, int ldc,"
       " Tensor? bias, int bias_axis, int act, float alpha, float beta, bool atomic, int splits, int tile,"
       " Tensor? aux, int ld_aux, int aux_act, int b_ones_row, float keep, int seed, Tensor? counter,"
-      " Tensor? pooled, Tensor? argmax, int PH, int PW, int PC, Tensor(b!)? out2, int ldc2, bool out2_trans) -> ()");
+      " Tensor? pooled, Tensor? argmax, int PH, int PW, int PC, Tensor(b!)? out2, int ldc2, bool out2_trans,"
+      " Tensor(c!)? bias_out) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");
@@ -340,9 +371,8 @@ TORCH_LIBRARY(dtfe, m) {
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
       " int OW, int KH, int KW, int stride, int pad, float scale) -> ()");
   m.def(
-      "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!)? db,"
-      " Tensor(d!)? dbh, Tensor(e!)? loss_sum, Tensor(f!)? correct, Tensor(g!)? logits, float scale,"
-      " float inv_keep) -> ()");
+      "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl,"
+      " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep) -> ()");
   m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
   m.def(
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
@@ -381,6 +411,8 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("colsum", &colsum);
   m.impl("act_grad", &act_grad);
   m.impl("bias_act", &bias_act);
+  m.impl("lstm_cell_fwd", &lstm_cell_fwd);
+  m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }
 
 TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) { m.impl("opt_pack", &opt_pack); }

@@ -66,4 +66,18 @@ struct BiasActArgs {
 };
 void launch_bias_act(const BiasActArgs& a, hipStream_t s);
 
+// TF BasicLSTMCell (gate order i, j, f, o; forget_bias added to f) - SURVEY K05/K06.
+// fwd:  gates [B][4H] pre-activations (incl. bias) -> act [B][4H] (sigmoid i, tanh j,
+//       sigmoid f+fb, sigmoid o), c [B][H], h written to h_out (row stride ld_h).
+// bwd:  dh [B][H] (+ dh2 optional), dc_next [B][H] -> dgates [B][4H] (pre-activation),
+//       dc_prev [B][H] (may alias dc_next).
+struct LstmCellArgs {
+  int B, H;
+  const float* gates; float* act; const float* c_prev; float* c; float* h_out; long ld_h;
+  const float* dh; const float* dh2; const float* dc_next; float* dgates; float* dc_prev;
+  float forget_bias;
+};
+void launch_lstm_cell_fwd(const LstmCellArgs& a, hipStream_t s);
+void launch_lstm_cell_bwd(const LstmCellArgs& a, hipStream_t s);
+
 }  // namespace dtfe

@@ -240,6 +240,60 @@ __global__ void bias_act_kernel(BiasActArgs a) {
     else reinterpret_cast<bf16*>(a.out)[i] = f2bf(v);
   }
 }
+__global__ void lstm_cell_fwd_kernel(LstmCellArgs a) {
+  const long n = (long)a.B * a.H;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < n; idx += (long)gridDim.x * 256) {
+    const long b = idx / a.H;
+    const int u = (int)(idx % a.H);
+    const float* g = a.gates + b * 4 * a.H;
+    const float si = sigmoidf_(g[u]);
+    const float tj = tanhf(g[a.H + u]);
+    const float sf = sigmoidf_(g[2 * a.H + u] + a.forget_bias);
+    const float so = sigmoidf_(g[3 * a.H + u]);
+    const float cp = a.c_prev ? a.c_prev[idx] : 0.f;
+    const float c = cp * sf + si * tj;
+    a.c[idx] = c;
+    a.h_out[b * a.ld_h + u] = tanhf(c) * so;
+    float* ac = a.act + b * 4 * a.H;
+    ac[u] = si;
+    ac[a.H + u] = tj;
+    ac[2 * a.H + u] = sf;
+    ac[3 * a.H + u] = so;
+  }
+}
+void launch_lstm_cell_fwd(const LstmCellArgs& a, hipStream_t s) {
+  long blocks = ((long)a.B * a.H + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(blocks), dim3(256), 0, s, a);
+}
+
+__global__ void lstm_cell_bwd_kernel(LstmCellArgs a) {
+  const long n = (long)a.B * a.H;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < n; idx += (long)gridDim.x * 256) {
+    const long b = idx / a.H;
+    const int u = (int)(idx % a.H);
+    const float* ac = a.act + b * 4 * a.H;
+    const float si = ac[u], tj = ac[a.H + u], sf = ac[2 * a.H + u], so = ac[3 * a.H + u];
+    const float c = a.c[idx];
+    const float cp = a.c_prev ? a.c_prev[idx] : 0.f;
+    float dh = a.dh ? a.dh[idx] : 0.f;
+    if (a.dh2) dh += a.dh2[idx];
+    const float tc = tanhf(c);
+    const float dc = (a.dc_next ? a.dc_next[idx] : 0.f) + dh * so * (1.f - tc * tc);
+    float* dg = a.dgates + b * 4 * a.H;
+    dg[u] = dc * tj * si * (1.f - si);
+    dg[a.H + u] = dc * si * (1.f - tj * tj);
+    dg[2 * a.H + u] = dc * cp * sf * (1.f - sf);
+    dg[3 * a.H + u] = dh * tc * so * (1.f - so);
+    a.dc_prev[idx] = dc * sf;
+  }
+}
+void launch_lstm_cell_bwd(const LstmCellArgs& a, hipStream_t s) {
+  long blocks = ((long)a.B * a.H + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(blocks), dim3(256), 0, s, a);
+}
+
 void launch_bias_act(const BiasActArgs& a, hipStream_t s) {
   long n = (long)a.M * a.N;
   long blocks = (n + 255) / 256;

@@ -26,6 +26,8 @@ struct DenseGemmArgs {
   // fused dropout after the activation: keep with prob `keep` (hash RNG of
   // (seed, *counter, element)), scale kept values by 1/keep
   float keep; uint64_t seed; const int64_t* counter;
+  // weight-gradient GEMMs: column b_ones_row (B row of ones) is routed to bias_out[m]
+  float* bias_out;
 };
 
 template <typename T, typename Cfg, int AMODE, int BMODE>
@@ -54,6 +56,11 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
       if (row >= a.M) continue;
       float x = v[j];
       const long o = (long)row * a.ldc + col;
+      if (a.bias_out && col == a.b_ones_row) {  // the ones column = this layer's bias gradient
+        if (a.atomic) atomicAdd(a.bias_out + row, a.alpha * x);
+        else a.bias_out[row] = a.alpha * x;
+        continue;
+      }
       if (a.atomic) {
         atomicAdd(reinterpret_cast<float*>(a.out) + o, a.alpha * x);
         continue;

@@ -10,7 +10,7 @@ struct HeadArgs {
   float scale;        // d(loss)/d(logit) scale: 1 / batch
   float inv_keep;     // dropout scale of h (1 when no dropout)
   bf16* dz;           // [B][K]
-  float* dw; float* db; float* dbh;
+  bf16* dl; int ld_dl;  // d(loss)/d(logit) rows, bf16 [B][ld_dl]
   float* loss_sum; int32_t* correct; float* logits_out;
 };
 

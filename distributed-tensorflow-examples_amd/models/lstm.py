@@ -1,0 +1,126 @@
+"""MNIST row-sequence LSTM classifier (reference ``lstm/distributed_lstm.py``).
+
+x[B,28,28] -> 28 steps of BasicLSTMCell(128, forget_bias=1.0) -> h_T . W_out + b_out
+-> softmax cross-entropy; GradientDescent(0.001); accuracy on 128 test images.
+Variables in creation order: Variable (W_out [128,10]), Variable_1 (b_out [10]),
+rnn/basic_lstm_cell/kernel [156,512] (glorot-uniform), rnn/basic_lstm_cell/bias
+[512] (zeros), Variable_2 (global_step).
+
+MI355X step program (fp32): the per-step gate GEMM reads one [x_t, h_{t-1}]
+row buffer (h_{t-1} is written straight into it by the previous cell kernel),
+so each timestep is one exact-fp32 MFMA GEMM + one fused cell kernel; BPTT is
+one fused cell-backward kernel + one dgrad GEMM per step, and the kernel
+gradient is a single [156 x 512] GEMM reducing over all T*B rows at the end
+(TF accumulates 28 separate MatMul grads).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..optim import OptimizerConfig, VarSpec
+from .base import ModelDef, StepProgram, glorot_uniform_init, normal_init, zeros_init
+
+T, I, H, NC = 28, 28, 128, 10
+LR = 0.001
+
+
+class LstmModel(ModelDef):
+    name = "lstm"
+    default_batch = 128
+    default_steps = 10000
+
+    def __init__(self, lr: float = LR):
+        self.kname, self.bname = "rnn/basic_lstm_cell/kernel", "rnn/basic_lstm_cell/bias"
+        self.specs = [
+            VarSpec("Variable", (H, NC), normal_init(1.0)),
+            VarSpec("Variable_1", (NC,), normal_init(1.0)),
+            VarSpec(self.kname, (I + H, 4 * H), glorot_uniform_init),
+            VarSpec(self.bname, (4 * H,), zeros_init),
+        ]
+        self.var_order = ["Variable", "Variable_1", self.kname, self.bname, "Variable_2"]
+        self.gs_name = "Variable_2"
+        self.opt_groups = [(OptimizerConfig(kind="sgd", lr=lr), [s.name for s in self.specs],
+                            ("beta1_power", "beta2_power"))]
+
+    def program(self, device, batch_size=None, seed: int = 0):
+        return LstmProgram(self, device, batch_size or self.default_batch, seed)
+
+
+class LstmProgram(StepProgram):
+    def __init__(self, model: LstmModel, device, batch_size: int, seed: int = 0):
+        super().__init__(model, device, batch_size, seed)
+        B = batch_size
+        f = dict(device=self.device, dtype=torch.float32)
+        self.xh = torch.zeros(T, B, I + H, **f)      # [x_t, h_{t-1}] rows
+        self.gates = torch.empty(T, B, 4 * H, **f)
+        self.act = torch.empty(T, B, 4 * H, **f)
+        self.c = torch.empty(T, B, H, **f)
+        self.hT = torch.empty(B, H, **f)
+        self.logits = torch.empty(B, NC, **f)
+        self.y = torch.empty(B, NC, **f)
+        self.dlogits = torch.empty(B, NC, **f)
+        self.dh = torch.empty(B, H, **f)
+        self.dc = torch.empty(B, H, **f)
+        self.dg = torch.empty(T, B, 4 * H, **f)
+        self.loss = torch.zeros(1, **f)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=self.device)
+        m = model
+        self.Wo, self.bo = self.P.view("Variable"), self.P.view("Variable_1")
+        self.K, self.b = self.P.view(m.kname), self.P.view(m.bname)
+        self.gWo, self.gbo = self.P.gview("Variable"), self.P.gview("Variable_1")
+        self.gK, self.gb = self.P.gview(m.kname), self.P.gview(m.bname)
+
+    def load_batch(self, batch):
+        x, y = batch
+        B = self.batch_size
+        # batch_x.reshape((B, timesteps, num_input)) (LSTM:127): row t of the image is step t
+        self.xh[:, :, :I].copy_(x.reshape(B, T, I).transpose(0, 1))
+        self.xh[0, :, I:].zero_()
+        self.y.copy_(y.reshape(B, NC))
+
+    def forward(self):
+        B = self.batch_size
+        for t in range(T):
+            ops.gemm(self.xh[t], self.K, self.gates[t], M=B, N=4 * H, K=I + H, bmode=ops.RMAJ, ldb=4 * H,
+                     bias=self.b)
+            if t + 1 < T:
+                h_out, ld = self.xh[t + 1, :, I:], I + H
+            else:
+                h_out, ld = self.hT, H
+            ops.lstm_cell_fwd(self.gates[t], self.act[t], self.c[t - 1] if t > 0 else None, self.c[t], h_out, ld,
+                              1.0)
+        ops.gemm(self.hT, self.Wo, self.logits, M=B, N=NC, K=H, bmode=ops.RMAJ, ldb=NC, bias=self.bo)
+
+    def compute_grads(self):
+        B = self.batch_size
+        self.P.grad.zero_()
+        self.loss.zero_()
+        self.correct.zero_()
+        self.forward()
+        ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
+                         correct=self.correct)
+        ops.gemm(self.hT, self.dlogits, self.gWo, M=H, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ, ldb=NC)
+        ops.colsum(self.dlogits, B, NC, NC, self.gbo)
+        ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
+        self.dc.zero_()
+        Kh = self.K[I:]  # recurrent rows [H][4H]
+        for t in range(T - 1, -1, -1):
+            ops.lstm_cell_bwd(self.act[t], self.c[t - 1] if t > 0 else None, self.c[t], self.dh, None, self.dc,
+                              self.dg[t], self.dc)
+            if t > 0:
+                ops.gemm(self.dg[t], Kh, self.dh, M=B, N=H, K=4 * H, bmode=ops.KMAJ, ldb=4 * H)
+        ops.gemm(self.xh, self.dg, self.gK, M=I + H, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H, bmode=ops.RMAJ,
+                 ldb=4 * H)
+        ops.colsum(self.dg, T * B, 4 * H, 4 * H, self.gb)
+        return {"loss": self.loss / B}
+
+    def evaluate(self, images, labels) -> float:
+        """accuracy = mean(argmax(softmax(logits)) == argmax(Y)) (LSTM:98-100, 134-138)."""
+        n = images.shape[0]
+        assert n == self.batch_size, "evaluation batch must equal the program batch"
+        self.load_batch((images, labels))
+        self.forward()
+        self.correct.zero_()
+        ops.softmax_xent(self.logits, labels_oh=self.y, correct=self.correct)
+        return int(self.correct.item()) / n

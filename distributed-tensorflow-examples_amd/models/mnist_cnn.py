@@ -16,9 +16,11 @@ one flat buffer), captured into one hipGraph:
   conv1/pool  implicit-GEMM MFMA, bias+ReLU+2x2 max-pool+argmax in registers
   conv2/pool  same
   fc1         MFMA GEMM, bias+ReLU+dropout epilogue
-  head        fc2 + softmax-xent + fc2 backward + dropout/ReLU grad (+ fc1 bias grad)
+  head        fc2 + softmax-xent + dlogit rows + dropout/ReLU grad (one wave per row)
+  head wgrad  split-K MFMA GEMM dlogit^T . H, bias grad through a ones column
   fc1 dgrad   MFMA GEMM with the un-pool(argmax2)+ReLU' epilogue -> dZ2 full-res
-  fc1 wgrad   MFMA GEMM (both operands via ds_read_b64_tr_b16)
+  fc1 wgrad   MFMA GEMM (both operands via ds_read_b64_tr_b16), fc1 bias grad as
+              its ones column
   conv2 dgrad implicit-GEMM with the un-pool(argmax1)+ReLU' epilogue -> dZ1
   conv2/conv1 wgrad  split-K implicit GEMM, bias grad as an extra ones column
   Adam        one fused TF1 Adam launch, writes bf16 + transposed bf16 copies
@@ -146,6 +148,7 @@ class MnistCnnTrainer:
         self.a2 = torch.empty(B, 7, 7, C2, device=d, dtype=torch.uint8)
         self.h = torch.empty(B, FC, device=d, dtype=bf)
         self.dzf = torch.empty(B, FC, device=d, dtype=bf)
+        self.dl = torch.empty(B, 16, device=d, dtype=bf)      # dlogit rows (10 classes, padded to 16)
         self.dz2 = torch.empty(B, 14, 14, C2, device=d, dtype=bf)
         self.dz1 = torch.empty(B, IMG, IMG, C1, device=d, dtype=bf)
         self.loss_sum = torch.zeros(1, device=d)
@@ -179,14 +182,18 @@ class MnistCnnTrainer:
         K1 = 7 * 7 * C2
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
                  keep=self.keep, seed=self.seed + 2, counter=self.data_ctr)
-        ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.gw["out"], self.gw["bout"],
-                      self.gw["bd1"], self.loss_sum, self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
+        ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
+                      self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
+        # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
+        ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
+                 bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
+                 splits=max(1, min(16, B // 128)), tile=4)
         # fc1 dgrad -> dZ2 (full resolution, un-pooled through argmax2, ReLU-masked)
         ops.gemm(self.dzf, self.wt["wd1"], self.dz2, M=B, N=K1, K=FC, pooled=self.p2, argmax=self.a2, PH=7, PW=7,
                  PC=C2)
-        # fc1 wgrad: dW[1024][3136] = dZf^T . P2
-        ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
-                 ldb=K1)
+        # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
+        ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
+                 ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
         if self.allreduce is not None:
             self.allreduce.launch(0)
         ops.conv_dgrad(self.dz2, self.wt["wc2"], self.dz1, self.g2, pooled=self.p1, argmax=self.a1)

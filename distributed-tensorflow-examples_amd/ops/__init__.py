@@ -71,11 +71,13 @@ def _mat(t, mode, rows, K, ld):
 def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=None, bias=None, bias_axis=0,
          act=ACT_NONE, alpha=1.0, beta=0.0, atomic=False, splits=1, tile=None, aux=None, ld_aux=None, aux_act=0,
          b_ones_row=-1, keep=1.0, seed=0, counter=None, pooled=None, argmax=None, PH=0, PW=0, PC=0, out2=None,
-         ldc2=0, out2_trans=False):
+         ldc2=0, out2_trans=False, bias_out=None):
     """out[M,N] = epilogue( A(m,k) . B(n,k) ).
 
     A(m,k) = A[m*lda+k] (KMAJ) or A[k*lda+m] (RMAJ); likewise B(n,k).
     Epilogue order: alpha*acc, +bias, act, dropout(keep), *act'(aux), [unpool | +beta*out], store.
+    b_ones_row >= 0 makes B row n=b_ones_row all ones; with bias_out that output
+    column goes to bias_out[m] (a weight-gradient GEMM producing the bias gradient).
     """
     if lda is None:
         lda = K if amode == KMAJ else M
@@ -90,14 +92,24 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
             tile = pick_tile(M, N)
         require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
                        splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
-                       PC, out2, ldc2, out2_trans)
+                       PC, out2, ldc2, out2_trans, bias_out)
         return out
     # CPU reference
     a = _mat(A, amode, M, K, lda)
-    b = _mat(B, bmode, N, K, ldb)
     if b_ones_row >= 0:
-        b[b_ones_row, :] = 1.0
+        b = _mat(B, bmode, b_ones_row, K, ldb) if b_ones_row > 0 else torch.zeros(0, K)
+        b = torch.cat([b, torch.ones(1, K), _mat_tail(B, bmode, b_ones_row + 1, N, K, ldb)], 0)
+    else:
+        b = _mat(B, bmode, N, K, ldb)
     acc = a @ b.t()
+    if bias_out is not None:
+        if atomic:
+            bias_out += alpha * acc[:, b_ones_row]
+        else:
+            bias_out.copy_(alpha * acc[:, b_ones_row])
+        keep_cols = [c for c in range(N) if c != b_ones_row]
+        acc = acc[:, keep_cols]
+        N = len(keep_cols)
     oflat = out.view(-1)
     oidx = torch.arange(M).unsqueeze(1) * ldc + torch.arange(N).unsqueeze(0)
     if atomic:
@@ -124,6 +136,19 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
             (torch.arange(M).unsqueeze(1) * ldc2 + torch.arange(N).unsqueeze(0))
         o2[idx2] = x.to(out2.dtype)
     return out
+
+
+def _mat_tail(t, mode, r0, rows, K, ld):
+    """Rows r0..rows-1 of the logical [rows, K] operand (those that exist in memory)."""
+    if r0 >= rows:
+        return torch.zeros(0, K)
+    flat = t.reshape(-1).float()
+    r = torch.arange(r0, rows)
+    if mode == KMAJ:
+        idx = r.unsqueeze(1) * ld + torch.arange(K).unsqueeze(0)
+    else:
+        idx = torch.arange(K).unsqueeze(0) * ld + r.unsqueeze(1)
+    return flat[idx]
 
 
 def _unpool_ref(g, pooled, argmax, PH, PW, C, dz):
@@ -210,9 +235,11 @@ def conv_wgrad(dz, x, dw, db, g, scale=1.0):
 
 
 # -------------------------------------------------------------------- head
-def head_xent(h, w, b, labels, dz, dw, db, dbh, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0):
+def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0):
+    """Per-row classifier head: logits, softmax-xent (loss/correct sums), dlogit rows (bf16 [B][ld] into
+    ``dl``) and dZ = (dlogit . W) * inv_keep * (h > 0).  dW/db come from a wgrad GEMM over ``dl``."""
     if h.is_cuda:
-        require().head_xent(h, w, b, labels, dz, dw, db, dbh, loss_sum, correct, logits, scale, inv_keep)
+        require().head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits, scale, inv_keep)
         return
     hf, wf = h.float(), w.float()
     lg = hf @ wf.t() + (b.float() if b is not None else 0)
@@ -226,14 +253,11 @@ def head_xent(h, w, b, labels, dz, dw, db, dbh, loss_sum, correct, logits=None, 
         correct += (lg.argmax(1) == lab).sum().to(correct.dtype)
     p = torch.softmax(lg, dim=1)
     p[torch.arange(len(lab)), lab] -= 1
-    dl = p * scale
-    dw += dl.t() @ hf
-    if db is not None:
-        db += dl.sum(0)
-    g = (dl @ wf) * (hf > 0).float() * inv_keep
+    d = p * scale
+    dl.zero_()
+    dl[:, : d.shape[1]] = d.to(dl.dtype)
+    g = (d @ wf) * (hf > 0).float() * inv_keep
     dz.copy_(g.to(dz.dtype))
-    if dbh is not None:
-        dbh += g.sum(0)
 
 
 # --------------------------------------------------------------- optimizer
@@ -349,3 +373,33 @@ def bias_act(x, bias, out, act, keep=1.0, seed=0, counter=None):
         return
     v = x.float() + (bias.float() if bias is not None else 0)
     out.copy_(_act_ref(v, act).to(out.dtype))
+
+
+# -------------------------------------------------------------------- LSTM
+def lstm_cell_fwd(gates, act, c_prev, c, h_out, ld_h, forget_bias=1.0):
+    """TF BasicLSTMCell step on pre-activation gates [B,4H] (order i, j, f, o)."""
+    if gates.is_cuda:
+        require().lstm_cell_fwd(gates, act, c_prev, c, h_out, ld_h, forget_bias)
+        return
+    H = c.shape[1]
+    i, j, f, o = gates.split(H, dim=1)
+    si, tj, sf, so = torch.sigmoid(i), torch.tanh(j), torch.sigmoid(f + forget_bias), torch.sigmoid(o)
+    cn = (c_prev * sf if c_prev is not None else 0) + si * tj
+    c.copy_(cn)
+    act.copy_(torch.cat([si, tj, sf, so], dim=1))
+    h_out.copy_(torch.tanh(cn) * so)  # h_out is a [B, H] (possibly strided) view
+
+
+def lstm_cell_bwd(act, c_prev, c, dh, dh2, dc_next, dgates, dc_prev):
+    if act.is_cuda:
+        require().lstm_cell_bwd(act, c_prev, c, dh, dh2, dc_next, dgates, dc_prev)
+        return
+    H = c.shape[1]
+    si, tj, sf, so = act.split(H, dim=1)
+    d = (dh if dh is not None else 0) + (dh2 if dh2 is not None else 0)
+    tc = torch.tanh(c)
+    dc = (dc_next if dc_next is not None else 0) + d * so * (1 - tc * tc)
+    cp = c_prev if c_prev is not None else torch.zeros_like(c)
+    dgates.copy_(torch.cat([dc * tj * si * (1 - si), dc * si * (1 - tj * tj), dc * cp * sf * (1 - sf),
+                            d * tc * so * (1 - so)], dim=1))
+    dc_prev.copy_(dc * sf)

@@ -1,0 +1,393 @@
+"""The shared ``main(_)`` of every example script.
+
+``run(model_name, argv)`` reproduces the reference scripts' behaviour once,
+for every model (the reference copy-pastes it three times, GAN/ENC/LSTM):
+
+* ``--job_name=ps``: host this task's variable shard, serve the workers, count
+  done signals (``ps %d received done %d`` / ``ps %d: quitting``);
+* ``--job_name=worker``: build the step program, join the Supervisor (chief =
+  task 0), pull -> compute gradients -> push/pull per step printing
+  ``Global step %d Local step %d  AvgTime: %3.2fms``, print ``Total Time``,
+  (LSTM) ``Test-Accuracy``, signal done to every ps, stop.
+
+plus the north-star modes: ``--sync`` (sync SGD with a chief over the ps) and
+``--mode=allreduce`` (ring all-reduce data parallelism, no ps).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ckpt
+from .data.mnist import DeviceBatcher, read_data_sets
+from .models.autoencoder import AutoencoderModel
+from .models.gan import LR as GAN_LR, GanModel
+from .models.lstm import LR as LSTM_LR, LstmModel
+from .models.softmax_reg import SoftmaxRegressionModel
+from .models.autoencoder import LR as ENC_LR
+from .optim import Optimizer
+from .parallel.allreduce import BucketAllReduce
+from .parallel.cluster import ClusterSpec, Server
+from .parallel.placement import round_robin
+from .parallel.ps import PSClient, PSServer, Shard, wait_for_init
+from .parallel.supervisor import Supervisor
+from .utils import flags as flagmod
+from .utils.graphs import StepGraph
+
+MODELS = {
+    "gan": (GanModel, GAN_LR),
+    "encoder": (AutoencoderModel, ENC_LR),
+    "lstm": (LstmModel, LSTM_LR),
+    "softmax": (SoftmaxRegressionModel, 0.01),
+}
+
+
+def _print(*args):
+    print(*args, flush=True)
+
+
+def resolve_device(flag: str, local_rank: int = 0):
+    if flag == "cpu" or (flag == "auto" and not torch.cuda.is_available()):
+        return torch.device("cpu")
+    if not torch.cuda.is_available():
+        raise RuntimeError("--device=cuda but no GPU is visible")
+    n = torch.cuda.device_count()
+    return torch.device("cuda", local_rank % max(n, 1))
+
+
+def resolve_backend(flag: str, device) -> str:
+    if flag != "auto":
+        return flag
+    return "nccl" if device.type == "cuda" else "gloo"
+
+
+# ------------------------------------------------------------------ logging
+def step_line(step, local_step, ms, py2=False):
+    parts = ("Global step %d" % step, "Local step %d" % local_step, " AvgTime: %3.2fms" % ms)
+    return repr(parts) if py2 else " ".join(parts)
+
+
+def model_step_hook(model, step, metrics, log):
+    if model.name == "gan" and (step % 1000 == 0 or step == 1):
+        log("Step %i: Generator Loss: %f, Discriminator Loss: %f"
+            % (step, float(metrics["gen_loss"].item()), float(metrics["disc_loss"].item())))
+
+
+class MetricsLog:
+    def __init__(self, path):
+        self.f = open(path, "a") if path else None
+
+    def write(self, **kw):
+        if self.f:
+            self.f.write(json.dumps(kw) + "\n")
+            self.f.flush()
+
+
+# ---------------------------------------------------------------- batching
+class Feeder:
+    """next batch for a program: host next_batch on CPU, HBM gather on GPU."""
+
+    def __init__(self, data, program, device):
+        self.B = program.batch_size
+        self.dev = None
+        if device.type == "cuda":
+            self.dev = DeviceBatcher(data.train, device, self.B, one_hot=True)
+        self.data = data
+
+    def next(self):
+        if self.dev is not None:
+            return self.dev.next_batch()
+        x, y = self.data.train.next_batch(self.B)
+        return torch.from_numpy(x), torch.from_numpy(y)
+
+
+# ---------------------------------------------------------- checkpoint glue
+def var_list(model):
+    shapes = model.tf_shapes()
+    out = []
+    for n in model.var_order:
+        if n == model.gs_name:
+            out.append((n, ckpt.DT_INT32, []))
+        else:
+            out.append((n, ckpt.DT_FLOAT, list(shapes[n])))
+    return out
+
+
+def tensors_from_flat(model, P, optimizers, gs: int):
+    """Checkpoint dict (TF names and layouts) from a FlatParams + its optimizers."""
+    out = {}
+    for s in model.specs:
+        out[s.name] = model.to_tf(s.name, P.view(s.name).detach().cpu())
+    for o in optimizers:
+        for k, t in o.slot_tensors().items():
+            base = k.rsplit("/", 1)[0]  # "<var>/Adam" -> "<var>"; beta powers have no slash
+            if "/" in k and base in P.offsets:
+                t = model.to_tf(base, t)
+            out[k] = t
+    out[model.gs_name] = torch.tensor(int(gs), dtype=torch.int32)
+    return out
+
+
+def load_flat_from_tensors(model, P, optimizers, tensors):
+    for s in model.specs:
+        if s.name in tensors:
+            P.view(s.name).copy_(model.from_tf(s.name, tensors[s.name]).reshape(s.shape).to(P.device))
+    conv = {}
+    for k, t in tensors.items():
+        if "/" in k:
+            base = k.rsplit("/", 1)[0]
+            if base in P.offsets:
+                t = model.from_tf(base, t)
+        conv[k] = t
+    for o in optimizers:
+        o.load_slot_tensors(conv)
+    P.refresh_copies()
+    return int(tensors.get(model.gs_name, torch.tensor(0)).item())
+
+
+# --------------------------------------------------------------------- ps
+def _shard_layout(model, num_ps):
+    placement = round_robin(model.var_order, num_ps)
+    shard_specs = {k: [s for s in model.specs if placement[s.name] == k] for k in range(num_ps)}
+    return placement, shard_specs
+
+
+def run_ps(flags, model, server, device, log):
+    placement, shard_specs = _shard_layout(model, len(server.cluster.ps))
+    k = server.task_index
+    gs_here = placement[model.gs_name] == k
+    shard = Shard(shard_specs[k], model.opt_groups, device, gs_here, model.gs_increments)
+    comm = "cpu" if server.backend == "gloo" else device
+    PSServer(server, shard, num_workers=flags.workers, sync=flags.sync,
+             replicas_to_aggregate=flags.replicas_to_aggregate, hogwild=flags.hogwild, comm_device=comm,
+             log=log).serve_forever()
+
+
+def ps_state(client, model, shard_specs, placement):
+    """Gather every shard's params + slots from the ps tasks into one TF-named dict."""
+    states, gs = client.fetch_state()
+    out = {}
+    for k, flat in states.items():
+        mirror = Shard(shard_specs[k], model.opt_groups, "cpu", False, model.gs_increments)
+        mirror.load_state_payload(flat)
+        out.update(tensors_from_flat(model, mirror.P, mirror.opts, gs))
+    out[model.gs_name] = torch.tensor(int(gs), dtype=torch.int32)
+    return out, gs
+
+
+def ps_restore(client, model, shard_specs, tensors):
+    states = {}
+    gs = int(tensors.get(model.gs_name, torch.tensor(0)).item())
+    for k, specs in shard_specs.items():
+        if not specs:
+            continue
+        mirror = Shard(specs, model.opt_groups, "cpu", False, model.gs_increments)
+        load_flat_from_tensors(model, mirror.P, mirror.opts, tensors)
+        states[k] = mirror.state_payload()
+    client.set_state(states, gs)
+
+
+def run_worker_ps(flags, model, server, device, log):
+    cl = server.cluster
+    placement, shard_specs = _shard_layout(model, len(cl.ps))
+    gs_rank = cl.rank_of("ps", placement[model.gs_name])
+    prog = model.program(device, flags.batch_size, seed=flags.seed)
+    comm = "cpu" if server.backend == "gloo" else device
+    client = PSClient(server, prog.P, placement, shard_specs, gs_rank, model.opt_groups, comm_device=comm)
+    is_chief = server.task_index == 0
+    sv = Supervisor(
+        is_chief, flags.model_dir,
+        state_fn=lambda: ps_state(client, model, shard_specs, placement),
+        restore_fn=lambda t: ps_restore(client, model, shard_specs, t),
+        init_fn=client.init_variables,
+        wait_fn=lambda: wait_for_init(client),
+        var_list_fn=lambda: var_list(model),
+        gs_fn=lambda: client.status()[1],
+        save_model_secs=flags.save_model_secs, save_summaries_secs=flags.save_summaries_secs,
+        max_to_keep=flags.max_to_keep, log=log)
+    data = read_data_sets("" if flags.synthetic else flags.data_dir, one_hot=True,
+                          seed=flags.seed * 1000 + server.task_index + 1, log=log)
+    feeder = Feeder(data, prog, device)
+    metrics_log = MetricsLog(flags.metrics_jsonl)
+    begin_time = time.time()
+    sv.prepare()
+    if flags.reinit_on_join:
+        # GAN:181 / ENC:160: every worker re-runs init, clobbering restore + progress
+        prog.P.initialize(flags.seed)
+        client.init_variables()
+    client.pull()
+    step = 0
+    local_step = 0
+    try:
+        while not sv.should_stop() and step < flags.num_steps:
+            t0 = time.time()
+            prog.load_batch(feeder.next())
+            metrics = prog.compute_grads()
+            step = client.push_pull(prog.P.grad)
+            elapsed = time.time() - t0
+            if local_step % flags.log_every == 0:
+                log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
+            model_step_hook(model, step, metrics, log)
+            metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000,
+                              images_per_sec=prog.batch_size / max(elapsed, 1e-9))
+            local_step += 1
+        log("Total Time: %3.2fs" % float(time.time() - begin_time))
+        if model.name == "lstm":
+            client.pull()
+            test_len = 128
+            acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
+                                torch.from_numpy(data.test.labels[:test_len]).to(device))
+            log("Test-Accuracy: %2.4f" % acc)
+        client.done()
+    finally:
+        sv.stop()
+
+
+# --------------------------------------------------------------- allreduce
+def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
+    prog = model.program(device, flags.batch_size, seed=flags.seed)
+    gstep = torch.zeros(1, dtype=torch.int32, device=device)
+    opts = []
+    for i, (cfg, var_list_, bp) in enumerate(model.opt_groups):
+        cfg.lr = flags.learning_rate if flags.learning_rate is not None else cfg.lr
+        opts.append(Optimizer(cfg, prog.P, var_list=var_list_, global_step=gstep, beta_power_names=bp))
+    is_chief = rank == 0
+    sv = Supervisor(
+        is_chief, flags.model_dir,
+        state_fn=lambda: (tensors_from_flat(model, prog.P, opts, int(gstep.item())), int(gstep.item())),
+        restore_fn=lambda t: gstep.fill_(load_flat_from_tensors(model, prog.P, opts, t)),
+        init_fn=lambda: None, wait_fn=lambda: None, var_list_fn=lambda: var_list(model),
+        gs_fn=lambda: int(gstep.item()),
+        save_model_secs=flags.save_model_secs, save_summaries_secs=flags.save_summaries_secs,
+        max_to_keep=flags.max_to_keep, log=log)
+    sv.prepare()
+    ar = None
+    if world > 1:
+        # chief's (possibly restored) state is the starting point of every replica
+        dist.broadcast(prog.P.master, src=0, group=group)
+        dist.broadcast(gstep, src=0, group=group)
+        for o in opts:
+            for b in (o.s1, o.s2, o.beta_pow):
+                if b is not None:
+                    dist.broadcast(b, src=0, group=group)
+        prog.P.refresh_copies()
+        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), group=group,
+                             comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
+    data = read_data_sets("" if flags.synthetic else flags.data_dir, one_hot=True, seed=flags.seed * 1000 + rank + 1,
+                          log=log if is_chief else (lambda *_: None))
+    feeder = Feeder(data, prog, device)
+    metrics_log = MetricsLog(flags.metrics_jsonl)
+
+    state = {}
+
+    def train_step():
+        state["m"] = prog.compute_grads()
+        g16 = None
+        if ar is not None:
+            for i in range(len(ar.buckets)):
+                ar.launch(i)
+            ar.wait()
+            g16 = ar.grad16
+        for i, o in enumerate(opts):
+            last = i == len(opts) - 1
+            o.step(grad16=g16, gscale=1.0 / world, gs_inc=model.gs_increments if last else 0) if g16 is not None \
+                else o.step(gscale=1.0 / world, gs_inc=model.gs_increments if last else 0)
+
+    runner = StepGraph(train_step, warmup=2,
+                       enabled=device.type == "cuda" and world == 1 and flags.hip_graph)
+    begin_time = time.time()
+    step = int(gstep.item())
+    local_step = 0
+    try:
+        while not sv.should_stop() and step < flags.num_steps:
+            t0 = time.time()
+            prog.load_batch(feeder.next())
+            runner()
+            step = int(gstep.item())
+            elapsed = time.time() - t0
+            if local_step % flags.log_every == 0:
+                log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
+            if "m" in state:
+                model_step_hook(model, step, state["m"], log)
+            metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000,
+                              images_per_sec=prog.batch_size * world / max(elapsed, 1e-9))
+            local_step += 1
+        log("Total Time: %3.2fs" % float(time.time() - begin_time))
+        if model.name == "lstm" and is_chief:
+            test_len = 128
+            acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
+                                torch.from_numpy(data.test.labels[:test_len]).to(device))
+            log("Test-Accuracy: %2.4f" % acc)
+    finally:
+        sv.stop()
+    return prog, opts, gstep
+
+
+def _buckets(P, bucket_elems: int = 4 << 20):
+    """Contiguous gradient buckets of ~16 MB fp32 (back of the flat buffer first = backward order)."""
+    total = P.total
+    b = []
+    hi = total
+    while hi > 0:
+        lo = max(0, hi - bucket_elems)
+        b.append((lo, hi))
+        hi = lo
+    return b
+
+
+# ------------------------------------------------------------------- entry
+def run(model_name: str, argv=None, log=_print):
+    cls, lr = MODELS[model_name]
+    m0 = cls()
+    flags = flagmod.parse(argv, model_defaults=dict(batch_size=m0.default_batch, num_steps=m0.default_steps,
+                                                    learning_rate=lr), prog="distributed_%s.py" % model_name)
+    model = cls(lr=flags.learning_rate)
+    torch.manual_seed(flags.seed)
+    np.random.seed(flags.seed)
+    mode = flags.mode or ("ps" if flags.ps_hosts else ("allreduce" if flags.worker_hosts else "local"))
+    local_rank = int(os.environ.get("LOCAL_RANK", flags.task_index if flags.job_name == "worker" else 0))
+    device = resolve_device(flags.device, local_rank)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    backend = resolve_backend(flags.backend, device)
+    if mode == "local":
+        run_allreduce(flags, model, device, log)
+        return 0
+    cluster = ClusterSpec.from_flags(flags.ps_hosts, flags.worker_hosts)
+    if mode == "ps":
+        if not cluster.ps:
+            raise SystemExit("--mode=ps needs --ps_hosts")
+        server = Server(cluster, flags.job_name, flags.task_index, backend=backend,
+                        device=device if backend == "nccl" else None)
+        try:
+            if flags.job_name == "ps":
+                run_ps(flags, model, server, device, log)
+            elif flags.job_name == "worker":
+                run_worker_ps(flags, model, server, device, log)
+            else:
+                raise SystemExit("--job_name must be 'ps' or 'worker'")
+        finally:
+            server.shutdown()
+        return 0
+    # ring all-reduce: workers only
+    if flags.job_name == "ps":
+        log("ps %d: nothing to serve in --mode=allreduce; quitting" % flags.task_index)
+        return 0
+    cluster = ClusterSpec([], cluster.worker)
+    server = Server(cluster, "worker", flags.task_index, backend=backend,
+                    device=device if backend == "nccl" else None)
+    try:
+        run_allreduce(flags, model, device, log, world=cluster.world_size, rank=server.rank)
+    finally:
+        server.shutdown()
+    return 0
+
+
+def main(model_name: str):
+    sys.exit(run(model_name, sys.argv[1:]))

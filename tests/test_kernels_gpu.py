@@ -186,19 +186,24 @@ def test_head_xent():
 
     def run(dev):
         dz = torch.empty(B, K, device=dev, dtype=torch.bfloat16 if dev == DEV else torch.float32)
-        dw = torch.zeros(NC, K, device=dev)
-        db = torch.zeros(NC, device=dev)
-        dbh = torch.zeros(K, device=dev)
+        dl = torch.empty(B, 16, device=dev, dtype=torch.bfloat16)
         loss = torch.zeros(1, device=dev)
         corr = torch.zeros(1, dtype=torch.int32, device=dev)
-        ops.head_xent(h.to(dev), w.to(dev), b.to(dev), labels.to(dev), dz, dw, db, dbh, loss, corr,
+        logits = torch.empty(B, NC, device=dev)
+        ops.head_xent(h.to(dev), w.to(dev), b.to(dev), labels.to(dev), dz, dl, loss, corr, logits,
                       scale=1.0 / B, inv_keep=1.25)
-        return [t.cpu() for t in (dz, dw, db, dbh, loss, corr)]
+        # layer weight/bias grads: split-K wgrad GEMM over the dlogit rows with a ones column
+        dw = torch.zeros(NC, K, device=dev)
+        db = torch.zeros(NC, device=dev)
+        ops.gemm(dl, h.to(dev), dw, M=NC, N=K + 1, K=B, amode=ops.RMAJ, lda=16, bmode=ops.RMAJ, ldb=K, ldc=K,
+                 b_ones_row=K, bias_out=db, atomic=True, splits=3, tile=4)
+        return [t.cpu() for t in (dz, dl, dw, db, loss, logits, corr)]
 
     got, exp = run(DEV), run("cpu")
-    for gt, ex in zip(got[:5], exp[:5]):
+    for gt, ex in zip(got[:6], exp[:6]):
         assert _rel(gt, ex) < 2e-2
-    assert abs(int(got[5]) - int(exp[5])) <= 2
+    assert float(got[1][:, 10:].abs().max()) == 0.0
+    assert abs(int(got[6]) - int(exp[6])) <= 2
 
 
 def _plan(n, dev):

@@ -34,10 +34,11 @@ def _reference_grads(trainer):
 
     wc1, wc2, wd1, wo = w("wc1"), w("wc2"), w("wd1"), w("out")
     bc1, bc2, bd1, bo = b("bc1"), b("bc2"), b("bd1"), b("bout")
-    z = q(F.conv2d(x, wc1.permute(0, 3, 1, 2), bc1, padding=2))
-    z = F.max_pool2d(F.relu(z), 2)
-    z = q(F.conv2d(z, wc2.permute(0, 3, 1, 2), bc2, padding=2))
-    z = F.max_pool2d(F.relu(z), 2)
+    # the kernels pool the fp32 accumulators and round the pooled value (argmax on exact values)
+    z = F.conv2d(x, wc1.permute(0, 3, 1, 2), bc1, padding=2)
+    z = q(F.max_pool2d(F.relu(z), 2))
+    z = F.conv2d(z, wc2.permute(0, 3, 1, 2), bc2, padding=2)
+    z = q(F.max_pool2d(F.relu(z), 2))
     z = z.permute(0, 2, 3, 1).reshape(x.shape[0], -1)           # NHWC flatten, as the kernels
     h = F.relu(q(z @ wd1.t() + bd1))
     logits = h @ wo.t() + bo
@@ -61,7 +62,7 @@ def test_cnn_step_matches_autograd():
     for k, gref in grads.items():
         got = tr.gw[k].detach().cpu()
         errs[k] = ((got - gref).norm() / (gref.norm() + 1e-12)).item()
-    assert all(e < 3e-2 for e in errs.values()), errs
+    assert all(e < 3e-2 for e in errs.values()), sorted(errs.items(), key=lambda kv: -kv[1])
 
 
 def test_cnn_trains_and_graph_replays():
