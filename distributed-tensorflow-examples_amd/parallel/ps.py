@@ -71,6 +71,19 @@ class Shard:
             self.gs += self.gs_increments
         self.version += 1
 
+    def reset_optimizer_state(self):
+        for o in self.opts:
+            if o.s1 is not None:
+                o.s1.fill_(1.0 if o.cfg.kind == "rmsprop" else 0.0)
+            if o.s2 is not None:
+                o.s2.zero_()
+            if o.beta_pow is not None:
+                o.beta_pow[0] = o.cfg.beta1
+                o.beta_pow[1] = o.cfg.beta2
+        if self.gs is not None:
+            self.gs.zero_()
+        self.version = 0
+
     def global_step(self) -> int:
         return int(self.gs.item()) if self.gs is not None else -1
 
@@ -154,10 +167,13 @@ class PSServer:
                     self._reply_hdr(worker_rank, g)
                     continue
                 if typ == INIT:
+                    # global_variables_initializer: params from the chief, slots / beta powers /
+                    # global_step back to their initial values
                     dist.recv(pay, src=worker_rank, group=g)
                     with sh.lock:
                         sh.P.master.copy_(pay.to(sh.device))
                         sh.P.refresh_copies()
+                        sh.reset_optimizer_state()
                         sh.initialized = True
                     self._reply_hdr(worker_rank, g)
                     continue

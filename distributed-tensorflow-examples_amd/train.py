@@ -123,7 +123,8 @@ def tensors_from_flat(model, P, optimizers, gs: int):
     """Checkpoint dict (TF names and layouts) from a FlatParams + its optimizers."""
     out = {}
     for s in model.specs:
-        out[s.name] = model.to_tf(s.name, P.view(s.name).detach().cpu())
+        if s.name in P.offsets:  # a ps shard holds a subset
+            out[s.name] = model.to_tf(s.name, P.view(s.name).detach().cpu())
     for o in optimizers:
         for k, t in o.slot_tensors().items():
             base = k.rsplit("/", 1)[0]  # "<var>/Adam" -> "<var>"; beta powers have no slash
@@ -136,7 +137,7 @@ def tensors_from_flat(model, P, optimizers, gs: int):
 
 def load_flat_from_tensors(model, P, optimizers, tensors):
     for s in model.specs:
-        if s.name in tensors:
+        if s.name in tensors and s.name in P.offsets:
             P.view(s.name).copy_(model.from_tf(s.name, tensors[s.name]).reshape(s.shape).to(P.device))
     conv = {}
     for k, t in tensors.items():

@@ -1,0 +1,147 @@
+"""T1/T2: multi-process clusters on 127.0.0.1 with the exact reference CLI (gloo, CPU).
+
+BASELINE.json config 1 (softmax regression, 1 ps + 2 workers, async SGD on
+CPU/gloo) plus the reference lifecycle: done protocol, chief-only
+checkpoints, global step budget, restore-on-restart, sync mode, 2 ps shards,
+all-reduce mode and a killed non-chief worker.
+"""
+import os
+import re
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+from dtfe import ckpt
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "launch"))
+import local_cluster  # noqa: E402
+
+pytestmark = pytest.mark.slow
+COMMON = ["--data_dir=/nonexistent", "--device=cpu", "--seed=1"]
+
+
+def _gs_lines(lines):
+    return [int(m.group(1)) for l in lines for m in [re.match(r"Global step (\d+) Local step \d+  AvgTime: [\d.]+ms", l)]
+            if m]
+
+
+def test_softmax_1ps_2workers_async(tmp_path):
+    md = str(tmp_path / "ck")
+    codes, out, _ = local_cluster.launch("softmax", 1, 2, COMMON + ["--num_steps=60", "--workers=2",
+                                                                     "--model_dir=" + md, "--save_model_secs=0.2"],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), (codes, out)
+    ps = out[("ps", 0)]
+    assert "ps 0 received done 0" in ps and "ps 0 received done 1" in ps
+    assert ps[-1] == "ps 0: quitting"
+    for w in (0, 1):
+        assert any(l.startswith("Total Time: ") for l in out[("worker", w)])
+    gs = _gs_lines(out[("worker", 0)]) + _gs_lines(out[("worker", 1)])
+    assert max(gs) >= 60 and max(gs) <= 61  # async total ~N (<= 1 extra step per worker)
+    # chief-only checkpoints, TF layout
+    latest = ckpt.latest_checkpoint(md)
+    assert latest is not None
+    t = ckpt.load_bundle(latest)
+    assert set(t) == {"Variable", "Variable_1", "Variable_2"} and t["Variable"].shape == (784, 10)
+    assert os.path.exists(os.path.join(md, "graph.pbtxt"))
+    assert any(f.startswith("events.out.tfevents.") for f in os.listdir(md))
+
+
+def test_chief_restart_restores_global_step(tmp_path):
+    md = str(tmp_path / "ck")
+    args = COMMON + ["--workers=1", "--model_dir=" + md, "--save_model_secs=0.05"]
+    codes, out, _ = local_cluster.launch("softmax", 1, 1, args + ["--num_steps=40"], timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    saved = int(ckpt.load_bundle(ckpt.latest_checkpoint(md))["Variable_2"])
+    assert saved > 0
+    codes, out, _ = local_cluster.launch("softmax", 1, 1, args + ["--num_steps=%d" % (saved + 10)], timeout=240,
+                                         stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    gs = _gs_lines(out[("worker", 0)])
+    assert gs[0] == saved + 1, (saved, gs[:3])  # resumed, not re-initialised (LSTM-style correct resume)
+
+
+def test_reinit_on_join_quirk(tmp_path):
+    md = str(tmp_path / "ck")
+    args = COMMON + ["--workers=1", "--model_dir=" + md, "--save_model_secs=0.05"]
+    local_cluster.launch("softmax", 1, 1, args + ["--num_steps=30"], timeout=240, stream=False)
+    codes, out, _ = local_cluster.launch("softmax", 1, 1, args + ["--num_steps=10", "--reinit_on_join"],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values())
+    # GAN:181 / ENC:160 behaviour: the re-init clobbers the restored step counter
+    assert _gs_lines(out[("worker", 0)])[0] == 1
+
+
+def test_two_ps_shards_and_lstm_eval(tmp_path):
+    md = str(tmp_path / "ck")
+    codes, out, _ = local_cluster.launch("lstm", 2, 2, COMMON + ["--num_steps=6", "--workers=2", "--batch_size=128",
+                                                                  "--model_dir=" + md, "--save_model_secs=0.3"],
+                                         timeout=300, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    for p in (0, 1):
+        assert out[("ps", p)][-1] == "ps %d: quitting" % p
+    for w in (0, 1):
+        assert any(re.match(r"Test-Accuracy: \d\.\d{4}$", l) for l in out[("worker", w)])
+    t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
+    assert t["rnn/basic_lstm_cell/kernel"].shape == (156, 512)
+    assert t["Variable_2"].dtype == torch.int32
+
+
+def test_sync_mode_steps_in_lockstep(tmp_path):
+    codes, out, _ = local_cluster.launch("softmax", 1, 2, COMMON + ["--num_steps=20", "--workers=2", "--sync",
+                                                                     "--save_model_secs=0",
+                                                                     "--model_dir=" + str(tmp_path)],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    g0, g1 = _gs_lines(out[("worker", 0)]), _gs_lines(out[("worker", 1)])
+    # every global step aggregates both replicas: each worker sees consecutive steps 1, 2, 3 ...
+    assert g0[:5] == [1, 2, 3, 4, 5] and g1[:5] == [1, 2, 3, 4, 5]
+
+
+def test_gan_global_step_advances_by_two(tmp_path):
+    codes, out, _ = local_cluster.launch("gan", 1, 1, COMMON + ["--num_steps=10", "--workers=1",
+                                                                 "--save_model_secs=0", "--batch_size=16",
+                                                                 "--model_dir=" + str(tmp_path)],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    assert _gs_lines(out[("worker", 0)])[:3] == [2, 4, 6]
+
+
+def test_allreduce_mode_two_workers(tmp_path):
+    codes, out, _ = local_cluster.launch("encoder", 0, 2, COMMON + ["--num_steps=5", "--mode=allreduce",
+                                                                     "--batch_size=32", "--save_model_secs=0",
+                                                                     "--model_dir=" + str(tmp_path)],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    assert _gs_lines(out[("worker", 0)]) == [1, 2, 3, 4, 5]
+    assert _gs_lines(out[("worker", 1)]) == [1, 2, 3, 4, 5]
+
+
+def test_killed_non_chief_worker_does_not_stall_others(tmp_path):
+    """device_filters semantics: worker 1 dies, worker 0 finishes; the ps keeps waiting
+    for the missing done signal exactly like the reference (C07) until we stop it."""
+    ports = local_cluster.free_ports(3)
+    ps_hosts = "127.0.0.1:%d" % ports[0]
+    wh = "127.0.0.1:%d,127.0.0.1:%d" % (ports[1], ports[2])
+    base = COMMON + ["--workers=2", "--save_model_secs=0", "--model_dir=" + str(tmp_path)]
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    mk = lambda job, i, extra: subprocess.Popen(local_cluster.task_argv("softmax", ps_hosts, wh, job, i, base + extra),
+                                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+    ps = mk("ps", 0, ["--num_steps=400"])
+    w0 = mk("worker", 0, ["--num_steps=400"])
+    w1 = mk("worker", 1, ["--num_steps=100000"])
+    try:
+        time.sleep(8)
+        w1.kill()
+        out0, _ = w0.communicate(timeout=180)
+        assert w0.returncode == 0, out0
+        assert "Total Time" in out0
+        time.sleep(1)
+        assert ps.poll() is None  # still waiting for worker 1's done signal
+    finally:
+        for p in (ps, w0, w1):
+            if p.poll() is None:
+                p.kill()
