@@ -9,6 +9,8 @@
 #include <vector>
 
 #include "../kernels/conv.h"
+#include "../kernels/conv1.h"
+#include "../kernels/imgconv.h"
 #include "../kernels/elementwise.h"
 #include "../kernels/gemm_dense.h"
 #include "../kernels/head.h"
@@ -111,13 +113,14 @@ void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, co
 
 void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B, int64_t H, int64_t W, int64_t C,
                 int64_t Cout, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                const optional<Tensor>& pooled, const optional<Tensor>& argmax) {
+                const optional<Tensor>& pooled, const optional<Tensor>& argmax, const optional<Tensor>& relu_mask) {
   check_cuda(dy, "dy");
   dtfe::ConvDgradArgs a{};
   a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
   a.wt = reinterpret_cast<const dtfe::bf16*>(wt.data_ptr());
   a.dx = reinterpret_cast<dtfe::bf16*>(dx.data_ptr());
+  a.relu_mask = ptr_or_null<dtfe::bf16>(relu_mask);
   a.unpool = (pooled.has_value() && pooled->defined()) ? 1 : 0;
   if (a.unpool) {
     a.up.pooled = reinterpret_cast<const dtfe::bf16*>(pooled->data_ptr());
@@ -125,6 +128,81 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
     a.up.PH = (int)H; a.up.PW = (int)W; a.up.C = (int)C;
   }
   dtfe::launch_conv_dgrad(a, cur_stream());
+}
+
+void conv1_fwd_pool(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
+                    const Tensor& argmax) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.numel() % 784 == 0 && w.numel() == 32 * 25, "conv1_fwd_pool: MNIST conv1 geometry only");
+  dtfe::Conv1Args a{};
+  a.B = (int)(x.numel() / 784);
+  a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
+  a.bias = ptr_or_null<float>(bias);
+  a.y = reinterpret_cast<dtfe::bf16*>(y.data_ptr());
+  a.argmax = reinterpret_cast<uint8_t*>(argmax.data_ptr());
+  TORCH_CHECK(y.numel() == (int64_t)a.B * 14 * 14 * 32 && argmax.numel() == y.numel(), "conv1_fwd_pool: out shape");
+  dtfe::launch_conv1_fwd_pool(a, cur_stream());
+}
+
+void conv1_wgrad_pooled(const Tensor& x, const Tensor& dp, const Tensor& argmax, const Tensor& dw,
+                        const optional<Tensor>& db, double scale) {
+  check_cuda(x, "x");
+  dtfe::Conv1Args a{};
+  a.B = (int)(x.numel() / 784);
+  TORCH_CHECK(dp.numel() == (int64_t)a.B * 14 * 14 * 32 && dw.numel() == 32 * 25, "conv1_wgrad_pooled: shapes");
+  a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  a.dp = reinterpret_cast<const dtfe::bf16*>(dp.data_ptr());
+  a.argmax = reinterpret_cast<uint8_t*>(argmax.data_ptr());
+  a.dw = dw.data_ptr<float>();
+  a.db = ptr_or_null<float>(db);
+  a.scale = (float)scale;
+  dtfe::launch_conv1_wgrad_pooled(a, cur_stream());
+}
+
+void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, const optional<Tensor>& src_argmax,
+             const Tensor& w, const optional<Tensor>& bias, const Tensor& y, const optional<Tensor>& argmax,
+             const optional<Tensor>& relu_mask, int64_t B, int64_t SH, int64_t SW, int64_t CS, int64_t OH, int64_t OW,
+             int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool) {
+  check_cuda(w, "w");
+  TORCH_CHECK((src.has_value() && src->defined()) != (src_pooled.has_value() && src_pooled->defined()),
+              "imgconv: exactly one of src / src_pooled");
+  dtfe::ImgConvArgs a{};
+  a.B = (int)B; a.SH = (int)SH; a.SW = (int)SW; a.CS = (int)CS; a.OH = (int)OH; a.OW = (int)OW; a.N = (int)N;
+  a.KH = (int)KH; a.KW = (int)KW; a.stride = (int)stride; a.pad = (int)pad; a.flip_taps = flip_taps;
+  a.src = ptr_or_null<dtfe::bf16>(src);
+  a.src_pooled = ptr_or_null<dtfe::bf16>(src_pooled);
+  a.src_argmax = ptr_or_null<uint8_t>(src_argmax);
+  TORCH_CHECK(a.src || a.src_argmax, "imgconv: src_pooled needs src_argmax");
+  a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
+  a.bias = ptr_or_null<float>(bias);
+  a.act = (int)act; a.pool = pool;
+  a.y = reinterpret_cast<dtfe::bf16*>(y.data_ptr());
+  a.argmax = ptr_or_null<uint8_t>(argmax);
+  a.relu_mask = ptr_or_null<dtfe::bf16>(relu_mask);
+  TORCH_CHECK(w.numel() == N * KH * KW * CS, "imgconv: weight size");
+  TORCH_CHECK(y.numel() == B * OH * OW * N / (pool ? 4 : 1), "imgconv: output size");
+  dtfe::launch_imgconv(a, cur_stream());
+}
+
+void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
+              const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
+              int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
+              int64_t pad, double scale) {
+  check_cuda(src, "src");
+  dtfe::ImgWgradArgs a{};
+  a.B = (int)B; a.SH = (int)SH; a.SW = (int)SW; a.CS = (int)CS; a.OH = (int)OH; a.OW = (int)OW; a.N = (int)N;
+  a.KH = (int)KH; a.KW = (int)KW; a.stride = (int)stride; a.pad = (int)pad;
+  a.src = reinterpret_cast<const dtfe::bf16*>(src.data_ptr());
+  a.dy = ptr_or_null<dtfe::bf16>(dy);
+  a.dy_pooled = ptr_or_null<dtfe::bf16>(dy_pooled);
+  a.dy_argmax = ptr_or_null<uint8_t>(dy_argmax);
+  TORCH_CHECK((a.dy != nullptr) != (a.dy_pooled != nullptr), "imgwgrad: exactly one of dy / dy_pooled");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.numel() == N * KH * KW * CS, "imgwgrad: dw");
+  a.dw = dw.data_ptr<float>();
+  a.db = ptr_or_null<float>(db);
+  a.scale = (float)scale;
+  dtfe::launch_imgwgrad(a, cur_stream());
 }
 
 void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t H,
@@ -366,7 +444,16 @@ TORCH_LIBRARY(dtfe, m) {
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");
   m.def(
       "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
-      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax) -> ()");
+      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask) -> ()");
+  m.def("conv1_fwd_pool(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!) argmax) -> ()");
+  m.def(
+      "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
+      " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
+      " int stride, int pad, bool flip_taps, int act, bool pool) -> ()");
+  m.def(
+      "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
+      " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale) -> ()");
+  m.def("conv1_wgrad_pooled(Tensor x, Tensor dp, Tensor argmax, Tensor(a!) dw, Tensor(b!)? db, float scale) -> ()");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
       " int OW, int KH, int KW, int stride, int pad, float scale) -> ()");
@@ -411,6 +498,10 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("colsum", &colsum);
   m.impl("act_grad", &act_grad);
   m.impl("bias_act", &bias_act);
+  m.impl("conv1_fwd_pool", &conv1_fwd_pool);
+  m.impl("imgconv", &imgconv);
+  m.impl("imgwgrad", &imgwgrad);
+  m.impl("conv1_wgrad_pooled", &conv1_wgrad_pooled);
   m.impl("lstm_cell_fwd", &lstm_cell_fwd);
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }

@@ -20,6 +20,14 @@
 
 namespace dtfe {
 
+// m / d for 0 <= m < 2^24 via a float reciprocal, corrected to exact
+__device__ __forceinline__ int fast_div(int m, int d, float inv_d) {
+  int q = (int)((float)m * inv_d);
+  const int r = m - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
 // decode a GEMM row into an NHWC pixel of a (RH x RW) grid
 __device__ __forceinline__ void decode_row(int m, int RH, int RW, int pool_order, int& b, int& y, int& x) {
   if (pool_order) {
@@ -61,11 +69,18 @@ __device__ __forceinline__ bool src_pixel(const ConvGeom& g, bool transposed, in
 
 // A operand (KMAJ): rows = pixels of the row grid, k = (kh, kw, c) over the
 // source tensor (x for forward, dY for dgrad).
+//
+// Every thread stages the same rows at every k-step, so each row's pixel is
+// decoded once (constructor).  When the source channel count is a multiple of
+// BK a k-tile never straddles two taps: (kh, kw) is wave-uniform per k-step
+// and a chunk address is base + ((sy*W + sx)*C + ch) with no division.
 template <int R, bool TRANS>
 struct Im2colLoader {
   using Lay = LdsLayout<bf16, R, KMAJ>;
   using C = Chunks<bf16, R, KMAJ>;
-  const bf16* src; ConvGeom g; int rows; int K; int r0; int SC; int RH, RW; bool cvec;
+  const bf16* src; ConvGeom g; int rows; int K; int r0; int SC; int RH, RW; bool cvec, fast;
+  long rbase[C::NC];  // image base offset of the chunk's row (-1: row out of range)
+  int ry[C::NC], rx[C::NC];
   u32x4_t regs[C::NC];
 
   __device__ __forceinline__ Im2colLoader(const bf16* s, const ConvGeom& g_, int r0_) : src(s), g(g_), r0(r0_) {
@@ -74,9 +89,46 @@ struct Im2colLoader {
     rows = g.B * RH * RW;
     K = g.KH * g.KW * SC;
     cvec = (SC % 8) == 0;
+    fast = (SC % BK) == 0 && g.stride == 1;
+    const int SH = TRANS ? g.OH : g.H, SW = TRANS ? g.OW : g.W;
+#pragma unroll
+    for (int c = 0; c < C::NC; ++c) {
+      const int idx = threadIdx.x + c * GEMM_THREADS;
+      int r, k;
+      C::rk(idx, r, k);
+      const int m = r0 + r;
+      rbase[c] = -1;
+      ry[c] = rx[c] = 0;
+      if ((C::N % GEMM_THREADS == 0 || idx < C::N) && m < rows) {
+        int b, y, x;
+        decode_row(m, RH, RW, TRANS ? 0 : g.pool_order, b, y, x);
+        rbase[c] = (long)b * SH * SW * SC;
+        // stride-1 source coordinate of tap (kh,kw): forward y - p + kh ; dgrad y + p - kh
+        ry[c] = TRANS ? y + g.pad : y - g.pad;
+        rx[c] = TRANS ? x + g.pad : x - g.pad;
+      }
+    }
   }
   __device__ __forceinline__ void load(int k0) {
     const int SH = TRANS ? g.OH : g.H, SW = TRANS ? g.OW : g.W;
+    if (fast) {
+      const int tap = k0 / SC, ch0 = k0 - tap * SC;
+      const int kh = tap / g.KW, kw = tap - kh * g.KW;
+      const int dy = TRANS ? -kh : kh, dx = TRANS ? -kw : kw;
+      const bool tap_ok = k0 < K;
+#pragma unroll
+      for (int c = 0; c < C::NC; ++c) {
+        const int idx = threadIdx.x + c * GEMM_THREADS;
+        int r, k;
+        C::rk(idx, r, k);
+        u32x4_t v = {0u, 0u, 0u, 0u};
+        const int sy = ry[c] + dy, sx = rx[c] + dx;
+        if (tap_ok && rbase[c] >= 0 && sy >= 0 && sy < SH && sx >= 0 && sx < SW)
+          v = *reinterpret_cast<const u32x4_t*>(src + rbase[c] + ((long)sy * SW + sx) * SC + ch0 + k);
+        regs[c] = v;
+      }
+      return;
+    }
 #pragma unroll
     for (int c = 0; c < C::NC; ++c) {
       const int idx = threadIdx.x + c * GEMM_THREADS;
@@ -120,12 +172,31 @@ struct Im2colWgradLoader {
   using Lay = LdsLayout<bf16, R, RMAJ>;
   using C = Chunks<bf16, R, RMAJ>;
   const bf16* x; ConvGeom g; int Kw; int Mred; int r0; bool cvec;
+  float inv_ow, inv_oh;
+  int tkh[C::NC], tkw[C::NC], tch[C::NC];  // this thread's fixed k rows: tap + channel (-1: slow path)
   u32x4_t regs[C::NC];
 
   __device__ __forceinline__ Im2colWgradLoader(const bf16* x_, const ConvGeom& g_, int r0_) : x(x_), g(g_), r0(r0_) {
     Kw = g.KH * g.KW * g.C;
     Mred = g.B * g.OH * g.OW;
     cvec = (g.C % 8) == 0;
+    inv_ow = 1.f / (float)g.OW;
+    inv_oh = 1.f / (float)g.OH;
+#pragma unroll
+    for (int c = 0; c < C::NC; ++c) {
+      const int idx = threadIdx.x + c * GEMM_THREADS;
+      int r, k;
+      C::rk(idx, r, k);
+      const int gr = r0 + r;
+      tch[c] = -1;
+      tkh[c] = tkw[c] = 0;
+      if (cvec && gr + 8 <= Kw) {
+        const int tap = gr / g.C;
+        tch[c] = gr - tap * g.C;
+        tkh[c] = tap / g.KW;
+        tkw[c] = tap - tkh[c] * g.KW;
+      }
+    }
   }
   __device__ __forceinline__ void load(int k0) {
 #pragma unroll
@@ -137,14 +208,16 @@ struct Im2colWgradLoader {
         C::rk(idx, r, k);
         const int m = k0 + k, gr = r0 + r;
         if (m < Mred) {
-          int b, y, xx;
-          decode_row(m, g.OH, g.OW, 0, b, y, xx);
+          // m -> (b, y, x) without integer division
+          const int q1 = fast_div(m, g.OW, inv_ow);
+          const int xx = m - q1 * g.OW;
+          const int b = fast_div(q1, g.OH, inv_oh);
+          const int y = q1 - b * g.OH;
           bf16* e = reinterpret_cast<bf16*>(&v);
-          if (cvec && gr + 8 <= Kw) {
-            const int ch = gr % g.C, tap = gr / g.C, kw = tap % g.KW, kh = tap / g.KW;
-            int sy, sx;
-            if (src_pixel(g, false, y, xx, kh, kw, sy, sx))
-              v = *reinterpret_cast<const u32x4_t*>(x + (((long)b * g.H + sy) * g.W + sx) * g.C + ch);
+          if (tch[c] >= 0) {
+            const int sy = y * g.stride - g.pad + tkh[c], sx = xx * g.stride - g.pad + tkw[c];
+            if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W)
+              v = *reinterpret_cast<const u32x4_t*>(x + (((long)b * g.H + sy) * g.W + sx) * g.C + tch[c]);
           } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -229,6 +302,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void conv_dgrad_kernel(ConvDgradArgs 
       if (m >= M) continue;
       const long pidx = (long)m * N + col;
       if (a.unpool) unpool_store(a.up, pidx, v[j], a.dx);
+      else if (a.relu_mask) a.dx[pidx] = f2bf(bf2f(a.relu_mask[pidx]) > 0.f ? v[j] : 0.f);
       else a.dx[pidx] = f2bf(v[j]);
     }
   });
@@ -270,35 +344,46 @@ template <typename Cfg> static int tiles_of(int M, int N) {
   return ((M + Cfg::BM - 1) / Cfg::BM) * ((N + Cfg::BN - 1) / Cfg::BN);
 }
 
+// Tile policy for the skinny-N convolutions (N = Cout or C <= 64, M = pixels):
+// tall 256-row tiles (4 waves stacked along M, each wave 64 x N) give 8-16
+// MFMAs per wave per k-step and still >= 1 workgroup per CU once M >= 64K.
+template <template <typename> class KERN, typename ARGS>
+static void launch_skinny(const ARGS& a, int M, int N, hipStream_t s) {
+  const bool tall = M >= 256 * 256;
+  if (N <= 32) {
+    if (tall) {
+      using Cfg = TileCfg<bf16, 256, 32, 4, 1>;
+      hipLaunchKernelGGL(KERN<Cfg>::fn, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
+    } else {
+      using Cfg = TileCfg<bf16, 128, 32, 4, 1>;
+      hipLaunchKernelGGL(KERN<Cfg>::fn, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
+    }
+  } else if (N <= 64) {
+    if (tall) {
+      using Cfg = TileCfg<bf16, 256, 64, 4, 1>;
+      hipLaunchKernelGGL(KERN<Cfg>::fn, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
+    } else {
+      using Cfg = TileCfg<bf16, 128, 64, 2, 2>;
+      hipLaunchKernelGGL(KERN<Cfg>::fn, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
+    }
+  } else {
+    using Cfg = TileCfg<bf16, 128, 128, 2, 2>;
+    hipLaunchKernelGGL(KERN<Cfg>::fn, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
+  }
+}
+
+template <typename Cfg> struct FwdK { static constexpr auto fn = conv_fwd_kernel<Cfg>; };
+template <typename Cfg> struct DgradK { static constexpr auto fn = conv_dgrad_kernel<Cfg>; };
+
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   const ConvGeom& g = a.g;
   if (g.pool_order && ((g.OH | g.OW) & 1)) throw std::runtime_error("conv_fwd: pool needs even output dims");
-  const int M = g.B * g.OH * g.OW, N = g.Cout;
-  if (N <= 32) {
-    using Cfg = TileCfg<bf16, 128, 32, 4, 1>;
-    hipLaunchKernelGGL(conv_fwd_kernel<Cfg>, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
-  } else if (N <= 64) {
-    using Cfg = TileCfg<bf16, 128, 64, 2, 2>;
-    hipLaunchKernelGGL(conv_fwd_kernel<Cfg>, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
-  } else {
-    using Cfg = TileCfg<bf16, 128, 128, 2, 2>;
-    hipLaunchKernelGGL(conv_fwd_kernel<Cfg>, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
-  }
+  launch_skinny<FwdK>(a, g.B * g.OH * g.OW, g.Cout, s);
 }
 
 void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s) {
   const ConvGeom& g = a.g;
-  const int M = g.B * g.H * g.W, N = g.C;
-  if (N <= 32) {
-    using Cfg = TileCfg<bf16, 128, 32, 4, 1>;
-    hipLaunchKernelGGL(conv_dgrad_kernel<Cfg>, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
-  } else if (N <= 64) {
-    using Cfg = TileCfg<bf16, 128, 64, 2, 2>;
-    hipLaunchKernelGGL(conv_dgrad_kernel<Cfg>, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
-  } else {
-    using Cfg = TileCfg<bf16, 128, 128, 2, 2>;
-    hipLaunchKernelGGL(conv_dgrad_kernel<Cfg>, dim3(tiles_of<Cfg>(M, N)), dim3(GEMM_THREADS), 0, s, a);
-  }
+  launch_skinny<DgradK>(a, g.B * g.H * g.W, g.C, s);
 }
 
 template <typename Cfg>
@@ -321,7 +406,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   const int M = g.Cout, N = g.KH * g.KW * g.C + (a.db ? 1 : 0);
   const int target = 1024;  // 4 workgroups per CU
   if (M <= 32 && N <= 32) wgrad_launch<TileCfg<bf16, 32, 32, 2, 2>>(a, target, s);
-  else if (M <= 64) wgrad_launch<TileCfg<bf16, 64, 64, 2, 2>>(a, target, s);
+  else if (M <= 64) wgrad_launch<TileCfg<bf16, 64, 128, 2, 2>>(a, target, s);
   else wgrad_launch<TileCfg<bf16, 128, 128, 2, 2>>(a, target, s);
 }
 

@@ -21,27 +21,67 @@ __device__ __forceinline__ void advance_counter_last_block(int64_t* counter, uin
   }
 }
 
+// 8 source elements -> floats (vector loads: u8 8 B, bf16 16 B, f32 2x16 B)
+__device__ __forceinline__ void load8(const void* src, int dt, long off, float (&v)[8]) {
+  if (dt == 0) {
+    const u32x2_t w = *reinterpret_cast<const u32x2_t*>(reinterpret_cast<const uint8_t*>(src) + off);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)((w[i >> 2] >> (8 * (i & 3))) & 0xffu) * (1.f / 255.f);
+  } else if (dt == 1) {
+    const f32x4_t* p = reinterpret_cast<const f32x4_t*>(reinterpret_cast<const float*>(src) + off);
+    const f32x4_t lo = p[0], hi = p[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = lo[i]; v[4 + i] = hi[i]; }
+  } else {
+    const u32x4_t w = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const bf16*>(src) + off);
+    const bf16* e = reinterpret_cast<const bf16*>(&w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = bf2f(e[i]);
+  }
+}
+
+// one wave per batch row, 8 elements per lane per iteration
 __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
   const int64_t step = a.counter ? *a.counter : 0;
-  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  const bool vec = (a.D % 8) == 0;
+  for (int b = blockIdx.x * 4 + (threadIdx.x >> 6); b < a.B; b += gridDim.x * 4) {
     long r;
     if (a.idx) r = a.idx[b];
     else r = (long)(hash_u32(a.seed, (uint64_t)step * a.B + b) % (uint32_t)a.n_rows);
-    if (a.labels_dst && threadIdx.x == 0) a.labels_dst[b] = a.labels_src[r];
-    for (int d = threadIdx.x; d < a.D; d += 256) {
-      float v;
-      if (a.src_dtype == 0) v = reinterpret_cast<const uint8_t*>(a.src)[r * a.D + d] * (1.f / 255.f);
-      else if (a.src_dtype == 1) v = reinterpret_cast<const float*>(a.src)[r * a.D + d];
-      else v = bf2f(reinterpret_cast<const bf16*>(a.src)[r * a.D + d]);
-      if (a.dst_dtype == 1) reinterpret_cast<float*>(a.dst)[(long)b * a.D + d] = v;
-      else reinterpret_cast<bf16*>(a.dst)[(long)b * a.D + d] = f2bf(v);
+    if (a.labels_dst && lane == 0) a.labels_dst[b] = a.labels_src[r];
+    if (vec) {
+      for (int d = lane * 8; d < a.D; d += 64 * 8) {
+        float v[8];
+        load8(a.src, a.src_dtype, r * a.D + d, v);
+        const long o = (long)b * a.D + d;
+        if (a.dst_dtype == 1) {
+          f32x4_t* q = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.dst) + o);
+          q[0] = f32x4_t{v[0], v[1], v[2], v[3]};
+          q[1] = f32x4_t{v[4], v[5], v[6], v[7]};
+        } else {
+          *reinterpret_cast<u32x4_t*>(reinterpret_cast<bf16*>(a.dst) + o) =
+              u32x4_t{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                      pack_bf16x2(v[6], v[7])};
+        }
+      }
+    } else {
+      for (int d = lane; d < a.D; d += 64) {
+        float v;
+        if (a.src_dtype == 0) v = reinterpret_cast<const uint8_t*>(a.src)[r * a.D + d] * (1.f / 255.f);
+        else if (a.src_dtype == 1) v = reinterpret_cast<const float*>(a.src)[r * a.D + d];
+        else v = bf2f(reinterpret_cast<const bf16*>(a.src)[r * a.D + d]);
+        if (a.dst_dtype == 1) reinterpret_cast<float*>(a.dst)[(long)b * a.D + d] = v;
+        else reinterpret_cast<bf16*>(a.dst)[(long)b * a.D + d] = f2bf(v);
+      }
     }
   }
   advance_counter_last_block(a.counter, a.done, 1);
 }
 
 void launch_gather_rows(const GatherArgs& a, hipStream_t s) {
-  int blocks = a.B < 1024 ? a.B : 1024;
+  int blocks = (a.B + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
 

@@ -1,0 +1,53 @@
+#pragma once
+#include "common.h"
+
+namespace dtfe {
+
+// Whole-image implicit-GEMM convolution for small feature maps (MNIST 14x14,
+// CIFAR 32x32 ... 8x8): one workgroup stages a complete zero-padded NHWC image
+// in LDS and builds every MFMA A fragment straight from it (one ds_read_b128
+// of 8 channels at pixel + tap), instead of re-reading the 25x im2col
+// expansion from L2 for every k-step.  The weights stream through registers
+// (16-byte fragment loads, L2-resident).
+//
+// Forward:  y[p][n] = sum_{tap,c} src[p*stride - pad + tap][c] * w[n][tap][c]
+// CS == 1 (the network input) uses a tap-packed variant: k = tap (<= 32).
+// Data-grad (stride 1): the same loop over dY with pad' = K-1-pad and the taps
+// of Wt[n=cin][tap][c=cout] flipped (flip_taps = 1).
+// Optional on-load un-pool of the source (src = unpool(src_pooled, src_argmax)),
+// and epilogues: +bias, activation, 2x2 max-pool + argmax (rows in pool order),
+// ReLU mask of a pooled tensor (dgrad), plain store.
+struct ImgConvArgs {
+  int B, SH, SW, CS;        // source image (per batch element) [SH][SW][CS]
+  int OH, OW, N;            // output pixels and channels
+  int KH, KW, stride, pad;
+  int flip_taps;
+  const bf16* src;          // [B][SH][SW][CS]   (or nullptr with src_pooled)
+  const bf16* src_pooled;   // [B][SH/2][SW/2][CS] pooled values to route through src_argmax
+  const uint8_t* src_argmax;
+  const bf16* w;            // [N][KH*KW][CS]
+  const float* bias;
+  int act, pool;
+  bf16* y;                  // [B][OH'][OW'][N]  (OH' = OH/2 when pooling)
+  uint8_t* argmax;          // pool argmax out (optional)
+  const bf16* relu_mask;    // dgrad epilogue: y = mask > 0 ? y : 0 (same indexing as y)
+};
+
+// Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]
+// (+ db[n] += sum_p dY[p][n]); dY optionally un-pooled on load from (dy_pooled, dy_argmax).
+// CS == 1 uses a tap-packed variant (dW^T = shifted-image^T x dY, <= 32 taps).
+struct ImgWgradArgs {
+  int B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad;
+  const bf16* src;                                   // [B][SH][SW][CS]
+  const bf16* dy;                                    // [B][OH][OW][N]  or nullptr with dy_pooled
+  const bf16* dy_pooled; const uint8_t* dy_argmax;   // [B][OH/2][OW/2][N]
+  float* dw; float* db; float scale;
+  int imgs_per_block;
+};
+
+bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
+void launch_imgconv(const ImgConvArgs& a, hipStream_t s);
+bool imgwgrad_supported(const ImgWgradArgs& a);
+void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s);
+
+}  // namespace dtfe

@@ -12,44 +12,40 @@
 //               v2 = b2 v2 + (1-b2) g^2; v -= lr_t * m / (sqrt(v2) + eps)
 //   RMSProp   : ms = rho ms + (1-rho) g^2 ; mom = mu mom + lr g / sqrt(ms + eps); v -= mom
 //               (ms slot initialised to ONES by the host)
+//
+// Memory-bound: the flat path moves 4 elements per thread per iteration with
+// 16-byte loads/stores of every stream (p, g, slots) and 8-byte bf16 stores.
 #include "optim.h"
 
 namespace dtfe {
 
-struct Hyper {
-  float lr_t;
-};
-
-__device__ __forceinline__ float update_one(const OptArgs& a, float lr_t, long i, float g) {
-  float v = a.p[i];
-  switch (a.kind) {
-    case OPT_SGD:
-      v -= a.lr * g;
-      break;
-    case OPT_MOMENTUM: {
-      const float acc = a.s1[i] * a.momentum + g;
-      a.s1[i] = acc;
-      v -= a.lr * acc;
-      break;
-    }
-    case OPT_ADAM: {
-      const float m = a.s1[i] * a.beta1 + (1.f - a.beta1) * g;
-      const float v2 = a.s2[i] * a.beta2 + (1.f - a.beta2) * g * g;
-      a.s1[i] = m;
-      a.s2[i] = v2;
-      v -= lr_t * m / (sqrtf(v2) + a.eps);
-      break;
-    }
-    case OPT_RMSPROP: {
-      const float ms = a.s1[i] * a.rho + (1.f - a.rho) * g * g;
-      const float mom = a.s2[i] * a.momentum + a.lr * g / sqrtf(ms + a.eps);
-      a.s1[i] = ms;
-      a.s2[i] = mom;
-      v -= mom;
-      break;
-    }
+template <int KIND>
+__device__ __forceinline__ float upd(const OptArgs& a, float lr_t, float v, float g, float& s1, float& s2) {
+  if constexpr (KIND == OPT_SGD) {
+    return v - a.lr * g;
+  } else if constexpr (KIND == OPT_MOMENTUM) {
+    s1 = s1 * a.momentum + g;
+    return v - a.lr * s1;
+  } else if constexpr (KIND == OPT_ADAM) {
+    s1 = s1 * a.beta1 + (1.f - a.beta1) * g;
+    s2 = s2 * a.beta2 + (1.f - a.beta2) * g * g;
+    return v - lr_t * s1 / (sqrtf(s2) + a.eps);
+  } else {
+    s1 = s1 * a.rho + (1.f - a.rho) * g * g;
+    s2 = s2 * a.momentum + a.lr * g / sqrtf(s1 + a.eps);
+    return v - s2;
   }
+}
+
+template <int KIND>
+__device__ __forceinline__ float update_one(const OptArgs& a, float lr_t, long i, float g) {
+  float s1 = 0.f, s2 = 0.f;
+  if (KIND != OPT_SGD) s1 = a.s1[i];
+  if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) s2 = a.s2[i];
+  const float v = upd<KIND>(a, lr_t, a.p[i], g, s1, s2);
   a.p[i] = v;
+  if (KIND != OPT_SGD) a.s1[i] = s1;
+  if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) a.s2[i] = s2;
   return v;
 }
 
@@ -57,10 +53,38 @@ __device__ __forceinline__ float load_grad(const OptArgs& a, long i) {
   return (a.g ? a.g[i] : bf2f(a.g16[i])) * a.gscale;
 }
 
+template <int KIND>
+__device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i, bf16* w16) {
+  f32x4_t g;
+  if (a.g) {
+    g = *reinterpret_cast<const f32x4_t*>(a.g + i);
+  } else {
+    const u32x2_t w = *reinterpret_cast<const u32x2_t*>(a.g16 + i);
+    g = f32x4_t{__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u), __uint_as_float(w[1] << 16),
+                __uint_as_float(w[1] & 0xffff0000u)};
+  }
+  f32x4_t p = *reinterpret_cast<const f32x4_t*>(a.p + i);
+  f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  if (KIND != OPT_SGD) s1 = *reinterpret_cast<const f32x4_t*>(a.s1 + i);
+  if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) s2 = *reinterpret_cast<const f32x4_t*>(a.s2 + i);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x1 = s1[j], x2 = s2[j];
+    p[j] = upd<KIND>(a, lr_t, p[j], g[j] * a.gscale, x1, x2);
+    s1[j] = x1;
+    s2[j] = x2;
+  }
+  *reinterpret_cast<f32x4_t*>(a.p + i) = p;
+  if (KIND != OPT_SGD) *reinterpret_cast<f32x4_t*>(a.s1 + i) = s1;
+  if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) *reinterpret_cast<f32x4_t*>(a.s2 + i) = s2;
+  if (w16) *reinterpret_cast<u32x2_t*>(w16) = u32x2_t{pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3])};
+}
+
+template <int KIND>
 __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
   __shared__ bf16 tile[64][66];
   float lr_t = a.lr;
-  if (a.kind == OPT_ADAM) {
+  if (KIND == OPT_ADAM) {
     const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
     lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   }
@@ -68,19 +92,23 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
     const OptWork w = a.work[wi];
     const OptSeg sg = a.segs[w.seg];
     if (w.kind == 0) {
-      for (long j = threadIdx.x; j < w.count; j += 256) {
+      const long base = sg.off + w.start;
+      const long n4 = ((base & 3) == 0) ? (w.count / 4) * 4 : 0;  // segments are 64-aligned; chunks 8192
+      for (long j = threadIdx.x * 4; j < n4; j += 256 * 4)
+        update_vec4<KIND>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
+      for (long j = n4 + threadIdx.x; j < w.count; j += 256) {
         const long li = w.start + j, i = sg.off + li;
-        const float v = update_one(a, lr_t, i, load_grad(a, i));
+        const float v = update_one<KIND>(a, lr_t, i, load_grad(a, i));
         if (sg.w16) sg.w16[li] = f2bf(v);
       }
     } else {
-      // 64x64 tile of tap t: rows r0.., cols c0.. of the [R][C] slice
+      // 64x64 tile of tap t: rows r0.., cols c0.. of the [R][C] slice; transposed copy via LDS
       const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
       for (int rr = ty; rr < 64; rr += 4) {
         const int r = w.r0 + rr, c = w.c0 + tx;
         if (r < sg.R && c < sg.C) {
           const long li = ((long)r * sg.T + w.t) * sg.C + c, i = sg.off + li;
-          const float v = update_one(a, lr_t, i, load_grad(a, i));
+          const float v = update_one<KIND>(a, lr_t, i, load_grad(a, i));
           const bf16 b = f2bf(v);
           if (sg.w16) sg.w16[li] = b;
           tile[rr][tx] = b;
@@ -99,7 +127,7 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
     __threadfence();
     const uint32_t prev = atomicAdd(a.done_counter, 1u);
     if (prev == gridDim.x - 1) {
-      if (a.kind == OPT_ADAM) {
+      if (KIND == OPT_ADAM) {
         a.beta_pow[0] *= a.beta1;
         a.beta_pow[1] *= a.beta2;
       }
@@ -113,7 +141,14 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
 void launch_apply_gradients(const OptArgs& a, hipStream_t s) {
   int blocks = a.nwork < 2048 ? a.nwork : 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(apply_gradients_kernel, dim3(blocks), dim3(256), 0, s, a);
+  switch (a.kind) {
+    case OPT_SGD: hipLaunchKernelGGL(apply_gradients_kernel<OPT_SGD>, dim3(blocks), dim3(256), 0, s, a); break;
+    case OPT_MOMENTUM:
+      hipLaunchKernelGGL(apply_gradients_kernel<OPT_MOMENTUM>, dim3(blocks), dim3(256), 0, s, a);
+      break;
+    case OPT_ADAM: hipLaunchKernelGGL(apply_gradients_kernel<OPT_ADAM>, dim3(blocks), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(apply_gradients_kernel<OPT_RMSPROP>, dim3(blocks), dim3(256), 0, s, a); break;
+  }
 }
 
 }  // namespace dtfe

@@ -13,17 +13,22 @@ pre-allocated NHWC bf16 buffers (fp32 master weights / grads / Adam slots in
 one flat buffer), captured into one hipGraph:
 
   gather      batch from the HBM-resident dataset (device RNG, no host feed)
-  conv1/pool  implicit-GEMM MFMA, bias+ReLU+2x2 max-pool+argmax in registers
-  conv2/pool  same
+  conv1/pool  1-channel LDS image, tap-packed MFMA (k = 25 taps in one step),
+              bias+ReLU+2x2 max-pool+argmax in registers
+  conv2/pool  whole-image LDS conv (A fragments = ds_read_b128 of the staged image),
+              same fused pool epilogue (rows in pool-window order)
   fc1         MFMA GEMM, bias+ReLU+dropout epilogue
   head        fc2 + softmax-xent + dlogit rows + dropout/ReLU grad (one wave per row)
   head wgrad  split-K MFMA GEMM dlogit^T . H, bias grad through a ones column
-  fc1 dgrad   MFMA GEMM with the un-pool(argmax2)+ReLU' epilogue -> dZ2 full-res
-  fc1 wgrad   MFMA GEMM (both operands via ds_read_b64_tr_b16), fc1 bias grad as
-              its ones column
-  conv2 dgrad implicit-GEMM with the un-pool(argmax1)+ReLU' epilogue -> dZ1
-  conv2/conv1 wgrad  split-K implicit GEMM, bias grad as an extra ones column
-  Adam        one fused TF1 Adam launch, writes bf16 + transposed bf16 copies
+  fc1 dgrad   MFMA GEMM (W1 read through ds_read_b64_tr_b16), ReLU'(P2) epilogue
+              -> pooled-res dP2 (never un-pooled in memory)
+  fc1 wgrad   MFMA GEMM (both operands via the transposing LDS read), fc1 bias
+              grad as its ones column
+  conv2 dgrad whole-image LDS conv over un-pool(dP2) (argmax routing while staging),
+              flipped taps, ReLU'(P1) epilogue -> pooled-res dP1
+  conv2 wgrad whole-image LDS wgrad, both operands by ds_read_b64_tr_b16, bias grad
+  conv1 wgrad tap-packed (dW^T = shifted image^T . un-pool(dP1)), un-pooling while staging
+  Adam        one fused TF1 Adam launch, writes the bf16 (+ transposed) copies
 
 In data-parallel mode the fc/head gradient bucket (98% of the bytes) is
 all-reduced over RCCL while the conv backward kernels still run.
@@ -96,7 +101,7 @@ def var_specs():
         spec[k] = VarSpec(**kw)
     # transposed bf16 copies needed by the backward GEMMs
     spec["wc2"].transpose = (C2, KS * KS, C1)    # -> Wt[C1][25][C2] for conv2 dgrad
-    spec["wd1"].transpose = (FC, 1, 7 * 7 * C2)  # -> Wt[3136][1024] for fc1 dgrad
+    # fc1 dgrad reads W1 [1024][3136] itself through the transposing LDS read (RMAJ operand)
     flat_order = ["out", "bout", "bd1", "wd1", "wc2", "bc2", "wc1", "bc1"]
     return [spec[k] for k in flat_order], names
 
@@ -149,18 +154,23 @@ class MnistCnnTrainer:
         self.h = torch.empty(B, FC, device=d, dtype=bf)
         self.dzf = torch.empty(B, FC, device=d, dtype=bf)
         self.dl = torch.empty(B, 16, device=d, dtype=bf)      # dlogit rows (10 classes, padded to 16)
-        self.dz2 = torch.empty(B, 14, 14, C2, device=d, dtype=bf)
-        self.dz1 = torch.empty(B, IMG, IMG, C1, device=d, dtype=bf)
+        self.dp2 = torch.empty(B, 7, 7, C2, device=d, dtype=bf)    # pooled-res conv2 grad (ReLU-masked)
+        self.dp1 = torch.empty(B, 14, 14, C1, device=d, dtype=bf)  # pooled-res conv1 grad (ReLU-masked)
         self.loss_sum = torch.zeros(1, device=d)
         self.correct = torch.zeros(1, dtype=torch.int32, device=d)
         self.data_ctr = torch.zeros(1, dtype=torch.int64, device=d)
         self.data_done = torch.zeros(1, dtype=torch.int32, device=d)
         self.g1 = dict(B=B, H=IMG, W=IMG, C=1, Cout=C1, OH=IMG, OW=IMG, KH=KS, KW=KS, stride=1, pad=2)
         self.g2 = dict(B=B, H=14, W=14, C=C1, Cout=C2, OH=14, OW=14, KH=KS, KW=KS, stride=1, pad=2)
+        # whole-image LDS conv geometry: conv1 (1-channel tap-packed kernels), conv2 (forward /
+        # weight-grad) and conv2's data-grad
+        self.ic1 = dict(B=B, SH=IMG, SW=IMG, CS=1, OH=IMG, OW=IMG, N=C1, KH=KS, KW=KS, stride=1, pad=2)
+        self.ic2 = dict(B=B, SH=14, SW=14, CS=C1, OH=14, OW=14, N=C2, KH=KS, KW=KS, stride=1, pad=2)
+        self.ic2_dgrad = dict(B=B, SH=14, SW=14, CS=C2, OH=14, OW=14, N=C1, KH=KS, KW=KS, stride=1, pad=KS - 1 - 2)
         n = self.names
         P = self.P
         self.w = {k: P.w16[n[k]] for k in ("wc1", "wc2", "wd1", "out")}
-        self.wt = {k: P.wt16[n[k]] for k in ("wc2", "wd1")}
+        self.wt = {"wc2": P.wt16[n["wc2"]]}
         self.b = {k: P.view(n[k]) for k in ("bc1", "bc2", "bd1", "bout")}
         self.gw = {k: P.gview(n[k]) for k in ("wc1", "wc2", "wd1", "out", "bc1", "bc2", "bd1", "bout")}
         # gradient buckets in flat order: [head + fc1] then [conv2 + conv1]
@@ -177,8 +187,10 @@ class MnistCnnTrainer:
         self.correct.zero_()
         ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
                         seed=self.seed + 1, counter=self.data_ctr, done=self.data_done)
-        ops.conv_fwd(self.x, self.w["wc1"], self.b["bc1"], self.p1, self.a1, self.g1, pool=True, act=ops.ACT_RELU)
-        ops.conv_fwd(self.p1, self.w["wc2"], self.b["bc2"], self.p2, self.a2, self.g2, pool=True, act=ops.ACT_RELU)
+        ops.imgconv(self.w["wc1"], self.p1, src=self.x, bias=self.b["bc1"], argmax=self.a1, act=ops.ACT_RELU,
+                    pool=True, **self.ic1)
+        ops.imgconv(self.w["wc2"], self.p2, src=self.p1, bias=self.b["bc2"], argmax=self.a2, act=ops.ACT_RELU,
+                    pool=True, **self.ic2)
         K1 = 7 * 7 * C2
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
                  keep=self.keep, seed=self.seed + 2, counter=self.data_ctr)
@@ -188,17 +200,20 @@ class MnistCnnTrainer:
         ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
                  bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
                  splits=max(1, min(16, B // 128)), tile=4)
-        # fc1 dgrad -> dZ2 (full resolution, un-pooled through argmax2, ReLU-masked)
-        ops.gemm(self.dzf, self.wt["wd1"], self.dz2, M=B, N=K1, K=FC, pooled=self.p2, argmax=self.a2, PH=7, PW=7,
-                 PC=C2)
+        # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
+        ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
+                 aux_act=ops.ACT_RELU)
         # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
         ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
                  ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
         if self.allreduce is not None:
             self.allreduce.launch(0)
-        ops.conv_dgrad(self.dz2, self.wt["wc2"], self.dz1, self.g2, pooled=self.p1, argmax=self.a1)
-        ops.conv_wgrad(self.dz2, self.p1, self.gw["wc2"], self.gw["bc2"], self.g2)
-        ops.conv_wgrad(self.dz1, self.x, self.gw["wc1"], self.gw["bc1"], self.g1)
+        # conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)
+        ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
+                    flip_taps=True, **self.ic2_dgrad)
+        # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
+        ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2, **self.ic2)
+        ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
         if self.allreduce is not None:
             self.allreduce.launch(1)
             self.allreduce.wait()

@@ -203,10 +203,86 @@ def _pool_ref(z):
     return p, idx
 
 
-def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None):
-    """dX of an NHWC conv (wt = W laid out [C][KH][KW][Cout]); optional un-pool epilogue."""
+def _unpooled_nhwc(pooled, argmax, B, H, W, C):
+    """Full-resolution NHWC tensor holding pooled[w] at argmax position of each 2x2 window."""
+    out = torch.zeros(B * H * W * C)
+    _unpool_ref(pooled.reshape(-1).float(), torch.ones(B, H // 2, W // 2, C), argmax, H // 2, W // 2, C, out)
+    return out.view(B, H, W, C)
+
+
+def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None, src_pooled=None,
+            src_argmax=None, bias=None, argmax=None, relu_mask=None, flip_taps=False, act=ACT_NONE, pool=False):
+    """Whole-image LDS convolution (small feature maps): forward (+bias/act/pool) or, with
+    flip_taps and pad = K-1-pad, the data gradient of a stride-1 conv (w = Wt [cin][tap][cout]).
+    The source may be un-pooled on load from (src_pooled, src_argmax)."""
+    if y.is_cuda:
+        require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW, N, KH,
+                          KW, stride, pad, flip_taps, act, pool)
+        return y
+    s = src.float().view(B, SH, SW, CS) if src is not None else _unpooled_nhwc(src_pooled, src_argmax, B, SH, SW, CS)
+    wt = w.float().view(N, KH, KW, CS)
+    if flip_taps:
+        wt = wt.flip(1, 2)
+    z = torch.nn.functional.conv2d(s.permute(0, 3, 1, 2), wt.permute(0, 3, 1, 2),
+                                   bias.float() if bias is not None else None, stride=stride, padding=pad)
+    z = z[:, :, :OH, :OW]
+    z = _act_ref(z, act)
+    if pool:
+        p, idx = _pool_ref(z)
+        y.view(-1)[:] = p.permute(0, 2, 3, 1).reshape(-1).to(y.dtype)
+        if argmax is not None:
+            argmax.view(-1)[:] = idx.permute(0, 2, 3, 1).reshape(-1).to(argmax.dtype)
+        return y
+    flat = z.permute(0, 2, 3, 1).reshape(-1)
+    if relu_mask is not None:
+        flat = flat * (relu_mask.reshape(-1).float() > 0)
+    y.view(-1)[:] = flat.to(y.dtype)
+    return y
+
+
+def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
+             dy_argmax=None, scale=1.0):
+    """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY."""
+    if dw.is_cuda:
+        require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
+                           scale)
+        return
+    d = dy.float().view(B, OH, OW, N) if dy is not None else _unpooled_nhwc(dy_pooled, dy_argmax, B, OH, OW, N)
+    gw = torch.nn.grad.conv2d_weight(src.float().view(B, SH, SW, CS).permute(0, 3, 1, 2), (N, CS, KH, KW),
+                                     d.permute(0, 3, 1, 2), stride=stride, padding=pad)
+    dw.view(-1)[:] += scale * gw.permute(0, 2, 3, 1).reshape(-1)
+    if db is not None:
+        db += scale * d.sum(dim=(0, 1, 2))
+
+
+def conv1_fwd_pool(x, w, bias, y, argmax):
+    """MNIST conv1 (5x5, 1->32, SAME) + bias + ReLU + 2x2 max-pool (dedicated LDS-image MFMA kernel)."""
+    if y.is_cuda:
+        require().conv1_fwd_pool(x, w, bias, y, argmax)
+        return y
+    B = x.numel() // 784
+    g = dict(B=B, H=28, W=28, C=1, Cout=32, OH=28, OW=28, KH=5, KW=5, stride=1, pad=2)
+    return conv_fwd(x, w, bias, y, argmax, g, pool=True, act=ACT_RELU)
+
+
+def conv1_wgrad_pooled(x, dp, argmax, dw, db, scale=1.0):
+    """conv1 weight/bias grads from the pooled (ReLU-masked) gradient + argmax (no un-pooled tensor)."""
+    if dw.is_cuda:
+        require().conv1_wgrad_pooled(x, dp, argmax, dw, db, scale)
+        return
+    B = x.numel() // 784
+    g = dict(B=B, H=28, W=28, C=1, Cout=32, OH=28, OW=28, KH=5, KW=5, stride=1, pad=2)
+    dz = torch.zeros(B, 28, 28, 32)
+    ones = torch.ones(B, 14, 14, 32)
+    _unpool_ref(dp.reshape(-1).float(), ones, argmax, 14, 14, 32, dz)
+    conv_wgrad(dz, x, dw, db, g, scale)
+
+
+def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None):
+    """dX of an NHWC conv (wt = W laid out [C][KH][KW][Cout]); optional un-pool epilogue, or a
+    ReLU mask (dx = mask > 0 ? dx : 0) when the consumer un-pools itself."""
     if dx.is_cuda:
-        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax)
+        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask)
         return dx
     dyt = dy.float().view(g["B"], g["OH"], g["OW"], g["Cout"]).permute(0, 3, 1, 2)
     w = wt.float().view(g["C"], g["KH"], g["KW"], g["Cout"]).permute(3, 0, 1, 2)
@@ -215,6 +291,8 @@ def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None):
     if pooled is not None:
         _unpool_ref(flat, pooled, argmax, g["H"], g["W"], g["C"], dx)
     else:
+        if relu_mask is not None:
+            flat = flat * (relu_mask.reshape(-1).float() > 0)
         dx.view(-1)[:] = flat.to(dx.dtype)
     return dx
 

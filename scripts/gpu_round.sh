@@ -1,6 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/ -m gpu -x -q > gpurun_out/t2.log 2>&1; echo "TEST EXIT $?" >> gpurun_out/t2.log
-tail -5 gpurun_out/t2.log
-for b in 128 1024; do timeout -k 10 120 python bench.py --steps 100 --warmup 10 --batch_size $b 2>&1 | grep metric; done
-bash scripts/profile.sh b1024 --steps 30 --warmup 5 --batch_size 1024
+timeout -k 10 300 python3 -m pytest tests/test_imgconv.py -x -q > gpurun_out/t_img.log 2>&1; echo "TEST EXIT $?" >> gpurun_out/t_img.log
+tail -3 gpurun_out/t_img.log
+grep -q "TEST EXIT 0" gpurun_out/t_img.log || { grep -E "assert|Error" gpurun_out/t_img.log | head -20; exit 1; }
+timeout -k 10 300 python3 bench/cnn_kernels.py --batch_size 1024 --iters 30 > gpurun_out/ck.log 2>&1 && cat gpurun_out/ck.log
+timeout -k 10 300 python3 bench.py --steps 100 --warmup 10 > gpurun_out/bench.log 2>&1; tail -2 gpurun_out/bench.log

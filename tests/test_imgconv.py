@@ -1,0 +1,113 @@
+"""Whole-image LDS convolution kernels (imgconv / imgwgrad) vs the fp32 reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dtfe.ops as ops
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+def test_flip_formulation_is_the_data_gradient_cpu():
+    """imgconv(flip_taps, pad'=K-1-pad) over dY with Wt[cin][tap][cout] == dX of the conv (CPU, fp64-ish)."""
+    torch.manual_seed(0)
+    B, H, C, CO, K, pad = 2, 14, 8, 16, 5, 2
+    x = torch.randn(B, C, H, H, requires_grad=True)
+    w = torch.randn(CO, C, K, K)
+    y = F.conv2d(x, w, padding=pad)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    wt = w.permute(1, 2, 3, 0).contiguous()  # [cin][kh][kw][cout]
+    out = torch.empty(B, H, H, C)
+    ops.imgconv(wt, out, B=B, SH=H, SW=H, CS=CO, OH=H, OW=H, N=C, KH=K, KW=K, pad=K - 1 - pad,
+                src=gy.permute(0, 2, 3, 1).contiguous(), flip_taps=True)
+    assert torch.allclose(out, x.grad.permute(0, 2, 3, 1), atol=1e-4)
+
+
+CASES = [  # (B, SH, CS, N, K, stride, pad, pool)
+    (3, 14, 32, 64, 5, 1, 2, True),     # MNIST conv2 fwd
+    (2, 32, 16, 16, 3, 1, 1, False),    # ResNet-20 stage 1
+    (2, 32, 16, 32, 3, 2, 1, False),    # ResNet-20 downsample
+    (2, 8, 64, 64, 3, 1, 1, False),     # ResNet-20 stage 3
+    (3, 28, 1, 32, 5, 1, 2, True),      # MNIST conv1 fwd (1-channel tap-packed kernel)
+    (2, 28, 1, 16, 3, 2, 1, False),     # 1-channel, strided, N=16
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_imgconv_fwd(case):
+    B, SH, CS, N, K, s, pad, pool = case
+    OH = (SH + 2 * pad - K) // s + 1
+    torch.manual_seed(1)
+    x = torch.randn(B, SH, SH, CS).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, K, CS) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    shp = (B, OH // 2, OH // 2, N) if pool else (B, OH, OH, N)
+    y = torch.empty(shp, device=DEV, dtype=torch.bfloat16)
+    am = torch.empty(shp, device=DEV, dtype=torch.uint8) if pool else None
+    kw = dict(B=B, SH=SH, SW=SH, CS=CS, OH=OH, OW=OH, N=N, KH=K, KW=K, stride=s, pad=pad, act=ops.ACT_RELU, pool=pool)
+    ops.imgconv(w, y, src=x, bias=bias, argmax=am, **kw)
+    yr = torch.empty(shp)
+    amr = torch.empty(shp, dtype=torch.uint8) if pool else None
+    ops.imgconv(w.cpu(), yr, src=x.cpu(), bias=bias.cpu(), argmax=amr, **kw)
+    assert _rel(y.cpu(), yr) < 2e-2
+    if pool:
+        pos = yr > 0.05
+        assert (am.cpu()[pos] == amr[pos]).float().mean().item() > 0.97
+
+
+@pytest.mark.gpu
+def test_imgconv_dgrad_unpool_source_and_mask():
+    torch.manual_seed(2)
+    B, H, CIN, COUT, K = 3, 14, 32, 64, 5
+    dp = torch.randn(B, 7, 7, COUT).to(DEV, torch.bfloat16)
+    am = torch.randint(0, 4, (B, 7, 7, COUT), dtype=torch.uint8).to(DEV)
+    wt = (torch.randn(CIN, K, K, COUT) * 0.1).to(DEV, torch.bfloat16)
+    mask = torch.randn(B, H, H, CIN).to(DEV, torch.bfloat16)
+    y = torch.empty(B, H, H, CIN, device=DEV, dtype=torch.bfloat16)
+    kw = dict(B=B, SH=H, SW=H, CS=COUT, OH=H, OW=H, N=CIN, KH=K, KW=K, pad=K - 1 - 2, flip_taps=True)
+    ops.imgconv(wt, y, src_pooled=dp, src_argmax=am, relu_mask=mask, **kw)
+    yr = torch.empty(B, H, H, CIN)
+    ops.imgconv(wt.cpu(), yr, src_pooled=dp.cpu(), src_argmax=am.cpu(), relu_mask=mask.cpu(), **kw)
+    assert _rel(y.cpu(), yr) < 2e-2
+    assert float(y.cpu()[mask.cpu() <= 0].abs().max()) == 0.0
+
+
+WG_CASES = [  # (B, SH, CS, N, K, stride, pad, pooled_dy)
+    (5, 14, 32, 64, 5, 1, 2, True),     # MNIST conv2 (dY = un-pooled dP2)
+    (3, 32, 16, 16, 3, 1, 1, False),
+    (3, 32, 16, 32, 3, 2, 1, False),
+    (6, 8, 64, 64, 3, 1, 1, False),
+    (5, 28, 1, 32, 5, 1, 2, True),      # MNIST conv1 (1-channel tap-packed kernel, dY = un-pooled dP1)
+    (3, 28, 1, 64, 3, 2, 1, False),     # 1-channel, strided, N=64
+    (7, 12, 1, 16, 5, 1, 0, False),     # 1-channel, valid padding, OW=8
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", WG_CASES)
+def test_imgwgrad(case):
+    B, SH, CS, N, K, s, pad, pooled = case
+    OH = (SH + 2 * pad - K) // s + 1
+    torch.manual_seed(3)
+    x = torch.randn(B, SH, SH, CS).to(DEV, torch.bfloat16)
+    kw = dict(B=B, SH=SH, SW=SH, CS=CS, OH=OH, OW=OH, N=N, KH=K, KW=K, stride=s, pad=pad, scale=0.5)
+    dw = torch.zeros(N, K, K, CS, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    dwr, dbr = torch.zeros(N, K, K, CS), torch.zeros(N)
+    if pooled:
+        dp = torch.randn(B, OH // 2, OH // 2, N).to(DEV, torch.bfloat16)
+        am = torch.randint(0, 4, dp.shape, dtype=torch.uint8).to(DEV)
+        ops.imgwgrad(x, dw, db, dy_pooled=dp, dy_argmax=am, **kw)
+        ops.imgwgrad(x.cpu(), dwr, dbr, dy_pooled=dp.cpu(), dy_argmax=am.cpu(), **kw)
+    else:
+        dy = torch.randn(B, OH, OH, N).to(DEV, torch.bfloat16)
+        ops.imgwgrad(x, dw, db, dy=dy, **kw)
+        ops.imgwgrad(x.cpu(), dwr, dbr, dy=dy.cpu(), **kw)
+    assert _rel(dw.cpu(), dwr) < 1e-2
+    assert _rel(db.cpu(), dbr) < 1e-2

@@ -68,6 +68,9 @@ def test_lstm_trains_on_gpu_with_graph():
     prog = model.program("cuda", 128, seed=0)
     opt = Optimizer(model.opt_groups[0][0], prog.P)
     (xs, ys), _ = synthetic_arrays(4096, 10)
+    xs = xs.copy()
+    for k in range(10):  # class k also lights a vertical band: visible at every timestep
+        xs[ys == k, :, 2 + 2 * k:4 + 2 * k] = 255
     X = torch.from_numpy(xs.reshape(4096, 784)).float().cuda() / 255
     Y = F.one_hot(torch.from_numpy(ys).long(), 10).float().cuda()
 
