@@ -45,7 +45,7 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
           const optional<Tensor>& aux, int64_t ld_aux, int64_t aux_act, int64_t b_ones_row, double keep, int64_t seed,
           const optional<Tensor>& counter, const optional<Tensor>& pooled, const optional<Tensor>& argmax,
           int64_t PH, int64_t PW, int64_t PC, const optional<Tensor>& out2, int64_t ldc2, bool out2_trans,
-          const optional<Tensor>& bias_out) {
+          const optional<Tensor>& bias_out, const optional<Tensor>& ws, const optional<Tensor>& tile_ctr) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(out, "out");
@@ -57,15 +57,27 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   a.B = B.data_ptr(); a.ldb = ldb;
   a.b_ones_row = (int)b_ones_row;
   if (splits < 1) splits = 1;
+  int bm = 0, bn = 0;
+  const int kt = dtfe::gemm_dense_tile_dims((int)tile, bm, bn);
+  TORCH_CHECK(kt > 0, "gemm: bad tile id");
   int chunk = (int)((K + splits - 1) / splits);
-  chunk = ((chunk + dtfe::BK - 1) / dtfe::BK) * dtfe::BK;
-  if (chunk < dtfe::BK) chunk = dtfe::BK;
+  chunk = ((chunk + kt - 1) / kt) * kt;
+  if (chunk < kt) chunk = kt;
   const int real_splits = (int)((K + chunk - 1) / chunk);
   a.k_chunk = chunk;
   a.out = out.data_ptr(); a.ldc = ldc; a.out_f32 = out.scalar_type() == at::kFloat;
   a.bias = ptr_or_null<float>(bias); a.bias_axis = (int)bias_axis;
   a.act = (int)act; a.alpha = (float)alpha; a.beta = (float)beta; a.atomic = atomic;
-  TORCH_CHECK(!(real_splits > 1 && !atomic), "gemm: split-K needs atomic accumulation");
+  if (real_splits > 1 && !atomic) {
+    const int64_t ntiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    TORCH_CHECK(ws.has_value() && ws->defined() && tile_ctr.has_value() && tile_ctr->defined(),
+                "gemm: split-K with a fused epilogue needs ws/tile_ctr");
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= real_splits * ntiles * bm * bn,
+                "gemm: split-K workspace too small");
+    TORCH_CHECK(tile_ctr->scalar_type() == at::kInt && tile_ctr->numel() >= ntiles, "gemm: tile counters too small");
+    a.ws = ws->data_ptr<float>();
+    a.tile_ctr = tile_ctr->data_ptr<int>();
+  }
   TORCH_CHECK(!atomic || a.out_f32, "gemm: atomic accumulation needs an fp32 output");
   a.out2 = ptr_or_null<void>(out2); a.ldc2 = ldc2;
   a.out2_f32 = (out2.has_value() && out2->defined()) ? out2->scalar_type() == at::kFloat : 0;
@@ -438,7 +450,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor? bias, int bias_axis, int act, float alpha, float beta, bool atomic, int splits, int tile,"
       " Tensor? aux, int ld_aux, int aux_act, int b_ones_row, float keep, int seed, Tensor? counter,"
       " Tensor? pooled, Tensor? argmax, int PH, int PW, int PC, Tensor(b!)? out2, int ldc2, bool out2_trans,"
-      " Tensor(c!)? bias_out) -> ()");
+      " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");

@@ -109,6 +109,7 @@ struct Im2colLoader {
       }
     }
   }
+  template <bool FAST = false>
   __device__ __forceinline__ void load(int k0) {
     const int SH = TRANS ? g.OH : g.H, SW = TRANS ? g.OW : g.W;
     if (fast) {
@@ -198,6 +199,7 @@ struct Im2colWgradLoader {
       }
     }
   }
+  template <bool FAST = false>
   __device__ __forceinline__ void load(int k0) {
 #pragma unroll
     for (int c = 0; c < C::NC; ++c) {

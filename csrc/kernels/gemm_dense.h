@@ -6,6 +6,8 @@
 
 namespace dtfe {
 
+constexpr int GEMM_KTILE = 64;  // k-tile depth of the dense GEMMs (2 MFMA k-steps per barrier)
+
 struct DenseGemmArgs {
   int M, N, K;
   const void* A; long lda;     // A(m,k): KMAJ a[m*lda+k], RMAJ a[k*lda+m]
@@ -28,13 +30,62 @@ struct DenseGemmArgs {
   float keep; uint64_t seed; const int64_t* counter;
   // weight-gradient GEMMs: column b_ones_row (B row of ones) is routed to bias_out[m]
   float* bias_out;
+  // split-K with a fused (non-atomic) epilogue: every split stores its partial
+  // tile to ws[split][tile]; the last split to arrive (tile_ctr) sums them in
+  // fixed split order (deterministic), resets the counter and runs the epilogue
+  float* ws; int* tile_ctr;
 };
+
+// Epilogue of one output element (row < M, col < N); returns false when the
+// element was fully handled (atomic / bias column / unpool) and x must not be stored.
+__device__ __forceinline__ bool dense_epi(const DenseGemmArgs& a, int row, int col, float& x, int64_t drop_step,
+                                          float inv_keep) {
+  const long o = (long)row * a.ldc + col;
+  if (a.bias_out && col == a.b_ones_row) {  // the ones column = this layer's bias gradient
+    if (a.atomic) atomicAdd(a.bias_out + row, a.alpha * x);
+    else a.bias_out[row] = a.alpha * x;
+    return false;
+  }
+  if (a.atomic) {
+    atomicAdd(reinterpret_cast<float*>(a.out) + o, a.alpha * x);
+    return false;
+  }
+  x *= a.alpha;
+  if (a.bias) x += a.bias[a.bias_axis ? row : col];
+  x = apply_act(x, a.act);
+  if (a.keep < 1.f)
+    x = hash_uniform(a.seed, (uint64_t)drop_step * ((uint64_t)a.M * a.N) + (uint64_t)o) < a.keep ? x * inv_keep : 0.f;
+  if (a.aux) {
+    const long oa = (long)row * a.ld_aux + col;
+    const float y = a.aux_f32 ? reinterpret_cast<const float*>(a.aux)[oa] : bf2f(reinterpret_cast<const bf16*>(a.aux)[oa]);
+    x *= act_grad_from_out(y, a.aux_act);
+  }
+  if (a.unpool) {
+    unpool_store(a.up, o, x, reinterpret_cast<bf16*>(a.out));
+    return false;
+  }
+  if (a.beta != 0.f) {
+    const float old = a.out_f32 ? reinterpret_cast<float*>(a.out)[o] : bf2f(reinterpret_cast<bf16*>(a.out)[o]);
+    x += a.beta * old;
+  }
+  if (a.out2) {
+    const long o2 = a.out2_trans ? (long)col * a.ldc2 + row : (long)row * a.ldc2 + col;
+    if (a.out2_f32) reinterpret_cast<float*>(a.out2)[o2] = x;
+    else reinterpret_cast<bf16*>(a.out2)[o2] = f2bf(x);
+  }
+  return true;
+}
 
 template <typename T, typename Cfg, int AMODE, int BMODE>
 __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs a) {
-  using LA = DenseLoader<T, Cfg::BM, AMODE>;
-  using LB = DenseLoader<T, Cfg::BN, BMODE>;
-  __shared__ __attribute__((aligned(16))) T smem[SmemSize<T, Cfg, LA, LB>::ELEMS];
+  using LA = DenseLoader<T, Cfg::BM, AMODE, Cfg::BK>;
+  using LB = DenseLoader<T, Cfg::BN, BMODE, Cfg::BK>;
+  constexpr int CLD = Cfg::BN + 4;  // f32 C tile row stride: 16*(odd) bytes, conflict-free quad writes
+  constexpr int SMEM_BYTES = SmemSize<T, Cfg, LA, LB>::BYTES > Cfg::BM * CLD * 4 ? SmemSize<T, Cfg, LA, LB>::BYTES
+                                                                                   : Cfg::BM * CLD * 4;
+  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM_BYTES];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+  float* Cs = reinterpret_cast<float*>(smem_raw);
   const int tiles_m = (a.M + Cfg::BM - 1) / Cfg::BM, tiles_n = (a.N + Cfg::BN - 1) / Cfg::BN;
   int tm, tn;
   tile_coords(tiles_m, tiles_n, tm, tn);
@@ -44,59 +95,130 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
   LA la((const T*)a.A, a.lda, a.M, a.K, m_base, -1);
   LB lb((const T*)a.B, a.ldb, a.N, a.K, n_base, a.b_ones_row);
   f32x4_t acc[Cfg::TM][Cfg::TN];
-  gemm_mainloop<T, Cfg, AMODE, BMODE>(la, lb, k_begin, k_end, smem, acc);
+  gemm_mainloop<T, Cfg, AMODE, BMODE>(la, lb, k_begin, k_end, smem, acc);  // ends with a barrier
+
+  // accumulators -> f32 C tile in LDS (the operand buffers are dead), so the
+  // epilogue walks 8-column chunks: coalesced 16-32 B stores, no register-array indexing
+  {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid / Cfg::WARPS_N, wn = wid % Cfg::WARPS_N;
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < Cfg::TN; ++j) {
+        const int r = wm * Cfg::WM + i * 16 + (lane >> 4) * 4, c = wn * Cfg::WN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Cs[(r + q) * CLD + c] = acc[i][j][q];
+      }
+  }
+  __syncthreads();
+  constexpr int CPR = Cfg::BN / 8;              // 8-column chunks per row
+  constexpr int NCH = Cfg::BM * CPR;            // chunks per tile
+  if (gridDim.z > 1 && !a.atomic) {
+    // deterministic split-K: partial tile -> ws[z][tile], the last split to arrive sums in split order
+    const int tile = tm * tiles_n + tn, ntiles = tiles_m * tiles_n;
+    float* mine = a.ws + ((long)blockIdx.z * ntiles + tile) * (Cfg::BM * Cfg::BN);
+    for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
+      const int r = ch / CPR, c = (ch % CPR) * 8;
+      f32x4_t* dst = reinterpret_cast<f32x4_t*>(mine + ch * 8);
+      dst[0] = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c);
+      dst[1] = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c + 4);
+    }
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = atomicAdd(a.tile_ctr + tile, 1);
+      s_last = prev == (int)gridDim.z - 1;
+      if (s_last) a.tile_ctr[tile] = 0;  // ready for the next launch / graph replay
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
+      const int r = ch / CPR, c = (ch % CPR) * 8;
+      f32x4_t v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      for (int z = 0; z < (int)gridDim.z; ++z) {
+        const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.ws + ((long)z * ntiles + tile) * (Cfg::BM * Cfg::BN) + ch * 8);
+        v0 += __builtin_nontemporal_load(src);
+        v1 += __builtin_nontemporal_load(src + 1);
+      }
+      *reinterpret_cast<f32x4_t*>(Cs + r * CLD + c) = v0;
+      *reinterpret_cast<f32x4_t*>(Cs + r * CLD + c + 4) = v1;
+    }
+    __syncthreads();
+  }
   const int64_t drop_step = (a.keep < 1.f && a.counter) ? *a.counter : 0;
   const float inv_keep = 1.f / a.keep;
-
-  for_each_quad<Cfg>(m_base, n_base, acc, [&](int row0, int col, f32x4_t v) {
-    if (col >= a.N) return;
+  // plain-store fast path: no per-element side outputs, 16 B aligned rows
+  const bool vec_store = !a.atomic && !a.unpool && !a.out2 && !a.bias_out && a.beta == 0.f &&
+                         (a.ldc % 8) == 0 && ((((uintptr_t)a.out) & 15) == 0);
+  for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
+    const int r = ch / CPR, c = (ch % CPR) * 8;
+    const int row = m_base + r, col0 = n_base + c;
+    if (row >= a.M || col0 >= a.N) continue;
+    float x[8];
+    *reinterpret_cast<f32x4_t*>(x) = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c);
+    *reinterpret_cast<f32x4_t*>(x + 4) = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c + 4);
+    if (vec_store && col0 + 8 <= a.N) {
+      const long o = (long)row * a.ldc + col0;
+      float g[8];  // act'(aux) factors, one 16 B load when aux is bf16 and aligned
+      if (a.aux && !a.aux_f32 && (a.ld_aux % 8) == 0) {
+        const u32x4_t av = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const bf16*>(a.aux) +
+                                                              (long)row * a.ld_aux + col0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = row0 + j;
-      if (row >= a.M) continue;
-      float x = v[j];
-      const long o = (long)row * a.ldc + col;
-      if (a.bias_out && col == a.b_ones_row) {  // the ones column = this layer's bias gradient
-        if (a.atomic) atomicAdd(a.bias_out + row, a.alpha * x);
-        else a.bias_out[row] = a.alpha * x;
-        continue;
+        for (int e = 0; e < 8; ++e) g[e] = act_grad_from_out(bf2f((bf16)(av[e >> 1] >> (16 * (e & 1)))), a.aux_act);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float y = 1.f;
+          if (a.aux) {
+            const long oa = (long)row * a.ld_aux + col0 + e;
+            y = act_grad_from_out(a.aux_f32 ? reinterpret_cast<const float*>(a.aux)[oa]
+                                            : bf2f(reinterpret_cast<const bf16*>(a.aux)[oa]), a.aux_act);
+          }
+          g[e] = y;
+        }
       }
-      if (a.atomic) {
-        atomicAdd(reinterpret_cast<float*>(a.out) + o, a.alpha * x);
-        continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = x[e] * a.alpha;
+        if (a.bias) v += a.bias[a.bias_axis ? row : col0 + e];
+        v = apply_act(v, a.act);
+        if (a.keep < 1.f)
+          v = hash_uniform(a.seed, (uint64_t)drop_step * ((uint64_t)a.M * a.N) + (uint64_t)(o + e)) < a.keep ? v * inv_keep
+                                                                                                         : 0.f;
+        x[e] = v * g[e];
       }
-      x *= a.alpha;
-      if (a.bias) x += a.bias[a.bias_axis ? row : col];
-      x = apply_act(x, a.act);
-      if (a.keep < 1.f)
-        x = hash_uniform(a.seed, (uint64_t)drop_step * ((uint64_t)a.M * a.N) + (uint64_t)o) < a.keep ? x * inv_keep : 0.f;
-      if (a.aux) {
-        const long oa = (long)row * a.ld_aux + col;
-        const float y = a.aux_f32 ? reinterpret_cast<const float*>(a.aux)[oa] : bf2f(reinterpret_cast<const bf16*>(a.aux)[oa]);
-        x *= act_grad_from_out(y, a.aux_act);
+      if (a.out_f32) {
+        reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + o)[0] = *reinterpret_cast<f32x4_t*>(x);
+        reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + o)[1] = *reinterpret_cast<f32x4_t*>(x + 4);
+      } else {
+        u32x4_t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = pack_bf16x2(x[2 * e], x[2 * e + 1]);
+        *reinterpret_cast<u32x4_t*>(reinterpret_cast<bf16*>(a.out) + o) = v;
       }
-      if (a.unpool) {
-        unpool_store(a.up, (long)row * a.ldc + col, x, reinterpret_cast<bf16*>(a.out));
-        continue;
-      }
-      if (a.beta != 0.f) {
-        const float old = a.out_f32 ? reinterpret_cast<float*>(a.out)[o] : bf2f(reinterpret_cast<bf16*>(a.out)[o]);
-        x += a.beta * old;
-      }
-      if (a.out_f32) reinterpret_cast<float*>(a.out)[o] = x;
-      else reinterpret_cast<bf16*>(a.out)[o] = f2bf(x);
-      if (a.out2) {
-        const long o2 = a.out2_trans ? (long)col * a.ldc2 + row : (long)row * a.ldc2 + col;
-        if (a.out2_f32) reinterpret_cast<float*>(a.out2)[o2] = x;
-        else reinterpret_cast<bf16*>(a.out2)[o2] = f2bf(x);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = col0 + e;
+        if (col >= a.N) break;
+        float xe = x[e];
+        if (!dense_epi(a, row, col, xe, drop_step, inv_keep)) continue;
+        const long o = (long)row * a.ldc + col;
+        if (a.out_f32) reinterpret_cast<float*>(a.out)[o] = xe;
+        else reinterpret_cast<bf16*>(a.out)[o] = f2bf(xe);
       }
     }
-  });
+  }
 }
 
-// host-side launcher (defined in gemm_dense_*.hip)
+// host-side launcher (defined in gemm_dense.hip)
 // dtype: 0 = bf16, 1 = f32.  tile: 0 = 64x64, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 32x32
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream);
+// block tile of a tile id; returns the k-tile depth (split-K chunks are multiples of it)
+int gemm_dense_tile_dims(int tile, int& bm, int& bn);
 
 }  // namespace dtfe

@@ -47,6 +47,9 @@ struct ImgWgradArgs {
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
 void launch_imgconv(const ImgConvArgs& a, hipStream_t s);
+// persistent variant (weights resident in LDS, one workgroup per CU streaming images);
+// returns false when the shape does not fit it (launch_imgconv then uses the per-image kernel)
+bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s);
 bool imgwgrad_supported(const ImgWgradArgs& a);
 void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s);
 

@@ -312,6 +312,7 @@ void launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
     throw std::runtime_error("imgconv: shape not supported");
   if (a.CS == 1 && (!a.src || a.flip_taps)) throw std::runtime_error("imgconv: 1-channel path is forward-only");
   if (a.pool && ((a.OH | a.OW) & 1)) throw std::runtime_error("imgconv: pool needs even output dims");
+  if (a.CS != 1 && launch_imgconv_persistent(a, s)) return;
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
   const size_t lds = (size_t)LH * LW * a.CS * sizeof(bf16);
   if (a.N <= 16) launch_nt<1>(a, lds, s);

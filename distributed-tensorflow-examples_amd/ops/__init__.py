@@ -20,10 +20,31 @@ __all__ = [
     "gemm", "linear_fwd", "conv_fwd", "conv_dgrad", "conv_wgrad", "head_xent", "apply_gradients", "opt_pack",
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
-    "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile",
+    "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
+    "TILE_DIMS", "GEMM_KTILE",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
+TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)}
+GEMM_KTILE = 64  # k-tile depth of the dense GEMM kernels (split-K chunks are multiples of it)
+_WS = {}
+
+
+def split_workspace(device, splits, M, N, tile):
+    """(ws, tile_ctr) for a split-K GEMM with a fused epilogue: fp32 partial tiles
+    [splits][tiles][BM*BN] + per-tile arrival counters (zeroed once; the kernel
+    resets them).  Cached per device and grown on demand - callers that run
+    split-K GEMMs concurrently on several streams must pass their own."""
+    bm, bn = TILE_DIMS[tile]
+    ntiles = math.ceil(M / bm) * math.ceil(N / bn)
+    need = splits * ntiles * bm * bn
+    key = torch.device(device)
+    ws, ctr = _WS.get(key, (None, None))
+    if ws is None or ws.numel() < need or ctr.numel() < ntiles:
+        ws = torch.empty(max(need, 0 if ws is None else ws.numel()), device=key, dtype=torch.float32)
+        ctr = torch.zeros(max(ntiles, 0 if ctr is None else ctr.numel()), device=key, dtype=torch.int32)
+        _WS[key] = (ws, ctr)
+    return ws, ctr
 
 
 def pick_tile(M: int, N: int) -> int:
@@ -71,13 +92,15 @@ def _mat(t, mode, rows, K, ld):
 def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=None, bias=None, bias_axis=0,
          act=ACT_NONE, alpha=1.0, beta=0.0, atomic=False, splits=1, tile=None, aux=None, ld_aux=None, aux_act=0,
          b_ones_row=-1, keep=1.0, seed=0, counter=None, pooled=None, argmax=None, PH=0, PW=0, PC=0, out2=None,
-         ldc2=0, out2_trans=False, bias_out=None):
+         ldc2=0, out2_trans=False, bias_out=None, workspace=None):
     """out[M,N] = epilogue( A(m,k) . B(n,k) ).
 
     A(m,k) = A[m*lda+k] (KMAJ) or A[k*lda+m] (RMAJ); likewise B(n,k).
     Epilogue order: alpha*acc, +bias, act, dropout(keep), *act'(aux), [unpool | +beta*out], store.
     b_ones_row >= 0 makes B row n=b_ones_row all ones; with bias_out that output
     column goes to bias_out[m] (a weight-gradient GEMM producing the bias gradient).
+    splits > 1 without atomic: split-K whose last-arriving split runs the fused
+    epilogue (workspace = (ws, tile_ctr), default: a per-device cached one).
     """
     if lda is None:
         lda = K if amode == KMAJ else M
@@ -90,9 +113,12 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
     if out.is_cuda:
         if tile is None:
             tile = pick_tile(M, N)
+        ws = ctr = None
+        if splits > 1 and not atomic:
+            ws, ctr = workspace if workspace is not None else split_workspace(out.device, splits, M, N, tile)
         require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
                        splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
-                       PC, out2, ldc2, out2_trans, bias_out)
+                       PC, out2, ldc2, out2_trans, bias_out, ws, ctr)
         return out
     # CPU reference
     a = _mat(A, amode, M, K, lda)

@@ -78,6 +78,36 @@ def test_imgconv_dgrad_unpool_source_and_mask():
     assert float(y.cpu()[mask.cpu() <= 0].abs().max()) == 0.0
 
 
+PERSIST_CASES = [  # B > 256 so persistent workgroups loop over several images
+    (300, 14, 32, 64, 5, 1, 2, True),   # MNIST conv2 fwd
+    (300, 32, 16, 16, 3, 1, 1, False),  # ResNet-20 stage 1
+    (270, 16, 32, 32, 3, 2, 1, False),  # strided
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PERSIST_CASES)
+def test_imgconv_persistent_fwd(case):
+    test_imgconv_fwd(case)
+
+
+@pytest.mark.gpu
+def test_imgconv_persistent_dgrad_unpool_source_and_mask():
+    torch.manual_seed(4)
+    B, H, CIN, COUT, K = 300, 14, 32, 64, 5
+    dp = torch.randn(B, 7, 7, COUT).to(DEV, torch.bfloat16)
+    am = torch.randint(0, 4, (B, 7, 7, COUT), dtype=torch.uint8).to(DEV)
+    wt = (torch.randn(CIN, K, K, COUT) * 0.1).to(DEV, torch.bfloat16)
+    mask = torch.randn(B, H, H, CIN).to(DEV, torch.bfloat16)
+    y = torch.empty(B, H, H, CIN, device=DEV, dtype=torch.bfloat16)
+    kw = dict(B=B, SH=H, SW=H, CS=COUT, OH=H, OW=H, N=CIN, KH=K, KW=K, pad=K - 1 - 2, flip_taps=True)
+    ops.imgconv(wt, y, src_pooled=dp, src_argmax=am, relu_mask=mask, **kw)
+    yr = torch.empty(B, H, H, CIN)
+    ops.imgconv(wt.cpu(), yr, src_pooled=dp.cpu(), src_argmax=am.cpu(), relu_mask=mask.cpu(), **kw)
+    assert _rel(y.cpu(), yr) < 2e-2
+    assert float(y.cpu()[mask.cpu() <= 0].abs().max()) == 0.0
+
+
 WG_CASES = [  # (B, SH, CS, N, K, stride, pad, pooled_dy)
     (5, 14, 32, 64, 5, 1, 2, True),     # MNIST conv2 (dY = un-pooled dP2)
     (3, 32, 16, 16, 3, 1, 1, False),

@@ -85,6 +85,23 @@ def test_gemm_split_k_atomic_and_aux():
     assert _rel(out2.cpu(), exp) < 1e-5
 
 
+@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_split_k_fused_epilogue(tile, dtype):
+    """split-K without atomics: last-arriving split sums the partials and runs bias+ReLU;
+    run twice so the per-tile arrival counters must have been reset by the kernel."""
+    torch.manual_seed(5)
+    M, N, K = 200, 300, 1500
+    A = torch.randn(M, K).to(DEV, dtype)
+    B = torch.randn(N, K).to(DEV, dtype)
+    bias = torch.randn(N, device=DEV)
+    exp = torch.relu(A.float().cpu() @ B.float().cpu().t() + bias.cpu())
+    for _ in range(2):
+        out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+        ops.gemm(A, B, out, M=M, N=N, K=K, bias=bias, act=ops.ACT_RELU, splits=5, tile=tile)
+        assert _rel(out.cpu(), exp) < (2e-2 if dtype == torch.bfloat16 else 1e-5)
+
+
 def test_gemm_ones_row_bias_column():
     M, N, K = 48, 33, 80
     A = torch.randn(M, K, device=DEV)
