@@ -200,9 +200,14 @@ void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
 void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
-              int64_t pad, double scale) {
+              int64_t pad, double scale, const optional<Tensor>& ws) {
   check_cuda(src, "src");
   dtfe::ImgWgradArgs a{};
+  if (ws.has_value() && ws->defined()) {
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= 256 * (N * KH * KW * CS + N),
+                "imgwgrad: workspace too small");
+    a.ws = ws->data_ptr<float>();
+  }
   a.B = (int)B; a.SH = (int)SH; a.SW = (int)SW; a.CS = (int)CS; a.OH = (int)OH; a.OW = (int)OW; a.N = (int)N;
   a.KH = (int)KH; a.KW = (int)KW; a.stride = (int)stride; a.pad = (int)pad;
   a.src = reinterpret_cast<const dtfe::bf16*>(src.data_ptr());
@@ -464,7 +469,7 @@ TORCH_LIBRARY(dtfe, m) {
       " int stride, int pad, bool flip_taps, int act, bool pool) -> ()");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
-      " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale) -> ()");
+      " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None) -> ()");
   m.def("conv1_wgrad_pooled(Tensor x, Tensor dp, Tensor argmax, Tensor(a!) dw, Tensor(b!)? db, float scale) -> ()");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"

@@ -43,6 +43,10 @@ struct ImgWgradArgs {
   const bf16* dy_pooled; const uint8_t* dy_argmax;   // [B][OH/2][OW/2][N]
   float* dw; float* db; float scale;
   int imgs_per_block;
+  // optional partial-sum workspace for the persistent kernel, >= 256 * (N*KH*KW*CS + N) floats:
+  // per-workgroup partials are stored plainly and summed by a second kernel (cheaper than
+  // 256-way contended fp32 atomics on every dW element); null -> atomics
+  float* ws;
 };
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
@@ -52,5 +56,8 @@ void launch_imgconv(const ImgConvArgs& a, hipStream_t s);
 bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s);
 bool imgwgrad_supported(const ImgWgradArgs& a);
 void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s);
+// persistent variant (dW accumulated in registers across a workgroup's images);
+// returns false when the shape does not fit it
+bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s);
 
 }  // namespace dtfe

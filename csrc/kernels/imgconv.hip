@@ -651,6 +651,7 @@ void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s) {
     }
     return;
   }
+  if (launch_imgwgrad_persistent(a, s)) return;
   if (a.N <= 16) launch_wg<1, 8>(a, s);
   else if (a.N <= 32) launch_wg<2, 6>(a, s);
   else launch_wg<4, 4>(a, s);

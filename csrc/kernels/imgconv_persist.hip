@@ -30,6 +30,7 @@
 #include "imgconv.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -378,7 +379,22 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
     const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
     if (pooled && (a.SH + a.pad > LH || a.SW + a.pad > LW)) return false;
   }
-  // wave grid: 4 waves over output-row tiles x 2 over n-tiles (8 waves, 2 per SIMD)
+  // wave grid (measured on MNIST conv2, B=1024): 8 x 2 waves, 4 per SIMD (default: fwd 48 us, dgrad 68)
+  // beat 4 x 2 (48 / 74) and 4 x 1 waves holding
+  // every n-tile (fewer LDS reads, but one wave per SIMD exposes the read latency: fwd 48 vs 63 us).
+  // DTFE_IC_WAVES=4 / 8 select 4 x 1 / 4 x 2 for experiments.
+  static const int waves = [] {
+    const char* e = getenv("DTFE_IC_WAVES");
+    return e ? atoi(e) : 16;
+  }();
+  if (waves == 4) {
+    if (a.N <= 32) return pooled ? launch_cfg<2, 4, 4, 1, true>(a, s) : launch_cfg<2, 4, 4, 1, false>(a, s);
+    return pooled ? launch_cfg<4, 4, 4, 1, true>(a, s) : launch_cfg<4, 4, 4, 1, false>(a, s);
+  }
+  if (waves == 16) {  // 8 x 2 waves, 4 per SIMD
+    if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s) : launch_cfg<1, 2, 8, 2, false>(a, s);
+    return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s) : launch_cfg<2, 2, 8, 2, false>(a, s);
+  }
   if (a.N <= 32) return pooled ? launch_cfg<1, 4, 4, 2, true>(a, s) : launch_cfg<1, 4, 4, 2, false>(a, s);
   return pooled ? launch_cfg<2, 4, 4, 2, true>(a, s) : launch_cfg<2, 4, 4, 2, false>(a, s);
 }

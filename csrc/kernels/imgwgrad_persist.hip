@@ -1,0 +1,336 @@
+// Persistent whole-image weight gradient: dW accumulates in registers across
+// the images of a workgroup, one flush per workgroup.
+//
+//   dW[n][tap*CS + c] += scale * sum_{images, pixels p} dY[p][n] * X[p*stride - pad + tap][c]
+//   db[n]            += scale * sum dY[p][n]
+//
+// GEMM view per image: M = N (dY channels, MT 16-row tiles), columns = (tap, c)
+// (KC = T*CS, 16-wide column tiles spread over the 8 waves), reduction k = the
+// output pixels.  Both operands are read from LDS with ds_read_b64_tr_b16:
+//   A(m = n, k = pixel)        from the dY image   dimg[pixel][NPS]
+//   B(k = pixel, col = tap, c) from the source     simg[(y, x)][PS] at pixel + tap
+// The earlier per-launch kernel (imgconv.hip) re-staged both images for every
+// 16-column slab and flushed partial sums per 4 images; here every image is
+// staged once per CU (the next one prefetched into registers while this one's
+// MFMAs run) and the whole 64 x 800 dW of MNIST conv2 lives in the 8 waves'
+// accumulators (7 column tiles x 4 row tiles per wave).
+//
+// k order inside a 32-step: MFMA operand element j of lane (g = lane>>4) is
+// k = 16*(j>>2) + 4*g + (j&3), so each of the two transposed reads of a
+// fragment covers 8 CONSECUTIVE pixels per 32-lane half; with the pixel strides
+// of both images an odd multiple of 32 bytes those 8 x 32 B land on 8 distinct
+// 32 B bank slots (MI355X_MICROARCH.md §LDS: ds_read_b64_tr_b16 is serviced in
+// two 32-lane groups) - conflict-free.  Pixels are enumerated row by row with
+// OWP (8/16/32) pixels per row so a 32-step spans whole rows; the dummy pixels
+// (x >= OW) carry zero dY.
+#include "imgconv.h"
+
+#include <stdexcept>
+
+namespace dtfe {
+
+namespace {
+
+struct WPGeom {
+  int LH, LW;       // LDS source extent (pixels), row pitch = LW
+  int PS;           // source pixel stride (elements): 16 * odd >= CS
+  int NPS;          // dY pixel stride (elements): 16 * odd >= N
+  int OWP;          // pixels per enumerated output row (8, 16 or 32)
+  int nk;           // 32-pixel k-steps per image
+  int img_off;      // dY image offset (elements)
+  int slack;        // zero elements after the source image (dummy-pixel reads)
+  int schunks;      // 16 B source chunks per image
+  int dchunks;      // 16 B dY chunks per image (pooled chunks when pooled)
+  int ctiles;       // 16-wide column tiles (KC / 16)
+};
+
+__host__ __device__ inline int odd16(int e) {  // round up to 16 * odd elements
+  int u = (e + 15) / 16;
+  return 16 * (u | 1);
+}
+
+template <int MT, int CTW, int NPFS, int NPFD, bool POOLED>
+__global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, WPGeom G) {
+  constexpr int THREADS = 512;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* simg = lds;
+  bf16* dimg = lds + G.img_off;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+  const int CS = a.CS, PS = G.PS, NPS = G.NPS, LW = G.LW;
+  const int T = a.KH * a.KW, KC = T * CS;
+
+  for (int i = tid; i < (G.LH * LW * PS + G.slack) / 8; i += THREADS)
+    reinterpret_cast<u32x4_t*>(simg)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  for (int i = tid; i < G.nk * 32 * NPS / 8; i += THREADS)
+    reinterpret_cast<u32x4_t*>(dimg)[i] = u32x4_t{0u, 0u, 0u, 0u};
+
+  // ---- per-thread staging destinations (identical for every image)
+  int sdst[NPFS], ddst[NPFD];
+#pragma unroll
+  for (int j = 0; j < NPFS; ++j) {
+    const int i = tid + j * THREADS;
+    sdst[j] = -1;
+    if (i < G.schunks) {
+      const int cpp = CS / 8, pix = i / cpp, cc = i - pix * cpp;
+      const int sy = pix / a.SW, sx = pix - sy * a.SW, ly = sy + a.pad, lx = sx + a.pad;
+      if (ly < G.LH && lx < LW) sdst[j] = (ly * LW + lx) * PS + cc * 8;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NPFD; ++j) {
+    const int i = tid + j * THREADS;
+    ddst[j] = -1;
+    if (i < G.dchunks) {
+      const int cpp = a.N / 8, pix = i / cpp, cc = i - pix * cpp;
+      int oy, ox;
+      if (POOLED) {
+        const int PW = a.OW >> 1, py = pix / PW, px = pix - py * PW;
+        oy = 2 * py;
+        ox = 2 * px;
+      } else {
+        oy = pix / a.OW;
+        ox = pix - oy * a.OW;
+      }
+      ddst[j] = (oy * G.OWP + ox) * NPS + cc * 8;
+    }
+  }
+  u32x4_t sreg[NPFS], dreg[NPFD];
+  u32x2_t dam[NPFD];
+  auto load_img = [&](long b) {
+#pragma unroll
+    for (int j = 0; j < NPFS; ++j) {
+      const long i = tid + j * THREADS;
+      if (i < G.schunks) sreg[j] = *reinterpret_cast<const u32x4_t*>(a.src + b * G.schunks * 8 + i * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < NPFD; ++j) {
+      const long i = tid + j * THREADS;
+      if (i < G.dchunks) {
+        const long off = b * G.dchunks * 8 + i * 8;
+        if (POOLED) {
+          dreg[j] = *reinterpret_cast<const u32x4_t*>(a.dy_pooled + off);
+          dam[j] = *reinterpret_cast<const u32x2_t*>(a.dy_argmax + off);
+        } else {
+          dreg[j] = *reinterpret_cast<const u32x4_t*>(a.dy + off);
+        }
+      }
+    }
+  };
+  auto write_img = [&]() {
+#pragma unroll
+    for (int j = 0; j < NPFS; ++j)
+      if (sdst[j] >= 0) *reinterpret_cast<u32x4_t*>(simg + sdst[j]) = sreg[j];
+#pragma unroll
+    for (int j = 0; j < NPFD; ++j) {
+      if (ddst[j] < 0) continue;
+      if (!POOLED) {
+        *reinterpret_cast<u32x4_t*>(dimg + ddst[j]) = dreg[j];
+      } else {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          u32x4_t v;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t x = (dam[j][w >> 1] ^ ((uint32_t)qq * 0x01010101u)) >> (16 * (w & 1));
+            const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
+            const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
+            v[w] = dreg[j][w] & (lo_ok | hi_ok);
+          }
+          *reinterpret_cast<u32x4_t*>(dimg + ddst[j] + ((qq >> 1) * G.OWP + (qq & 1)) * NPS) = v;
+        }
+      }
+    }
+  };
+
+  // ---- per-lane read offsets.  Lane (g, q, p4) of transposed read h covers local k = 16h + 4g + q.
+  const int rows_per_step = 32 / G.OWP;
+  int koff[2];  // (oy, ox) of local k at step 0 -> source pixel offset (without tap)
+  int doff[2];  // dY row offset
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kl = 16 * h + 4 * g + q, oy = kl / G.OWP, ox = kl - oy * G.OWP;
+    koff[h] = (oy * a.stride * LW + ox * a.stride) * PS;
+    doff[h] = kl * NPS + 4 * p4;
+  }
+  const int sstep = rows_per_step * a.stride * LW * PS, dstep = 32 * NPS;
+  const int ct0 = wid * CTW;
+  int coff[CTW];  // column tile -> tap offset + channel chunk of this lane
+#pragma unroll
+  for (int c = 0; c < CTW; ++c) {
+    int col = (ct0 + c) * 16 + 4 * p4;
+    if (col >= KC) col = 0;  // dead tile: read anything, never flushed
+    const int tap = col / CS, ch = col - tap * CS, kh = tap / a.KW, kw = tap - kh * a.KW;
+    coff[c] = (kh * LW + kw) * PS + ch;
+  }
+  const int nct = min(CTW, G.ctiles - ct0);  // live column tiles of this wave (wave-uniform)
+
+  f32x4_t acc[MT][CTW];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < CTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dbacc[MT] = {};
+
+  long b = blockIdx.x;
+  if (b < a.B) load_img(b);
+  __syncthreads();
+  for (; b < a.B; b += gridDim.x) {
+    write_img();
+    __syncthreads();
+    if (b + gridDim.x < a.B) load_img(b + gridDim.x);
+    for (int s = 0; s < G.nk; ++s) {
+      bf16x8_t af[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4_t, dimg + s * dstep + doff[0] + mt * 16));
+        const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4_t, dimg + s * dstep + doff[1] + mt * 16));
+        const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        af[mt] = __builtin_bit_cast(bf16x8_t, v);
+      }
+      if (wid == 0) {  // bias gradient from the dY fragments (wave-uniform branch)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const s16x8_t v = __builtin_bit_cast(s16x8_t, af[mt]);
+          float sum = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sum += bf2f((bf16)v[e]);
+          dbacc[mt] += sum;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) {
+        if (c >= nct) break;  // wave-uniform
+        const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4_t, simg + s * sstep + koff[0] + coff[c]));
+        const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4_t, simg + s * sstep + koff[1] + coff[c]));
+        const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr, acc[mt][c], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- flush: row n = mt*16 + (lane>>4)*4 + j, column = (ct0 + c)*16 + (lane&15)
+  float* part = a.ws ? a.ws + (long)blockIdx.x * ((long)a.N * KC + a.N) : nullptr;
+#pragma unroll
+  for (int c = 0; c < CTW; ++c) {
+    if (c >= nct) break;
+    const int col = (ct0 + c) * 16 + i16;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = mt * 16 + g * 4 + j;
+        if (n >= a.N) continue;
+        if (part) part[(long)n * KC + col] = acc[mt][c][j];
+        else atomicAdd(a.dw + (long)n * KC + col, acc[mt][c][j] * a.scale);
+      }
+  }
+  if (wid == 0 && (a.db || part)) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float v = dbacc[mt];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int n = mt * 16 + i16;
+      if (lane < 16 && n < a.N) {
+        if (part) part[(long)a.N * KC + n] = v;
+        else atomicAdd(a.db + n, v * a.scale);
+      }
+    }
+  }
+}
+
+// dw[i] += scale * sum_b part[b][i] (and the bias tail into db).  blockIdx.y picks a
+// chunk of RCH partials (all loads of a thread in flight together), then one
+// atomic per element and chunk: 256 partials -> 16-way contention.
+constexpr int RCH = 16;
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int nblk, int len, int nw,
+                                                           float* dw, float* db, float scale) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= len) return;
+  const int b0 = blockIdx.y * RCH;
+  f32x4_t v[RCH];
+#pragma unroll
+  for (int j = 0; j < RCH; ++j)
+    v[j] = b0 + j < nblk ? *reinterpret_cast<const f32x4_t*>(ws + (long)(b0 + j) * len + i) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = RCH / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int j = 0; j < w; ++j) v[j] += v[j + w];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = i + e;
+    if (k < nw) atomicAdd(dw + k, scale * v[0][e]);
+    else if (k < len && db) atomicAdd(db + k - nw, scale * v[0][e]);
+  }
+}
+
+WPGeom wp_geom(const ImgWgradArgs& a) {
+  WPGeom G;
+  G.LH = (a.OH - 1) * a.stride + a.KH;
+  G.LW = (a.OW - 1) * a.stride + a.KW;
+  G.PS = odd16(a.CS);
+  G.NPS = odd16(a.N);
+  G.OWP = a.OW <= 8 ? 8 : (a.OW <= 16 ? 16 : 32);
+  const int rows = (a.OH + (32 / G.OWP) - 1) / (32 / G.OWP) * (32 / G.OWP);  // enumerated rows
+  G.nk = rows * G.OWP / 32;
+  // dummy pixels (x in [OW, OWP), rows >= OH) read up to one enumerated row past the image
+  G.slack = ((rows - a.OH + 1) * a.stride * G.LW + G.OWP * a.stride + 8) * G.PS;
+  G.img_off = (G.LH * G.LW * G.PS + G.slack + 7) / 8 * 8;
+  G.schunks = a.SH * a.SW * a.CS / 8;
+  const bool pooled = a.dy == nullptr;
+  G.dchunks = (pooled ? (a.OH / 2) * (a.OW / 2) : a.OH * a.OW) * a.N / 8;
+  G.ctiles = a.KH * a.KW * a.CS / 16;
+  return G;
+}
+
+size_t wp_lds(const WPGeom& G) { return ((size_t)G.img_off + (size_t)G.nk * 32 * G.NPS) * sizeof(bf16); }
+
+template <int MT, int CTW, bool POOLED>
+bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
+  const size_t lds = wp_lds(G);
+  if (lds > 150 * 1024) return false;
+  if ((G.ctiles + CTW - 1) / CTW > 8) return false;
+  const int npfs = (G.schunks + 511) / 512, npfd = (G.dchunks + 511) / 512;
+  const int grid = a.B < 256 ? a.B : 256;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a, G);
+    if (a.ws) {
+      const int nw = a.N * a.KH * a.KW * a.CS, len = nw + a.N;  // len % 4 == 0: N % 8 == 0
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len / 4 + 255) / 256, (grid + RCH - 1) / RCH), dim3(256), 0, s,
+                         a.ws, grid, len, nw, a.dw, a.db, a.scale);
+    }
+    return true;
+  };
+  if (npfs == 1 && npfd == 1) return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED>);
+  if (npfs == 2 && npfd == 1) return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED>);
+  if (npfs == 2 && npfd == 2) return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED>);
+  if (npfs == 1 && npfd == 2) return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED>);
+  return false;
+}
+
+}  // namespace
+
+bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s) {
+  if (a.CS % 16 || a.N % 8 || a.N > 64 || a.OW > 32 || a.B < 128) return false;
+  const bool pooled = a.dy == nullptr;
+  if (pooled && ((a.OH | a.OW) & 1)) return false;
+  const WPGeom G = wp_geom(a);
+  // 8 waves share the column tiles; MNIST conv2: 50 tiles -> 7 per wave
+  const int ctw = (G.ctiles + 7) / 8;
+  if (a.N > 32) {
+    if (ctw <= 7) return pooled ? wp_launch<4, 7, true>(a, G, s) : wp_launch<4, 7, false>(a, G, s);
+    return false;
+  }
+  if (ctw <= 8) return pooled ? wp_launch<2, 8, true>(a, G, s) : wp_launch<2, 8, false>(a, G, s);
+  return false;
+}
+
+}  // namespace dtfe

@@ -266,12 +266,30 @@ def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None
     return y
 
 
+_WG_WS = {}
+
+
+def wgrad_workspace(device, numel):
+    """Cached fp32 partial-sum buffer for the persistent weight-gradient kernel
+    (per device, grown on demand; single-stream use)."""
+    key = torch.device(device)
+    ws = _WG_WS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(numel, device=key, dtype=torch.float32)
+        _WG_WS[key] = ws
+    return ws
+
+
 def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
-             dy_argmax=None, scale=1.0):
-    """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY."""
+             dy_argmax=None, scale=1.0, workspace=None):
+    """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY.
+    On the GPU the persistent kernel stores per-workgroup partials in `workspace`
+    (default: a cached per-device buffer) and a second kernel sums them."""
     if dw.is_cuda:
+        if workspace is None and CS % 16 == 0:
+            workspace = wgrad_workspace(dw.device, 256 * (N * KH * KW * CS + N))
         require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
-                           scale)
+                           scale, workspace)
         return
     d = dy.float().view(B, OH, OW, N) if dy is not None else _unpooled_nhwc(dy_pooled, dy_argmax, B, OH, OW, N)
     gw = torch.nn.grad.conv2d_weight(src.float().view(B, SH, SW, CS).permute(0, 3, 1, 2), (N, CS, KH, KW),

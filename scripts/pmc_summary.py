@@ -7,9 +7,11 @@ import sys
 
 
 def short(name):
-    n = re.sub(r"\(.*$", "", name)
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(dtfe::.*$", "", n)
+    n = re.sub(r"\(.*$", "", n)
     n = n.replace("void ", "").replace("dtfe::", "")
-    return n[:60]
+    return n[:80]
 
 
 def main(paths):

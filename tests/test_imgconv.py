@@ -141,3 +141,19 @@ def test_imgwgrad(case):
         ops.imgwgrad(x.cpu(), dwr, dbr, dy=dy.cpu(), **kw)
     assert _rel(dw.cpu(), dwr) < 1e-2
     assert _rel(db.cpu(), dbr) < 1e-2
+
+
+PERSIST_WG_CASES = [  # B >= 128: persistent register-accumulating kernel
+    (300, 14, 32, 64, 5, 1, 2, True),   # MNIST conv2 (dY = un-pooled dP2)
+    (300, 16, 32, 32, 3, 1, 1, False),
+    (260, 8, 64, 64, 3, 1, 1, False),
+    (300, 32, 16, 16, 3, 1, 1, False),
+    (200, 16, 16, 32, 3, 2, 1, False),  # strided
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PERSIST_WG_CASES)
+def test_imgwgrad_persistent(case):
+    test_imgwgrad(case)
+
