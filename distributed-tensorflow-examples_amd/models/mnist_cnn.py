@@ -41,6 +41,7 @@ import torch
 
 from .. import ops
 from ..optim import FlatParams, Optimizer, OptimizerConfig, VarSpec
+from .base import ModelDef, StepProgram
 
 IMG, C1, C2, FC, NCLS = 28, 32, 64, 1024, 10
 KS = 5
@@ -128,20 +129,25 @@ class MnistCnnTrainer:
     """Per-rank training-step program for the MNIST CNN."""
 
     def __init__(self, batch: int, device, lr: float = 1e-3, keep_prob: float = 0.75, seed: int = 0,
-                 data: SyntheticMnist | None = None, allreduce=None, world_size: int = 1):
+                 data: SyntheticMnist | None = None, allreduce=None, world_size: int = 1, P: FlatParams | None = None,
+                 standalone: bool = True):
+        """standalone: own optimizer + HBM dataset (bench / smoke).  With standalone=False the
+        caller supplies P and the batches (``CnnProgram``: ps / all-reduce roles of train.py)."""
         self.B = batch
         self.device = torch.device(device)
-        assert self.device.type == "cuda", "MnistCnnTrainer runs on the MI355X kernel path"
-        ops.require()
+        if self.device.type == "cuda":
+            ops.require()  # GPU buffers always take the HIP kernels; fail loudly without them
         self.keep = keep_prob
         self.seed = seed
         self.world = world_size
         self.allreduce = allreduce
         specs, self.names = var_specs()
-        self.P = FlatParams(specs, self.device, seed=seed)
+        self.P = P if P is not None else FlatParams(specs, self.device, seed=seed)
         self.global_step = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.opt = Optimizer(OptimizerConfig(kind="adam", lr=lr), self.P, global_step=self.global_step)
-        self.data = data or SyntheticMnist(60000, self.device, seed=seed + 17)
+        self.opt = self.data = None
+        if standalone:
+            self.opt = Optimizer(OptimizerConfig(kind="adam", lr=lr), self.P, global_step=self.global_step)
+            self.data = data or SyntheticMnist(60000, self.device, seed=seed + 17)
         d = self.device
         B = batch
         bf = torch.bfloat16
@@ -185,8 +191,9 @@ class MnistCnnTrainer:
         P.grad.zero_()
         self.loss_sum.zero_()
         self.correct.zero_()
-        ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
-                        seed=self.seed + 1, counter=self.data_ctr, done=self.data_done)
+        if self.data is not None:  # standalone: sample the batch on device (advances data_ctr)
+            ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
+                            seed=self.seed + 1, counter=self.data_ctr, done=self.data_done)
         ops.imgconv(self.w["wc1"], self.p1, src=self.x, bias=self.b["bc1"], argmax=self.a1, act=ops.ACT_RELU,
                     pool=True, **self.ic1)
         ops.imgconv(self.w["wc2"], self.p2, src=self.p1, bias=self.b["bc2"], argmax=self.a2, act=ops.ACT_RELU,
@@ -232,3 +239,56 @@ class MnistCnnTrainer:
         f1 = 2 * 7 * 7 * C2 * FC
         f2 = 2 * FC * NCLS
         return c1 * 2 + c2 * 3 + f1 * 3 + f2 * 3  # conv1 has no dgrad
+
+
+# ----------------------------------------------------------------------------
+# ModelDef for the cluster roles of train.py (ps / sync ps / all-reduce / local):
+# BASELINE.json config 4 "MNIST CNN parameter-server async SGD, 1 ps + 8 workers".
+def tf_var_order():
+    """TF creation order: weights dict, biases dict (Variable..Variable_7), then global_step."""
+    return ["Variable"] + ["Variable_%d" % i for i in range(1, 9)]
+
+
+class MnistCnnModel(ModelDef):
+    """``ModelDef`` of the CNN (TensorFlow-Examples convolutional_network hyper-parameters:
+    batch 128, Adam 1e-3, dropout keep 0.75)."""
+    name = "cnn"
+    default_batch = 128
+    default_steps = 500
+    gs_increments = 1
+    needs_labels = True
+
+    def __init__(self, lr: float = 1e-3):
+        self.specs, self.names = var_specs()
+        self.var_order = tf_var_order()
+        self.gs_name = "Variable_8"
+        self.opt_groups = [(OptimizerConfig(kind="adam", lr=lr), [s.name for s in self.specs],
+                            ("beta1_power", "beta2_power"))]
+
+    def program(self, device, batch_size=None, seed: int = 0):
+        return CnnProgram(self, device, batch_size or self.default_batch, seed)
+
+
+class CnnProgram(StepProgram):
+    """StepProgram over MnistCnnTrainer's fused kernels (batches fed by the caller)."""
+
+    def __init__(self, model, device, batch_size: int, seed: int = 0):
+        super().__init__(model, device, batch_size, seed)
+        self.core = MnistCnnTrainer(batch_size, self.device, seed=seed, P=self.P, standalone=False)
+
+    def load_batch(self, batch):
+        x, y = batch
+        B = self.batch_size
+        c = self.core
+        c.x.copy_(x.reshape(B, IMG, IMG, 1).to(c.x.dtype))
+        lab = y.reshape(B, -1)
+        c.labels.copy_((lab.argmax(1) if lab.shape[1] > 1 else lab[:, 0]).to(c.labels.dtype))
+        c.data_ctr += 1  # dropout stream position (the HBM gather advances it in standalone mode)
+
+    def compute_grads(self):
+        self.core.forward_backward()
+        return {"loss": self.core.loss_sum / self.batch_size, "correct": self.core.correct}
+
+    def evaluate(self, images, labels) -> float:
+        raise NotImplementedError("the CNN example has no evaluation step")
+

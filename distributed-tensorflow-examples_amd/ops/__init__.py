@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
 from ._lib import (ACT_CODES, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, KMAJ, OPT_ADAM, OPT_MOMENTUM,
@@ -58,6 +59,18 @@ def pick_tile(M: int, N: int) -> int:
 
 
 # --------------------------------------------------------------- references
+def hash_uniform(seed, idx):
+    """Host mirror of the kernels' counter-based RNG (common.h hash_u32/hash_uniform):
+    splitmix-style 64-bit mix of (seed, element index) -> uniform [0, 1) with 24 bits."""
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + np.asarray(idx, dtype=np.uint64)
+             * np.uint64(0xD1B54A32D192ED03) + np.uint64(0x632BE59BD9B4E019))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return ((z & np.uint64(0xFFFFFFFF)) >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
 def _act_ref(x, act):
     if act == ACT_RELU:
         return torch.relu(x)
@@ -146,7 +159,10 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
         x = x + (bias.float().view(1, -1) if bias_axis == 0 else bias.float().view(-1, 1))
     x = _act_ref(x, act)
     if keep < 1.0:
-        raise NotImplementedError("dropout reference path: use the GPU kernels")
+        step = int(counter.reshape(-1)[0].item()) if counter is not None else 0
+        oidx0 = torch.arange(M).unsqueeze(1) * ldc + torch.arange(N).unsqueeze(0)
+        u = hash_uniform(seed, oidx0.reshape(-1).numpy().astype(np.uint64) + np.uint64(step * M * N))
+        x = torch.where(torch.from_numpy(u).reshape(M, N) < keep, x / keep, torch.zeros_like(x))
     if aux is not None:
         aidx = torch.arange(M).unsqueeze(1) * ld_aux + torch.arange(N).unsqueeze(0)
         x = x * _act_grad_from_out_ref(aux.reshape(-1).float()[aidx], aux_act)

@@ -17,9 +17,11 @@ and starts an in-process gRPC server per task (GAN:97-106).  Here the same
 from __future__ import annotations
 
 import datetime
+import socket
 import os
 from dataclasses import dataclass
 
+import torch
 import torch.distributed as dist
 
 
@@ -96,21 +98,38 @@ class Server:
                                    use_libuv=True)
         self.target = "grpc://" + (cluster.ps + cluster.worker)[self.rank]
         if not dist.is_initialized():
-            kw = {}
-            if backend == "nccl" and device is not None:
-                kw["device_id"] = device
-            dist.init_process_group(backend, store=dist.PrefixStore("pg", self.store), rank=self.rank,
-                                    world_size=self.world, timeout=timeout, **kw)
+            # RCCL for device tensors, gloo for the small host-side headers / control tensors
+            pg_backend = "cpu:gloo,cuda:nccl" if backend == "nccl" else backend
+            dist.init_process_group(pg_backend, store=dist.PrefixStore("pg", self.store), rank=self.rank,
+                                    world_size=self.world, timeout=timeout)
+        # which GPU every rank drives: a (ps, worker) pair on one GPU cannot share an RCCL
+        # communicator (duplicate device), so that pair moves its payloads through host memory
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        ident = "%s/%s" % (socket.gethostname(), self.device)
+        self.store.set("dtfe/dev/%d" % self.rank, ident)
+        self._dev_ident = {r: self.store.get("dtfe/dev/%d" % r).decode() for r in range(self.world)}
         # one 2-rank group per (ps, worker) pair, created in the same order on every rank
         self.pair_groups = {}
         for p in cluster.ps_ranks():
             for w in cluster.worker_ranks():
-                g = dist.new_group([p, w], backend=backend if backend != "nccl" else None)
-                self.pair_groups[(p, w)] = g
+                self.pair_groups[(p, w)] = dist.new_group([p, w])
         self.worker_group = dist.new_group(cluster.worker_ranks()) if cluster.worker else None
 
     def pair(self, ps_rank: int, worker_rank: int):
         return self.pair_groups[(ps_rank, worker_rank)]
+
+    def colocated(self, a: int, b: int) -> bool:
+        """True when ranks a and b drive the same GPU of the same host."""
+        ia, ib = self._dev_ident[a], self._dev_ident[b]
+        return ia == ib and not ia.endswith("/cpu")
+
+    def pair_comm_device(self, ps_rank: int, worker_rank: int, device):
+        """Device of the payload tensors a (ps, worker) pair exchanges: the GPU (RCCL
+        over xGMI) unless the backend is gloo or both ranks share one GPU (host)."""
+        device = torch.device(device)
+        if self.backend != "nccl" or device.type != "cuda" or self.colocated(ps_rank, worker_rank):
+            return torch.device("cpu")
+        return device
 
     def shutdown(self):
         if dist.is_initialized():

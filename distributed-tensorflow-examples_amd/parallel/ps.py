@@ -150,8 +150,9 @@ class PSServer:
     def _serve(self, worker_rank: int):
         g = self.server.pair(self.server.rank, worker_rank)
         sh = self.shard
+        cdev = self.server.pair_comm_device(self.server.rank, worker_rank, self.comm_device)
         hdr = torch.zeros(4, dtype=torch.int64)
-        pay = torch.zeros(sh.numel, dtype=torch.float32, device=self.comm_device)
+        pay = torch.zeros(sh.numel, dtype=torch.float32, device=cdev)
         try:
             while True:
                 dist.recv(hdr, src=worker_rank, group=g)
@@ -178,7 +179,7 @@ class PSServer:
                     self._reply_hdr(worker_rank, g)
                     continue
                 if typ == SET_STATE:
-                    st = torch.zeros(sh.state_numel(), dtype=torch.float32, device=self.comm_device)
+                    st = torch.zeros(sh.state_numel(), dtype=torch.float32, device=cdev)
                     gsv = torch.zeros(1, dtype=torch.int64)
                     dist.recv(st, src=worker_rank, group=g)
                     dist.recv(gsv, src=worker_rank, group=g)
@@ -191,7 +192,7 @@ class PSServer:
                     continue
                 if typ == SAVE:
                     with sh.lock:
-                        st = sh.state_payload().to(self.comm_device)
+                        st = sh.state_payload().to(cdev)
                     self._reply_hdr(worker_rank, g)
                     dist.send(st, dst=worker_rank, group=g)
                     continue
@@ -206,7 +207,7 @@ class PSServer:
                             sh.apply(pay.to(sh.device))
                 # PULL and PUSH both answer with fresh parameters
                 with sh.lock:
-                    params = sh.P.master.to(self.comm_device, copy=True)
+                    params = sh.P.master.to(cdev, copy=True)
                 self._reply_hdr(worker_rank, g)
                 dist.send(params, dst=worker_rank, group=g)
         except Exception as e:  # noqa: BLE001 - a worker vanished: keep serving the others
@@ -271,10 +272,12 @@ class PSClient:
                 o_sh = layout.offsets[s.name]
                 idx_src.append(torch.arange(o_full, o_full + s.numel))
                 idx_dst.append(torch.arange(o_sh, o_sh + s.numel))
+            ps_rank = server.cluster.rank_of("ps", ps_task)
+            dev = server.pair_comm_device(ps_rank, server.rank, self.comm_device)
             self.shards[ps_task] = dict(
-                rank=server.cluster.rank_of("ps", ps_task), numel=layout.total,
-                src=torch.cat(idx_src).to(full.device), dst=torch.cat(idx_dst).to(self.comm_device),
-                buf=torch.zeros(layout.total, dtype=torch.float32, device=self.comm_device), layout=layout)
+                rank=ps_rank, numel=layout.total, dev=dev,
+                src=torch.cat(idx_src).to(full.device), dst=torch.cat(idx_dst).to(dev),
+                buf=torch.zeros(layout.total, dtype=torch.float32, device=dev), layout=layout)
         self.versions = {k: 0 for k in self.shards}
         self.global_step = 0
         self.initialized = False
@@ -292,7 +295,7 @@ class PSClient:
 
     def _gather(self, src_flat, sh):
         sh["buf"].zero_()
-        sh["buf"][sh["dst"]] = src_flat[sh["src"]].to(self.comm_device)
+        sh["buf"][sh["dst"]] = src_flat[sh["src"]].to(sh["dev"])
         return sh["buf"]
 
     def _scatter_params(self, sh):
@@ -355,7 +358,7 @@ class PSClient:
                 if sh["rank"] == self.gs_ps:
                     gs = g
                 n = int(self._state_numel[k])
-                st = torch.zeros(n, dtype=torch.float32, device=self.comm_device)
+                st = torch.zeros(n, dtype=torch.float32, device=sh["dev"])
                 dist.recv(st, src=sh["rank"], group=self._g(sh["rank"]))
                 out[k] = st.cpu()
         return out, gs
@@ -365,7 +368,7 @@ class PSClient:
         with self.lock:
             for k, sh in self.shards.items():
                 self._send_hdr(sh["rank"], SET_STATE)
-                dist.send(states[k].to(self.comm_device), dst=sh["rank"], group=self._g(sh["rank"]))
+                dist.send(states[k].to(sh["dev"]), dst=sh["rank"], group=self._g(sh["rank"]))
                 dist.send(torch.tensor([gs], dtype=torch.int64), dst=sh["rank"], group=self._g(sh["rank"]))
             for sh in self.shards.values():
                 self._recv_hdr(sh["rank"])

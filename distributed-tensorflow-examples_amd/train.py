@@ -29,6 +29,7 @@ from .data.mnist import DeviceBatcher, read_data_sets
 from .models.autoencoder import AutoencoderModel
 from .models.gan import LR as GAN_LR, GanModel
 from .models.lstm import LR as LSTM_LR, LstmModel
+from .models.mnist_cnn import MnistCnnModel
 from .models.softmax_reg import SoftmaxRegressionModel
 from .models.autoencoder import LR as ENC_LR
 from .optim import Optimizer
@@ -45,6 +46,7 @@ MODELS = {
     "encoder": (AutoencoderModel, ENC_LR),
     "lstm": (LstmModel, LSTM_LR),
     "softmax": (SoftmaxRegressionModel, 0.01),
+    "cnn": (MnistCnnModel, 0.001),
 }
 
 

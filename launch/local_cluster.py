@@ -21,7 +21,7 @@ import threading
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPTS = {m: os.path.join(ROOT, "examples", m, "distributed_%s.py" % m) for m in ("gan", "encoder", "lstm",
-                                                                                   "softmax")}
+                                                                                   "softmax", "cnn")}
 
 
 def free_ports(n):

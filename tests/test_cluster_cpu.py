@@ -145,3 +145,20 @@ def test_killed_non_chief_worker_does_not_stall_others(tmp_path):
         for p in (ps, w0, w1):
             if p.poll() is None:
                 p.kill()
+
+
+def test_cnn_1ps_2workers_async_checkpoint_keys(tmp_path):
+    """BASELINE.json config 4 on CPU/gloo: the MNIST CNN through the ps roles, TF variable names
+    (Variable..Variable_7 + Adam slots + beta powers + global step Variable_8) in the checkpoint."""
+    md = str(tmp_path / "ck")
+    codes, out, _ = local_cluster.launch("cnn", 1, 2, COMMON + ["--num_steps=6", "--workers=2", "--batch_size=8",
+                                                                 "--model_dir=" + md, "--save_model_secs=0.1"],
+                                         timeout=300, stream=False)
+    assert all(c == 0 for c in codes.values()), (codes, out)
+    steps = _gs_lines(out[("worker", 0)]) + _gs_lines(out[("worker", 1)])
+    assert max(steps) >= 6
+    t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
+    assert tuple(t["Variable"].shape) == (5, 5, 1, 32)          # TF layout [KH][KW][Cin][Cout]
+    assert tuple(t["Variable_2"].shape) == (3136, 1024)         # fc1 [in][out]
+    assert "Variable_2/Adam" in t and "Variable_2/Adam_1" in t and "beta1_power" in t
+    assert int(t["Variable_8"]) >= 1
