@@ -11,6 +11,7 @@
 #include "../kernels/conv.h"
 #include "../kernels/conv1.h"
 #include "../kernels/imgconv.h"
+#include "../kernels/norm.h"
 #include "../kernels/elementwise.h"
 #include "../kernels/gemm_dense.h"
 #include "../kernels/head.h"
@@ -445,7 +446,121 @@ void lstm_cell_bwd(const Tensor& act, const optional<Tensor>& c_prev, const Tens
 
 }  // namespace
 
+// ------------------------------------------------------------------- norm
+dtfe::BnArgs bn_common(const Tensor& x, const Tensor& stats, int64_t act) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() >= 2, "bn: bf16 [..., C] input");
+  dtfe::BnArgs a{};
+  a.C = (int)x.size(-1);
+  a.R = x.numel() / a.C;
+  a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 2 * a.C, "bn: stats [2][C] fp32");
+  a.stats = stats.data_ptr<float>();
+  a.act = (int)act;
+  return a;
+}
+
+void bn_stats(const Tensor& x, const Tensor& stats) {
+  dtfe::launch_bn_stats(bn_common(x, stats, 0), cur_stream());
+}
+
+void bn_apply(const Tensor& x, const Tensor& stats, const Tensor& gamma, const Tensor& beta,
+              const optional<Tensor>& mean, const optional<Tensor>& invstd, const optional<Tensor>& moving_mean,
+              const optional<Tensor>& moving_var, double eps, double momentum, int64_t act,
+              const optional<Tensor>& res, int64_t rstride, int64_t OH, int64_t OW, const Tensor& out) {
+  dtfe::BnArgs a = bn_common(x, stats, act);
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.mean = ptr_or_null<float>(mean);
+  a.invstd = ptr_or_null<float>(invstd);
+  a.moving_mean = ptr_or_null<float>(moving_mean);
+  a.moving_var = ptr_or_null<float>(moving_var);
+  a.eps = (float)eps; a.momentum = (float)momentum;
+  a.res = ptr_or_null<dtfe::bf16>(res);
+  if (a.res) {
+    TORCH_CHECK(res->dim() == 4, "bn_apply: residual NHWC");
+    a.RH = (int)res->size(1); a.RW = (int)res->size(2); a.RC = (int)res->size(3);
+    a.rstride = (int)rstride; a.OH = (int)OH; a.OW = (int)OW;
+  }
+  TORCH_CHECK(out.numel() == x.numel() && out.scalar_type() == at::kBFloat16, "bn_apply: out");
+  a.out = reinterpret_cast<dtfe::bf16*>(out.data_ptr());
+  dtfe::launch_bn_apply(a, cur_stream());
+}
+
+void bn_bwd_stats(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
+                  const Tensor& invstd, const Tensor& stats, int64_t act) {
+  dtfe::BnArgs a = bn_common(x, stats, act);
+  a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
+  a.y = ptr_or_null<dtfe::bf16>(y);
+  TORCH_CHECK(act == 0 || a.y, "bn_bwd: the activation gradient needs the forward output");
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  dtfe::launch_bn_bwd_stats(a, cur_stream());
+}
+
+void bn_bwd_apply(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
+                  const Tensor& invstd, const Tensor& gamma, const Tensor& stats, int64_t act, const Tensor& dx,
+                  const optional<Tensor>& dres, const optional<Tensor>& dgamma, const optional<Tensor>& dbeta) {
+  dtfe::BnArgs a = bn_common(x, stats, act);
+  a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
+  a.y = ptr_or_null<dtfe::bf16>(y);
+  TORCH_CHECK(act == 0 || a.y, "bn_bwd: the activation gradient needs the forward output");
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.gamma = gamma.data_ptr<float>();
+  a.out = reinterpret_cast<dtfe::bf16*>(dx.data_ptr());
+  a.dres = ptr_or_null<dtfe::bf16>(dres);
+  a.dgamma = ptr_or_null<float>(dgamma);
+  a.dbeta = ptr_or_null<float>(dbeta);
+  dtfe::launch_bn_bwd_apply(a, cur_stream());
+}
+
+void shortcut_grad_add(const Tensor& g, const Tensor& dx, int64_t stride) {
+  TORCH_CHECK(g.dim() == 4 && dx.dim() == 4, "shortcut_grad_add: NHWC tensors");
+  dtfe::launch_shortcut_grad_add(reinterpret_cast<const dtfe::bf16*>(g.data_ptr()),
+                                 reinterpret_cast<dtfe::bf16*>(dx.data_ptr()), (int)g.size(0), (int)g.size(1),
+                                 (int)g.size(2), (int)g.size(3), (int)dx.size(1), (int)dx.size(2), (int)dx.size(3),
+                                 (int)stride, cur_stream());
+}
+
+void gap_fwd(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.dim() == 4, "gap_fwd: NHWC input");
+  dtfe::launch_gap_fwd(reinterpret_cast<const dtfe::bf16*>(x.data_ptr()), reinterpret_cast<dtfe::bf16*>(y.data_ptr()),
+                       (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(3), cur_stream());
+}
+
+void gap_bwd(const Tensor& dy, const Tensor& dx) {
+  TORCH_CHECK(dx.dim() == 4, "gap_bwd: NHWC output");
+  dtfe::launch_gap_bwd(reinterpret_cast<const dtfe::bf16*>(dy.data_ptr()), reinterpret_cast<dtfe::bf16*>(dx.data_ptr()),
+                       (int)dx.size(0), (int)(dx.size(1) * dx.size(2)), (int)dx.size(3), cur_stream());
+}
+
+void maxpool3_fwd(const Tensor& x, const Tensor& y, const Tensor& am) {
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4, "maxpool3: NHWC tensors");
+  dtfe::launch_maxpool3_fwd(reinterpret_cast<const dtfe::bf16*>(x.data_ptr()), reinterpret_cast<dtfe::bf16*>(y.data_ptr()),
+                            am.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+                            (int)y.size(1), (int)y.size(2), cur_stream());
+}
+
+void maxpool3_bwd(const Tensor& dy, const Tensor& am, const Tensor& dx) {
+  dtfe::launch_maxpool3_bwd(reinterpret_cast<const dtfe::bf16*>(dy.data_ptr()), am.data_ptr<uint8_t>(),
+                            reinterpret_cast<dtfe::bf16*>(dx.data_ptr()), (int)dx.size(0), (int)dx.size(1),
+                            (int)dx.size(2), (int)dx.size(3), (int)dy.size(1), (int)dy.size(2), cur_stream());
+}
+
 TORCH_LIBRARY(dtfe, m) {
+  m.def("bn_stats(Tensor x, Tensor(a!) stats) -> ()");
+  m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
+        " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
+        " int rstride, int OH, int OW, Tensor(e!) out) -> ()");
+  m.def("bn_bwd_stats(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) stats, int act) -> ()");
+  m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor stats,"
+        " int act, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta) -> ()");
+  m.def("shortcut_grad_add(Tensor g, Tensor(a!) dx, int stride) -> ()");
+  m.def("gap_fwd(Tensor x, Tensor(a!) y) -> ()");
+  m.def("gap_bwd(Tensor dy, Tensor(a!) dx) -> ()");
+  m.def("maxpool3_fwd(Tensor x, Tensor(a!) y, Tensor(b!) am) -> ()");
+  m.def("maxpool3_bwd(Tensor dy, Tensor am, Tensor(a!) dx) -> ()");
   m.def("lstm_cell_fwd(Tensor gates, Tensor(a!) act, Tensor? c_prev, Tensor(b!) c, Tensor(c!) h_out, int ld_h,"
         " float forget_bias) -> ()");
   m.def("lstm_cell_bwd(Tensor act, Tensor? c_prev, Tensor c, Tensor? dh, Tensor? dh2, Tensor? dc_next,"
@@ -500,6 +615,15 @@ TORCH_LIBRARY(dtfe, m) {
 }
 
 TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
+  m.impl("bn_stats", &bn_stats);
+  m.impl("bn_apply", &bn_apply);
+  m.impl("bn_bwd_stats", &bn_bwd_stats);
+  m.impl("bn_bwd_apply", &bn_bwd_apply);
+  m.impl("shortcut_grad_add", &shortcut_grad_add);
+  m.impl("gap_fwd", &gap_fwd);
+  m.impl("gap_bwd", &gap_bwd);
+  m.impl("maxpool3_fwd", &maxpool3_fwd);
+  m.impl("maxpool3_bwd", &maxpool3_bwd);
   m.impl("gemm", &gemm);
   m.impl("conv_fwd", &conv_fwd);
   m.impl("conv_dgrad", &conv_dgrad);

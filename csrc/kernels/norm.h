@@ -1,0 +1,55 @@
+#pragma once
+#include "common.h"
+
+namespace dtfe {
+
+// BatchNorm (training mode) over NHWC bf16 activations viewed as [R = B*H*W][C]
+// (C % 8 == 0), plus the residual-shortcut and pooling pieces of a ResNet block.
+//
+// Forward:   stats += (sum d, sum d^2), d = x - x[row 0]        (bn_stats, atomics into a zeroed [2][C])
+//            y = act(gamma * (x - mean) * invstd + beta + shortcut(res))   (bn_apply)
+//            the apply launch also stores mean / invstd and updates the moving averages
+// Backward:  g = dy * act'(y);  stats += (sum g, sum g * xhat)  (bn_bwd_stats)
+//            dx = gamma * invstd * (g - sum g / R - xhat * sum(g xhat) / R)   (bn_bwd_apply)
+//            dgamma += sum(g xhat), dbeta += sum g; optional dres = g (shortcut gradient)
+//
+// Shortcut modes (ResNet v1 "option A" identity): the residual tensor has
+// (RH, RW, RC) and is read at (y*rstride, x*rstride, c) for c < RC, zero for
+// the extra channels of a widening block.
+struct BnArgs {
+  long R; int C;
+  const bf16* x;                 // [R][C] pre-normalisation input (conv output)
+  const bf16* y;                 // forward output (backward: ReLU mask source)
+  const bf16* dy;                // backward: upstream gradient [R][C]
+  float* stats;                  // [2][C] accumulators (zeroed by the caller)
+  const float* gamma; const float* beta;
+  float* mean; float* invstd;    // saved batch statistics [C]
+  float* moving_mean; float* moving_var;
+  float eps, momentum;           // TF: moving = moving * momentum + batch * (1 - momentum)
+  int act;
+  // residual (forward add / backward copy of the masked gradient)
+  const bf16* res; bf16* dres; int RH, RW, RC, rstride, OH, OW;
+  bf16* out;                     // forward y / backward dx
+  float* dgamma; float* dbeta;   // backward parameter gradients (+=)
+};
+
+void launch_bn_stats(const BnArgs& a, hipStream_t s);
+void launch_bn_apply(const BnArgs& a, hipStream_t s);
+void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s);
+void launch_bn_bwd_apply(const BnArgs& a, hipStream_t s);
+
+// dx[b, y*stride, x*stride, c] += g[b, y, x, c] for c < XC (option-A shortcut gradient)
+void launch_shortcut_grad_add(const bf16* g, bf16* dx, int B, int OH, int OW, int C, int XH, int XW, int XC,
+                              int stride, hipStream_t s);
+
+// global average pool: x [B][HW][C] -> y [B][C] (bf16), and its backward
+void launch_gap_fwd(const bf16* x, bf16* y, int B, int HW, int C, hipStream_t s);
+void launch_gap_bwd(const bf16* dy, bf16* dx, int B, int HW, int C, hipStream_t s);
+
+// 3x3/stride-2/pad-1 max pool (ResNet-50 stem) with argmax (0..8), and its backward
+void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int W, int C, int OH, int OW,
+                         hipStream_t s);
+void launch_maxpool3_bwd(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH, int OW,
+                         hipStream_t s);
+
+}  // namespace dtfe

@@ -43,10 +43,11 @@ def _find(data_dir, stem):
 
 
 class DataSet:
-    def __init__(self, images_u8: np.ndarray, labels: np.ndarray, one_hot: bool, seed: int):
+    def __init__(self, images_u8: np.ndarray, labels: np.ndarray, one_hot: bool, seed: int, num_classes: int = 10):
         self.images_u8 = images_u8.reshape(images_u8.shape[0], -1)
         self.labels_int = labels.astype(np.int64)
         self.one_hot = one_hot
+        self.num_classes = num_classes
         self._batcher = native.rt().EpochBatcher(self.num_examples, seed)
 
     @property
@@ -60,7 +61,7 @@ class DataSet:
     @property
     def labels(self):
         if self.one_hot:
-            out = np.zeros((len(self.labels_int), 10), dtype=np.float32)
+            out = np.zeros((len(self.labels_int), self.num_classes), dtype=np.float32)
             out[np.arange(len(self.labels_int)), self.labels_int] = 1.0
             return out
         return self.labels_int
@@ -76,7 +77,7 @@ class DataSet:
         idx = self.next_batch_indices(batch_size)
         x = self.images_u8[idx].astype(np.float32) / 255.0
         if self.one_hot:
-            y = np.zeros((batch_size, 10), dtype=np.float32)
+            y = np.zeros((batch_size, self.num_classes), dtype=np.float32)
             y[np.arange(batch_size), self.labels_int[idx]] = 1.0
         else:
             y = self.labels_int[idx]
@@ -141,9 +142,9 @@ class DeviceBatcher:
         self.images = torch.from_numpy(ds.images_u8).to(self.device)
         self.labels = torch.from_numpy(ds.labels_int.astype(np.int32)).to(self.device)
         self.idx = torch.empty(batch_size, dtype=torch.int32, device=self.device)
-        self.x = torch.empty(batch_size, 784, dtype=torch.float32, device=self.device)
+        self.x = torch.empty(batch_size, ds.images_u8.shape[1], dtype=torch.float32, device=self.device)
         self.y_int = torch.empty(batch_size, dtype=torch.int32, device=self.device)
-        self.y = torch.empty(batch_size, 10, dtype=torch.float32, device=self.device)
+        self.y = torch.empty(batch_size, ds.num_classes, dtype=torch.float32, device=self.device)
         self.one_hot = one_hot
         self._host_idx = torch.empty(batch_size, dtype=torch.int32).pin_memory() \
             if self.device.type == "cuda" else torch.empty(batch_size, dtype=torch.int32)

@@ -1,0 +1,484 @@
+"""ResNet family: CIFAR-10 ResNet-20 and ImageNet-shape ResNet-50 (BASELINE.json configs 3 and 5).
+
+Neither model exists in the reference; they are the
+north-star workloads of the conv2d MFMA path.  Both are ResNet v1 in the
+TensorFlow layer conventions so checkpoints use ``tf.layers`` names
+(``conv2d_3/kernel``, ``batch_normalization_3/{gamma,beta,moving_mean,
+moving_variance}``, ``dense/{kernel,bias}``, ``global_step``) and TF layouts.
+
+* ResNet-20 (He et al. 2016, CIFAR): 3x3 conv 16 -> 3 stages x 3 basic blocks
+  (16/32/64 channels, stride 2 at stages 2 and 3) -> global average pool -> fc 10.
+  Shortcuts are the paper's parameter-free "option A" (identity, stride-2
+  subsample, zero-padded channels): 0.27 M parameters.
+* ResNet-50 (v1.5: stride on the 3x3 conv): 7x7/2 conv 64 + 3x3/2 max pool ->
+  bottleneck stages [3, 4, 6, 3] (64/128/256/512 x 4) with projection
+  shortcuts -> global average pool -> fc 1000: 25.6 M parameters.
+
+Execution: NHWC bf16 activations in pre-allocated buffers, fp32 master weights /
+grads / Momentum slots in one flat buffer, BatchNorm in training mode (batch
+statistics; TF defaults momentum 0.99, epsilon 1e-3), every op a HIP kernel:
+
+  conv fwd     whole-image LDS conv (persistent, weights in LDS) when the image
+               and weights fit (all of ResNet-20), else the implicit-GEMM conv
+  conv dgrad   stride 1: the same kernel over dY with flipped taps; else implicit GEMM
+  conv wgrad   persistent register-accumulating kernel, else implicit GEMM
+  BN           channel statistics (one atomic per channel and workgroup),
+               apply + ReLU + residual add fused, backward stats + apply fused
+               with the ReLU mask and the shortcut-gradient copy
+  head         global average pool, fp32 fc + softmax-xent (exact fp32 MFMA GEMMs)
+
+BatchNorm moving statistics live in the flat buffer (so checkpoints and the
+all-reduce broadcast carry them) but outside every optimizer var_list; in
+--mode=ps they stay worker-local.  No weight decay (not part of the reference
+contract).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..optim import OptimizerConfig, VarSpec
+from .base import ModelDef, StepProgram
+
+BN_EPS, BN_MOMENTUM = 1e-3, 0.99
+# activation / activation-gradient storage dtype: bf16 on the GPU kernels; the CPU reference
+# path also runs with fp32 storage (exactness tests of the program logic)
+ACT_DTYPE = torch.bfloat16
+
+
+def _conv_to_tf(t):    # ours [Cout][KH][KW][Cin] -> TF [KH][KW][Cin][Cout]
+    return t.permute(1, 2, 3, 0).contiguous()
+
+
+def _conv_from_tf(t):
+    return t.permute(3, 0, 1, 2).contiguous()
+
+
+def _fc_to_tf(t):      # ours [out][in] -> TF [in][out]
+    return t.t().contiguous()
+
+
+def _he_normal(fan_in):
+    std = math.sqrt(2.0 / fan_in)
+    return lambda shape, g: torch.randn(*shape, generator=g) * std
+
+
+def _const(v):
+    return lambda shape, g: torch.full(shape, float(v))
+
+
+def _glorot(fan_in, fan_out):
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return lambda shape, g: (torch.rand(*shape, generator=g) * 2 - 1) * lim
+
+
+class Registry:
+    """tf.layers-style auto names (conv2d, conv2d_1, ...) and the VarSpecs in creation order."""
+
+    def __init__(self):
+        self.specs = []
+        self._count = {}
+
+    def scope(self, base):
+        i = self._count.get(base, 0)
+        self._count[base] = i + 1
+        return base if i == 0 else "%s_%d" % (base, i)
+
+    def add(self, spec):
+        self.specs.append(spec)
+        return spec.name
+
+
+# ------------------------------------------------------------------ layers
+class Conv:
+    """NHWC conv without bias (ResNet convs are followed by BatchNorm)."""
+
+    def __init__(self, reg, cin, cout, k, stride, H, W):
+        self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.pad = (k - 1) // 2
+        self.H, self.W = H, W
+        self.OH = (H + 2 * self.pad - k) // stride + 1
+        self.OW = (W + 2 * self.pad - k) // stride + 1
+        self.name = reg.add(VarSpec(reg.scope("conv2d") + "/kernel", (cout, k, k, cin), _he_normal(k * k * cin),
+                                    bf16=True, transpose=(cout, k * k, cin), tf_shape=(k, k, cin, cout),
+                                    to_tf=_conv_to_tf, from_tf=_conv_from_tf))
+
+    def bind(self, P, B, dev):
+        self.B = B
+        self.w, self.wt, self.gw = P.w16[self.name], P.wt16[self.name], P.gview(self.name)
+        self.y = torch.empty(B, self.OH, self.OW, self.cout, device=dev, dtype=ACT_DTYPE)
+        self.g = dict(B=B, H=self.H, W=self.W, C=self.cin, Cout=self.cout, OH=self.OH, OW=self.OW, KH=self.k,
+                      KW=self.k, stride=self.stride, pad=self.pad)
+        self.ic = dict(B=B, SH=self.H, SW=self.W, CS=self.cin, OH=self.OH, OW=self.OW, N=self.cout, KH=self.k,
+                       KW=self.k, stride=self.stride, pad=self.pad)
+        LH = (self.OH - 1) * self.stride + self.k
+        LW = (self.OW - 1) * self.stride + self.k
+        self.img_fwd = self.cin % 8 == 0 and self.cout <= 64 and LH * LW * self.cin * 2 <= 150 * 1024
+        self.img_dgrad = (self.stride == 1 and self.cout % 8 == 0 and self.cin <= 64
+                          and (self.H + self.k - 1) * (self.W + self.k - 1) * self.cout * 2 <= 150 * 1024)
+        self.img_wgrad = self.cin % 8 == 0 and self.cout <= 64 and self.OW <= 32 and self.cout % 8 == 0
+
+    def fwd(self, x):
+        if self.img_fwd:
+            ops.imgconv(self.w, self.y, src=x, **self.ic)
+        else:
+            ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE)
+        return self.y
+
+    def wgrad(self, dy, x):
+        if self.img_wgrad:
+            ops.imgwgrad(x, self.gw, None, dy=dy, **self.ic)
+        else:
+            ops.conv_wgrad(dy, x, self.gw, None, self.g)
+
+    def dgrad(self, dy, dx):
+        if self.img_dgrad:
+            ops.imgconv(self.wt, dx, src=dy, flip_taps=True, B=self.B, SH=self.OH, SW=self.OW, CS=self.cout,
+                        OH=self.H, OW=self.W, N=self.cin, KH=self.k, KW=self.k, stride=1,
+                        pad=self.k - 1 - self.pad)
+        else:
+            ops.conv_dgrad(dy, self.wt, dx, self.g)
+
+
+class BN:
+    def __init__(self, reg, C):
+        self.C = C
+        s = reg.scope("batch_normalization")
+        self.gamma = reg.add(VarSpec(s + "/gamma", (C,), _const(1.0)))
+        self.beta = reg.add(VarSpec(s + "/beta", (C,), _const(0.0)))
+        self.mm = reg.add(VarSpec(s + "/moving_mean", (C,), _const(0.0)))
+        self.mv = reg.add(VarSpec(s + "/moving_variance", (C,), _const(1.0)))
+
+    def bind(self, P, shape, dev, arena):
+        self.P = P
+        self.y = torch.empty(*shape, device=dev, dtype=ACT_DTYPE)
+        self.stats, self.dstats, self.mean, self.invstd = arena.take(2 * self.C), arena.take(2 * self.C), \
+            arena.take(self.C), arena.take(self.C)
+
+    def fwd(self, x, act=ops.ACT_RELU, res=None, rstride=1):
+        P = self.P
+        ops.bn_stats(x, self.stats)
+        ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
+                     invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
+                     momentum=BN_MOMENTUM, act=act, res=res, rstride=rstride)
+        return self.y
+
+    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None):
+        P = self.P
+        y = self.y if act != ops.ACT_NONE else None
+        ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act)
+        ops.bn_bwd_apply(dy, y, x, self.mean, self.invstd, P.view(self.gamma), self.dstats, dx, act=act, dres=dres,
+                         dgamma=P.gview(self.gamma), dbeta=P.gview(self.beta))
+
+
+class Arena:
+    """One zero-per-step fp32 buffer holding every BN layer's statistics accumulators."""
+
+    def __init__(self, n, dev):
+        self.buf = torch.zeros(n, device=dev)
+        self.off = 0
+
+    def take(self, n):
+        t = self.buf[self.off:self.off + n]
+        self.off += (n + 15) // 16 * 16
+        return t
+
+
+class BasicBlock:
+    """ResNet v1 basic block with the option-A shortcut (identity / subsample + zero channels)."""
+
+    def __init__(self, reg, cin, cout, stride, H, W):
+        self.cin, self.cout, self.stride = cin, cout, stride
+        self.conv1 = Conv(reg, cin, cout, 3, stride, H, W)
+        self.bn1 = BN(reg, cout)
+        self.conv2 = Conv(reg, cout, cout, 3, 1, self.conv1.OH, self.conv1.OW)
+        self.bn2 = BN(reg, cout)
+        self.OH, self.OW = self.conv2.OH, self.conv2.OW
+        self.stats_len = 6 * cout * 2 + 64
+
+    def bind(self, P, B, dev, arena):
+        for c in (self.conv1, self.conv2):
+            c.bind(P, B, dev)
+        shp = (B, self.OH, self.OW, self.cout)
+        self.bn1.bind(P, shp, dev, arena)
+        self.bn2.bind(P, shp, dev, arena)
+        bf = dict(device=dev, dtype=ACT_DTYPE)
+        self.dc2, self.dh1, self.dc1, self.dres = (torch.empty(*shp, **bf) for _ in range(4))
+
+    def fwd(self, x):
+        self.x = x
+        c1 = self.conv1.fwd(x)
+        h1 = self.bn1.fwd(c1)
+        c2 = self.conv2.fwd(h1)
+        return self.bn2.fwd(c2, res=x, rstride=self.stride)
+
+    def bwd(self, dout, dx):
+        self.bn2.bwd(dout, self.conv2.y, self.dc2, dres=self.dres)
+        self.conv2.wgrad(self.dc2, self.bn1.y)
+        self.conv2.dgrad(self.dc2, self.dh1)
+        self.bn1.bwd(self.dh1, self.conv1.y, self.dc1)
+        self.conv1.wgrad(self.dc1, self.x)
+        if dx is not None:
+            self.conv1.dgrad(self.dc1, dx)
+            ops.shortcut_grad_add(self.dres, dx, self.stride)
+
+
+class Bottleneck:
+    """ResNet v1.5 bottleneck: 1x1 -> 3x3 (stride) -> 1x1 (x4), projection shortcut when the shape changes."""
+
+    def __init__(self, reg, cin, width, stride, H, W):
+        cout = 4 * width
+        self.cin, self.cout, self.stride = cin, cout, stride
+        self.proj = stride != 1 or cin != cout
+        if self.proj:  # tf.layers creation order: shortcut conv first (as in the TF official model)
+            self.convs = Conv(reg, cin, cout, 1, stride, H, W)
+            self.bns = BN(reg, cout)
+        self.conv1 = Conv(reg, cin, width, 1, 1, H, W)
+        self.bn1 = BN(reg, width)
+        self.conv2 = Conv(reg, width, width, 3, stride, H, W)
+        self.bn2 = BN(reg, width)
+        self.conv3 = Conv(reg, width, cout, 1, 1, self.conv2.OH, self.conv2.OW)
+        self.bn3 = BN(reg, cout)
+        self.OH, self.OW = self.conv3.OH, self.conv3.OW
+
+    def bind(self, P, B, dev, arena):
+        bf = dict(device=dev, dtype=ACT_DTYPE)
+        w = self.conv1.cout
+        convs = [self.conv1, self.conv2, self.conv3] + ([self.convs] if self.proj else [])
+        for c in convs:
+            c.bind(P, B, dev)
+        self.bn1.bind(P, (B, self.conv1.OH, self.conv1.OW, w), dev, arena)
+        self.bn2.bind(P, (B, self.OH, self.OW, w), dev, arena)
+        self.bn3.bind(P, (B, self.OH, self.OW, self.cout), dev, arena)
+        if self.proj:
+            self.bns.bind(P, (B, self.OH, self.OW, self.cout), dev, arena)
+            self.dsc = torch.empty(B, self.OH, self.OW, self.cout, **bf)
+            self.dxs = torch.empty(B, self.conv1.H, self.conv1.W, self.cin, **bf)
+        self.dc3 = torch.empty(B, self.OH, self.OW, self.cout, **bf)
+        self.dres = torch.empty(B, self.OH, self.OW, self.cout, **bf)
+        self.dh2 = torch.empty(B, self.OH, self.OW, w, **bf)
+        self.dc2 = torch.empty(B, self.OH, self.OW, w, **bf)
+        self.dh1 = torch.empty(B, self.conv1.OH, self.conv1.OW, w, **bf)
+        self.dc1 = torch.empty(B, self.conv1.OH, self.conv1.OW, w, **bf)
+
+    def fwd(self, x):
+        self.x = x
+        res = x
+        if self.proj:
+            res = self.bns.fwd(self.convs.fwd(x), act=ops.ACT_NONE)
+        h1 = self.bn1.fwd(self.conv1.fwd(x))
+        h2 = self.bn2.fwd(self.conv2.fwd(h1))
+        return self.bn3.fwd(self.conv3.fwd(h2), res=res, rstride=1)
+
+    def bwd(self, dout, dx):
+        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=self.dres)
+        self.conv3.wgrad(self.dc3, self.bn2.y)
+        self.conv3.dgrad(self.dc3, self.dh2)
+        self.bn2.bwd(self.dh2, self.conv2.y, self.dc2)
+        self.conv2.wgrad(self.dc2, self.bn1.y)
+        self.conv2.dgrad(self.dc2, self.dh1)
+        self.bn1.bwd(self.dh1, self.conv1.y, self.dc1)
+        self.conv1.wgrad(self.dc1, self.x)
+        if self.proj:
+            self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
+            self.convs.wgrad(self.dsc, self.x)
+        if dx is not None:
+            self.conv1.dgrad(self.dc1, dx)
+            if self.proj:
+                self.convs.dgrad(self.dsc, self.dxs)
+                ops.shortcut_grad_add(self.dxs, dx, 1)
+            else:
+                ops.shortcut_grad_add(self.dres, dx, 1)
+
+
+class Dense:
+    """fp32 classifier layer (exact-fp32 MFMA GEMMs; tiny next to the convs)."""
+
+    def __init__(self, reg, cin, cout):
+        self.cin, self.cout = cin, cout
+        s = reg.scope("dense")
+        self.kernel = reg.add(VarSpec(s + "/kernel", (cout, cin), _glorot(cin, cout), tf_shape=(cin, cout),
+                                      to_tf=_fc_to_tf, from_tf=_fc_to_tf))
+        self.bias = reg.add(VarSpec(s + "/bias", (cout,), _const(0.0)))
+
+
+# ------------------------------------------------------------------- model
+ARCHS = {
+    # name: (image, channels, classes, builder)
+    "resnet20": (32, 3, 10),
+    "resnet50": (224, 3, 1000),
+}
+
+
+def build(arch, reg):
+    """Create the layers (and their VarSpecs, in TF creation order) of an architecture."""
+    img, ch, ncls = ARCHS[arch]
+    L = {}
+    if arch == "resnet20":
+        L["stem"] = Conv(reg, ch, 16, 3, 1, img, img)
+        L["stem_bn"] = BN(reg, 16)
+        blocks, H, cin = [], img, 16
+        for stage, cout in enumerate((16, 32, 64)):
+            for i in range(3):
+                stride = 2 if (stage > 0 and i == 0) else 1
+                b = BasicBlock(reg, cin, cout, stride, H, H)
+                blocks.append(b)
+                H, cin = b.OH, cout
+        L["blocks"], L["feat"], L["HW"] = blocks, cin, H
+    else:
+        L["stem"] = Conv(reg, ch, 64, 7, 2, img, img)
+        L["stem_bn"] = BN(reg, 64)
+        H = L["stem"].OH
+        L["pool_hw"] = ((H + 2 - 3) // 2 + 1)
+        H, cin = L["pool_hw"], 64
+        blocks = []
+        for stage, (width, n) in enumerate(((64, 3), (128, 4), (256, 6), (512, 3))):
+            for i in range(n):
+                stride = 2 if (stage > 0 and i == 0) else 1
+                b = Bottleneck(reg, cin, width, stride, H, H)
+                blocks.append(b)
+                H, cin = b.OH, b.cout
+        L["blocks"], L["feat"], L["HW"] = blocks, cin, H
+    L["dense"] = Dense(reg, L["feat"], ncls)
+    return L
+
+
+class ResNetModel(ModelDef):
+    default_steps = 1000
+
+    def __init__(self, lr: float = 0.1, arch: str = "resnet20"):
+        self.name = arch
+        self.arch = arch
+        self.default_batch = 128 if arch == "resnet20" else 64
+        reg = Registry()
+        self.layers = build(arch, reg)
+        creation = [s.name for s in reg.specs]
+        self.var_order = creation + ["global_step"]
+        self.gs_name = "global_step"
+        # flat (gradient bucket) order = backward completion order: head first, stem last
+        self.specs = list(reversed(reg.specs))
+        trainable = [n for n in creation if not n.endswith(("/moving_mean", "/moving_variance"))]
+        self.opt_groups = [(OptimizerConfig(kind="momentum", lr=lr, momentum=0.9), trainable,
+                            ("beta1_power", "beta2_power"))]
+        self.image, self.channels, self.num_classes = ARCHS[arch]
+
+    def num_params(self, trainable_only=True):
+        names = set(self.opt_groups[0][1]) if trainable_only else None
+        return sum(s.numel for s in self.specs if names is None or s.name in names)
+
+    def flops_per_image(self) -> float:
+        """fwd+bwd conv/fc FLOPs per image (3x the forward MACs*2; the stem has no dgrad)."""
+        L = self.layers
+        convs = [L["stem"]]
+        for b in L["blocks"]:
+            convs += [c for c in (getattr(b, "convs", None), b.conv1, b.conv2, getattr(b, "conv3", None)) if c]
+        f = 0.0
+        for i, c in enumerate(convs):
+            fwd = 2.0 * c.OH * c.OW * c.cout * c.k * c.k * c.cin
+            f += fwd * (2 if i == 0 else 3)
+        d = L["dense"]
+        return f + 3 * 2.0 * d.cin * d.cout
+
+    def program(self, device, batch_size=None, seed: int = 0):
+        return ResNetProgram(self, device, batch_size or self.default_batch, seed)
+
+
+class ResNetProgram(StepProgram):
+    def __init__(self, model, device, batch_size: int, seed: int = 0):
+        super().__init__(model, device, batch_size, seed)
+        if self.device.type == "cuda":
+            ops.require()
+        reg = Registry()
+        self.L = L = build(model.arch, reg)  # same names as the ModelDef (deterministic)
+        B, dev, P = batch_size, self.device, self.P
+        img, ch = model.image, model.channels
+        n_bn = sum(1 for s in reg.specs if s.name.endswith("/gamma"))
+        max_c = max(s.shape[0] for s in reg.specs if s.name.endswith("/gamma"))
+        self.arena = Arena(n_bn * (6 * max_c + 64), dev)
+        bf = dict(device=dev, dtype=ACT_DTYPE)
+        self.x = torch.empty(B, img, img, ch, **bf)
+        self.y = torch.empty(B, model.num_classes, device=dev)
+        L["stem"].bind(P, B, dev)
+        st = L["stem"]
+        L["stem_bn"].bind(P, (B, st.OH, st.OW, st.cout), dev, self.arena)
+        self.d_stem = torch.empty(B, st.OH, st.OW, st.cout, **bf)
+        self.dc_stem = torch.empty(B, st.OH, st.OW, st.cout, **bf)
+        if "pool_hw" in L:
+            ph = L["pool_hw"]
+            self.pool = torch.empty(B, ph, ph, st.cout, **bf)
+            self.pool_am = torch.empty(B, ph, ph, st.cout, device=dev, dtype=torch.uint8)
+            self.d_pool = torch.empty(B, ph, ph, st.cout, **bf)
+        for b in L["blocks"]:
+            b.bind(P, B, dev, self.arena)
+        # block input-gradient buffers: d_in[i] is the gradient w.r.t. block i's input
+        self.d_in = [torch.empty(B, b.conv1.H, b.conv1.W, b.cin, **bf) for b in L["blocks"]]
+        self.d_last = torch.empty(B, L["HW"], L["HW"], L["feat"], **bf)
+        d = L["dense"]
+        self.feat16 = torch.empty(B, d.cin, **bf)
+        self.feat = torch.empty(B, d.cin, device=dev)
+        self.logits = torch.empty(B, d.cout, device=dev)
+        self.dlogits = torch.empty(B, d.cout, device=dev)
+        self.dfeat = torch.empty(B, d.cin, device=dev)
+        self.dfeat16 = torch.empty(B, d.cin, **bf)
+        self.loss = torch.zeros(1, device=dev)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def load_batch(self, batch):
+        x, y = batch
+        self.x.copy_(x.reshape(self.x.shape).to(self.x.dtype))
+        yy = y.reshape(self.batch_size, -1)
+        if yy.shape[1] == 1:
+            self.y.zero_()
+            self.y.scatter_(1, yy.long(), 1.0)
+        else:
+            self.y.copy_(yy)
+
+    def forward(self):
+        L = self.L
+        h = L["stem_bn"].fwd(L["stem"].fwd(self.x))
+        if "pool_hw" in L:
+            ops.maxpool3_fwd(h, self.pool, self.pool_am)
+            h = self.pool
+        for b in L["blocks"]:
+            h = b.fwd(h)
+        ops.gap_fwd(h, self.feat16)
+        ops.cast_(self.feat16, self.feat)
+        d, P, B = L["dense"], self.P, self.batch_size
+        ops.gemm(self.feat, P.view(d.kernel), self.logits, M=B, N=d.cout, K=d.cin, bias=P.view(d.bias))
+        ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
+                         correct=self.correct)
+
+    def backward(self):
+        L, P, B = self.L, self.P, self.batch_size
+        d = L["dense"]
+        ops.gemm(self.dlogits, self.feat, P.gview(d.kernel), M=d.cout, N=d.cin, K=B, amode=ops.RMAJ, lda=d.cout,
+                 bmode=ops.RMAJ, ldb=d.cin)
+        ops.colsum(self.dlogits, B, d.cout, d.cout, P.gview(d.bias))
+        ops.gemm(self.dlogits, P.view(d.kernel), self.dfeat, M=B, N=d.cin, K=d.cout, bmode=ops.RMAJ, ldb=d.cin)
+        ops.cast_(self.dfeat, self.dfeat16)
+        ops.gap_bwd(self.dfeat16, self.d_last)
+        dout = self.d_last
+        blocks = L["blocks"]
+        for i in range(len(blocks) - 1, -1, -1):
+            blocks[i].bwd(dout, self.d_in[i])
+            dout = self.d_in[i]
+        st = L["stem"]
+        if "pool_hw" in L:
+            ops.maxpool3_bwd(dout, self.pool_am, self.d_stem)
+            dout = self.d_stem
+        L["stem_bn"].bwd(dout, st.y, self.dc_stem)
+        st.wgrad(self.dc_stem, self.x)
+
+    def compute_grads(self):
+        self.P.grad.zero_()
+        self.arena.buf.zero_()
+        self.loss.zero_()
+        self.correct.zero_()
+        self.forward()
+        self.backward()
+        return {"loss": self.loss / self.batch_size, "correct": self.correct}
+
+    def evaluate(self, images, labels) -> float:
+        raise NotImplementedError("training-mode BN only; no evaluation step in this example")

@@ -22,7 +22,8 @@ __all__ = [
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
-    "TILE_DIMS", "GEMM_KTILE",
+    "TILE_DIMS", "GEMM_KTILE", "bn_stats", "bn_apply", "bn_bwd_stats", "bn_bwd_apply", "shortcut_grad_add",
+    "gap_fwd", "gap_bwd", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -541,3 +542,161 @@ def lstm_cell_bwd(act, c_prev, c, dh, dh2, dc_next, dgates, dc_prev):
     dgates.copy_(torch.cat([dc * tj * si * (1 - si), dc * si * (1 - tj * tj), dc * cp * sf * (1 - sf),
                             d * tc * so * (1 - so)], dim=1))
     dc_prev.copy_(dc * sf)
+
+
+# ------------------------------------------------------------- batch norm
+# NHWC bf16 activations viewed as [R][C]; stats are fp32 [2][C] accumulators the
+# caller zeroes: forward (sum, sum of squares) of x - x[row 0] (per-channel shift),
+# backward (sum g, sum g*xhat).
+def _rows(t):
+    return t.reshape(-1, t.shape[-1]).float()
+
+
+def bn_stats(x, stats):
+    if x.is_cuda:
+        require().bn_stats(x, stats)
+        return
+    r = _rows(x)
+    C = r.shape[1]
+    d = r - r[0]  # shifted by row 0 (as the kernel) against E[x^2]-E[x]^2 cancellation
+    stats[:C] += d.sum(0)
+    stats[C:] += (d * d).sum(0)
+
+
+def _bn_params(stats, R, eps, shift):
+    C = stats.numel() // 2
+    d = stats[:C] / R
+    var = (stats[C:] / R - d * d).clamp_min(0)
+    return shift + d, torch.rsqrt(var + eps), var
+
+
+def _shortcut_view(res, OH, OW, C, rstride):
+    """option-A shortcut read: res[:, ::s, ::s, :] zero-padded to C channels (NHWC fp32)."""
+    r = res.float()[:, ::rstride, ::rstride, :][:, :OH, :OW, :]
+    if r.shape[-1] < C:
+        r = torch.nn.functional.pad(r, (0, C - r.shape[-1]))
+    return r
+
+
+def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=None, moving_var=None, eps=1e-3,
+             momentum=0.99, act=ACT_RELU, res=None, rstride=1):
+    """out = act(gamma * (x - mean) * invstd + beta [+ shortcut(res)]) with batch statistics from
+    ``stats``; stores mean/invstd and updates the moving averages (TF momentum convention)."""
+    OH, OW = (x.shape[1], x.shape[2]) if x.dim() == 4 else (1, 1)
+    if x.is_cuda:
+        require().bn_apply(x, stats, gamma, beta, mean, invstd, moving_mean, moving_var, eps, momentum, act, res,
+                           rstride, OH, OW, out)
+        return out
+    r = _rows(x)
+    R, C = r.shape
+    m, inv, var = _bn_params(stats, R, eps, r[0])
+    if mean is not None:
+        mean.copy_(m)
+    if invstd is not None:
+        invstd.copy_(inv)
+    if moving_mean is not None:
+        unb = var * R / max(R - 1, 1)
+        moving_mean.mul_(momentum).add_(m * (1 - momentum))
+        moving_var.mul_(momentum).add_(unb * (1 - momentum))
+    y = (r - m) * inv * gamma.float() + beta.float()
+    if res is not None:
+        y = y + _shortcut_view(res, OH, OW, C, rstride).reshape(R, C)
+    out.copy_(_act_ref(y, act).reshape(out.shape).to(out.dtype))
+    return out
+
+
+def _masked_grad(dy, y, act):
+    g = _rows(dy)
+    if act != ACT_NONE:
+        g = g * _act_grad_from_out_ref(_rows(y), act)
+    return g
+
+
+def bn_bwd_stats(dy, y, x, mean, invstd, stats, act=ACT_RELU):
+    if x.is_cuda:
+        require().bn_bwd_stats(dy, y, x, mean, invstd, stats, act)
+        return
+    g = _masked_grad(dy, y, act)
+    xh = (_rows(x) - mean) * invstd
+    C = g.shape[1]
+    stats[:C] += g.sum(0)
+    stats[C:] += (g * xh).sum(0)
+
+
+def bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, dx, *, act=ACT_RELU, dres=None, dgamma=None, dbeta=None):
+    """dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*act'(y); dgamma/dbeta += sums;
+    dres = g (gradient of an added shortcut)."""
+    if x.is_cuda:
+        require().bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, act, dx, dres, dgamma, dbeta)
+        return dx
+    g = _masked_grad(dy, y, act)
+    R, C = g.shape
+    xh = (_rows(x) - mean) * invstd
+    d = gamma.float() * invstd * (g - stats[:C] / R - xh * stats[C:] / R)
+    dx.copy_(d.reshape(dx.shape).to(dx.dtype))
+    if dres is not None:
+        dres.copy_(g.reshape(dres.shape).to(dres.dtype))
+    if dgamma is not None:
+        dgamma += stats[C:]
+    if dbeta is not None:
+        dbeta += stats[:C]
+    return dx
+
+
+def shortcut_grad_add(g, dx, stride=1):
+    """dx[:, ::s, ::s, :XC] += g[..., :XC] (gradient of the option-A identity shortcut)."""
+    if dx.is_cuda:
+        require().shortcut_grad_add(g, dx, stride)
+        return dx
+    XC = dx.shape[-1]
+    OH, OW = g.shape[1], g.shape[2]
+    v = dx[:, ::stride, ::stride, :][:, :OH, :OW, :]
+    v.copy_((v.float() + g[..., :XC].float()).to(dx.dtype))
+    return dx
+
+
+def gap_fwd(x, y):
+    if x.is_cuda:
+        require().gap_fwd(x, y)
+        return y
+    y.copy_(x.float().mean(dim=(1, 2)).reshape(y.shape).to(y.dtype))
+    return y
+
+
+def gap_bwd(dy, dx):
+    if dx.is_cuda:
+        require().gap_bwd(dy, dx)
+        return dx
+    B, H, W, C = dx.shape
+    dx.copy_((dy.float().reshape(B, 1, 1, C) / (H * W)).expand(B, H, W, C).to(dx.dtype))
+    return dx
+
+
+def maxpool3_fwd(x, y, am):
+    """3x3 / stride 2 / pad 1 max pool (NHWC) with the window argmax (0..8, first max wins)."""
+    if x.is_cuda:
+        require().maxpool3_fwd(x, y, am)
+        return y
+    B, H, W, C = x.shape
+    xp = torch.nn.functional.pad(x.float().permute(0, 3, 1, 2), (1, 1, 1, 1), value=-3.0e38)
+    cols = torch.nn.functional.unfold(xp, 3, stride=2)  # [B, C*9, L]
+    OH, OW = y.shape[1], y.shape[2]
+    cols = cols.view(B, C, 9, OH * OW)
+    v, i = cols.max(dim=2)
+    y.copy_(v.view(B, C, OH, OW).permute(0, 2, 3, 1).to(y.dtype))
+    am.copy_(i.view(B, C, OH, OW).permute(0, 2, 3, 1).to(am.dtype))
+    return y
+
+
+def maxpool3_bwd(dy, am, dx):
+    if dx.is_cuda:
+        require().maxpool3_bwd(dy, am, dx)
+        return dx
+    B, H, W, C = dx.shape
+    OH, OW = dy.shape[1], dy.shape[2]
+    cols = torch.zeros(B, C, 9, OH * OW)
+    g = dy.float().permute(0, 3, 1, 2).reshape(B, C, 1, OH * OW)
+    cols.scatter_(2, am.long().permute(0, 3, 1, 2).reshape(B, C, 1, OH * OW), g)
+    d = torch.nn.functional.fold(cols.view(B, C * 9, OH * OW), (H + 2, W + 2), 3, stride=2)[:, :, 1:H + 1, 1:W + 1]
+    dx.copy_(d.permute(0, 2, 3, 1).to(dx.dtype))
+    return dx

@@ -25,11 +25,13 @@ import torch
 import torch.distributed as dist
 
 from . import ckpt
-from .data.mnist import DeviceBatcher, read_data_sets
+from .data import cifar, imagenet_synth
+from .data.mnist import DeviceBatcher, read_data_sets as read_mnist
 from .models.autoencoder import AutoencoderModel
 from .models.gan import LR as GAN_LR, GanModel
 from .models.lstm import LR as LSTM_LR, LstmModel
 from .models.mnist_cnn import MnistCnnModel
+from .models.resnet import ResNetModel
 from .models.softmax_reg import SoftmaxRegressionModel
 from .models.autoencoder import LR as ENC_LR
 from .optim import Optimizer
@@ -47,7 +49,20 @@ MODELS = {
     "lstm": (LstmModel, LSTM_LR),
     "softmax": (SoftmaxRegressionModel, 0.01),
     "cnn": (MnistCnnModel, 0.001),
+    "resnet20": (lambda lr=0.1: ResNetModel(lr, "resnet20"), 0.1),
+    "resnet50": (lambda lr=0.1: ResNetModel(lr, "resnet50"), 0.1),
 }
+
+
+def read_data_sets(model, data_dir, one_hot=True, seed=0, log=print):
+    """The model's dataset: MNIST (reference models + CNN), CIFAR-10 (ResNet-20) or a
+    synthetic ImageNet-shape set (ResNet-50)."""
+    name = getattr(model, "name", "")
+    if name == "resnet20":
+        return cifar.read_data_sets(data_dir, one_hot=one_hot, seed=seed, log=log)
+    if name == "resnet50":
+        return imagenet_synth.read_data_sets(one_hot=one_hot, seed=seed, log=log)
+    return read_mnist(data_dir, one_hot=one_hot, seed=seed, log=log)
 
 
 def _print(*args):
@@ -214,7 +229,7 @@ def run_worker_ps(flags, model, server, device, log):
         gs_fn=lambda: client.status()[1],
         save_model_secs=flags.save_model_secs, save_summaries_secs=flags.save_summaries_secs,
         max_to_keep=flags.max_to_keep, log=log)
-    data = read_data_sets("" if flags.synthetic else flags.data_dir, one_hot=True,
+    data = read_data_sets(model, "" if flags.synthetic else flags.data_dir, one_hot=True,
                           seed=flags.seed * 1000 + server.task_index + 1, log=log)
     feeder = Feeder(data, prog, device)
     metrics_log = MetricsLog(flags.metrics_jsonl)
@@ -282,7 +297,7 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         prog.P.refresh_copies()
         ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), group=group,
                              comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
-    data = read_data_sets("" if flags.synthetic else flags.data_dir, one_hot=True, seed=flags.seed * 1000 + rank + 1,
+    data = read_data_sets(model, "" if flags.synthetic else flags.data_dir, one_hot=True, seed=flags.seed * 1000 + rank + 1,
                           log=log if is_chief else (lambda *_: None))
     feeder = Feeder(data, prog, device)
     metrics_log = MetricsLog(flags.metrics_jsonl)

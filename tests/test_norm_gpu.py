@@ -1,0 +1,87 @@
+"""BatchNorm / shortcut / pooling HIP kernels vs the fp32 reference path of the same ops."""
+import pytest
+import torch
+
+import dtfe  # noqa: F401
+from dtfe import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float().cpu() - b.float().cpu()).abs().max() / (b.float().cpu().abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("shape,res_shape,rstride", [
+    ((8, 16, 16, 32), None, 1),
+    ((8, 16, 16, 32), (8, 16, 16, 32), 1),        # identity shortcut
+    ((8, 8, 8, 64), (8, 16, 16, 32), 2),          # option A: subsample + zero channels
+    ((4, 7, 7, 2048), None, 1),                   # ResNet-50 widest layer
+])
+def test_bn_forward_backward(shape, res_shape, rstride):
+    torch.manual_seed(0)
+    C = shape[-1]
+    x = (torch.randn(*shape) * 2 + 3).to(torch.bfloat16)  # |mean| >> std: the shifted statistics matter
+    res = torch.randn(*res_shape).to(torch.bfloat16) if res_shape else None
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    dy = torch.randn(*shape).to(torch.bfloat16)
+    out = {}
+    for dev in ("cpu", DEV):
+        st = torch.zeros(2 * C, device=dev)
+        mean, inv = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        y = torch.empty(*shape, device=dev, dtype=torch.bfloat16)
+        xd = x.to(dev)
+        ops.bn_stats(xd, st)
+        ops.bn_apply(xd, st, gamma.to(dev), beta.to(dev), y, mean=mean, invstd=inv, moving_mean=mm, moving_var=mv,
+                     act=ops.ACT_RELU, res=res.to(dev) if res is not None else None, rstride=rstride)
+        st2 = torch.zeros(2 * C, device=dev)
+        dx = torch.empty(*shape, device=dev, dtype=torch.bfloat16)
+        dres = torch.empty(*shape, device=dev, dtype=torch.bfloat16)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        ops.bn_bwd_stats(dy.to(dev), y, xd, mean, inv, st2, ops.ACT_RELU)
+        ops.bn_bwd_apply(dy.to(dev), y, xd, mean, inv, gamma.to(dev), st2, dx, act=ops.ACT_RELU, dres=dres,
+                         dgamma=dg, dbeta=db)
+        out[dev] = dict(y=y, mean=mean, inv=inv, mm=mm, mv=mv, dx=dx, dres=dres, dg=dg, db=db)
+    c, g = out["cpu"], out[DEV]
+    for k in ("mean", "inv", "mm", "mv", "dg", "db"):
+        assert _rel(g[k], c[k]) < 2e-3, k
+    for k in ("y", "dx", "dres"):
+        assert _rel(g[k], c[k]) < 2e-2, k
+
+
+def test_shortcut_grad_add_and_gap():
+    torch.manual_seed(1)
+    g = torch.randn(4, 8, 8, 64).to(torch.bfloat16)
+    dx0 = torch.randn(4, 16, 16, 32).to(torch.bfloat16)
+    a, b = dx0.clone(), dx0.clone().to(DEV)
+    ops.shortcut_grad_add(g, a, 2)
+    ops.shortcut_grad_add(g.to(DEV), b, 2)
+    assert _rel(b, a) < 1e-2
+    x = torch.randn(4, 8, 8, 64).to(torch.bfloat16)
+    y1, y2 = torch.empty(4, 64, dtype=torch.bfloat16), torch.empty(4, 64, dtype=torch.bfloat16, device=DEV)
+    ops.gap_fwd(x, y1)
+    ops.gap_fwd(x.to(DEV), y2)
+    assert _rel(y2, y1) < 1e-2
+    d1, d2 = torch.empty(4, 8, 8, 64, dtype=torch.bfloat16), torch.empty(4, 8, 8, 64, dtype=torch.bfloat16, device=DEV)
+    ops.gap_bwd(y1, d1)
+    ops.gap_bwd(y1.to(DEV), d2)
+    assert _rel(d2, d1) < 1e-2
+
+
+def test_maxpool3():
+    torch.manual_seed(2)
+    x = torch.randn(2, 112, 112, 64).to(torch.bfloat16)
+    ys, ams, dxs = [], [], []
+    dy = torch.randn(2, 56, 56, 64).to(torch.bfloat16)
+    for dev in ("cpu", DEV):
+        y = torch.empty(2, 56, 56, 64, dtype=torch.bfloat16, device=dev)
+        am = torch.empty(2, 56, 56, 64, dtype=torch.uint8, device=dev)
+        dx = torch.empty(2, 112, 112, 64, dtype=torch.bfloat16, device=dev)
+        ops.maxpool3_fwd(x.to(dev), y, am)
+        ops.maxpool3_bwd(dy.to(dev), am, dx)
+        ys.append(y.cpu()), ams.append(am.cpu()), dxs.append(dx.cpu())
+    assert torch.equal(ys[0], ys[1])
+    assert (ams[0] == ams[1]).float().mean() > 0.999
+    assert _rel(dxs[1], dxs[0]) < 1e-2
