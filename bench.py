@@ -4,6 +4,7 @@ images/sec for the whole job (BASELINE.json metric).
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python bench.py --model resnet20 | resnet50     (BASELINE.json configs 3 and 5)
 
 Weak scaling: every rank trains --batch_size images per step (global batch =
 batch_size * N).  Synthetic MNIST-shaped data resident in HBM, random-init
@@ -54,7 +55,10 @@ def main():
     ap.add_argument("--batch_size", type=int, default=DEFAULT_BATCH, help="per-GPU batch")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
     args = ap.parse_args()
+    if args.model != "mnist_cnn":
+        return bench_resnet(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -128,6 +132,92 @@ def main():
                 "hip_graph": runner.graph is not None,
                 "last_loss": round(loss, 4),
             },
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_resnet(args):
+    """ResNet-20 (CIFAR-10 shape) / ResNet-50 (ImageNet shape) sync all-reduce step: device-side
+    batch sampling from an HBM-resident synthetic set, fwd+bwd, RCCL all-reduce, Momentum apply."""
+    from dtfe import ops
+    from dtfe.models.resnet import ResNetModel
+    from dtfe.optim import Optimizer
+    from dtfe.train import _buckets
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    model = ResNetModel(arch=args.model)
+    B = args.batch_size if args.batch_size != DEFAULT_BATCH else (256 if args.model == "resnet20" else 64)
+    prog = model.program(device, B, seed=0)
+    gstep = torch.zeros(1, dtype=torch.int32, device=device)
+    cfg, names, bp = model.opt_groups[0]
+    opt = Optimizer(cfg, prog.P, var_list=names, global_step=gstep, beta_power_names=bp)
+    ar = None
+    if world > 1:
+        dist.broadcast(prog.P.master, src=0)
+        prog.P.refresh_copies()
+        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P),
+                             comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+    n_pool = 4096 if args.model == "resnet20" else 512
+    g = torch.Generator().manual_seed(rank + 11)
+    pix = model.image * model.image * model.channels
+    images = torch.randint(0, 256, (n_pool, pix), generator=g, dtype=torch.uint8).to(device)
+    labels = torch.randint(0, model.num_classes, (n_pool,), generator=g, dtype=torch.int32).to(device)
+    lab = torch.empty(B, dtype=torch.int32, device=device)
+    ctr = torch.zeros(1, dtype=torch.int64, device=device)
+    done = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def step():
+        ops.gather_rows(images, prog.x.view(B, -1), None, labels, lab, seed=rank + 1, counter=ctr, done=done)
+        prog.y.zero_()
+        prog.y.scatter_(1, lab.long().unsqueeze(1), 1.0)
+        prog.compute_grads()
+        g16 = None
+        if ar is not None:
+            for i in range(len(ar.buckets)):
+                ar.launch(i)
+            ar.wait()
+            g16 = ar.grad16
+        opt.step(grad16=g16, gscale=1.0 / world) if g16 is not None else opt.step(gscale=1.0 / world)
+
+    runner = StepGraph(step, warmup=2, enabled=(world == 1 and not args.no_graph and graphs_enabled()))
+    for _ in range(args.warmup):
+        runner()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = B * world * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node), %s sync all-reduce" % args.model,
+            "value": round(value, 1), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (HBM-resident %dx%dx%d uint8 images, random labels; random-init weights)"
+                    % (model.image, model.image, model.channels),
+            "config": {"model": "%s (%d params)" % (args.model, model.num_params()), "global_batch": B * world,
+                       "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_batch": B,
+                       "optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None,
+                       "last_loss": round(float(prog.loss.item()) / B, 4)},
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

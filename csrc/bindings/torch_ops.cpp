@@ -176,13 +176,15 @@ void conv1_wgrad_pooled(const Tensor& x, const Tensor& dp, const Tensor& argmax,
 void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, const optional<Tensor>& src_argmax,
              const Tensor& w, const optional<Tensor>& bias, const Tensor& y, const optional<Tensor>& argmax,
              const optional<Tensor>& relu_mask, int64_t B, int64_t SH, int64_t SW, int64_t CS, int64_t OH, int64_t OW,
-             int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool) {
+             int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool,
+             int64_t dil) {
   check_cuda(w, "w");
   TORCH_CHECK((src.has_value() && src->defined()) != (src_pooled.has_value() && src_pooled->defined()),
               "imgconv: exactly one of src / src_pooled");
   dtfe::ImgConvArgs a{};
   a.B = (int)B; a.SH = (int)SH; a.SW = (int)SW; a.CS = (int)CS; a.OH = (int)OH; a.OW = (int)OW; a.N = (int)N;
   a.KH = (int)KH; a.KW = (int)KW; a.stride = (int)stride; a.pad = (int)pad; a.flip_taps = flip_taps;
+  a.dil = (int)dil;
   a.src = ptr_or_null<dtfe::bf16>(src);
   a.src_pooled = ptr_or_null<dtfe::bf16>(src_pooled);
   a.src_argmax = ptr_or_null<uint8_t>(src_argmax);
@@ -581,7 +583,7 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
-      " int stride, int pad, bool flip_taps, int act, bool pool) -> ()");
+      " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1) -> ()");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None) -> ()");

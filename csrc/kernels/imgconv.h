@@ -22,6 +22,8 @@ struct ImgConvArgs {
   int OH, OW, N;            // output pixels and channels
   int KH, KW, stride, pad;
   int flip_taps;
+  int dil;                  // source dilation (0/1: none): source pixel (y, x) sits at (y*dil, x*dil)
+                            // of the zero-padded image - the data gradient of a strided conv
   const bf16* src;          // [B][SH][SW][CS]   (or nullptr with src_pooled)
   const bf16* src_pooled;   // [B][SH/2][SW/2][CS] pooled values to route through src_argmax
   const uint8_t* src_argmax;

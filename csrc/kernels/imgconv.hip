@@ -89,16 +89,17 @@ __device__ __forceinline__ void stage_image(bf16* img, int LH, int LW, int lo, i
     reinterpret_cast<u32x4_t*>(img + (size_t)npix * CS)[i] = u32x4_t{0u, 0u, 0u, 0u};
 }
 
-// Single-channel LDS image [LH][LW] (source [SH][SW] at offset lo), then `extra` zeros.
-__device__ __forceinline__ void stage_image1(bf16* img, int LH, int LW, int lo, int SH, int SW, const bf16* src,
-                                             int extra) {
+// Few-channel LDS image [LH][LW][CS] (CS <= 4; source [SH][SW][CS] at offset lo), then `extra` zeros.
+__device__ __forceinline__ void stage_image_small(bf16* img, int LH, int LW, int CS, int lo, int SH, int SW,
+                                                  const bf16* src, int extra) {
   const int npix = LH * LW;
   const float inv_lw = 1.f / (float)LW;
   for (int pix = threadIdx.x; pix < npix; pix += IC_THREADS) {
     const int ly = fdiv(pix, LW, inv_lw), sy = ly - lo, sx = pix - ly * LW - lo;
-    img[pix] = (sy >= 0 && sy < SH && sx >= 0 && sx < SW) ? src[sy * SW + sx] : (bf16)0;
+    const bool in = sy >= 0 && sy < SH && sx >= 0 && sx < SW;
+    for (int c = 0; c < CS; ++c) img[pix * CS + c] = in ? src[(sy * SW + sx) * CS + c] : (bf16)0;
   }
-  for (int i = threadIdx.x; i < extra; i += IC_THREADS) img[npix + i] = (bf16)0;
+  for (int i = threadIdx.x; i < extra; i += IC_THREADS) img[npix * CS + i] = (bf16)0;
 }
 
 // epilogue: lane holds rows (lane>>4)*4 + j of each 16-row tile, column lane&15 of each n-tile
@@ -232,31 +233,33 @@ __global__ __launch_bounds__(IC_THREADS) void imgconv_kernel(ImgConvArgs a) {
   }
 }
 
-// Single-channel source (network input): k = tap (KH*KW <= 32, one k-step),
-// A fragment = 8 taps of one output pixel gathered from the 1-channel LDS image
-// with per-lane constant offsets, weights [N][T] held in registers.
+// Few-channel source (network inputs: MNIST 1, CIFAR/ImageNet 3 channels):
+// k = tap*CS + c (KH*KW*CS <= 32, one k-step), A fragment = 8 (tap, c) values
+// of one output pixel gathered from the LDS image with per-lane constant
+// offsets, weights [N][T*CS] held in registers.
 template <int NT, int RT>
 __global__ __launch_bounds__(IC_THREADS) void imgconv1_kernel(ImgConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 img[];
   const long b = blockIdx.x;
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
-  stage_image1(img, LH, LW, a.pad, a.SH, a.SW, a.src + b * a.SH * a.SW, 0);
+  const int CS = a.CS;
+  stage_image_small(img, LH, LW, CS, a.pad, a.SH, a.SW, a.src + b * a.SH * a.SW * CS, 0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4;
-  const int M = a.OH * a.OW, tiles = (M + 15) >> 4, T = a.KH * a.KW, POW = a.OW >> 1;
+  const int M = a.OH * a.OW, tiles = (M + 15) >> 4, K = a.KH * a.KW * CS, POW = a.OW >> 1;
   int toff[8];
   bf16x8_t bf[NT];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int tap = 8 * g + j, kh = tap / a.KW;
-    toff[j] = tap < T ? kh * LW + (tap - kh * a.KW) : -1;
+    const int k = 8 * g + j, tap = k / CS, c = k - tap * CS, kh = tap / a.KW;
+    toff[j] = k < K ? (kh * LW + (tap - kh * a.KW)) * CS + c : -1;
   }
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int col = n * 16 + (lane & 15);
     s16x8_t v;  // bf16 bit patterns (bf16 is the uint16 storage type: never convert numerically)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (short)((col < a.N && toff[j] >= 0) ? a.w[(long)col * T + 8 * g + j] : 0);
+    for (int j = 0; j < 8; ++j) v[j] = (short)((col < a.N && toff[j] >= 0) ? a.w[(long)col * K + 8 * g + j] : 0);
     bf[n] = __builtin_bit_cast(bf16x8_t, v);
   }
   for (int t0 = wid; t0 < tiles; t0 += 4 * RT) {
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(IC_THREADS) void imgconv1_kernel(ImgConvArgs a) {
           oy = m / a.OW;
           ox = m % a.OW;
         }
-        pix = oy * a.stride * LW + ox * a.stride;
+        pix = (oy * a.stride * LW + ox * a.stride) * CS;
       }
       s16x8_t av;
 #pragma unroll
@@ -295,14 +298,14 @@ __global__ __launch_bounds__(IC_THREADS) void imgconv1_kernel(ImgConvArgs a) {
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad) {
   const int OH = (SH + 2 * pad - KH) / stride + 1, OW = (SW + 2 * pad - KW) / stride + 1;
   const long LH = (long)(OH - 1) * stride + KH, LW = (long)(OW - 1) * stride + KW;
-  if (CS == 1) return KH * KW <= 32 && N <= 64 && LH * LW * 2 <= 150 * 1024;
+  if (CS <= 4) return KH * KW * CS <= 32 && N <= 64 && LH * LW * CS * 2 <= 150 * 1024;
   return CS % 8 == 0 && N <= 64 && LH * LW * CS * 2 <= 150 * 1024;
 }
 
 template <int NT>
 static void launch_nt(const ImgConvArgs& a, size_t lds, hipStream_t s) {
   constexpr int RT = 4;
-  auto k = a.CS == 1 ? imgconv1_kernel<NT, RT> : imgconv_kernel<NT, RT>;
+  auto k = a.CS <= 4 ? imgconv1_kernel<NT, RT> : imgconv_kernel<NT, RT>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, dim3(a.B), dim3(IC_THREADS), lds, s, a);
 }
@@ -310,9 +313,11 @@ static void launch_nt(const ImgConvArgs& a, size_t lds, hipStream_t s) {
 void launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
   if (!imgconv_supported(a.SH, a.SW, a.CS, a.N, a.KH, a.KW, a.stride, a.pad))
     throw std::runtime_error("imgconv: shape not supported");
-  if (a.CS == 1 && (!a.src || a.flip_taps)) throw std::runtime_error("imgconv: 1-channel path is forward-only");
+  if (a.CS <= 4 && (!a.src || a.flip_taps || a.dil > 1))
+    throw std::runtime_error("imgconv: the few-channel path is forward-only");
   if (a.pool && ((a.OH | a.OW) & 1)) throw std::runtime_error("imgconv: pool needs even output dims");
-  if (a.CS != 1 && launch_imgconv_persistent(a, s)) return;
+  if (a.CS > 4 && launch_imgconv_persistent(a, s)) return;
+  if (a.dil > 1) throw std::runtime_error("imgconv: dilated sources need the persistent kernel (B >= 64)");
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
   const size_t lds = (size_t)LH * LW * a.CS * sizeof(bf16);
   if (a.N <= 16) launch_nt<1>(a, lds, s);
@@ -334,7 +339,7 @@ __host__ __device__ inline WgGeom wg_geom(const ImgWgradArgs& a, int CS) {
   WgGeom g;
   g.LH = (a.OH - 1) * a.stride + a.KH;
   g.LW = (a.OW - 1) * a.stride + a.KW;
-  g.OWP = CS == 1 ? 8 : 4;  // 8 consecutive k (1-channel A fragment) / 4 (tr read) in one row
+  g.OWP = CS <= 4 ? 8 : 4;  // 8 consecutive k (few-channel A fragment) / 4 (tr read) in one row
   while (g.OWP < a.OW) g.OWP <<= 1;
   g.Kpad = ((a.OH * g.OWP + 31) / 32) * 32;
   g.nk = g.Kpad / 32;
@@ -486,15 +491,17 @@ __global__ __launch_bounds__(IC_THREADS) void imgwgrad_kernel(ImgWgradArgs a) {
   }
 }
 
-// Single-channel source: C[tap][n] = sum_pixel X[pixel + tap] * dY[pixel][n].
-// A = shifted-image rows (tap, 8 consecutive pixels of one output row: 8
-// scalar LDS reads at per-lane constant tap offsets), B = dY image through the
-// transposing read.  The 4 waves split the k-steps and reduce through LDS, so
+// Few-channel source (CS <= 4, K = T*CS <= 32):
+// C[k = (tap, c)][n] = sum_pixel X[pixel + tap][c] * dY[pixel][n].
+// A = shifted-image rows (k, 8 consecutive pixels of one output row: 8
+// scalar LDS reads at per-lane constant (tap, c) offsets), B = dY image through
+// the transposing read.  The 4 waves split the k-steps and reduce through LDS, so
 // a workgroup issues one set of N*T global atomics for all its images.
 template <int NC>
 __global__ __launch_bounds__(IC_THREADS) void imgwgrad1_kernel(ImgWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 smem[];
-  const WgGeom G = wg_geom(a, 1);
+  const int CS = a.CS;
+  const WgGeom G = wg_geom(a, CS);
   constexpr int NP = NC * 16;
   bf16* simg = smem;
   const int soff = (G.src_elems + G.slack + 7) / 8 * 8;
@@ -502,14 +509,14 @@ __global__ __launch_bounds__(IC_THREADS) void imgwgrad1_kernel(ImgWgradArgs a) {
   float* red = reinterpret_cast<float*>(dimg + G.Kpad * NP);  // [32 taps][NP] + db[NP]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
-  const int T = a.KH * a.KW;
+  const int K = a.KH * a.KW * CS;
   for (int i = threadIdx.x; i < 33 * NP; i += IC_THREADS) red[i] = 0.f;
 
   int toff[2];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
-    const int tap = rt * 16 + i16, kh = tap / a.KW;
-    toff[rt] = tap < T ? kh * G.LW + (tap - kh * a.KW) : 0;  // rows >= T are dropped at the flush
+    const int k = rt * 16 + i16, tap = k / CS, c = k - tap * CS, kh = tap / a.KW;
+    toff[rt] = k < K ? (kh * G.LW + (tap - kh * a.KW)) * CS + c : 0;  // rows >= K are dropped at the flush
   }
   // this lane's 8 pixels at k-step s: k = 32s + 8g + j, one output row (OWP >= 8)
   const int k0 = 8 * g, oy0 = k0 / G.OWP, ox0 = k0 - oy0 * G.OWP;
@@ -530,7 +537,7 @@ __global__ __launch_bounds__(IC_THREADS) void imgwgrad1_kernel(ImgWgradArgs a) {
     const long b = (long)blockIdx.x * a.imgs_per_block + im;
     if (b >= a.B) break;
     __syncthreads();
-    stage_image1(simg, G.LH, G.LW, a.pad, a.SH, a.SW, a.src + b * a.SH * a.SW, G.slack);
+    stage_image_small(simg, G.LH, G.LW, CS, a.pad, a.SH, a.SW, a.src + b * a.SH * a.SW * CS, G.slack);
     stage_dy<NP>(dimg, a, G, b);
     __syncthreads();
     for (int s = wid; s < G.nk; s += 4) {
@@ -553,14 +560,14 @@ __global__ __launch_bounds__(IC_THREADS) void imgwgrad1_kernel(ImgWgradArgs a) {
       for (int rt = 0; rt < 2; ++rt) {
         s16x8_t av;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) av[j] = (short)simg[apix + toff[rt] + j * a.stride];
+        for (int j = 0; j < 8; ++j) av[j] = (short)simg[(apix + j * a.stride) * CS + toff[rt]];
         const bf16x8_t af = __builtin_bit_cast(bf16x8_t, av);
 #pragma unroll
         for (int ct = 0; ct < NC; ++ct) acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[ct], acc[rt][ct], 0, 0, 0);
       }
     }
   }
-  // cross-wave reduction in LDS, then one global atomic per (n, tap)
+  // cross-wave reduction in LDS, then one global atomic per (n, k)
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -577,9 +584,9 @@ __global__ __launch_bounds__(IC_THREADS) void imgwgrad1_kernel(ImgWgradArgs a) {
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < T * a.N; i += IC_THREADS) {
-    const int n = i / T, tap = i - n * T;
-    atomicAdd(a.dw + i, red[tap * NP + n] * a.scale);
+  for (int i = threadIdx.x; i < K * a.N; i += IC_THREADS) {
+    const int n = i / K, k = i - n * K;
+    atomicAdd(a.dw + i, red[k * NP + n] * a.scale);
   }
   if (a.db)
     for (int n = threadIdx.x; n < a.N; n += IC_THREADS) atomicAdd(a.db + n, red[32 * NP + n] * a.scale);
@@ -589,8 +596,8 @@ static int wg_nt(int N) { return N <= 16 ? 1 : (N <= 32 ? 2 : 4); }
 
 static size_t wg_lds(const ImgWgradArgs& a) {
   const int MT = wg_nt(a.N);
-  if (a.CS == 1) {
-    const WgGeom G = wg_geom(a, 1);
+  if (a.CS <= 4) {
+    const WgGeom G = wg_geom(a, a.CS);
     return ((size_t)(G.src_elems + G.slack + 7) / 8 * 8 + (size_t)G.Kpad * MT * 16) * sizeof(bf16) +
            33 * MT * 16 * sizeof(float);
   }
@@ -600,8 +607,8 @@ static size_t wg_lds(const ImgWgradArgs& a) {
 
 bool imgwgrad_supported(const ImgWgradArgs& a) {
   if (a.N > 64 || a.OW > 32) return false;
-  if (a.CS == 1) {
-    if (a.KH * a.KW > 32) return false;
+  if (a.CS <= 4) {
+    if (a.KH * a.KW * a.CS > 32) return false;
   } else if (a.CS % 8) {
     return false;
   }
@@ -642,8 +649,8 @@ static void launch_wg1(const ImgWgradArgs& a0, hipStream_t s) {
 
 void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s) {
   if (!imgwgrad_supported(a)) throw std::runtime_error("imgwgrad: shape not supported");
-  if (a.CS == 1) {
-    if (!a.src) throw std::runtime_error("imgwgrad: 1-channel path needs src");
+  if (a.CS <= 4) {
+    if (!a.src) throw std::runtime_error("imgwgrad: few-channel path needs src");
     switch (wg_nt(a.N)) {
       case 1: launch_wg1<1>(a, s); break;
       case 2: launch_wg1<2>(a, s); break;

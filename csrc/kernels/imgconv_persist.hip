@@ -129,7 +129,8 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
         sy = pix / a.SW;
         sx = pix - sy * a.SW;
       }
-      const int ly = sy + a.pad, lx = sx + a.pad;
+      const int dil = a.dil > 1 ? a.dil : 1;
+      const int ly = sy * dil + a.pad, lx = sx * dil + a.pad;
       // host guarantees pooled windows lie inside the extent; plain pixels outside it are unused
       if (ly < G.LH && lx < G.LW) dst[j] = (ly * LWP + lx) * PS + cc * 8;
     }
@@ -375,6 +376,7 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
   const bool pooled = a.src == nullptr;
   if (pooled && ((a.SH | a.SW) & 1)) return false;
+  if (pooled && a.dil > 1) return false;
   {  // pooled windows must lie inside the LDS extent (plain pixels outside it are unused)
     const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
     if (pooled && (a.SH + a.pad > LH || a.SW + a.pad > LW)) return false;

@@ -309,11 +309,20 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
     }
     return true;
   };
-  if (npfs == 1 && npfd == 1) return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED>);
-  if (npfs == 2 && npfd == 1) return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED>);
-  if (npfs == 2 && npfd == 2) return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED>);
-  if (npfs == 1 && npfd == 2) return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED>);
-  return false;
+  // prefetch chunks per thread (source, dY): 1, 2 or 4 each
+  auto q = [](int n) { return n <= 1 ? 1 : (n <= 2 ? 2 : (n <= 4 ? 4 : 0)); };
+  switch (q(npfs) * 8 + q(npfd)) {
+    case 9: return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED>);
+    case 10: return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED>);
+    case 12: return go(imgwgrad_persist_kernel<MT, CTW, 1, 4, POOLED>);
+    case 17: return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED>);
+    case 18: return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED>);
+    case 20: return go(imgwgrad_persist_kernel<MT, CTW, 2, 4, POOLED>);
+    case 33: return go(imgwgrad_persist_kernel<MT, CTW, 4, 1, POOLED>);
+    case 34: return go(imgwgrad_persist_kernel<MT, CTW, 4, 2, POOLED>);
+    case 36: return go(imgwgrad_persist_kernel<MT, CTW, 4, 4, POOLED>);
+    default: return false;
+  }
 }
 
 }  // namespace

@@ -210,9 +210,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
   }
 }
 
-int grid_for(long R, int C, int max_blocks) {
+// workgroups for R rows: `per_thread` rows per thread, at most max_blocks.  The statistics
+// kernels use 8 rows per thread (fewer workgroups -> fewer contended per-channel atomics),
+// the apply kernels 2 (no atomics: as many workgroups as fill the chip).
+int grid_for(long R, int C, int max_blocks, int per_thread) {
   const int rpp = NT / (C / 8);
-  long rows_per_block = (long)rpp * 8;  // >= 8 rows per thread before adding workgroups
+  long rows_per_block = (long)rpp * per_thread;
   long g = (R + rows_per_block - 1) / rows_per_block;
   if (g > max_blocks) g = max_blocks;
   return g < 1 ? 1 : (int)g;
@@ -242,22 +245,29 @@ __global__ void shortcut_grad_kernel(const bf16* g, bf16* dx, int B, int OH, int
   }
 }
 
-__global__ void gap_fwd_kernel(const bf16* x, bf16* y, int B, int HW, int C) {
-  const int cpr = C / 8;
-  const long n = (long)B * cpr;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long b = i / cpr;
-    const int ch = (int)(i - b * cpr) * 8;
-    float s[8] = {};
-    for (int p = 0; p < HW; ++p) {
-      float f[8];
-      unpack8(*reinterpret_cast<const u32x4_t*>(x + (b * HW + p) * C + ch), f);
+// one workgroup per image: threads = (chunk, pixel lane); pixel lanes reduce through LDS
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* x, bf16* y, int B, int HW, int C) {
+  __shared__ float red[256 * 8];
+  const int cpr = C / 8;  // power of two <= 256
+  const int lanes = 256 / cpr, chunk = threadIdx.x % cpr, pl = threadIdx.x / cpr;
+  const long b = blockIdx.x;
+  float s[8] = {};
+  for (int p = pl; p < HW; p += lanes) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4_t*>(x + (b * HW + p) * C + chunk * 8), f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += f[e];
-    }
+    for (int e = 0; e < 8; ++e) s[e] += f[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = s[e];
+  __syncthreads();
+  if (pl == 0) {
+    for (int l = 1; l < lanes; ++l)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += red[(l * cpr + chunk) * 8 + e];
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] *= 1.f / (float)HW;
-    *reinterpret_cast<u32x4_t*>(y + b * C + ch) = pack8(s);
+    *reinterpret_cast<u32x4_t*>(y + b * C + chunk * 8) = pack8(s);
   }
 }
 
@@ -331,24 +341,24 @@ int ew_grid(long n) {
 void launch_bn_stats(const BnArgs& a, hipStream_t s) {
   check(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(grid_for(a.R, a.C, 1024)), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(grid_for(a.R, a.C, 1024, 8)), dim3(NT), lds, s, a);
 }
 
 void launch_bn_apply(const BnArgs& a, hipStream_t s) {
   check(a);
   if (a.res && (a.RC % 8 || a.RC > a.C)) throw std::runtime_error("bn_apply: residual channels");
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(a.R, a.C, 2048)), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(a.R, a.C, 2048, 2)), dim3(NT), 0, s, a);
 }
 
 void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s) {
   check(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(grid_for(a.R, a.C, 1024)), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(grid_for(a.R, a.C, 1024, 8)), dim3(NT), lds, s, a);
 }
 
 void launch_bn_bwd_apply(const BnArgs& a, hipStream_t s) {
   check(a);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(a.R, a.C, 2048)), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(a.R, a.C, 2048, 2)), dim3(NT), 0, s, a);
 }
 
 void launch_shortcut_grad_add(const bf16* g, bf16* dx, int B, int OH, int OW, int C, int XH, int XW, int XC,
@@ -359,8 +369,9 @@ void launch_shortcut_grad_add(const bf16* g, bf16* dx, int B, int OH, int OW, in
 }
 
 void launch_gap_fwd(const bf16* x, bf16* y, int B, int HW, int C, hipStream_t s) {
-  if (C % 8) throw std::runtime_error("gap: C % 8");
-  hipLaunchKernelGGL(gap_fwd_kernel, dim3(ew_grid((long)B * C / 8)), dim3(256), 0, s, x, y, B, HW, C);
+  const int t = C / 8;
+  if (C % 8 || t > 256 || (t & (t - 1))) throw std::runtime_error("gap: C must be 8 * 2^k <= 2048");
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(B), dim3(256), 0, s, x, y, B, HW, C);
 }
 
 void launch_gap_bwd(const bf16* dy, bf16* dx, int B, int HW, int C, hipStream_t s) {

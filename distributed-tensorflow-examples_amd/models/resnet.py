@@ -115,10 +115,13 @@ class Conv:
                        KW=self.k, stride=self.stride, pad=self.pad)
         LH = (self.OH - 1) * self.stride + self.k
         LW = (self.OW - 1) * self.stride + self.k
-        self.img_fwd = self.cin % 8 == 0 and self.cout <= 64 and LH * LW * self.cin * 2 <= 150 * 1024
-        self.img_dgrad = (self.stride == 1 and self.cout % 8 == 0 and self.cin <= 64
+        few = self.cin <= 4 and self.k * self.k * self.cin <= 32  # tap-packed network-input kernels
+        self.img_fwd = (self.cin % 8 == 0 or few) and self.cout <= 64 and LH * LW * self.cin * 2 <= 150 * 1024
+        # data gradient as a stride-1 flipped-tap conv over dY, dilated by the stride (persistent kernel: B >= 64)
+        self.dil = self.stride if (self.H == self.OH * self.stride and self.W == self.OW * self.stride) else 0
+        self.img_dgrad = (self.dil > 0 and (self.stride == 1 or B >= 64) and self.cout % 8 == 0 and self.cin <= 64
                           and (self.H + self.k - 1) * (self.W + self.k - 1) * self.cout * 2 <= 150 * 1024)
-        self.img_wgrad = self.cin % 8 == 0 and self.cout <= 64 and self.OW <= 32 and self.cout % 8 == 0
+        self.img_wgrad = (self.cin % 8 == 0 or few) and self.cout <= 64 and self.OW <= 32 and self.cout % 8 == 0
 
     def fwd(self, x):
         if self.img_fwd:
@@ -137,7 +140,7 @@ class Conv:
         if self.img_dgrad:
             ops.imgconv(self.wt, dx, src=dy, flip_taps=True, B=self.B, SH=self.OH, SW=self.OW, CS=self.cout,
                         OH=self.H, OW=self.W, N=self.cin, KH=self.k, KW=self.k, stride=1,
-                        pad=self.k - 1 - self.pad)
+                        pad=self.k - 1 - self.pad, dil=self.dil)
         else:
             ops.conv_dgrad(dy, self.wt, dx, self.g)
 

@@ -254,15 +254,21 @@ def _unpooled_nhwc(pooled, argmax, B, H, W, C):
 
 
 def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None, src_pooled=None,
-            src_argmax=None, bias=None, argmax=None, relu_mask=None, flip_taps=False, act=ACT_NONE, pool=False):
+            src_argmax=None, bias=None, argmax=None, relu_mask=None, flip_taps=False, act=ACT_NONE, pool=False,
+            dil=1):
     """Whole-image LDS convolution (small feature maps): forward (+bias/act/pool) or, with
     flip_taps and pad = K-1-pad, the data gradient of a stride-1 conv (w = Wt [cin][tap][cout]).
-    The source may be un-pooled on load from (src_pooled, src_argmax)."""
+    The source may be un-pooled on load from (src_pooled, src_argmax), or dilated (``dil``: source
+    pixel (y, x) at (y*dil, x*dil), zeros between - the data gradient of a stride-``dil`` conv)."""
     if y.is_cuda:
         require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW, N, KH,
-                          KW, stride, pad, flip_taps, act, pool)
+                          KW, stride, pad, flip_taps, act, pool, dil)
         return y
     s = src.float().view(B, SH, SW, CS) if src is not None else _unpooled_nhwc(src_pooled, src_argmax, B, SH, SW, CS)
+    if dil > 1:
+        sd = torch.zeros(B, SH * dil, SW * dil, CS)
+        sd[:, ::dil, ::dil, :] = s
+        s = sd
     wt = w.float().view(N, KH, KW, CS)
     if flip_taps:
         wt = wt.flip(1, 2)

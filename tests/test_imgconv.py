@@ -157,3 +157,45 @@ PERSIST_WG_CASES = [  # B >= 128: persistent register-accumulating kernel
 def test_imgwgrad_persistent(case):
     test_imgwgrad(case)
 
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(96, 16, 32, 16, 3, 2, 1), (80, 8, 64, 32, 3, 2, 1)])
+def test_imgconv_dilated_dgrad_of_strided_conv(case):
+    """dX of a stride-2 conv = stride-1 flipped-tap conv over dY dilated by 2 (persistent kernel)."""
+    B, OHs, COUT, CIN, K, s, pad = case
+    H = OHs * s
+    torch.manual_seed(5)
+    dy = torch.randn(B, OHs, OHs, COUT).to(DEV, torch.bfloat16)
+    wt = (torch.randn(CIN, K, K, COUT) * 0.1).to(DEV, torch.bfloat16)
+    kw = dict(B=B, SH=OHs, SW=OHs, CS=COUT, OH=H, OW=H, N=CIN, KH=K, KW=K, stride=1, pad=K - 1 - pad,
+              flip_taps=True, dil=s)
+    y = torch.empty(B, H, H, CIN, device=DEV, dtype=torch.bfloat16)
+    ops.imgconv(wt, y, src=dy, **kw)
+    # oracle: autograd dX of the strided conv
+    x = torch.zeros(B, CIN, H, H, requires_grad=True)
+    w = wt.float().cpu().permute(3, 0, 1, 2)  # Wt[cin][kh][kw][cout] -> W[cout][cin][kh][kw]
+    out = torch.nn.functional.conv2d(x, w, stride=s, padding=pad)
+    out.backward(dy.float().cpu().permute(0, 3, 1, 2))
+    assert _rel(y.cpu(), x.grad.permute(0, 2, 3, 1)) < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cs", [2, 3])
+def test_few_channel_conv_fwd_wgrad(cs):
+    """Tap-packed network-input kernels with CS = 2, 3 (CIFAR stem: 3x3x3 = 27 taps)."""
+    B, H, N, K = 70, 32, 16, 3
+    torch.manual_seed(6)
+    x = torch.randn(B, H, H, cs).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, K, cs) * 0.2).to(DEV, torch.bfloat16)
+    kw = dict(B=B, SH=H, SW=H, CS=cs, OH=H, OW=H, N=N, KH=K, KW=K, stride=1, pad=1)
+    y = torch.empty(B, H, H, N, device=DEV, dtype=torch.bfloat16)
+    ops.imgconv(w, y, src=x, **kw)
+    yr = torch.empty(B, H, H, N)
+    ops.imgconv(w.cpu(), yr, src=x.cpu(), **kw)
+    assert _rel(y.cpu(), yr) < 2e-2
+    dy = torch.randn(B, H, H, N).to(DEV, torch.bfloat16)
+    dw, dwr = torch.zeros(N, K, K, cs, device=DEV), torch.zeros(N, K, K, cs)
+    ops.imgwgrad(x, dw, None, dy=dy, **kw)
+    ops.imgwgrad(x.cpu(), dwr, None, dy=dy.cpu(), **kw)
+    assert _rel(dw.cpu(), dwr) < 1e-2
+
