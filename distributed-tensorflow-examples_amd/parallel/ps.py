@@ -129,7 +129,7 @@ class PSServer:
     """The ps role of ``main(_)`` (GAN:108-117) plus the TF runtime's variable service."""
 
     def __init__(self, server, shard: Shard, num_workers: int, sync: bool = False, replicas_to_aggregate=None,
-                 hogwild: bool = False, comm_device="cpu", log=print):
+                 hogwild: bool = False, comm_device="cpu", log=print, watchdog=None, faults=None):
         self.server = server
         self.shard = shard
         self.num_workers = num_workers
@@ -145,6 +145,10 @@ class PSServer:
         self._acc_cv = threading.Condition()
         self._threads = []
         self.errors = []
+        self.watchdog = watchdog      # health.Watchdog over the workers (None: reference semantics)
+        self.faults = faults          # utils.faults.FaultInjector of this ps task
+        self.done_ranks = set()
+        self.lost = set()
 
     # ---- per-worker service thread
     def _serve(self, worker_rank: int):
@@ -161,6 +165,7 @@ class PSServer:
                     with self._done_cv:
                         i = self.done_count
                         self.done_count += 1
+                        self.done_ranks.add(worker_rank)
                         self.log("ps %d received done %d" % (self.server.task_index, i))
                         self._done_cv.notify_all()
                     return
@@ -205,6 +210,8 @@ class PSServer:
                     else:
                         with sh.lock:
                             sh.apply(pay.to(sh.device))
+                    if self.faults:
+                        self.faults.step(sh.global_step())
                 # PULL and PUSH both answer with fresh parameters
                 with sh.lock:
                     params = sh.P.master.to(cdev, copy=True)
@@ -243,9 +250,17 @@ class PSServer:
             t = threading.Thread(target=self._serve, args=(w,), daemon=True, name="ps-serve-%d" % w)
             t.start()
             self._threads.append(t)
+        cl = self.server.cluster
         with self._done_cv:
-            while self.done_count < self.num_workers:
+            while self.done_count + len(self.lost) < self.num_workers:
                 self._done_cv.wait(timeout=1.0)
+                if self.watchdog is None:
+                    continue
+                for _job, task, age in self.watchdog.poll():
+                    if cl.rank_of("worker", task) in self.done_ranks:
+                        continue  # finished normally, then exited
+                    self.lost.add(task)
+                    self.log("ps %d: worker %d lost (no heartbeat for %.0fs)" % (self.server.task_index, task, age))
         self.log("ps %d: quitting" % self.server.task_index)
 
 

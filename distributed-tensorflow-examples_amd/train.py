@@ -15,6 +15,7 @@ plus the north-star modes: ``--sync`` (sync SGD with a chief over the ps) and
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import sys
@@ -37,6 +38,9 @@ from .models.autoencoder import LR as ENC_LR
 from .optim import Optimizer
 from .parallel.allreduce import BucketAllReduce
 from .parallel.cluster import ClusterSpec, Server
+from .parallel.health import Heartbeat, Watchdog
+from .utils.faults import FaultInjector
+from .utils.timers import PhaseTimer
 from .parallel.placement import round_robin
 from .parallel.ps import PSClient, PSServer, Shard, wait_for_init
 from .parallel.supervisor import Supervisor
@@ -182,9 +186,18 @@ def run_ps(flags, model, server, device, log):
     gs_here = placement[model.gs_name] == k
     shard = Shard(shard_specs[k], model.opt_groups, device, gs_here, model.gs_increments)
     comm = "cpu" if server.backend == "gloo" else device
-    PSServer(server, shard, num_workers=flags.workers, sync=flags.sync,
-             replicas_to_aggregate=flags.replicas_to_aggregate, hogwild=flags.hogwild, comm_device=comm,
-             log=log).serve_forever()
+    hb = Heartbeat(server.store, "ps", k, flags.heartbeat_secs)
+    wd = Watchdog(server.store, [("worker", i) for i in range(len(server.cluster.worker))],
+                  flags.heartbeat_timeout) if flags.heartbeat_secs > 0 else None
+    ps = PSServer(server, shard, num_workers=flags.workers, sync=flags.sync,
+                  replicas_to_aggregate=flags.replicas_to_aggregate, hogwild=flags.hogwild, comm_device=comm,
+                  log=log, watchdog=wd, faults=FaultInjector("ps", k, log=log))
+    ps.serve_forever()
+    hb.stop()
+    if ps.lost:
+        # service threads of lost workers are blocked in recv: leave without the collective teardown
+        sys.stdout.flush()
+        os._exit(0)
 
 
 def ps_state(client, model, shard_specs, placement):
@@ -233,6 +246,8 @@ def run_worker_ps(flags, model, server, device, log):
                           seed=flags.seed * 1000 + server.task_index + 1, log=log)
     feeder = Feeder(data, prog, device)
     metrics_log = MetricsLog(flags.metrics_jsonl)
+    hb = Heartbeat(server.store, "worker", server.task_index, flags.heartbeat_secs)
+    faults = FaultInjector("worker", server.task_index, log=log)
     begin_time = time.time()
     sv.prepare()
     if flags.reinit_on_join:
@@ -248,6 +263,9 @@ def run_worker_ps(flags, model, server, device, log):
             prog.load_batch(feeder.next())
             metrics = prog.compute_grads()
             step = client.push_pull(prog.P.grad)
+            if flags.check_pull:
+                log("pull checksum gs=%d: %.9e" % (step, float(prog.P.master.double().sum().item())))
+            faults.step(step)
             elapsed = time.time() - t0
             if local_step % flags.log_every == 0:
                 log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
@@ -264,6 +282,7 @@ def run_worker_ps(flags, model, server, device, log):
             log("Test-Accuracy: %2.4f" % acc)
         client.done()
     finally:
+        hb.stop()
         sv.stop()
 
 
@@ -303,22 +322,28 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
     metrics_log = MetricsLog(flags.metrics_jsonl)
 
     state = {}
+    timer = PhaseTimer(device) if flags.phase_timers else None
+    phase = timer.phase if timer else (lambda _n: contextlib.nullcontext())
+    faults = FaultInjector("worker", rank, log=log)
 
     def train_step():
-        state["m"] = prog.compute_grads()
+        with phase("fwd+bwd"):
+            state["m"] = prog.compute_grads()
         g16 = None
         if ar is not None:
-            for i in range(len(ar.buckets)):
-                ar.launch(i)
-            ar.wait()
+            with phase("comm"):
+                for i in range(len(ar.buckets)):
+                    ar.launch(i)
+                ar.wait()
             g16 = ar.grad16
-        for i, o in enumerate(opts):
-            last = i == len(opts) - 1
-            o.step(grad16=g16, gscale=1.0 / world, gs_inc=model.gs_increments if last else 0) if g16 is not None \
-                else o.step(gscale=1.0 / world, gs_inc=model.gs_increments if last else 0)
+        with phase("apply"):
+            for i, o in enumerate(opts):
+                last = i == len(opts) - 1
+                o.step(grad16=g16, gscale=1.0 / world, gs_inc=model.gs_increments if last else 0) if g16 is not None \
+                    else o.step(gscale=1.0 / world, gs_inc=model.gs_increments if last else 0)
 
     runner = StepGraph(train_step, warmup=2,
-                       enabled=device.type == "cuda" and world == 1 and flags.hip_graph)
+                       enabled=device.type == "cuda" and world == 1 and flags.hip_graph and timer is None)
     begin_time = time.time()
     step = int(gstep.item())
     local_step = 0
@@ -328,9 +353,12 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
             prog.load_batch(feeder.next())
             runner()
             step = int(gstep.item())
+            faults.step(step)
             elapsed = time.time() - t0
             if local_step % flags.log_every == 0:
                 log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
+                if timer is not None:
+                    log(PhaseTimer.format(timer.summary()))
             if "m" in state:
                 model_step_hook(model, step, state["m"], log)
             metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000,

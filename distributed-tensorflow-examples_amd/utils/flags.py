@@ -65,6 +65,12 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     ap.add_argument("--log_every", type=int, default=1, help="print the per-step line every N local steps")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--metrics_jsonl", default="", help="append {step, gs, ms, images/sec, loss} lines here")
+    ap.add_argument("--heartbeat_secs", type=float, default=0.0,
+                    help="publish a TCPStore heartbeat every N s (0: off, the reference has none)")
+    ap.add_argument("--heartbeat_timeout", type=float, default=30.0,
+                    help="ps: count a worker silent for this long as lost (with --heartbeat_secs)")
+    add_bool(ap, "phase_timers", False, "time fwd+bwd / comm / apply per step with hipEvents (no hipGraph)")
+    add_bool(ap, "check_pull", False, "debug: checksum the pulled parameters every step (ps mode)")
     return ap
 
 

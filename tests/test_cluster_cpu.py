@@ -162,3 +162,26 @@ def test_cnn_1ps_2workers_async_checkpoint_keys(tmp_path):
     assert tuple(t["Variable_2"].shape) == (3136, 1024)         # fc1 [in][out]
     assert "Variable_2/Adam" in t and "Variable_2/Adam_1" in t and "beta1_power" in t
     assert int(t["Variable_8"]) >= 1
+
+
+def test_fault_injection_crash_with_heartbeat_lets_ps_quit(tmp_path):
+    """DTFE_FAULT crashes worker 1 at step 5 (no done signal, like a killed pod); with heartbeats
+    the ps counts it lost after the timeout and still quits, while worker 0 finishes normally."""
+    env = dict(os.environ, DTFE_FAULT="crash@worker:1:step=5")
+    codes, out, _ = local_cluster.launch("softmax", 1, 2, COMMON + [
+        "--num_steps=300", "--workers=2", "--model_dir=" + str(tmp_path / "ck"), "--save_model_secs=0",
+        "--heartbeat_secs=0.2", "--heartbeat_timeout=2"], env=env, timeout=240, stream=False)
+    assert codes[("worker", 1)] == 17, out[("worker", 1)]
+    assert any("fault injection: worker 1 crashes" in l for l in out[("worker", 1)])
+    assert codes[("worker", 0)] == 0 and any(l.startswith("Total Time") for l in out[("worker", 0)])
+    ps = out[("ps", 0)]
+    assert codes[("ps", 0)] == 0, ps
+    assert any("ps 0: worker 1 lost" in l for l in ps) and ps[-1] == "ps 0: quitting"
+
+
+def test_phase_timers_and_check_pull(tmp_path):
+    codes, out, _ = local_cluster.launch("softmax", 1, 1, COMMON + [
+        "--num_steps=3", "--workers=1", "--model_dir=" + str(tmp_path / "ck"), "--save_model_secs=0",
+        "--check_pull"], timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    assert any(l.startswith("pull checksum gs=") for l in out[("worker", 0)])
