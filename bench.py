@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
     if args.model != "mnist_cnn":
         return bench_resnet(args)
@@ -64,8 +66,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local_rank %= torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
     device = torch.device("cuda", local_rank)
 
     allreduce = None
@@ -99,7 +105,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -128,7 +134,8 @@ def main():
                 "parallelism": "dp%d" % world,
                 "per_gpu_batch": args.batch_size,
                 "optimizer": "adam (TF1)",
-                "grad_allreduce": ("rccl bucketed %s" % args.comm_dtype) if world > 1 else "none (1 rank)",
+                "grad_allreduce": ("%s bucketed %s" % ("rccl" if args.backend == "nccl" else "gloo", args.comm_dtype))
+                if world > 1 else "none (1 rank)",
                 "hip_graph": runner.graph is not None,
                 "last_loss": round(loss, 4),
             },
