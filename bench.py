@@ -35,14 +35,16 @@ from dtfe.utils.graphs import StepGraph, graphs_enabled  # noqa: E402
 DEFAULT_BATCH = 1024  # per GPU
 
 
-def _baseline(n_gpus, batch):
+def _baseline(n_gpus, batch, model="mnist_cnn"):
     """Stock-PyTorch (DDP + MIOpen/hipBLASLt, bf16) images/sec measured on the same MI355X
-    box and config by bench/stock_torch_cnn.py; see BASELINE.md."""
+    box and config by bench/stock_torch_cnn.py (bench/stock_torch_resnet.py for the
+    ResNets); see BASELINE.md."""
     p = os.path.join(ROOT, "bench", "stock_baseline.json")
     try:
         with open(p) as f:
             tab = json.load(f)
-        return tab.get(f"{n_gpus}x{batch}")
+        key = f"{n_gpus}x{batch}" if model == "mnist_cnn" else f"{model}_{n_gpus}x{batch}"
+        return tab.get(key)
     except (OSError, ValueError):
         return None
 
@@ -213,12 +215,13 @@ def bench_resnet(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = B * world * args.steps / elapsed
+    base = _baseline(world, B, args.model)
     if rank == 0:
         print(json.dumps({
             "metric": "images/sec (whole node), %s sync all-reduce" % args.model,
             "value": round(value, 1), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": round(value / base, 3) if base else None, "dtype": "bf16",
             "data": "synthetic (HBM-resident %dx%dx%d uint8 images, random labels; random-init weights)"
                     % (model.image, model.image, model.channels),
             "config": {"model": "%s (%d params)" % (args.model, model.num_params()), "global_batch": B * world,

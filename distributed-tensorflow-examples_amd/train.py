@@ -198,6 +198,14 @@ def run_ps(flags, model, server, device, log):
         # service threads of lost workers are blocked in recv: leave without the collective teardown
         sys.stdout.flush()
         os._exit(0)
+    # The ps hosts the TCPStore and owns nothing the job still needs once every worker has
+    # said done (checkpoints are the chief's).  Tear the process groups down, then leave
+    # without interpreter finalisation: static destructors of the communicator / store
+    # threads racing the workers' own teardown end in std::terminate on a ROCm box.
+    server.shutdown()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 def ps_state(client, model, shard_specs, placement):

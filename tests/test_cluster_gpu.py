@@ -26,7 +26,8 @@ def test_cnn_ps_on_gpu(tmp_path, sync):
     extra = ["--device=cuda", "--synthetic", "--num_steps=8", "--workers=2", "--batch_size=64", "--seed=3",
              "--model_dir=" + md, "--save_model_secs=0.2"] + (["--sync"] if sync else [])
     codes, out, _ = local_cluster.launch("cnn", 1, 2, extra, timeout=600, stream=False, gpus=1)
-    assert all(c == 0 for c in codes.values()), (codes, out)
+    assert all(c == 0 for c in codes.values()), "%s\n%s" % (codes, "\n".join(
+        "---- %s\n%s" % (k, "\n".join(v[-40:])) for k, v in out.items()))
     assert out[("ps", 0)][-1] == "ps 0: quitting"
     gs = _gs(out[("worker", 0)]) + _gs(out[("worker", 1)])
     assert max(gs) >= 8
