@@ -16,6 +16,7 @@
 // (BASELINE.json configs 2-5).
 #include "gemm_core.h"
 #include "conv.h"
+#include "igemm.h"
 #include <stdexcept>
 
 namespace dtfe {
@@ -378,12 +379,14 @@ template <typename Cfg> struct FwdK { static constexpr auto fn = conv_fwd_kernel
 template <typename Cfg> struct DgradK { static constexpr auto fn = conv_dgrad_kernel<Cfg>; };
 
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
+  if (launch_igemm_fwd(a, s)) return;  // wide layers: DMA-staged 64-deep k-tiles
   const ConvGeom& g = a.g;
   if (g.pool_order && ((g.OH | g.OW) & 1)) throw std::runtime_error("conv_fwd: pool needs even output dims");
   launch_skinny<FwdK>(a, g.B * g.OH * g.OW, g.Cout, s);
 }
 
 void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s) {
+  if (launch_igemm_dgrad(a, s)) return;
   const ConvGeom& g = a.g;
   launch_skinny<DgradK>(a, g.B * g.H * g.W, g.C, s);
 }
@@ -404,6 +407,7 @@ static void wgrad_launch(const ConvWgradArgs& a0, int target_blocks, hipStream_t
 }
 
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
+  if (launch_igemm_wgrad(a, s)) return;
   const ConvGeom& g = a.g;
   const int M = g.Cout, N = g.KH * g.KW * g.C + (a.db ? 1 : 0);
   const int target = 1024;  // 4 workgroups per CU

@@ -1,0 +1,50 @@
+// Implicit-GEMM convolution for wide NHWC layers (C % 64 == 0, Cout % 64 == 0):
+// the ResNet-50 bottleneck / projection convs.  Operands are staged into LDS with
+// gfx950's direct global->LDS DMA (global_load_lds_dwordx4) in 64-deep k-tiles;
+// out-of-image taps read a zero page, so the main loop has no per-element branches.
+//
+//   forward   rows = output pixels, k = (tap, cin), B = W[cout][tap][cin]
+//   dgrad     the same kernel over dY with Wt[cin][tap][cout], one launch phase per
+//             output-pixel parity class (py, px) of a strided conv: phase p only
+//             visits the taps that reach its pixels (sub-pixel decomposition), so a
+//             stride-2 data gradient does no multiply-by-zero work
+//   wgrad     dW[cout][tap][cin] = sum_m dY[m][cout] X[src(m, tap)][cin]; the m
+//             reduction is split over workgroups, partial tiles go to a workspace
+//             and one reduce pass adds them (scaled) into the fp32 gradient.
+#pragma once
+#include "common.h"
+#include "conv.h"
+
+namespace dtfe {
+
+constexpr int IG_MAX_TAPS = 9;
+
+// One launch phase: rows are the pixels (b, i, j) of a RH x RW grid, written to
+// output pixel (i*ostr + oy, j*ostr + ox); tap t reads source pixel
+// (i*istr + dy[t], j*istr + dx[t]) and weight tap kt[t].
+struct IgPhase {
+  int ntaps, RH, RW, oy, ox;
+  int dy[IG_MAX_TAPS], dx[IG_MAX_TAPS], kt[IG_MAX_TAPS];
+};
+
+struct IgemmArgs {
+  const bf16* src; const bf16* w; bf16* out; float* ws; const bf16* zeros;
+  int B, SH, SW, SC;      // source tensor (NHWC)
+  int N, Ktot;            // output channels; weight row length = taps * SC
+  int istr, OHf, OWf, ostr;
+  int nphase, splits, tiles_m;
+  IgPhase ph[4];
+};
+
+struct IgWgradArgs {
+  const bf16* dy; const bf16* x; const bf16* zeros; float* ws;
+  int B, H, W, C, OH, OW, Cout, KH, KW, stride, pad;
+  int splits, mchunk;
+};
+
+// true when the igemm path handles the conv (and launches it)
+bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s);
+bool launch_igemm_dgrad(const ConvDgradArgs& a, hipStream_t s);
+bool launch_igemm_wgrad(const ConvWgradArgs& a, hipStream_t s);
+
+}  // namespace dtfe

@@ -1,0 +1,562 @@
+// Implicit-GEMM NHWC convolution for wide layers on gfx950 (see igemm.h).
+//
+// Main loop ("2-buffer glds" structure of the CDNA4 guide, §5): 4 waves, a
+// BM x BN output tile, 64-deep k-tiles.  Both operands of a k-tile are moved
+// HBM -> LDS by global_load_lds_dwordx4 (16 B per lane, no VGPR staging), tile
+// t+1 is in flight while the MFMAs of tile t run, one barrier per k-tile.
+//
+// LDS images are lane-linear (the DMA writes base + 16*lane), so the bank
+// swizzle is applied on the SOURCE address and undone on the fragment read:
+//   fwd/dgrad images [rows][64 k] (128-B rows): LDS slot s of row r holds
+//     logical 16-B chunk s ^ (r & 7)  -> the 16x16x32 A/B fragment reads
+//     (ds_read_b128, rows r..r+15 at one chunk) hit 16 distinct bank slots
+//   wgrad images [64 m][cols] read with ds_read_b64_tr_b16: 32-B segments of
+//     m-row k are XOR-ed by h(k) = (k & 3) | ((k >> 3) & 1) << 2 (256-B rows) or
+//     ((k >> 1) & 1) | ((k >> 3) & 1) << 1 (128-B rows): the 8 m-rows one
+//     32-lane half reads land on 8 distinct 32-B bank segments.
+// Out-of-image taps (padding) and rows past the end read a zero page.
+//
+// Replaces Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter of the ResNet-50
+// configuration (BASELINE.json config 5).
+#include "igemm.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+namespace dtfe {
+
+namespace {
+
+constexpr int IG_THREADS = 256;
+constexpr int IG_BK = 64;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void glds16(const void* g, bf16* lds_piece) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_piece, 16, 0, 0);
+}
+
+// exact m / d for 0 <= m < 2^24 through a float reciprocal
+__device__ __forceinline__ int qdiv(int m, int d, float inv_d) {
+  int q = (int)((float)m * inv_d);
+  const int r = m - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+// ------------------------------------------------------------ fwd / dgrad
+template <int BM, int BN>
+__global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int A_EL = BM * IG_BK, B_EL = BN * IG_BK;
+  constexpr int NA = BM / 32, NB = BN / 32;  // 1-KB glds pieces per thread and k-tile
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_n = a.N / BN;
+  const int id = xcd_remap(blockIdx.x, a.tiles_m * tiles_n);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const IgPhase& P = a.ph[blockIdx.z];
+  const int Mp = a.B * P.RH * P.RW;
+  const int m_base = tm * BM, n_base = tn * BN;
+  if (m_base >= Mp) return;
+
+  const int cpt = a.SC / IG_BK;
+  const int nk_all = P.ntaps * cpt;
+  const int kt0 = (int)((long)nk_all * blockIdx.y / a.splits);
+  const int nk = (int)((long)nk_all * (blockIdx.y + 1) / a.splits) - kt0;
+
+  // lane -> (row of an 8-row piece, logical 16-B chunk it fetches)
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
+  int a_pix[NA], a_iy[NA], a_ix[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int m = m_base + (j * 4 + w) * 8 + lrow;
+    a_pix[j] = 0;
+    a_iy[j] = -(1 << 20);
+    a_ix[j] = 0;
+    if (m < Mp) {
+      const int jx = m % P.RW, t = m / P.RW;
+      const int i = t % P.RH, b = t / P.RH;
+      a_pix[j] = b * a.SH * a.SW;
+      a_iy[j] = i * a.istr;
+      a_ix[j] = jx * a.istr;
+    }
+  }
+  const bf16* b_src[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) b_src[j] = a.w + (long)(n_base + (j * 4 + w) * 8 + lrow) * a.Ktot + lchunk * 8;
+
+  auto issue = [&](int kt, int buf) {
+    const int tap = kt / cpt, cb = kt - tap * cpt;
+    const int dy = P.dy[tap], dx = P.dx[tap];
+    const int woff = P.kt[tap] * a.SC + cb * IG_BK;
+    bf16* As = smem + buf * (A_EL + B_EL);
+    bf16* Bs = As + A_EL;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int sy = a_iy[j] + dy, sx = a_ix[j] + dx;
+      const bool ok = (unsigned)sy < (unsigned)a.SH && (unsigned)sx < (unsigned)a.SW;
+      const bf16* p = ok ? a.src + (long)(a_pix[j] + sy * a.SW + sx) * a.SC + cb * IG_BK + lchunk * 8 : a.zeros;
+      glds16(p, As + (j * 4 + w) * 512);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) glds16(b_src[j] + woff, Bs + (j * 4 + w) * 512);
+  };
+
+  const int wm = w >> 1, wn = w & 1;
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(kt0, 0);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nk) issue(kt0 + t + 1, (t + 1) & 1);
+    const bf16* As = smem + (t & 1) * (A_EL + B_EL);
+    const bf16* Bs = As + A_EL;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int pc = (kk * 4 + (lane >> 4)) ^ (lane & 7);
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(As + (wm * WM + i * 16 + (lane & 15)) * IG_BK + pc * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn * WN + j * 16 + (lane & 15)) * IG_BK + pc * 8);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  if (a.splits > 1) {
+    // fp32 partial tile (forward only: one phase, output row == m)
+    float* ws = a.ws + (long)blockIdx.y * Mp * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n_base + wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = m_base + wm * WM + i * 16 + (lane >> 4) * 4 + q;
+          if (m < Mp) ws[(long)m * a.N + col] = acc[i][j][q];
+        }
+      }
+    return;
+  }
+
+  // bf16 tile through LDS, then 16-B row-contiguous stores
+  constexpr int CLD = BN + 8;
+  static_assert(BM * CLD <= 2 * (A_EL + B_EL), "C tile fits the staging LDS");
+  __syncthreads();
+  bf16* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int q = tid; q < BM * CPR; q += IG_THREADS) {
+    const int r = q / CPR, c8 = q - r * CPR;
+    const int m = m_base + r;
+    if (m >= Mp) continue;
+    long opix = m;
+    if (a.nphase > 1) {
+      const int jx = m % P.RW, t = m / P.RW;
+      const int i = t % P.RH, b = t / P.RH;
+      opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
+    }
+    *reinterpret_cast<u32x4_t*>(a.out + opix * a.N + n_base + c8 * 8) =
+        *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c8 * 8);
+  }
+}
+
+// out[i] = bf16(sum_s ws[s][i])
+__global__ __launch_bounds__(256) void splitk_to_bf16_kernel(const float* __restrict__ ws, int splits, long len,
+                                                             bf16* __restrict__ out) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= len) return;
+  f32x4_t v = *reinterpret_cast<const f32x4_t*>(ws + i);
+  for (int s = 1; s < splits; ++s) v += *reinterpret_cast<const f32x4_t*>(ws + (long)s * len + i);
+  u32x2_t o = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+  *reinterpret_cast<u32x2_t*>(out + i) = o;
+}
+
+// ------------------------------------------------------------------ wgrad
+// swizzle (16-B chunk XOR) of m-row k in a [64][COLS] image
+template <int COLS> __device__ __forceinline__ int wg_swz(int k) {
+  if constexpr (COLS == 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
+
+// fragment of a [64 m][COLS] image for rows (output dims) rbase.., k = m rows kk..kk+31
+template <int COLS>
+__device__ __forceinline__ bf16x8_t wg_frag(const bf16* img, int rbase, int kk, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c = rbase + 4 * p;
+  const int k0 = kk + 8 * g + q, k1 = k0 + 4;
+  const bf16* p0 = img + k0 * COLS + (c ^ (wg_swz<COLS>(k0) * 8));
+  const bf16* p1 = img + k1 * COLS + (c ^ (wg_swz<COLS>(k1) * 8));
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p0));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p1));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int BM, int BN>  // BM output channels x BN input channels of one tap
+__global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgradArgs a, float* dw, float scale) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int A_EL = 64 * BM, B_EL = 64 * BN;
+  constexpr int CPA = BM / 8, RPA = 64 / CPA, NA = BM / 32;  // chunks per m-row, m-rows per piece
+  constexpr int CPB = BN / 8, RPB = 64 / CPB, NB = BN / 32;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cblocks = a.C / BN;
+  const int tiles_n = a.KH * a.KW * cblocks;
+  const int id = xcd_remap(blockIdx.x, (a.Cout / BM) * tiles_n);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int tap = tn / cblocks, cb = tn - tap * cblocks;
+  const int kh = tap / a.KW, kw = tap - kh * a.KW;
+  const int M = a.B * a.OH * a.OW;
+  const int m0 = blockIdx.y * a.mchunk, m1 = min(M, m0 + a.mchunk);
+  const int nk = (m1 - m0 + 63) / 64;
+  const float inv_ow = 1.f / (float)a.OW, inv_oh = 1.f / (float)a.OH;
+
+  // this lane's m-row within each piece and the logical chunk it fetches
+  int a_row[NA], a_chk[NA], b_row[NB], b_chk[NB];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    a_row[j] = (j * 4 + w) * RPA + lane / CPA;
+    a_chk[j] = (lane % CPA) ^ wg_swz<BM>(a_row[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    b_row[j] = (j * 4 + w) * RPB + lane / CPB;
+    b_chk[j] = (lane % CPB) ^ wg_swz<BN>(b_row[j]);
+  }
+  const bf16* dy_col = a.dy + tm * BM;
+  const bf16* x_col = a.x + cb * BN;
+
+  auto issue = [&](int t, int buf) {
+    bf16* As = smem + buf * (A_EL + B_EL);
+    bf16* Bs = As + A_EL;
+    const int mt = m0 + t * 64;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int m = mt + a_row[j];
+      const bf16* p = m < m1 ? dy_col + (long)m * a.Cout + a_chk[j] * 8 : a.zeros;
+      glds16(p, As + (j * 4 + w) * 512);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int m = mt + b_row[j];
+      const bf16* p = a.zeros;
+      if (m < m1) {
+        const int q1 = qdiv(m, a.OW, inv_ow);
+        const int ox = m - q1 * a.OW;
+        const int b = qdiv(q1, a.OH, inv_oh);
+        const int oy = q1 - b * a.OH;
+        const int sy = oy * a.stride - a.pad + kh, sx = ox * a.stride - a.pad + kw;
+        if ((unsigned)sy < (unsigned)a.H && (unsigned)sx < (unsigned)a.W)
+          p = x_col + ((long)(b * a.H + sy) * a.W + sx) * a.C + b_chk[j] * 8;
+      }
+      glds16(p, Bs + (j * 4 + w) * 512);
+    }
+  };
+
+  const int wm = w >> 1, wn = w & 1;
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+    const bf16* As = smem + (t & 1) * (A_EL + B_EL);
+    const bf16* Bs = As + A_EL;
+#pragma unroll
+    for (int kk = 0; kk < 64; kk += 32) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = wg_frag<BM>(As, wm * WM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = wg_frag<BN>(Bs, wn * WN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const int Kw = a.KH * a.KW * a.C;
+  const int col_base = tap * a.C + cb * BN + wn * WN;
+  const int row_base = tm * BM + wm * WM;
+  if (a.splits == 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float* d = dw + (long)(row_base + i * 16 + (lane >> 4) * 4 + q) * Kw + col_base + j * 16 + (lane & 15);
+          *d += scale * acc[i][j][q];
+        }
+    return;
+  }
+  float* ws = a.ws + (long)blockIdx.y * a.Cout * Kw;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ws[(long)(row_base + i * 16 + (lane >> 4) * 4 + q) * Kw + col_base + j * 16 + (lane & 15)] = acc[i][j][q];
+}
+
+// dw[i] += scale * sum_s ws[s][i]
+constexpr int WG_RCH = 8;
+__global__ __launch_bounds__(256) void wgrad_splits_reduce_kernel(const float* __restrict__ ws, int splits, long len,
+                                                                  float* dw, float scale) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= len) return;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + WG_RCH <= splits; s += WG_RCH) {
+    f32x4_t v[WG_RCH];
+#pragma unroll
+    for (int j = 0; j < WG_RCH; ++j) v[j] = *reinterpret_cast<const f32x4_t*>(ws + (long)(s + j) * len + i);
+#pragma unroll
+    for (int j = 0; j < WG_RCH; ++j) acc += v[j];
+  }
+  for (; s < splits; ++s) acc += *reinterpret_cast<const f32x4_t*>(ws + (long)s * len + i);
+  f32x4_t d = *reinterpret_cast<const f32x4_t*>(dw + i);
+  *reinterpret_cast<f32x4_t*>(dw + i) = d + scale * acc;
+}
+
+// ------------------------------------------------------------ host helpers
+struct DevScratch {
+  void* zeros = nullptr;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+};
+std::mutex g_mu;
+DevScratch g_dev[64];
+
+const bf16* zero_page(hipStream_t s) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_mu);
+  DevScratch& d = g_dev[dev];
+  if (!d.zeros) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &st);
+    if (st != hipStreamCaptureStatusNone) throw std::runtime_error("igemm: first use inside a graph capture");
+    if (hipMalloc(&d.zeros, 4096) != hipSuccess) throw std::runtime_error("igemm: zero page alloc");
+    if (hipMemset(d.zeros, 0, 4096) != hipSuccess) throw std::runtime_error("igemm: zero page memset");
+  }
+  return reinterpret_cast<const bf16*>(d.zeros);
+}
+
+float* workspace(size_t bytes, hipStream_t s) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_mu);
+  DevScratch& d = g_dev[dev];
+  if (d.ws_bytes < bytes) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &st);
+    if (st != hipStreamCaptureStatusNone)
+      throw std::runtime_error("igemm: workspace growth inside a graph capture (run the step eagerly first)");
+    if (d.ws) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(d.ws);
+    }
+    const size_t nb = std::max(bytes, d.ws_bytes * 3 / 2);
+    if (hipMalloc(&d.ws, nb) != hipSuccess) throw std::runtime_error("igemm: workspace alloc");
+    d.ws_bytes = nb;
+  }
+  return reinterpret_cast<float*>(d.ws);
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+struct Tile { int bm, bn; };
+
+// Largest tile that still gives >= ~one workgroup per CU; DTFE_IG_TILE=BMxBN overrides.
+Tile pick_tile(long M, int N, int nphase) {
+  const char* e = std::getenv("DTFE_IG_TILE");
+  if (e && *e) {
+    int bm = 0, bn = 0;
+    if (std::sscanf(e, "%dx%d", &bm, &bn) == 2 && (bm == 64 || bm == 128) && (bn == 64 || bn == 128) && N % bn == 0)
+      return {bm, bn};
+  }
+  const Tile cands[3] = {{128, 128}, {128, 64}, {64, 64}};
+  for (const Tile& t : cands) {
+    if (N % t.bn) continue;
+    const long blocks = ((M + t.bm - 1) / t.bm) * (N / t.bn) * nphase;
+    if (blocks >= 240) return t;
+  }
+  return {64, 64};
+}
+
+template <int BM, int BN>
+void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
+  a.tiles_m = (int)((Mmax + BM - 1) / BM);
+  dim3 grid(a.tiles_m * (a.N / BN), a.splits, a.nphase);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN>), grid, dim3(IG_THREADS), 0, s, a);
+}
+
+void run_igemm(IgemmArgs& a, hipStream_t s) {
+  long Mmax = 0;
+  for (int p = 0; p < a.nphase; ++p) Mmax = std::max(Mmax, (long)a.B * a.ph[p].RH * a.ph[p].RW);
+  Tile t = pick_tile(Mmax, a.N, a.nphase);
+  a.zeros = zero_page(s);
+  a.splits = 1;
+  a.ws = nullptr;
+  if (a.nphase == 1 && a.ostr == 1) {
+    // split-K when even the smallest tile leaves CUs idle and the k-loop is long
+    const long blocks = ((Mmax + t.bm - 1) / t.bm) * (a.N / t.bn);
+    const int nk = a.ph[0].ntaps * (a.SC / IG_BK);
+    int sp = env_int("DTFE_IG_SPLIT", 0);
+    if (sp <= 0) {
+      sp = 1;
+      while (blocks * sp < 400 && nk / (sp * 2) >= 6) sp *= 2;
+    }
+    sp = std::max(1, std::min(sp, nk));
+    if (sp > 1) {
+      a.splits = sp;
+      a.ws = workspace((size_t)sp * Mmax * a.N * sizeof(float), s);
+    }
+  }
+  if (t.bm == 128 && t.bn == 128) launch_ig<128, 128>(a, Mmax, s);
+  else if (t.bm == 128 && t.bn == 64) launch_ig<128, 64>(a, Mmax, s);
+  else if (t.bm == 64 && t.bn == 128) launch_ig<64, 128>(a, Mmax, s);
+  else launch_ig<64, 64>(a, Mmax, s);
+  if (a.splits > 1) {
+    const long len = Mmax * a.N;
+    hipLaunchKernelGGL(splitk_to_bf16_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws,
+                       a.splits, len, a.out);
+  }
+}
+
+}  // namespace
+
+bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s) {
+  const ConvGeom& g = f.g;
+  if (g.C % IG_BK || g.Cout % 64 || g.KH * g.KW > IG_MAX_TAPS || g.pool_order || f.bias || f.act != 0) return false;
+  if (env_int("DTFE_IG_OFF", 0)) return false;
+  IgemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.src = f.x; a.w = f.w; a.out = f.y;
+  a.B = g.B; a.SH = g.H; a.SW = g.W; a.SC = g.C;
+  a.N = g.Cout; a.Ktot = g.KH * g.KW * g.C;
+  a.istr = g.stride; a.OHf = g.OH; a.OWf = g.OW; a.ostr = 1;
+  a.nphase = 1;
+  IgPhase& P = a.ph[0];
+  P.RH = g.OH; P.RW = g.OW; P.oy = P.ox = 0;
+  P.ntaps = g.KH * g.KW;
+  for (int kh = 0; kh < g.KH; ++kh)
+    for (int kw = 0; kw < g.KW; ++kw) {
+      const int t = kh * g.KW + kw;
+      P.dy[t] = kh - g.pad; P.dx[t] = kw - g.pad; P.kt[t] = t;
+    }
+  run_igemm(a, s);
+  return true;
+}
+
+bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
+  const ConvGeom& g = d.g;
+  if (g.Cout % IG_BK || g.C % 64 || g.KH * g.KW > IG_MAX_TAPS || g.stride > 2 || d.unpool || d.relu_mask) return false;
+  if (env_int("DTFE_IG_OFF", 0)) return false;
+  IgemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.src = d.dy; a.w = d.wt; a.out = d.dx;
+  a.B = g.B; a.SH = g.OH; a.SW = g.OW; a.SC = g.Cout;
+  a.N = g.C; a.Ktot = g.KH * g.KW * g.Cout;
+  a.istr = 1; a.OHf = g.H; a.OWf = g.W; a.ostr = g.stride;
+  const int st = g.stride;
+  a.nphase = st * st;
+  for (int py = 0; py < st; ++py)
+    for (int px = 0; px < st; ++px) {
+      IgPhase& P = a.ph[py * st + px];
+      P.oy = py; P.ox = px;
+      P.RH = (g.H - py + st - 1) / st;
+      P.RW = (g.W - px + st - 1) / st;
+      P.ntaps = 0;
+      // dX[i*s+py][j*s+px] += dY[i + (py+pad-kh)/s][j + (px+pad-kw)/s] . W[kh][kw]  for exact divisions
+      for (int kh = 0; kh < g.KH; ++kh) {
+        const int ty = py + g.pad - kh;
+        if (((ty % st) + st) % st) continue;
+        for (int kw = 0; kw < g.KW; ++kw) {
+          const int tx = px + g.pad - kw;
+          if (((tx % st) + st) % st) continue;
+          P.dy[P.ntaps] = ty / st; P.dx[P.ntaps] = tx / st; P.kt[P.ntaps] = kh * g.KW + kw;
+          ++P.ntaps;
+        }
+      }
+    }
+  run_igemm(a, s);
+  return true;
+}
+
+bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
+  const ConvGeom& g = f.g;
+  if (g.C % 64 || g.Cout % 64 || f.db || g.pool_order) return false;
+  if (env_int("DTFE_IG_OFF", 0)) return false;
+  IgWgradArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.dy = f.dz; a.x = f.x;
+  a.B = g.B; a.H = g.H; a.W = g.W; a.C = g.C; a.OH = g.OH; a.OW = g.OW; a.Cout = g.Cout;
+  a.KH = g.KH; a.KW = g.KW; a.stride = g.stride; a.pad = g.pad;
+  a.zeros = zero_page(s);
+  const int bm = g.Cout % 128 == 0 ? 128 : 64, bn = g.C % 128 == 0 ? 128 : 64;
+  const long tiles = (long)(g.Cout / bm) * g.KH * g.KW * (g.C / bn);
+  const long M = (long)g.B * g.OH * g.OW;
+  int sp = env_int("DTFE_IG_WSPLIT", 0);
+  if (sp <= 0) sp = (int)std::max(1L, std::min((768 + tiles - 1) / tiles, (M + 255) / 256));
+  long mchunk = (M + sp - 1) / sp;
+  mchunk = (mchunk + 63) / 64 * 64;
+  sp = (int)((M + mchunk - 1) / mchunk);
+  a.splits = sp;
+  a.mchunk = (int)mchunk;
+  const long len = (long)g.Cout * g.KH * g.KW * g.C;
+  if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s);
+  dim3 grid((unsigned)tiles, sp);
+  if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else if (bm == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else if (bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<64, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else hipLaunchKernelGGL((igemm_wgrad_kernel<64, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  if (sp > 1)
+    hipLaunchKernelGGL(wgrad_splits_reduce_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws, sp,
+                       len, f.dw, f.scale);
+  return true;
+}
+
+}  // namespace dtfe
