@@ -490,11 +490,15 @@ void bn_apply(const Tensor& x, const Tensor& stats, const Tensor& gamma, const T
 }
 
 void bn_bwd_stats(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
-                  const Tensor& invstd, const Tensor& stats, int64_t act) {
+                  const Tensor& invstd, const Tensor& stats, int64_t act, const optional<Tensor>& gamma,
+                  const optional<Tensor>& beta) {
   dtfe::BnArgs a = bn_common(x, stats, act);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
   a.y = ptr_or_null<dtfe::bf16>(y);
-  TORCH_CHECK(act == 0 || a.y, "bn_bwd: the activation gradient needs the forward output");
+  a.gamma = ptr_or_null<float>(gamma);
+  a.beta = ptr_or_null<float>(beta);
+  TORCH_CHECK(act == 0 || a.y || (act == 1 && a.gamma && a.beta),
+              "bn_bwd: the activation gradient needs the forward output (or, for ReLU, gamma and beta)");
   a.mean = mean.data_ptr<float>();
   a.invstd = invstd.data_ptr<float>();
   dtfe::launch_bn_bwd_stats(a, cur_stream());
@@ -502,11 +506,14 @@ void bn_bwd_stats(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, 
 
 void bn_bwd_apply(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                   const Tensor& invstd, const Tensor& gamma, const Tensor& stats, int64_t act, const Tensor& dx,
-                  const optional<Tensor>& dres, const optional<Tensor>& dgamma, const optional<Tensor>& dbeta) {
+                  const optional<Tensor>& dres, const optional<Tensor>& dgamma, const optional<Tensor>& dbeta,
+                  const optional<Tensor>& beta) {
   dtfe::BnArgs a = bn_common(x, stats, act);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
   a.y = ptr_or_null<dtfe::bf16>(y);
-  TORCH_CHECK(act == 0 || a.y, "bn_bwd: the activation gradient needs the forward output");
+  a.beta = ptr_or_null<float>(beta);
+  TORCH_CHECK(act == 0 || a.y || (act == 1 && a.beta),
+              "bn_bwd: the activation gradient needs the forward output (or, for ReLU, beta)");
   a.mean = mean.data_ptr<float>();
   a.invstd = invstd.data_ptr<float>();
   a.gamma = gamma.data_ptr<float>();
@@ -555,9 +562,10 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
         " int rstride, int OH, int OW, Tensor(e!) out) -> ()");
-  m.def("bn_bwd_stats(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) stats, int act) -> ()");
+  m.def("bn_bwd_stats(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) stats, int act,"
+        " Tensor? gamma=None, Tensor? beta=None) -> ()");
   m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor stats,"
-        " int act, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta) -> ()");
+        " int act, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, Tensor? beta=None) -> ()");
   m.def("shortcut_grad_add(Tensor g, Tensor(a!) dx, int stride) -> ()");
   m.def("gap_fwd(Tensor x, Tensor(a!) y) -> ()");
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx) -> ()");

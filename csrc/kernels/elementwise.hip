@@ -40,32 +40,41 @@ __device__ __forceinline__ void load8(const void* src, int dt, long off, float (
   }
 }
 
-// one wave per batch row, 8 elements per lane per iteration
+__device__ __forceinline__ long gather_src_row(const GatherArgs& a, int b, int64_t step) {
+  if (a.idx) return a.idx[b];
+  return (long)(hash_u32(a.seed, (uint64_t)step * a.B + b) % (uint32_t)a.n_rows);
+}
+
+// D % 8 == 0: the batch is flattened into 8-element items (row b, chunk d) spread over the whole
+// grid, so a few long rows (224x224x3 images) still fill every CU; otherwise one wave per row.
 __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
   const int64_t step = a.counter ? *a.counter : 0;
-  const int lane = threadIdx.x & 63;
-  const bool vec = (a.D % 8) == 0;
-  for (int b = blockIdx.x * 4 + (threadIdx.x >> 6); b < a.B; b += gridDim.x * 4) {
-    long r;
-    if (a.idx) r = a.idx[b];
-    else r = (long)(hash_u32(a.seed, (uint64_t)step * a.B + b) % (uint32_t)a.n_rows);
-    if (a.labels_dst && lane == 0) a.labels_dst[b] = a.labels_src[r];
-    if (vec) {
-      for (int d = lane * 8; d < a.D; d += 64 * 8) {
-        float v[8];
-        load8(a.src, a.src_dtype, r * a.D + d, v);
-        const long o = (long)b * a.D + d;
-        if (a.dst_dtype == 1) {
-          f32x4_t* q = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.dst) + o);
-          q[0] = f32x4_t{v[0], v[1], v[2], v[3]};
-          q[1] = f32x4_t{v[4], v[5], v[6], v[7]};
-        } else {
-          *reinterpret_cast<u32x4_t*>(reinterpret_cast<bf16*>(a.dst) + o) =
-              u32x4_t{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                      pack_bf16x2(v[6], v[7])};
-        }
+  if ((a.D % 8) == 0) {
+    const int cpr = a.D / 8;
+    const long n = (long)a.B * cpr;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+      const int b = (int)(i / cpr);
+      const int d = (int)(i - (long)b * cpr) * 8;
+      const long r = gather_src_row(a, b, step);
+      if (a.labels_dst && d == 0) a.labels_dst[b] = a.labels_src[r];
+      float v[8];
+      load8(a.src, a.src_dtype, r * a.D + d, v);
+      const long o = (long)b * a.D + d;
+      if (a.dst_dtype == 1) {
+        f32x4_t* q = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.dst) + o);
+        q[0] = f32x4_t{v[0], v[1], v[2], v[3]};
+        q[1] = f32x4_t{v[4], v[5], v[6], v[7]};
+      } else {
+        *reinterpret_cast<u32x4_t*>(reinterpret_cast<bf16*>(a.dst) + o) =
+            u32x4_t{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                    pack_bf16x2(v[6], v[7])};
       }
-    } else {
+    }
+  } else {
+    const int lane = threadIdx.x & 63;
+    for (int b = blockIdx.x * 4 + (threadIdx.x >> 6); b < a.B; b += gridDim.x * 4) {
+      const long r = gather_src_row(a, b, step);
+      if (a.labels_dst && lane == 0) a.labels_dst[b] = a.labels_src[r];
       for (int d = lane; d < a.D; d += 64) {
         float v;
         if (a.src_dtype == 0) v = reinterpret_cast<const uint8_t*>(a.src)[r * a.D + d] * (1.f / 255.f);
@@ -80,8 +89,9 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
 }
 
 void launch_gather_rows(const GatherArgs& a, hipStream_t s) {
-  int blocks = (a.B + 3) / 4;
-  if (blocks > 1024) blocks = 1024;
+  long blocks = (a.D % 8) == 0 ? ((long)a.B * (a.D / 8) + 255) / 256 : (a.B + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
 

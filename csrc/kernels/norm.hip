@@ -62,21 +62,39 @@ __device__ void reduce_stats(const float (&s)[8], const float (&q)[8], int C, fl
   }
 }
 
+// Every row loop below keeps U independent 16-B loads in flight per thread (all
+// issued before any of them is consumed): the kernels are HBM-latency bound
+// otherwise (one outstanding load per thread ~ 1 KB per wave).
+constexpr int U_STATS = 8, U_APPLY = 4;
+
+__device__ __forceinline__ u32x4_t ld16(const bf16* p) { return *reinterpret_cast<const u32x4_t*>(p); }
+
 // Statistics are accumulated around a per-channel shift K = x[row 0][c] (sum (x-K), sum (x-K)^2):
 // the one-pass E[x^2] - E[x]^2 form loses the variance to cancellation when |mean| >> std.
+// Rows past the end re-read row 0 (= K), which contributes exactly zero.
 __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   const Slots S(a.C);
   float k[8];
-  unpack8(*reinterpret_cast<const u32x4_t*>(a.x + S.chunk * 8), k);
+  unpack8(ld16(a.x + S.chunk * 8), k);
   float s[8] = {}, q[8] = {};
-  for (long r = (long)blockIdx.x * S.rpp + S.slot; r < a.R; r += (long)gridDim.x * S.rpp) {
-    float f[8];
-    unpack8(*reinterpret_cast<const u32x4_t*>(a.x + r * a.C + S.chunk * 8), f);
+  const long step = (long)gridDim.x * S.rpp * U_STATS;
+  for (long r0 = (long)blockIdx.x * S.rpp * U_STATS + S.slot; r0 < a.R; r0 += step) {
+    u32x4_t v[U_STATS];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = f[e] - k[e];
-      s[e] += d;
-      q[e] += d * d;
+    for (int u = 0; u < U_STATS; ++u) {
+      const long r = r0 + (long)u * S.rpp;
+      v[u] = ld16(a.x + (r < a.R ? r : 0) * a.C + S.chunk * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U_STATS; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = f[e] - k[e];
+        s[e] += d;
+        q[e] += d * d;
+      }
     }
   }
   reduce_stats(s, q, a.C, a.stats);
@@ -88,6 +106,13 @@ __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean,
   mean = bf2f(a.x[c]) + d;
   const float var = fmaxf(a.stats[a.C + c] * inv_r - d * d, 0.f);
   invstd = rsqrtf(var + a.eps);
+}
+
+__device__ __forceinline__ long res_offset(const BnArgs& a, long r, int chunk, bool identity) {
+  if (identity) return r * a.C + chunk * 8;
+  const long hw = (long)a.OH * a.OW, b = r / hw;
+  const int p = (int)(r - b * hw), oy = p / a.OW, ox = p - oy * a.OW;
+  return ((b * a.RH + (long)oy * a.rstride) * a.RW + (long)ox * a.rstride) * a.RC + chunk * 8;
 }
 
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
@@ -117,37 +142,66 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
   }
   const bool res_identity = a.res && a.rstride == 1 && a.RC == a.C && a.RH == a.OH && a.RW == a.OW;
   const bool res_chunk = a.res && S.chunk * 8 < a.RC;
-  for (long r = (long)blockIdx.x * S.rpp + S.slot; r < a.R; r += (long)gridDim.x * S.rpp) {
-    float f[8];
-    unpack8(*reinterpret_cast<const u32x4_t*>(a.x + r * a.C + S.chunk * 8), f);
+  const long step = (long)gridDim.x * S.rpp * U_APPLY;
+  for (long r0 = (long)blockIdx.x * S.rpp * U_APPLY + S.slot; r0 < a.R; r0 += step) {
+    u32x4_t v[U_APPLY], w[U_APPLY];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = f[e] * scale[e] + shift[e];
-    if (res_chunk) {
-      long ro;
-      if (res_identity) {
-        ro = r * a.C + S.chunk * 8;
-      } else {
-        const long hw = (long)a.OH * a.OW, b = r / hw;
-        const int p = (int)(r - b * hw), oy = p / a.OW, ox = p - oy * a.OW;
-        ro = ((b * a.RH + (long)oy * a.rstride) * a.RW + (long)ox * a.rstride) * a.RC + S.chunk * 8;
-      }
-      float g[8];
-      unpack8(*reinterpret_cast<const u32x4_t*>(a.res + ro), g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += g[e];
+    for (int u = 0; u < U_APPLY; ++u) {
+      const long r = r0 + (long)u * S.rpp;
+      const long rr = r < a.R ? r : 0;
+      v[u] = ld16(a.x + rr * a.C + S.chunk * 8);
+      if (res_chunk) w[u] = ld16(a.res + res_offset(a, rr, S.chunk, res_identity));
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e], a.act);
-    *reinterpret_cast<u32x4_t*>(a.out + r * a.C + S.chunk * 8) = pack8(f);
+    for (int u = 0; u < U_APPLY; ++u) {
+      const long r = r0 + (long)u * S.rpp;
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * scale[e] + shift[e];
+      if (res_chunk) {
+        float g[8];
+        unpack8(w[u], g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += g[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e], a.act);
+      if (r < a.R) *reinterpret_cast<u32x4_t*>(a.out + r * a.C + S.chunk * 8) = pack8(f);
+    }
   }
 }
 
-// g = dy * act'(y) for 8 channels
-__device__ __forceinline__ void masked_grad(const BnArgs& a, long off, float (&g)[8]) {
-  unpack8(*reinterpret_cast<const u32x4_t*>(a.dy + off), g);
-  if (a.act != ACT_NONE) {
+// Backward activation mask source.  With a.y the mask is act'(y) of the stored output; with
+// a.y == nullptr and act == ReLU (no residual was added in the forward) it is recomputed from
+// x as (gamma*invstd*x + (beta - mean*gamma*invstd)) > 0 - bit-identical to the forward's
+// pre-activation (same fma on the same saved statistics) and one tensor read cheaper.
+struct BwdMask {
+  float scale[8], shift[8];
+  bool from_x;
+  __device__ BwdMask(const BnArgs& a, int chunk) {
+    from_x = a.y == nullptr && a.act == ACT_RELU;
+    if (from_x) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = chunk * 8 + e;
+        scale[e] = a.gamma[c] * a.invstd[c];
+        shift[e] = a.beta[c] - a.mean[c] * scale[e];
+      }
+    }
+  }
+};
+
+// g = dy * act'(.) for 8 channels, from loaded dy / y / x chunks
+__device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, const u32x4_t dyv, const u32x4_t yv,
+                                            const float (&x)[8], float (&g)[8]) {
+  unpack8(dyv, g);
+  if (M.from_x) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (x[e] * M.scale[e] + M.shift[e]) > 0.f ? g[e] : 0.f;
+  } else if (a.act != ACT_NONE) {
     float y[8];
-    unpack8(*reinterpret_cast<const u32x4_t*>(a.y + off), y);
+    unpack8(yv, y);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] *= act_grad_from_out(y[e], a.act);
   }
@@ -155,6 +209,8 @@ __device__ __forceinline__ void masked_grad(const BnArgs& a, long off, float (&g
 
 __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   const Slots S(a.C);
+  const BwdMask M(a, S.chunk);
+  const bool need_y = a.act != ACT_NONE && !M.from_x;
   float mean[8], invstd[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -162,15 +218,29 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
     invstd[e] = a.invstd[S.chunk * 8 + e];
   }
   float s[8] = {}, q[8] = {};
-  for (long r = (long)blockIdx.x * S.rpp + S.slot; r < a.R; r += (long)gridDim.x * S.rpp) {
-    const long off = r * a.C + S.chunk * 8;
-    float g[8], x[8];
-    masked_grad(a, off, g);
-    unpack8(*reinterpret_cast<const u32x4_t*>(a.x + off), x);
+  const long step = (long)gridDim.x * S.rpp * U_STATS;
+  for (long r0 = (long)blockIdx.x * S.rpp * U_STATS + S.slot; r0 < a.R; r0 += step) {
+    u32x4_t dv[U_STATS], xv[U_STATS], yv[U_STATS];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s[e] += g[e];
-      q[e] += g[e] * (x[e] - mean[e]) * invstd[e];
+    for (int u = 0; u < U_STATS; ++u) {
+      const long r = r0 + (long)u * S.rpp;
+      const long off = (r < a.R ? r : 0) * a.C + S.chunk * 8;
+      dv[u] = ld16(a.dy + off);
+      xv[u] = ld16(a.x + off);
+      if (need_y) yv[u] = ld16(a.y + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U_STATS; ++u) {
+      const float live = (r0 + (long)u * S.rpp) < a.R ? 1.f : 0.f;
+      float g[8], x[8];
+      unpack8(xv[u], x);
+      masked_grad(a, M, dv[u], yv[u], x, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gl = g[e] * live;
+        s[e] += gl;
+        q[e] += gl * (x[e] - mean[e]) * invstd[e];
+      }
     }
   }
   reduce_stats(s, q, a.C, a.stats);
@@ -184,6 +254,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
       if (a.dgamma) a.dgamma[c] += a.stats[a.C + c];
     }
   }
+  const BwdMask M(a, S.chunk);
+  const bool need_y = a.act != ACT_NONE && !M.from_x;
   const float inv_r = 1.f / (float)a.R;
   float mean[8], invstd[8], k[8], sg[8], sgx[8];
 #pragma unroll
@@ -195,29 +267,50 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
     sg[e] = a.stats[c] * inv_r;
     sgx[e] = a.stats[a.C + c] * inv_r;
   }
-  for (long r = (long)blockIdx.x * S.rpp + S.slot; r < a.R; r += (long)gridDim.x * S.rpp) {
-    const long off = r * a.C + S.chunk * 8;
-    float g[8], x[8], dx[8];
-    masked_grad(a, off, g);
-    unpack8(*reinterpret_cast<const u32x4_t*>(a.x + off), x);
+  const long step = (long)gridDim.x * S.rpp * U_APPLY;
+  for (long r0 = (long)blockIdx.x * S.rpp * U_APPLY + S.slot; r0 < a.R; r0 += step) {
+    u32x4_t dv[U_APPLY], xv[U_APPLY], yv[U_APPLY];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float xh = (x[e] - mean[e]) * invstd[e];
-      dx[e] = k[e] * (g[e] - sg[e] - xh * sgx[e]);
+    for (int u = 0; u < U_APPLY; ++u) {
+      const long r = r0 + (long)u * S.rpp;
+      const long off = (r < a.R ? r : 0) * a.C + S.chunk * 8;
+      dv[u] = ld16(a.dy + off);
+      xv[u] = ld16(a.x + off);
+      if (need_y) yv[u] = ld16(a.y + off);
     }
-    *reinterpret_cast<u32x4_t*>(a.out + off) = pack8(dx);
-    if (a.dres) *reinterpret_cast<u32x4_t*>(a.dres + off) = pack8(g);
+#pragma unroll
+    for (int u = 0; u < U_APPLY; ++u) {
+      const long r = r0 + (long)u * S.rpp;
+      if (r >= a.R) continue;
+      const long off = r * a.C + S.chunk * 8;
+      float g[8], x[8], dx[8];
+      unpack8(xv[u], x);
+      masked_grad(a, M, dv[u], yv[u], x, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (x[e] - mean[e]) * invstd[e];
+        dx[e] = k[e] * (g[e] - sg[e] - xh * sgx[e]);
+      }
+      *reinterpret_cast<u32x4_t*>(a.out + off) = pack8(dx);
+      if (a.dres) *reinterpret_cast<u32x4_t*>(a.dres + off) = pack8(g);
+    }
   }
 }
 
-// workgroups for R rows: `per_thread` rows per thread, at most max_blocks.  The statistics
-// kernels use 8 rows per thread (fewer workgroups -> fewer contended per-channel atomics),
-// the apply kernels 2 (no atomics: as many workgroups as fill the chip).
-int grid_for(long R, int C, int max_blocks, int per_thread) {
-  const int rpp = NT / (C / 8);
-  long rows_per_block = (long)rpp * per_thread;
+// Statistics kernels: few enough workgroups that the per-channel atomics stay cheap
+// (about 2 per CU), each looping over U_STATS-row batches.  Apply kernels: one U_APPLY-row
+// batch per thread, as many workgroups as that takes (no atomics to amortise).
+int stats_grid(long R, int C) {
+  const long rows_per_block = (long)(NT / (C / 8)) * U_STATS;
   long g = (R + rows_per_block - 1) / rows_per_block;
-  if (g > max_blocks) g = max_blocks;
+  if (g > 512) g = 512;
+  return g < 1 ? 1 : (int)g;
+}
+
+int apply_grid(long R, int C) {
+  const long rows_per_block = (long)(NT / (C / 8)) * U_APPLY;
+  long g = (R + rows_per_block - 1) / rows_per_block;
+  if (g > (1L << 20)) g = 1L << 20;
   return g < 1 ? 1 : (int)g;
 }
 
@@ -286,53 +379,84 @@ __global__ void gap_bwd_kernel(const bf16* dy, bf16* dx, int B, int HW, int C) {
   }
 }
 
-__global__ void maxpool3_fwd_kernel(const bf16* x, bf16* y, uint8_t* am, int B, int H, int W, int C, int OH,
-                                    int OW) {
-  const long n = (long)B * OH * OW * C;
+// 3x3/s2/p1 max pool, one thread per (output pixel, 8-channel chunk): 16-B loads of every tap,
+// argmax (tap 0..8, first max wins) packed 8 bytes per chunk.
+__global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const bf16* x, bf16* y, uint8_t* am, int B, int H, int W,
+                                                           int C, int OH, int OW) {
+  const int cpr = C / 8;
+  const long n = (long)B * OH * OW * cpr;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long row = i / C;
+    const long row = i / cpr;
+    const int ch = (int)(i - row * cpr) * 8;
     const long hw = (long)OH * OW, b = row / hw;
     const int p = (int)(row - b * hw), oy = p / OW, ox = p - oy * OW;
-    float best = -3.0e38f;
-    int arg = 0;
+    u32x4_t v[9];
+    bool ok[9];
+#pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int iy = oy * 2 - 1 + t / 3, ix = ox * 2 - 1 + t % 3;
-      if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
-      const float v = bf2f(x[((b * H + iy) * W + ix) * C + c]);
-      if (v > best) { best = v; arg = t; }
+      ok[t] = iy >= 0 && iy < H && ix >= 0 && ix < W;
+      if (ok[t]) v[t] = ld16(x + ((b * H + iy) * W + ix) * C + ch);
     }
-    y[i] = f2bf(best);
-    am[i] = (uint8_t)arg;
+    float best[8];
+    uint32_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -3.0e38f; arg[e] = 0; }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!ok[t]) continue;
+      float f[8];
+      unpack8(v[t], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (f[e] > best[e]) { best[e] = f[e]; arg[e] = t; }
+    }
+    *reinterpret_cast<u32x4_t*>(y + row * C + ch) = pack8(best);
+    u32x2_t packed = {arg[0] | arg[1] << 8 | arg[2] << 16 | arg[3] << 24, arg[4] | arg[5] << 8 | arg[6] << 16 | arg[7] << 24};
+    *reinterpret_cast<u32x2_t*>(am + row * C + ch) = packed;
   }
 }
 
-__global__ void maxpool3_bwd_kernel(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH,
-                                    int OW) {
-  const long n = (long)B * H * W * C;
+// one thread per (input pixel, 8-channel chunk): sums dy over the (at most 2x2) windows whose
+// argmax is this pixel
+__global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H,
+                                                           int W, int C, int OH, int OW) {
+  const int cpr = C / 8;
+  const long n = (long)B * H * W * cpr;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long row = i / C;
+    const long row = i / cpr;
+    const int ch = (int)(i - row * cpr) * 8;
     const long hw = (long)H * W, b = row / hw;
     const int p = (int)(row - b * hw), iy = p / W, ix = p - iy * W;
-    float g = 0.f;
-    // outputs whose window (oy*2-1 .. oy*2+1) covers iy
-    for (int oy = (iy + 1) / 2 - 1; oy <= (iy + 1) / 2; ++oy) {
+    float g[8] = {};
+    const int oy0 = (iy + 1) / 2 - 1, ox0 = (ix + 1) / 2 - 1;
+#pragma unroll
+    for (int dyo = 0; dyo < 2; ++dyo) {
+      const int oy = oy0 + dyo;
       if (oy < 0 || oy >= OH || iy < oy * 2 - 1 || iy > oy * 2 + 1) continue;
-      for (int ox = (ix + 1) / 2 - 1; ox <= (ix + 1) / 2; ++ox) {
+#pragma unroll
+      for (int dxo = 0; dxo < 2; ++dxo) {
+        const int ox = ox0 + dxo;
         if (ox < 0 || ox >= OW || ix < ox * 2 - 1 || ix > ox * 2 + 1) continue;
-        const long o = ((b * OH + oy) * OW + ox) * C + c;
-        const int t = (iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1));
-        if (am[o] == t) g += bf2f(dy[o]);
+        const long o = ((b * OH + oy) * OW + ox) * C + ch;
+        const uint32_t t = (uint32_t)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
+        const u32x2_t m = *reinterpret_cast<const u32x2_t*>(am + o);
+        float d[8];
+        unpack8(ld16(dy + o), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ae = ((e < 4 ? m[0] : m[1]) >> (8 * (e & 3))) & 0xffu;
+          if (ae == t) g[e] += d[e];
+        }
       }
     }
-    dx[i] = f2bf(g);
+    *reinterpret_cast<u32x4_t*>(dx + row * C + ch) = pack8(g);
   }
 }
 
 int ew_grid(long n) {
   long g = (n + 255) / 256;
-  if (g > 4096) g = 4096;
+  if (g > 65536) g = 65536;
   return g < 1 ? 1 : (int)g;
 }
 
@@ -341,24 +465,30 @@ int ew_grid(long n) {
 void launch_bn_stats(const BnArgs& a, hipStream_t s) {
   check(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(grid_for(a.R, a.C, 1024, 8)), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(stats_grid(a.R, a.C)), dim3(NT), lds, s, a);
 }
 
 void launch_bn_apply(const BnArgs& a, hipStream_t s) {
   check(a);
   if (a.res && (a.RC % 8 || a.RC > a.C)) throw std::runtime_error("bn_apply: residual channels");
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(a.R, a.C, 2048, 2)), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(a.R, a.C)), dim3(NT), 0, s, a);
+}
+
+void check_bwd(const BnArgs& a) {
+  check(a);
+  if (a.act != ACT_NONE && !a.y && (a.act != ACT_RELU || !a.gamma || !a.beta))
+    throw std::runtime_error("bn_bwd: the activation mask needs y, or (ReLU) gamma and beta");
 }
 
 void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s) {
-  check(a);
+  check_bwd(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(grid_for(a.R, a.C, 1024, 8)), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(stats_grid(a.R, a.C)), dim3(NT), lds, s, a);
 }
 
 void launch_bn_bwd_apply(const BnArgs& a, hipStream_t s) {
-  check(a);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(a.R, a.C, 2048, 2)), dim3(NT), 0, s, a);
+  check_bwd(a);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(apply_grid(a.R, a.C)), dim3(NT), 0, s, a);
 }
 
 void launch_shortcut_grad_add(const bf16* g, bf16* dx, int B, int OH, int OW, int C, int XH, int XW, int XC,
@@ -381,14 +511,16 @@ void launch_gap_bwd(const bf16* dy, bf16* dx, int B, int HW, int C, hipStream_t 
 
 void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int W, int C, int OH, int OW,
                          hipStream_t s) {
-  hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(ew_grid((long)B * OH * OW * C)), dim3(256), 0, s, x, y, am, B, H, W,
-                     C, OH, OW);
+  if (C % 8) throw std::runtime_error("maxpool3: C % 8");
+  hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(ew_grid((long)B * OH * OW * C / 8)), dim3(256), 0, s, x, y, am, B, H,
+                     W, C, OH, OW);
 }
 
 void launch_maxpool3_bwd(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH, int OW,
                          hipStream_t s) {
-  hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(ew_grid((long)B * H * W * C)), dim3(256), 0, s, dy, am, dx, B, H, W,
-                     C, OH, OW);
+  if (C % 8) throw std::runtime_error("maxpool3: C % 8");
+  hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(ew_grid((long)B * H * W * C / 8)), dim3(256), 0, s, dy, am, dx, B, H,
+                     W, C, OH, OW);
 }
 
 }  // namespace dtfe

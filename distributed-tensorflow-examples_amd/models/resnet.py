@@ -162,6 +162,8 @@ class BN:
 
     def fwd(self, x, act=ops.ACT_RELU, res=None, rstride=1):
         P = self.P
+        # backward recomputes the ReLU mask from x unless a shortcut was added before the ReLU
+        self.mask_from_x = act == ops.ACT_RELU and res is None
         ops.bn_stats(x, self.stats)
         ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
                      invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
@@ -170,10 +172,12 @@ class BN:
 
     def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None):
         P = self.P
-        y = self.y if act != ops.ACT_NONE else None
-        ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act)
+        from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
+        y = self.y if act != ops.ACT_NONE and not from_x else None
+        beta = P.view(self.beta) if from_x else None
+        ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta)
         ops.bn_bwd_apply(dy, y, x, self.mean, self.invstd, P.view(self.gamma), self.dstats, dx, act=act, dres=dres,
-                         dgamma=P.gview(self.gamma), dbeta=P.gview(self.beta))
+                         dgamma=P.gview(self.gamma), dbeta=P.gview(self.beta), beta=beta)
 
 
 class Arena:

@@ -611,31 +611,38 @@ def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=
     return out
 
 
-def _masked_grad(dy, y, act):
+def _masked_grad(dy, y, act, x=None, mean=None, invstd=None, gamma=None, beta=None):
     g = _rows(dy)
     if act != ACT_NONE:
+        if y is None:  # ReLU mask recomputed from the pre-normalisation input (no residual in the forward)
+            scale = gamma.float() * invstd
+            pre = _rows(x) * scale + (beta.float() - mean * scale)
+            return g * (pre > 0)
         g = g * _act_grad_from_out_ref(_rows(y), act)
     return g
 
 
-def bn_bwd_stats(dy, y, x, mean, invstd, stats, act=ACT_RELU):
+def bn_bwd_stats(dy, y, x, mean, invstd, stats, act=ACT_RELU, gamma=None, beta=None):
+    """stats += (sum g, sum g*xhat), g = dy*act'(y).  With y=None and act=ReLU the mask is
+    recomputed from x (the forward had no residual add): pass gamma and beta."""
     if x.is_cuda:
-        require().bn_bwd_stats(dy, y, x, mean, invstd, stats, act)
+        require().bn_bwd_stats(dy, y, x, mean, invstd, stats, act, gamma, beta)
         return
-    g = _masked_grad(dy, y, act)
+    g = _masked_grad(dy, y, act, x, mean, invstd, gamma, beta)
     xh = (_rows(x) - mean) * invstd
     C = g.shape[1]
     stats[:C] += g.sum(0)
     stats[C:] += (g * xh).sum(0)
 
 
-def bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, dx, *, act=ACT_RELU, dres=None, dgamma=None, dbeta=None):
+def bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, dx, *, act=ACT_RELU, dres=None, dgamma=None, dbeta=None,
+                 beta=None):
     """dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*act'(y); dgamma/dbeta += sums;
-    dres = g (gradient of an added shortcut)."""
+    dres = g (gradient of an added shortcut).  y=None + beta: ReLU mask from x (see bn_bwd_stats)."""
     if x.is_cuda:
-        require().bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, act, dx, dres, dgamma, dbeta)
+        require().bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, act, dx, dres, dgamma, dbeta, beta)
         return dx
-    g = _masked_grad(dy, y, act)
+    g = _masked_grad(dy, y, act, x, mean, invstd, gamma, beta)
     R, C = g.shape
     xh = (_rows(x) - mean) * invstd
     d = gamma.float() * invstd * (g - stats[:C] / R - xh * stats[C:] / R)

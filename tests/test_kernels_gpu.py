@@ -358,6 +358,19 @@ def test_gather_and_noise():
     assert -1.0 <= z.min().item() and z.max().item() < 1.0 and abs(z.mean().item()) < 0.05
 
 
+def test_gather_long_rows():
+    # 224x224x3 images: items of one row spread over many workgroups
+    src = torch.randint(0, 256, (20, 224 * 224 * 3), dtype=torch.uint8, device=DEV)
+    labels = torch.randint(0, 1000, (20,), dtype=torch.int32, device=DEV)
+    idx = torch.tensor([3, 19, 0, 7, 7], dtype=torch.int32, device=DEV)
+    dst = torch.empty(5, 224 * 224 * 3, device=DEV, dtype=torch.bfloat16)
+    ld = torch.empty(5, dtype=torch.int32, device=DEV)
+    ops.gather_rows(src, dst, idx, labels, ld)
+    exp = src.cpu()[idx.cpu().long()].float() / 255
+    assert _rel(dst.cpu(), exp) < 1e-2
+    assert torch.equal(ld.cpu(), labels.cpu()[idx.cpu().long()])
+
+
 def test_softmax_xent_and_losses():
     torch.manual_seed(9)
     B, NC = 77, 10

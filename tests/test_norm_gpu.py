@@ -13,13 +13,17 @@ def _rel(a, b):
     return ((a.float().cpu() - b.float().cpu()).abs().max() / (b.float().cpu().abs().max() + 1e-6)).item()
 
 
-@pytest.mark.parametrize("shape,res_shape,rstride", [
-    ((8, 16, 16, 32), None, 1),
-    ((8, 16, 16, 32), (8, 16, 16, 32), 1),        # identity shortcut
-    ((8, 8, 8, 64), (8, 16, 16, 32), 2),          # option A: subsample + zero channels
-    ((4, 7, 7, 2048), None, 1),                   # ResNet-50 widest layer
+@pytest.mark.parametrize("shape,res_shape,rstride,from_x", [
+    ((8, 16, 16, 32), None, 1, False),
+    ((8, 16, 16, 32), None, 1, True),             # ReLU mask recomputed from x (no y read)
+    ((8, 16, 16, 32), (8, 16, 16, 32), 1, False),  # identity shortcut
+    ((8, 8, 8, 64), (8, 16, 16, 32), 2, False),   # option A: subsample + zero channels
+    ((4, 7, 7, 2048), None, 1, False),            # ResNet-50 widest layer
+    ((4, 7, 7, 2048), None, 1, True),
+    ((3, 17, 19, 64), None, 1, True),             # row count with ragged unroll tails
+    ((16, 56, 56, 64), None, 1, False),           # many row batches per stats thread
 ])
-def test_bn_forward_backward(shape, res_shape, rstride):
+def test_bn_forward_backward(shape, res_shape, rstride, from_x):
     torch.manual_seed(0)
     C = shape[-1]
     x = (torch.randn(*shape) * 2 + 3).to(torch.bfloat16)  # |mean| >> std: the shifted statistics matter
@@ -40,9 +44,10 @@ def test_bn_forward_backward(shape, res_shape, rstride):
         dx = torch.empty(*shape, device=dev, dtype=torch.bfloat16)
         dres = torch.empty(*shape, device=dev, dtype=torch.bfloat16)
         dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
-        ops.bn_bwd_stats(dy.to(dev), y, xd, mean, inv, st2, ops.ACT_RELU)
-        ops.bn_bwd_apply(dy.to(dev), y, xd, mean, inv, gamma.to(dev), st2, dx, act=ops.ACT_RELU, dres=dres,
-                         dgamma=dg, dbeta=db)
+        ym, bt = (None, beta.to(dev)) if from_x else (y, None)
+        ops.bn_bwd_stats(dy.to(dev), ym, xd, mean, inv, st2, ops.ACT_RELU, gamma=gamma.to(dev), beta=bt)
+        ops.bn_bwd_apply(dy.to(dev), ym, xd, mean, inv, gamma.to(dev), st2, dx, act=ops.ACT_RELU, dres=dres,
+                         dgamma=dg, dbeta=db, beta=bt)
         out[dev] = dict(y=y, mean=mean, inv=inv, mm=mm, mv=mv, dx=dx, dres=dres, dg=dg, db=db)
     c, g = out["cpu"], out[DEV]
     for k in ("mean", "inv", "mm", "mv", "dg", "db"):
