@@ -16,17 +16,20 @@ import dtfe  # noqa: E402,F401
 from dtfe import ops  # noqa: E402
 
 
-def timeit(fn, iters):
+def timeit(fn, iters, batch=10):
+    """median over `iters` rounds of `batch` back-to-back launches (a single launch between two
+    events on an idle GPU would also time the host's launch latency)"""
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     fn()
     torch.cuda.synchronize()
     ts = []
     for _ in range(iters):
         ev[0].record()
-        fn()
+        for _ in range(batch):
+            fn()
         ev[1].record()
         ev[1].synchronize()
-        ts.append(ev[0].elapsed_time(ev[1]) * 1000)
+        ts.append(ev[0].elapsed_time(ev[1]) * 1000 / batch)
     return statistics.median(ts)
 
 

@@ -7,16 +7,19 @@ namespace dtfe {
 
 // last-workgroup counter advance (see optim.hip): every workgroup has read
 // *counter before it arrives, so the bump is invisible to this launch.
+// Every workgroup read *counter at its start (and used the value, so the load has completed);
+// after a barrier one lane takes a ticket and the last one advances the counter.  No data is
+// handed between workgroups, so relaxed agent-scope atomics suffice (no fences: a
+// __threadfence() costs microseconds per workgroup); the next kernel sees the new value.
 __device__ __forceinline__ void advance_counter_last_block(int64_t* counter, uint32_t* done, int64_t by) {
   if (!counter || !done) return;
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    const uint32_t prev = atomicAdd(done, 1u);
+    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x * gridDim.y - 1) {
-      atomicAdd((unsigned long long*)counter, (unsigned long long)by);
-      atomicExch(done, 0u);
-      __threadfence();
+      __hip_atomic_fetch_add((unsigned long long*)counter, (unsigned long long)by, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -178,6 +178,17 @@ struct DenseLoader {
     }
   }
   __device__ __forceinline__ void store(T* lds) const { stage_store<T, R, MODE, KB>(lds, regs); }
+  // interior-tile load into a caller-owned register set (the deep-prefetch k-loop's ring)
+  __device__ __forceinline__ void load_into(int k0, u32x4_t (&r)[C::NC]) const {
+    const long step = MODE == KMAJ ? (long)k0 : (long)k0 * ld;
+#pragma unroll
+    for (int c = 0; c < C::NC; ++c)
+      if (C::N % GEMM_THREADS == 0 || threadIdx.x + c * GEMM_THREADS < C::N)
+        r[c] = *reinterpret_cast<const u32x4_t*>(base[c] + step);
+  }
+  __device__ __forceinline__ void store_from(T* lds, const u32x4_t (&r)[C::NC]) const {
+    stage_store<T, R, MODE, KB>(lds, r);
+  }
   // every k-tile of [k_begin, k_end) is interior (block-uniform)
   __device__ __forceinline__ bool all_fast(int k_begin, int k_end) const {
     return rows_full && (k_end - k_begin) % KB == 0 && k_end <= K;
@@ -300,6 +311,60 @@ __device__ __forceinline__ void gemm_kloop(LA& la, LB& lb, int k_begin, int nk, 
   }
 }
 
+// Interior-tile k-loop with a DEPTH-deep register prefetch ring: tile t+DEPTH is in flight
+// while tile t is multiplied, so DEPTH global-load latencies overlap instead of one (the
+// one-ahead loop above is latency-bound whenever a CU holds a single workgroup and a
+// k-tile is only a few MFMAs per wave - the skinny dense layers).  Plain VGPR loads: the
+// compiler's counted vmcnt waits retire exactly the set being written to LDS, and the
+// barrier does not drain the others.
+template <int DEPTH, typename T, typename Cfg, int AMODE, int BMODE, typename LA, typename LB>
+__device__ __forceinline__ void gemm_kloop_deep(LA& la, LB& lb, int k_begin, int nk, T* smem,
+                                                f32x4_t (&acc)[Cfg::TM][Cfg::TN]) {
+  constexpr int KB = Cfg::BK;
+  constexpr int A_ELEMS = LA::Lay::ELEMS, B_ELEMS = LB::Lay::ELEMS;
+  T* As[2] = {smem, smem + A_ELEMS};
+  T* Bs[2] = {smem + 2 * A_ELEMS, smem + 2 * A_ELEMS + B_ELEMS};
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / Cfg::WARPS_N, wn = wid % Cfg::WARPS_N;
+  u32x4_t ra[DEPTH][LA::C::NC], rb[DEPTH][LB::C::NC];
+  // prologue: tile 0 -> LDS, tiles 1..DEPTH in flight (ring slot of tile j = (j - 1) % DEPTH)
+  la.load_into(k_begin, ra[0]);
+  lb.load_into(k_begin, rb[0]);
+  la.store_from(As[0], ra[0]);
+  lb.store_from(Bs[0], rb[0]);
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (1 + d < nk) {
+      la.load_into(k_begin + (1 + d) * KB, ra[d]);
+      lb.load_into(k_begin + (1 + d) * KB, rb[d]);
+    }
+  __syncthreads();
+  for (int t0 = 0; t0 < nk; t0 += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int t = t0 + d;  // tile t + 1 sits in slot d
+      if (t < nk) {
+        tile_compute<T, Cfg, AMODE, BMODE>(As[t & 1], Bs[t & 1], wm, wn, lane, acc);
+        if (t + 1 < nk) {
+          la.store_from(As[(t + 1) & 1], ra[d]);
+          lb.store_from(Bs[(t + 1) & 1], rb[d]);
+          if (t + 1 + DEPTH < nk) {
+            la.load_into(k_begin + (t + 1 + DEPTH) * KB, ra[d]);
+            lb.load_into(k_begin + (t + 1 + DEPTH) * KB, rb[d]);
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+template <typename T, typename Cfg> struct PrefetchDepth {
+  // register ring depth: ~96 VGPRs of staged tiles at most
+  static constexpr int SLOT_REGS = 4 * ((Cfg::BM + Cfg::BN) * Cfg::BK * (int)sizeof(T) / 16 / GEMM_THREADS);
+  static constexpr int VALUE = SLOT_REGS <= 16 ? 4 : (SLOT_REGS <= 24 ? 4 : (SLOT_REGS <= 32 ? 3 : 1));
+};
+
 template <typename T, typename Cfg, int AMODE, int BMODE, typename LA, typename LB>
 __device__ __forceinline__ void gemm_mainloop(LA& la, LB& lb, int k_begin, int k_end, T* smem,
                                               f32x4_t (&acc)[Cfg::TM][Cfg::TN]) {
@@ -312,6 +377,13 @@ __device__ __forceinline__ void gemm_mainloop(LA& la, LB& lb, int k_begin, int k
   if (nk <= 0) return;
   if constexpr (requires_fast_check<LA>::value && requires_fast_check<LB>::value) {
     if (la.all_fast(k_begin, k_end) && lb.all_fast(k_begin, k_end)) {
+      constexpr int D = PrefetchDepth<T, Cfg>::VALUE;
+      if constexpr (D > 1) {
+        if (nk > 2) {
+          gemm_kloop_deep<D, T, Cfg, AMODE, BMODE>(la, lb, k_begin, nk, smem, acc);
+          return;
+        }
+      }
       gemm_kloop<true, T, Cfg, AMODE, BMODE>(la, lb, k_begin, nk, smem, acc);
       return;
     }

@@ -124,24 +124,36 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
       dst[0] = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c);
       dst[1] = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c + 4);
     }
-    __shared__ int s_last;
-    __threadfence();
+    // hand-off (MI355X guide, split-K counter form): plain slab stores -> every wave waits for
+    // them -> barrier -> ONE lane releases at agent scope and takes a ticket; the last arriver
+    // acquires once and reads every slab.  A __threadfence() in every thread instead costs
+    // microseconds per workgroup and serialises the whole grid.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem_raw);  // the one LDS array (Cs is free here)
     if (threadIdx.x == 0) {
-      const int prev = atomicAdd(a.tile_ctr + tile, 1);
-      s_last = prev == (int)gridDim.z - 1;
-      if (s_last) a.tile_ctr[tile] = 0;  // ready for the next launch / graph replay
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int prev = __hip_atomic_fetch_add(a.tile_ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == (int)gridDim.z - 1;
+      if (last) {
+        __hip_atomic_store(a.tile_ctr + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
     }
     __syncthreads();
-    if (!s_last) return;
-    __threadfence();
+    const int last = *flag;
+    __syncthreads();
+    if (!last) return;
     for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
       const int r = ch / CPR, c = (ch % CPR) * 8;
       f32x4_t v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
       for (int z = 0; z < (int)gridDim.z; ++z) {
         const f32x4_t* src = reinterpret_cast<const f32x4_t*>(a.ws + ((long)z * ntiles + tile) * (Cfg::BM * Cfg::BN) + ch * 8);
-        v0 += __builtin_nontemporal_load(src);
-        v1 += __builtin_nontemporal_load(src + 1);
+        v0 += src[0];
+        v1 += src[1];
       }
       *reinterpret_cast<f32x4_t*>(Cs + r * CLD + c) = v0;
       *reinterpret_cast<f32x4_t*>(Cs + r * CLD + c + 4) = v1;

@@ -35,10 +35,20 @@
 #include <mutex>
 #include <stdexcept>
 #include <tuple>
+#include <type_traits>
 
 namespace dtfe {
 
 namespace {
+
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 struct PGeom {
   int LH, LW;     // LDS image extent (pixels)
@@ -281,6 +291,217 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   }
 }
 
+// ----------------------------------------------------- compile-time geometry
+// The same persistent structure with the whole layer geometry as template constants (MNIST
+// conv2 forward and data gradient).  rocprof PMC of the runtime-geometry kernel above: 9-14
+// VALU instructions per MFMA (the per-step k walk, address adds and fragment register
+// copies of a 2-4 MFMA step) - the kernel was VALU-issue bound.  Here the k loop is fully
+// unrolled: every fragment read is `ds_read_b128 base + immediate` (tap offsets and weight
+// offsets are constants), the double-buffered fragment registers alternate by step parity
+// at compile time, and a step costs RT + NT reads, RT x NT MFMAs and no VALU.
+// One wave per RT 16-row tiles x all N columns (NT = N/16), WM waves cover the image.
+template <int CS, int KH, int KW, int LWP, int PS, int KP, int NT, int RT, int WM, int NPF, bool POOLED>
+__global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, PGeom G) {
+  constexpr int THREADS = 64 * WM;
+  constexpr int T = KH * KW, K = T * CS, NK = K / 32, CPP = CS / 8;
+  static_assert(K % 32 == 0 && CS % 32 == 0, "whole 32-deep steps within one tap");
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  bf16* wl = lds;
+  bf16* img = lds + G.img_off;
+  const int tid = threadIdx.x, lane = tid & 63, wm = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  for (int i = tid; i < (G.LH * LWP * PS) / 8; i += THREADS)
+    reinterpret_cast<u32x4_t*>(img)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  {
+    constexpr int kc_row = KP / 8;
+    const int total = G.NTOT * kc_row;
+    for (int i0 = tid; i0 < total; i0 += 8 * THREADS) {
+      u32x4_t v[8];
+      int off[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * THREADS;
+        const int n = i / kc_row, k = (i - n * kc_row) * 8;
+        off[u] = i < total ? n * KP + k : -1;
+        v[u] = u32x4_t{0u, 0u, 0u, 0u};
+        if (i < total && n < a.N && k < K) {
+          int sk = k;
+          if (a.flip_taps) {
+            const int tap = k / CS;
+            sk = (T - 1 - tap) * CS + (k - tap * CS);
+          }
+          v[u] = *reinterpret_cast<const u32x4_t*>(a.w + (long)n * K + sk);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (off[u] >= 0) *reinterpret_cast<u32x4_t*>(wl + off[u]) = v[u];
+    }
+  }
+
+  int dst[NPF];
+#pragma unroll
+  for (int j = 0; j < NPF; ++j) {
+    const int i = tid + j * THREADS;
+    dst[j] = -1;
+    if (i < G.nchunks) {
+      const int pix = i / CPP, cc = i - pix * CPP;
+      int sy, sx;
+      if (POOLED) {
+        const int PW = a.SW >> 1, py = pix / PW, px = pix - py * PW;
+        sy = 2 * py;
+        sx = 2 * px;
+      } else {
+        sy = pix / a.SW;
+        sx = pix - sy * a.SW;
+      }
+      const int ly = sy + a.pad, lx = sx + a.pad;
+      if (ly < G.LH && lx < G.LW) dst[j] = (ly * LWP + lx) * PS + cc * 8;
+    }
+  }
+  u32x4_t pf[NPF];
+  u32x2_t pam[NPF];
+  auto load_src = [&](long b) {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const long i = tid + j * THREADS;
+      if (i < G.nchunks) {
+        const long off = b * G.nchunks * 8 + i * 8;
+        if (POOLED) {
+          pf[j] = *reinterpret_cast<const u32x4_t*>(a.src_pooled + off);
+          pam[j] = *reinterpret_cast<const u32x2_t*>(a.src_argmax + off);
+        } else {
+          pf[j] = *reinterpret_cast<const u32x4_t*>(a.src + off);
+        }
+      }
+    }
+  };
+  auto write_src = [&]() {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      if (dst[j] < 0) continue;
+      if (!POOLED) {
+        *reinterpret_cast<u32x4_t*>(img + dst[j]) = pf[j];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          u32x4_t v;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t x = (pam[j][w >> 1] ^ ((uint32_t)q * 0x01010101u)) >> (16 * (w & 1));
+            const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
+            const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
+            v[w] = pf[j][w] & (lo_ok | hi_ok);
+          }
+          *reinterpret_cast<u32x4_t*>(img + dst[j] + ((q >> 1) * LWP + (q & 1)) * PS) = v;
+        }
+      }
+    }
+  };
+
+  const int g = lane >> 4;
+  const int M = a.OH * a.OW, tiles = (M + 15) >> 4;
+  const bf16* wlane = wl + (lane & 15) * KP + 8 * g;
+  float biasv[NT];  // loaded once, not once per image in the epilogue
+#pragma unroll
+  for (int n = 0; n < NT; ++n) biasv[n] = a.bias ? a.bias[n * 16 + (lane & 15)] : 0.f;
+
+  long b = blockIdx.x;
+  if (b < a.B) load_src(b);
+  __syncthreads();
+  for (; b < a.B; b += gridDim.x) {
+    write_src();
+    __syncthreads();
+    if (b + gridDim.x < a.B) load_src(b + gridDim.x);
+    // tiles past the image (a wave's last r) multiply pixel 0 and are dropped by the epilogue:
+    // no lane-divergent guards inside the k loop
+    const bf16* abase[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      int oy = 0, ox = 0;
+      row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
+      abase[r] = img + (oy * LWP + ox) * PS + 8 * g;
+    }
+    // data-gradient epilogue mask: loads issued now, in flight during the k loop
+    bf16 mask[RT][NT][4];
+    if (!a.pool && a.relu_mask) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int oy = 0, ox = 0;
+            row_pixel((wm + WM * r) * 16 + (lane >> 4) * 4 + j, a.OH, a.OW, G.blocked, oy, ox);
+            mask[r][n][j] = a.relu_mask[((b * a.OH + oy) * a.OW + ox) * a.N + n * 16 + (lane & 15)];
+          }
+    }
+    f32x4_t acc[RT][NT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[r][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    u32x4_t fa[2][RT], fb[2][NT];
+    auto fetch = [&](auto sc, int buf) {
+      constexpr int st = decltype(sc)::value;
+      constexpr int k0 = 32 * st, tap = k0 / CS, cs = k0 - tap * CS;
+      constexpr int toff = ((tap / KW) * LWP + (tap % KW)) * PS + cs;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) fa[buf][r] = *reinterpret_cast<const u32x4_t*>(abase[r] + toff);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) fb[buf][n] = *reinterpret_cast<const u32x4_t*>(wlane + n * 16 * KP + k0);
+    };
+    fetch(std::integral_constant<int, 0>{}, 0);
+    static_for<0, NK>([&](auto sc) {
+      constexpr int st = decltype(sc)::value;
+      if constexpr (st + 1 < NK) fetch(std::integral_constant<int, st + 1>{}, (st + 1) & 1);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[st & 1][r]),
+                                                              __builtin_bit_cast(bf16x8_t, fb[st & 1][n]), acc[r][n],
+                                                              0, 0, 0);
+      }
+    });
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int tile = wm + WM * r;
+      if (tile >= tiles) break;
+      const int m0 = tile * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int col = n * 16 + (lane & 15);
+        if (col >= a.N) continue;
+        const float bias = biasv[n];
+        const f32x4_t v = acc[r][n];
+        if (a.pool) {
+          int oy, ox;
+          if (!row_pixel(m0, a.OH, a.OW, 1, oy, ox)) continue;
+          int am = 0;
+          float mx = v[0];
+#pragma unroll
+          for (int j = 1; j < 4; ++j) if (v[j] > mx) { mx = v[j]; am = j; }
+          const long o = ((b * (a.OH >> 1) + (oy >> 1)) * (a.OW >> 1) + (ox >> 1)) * a.N + col;
+          a.y[o] = f2bf(apply_act(mx + bias, a.act));
+          if (a.argmax) a.argmax[o] = (uint8_t)am;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int oy, ox;
+            if (!row_pixel(m0 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
+            const long o = ((b * a.OH + oy) * a.OW + ox) * a.N + col;
+            float x = apply_act(v[j] + bias, a.act);
+            if (a.relu_mask && !(bf2f(mask[r][n][j]) > 0.f)) x = 0.f;
+            a.y[o] = f2bf(x);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- host side
 // Extra LDS cycles per A-fragment ds_read_b128 (averaged over the image's tiles)
 // for pixel stride PSs (16 B slots) and row pitch LWP, from the lane-group model.
@@ -372,8 +593,40 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
+// compile-time-geometry instances (MNIST conv2 forward / data gradient); false if `a` is not one
+template <int CS, int KH, int KW, int LWP, int PS, int NT, int RT, int WM, bool POOLED>
+bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
+  constexpr int K = KH * KW * CS, KP = (K + 31) / 32 * 32 + 16;
+  if (a.CS != CS || a.KH != KH || a.KW != KW || a.N != NT * 16 || a.stride != 1 || a.dil > 1) return false;
+  if ((a.src == nullptr) != POOLED) return false;
+  PGeom G = persist_geom(a, 1, NT, 64 * WM);
+  if (G.LWP != LWP || G.PS != PS || G.KP != KP || G.slack != 0) return false;
+  const int tiles = (a.OH * a.OW + 15) / 16;
+  if (tiles > WM * RT) return false;
+  const size_t lds = persist_lds(G);
+  if (lds > 160 * 1024 || (a.pool && !G.blocked)) return false;
+  const int grid = a.B < 256 ? a.B : 256;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM), lds, s, a, G);
+  };
+  switch (G.npf) {
+    case 1: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 1, POOLED>); return true;
+    case 2: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 2, POOLED>); return true;
+    default: return false;
+  }
+}
+
 bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
+  static const bool fixed_ok = [] {
+    const char* e = getenv("DTFE_IC_FIXED");
+    return !(e && atoi(e) == 0);
+  }();
+  if (fixed_ok && a.OH == 14 && a.OW == 14 && a.B >= 256) {
+    if (launch_fixed<32, 5, 5, 20, 48, 4, 1, 13, false>(a, s)) return true;  // conv2 forward
+    if (launch_fixed<64, 5, 5, 20, 80, 2, 1, 13, true>(a, s)) return true;   // conv2 data gradient
+  }
   const bool pooled = a.src == nullptr;
   if (pooled && ((a.SH | a.SW) & 1)) return false;
   if (pooled && a.dil > 1) return false;

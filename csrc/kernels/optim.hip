@@ -80,6 +80,43 @@ __device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i
   if (w16) *reinterpret_cast<u32x2_t*>(w16) = u32x2_t{pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3])};
 }
 
+// U vec4 updates at i, i+1024, ... (one workgroup-wide stride apart): every load is issued
+// before the first update, so each thread keeps U x (3-4) 16-B loads in flight
+template <int KIND, int U>
+__device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long i, bf16* w16) {
+  f32x4_t g[U], p[U], s1[U], s2[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long k = i + u * 1024;
+    if (a.g) {
+      g[u] = *reinterpret_cast<const f32x4_t*>(a.g + k);
+    } else {
+      const u32x2_t w = *reinterpret_cast<const u32x2_t*>(a.g16 + k);
+      g[u] = f32x4_t{__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u), __uint_as_float(w[1] << 16),
+                     __uint_as_float(w[1] & 0xffff0000u)};
+    }
+    p[u] = *reinterpret_cast<const f32x4_t*>(a.p + k);
+    s1[u] = s2[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (KIND != OPT_SGD) s1[u] = *reinterpret_cast<const f32x4_t*>(a.s1 + k);
+    if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) s2[u] = *reinterpret_cast<const f32x4_t*>(a.s2 + k);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long k = i + u * 1024;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float x1 = s1[u][j], x2 = s2[u][j];
+      p[u][j] = upd<KIND>(a, lr_t, p[u][j], g[u][j] * a.gscale, x1, x2);
+      s1[u][j] = x1;
+      s2[u][j] = x2;
+    }
+    *reinterpret_cast<f32x4_t*>(a.p + k) = p[u];
+    if (KIND != OPT_SGD) *reinterpret_cast<f32x4_t*>(a.s1 + k) = s1[u];
+    if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) *reinterpret_cast<f32x4_t*>(a.s2 + k) = s2[u];
+    if (w16) *reinterpret_cast<u32x2_t*>(w16 + u * 1024) = u32x2_t{pack_bf16x2(p[u][0], p[u][1]), pack_bf16x2(p[u][2], p[u][3])};
+  }
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
   __shared__ bf16 tile[64][66];
@@ -94,7 +131,10 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
     if (w.kind == 0) {
       const long base = sg.off + w.start;
       const long n4 = ((base & 3) == 0) ? (w.count / 4) * 4 : 0;  // segments are 64-aligned; chunks 8192
-      for (long j = threadIdx.x * 4; j < n4; j += 256 * 4)
+      long j = threadIdx.x * 4;
+      for (; j + 3 * 1024 < n4; j += 4 * 1024)  // 4 independent vec4 updates in flight per thread
+        update_vec4x<KIND, 4>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
+      for (; j < n4; j += 256 * 4)
         update_vec4<KIND>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
       for (long j = n4 + threadIdx.x; j < w.count; j += 256) {
         const long li = w.start + j, i = sg.off + li;
@@ -122,18 +162,19 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
       __syncthreads();
     }
   }
-  // last workgroup: advance the non-slot scalars (every workgroup has read them)
+  // last workgroup: advance the non-slot scalars.  Every thread read them at its start and
+  // used the value; after the barrier one lane takes a ticket (relaxed agent atomics - nothing
+  // is handed between workgroups, so no fences) and the last arriver updates them.
+  __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    const uint32_t prev = atomicAdd(a.done_counter, 1u);
+    const uint32_t prev = __hip_atomic_fetch_add(a.done_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {
       if (KIND == OPT_ADAM) {
         a.beta_pow[0] *= a.beta1;
         a.beta_pow[1] *= a.beta2;
       }
       if (a.global_step && a.gs_inc) atomicAdd(a.global_step, a.gs_inc);
-      atomicExch(a.done_counter, 0u);
-      __threadfence();
+      __hip_atomic_store(a.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -26,10 +26,10 @@ def main(paths):
                     if c and v:
                         acc[k][c].append(float(v))
     counters = sorted({c for d in acc.values() for c in d})
-    print("kernel," + ",".join(counters))
+    w = csv.writer(sys.stdout)  # kernel names hold commas (template arguments): quote them
+    w.writerow(["kernel"] + counters)
     for k, d in sorted(acc.items()):
-        vals = [("%.4g" % (sum(d[c]) / len(d[c]))) if d.get(c) else "" for c in counters]
-        print(k + "," + ",".join(vals))
+        w.writerow([k] + [("%.4g" % (sum(d[c]) / len(d[c]))) if d.get(c) else "" for c in counters])
 
 
 if __name__ == "__main__":
