@@ -18,99 +18,103 @@
 
 namespace dtfe {
 
+// One wave per batch row (K/64 features per lane).  The wave's slice of W (NC x K/64 bf16,
+// 80 VGPRs for 10 x 16) is loaded straight into registers together with the h row - one
+// round of global loads, no LDS staging and no barrier (the earlier LDS-staged version spent
+// most of its ~20 us in the serial W staging of every workgroup); the NC dot products are
+// reduced across the wave with independent butterfly chains that the scheduler interleaves.
 template <int NC, int K>
 __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   constexpr int E = K / 64;  // features per lane
   static_assert(E % 8 == 0, "K must be a multiple of 512");
-  __shared__ __attribute__((aligned(16))) float wl[NC * K];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int i = threadIdx.x * 8; i < NC * K; i += 256 * 8) {
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.w + i);
-    const bf16* e = reinterpret_cast<const bf16*>(&v);
+  __shared__ float red_loss[4];
+  __shared__ int red_correct[4];
+  const int row = min(blockIdx.x * 4 + wid, a.B - 1);  // a surplus wave recomputes the last row, unstored
+  const bool live = blockIdx.x * 4 + wid < a.B;
+  u32x4_t wv[NC][E / 8], hv[E / 8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wl[i + j] = bf2f(e[j]);
-  }
+  for (int c = 0; c < E / 8; ++c) hv[c] = *reinterpret_cast<const u32x4_t*>(a.h + (long)row * K + lane * E + c * 8);
+#pragma unroll
+  for (int n = 0; n < NC; ++n)
+#pragma unroll
+    for (int c = 0; c < E / 8; ++c) wv[n][c] = *reinterpret_cast<const u32x4_t*>(a.w + (long)n * K + lane * E + c * 8);
+  const int label = a.labels[row];
   float bias[NC];
 #pragma unroll
   for (int n = 0; n < NC; ++n) bias[n] = a.b ? a.b[n] : 0.f;
-  __syncthreads();
 
-  float loss_acc = 0.f;
-  int correct = 0;
-  const int waves_total = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + wid; row < a.B; row += waves_total) {
-    float h[E];
+  float h[E];
 #pragma unroll
-    for (int c = 0; c < E / 8; ++c) {
-      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.h + (long)row * K + lane * E + c * 8);
-      const bf16* e = reinterpret_cast<const bf16*>(&v);
+  for (int c = 0; c < E / 8; ++c)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) h[c * 8 + i] = bf2f(e[i]);
-    }
-    float logit[NC];
+    for (int i = 0; i < 8; ++i) h[c * 8 + i] = bf2f((bf16)(hv[c][i >> 1] >> (16 * (i & 1))));
+  auto wel = [&](int n, int i) { return bf2f((bf16)(wv[n][i / 8][(i % 8) >> 1] >> (16 * (i & 1)))); };
+  float logit[NC];
 #pragma unroll
-    for (int n = 0; n < NC; ++n) {
-      const f32x4_t* wr = reinterpret_cast<const f32x4_t*>(wl + n * K + lane * E);
-      float s = 0.f;
+  for (int n = 0; n < NC; ++n) {
+    float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < E / 4; ++i) {
-        const f32x4_t w4 = wr[i];
-        s = fmaf(h[4 * i], w4[0], s);
-        s = fmaf(h[4 * i + 1], w4[1], s);
-        s = fmaf(h[4 * i + 2], w4[2], s);
-        s = fmaf(h[4 * i + 3], w4[3], s);
-      }
-      logit[n] = wave_sum(s) + bias[n];
-    }
-    const int label = a.labels[row];
-    float mx = logit[0];
-    int am = 0;
-#pragma unroll
-    for (int n = 1; n < NC; ++n) if (logit[n] > mx) { mx = logit[n]; am = n; }
-    float se = 0.f;
-#pragma unroll
-    for (int n = 0; n < NC; ++n) se += __expf(logit[n] - mx);
-    const float lse = mx + __logf(se);
-    float dl[NC];
-    float lg_label = 0.f;
-#pragma unroll
-    for (int n = 0; n < NC; ++n) {
-      const float p = __expf(logit[n] - lse);
-      dl[n] = (p - (n == label ? 1.f : 0.f)) * a.scale;
-      if (n == label) lg_label = logit[n];
-    }
-    loss_acc += lse - lg_label;
-    correct += (am == label);
-    if (lane < a.ld_dl) {
-      float v = 0.f, lv = 0.f;
-#pragma unroll
-      for (int n = 0; n < NC; ++n) if (n == lane) { v = dl[n]; lv = logit[n]; }
-      a.dl[(long)row * a.ld_dl + lane] = f2bf(v);  // pad columns get 0
-      if (a.logits_out && lane < NC) a.logits_out[(long)row * NC + lane] = lv;
-    }
-    u32x4_t outv[E / 8];
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-      float g = 0.f;
-#pragma unroll
-      for (int n = 0; n < NC; ++n) g = fmaf(dl[n], wl[n * K + lane * E + i], g);
-      g = h[i] > 0.f ? g * a.inv_keep : 0.f;
-      reinterpret_cast<bf16*>(&outv[i / 8])[i % 8] = f2bf(g);
-    }
-#pragma unroll
-    for (int c = 0; c < E / 8; ++c)
-      *reinterpret_cast<u32x4_t*>(a.dz + (long)row * K + lane * E + c * 8) = outv[c];
+    for (int i = 0; i < E; ++i) s = fmaf(h[i], wel(n, i), s);
+    logit[n] = s;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int n = 0; n < NC; ++n) logit[n] += __shfl_xor(logit[n], o, 64);
+#pragma unroll
+  for (int n = 0; n < NC; ++n) logit[n] += bias[n];
+
+  float mx = logit[0];
+  int am = 0;
+#pragma unroll
+  for (int n = 1; n < NC; ++n) if (logit[n] > mx) { mx = logit[n]; am = n; }
+  float se = 0.f;
+#pragma unroll
+  for (int n = 0; n < NC; ++n) se += __expf(logit[n] - mx);
+  const float lse = mx + __logf(se);
+  float dl[NC];
+  float lg_label = 0.f;
+#pragma unroll
+  for (int n = 0; n < NC; ++n) {
+    const float p = __expf(logit[n] - lse);
+    dl[n] = (p - (n == label ? 1.f : 0.f)) * a.scale;
+    if (n == label) lg_label = logit[n];
+  }
+  if (live && lane < a.ld_dl) {
+    float v = 0.f, lv = 0.f;
+#pragma unroll
+    for (int n = 0; n < NC; ++n) if (n == lane) { v = dl[n]; lv = logit[n]; }
+    a.dl[(long)row * a.ld_dl + lane] = f2bf(v);  // pad columns get 0
+    if (a.logits_out && lane < NC) a.logits_out[(long)row * NC + lane] = lv;
+  }
+  u32x4_t outv[E / 8];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    float g = 0.f;
+#pragma unroll
+    for (int n = 0; n < NC; ++n) g = fmaf(dl[n], wel(n, i), g);
+    g = h[i] > 0.f ? g * a.inv_keep : 0.f;
+    reinterpret_cast<bf16*>(&outv[i / 8])[i % 8] = f2bf(g);
+  }
+  if (live)
+#pragma unroll
+    for (int c = 0; c < E / 8; ++c) *reinterpret_cast<u32x4_t*>(a.dz + (long)row * K + lane * E + c * 8) = outv[c];
+  // one atomic per workgroup (1024 same-address atomics per launch would serialise)
   if (lane == 0) {
-    if (a.loss_sum) atomicAdd(a.loss_sum, loss_acc);
-    if (a.correct) atomicAdd(a.correct, correct);
+    red_loss[wid] = live ? lse - lg_label : 0.f;
+    red_correct[wid] = live && am == label;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.loss_sum) atomicAdd(a.loss_sum, red_loss[0] + red_loss[1] + red_loss[2] + red_loss[3]);
+    if (a.correct) atomicAdd(a.correct, red_correct[0] + red_correct[1] + red_correct[2] + red_correct[3]);
   }
 }
 
 void launch_head_xent(const HeadArgs& a, hipStream_t s) {
   if (a.NC != 10 || a.K != 1024) throw std::runtime_error("head_xent: only NC=10, K=1024 instantiated");
-  int blocks = (a.B + 3) / 4;  // one row per wave
-  if (blocks > 1024) blocks = 1024;
+  const int blocks = (a.B + 3) / 4;  // one row per wave
   hipLaunchKernelGGL((head_xent_kernel<10, 1024>), dim3(blocks), dim3(256), 0, s, a);
 }
 

@@ -441,26 +441,33 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
     for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int n = 0; n < NT; ++n) acc[r][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    u32x4_t fa[2][RT], fb[2][NT];
-    auto fetch = [&](auto sc, int buf) {
+    // fragments are fetched PF steps ahead (ring of PF + 1 register sets): LDS read latency,
+    // not bandwidth, bounds this loop
+    constexpr int PF = 2;
+    u32x4_t fa[PF + 1][RT], fb[PF + 1][NT];
+    auto fetch = [&](auto sc) {
       constexpr int st = decltype(sc)::value;
       constexpr int k0 = 32 * st, tap = k0 / CS, cs = k0 - tap * CS;
       constexpr int toff = ((tap / KW) * LWP + (tap % KW)) * PS + cs;
+      constexpr int buf = st % (PF + 1);
 #pragma unroll
       for (int r = 0; r < RT; ++r) fa[buf][r] = *reinterpret_cast<const u32x4_t*>(abase[r] + toff);
 #pragma unroll
       for (int n = 0; n < NT; ++n) fb[buf][n] = *reinterpret_cast<const u32x4_t*>(wlane + n * 16 * KP + k0);
     };
-    fetch(std::integral_constant<int, 0>{}, 0);
+    static_for<0, PF>([&](auto sc) {
+      if constexpr (decltype(sc)::value < NK) fetch(sc);
+    });
     static_for<0, NK>([&](auto sc) {
       constexpr int st = decltype(sc)::value;
-      if constexpr (st + 1 < NK) fetch(std::integral_constant<int, st + 1>{}, (st + 1) & 1);
+      if constexpr (st + PF < NK) fetch(std::integral_constant<int, st + PF>{});
+      constexpr int buf = st % (PF + 1);
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
 #pragma unroll
         for (int n = 0; n < NT; ++n)
-          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[st & 1][r]),
-                                                              __builtin_bit_cast(bf16x8_t, fb[st & 1][n]), acc[r][n],
+          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[buf][r]),
+                                                              __builtin_bit_cast(bf16x8_t, fb[buf][n]), acc[r][n],
                                                               0, 0, 0);
       }
     });
