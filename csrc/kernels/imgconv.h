@@ -61,5 +61,9 @@ void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s);
 // persistent variant (dW accumulated in registers across a workgroup's images);
 // returns false when the shape does not fit it
 bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s);
+// MNIST conv1 (28x28x1, 5x5 SAME, 32 channels, B >= 256): shifted-copy kernels
+// (imgconv1_copies.hip); false when the shape is not that layer
+bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s);
+bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s);
 
 }  // namespace dtfe

@@ -316,6 +316,7 @@ void launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
   if (a.CS <= 4 && (!a.src || a.flip_taps || a.dil > 1))
     throw std::runtime_error("imgconv: the few-channel path is forward-only");
   if (a.pool && ((a.OH | a.OW) & 1)) throw std::runtime_error("imgconv: pool needs even output dims");
+  if (a.CS <= 4 && launch_conv1_copies_fwd(a, s)) return;
   if (a.CS > 4 && launch_imgconv_persistent(a, s)) return;
   if (a.dil > 1) throw std::runtime_error("imgconv: dilated sources need the persistent kernel (B >= 64)");
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
@@ -651,6 +652,7 @@ void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s) {
   if (!imgwgrad_supported(a)) throw std::runtime_error("imgwgrad: shape not supported");
   if (a.CS <= 4) {
     if (!a.src) throw std::runtime_error("imgwgrad: few-channel path needs src");
+    if (launch_conv1_copies_wgrad(a, s)) return;
     switch (wg_nt(a.N)) {
       case 1: launch_wg1<1>(a, s); break;
       case 2: launch_wg1<2>(a, s); break;

@@ -1,0 +1,307 @@
+// MNIST conv1 (28x28x1 -> 5x5 SAME -> 32 channels) forward (+bias, ReLU, 2x2 max-pool,
+// argmax) and weight gradient (dY un-pooled on load), persistent over the batch.
+//
+// Why a dedicated pair: with one input channel the MFMA reduction index is the tap, so an
+// operand fragment (8 consecutive k of one pixel) is 8 horizontally adjacent pixels that start
+// at an arbitrary column - the generic few-channel kernels gathered them with 8 ds_read_u16
+// and packed them in VALU (rocprof PMC: ~80 VALU per MFMA).  Here each image is staged once
+// as a zero-padded plane P and then as S column-shifted copies
+//
+//     copy_s[r][c] = P[r][c + s + 2]          P[r][c] = X[r - 2][c - 4]
+//
+// so that "8 pixels from column x" is one aligned ds_read_b128 of copy_(x mod 8) at column
+// x - x mod 8 (forward, S = 8) or of copy_kw at column 8g (weight gradient: tap column kw,
+// S = 5).  Forward: k = kh*8 + kw (kw >= 5 carry zero weights), two 32-deep MFMA steps per
+// 16-pixel tile.  Weight gradient: k = output pixel (one output row of 32 enumerated
+// columns per step), A = dY^T through the transposing ds_read_b64_tr_b16, B = shifted copies.
+// Both loop over several images per workgroup with the next image's global loads in flight;
+// the weight gradient accumulates in registers and flushes one partial per workgroup.
+#include "imgconv.h"
+
+#include <stdexcept>
+
+namespace dtfe {
+
+namespace {
+
+constexpr int TH = 256;                  // 4 waves
+constexpr int HI = 28;                   // image / output size
+constexpr int PWD = 48, PRW = 32;        // P: 32 rows x 48 columns (rows 16-B aligned)
+constexpr int CWD = 40;                  // copy row pitch (elements): 5 x 16-B slots
+constexpr int CSZ = PRW * CWD + 8;       // copy stride (+1 slot skew per copy)
+constexpr int NCH = 32;                  // output channels
+constexpr int XCH = HI * HI / 4;         // 8-byte chunks of an image (196)
+
+__device__ __forceinline__ u32x4_t ld16l(const bf16* p) { return *reinterpret_cast<const u32x4_t*>(p); }
+
+// image b -> P interior (8-byte chunks: 4 pixels of one row; rows are 56 B)
+__device__ __forceinline__ void load_img(const bf16* x, long b, u32x2_t& v) {
+  if (threadIdx.x < XCH) v = *reinterpret_cast<const u32x2_t*>(x + b * (HI * HI) + threadIdx.x * 4);
+}
+__device__ __forceinline__ void write_img(bf16* P, const u32x2_t& v) {
+  if (threadIdx.x < XCH) {
+    const int r = threadIdx.x / 7, c = (threadIdx.x - r * 7) * 4;
+    *reinterpret_cast<u32x2_t*>(P + (r + 2) * PWD + c + 4) = v;
+  }
+}
+
+// copies s < S (rows 0..31, 32 columns each = 4 chunks of 8)
+template <int S>
+__device__ __forceinline__ void build_copies(const bf16* P, bf16* C) {
+  for (int q = threadIdx.x; q < S * PRW * 4; q += TH) {
+    const int s = q / (PRW * 4), rem = q - s * PRW * 4, r = rem >> 2, c8 = (rem & 3) * 8;
+    const unsigned short* src = reinterpret_cast<const unsigned short*>(P + r * PWD + c8 + s + 2);
+    u32x4_t v;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v[w] = (uint32_t)src[2 * w] | ((uint32_t)src[2 * w + 1] << 16);
+    *reinterpret_cast<u32x4_t*>(C + s * CSZ + r * CWD + c8) = v;
+  }
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 P[PRW * PWD];
+  __shared__ __attribute__((aligned(16))) bf16 C[8 * CSZ];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4;
+  for (int i = threadIdx.x; i < PRW * PWD / 8; i += TH) reinterpret_cast<u32x4_t*>(P)[i] = u32x4_t{0u, 0u, 0u, 0u};
+
+  // weights as B fragments: step 0 rows kh = g (kw 0..7), step 1 row kh = 4 (g == 0 only)
+  bf16x8_t bw[2][2];
+  float biasv[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = nt * 16 + (lane & 15);
+    biasv[nt] = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int kh = st == 0 ? g : 4;
+      const bool rowok = st == 0 || g == 0;
+      s16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (short)((rowok && j < 5) ? a.w[n * 25 + kh * 5 + j] : 0);
+      bw[nt][st] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+
+  u32x2_t xv = {0u, 0u};
+  long b = blockIdx.x;
+  if (b < a.B) load_img(a.src, b, xv);
+  __syncthreads();
+  for (; b < a.B; b += gridDim.x) {
+    write_img(P, xv);
+    __syncthreads();
+    if (b + gridDim.x < a.B) load_img(a.src, b + gridDim.x, xv);
+    build_copies<8>(P, C);
+    __syncthreads();
+    // 49 tiles of 16 output pixels in 2x2-window order (4 windows per tile)
+    for (int t = wid; t < 49; t += 4) {
+      const int m = t * 16 + (lane & 15), q = m & 3, w = m >> 2;
+      const int oy = 2 * (w / 14) + (q >> 1), ox = 2 * (w % 14) + (q & 1);
+      const int s = ox & 7;
+      const bf16* ab = C + s * CSZ + (ox - s) + oy * CWD;
+      const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, ld16l(ab + g * CWD));
+      const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, ld16l(ab + 4 * CWD));
+      f32x4_t acc[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[nt][0], f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw[nt][1], acc[nt], 0, 0, 0);
+      }
+      // lane holds rows (lane>>4)*4 + j = one 2x2 window, column lane & 15 of each n-tile
+      const int wq = t * 4 + g, py = wq / 14, px = wq - py * 14;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4_t v = acc[nt];
+        int am = 0;
+        float mx = v[0];
+#pragma unroll
+        for (int j = 1; j < 4; ++j) if (v[j] > mx) { mx = v[j]; am = j; }
+        const long o = ((b * 14 + py) * 14 + px) * NCH + nt * 16 + (lane & 15);
+        a.y[o] = f2bf(apply_act(mx + biasv[nt], a.act));
+        if (a.argmax) a.argmax[o] = (uint8_t)am;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ weight grad
+constexpr int DP = NCH;  // dY image pitch (elements per pixel)
+
+__global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 P[PRW * PWD];
+  __shared__ __attribute__((aligned(16))) bf16 C[5 * CSZ];
+  __shared__ __attribute__((aligned(16))) bf16 D[HI * 32 * DP];  // dY [oy][ox < 32][n]
+  __shared__ float red[32 * 32 + 32];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int q4 = i16 >> 2, p4 = i16 & 3;
+  for (int i = threadIdx.x; i < PRW * PWD / 8; i += TH) reinterpret_cast<u32x4_t*>(P)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  for (int i = threadIdx.x; i < HI * 32 * DP / 8; i += TH) reinterpret_cast<u32x4_t*>(D)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  for (int i = threadIdx.x; i < 32 * 32 + 32; i += TH) red[i] = 0.f;
+
+  // B fragment addresses: tap ti = tt*16 + i16 -> (kh, kw); taps >= 25 read tap 24 (dropped)
+  int boff[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int ti = min(tt * 16 + i16, 24), kh = ti / 5, kw = ti - kh * 5;
+    boff[tt] = kw * CSZ + kh * CWD + 8 * g;
+  }
+  // A (dY^T) transposed-read addresses within one output row: pixels 8g + 4h + q4, columns 4*p4
+  int aoff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) aoff[h] = (8 * g + 4 * h + q4) * DP + 4 * p4;
+
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dbacc[2] = {0.f, 0.f};
+
+  // pooled dY chunks: 14*14 windows x 4 chunks of 8 channels = 784 per image
+  constexpr int PCH = 14 * 14 * (NCH / 8);
+  constexpr int NPF = (PCH + TH - 1) / TH;  // 4
+  u32x4_t pv[NPF];
+  u32x2_t pam[NPF];
+  u32x2_t xv = {0u, 0u};
+  auto load_all = [&](long b) {
+    load_img(a.src, b, xv);
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = threadIdx.x + j * TH;
+      if (i < PCH) {
+        const long o = b * (PCH * 8) + (long)i * 8;
+        pv[j] = *reinterpret_cast<const u32x4_t*>(a.dy_pooled + o);
+        pam[j] = *reinterpret_cast<const u32x2_t*>(a.dy_argmax + o);
+      }
+    }
+  };
+  auto write_dy = [&]() {
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = threadIdx.x + j * TH;
+      if (i >= PCH) continue;
+      const int win = i >> 2, c8 = (i & 3) * 8, py = win / 14, px = win - py * 14;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        u32x4_t v;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // keep bf16 element e where argmax byte e == qq
+          const uint32_t x = (pam[j][w >> 1] ^ ((uint32_t)qq * 0x01010101u)) >> (16 * (w & 1));
+          const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
+          const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
+          v[w] = pv[j][w] & (lo_ok | hi_ok);
+        }
+        const int oy = 2 * py + (qq >> 1), ox = 2 * px + (qq & 1);
+        *reinterpret_cast<u32x4_t*>(D + (oy * 32 + ox) * DP + c8) = v;
+      }
+    }
+  };
+
+  long b = blockIdx.x;
+  if (b < a.B) load_all(b);
+  __syncthreads();
+  for (; b < a.B; b += gridDim.x) {
+    write_img(P, xv);
+    write_dy();
+    __syncthreads();
+    if (b + gridDim.x < a.B) load_all(b + gridDim.x);
+    build_copies<5>(P, C);
+    __syncthreads();
+    for (int oy = wid; oy < HI; oy += 4) {
+      bf16x8_t af[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const bf16* base = D + oy * 32 * DP + nt * 16;
+        const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + aoff[0]));
+        const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + aoff[1]));
+        const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        af[nt] = __builtin_bit_cast(bf16x8_t, v);
+        float sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum += bf2f((bf16)v[e]);
+        dbacc[nt] += sum;
+      }
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, ld16l(C + boff[tt] + oy * CWD));
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[nt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nt], bf, acc[nt][tt], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // cross-wave reduction in LDS: red[n][tap] (+ db[n])
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(red + (nt * 16 + g * 4 + j) * 32 + tt * 16 + i16, acc[nt][tt][j]);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    float v = dbacc[nt];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 16) atomicAdd(red + 32 * 32 + nt * 16 + lane, v);
+  }
+  __syncthreads();
+  // flush: dW[n][tap] (tap < 25) and db[n]; one partial per workgroup (summed by the reduce
+  // kernel) or, without a workspace, scaled atomics
+  constexpr int KC = 25, LEN = NCH * KC + NCH;
+  float* part = a.ws ? a.ws + (long)blockIdx.x * LEN : nullptr;
+  for (int i = threadIdx.x; i < LEN; i += TH) {
+    const float v = i < NCH * KC ? red[(i / KC) * 32 + (i % KC)] : red[32 * 32 + (i - NCH * KC)];
+    if (part) part[i] = v;
+    else if (i < NCH * KC) atomicAdd(a.dw + i, v * a.scale);
+    else if (a.db) atomicAdd(a.db + (i - NCH * KC), v * a.scale);
+  }
+}
+
+// dw[i] += scale * sum_p part[p][i] (tail -> db): one thread per element, 16 partials per
+// y-block with all loads in flight, one atomic per element and y-block
+constexpr int RP = 16;
+__global__ __launch_bounds__(256) void conv1c_reduce_kernel(const float* __restrict__ ws, int parts, int len, int nw,
+                                                            float* dw, float* db, float scale) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  const int p0 = blockIdx.y * RP;
+  float v[RP];
+#pragma unroll
+  for (int j = 0; j < RP; ++j) v[j] = p0 + j < parts ? ws[(long)(p0 + j) * len + i] : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < RP; ++j) s += v[j];
+  if (i < nw) atomicAdd(dw + i, scale * s);
+  else if (db) atomicAdd(db + i - nw, scale * s);
+}
+
+bool mnist_conv1_shape(int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad) {
+  return B >= 256 && SH == HI && SW == HI && CS == 1 && OH == HI && OW == HI && N == NCH && KH == 5 && KW == 5 &&
+         stride == 1 && pad == 2;
+}
+
+}  // namespace
+
+bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s) {
+  if (!mnist_conv1_shape(a.B, a.SH, a.SW, a.CS, a.OH, a.OW, a.N, a.KH, a.KW, a.stride, a.pad)) return false;
+  if (!a.src || !a.pool || a.flip_taps || a.dil > 1 || a.relu_mask) return false;
+  const int grid = a.B < 1024 ? a.B : 1024;
+  hipLaunchKernelGGL(conv1c_fwd_kernel, dim3(grid), dim3(TH), 0, s, a);
+  return true;
+}
+
+bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s) {
+  if (!mnist_conv1_shape(a.B, a.SH, a.SW, a.CS, a.OH, a.OW, a.N, a.KH, a.KW, a.stride, a.pad)) return false;
+  if (!a.src || a.dy || !a.dy_pooled) return false;
+  const int grid = a.B < 256 ? a.B : 256;
+  hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a);
+  if (a.ws) {
+    constexpr int LEN = NCH * 25 + NCH;
+    hipLaunchKernelGGL(conv1c_reduce_kernel, dim3((LEN + 255) / 256, (grid + RP - 1) / RP), dim3(256), 0, s, a.ws,
+                       grid, LEN, NCH * 25, a.dw, a.db, a.scale);
+  }
+  return true;
+}
+
+}  // namespace dtfe

@@ -309,7 +309,7 @@ def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, 
     On the GPU the persistent kernel stores per-workgroup partials in `workspace`
     (default: a cached per-device buffer) and a second kernel sums them."""
     if dw.is_cuda:
-        if workspace is None and CS % 16 == 0:
+        if workspace is None and (CS % 16 == 0 or CS == 1):
             workspace = wgrad_workspace(dw.device, 256 * (N * KH * KW * CS + N))
         require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
                            scale, workspace)

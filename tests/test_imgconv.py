@@ -82,6 +82,7 @@ PERSIST_CASES = [  # B > 256 so persistent workgroups loop over several images
     (300, 14, 32, 64, 5, 1, 2, True),   # MNIST conv2 fwd
     (300, 32, 16, 16, 3, 1, 1, False),  # ResNet-20 stage 1
     (270, 16, 32, 32, 3, 2, 1, False),  # strided
+    (300, 28, 1, 32, 5, 1, 2, True),    # MNIST conv1 (shifted-copy kernel, B >= 256)
 ]
 
 
@@ -149,6 +150,7 @@ PERSIST_WG_CASES = [  # B >= 128: persistent register-accumulating kernel
     (260, 8, 64, 64, 3, 1, 1, False),
     (300, 32, 16, 16, 3, 1, 1, False),
     (200, 16, 16, 32, 3, 2, 1, False),  # strided
+    (300, 28, 1, 32, 5, 1, 2, True),    # MNIST conv1 (shifted-copy kernel + partial-sum reduce)
 ]
 
 
