@@ -173,6 +173,7 @@ def bench_resnet(args):
         prog.P.refresh_copies()
         ar = BucketAllReduce(prog.P.grad, _buckets(prog.P),
                              comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+        prog.grad_ready = ar.ready  # buckets launch during backward (overlap on RCCL's stream)
     n_pool = 4096 if args.model == "resnet20" else 512
     g = torch.Generator().manual_seed(rank + 11)
     pix = model.image * model.image * model.channels
@@ -189,8 +190,7 @@ def bench_resnet(args):
         prog.compute_grads()
         g16 = None
         if ar is not None:
-            for i in range(len(ar.buckets)):
-                ar.launch(i)
+            ar.flush()
             ar.wait()
             g16 = ar.grad16
         opt.step(grad16=g16, gscale=1.0 / world) if g16 is not None else opt.step(gscale=1.0 / world)

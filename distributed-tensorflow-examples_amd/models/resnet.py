@@ -330,7 +330,9 @@ def build(arch, reg):
         for stage, cout in enumerate((16, 32, 64)):
             for i in range(3):
                 stride = 2 if (stage > 0 and i == 0) else 1
+                n0 = len(reg.specs)
                 b = BasicBlock(reg, cin, cout, stride, H, H)
+                b.var_names = [sp.name for sp in reg.specs[n0:]]
                 blocks.append(b)
                 H, cin = b.OH, cout
         L["blocks"], L["feat"], L["HW"] = blocks, cin, H
@@ -344,7 +346,9 @@ def build(arch, reg):
         for stage, (width, n) in enumerate(((64, 3), (128, 4), (256, 6), (512, 3))):
             for i in range(n):
                 stride = 2 if (stage > 0 and i == 0) else 1
+                n0 = len(reg.specs)
                 b = Bottleneck(reg, cin, width, stride, H, H)
+                b.var_names = [sp.name for sp in reg.specs[n0:]]
                 blocks.append(b)
                 H, cin = b.OH, b.cout
         L["blocks"], L["feat"], L["HW"] = blocks, cin, H
@@ -431,6 +435,15 @@ class ResNetProgram(StepProgram):
         self.dfeat16 = torch.empty(B, d.cin, **bf)
         self.loss = torch.zeros(1, device=dev)
         self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+        # lowest flat offset of each block's variables: after block i's backward every gradient
+        # at or above it is final (variables are laid out in creation = forward order)
+        self.block_lo = [min(P.offsets[n] for n in b.var_names) for b in L["blocks"]]
+        self.dense_lo = min(P.offsets[d.kernel], P.offsets[d.bias])
+        self.grad_ready = None  # optional backward-progress hook (BucketAllReduce.ready)
+
+    def _ready(self, lo):
+        if self.grad_ready is not None:
+            self.grad_ready(lo)
 
     def load_batch(self, batch):
         x, y = batch
@@ -463,6 +476,7 @@ class ResNetProgram(StepProgram):
         ops.gemm(self.dlogits, self.feat, P.gview(d.kernel), M=d.cout, N=d.cin, K=B, amode=ops.RMAJ, lda=d.cout,
                  bmode=ops.RMAJ, ldb=d.cin)
         ops.colsum(self.dlogits, B, d.cout, d.cout, P.gview(d.bias))
+        self._ready(self.dense_lo)
         ops.gemm(self.dlogits, P.view(d.kernel), self.dfeat, M=B, N=d.cin, K=d.cout, bmode=ops.RMAJ, ldb=d.cin)
         ops.cast_(self.dfeat, self.dfeat16)
         ops.gap_bwd(self.dfeat16, self.d_last)
@@ -470,6 +484,7 @@ class ResNetProgram(StepProgram):
         blocks = L["blocks"]
         for i in range(len(blocks) - 1, -1, -1):
             blocks[i].bwd(dout, self.d_in[i])
+            self._ready(self.block_lo[i])
             dout = self.d_in[i]
         st = L["stem"]
         if "pool_hw" in L:
@@ -477,6 +492,7 @@ class ResNetProgram(StepProgram):
             dout = self.d_stem
         L["stem_bn"].bwd(dout, st.y, self.dc_stem)
         st.wgrad(self.dc_stem, self.x)
+        self._ready(0)
 
     def compute_grads(self):
         self.P.grad.zero_()

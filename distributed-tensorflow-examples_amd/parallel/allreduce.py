@@ -8,6 +8,10 @@ stream, ordered after the producer kernels by an event), so it overlaps the
 backward kernels that follow on the compute stream.  ``wait()`` joins the
 compute stream to every outstanding bucket before the optimizer.
 
+Programs that report backward progress call ``ready(lo)`` (every gradient at flat
+offset >= lo is final; buckets are ordered back to front, the order backward
+produces them) and ``flush()`` launches whatever is left.
+
 Optionally the wire format is bf16 (half the xGMI bytes): a cast kernel packs
 the bucket into a bf16 shadow buffer, the all-reduce runs on it, and the fused
 optimizer consumes the bf16 sums directly (``grad16``) with 1/world folded in.
@@ -31,6 +35,7 @@ class BucketAllReduce:
         if comm_dtype == torch.bfloat16:
             self.shadow = torch.empty(flat_grad.numel(), dtype=torch.bfloat16, device=flat_grad.device)
         self._works = []
+        self._next = 0  # next bucket (in launch order) not yet launched this step
 
     @property
     def grad16(self):
@@ -47,7 +52,22 @@ class BucketAllReduce:
             return
         self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
+    def ready(self, lo: int):
+        """Backward progress hook: every gradient at flat offset >= lo is final.  Launches the
+        buckets (in order) that lie entirely above lo, so their all-reduce overlaps the rest of
+        the backward pass."""
+        while self._next < len(self.buckets) and self.buckets[self._next][0] >= lo:
+            self.launch(self._next)
+            self._next += 1
+
+    def flush(self):
+        """Launch every bucket the backward hooks have not."""
+        while self._next < len(self.buckets):
+            self.launch(self._next)
+            self._next += 1
+
     def wait(self):
         for w in self._works:
             w.wait()
         self._works.clear()
+        self._next = 0

@@ -324,6 +324,8 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         prog.P.refresh_copies()
         ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), group=group,
                              comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
+        if hasattr(prog, "grad_ready"):  # programs that report backward progress overlap the all-reduce
+            prog.grad_ready = ar.ready
     data = read_data_sets(model, "" if flags.synthetic else flags.data_dir, one_hot=True, seed=flags.seed * 1000 + rank + 1,
                           log=log if is_chief else (lambda *_: None))
     feeder = Feeder(data, prog, device)
@@ -340,8 +342,7 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         g16 = None
         if ar is not None:
             with phase("comm"):
-                for i in range(len(ar.buckets)):
-                    ar.launch(i)
+                ar.flush()
                 ar.wait()
             g16 = ar.grad16
         with phase("apply"):

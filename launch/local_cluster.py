@@ -22,6 +22,7 @@ import threading
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPTS = {m: os.path.join(ROOT, "examples", m, "distributed_%s.py" % m) for m in ("gan", "encoder", "lstm",
                                                                                    "softmax", "cnn")}
+SCRIPTS.update({a: os.path.join(ROOT, "examples", "resnet", "distributed_%s.py" % a) for a in ("resnet20", "resnet50")})
 
 
 def free_ports(n):
