@@ -30,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 import dtfe  # noqa: E402,F401
 from dtfe.models.mnist_cnn import MnistCnnTrainer, num_params  # noqa: E402
 from dtfe.parallel.allreduce import BucketAllReduce  # noqa: E402
+from dtfe.parallel.rccl import RcclComm  # noqa: E402
 from dtfe.utils.graphs import StepGraph, graphs_enabled  # noqa: E402
 
 DEFAULT_BATCH = 1024  # per GPU
@@ -58,6 +59,9 @@ def main():
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
+    ap.add_argument("--comm", choices=["rccl", "pg"], default="rccl",
+                    help="rccl: dtfe's own RCCL communicator on a side stream, the whole step (all-reduce "
+                         "included) captured in one hipGraph; pg: torch.distributed ProcessGroupNCCL, eager steps")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
@@ -78,8 +82,11 @@ def main():
 
     allreduce = None
     trainer = MnistCnnTrainer(args.batch_size, device, seed=0, world_size=world)
+    comm = None
     if world > 1:
-        allreduce = BucketAllReduce(trainer.P.grad, trainer.buckets,
+        if args.backend == "nccl" and args.comm == "rccl":
+            comm = RcclComm(device)
+        allreduce = BucketAllReduce(trainer.P.grad, trainer.buckets, comm=comm,
                                     comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
         trainer.allreduce = allreduce
 
@@ -89,8 +96,9 @@ def main():
             trainer.opt.step(grad16=allreduce.grad16, gscale=1.0 / world)
     else:
         step = trainer.step
-    # world == 1: the whole step is one hipGraph replay
-    runner = StepGraph(step, warmup=2, enabled=(world == 1 and not args.no_graph and graphs_enabled()))
+    # the whole step (with the overlapped RCCL all-reduce at world > 1) is one hipGraph replay
+    runner = StepGraph(step, warmup=2, enabled=((world == 1 or comm is not None) and not args.no_graph
+                                                and graphs_enabled()), capture_error_mode="thread_local")
 
     for _ in range(args.warmup):
         runner()
@@ -136,7 +144,9 @@ def main():
                 "parallelism": "dp%d" % world,
                 "per_gpu_batch": args.batch_size,
                 "optimizer": "adam (TF1)",
-                "grad_allreduce": ("%s bucketed %s" % ("rccl" if args.backend == "nccl" else "gloo", args.comm_dtype))
+                "grad_allreduce": ("%s bucketed %s" % ("rccl (dtfe comm, in-graph)" if comm is not None else
+                                                       "rccl (ProcessGroupNCCL)" if args.backend == "nccl" else "gloo",
+                                                       args.comm_dtype))
                 if world > 1 else "none (1 rank)",
                 "hip_graph": runner.graph is not None,
                 "last_loss": round(loss, 4),
@@ -167,11 +177,12 @@ def bench_resnet(args):
     gstep = torch.zeros(1, dtype=torch.int32, device=device)
     cfg, names, bp = model.opt_groups[0]
     opt = Optimizer(cfg, prog.P, var_list=names, global_step=gstep, beta_power_names=bp)
-    ar = None
+    ar = comm = None
     if world > 1:
         dist.broadcast(prog.P.master, src=0)
         prog.P.refresh_copies()
-        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P),
+        comm = RcclComm(device) if args.comm == "rccl" else None
+        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), comm=comm,
                              comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
         prog.grad_ready = ar.ready  # buckets launch during backward (overlap on RCCL's stream)
     n_pool = 4096 if args.model == "resnet20" else 512
@@ -195,7 +206,8 @@ def bench_resnet(args):
             g16 = ar.grad16
         opt.step(grad16=g16, gscale=1.0 / world) if g16 is not None else opt.step(gscale=1.0 / world)
 
-    runner = StepGraph(step, warmup=2, enabled=(world == 1 and not args.no_graph and graphs_enabled()))
+    runner = StepGraph(step, warmup=2, enabled=((world == 1 or comm is not None) and not args.no_graph
+                                                and graphs_enabled()), capture_error_mode="thread_local")
     for _ in range(args.warmup):
         runner()
     torch.cuda.synchronize()

@@ -93,6 +93,8 @@ def build_kernels(jobs: int, verbose: bool) -> str:
     link = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", KERNEL_LIB + ".tmp"] + objs + [
         "-L" + libdir, "-Wl,-rpath," + libdir,
         "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip",
+        # RCCL: the librccl torch ships (same soname torch already loaded), for bindings/comm_ops.cpp
+        "-lrccl",
     ]
     _run(link, verbose)
     os.replace(KERNEL_LIB + ".tmp", KERNEL_LIB)

@@ -12,6 +12,12 @@ Programs that report backward progress call ``ready(lo)`` (every gradient at fla
 offset >= lo is final; buckets are ordered back to front, the order backward
 produces them) and ``flush()`` launches whatever is left.
 
+With ``comm`` (a ``parallel.rccl.RcclComm``) the buckets go through dtfe's own RCCL
+communicator on a side HIP stream forked from the compute stream instead of
+ProcessGroupNCCL: every launch / join is a plain stream operation, so a whole
+data-parallel step - backward, overlapped all-reduce, optimizer - can be captured
+into one hipGraph (bench.py, train.py at world > 1).
+
 Optionally the wire format is bf16 (half the xGMI bytes): a cast kernel packs
 the bucket into a bf16 shadow buffer, the all-reduce runs on it, and the fused
 optimizer consumes the bf16 sums directly (``grad16``) with 1/world folded in.
@@ -25,8 +31,11 @@ from .. import ops
 
 
 class BucketAllReduce:
-    def __init__(self, flat_grad: torch.Tensor, buckets, group=None, comm_dtype=torch.float32):
+    def __init__(self, flat_grad: torch.Tensor, buckets, group=None, comm_dtype=torch.float32, comm=None):
         self.flat = flat_grad
+        self.comm = comm
+        self.side = torch.cuda.Stream(device=flat_grad.device) if comm is not None else None
+        self._forked = False
         self.buckets = list(buckets)
         self.group = group
         self.comm_dtype = comm_dtype
@@ -48,6 +57,13 @@ class BucketAllReduce:
             buf = self.shadow[lo:hi]
         else:
             buf = self.flat[lo:hi]
+        if self.comm is not None:
+            # fork: the side stream waits for everything enqueued so far (the bucket's producers)
+            self.side.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(self.side):
+                self.comm.all_reduce(buf)
+            self._forked = True
+            return
         if self.world == 1:
             return
         self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
@@ -67,6 +83,9 @@ class BucketAllReduce:
             self._next += 1
 
     def wait(self):
+        if self._forked:  # join the side stream back into the compute stream
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.side)
+            self._forked = False
         for w in self._works:
             w.wait()
         self._works.clear()

@@ -37,6 +37,7 @@ from .models.softmax_reg import SoftmaxRegressionModel
 from .models.autoencoder import LR as ENC_LR
 from .optim import Optimizer
 from .parallel.allreduce import BucketAllReduce
+from .parallel.rccl import RcclComm
 from .parallel.cluster import ClusterSpec, Server
 from .parallel.health import Heartbeat, Watchdog
 from .utils.faults import FaultInjector
@@ -322,7 +323,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                 if b is not None:
                     dist.broadcast(b, src=0, group=group)
         prog.P.refresh_copies()
-        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), group=group,
+        # on GPUs the buckets go through dtfe's own RCCL communicator (capturable: the whole step,
+        # all-reduce included, replays as one hipGraph); gloo / CPU keeps ProcessGroup collectives
+        comm = RcclComm(device, group) if device.type == "cuda" and dist.get_backend(group) != "gloo" else None
+        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), group=group, comm=comm,
                              comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
         if hasattr(prog, "grad_ready"):  # programs that report backward progress overlap the all-reduce
             prog.grad_ready = ar.ready
@@ -351,8 +355,9 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                 o.step(grad16=g16, gscale=1.0 / world, gs_inc=model.gs_increments if last else 0) if g16 is not None \
                     else o.step(gscale=1.0 / world, gs_inc=model.gs_increments if last else 0)
 
-    runner = StepGraph(train_step, warmup=2,
-                       enabled=device.type == "cuda" and world == 1 and flags.hip_graph and timer is None)
+    runner = StepGraph(train_step, warmup=2, capture_error_mode="thread_local",
+                       enabled=(device.type == "cuda" and (world == 1 or ar.comm is not None) and flags.hip_graph
+                                and timer is None))
     begin_time = time.time()
     step = int(gstep.item())
     local_step = 0

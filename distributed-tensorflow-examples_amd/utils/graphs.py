@@ -23,8 +23,12 @@ def graphs_enabled(default: bool = True) -> bool:
 class StepGraph:
     """Capture ``fn`` (no args) into a hipGraph after ``warmup`` eager runs."""
 
-    def __init__(self, fn, warmup: int = 2, enabled: bool = True, pool=None):
+    def __init__(self, fn, warmup: int = 2, enabled: bool = True, pool=None, capture_error_mode: str = "global"):
+        """capture_error_mode "thread_local": only this thread's capture-unsafe HIP calls
+        invalidate the capture (other threads - e.g. the c10d watchdog - may keep polling
+        their own events while a step with an in-graph RCCL all-reduce is recorded)."""
         self.fn = fn
+        self.capture_error_mode = capture_error_mode
         self.warmup = warmup
         self.enabled = enabled and torch.cuda.is_available()
         self.graph = None
@@ -47,7 +51,7 @@ class StepGraph:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, pool=self.pool, stream=s):
+                with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode=self.capture_error_mode):
                     self.fn()
             torch.cuda.current_stream().wait_stream(s)
             self.graph = g
