@@ -35,6 +35,7 @@ all-reduced over RCCL while the conv backward kernels still run.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -183,6 +184,15 @@ class MnistCnnTrainer:
         lo1, hi1 = P.range_of([n["out"], n["bout"], n["bd1"], n["wd1"]])
         lo2, hi2 = P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
         self.buckets = [(lo1, hi1), (lo2, hi2)]
+        # backward branches that do not feed the critical path (head/fc1 weight grads, conv2
+        # weight grad) run on their own streams: inside the captured hipGraph they become
+        # parallel branches that fill the CUs the dgrad chain leaves idle.  conv2's weight
+        # grad gets its own partial-sum workspace (conv1's runs concurrently on the main stream).
+        self.par = self.device.type == "cuda"
+        if self.par:
+            self.s_fc = torch.cuda.Stream(device=d)
+            self.s_c2 = torch.cuda.Stream(device=d)
+            self.ws_c2 = torch.empty(256 * (C2 * KS * KS * C1 + C2), device=d, dtype=torch.float32)
 
     # ------------------------------------------------------------------
     def forward_backward(self):
@@ -203,27 +213,42 @@ class MnistCnnTrainer:
                  keep=self.keep, seed=self.seed + 2, counter=self.data_ctr)
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
-        # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
-        ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
-                 bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
-                 splits=max(1, min(16, B // 128)), tile=4)
+        main = torch.cuda.current_stream(self.device) if self.par else None
+        with self._branch(self.s_fc if self.par else None, main):
+            # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
+            ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
+                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
+                     splits=max(1, min(16, B // 128)), tile=4)
+            # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
+            ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
+                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
+            if self.allreduce is not None:  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
+                self.allreduce.launch(0)
         # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
                  aux_act=ops.ACT_RELU)
-        # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
-        ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
-                 ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
-        if self.allreduce is not None:
-            self.allreduce.launch(0)
+        with self._branch(self.s_c2 if self.par else None, main):
+            # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
+            ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
+                         workspace=self.ws_c2 if self.par else None, **self.ic2)
         # conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)
         ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
                     flip_taps=True, **self.ic2_dgrad)
-        # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
-        ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2, **self.ic2)
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
+        if self.par:  # join the weight-grad branches
+            main.wait_stream(self.s_fc)
+            main.wait_stream(self.s_c2)
         if self.allreduce is not None:
             self.allreduce.launch(1)
             self.allreduce.wait()
+
+    @staticmethod
+    def _branch(stream, main):
+        """Run the enclosed launches on ``stream`` forked from ``main`` (no-op without one)."""
+        if stream is None:
+            return contextlib.nullcontext()
+        stream.wait_stream(main)
+        return torch.cuda.stream(stream)
 
     def apply(self):
         self.opt.step(gscale=1.0 / self.world)

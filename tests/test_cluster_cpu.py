@@ -59,7 +59,7 @@ def test_chief_restart_restores_global_step(tmp_path):
     assert saved > 0
     codes, out, _ = local_cluster.launch("softmax", 1, 1, args + ["--num_steps=%d" % (saved + 10)], timeout=240,
                                          stream=False)
-    assert all(c == 0 for c in codes.values()), out
+    assert all(c == 0 for c in codes.values()), (codes, {k: v[-12:] for k, v in out.items()})
     gs = _gs_lines(out[("worker", 0)])
     assert gs[0] == saved + 1, (saved, gs[:3])  # resumed, not re-initialised (LSTM-style correct resume)
 
