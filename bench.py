@@ -30,7 +30,7 @@ import torch.distributed as dist  # noqa: E402
 import dtfe  # noqa: E402,F401
 from dtfe.models.mnist_cnn import MnistCnnTrainer, num_params  # noqa: E402
 from dtfe.parallel.allreduce import BucketAllReduce  # noqa: E402
-from dtfe.parallel.rccl import RcclComm  # noqa: E402
+from dtfe.parallel.comm import make_comm  # noqa: E402
 from dtfe.utils.graphs import StepGraph, graphs_enabled  # noqa: E402
 
 DEFAULT_BATCH = 1024  # per GPU
@@ -59,9 +59,10 @@ def main():
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
-    ap.add_argument("--comm", choices=["rccl", "pg"], default="rccl",
-                    help="rccl: dtfe's own RCCL communicator on a side stream, the whole step (all-reduce "
-                         "included) captured in one hipGraph; pg: torch.distributed ProcessGroupNCCL, eager steps")
+    ap.add_argument("--comm", choices=["auto", "rccl", "ipc", "pg"], default="auto",
+                    help="auto: per bucket size the faster of dtfe's RCCL communicator and the hipIpc two-shot "
+                         "kernel (timed at setup); rccl / ipc: force one; all three run on a side stream with the "
+                         "whole step captured in one hipGraph.  pg: torch.distributed ProcessGroupNCCL, eager steps")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
@@ -84,8 +85,11 @@ def main():
     trainer = MnistCnnTrainer(args.batch_size, device, seed=0, world_size=world)
     comm = None
     if world > 1:
-        if args.backend == "nccl" and args.comm == "rccl":
-            comm = RcclComm(device)
+        if args.comm != "pg" and (args.backend == "nccl" or args.comm == "ipc"):
+            esz = 2 if args.comm_dtype == "bf16" else 4
+            comm = make_comm(device, None, [(hi - lo) * esz for lo, hi in trainer.buckets],
+                             torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, mode=args.comm,
+                             log=(lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None)
         allreduce = BucketAllReduce(trainer.P.grad, trainer.buckets, comm=comm,
                                     comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
         trainer.allreduce = allreduce
@@ -144,7 +148,7 @@ def main():
                 "parallelism": "dp%d" % world,
                 "per_gpu_batch": args.batch_size,
                 "optimizer": "adam (TF1)",
-                "grad_allreduce": ("%s bucketed %s" % ("rccl (dtfe comm, in-graph)" if comm is not None else
+                "grad_allreduce": ("%s bucketed %s" % ("in-graph [%s]" % comm.describe() if comm is not None else
                                                        "rccl (ProcessGroupNCCL)" if args.backend == "nccl" else "gloo",
                                                        args.comm_dtype))
                 if world > 1 else "none (1 rank)",
@@ -181,8 +185,13 @@ def bench_resnet(args):
     if world > 1:
         dist.broadcast(prog.P.master, src=0)
         prog.P.refresh_copies()
-        comm = RcclComm(device) if args.comm == "rccl" else None
-        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), comm=comm,
+        bks = _buckets(prog.P)
+        esz = 2 if args.comm_dtype == "bf16" else 4
+        comm = make_comm(device, None, [(hi - lo) * esz for lo, hi in bks],
+                         torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, mode=args.comm,
+                         log=(lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None) \
+            if args.comm != "pg" else None
+        ar = BucketAllReduce(prog.P.grad, bks, comm=comm,
                              comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
         prog.grad_ready = ar.ready  # buckets launch during backward (overlap on RCCL's stream)
     n_pool = 4096 if args.model == "resnet20" else 512

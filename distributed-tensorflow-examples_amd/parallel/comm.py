@@ -1,0 +1,108 @@
+"""Gradient-collective selection for the data-parallel modes.
+
+Two capturable all-reduce engines exist (both issue on the caller's current stream):
+
+* ``RcclComm`` - dtfe's own RCCL communicator (ring / tree channels over xGMI);
+* ``IpcComm``  - the one-launch hipIpc two-shot kernel reading the 7 peers directly.
+
+``make_comm(mode="auto")`` builds both, self-checks the IPC path, then times each on the
+actual bucket sizes of the job (max over ranks, so every rank takes the same decision)
+and routes every bucket size to the faster engine.  An IPC failure of any kind degrades
+to RCCL instead of failing the job.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .ipc import IpcComm
+from .rccl import RcclComm
+
+
+class RoutedComm:
+    """``all_reduce`` dispatching on the tensor's byte size (decided once, at setup)."""
+
+    def __init__(self, default, routes=None, names=None):
+        self.default = default
+        self.routes = dict(routes or {})
+        self.names = dict(names or {})
+        self.comms = [default] + [c for c in self.routes.values() if c is not default]
+
+    def all_reduce(self, t: torch.Tensor, *args):
+        self.routes.get(t.numel() * t.element_size(), self.default).all_reduce(t, *args)
+
+    def describe(self) -> str:
+        if not self.names:
+            return type(self.default).__name__
+        return ", ".join("%.2fMB:%s" % (b / 1e6, n) for b, n in sorted(self.names.items()))
+
+    def close(self):
+        for c in self.comms:
+            c.close()
+
+
+def _time_comm(comm, t, group, iters=8):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        comm.all_reduce(t)
+    torch.cuda.synchronize()
+    dist.barrier(group=group)
+    s.record()
+    for _ in range(iters):
+        comm.all_reduce(t)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def _cpu_ok(group):
+    """True when the group can reduce a CPU tensor (gloo, or a cpu:gloo,cuda:nccl group)."""
+    try:
+        return "gloo" in str(dist.get_backend(group))
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def _agree(x: float, group, device) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if _cpu_ok(group) else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: str = "auto", log=None):
+    """Collective engine for buckets of the given byte sizes.  mode: rccl | ipc | auto."""
+    device = torch.device(device)
+    cap = max([int(b) for b in bucket_bytes] + [1 << 20]) + 4096
+    if mode == "ipc":  # IPC only (no RCCL communicator: also works for several ranks sharing one GPU)
+        ipc = IpcComm(device, group, cap_bytes=cap)
+        return RoutedComm(ipc, {int(b): ipc for b in bucket_bytes}, {int(b): "ipc" for b in bucket_bytes})
+    rccl = RcclComm(device, group)
+    if mode == "rccl":
+        return RoutedComm(rccl)
+    ipc = None
+    try:
+        ipc = IpcComm(device, group, cap_bytes=cap, fallback=rccl)
+        ok = 1.0
+    except Exception as e:  # noqa: BLE001 - any IPC trouble (mapping, self-check, timeout) -> RCCL
+        ok = 0.0
+        if log:
+            log("ipc all-reduce unavailable (%s); using RCCL" % (e,))
+    if _agree(1.0 - ok, group, device) > 0:   # one rank failed: nobody uses IPC
+        if ipc is not None:
+            ipc.close()
+        return RoutedComm(rccl)
+    routes, names = {}, {}
+    esz = torch.tensor([], dtype=dtype).element_size()
+    for b in sorted(set(int(x) for x in bucket_bytes)):
+        t = torch.zeros(max(1, b // esz), dtype=dtype, device=device)
+        t_r = _agree(_time_comm(rccl, t, group), group, device)
+        t_i = _agree(_time_comm(ipc, t, group), group, device)
+        routes[b] = ipc if t_i < t_r else rccl
+        names[b] = "ipc" if t_i < t_r else "rccl"
+        if log:
+            log("all-reduce %.2f MB %s: rccl %.1f us, ipc %.1f us -> %s"
+                % (b / 1e6, dtype, t_r * 1e3, t_i * 1e3, names[b]))
+    if _agree(float(ipc.status()), group, device) != 0:   # a timing run tripped a barrier timeout somewhere
+        ipc.close()
+        return RoutedComm(rccl)
+    return RoutedComm(rccl, routes, names)

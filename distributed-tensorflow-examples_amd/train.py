@@ -37,7 +37,7 @@ from .models.softmax_reg import SoftmaxRegressionModel
 from .models.autoencoder import LR as ENC_LR
 from .optim import Optimizer
 from .parallel.allreduce import BucketAllReduce
-from .parallel.rccl import RcclComm
+from .parallel.comm import make_comm
 from .parallel.cluster import ClusterSpec, Server
 from .parallel.health import Heartbeat, Watchdog
 from .utils.faults import FaultInjector
@@ -325,8 +325,13 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         prog.P.refresh_copies()
         # on GPUs the buckets go through dtfe's own RCCL communicator (capturable: the whole step,
         # all-reduce included, replays as one hipGraph); gloo / CPU keeps ProcessGroup collectives
-        comm = RcclComm(device, group) if device.type == "cuda" and dist.get_backend(group) != "gloo" else None
-        ar = BucketAllReduce(prog.P.grad, _buckets(prog.P), group=group, comm=comm,
+        bks = _buckets(prog.P)
+        comm = None
+        if device.type == "cuda" and dist.get_backend(group) != "gloo" and flags.comm != "pg":
+            cdt = torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32
+            comm = make_comm(device, group, [(hi - lo) * (2 if cdt == torch.bfloat16 else 4) for lo, hi in bks], cdt,
+                             mode=flags.comm, log=log if is_chief else None)
+        ar = BucketAllReduce(prog.P.grad, bks, group=group, comm=comm,
                              comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
         if hasattr(prog, "grad_ready"):  # programs that report backward progress overlap the all-reduce
             prog.grad_ready = ar.ready

@@ -64,6 +64,9 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     add_bool(ap, "hip_graph", True, "capture the per-step kernels into a hipGraph (GPU)")
     ap.add_argument("--log_every", type=int, default=1, help="print the per-step line every N local steps")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--comm", choices=["auto", "rccl", "ipc", "pg"], default="auto",
+                    help="all-reduce engine on GPUs: auto = faster of RCCL / hipIpc two-shot per bucket size "
+                         "(both in-graph); pg = torch.distributed ProcessGroupNCCL (eager)")
     ap.add_argument("--metrics_jsonl", default="", help="append {step, gs, ms, images/sec, loss} lines here")
     ap.add_argument("--heartbeat_secs", type=float, default=0.0,
                     help="publish a TCPStore heartbeat every N s (0: off, the reference has none)")

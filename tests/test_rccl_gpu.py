@@ -119,3 +119,25 @@ def test_mnist_cnn_step_with_rccl_bucket_graph(pg):
         assert ops.available()
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("mode", ["auto", "rccl", "ipc"])
+def test_make_comm_routes(pg, mode):
+    from dtfe.parallel.comm import make_comm
+
+    dev = torch.device("cuda", 0)
+    sizes = [6 << 20, 1 << 16]
+    comm = make_comm(dev, None, sizes, torch.bfloat16, mode=mode)
+    try:
+        for b in sizes:
+            x = torch.randn(b // 2, device=dev).to(torch.bfloat16)
+            ref = x.clone()
+            comm.all_reduce(x)
+            torch.cuda.synchronize()
+            assert torch.equal(x, ref)
+        d = comm.describe()
+        assert isinstance(d, str) and d
+        if mode == "ipc":
+            assert "rccl" not in d
+    finally:
+        comm.close()
