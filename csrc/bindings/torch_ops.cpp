@@ -333,9 +333,17 @@ int data_code(const Tensor& t) {
 
 void gather_rows(const Tensor& src, const Tensor& dst, const optional<Tensor>& idx, const optional<Tensor>& labels_src,
                  const optional<Tensor>& labels_dst, int64_t seed, const optional<Tensor>& counter,
-                 const optional<Tensor>& done) {
+                 const optional<Tensor>& done, at::TensorList zero) {
   check_cuda(src, "src");
   dtfe::GatherArgs a{};
+  TORCH_CHECK(zero.size() <= 4, "gather_rows: at most 4 zero ranges");
+  for (const Tensor& z : zero) {
+    check_cuda(z, "zero");
+    TORCH_CHECK(z.is_contiguous() && (z.numel() * z.element_size()) % 4 == 0, "gather_rows: zero ranges must be "
+                "contiguous whole 32-bit words");
+    a.zptr[a.nz] = reinterpret_cast<uint32_t*>(z.data_ptr());
+    a.zlen[a.nz++] = (long)(z.numel() * z.element_size() / 4);
+  }
   a.src = src.data_ptr(); a.src_dtype = data_code(src); a.n_rows = src.size(0); a.D = (int)(src.numel() / src.size(0));
   a.dst = dst.data_ptr(); a.dst_dtype = data_code(dst); a.B = (int)dst.size(0);
   TORCH_CHECK(a.dst_dtype != 0, "gather_rows: dst must be f32 or bf16");
@@ -609,7 +617,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork) -> ()");
   m.def(
       "gather_rows(Tensor src, Tensor(a!) dst, Tensor? idx, Tensor? labels_src, Tensor(b!)? labels_dst, int seed,"
-      " Tensor(c!)? counter, Tensor(d!)? done) -> ()");
+      " Tensor(c!)? counter, Tensor(d!)? done, Tensor(e!)[] zero) -> ()");
   m.def("uniform_fill(Tensor(a!) out, float lo, float hi, int seed, Tensor(b!)? counter, Tensor(c!)? done) -> ()");
   m.def("cast_(Tensor src, Tensor(a!) dst) -> ()");
   m.def(

@@ -14,6 +14,9 @@ struct GatherArgs {
   const int32_t* idx;
   const int32_t* labels_src; int32_t* labels_dst;
   uint64_t seed; int64_t* counter; uint32_t* done;
+  // step-prologue zeroing fused into the same launch: up to 4 word ranges (accumulators the
+  // step's atomics add into - loss / hit counters, atomically reduced weight grads)
+  uint32_t* zptr[4]; long zlen[4]; int nz;
 };
 void launch_gather_rows(const GatherArgs& a, hipStream_t s);
 

@@ -88,6 +88,8 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
       }
     }
   }
+  for (int z = 0; z < a.nz; ++z)
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < a.zlen[z]; i += (long)gridDim.x * 256) a.zptr[z][i] = 0u;
   advance_counter_last_block(a.counter, a.done, 1);
 }
 

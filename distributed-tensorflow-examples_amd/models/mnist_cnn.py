@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 
 import torch
 
@@ -184,11 +185,20 @@ class MnistCnnTrainer:
         lo1, hi1 = P.range_of([n["out"], n["bout"], n["bd1"], n["wd1"]])
         lo2, hi2 = P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
         self.buckets = [(lo1, hi1), (lo2, hi2)]
+        # the only step state that is accumulated into (atomics) rather than stored: the head
+        # weight grad (split-K atomics), the conv weight grads (partial-sum reduce), the loss /
+        # hit counters.  fc1's weight + bias grads (98% of P.grad) are plain stores.
+        ra = P.range_of([n["out"], n["bout"]])
+        rc = P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
+        self.accum = [P.grad[ra[0]:ra[1]], P.grad[rc[0]:rc[1]], self.loss_sum, self.correct]
         # backward branches that do not feed the critical path (head/fc1 weight grads, conv2
         # weight grad) run on their own streams: inside the captured hipGraph they become
         # parallel branches that fill the CUs the dgrad chain leaves idle.  conv2's weight
         # grad gets its own partial-sum workspace (conv1's runs concurrently on the main stream).
-        self.par = self.device.type == "cuda"
+        br = os.environ.get("DTFE_CNN_BRANCHES", "fc,c2").split(",")
+        self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2"})
+        self.br_fc = self.par and "fc" in br
+        self.br_c2 = self.par and "c2" in br
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
@@ -197,13 +207,12 @@ class MnistCnnTrainer:
     # ------------------------------------------------------------------
     def forward_backward(self):
         B = self.B
-        P = self.P
-        P.grad.zero_()
-        self.loss_sum.zero_()
-        self.correct.zero_()
-        if self.data is not None:  # standalone: sample the batch on device (advances data_ctr)
+        if self.data is not None:  # standalone: sample the batch on device (advances data_ctr) and clear
             ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
-                            seed=self.seed + 1, counter=self.data_ctr, done=self.data_done)
+                            seed=self.seed + 1, counter=self.data_ctr, done=self.data_done, zero=self.accum)
+        else:
+            for t in self.accum:
+                t.zero_()
         ops.imgconv(self.w["wc1"], self.p1, src=self.x, bias=self.b["bc1"], argmax=self.a1, act=ops.ACT_RELU,
                     pool=True, **self.ic1)
         ops.imgconv(self.w["wc2"], self.p2, src=self.p1, bias=self.b["bc2"], argmax=self.a2, act=ops.ACT_RELU,
@@ -214,7 +223,7 @@ class MnistCnnTrainer:
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
         main = torch.cuda.current_stream(self.device) if self.par else None
-        with self._branch(self.s_fc if self.par else None, main):
+        with self._branch(self.s_fc if self.br_fc else None, main):
             # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
             ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
                      bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
@@ -227,16 +236,17 @@ class MnistCnnTrainer:
         # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
                  aux_act=ops.ACT_RELU)
-        with self._branch(self.s_c2 if self.par else None, main):
+        with self._branch(self.s_c2 if self.br_c2 else None, main):
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                         workspace=self.ws_c2 if self.par else None, **self.ic2)
+                         workspace=self.ws_c2 if self.br_c2 else None, **self.ic2)
         # conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)
         ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
                     flip_taps=True, **self.ic2_dgrad)
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
-        if self.par:  # join the weight-grad branches
+        if self.br_fc:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
+        if self.br_c2:
             main.wait_stream(self.s_c2)
         if self.allreduce is not None:
             self.allreduce.launch(1)

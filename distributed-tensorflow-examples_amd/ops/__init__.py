@@ -417,10 +417,14 @@ def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, mome
 
 
 # ------------------------------------------------------------- elementwise
-def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, counter=None, done=None):
+def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, counter=None, done=None, zero=()):
+    """dst[b] = src[row(b)] (+ labels); ``zero``: up to 4 contiguous tensors cleared in the same
+    launch (a step's accumulators), saving one fill kernel each."""
     if dst.is_cuda:
-        require().gather_rows(src, dst, idx, labels_src, labels_dst, seed, counter, done)
+        require().gather_rows(src, dst, idx, labels_src, labels_dst, seed, counter, done, list(zero))
         return dst
+    for z in zero:
+        z.zero_()
     assert idx is not None, "CPU gather needs explicit indices"
     rows = src[idx.long()]
     if src.dtype == torch.uint8:

@@ -86,3 +86,30 @@ def test_cnn_trains_and_graph_replays():
     assert run.graph is not None, run.capture_error
     assert losses[-1] < 0.5 * losses[0]
     assert int(tr.global_step.item()) == 60
+
+
+@pytest.mark.parametrize("branches", ["fc,c2", "fc", "none"])
+def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
+    """Only the atomically-accumulated grads are cleared per step (fused into the batch gather);
+    every other gradient must be fully overwritten: the same batch twice -> the same grads,
+    and the result matches autograd after a previous step left garbage behind."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    monkeypatch.setenv("DTFE_CNN_BRANCHES", branches)
+    tr = MnistCnnTrainer(64, "cuda", keep_prob=1.0, seed=5)
+    tr.P.grad.fill_(7.0)            # stale values everywhere
+    tr.loss_sum.fill_(3.0)
+    ctr0 = int(tr.data_ctr.item())
+    tr.forward_backward()
+    g1 = tr.P.grad.clone()
+    l1 = tr.loss_sum.clone()
+    tr.data_ctr.fill_(ctr0)         # same batch again
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(tr.P.grad, g1, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(tr.loss_sum, l1, rtol=1e-5)
+    loss_ref, grads = _reference_grads(tr)
+    assert abs(tr.loss_sum.item() / tr.B - loss_ref) < 2e-2 * max(1.0, abs(loss_ref))
+    for k, gref in grads.items():
+        got = tr.gw[k].detach().cpu()
+        assert ((got - gref).norm() / (gref.norm() + 1e-12)).item() < 3e-2, k
