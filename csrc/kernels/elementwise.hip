@@ -266,9 +266,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* x, int x_f32, i
   }
 }
 void launch_colsum(const void* x, int x_f32, int M, int N, long ld, float* db, float scale, hipStream_t s) {
+  // enough row groups that each thread sums only a few rows (the sums are latency-bound
+  // dependent chains otherwise) while the grid still fills the CUs
   int gx = (N + 63) / 64;
-  int gy = (M + 255) / 256;
-  if (gy > 64) gy = 64;
+  int gy = (M + 31) / 32;
+  if (gy * gx > 1024) gy = (1024 + gx - 1) / gx;
   if (gy < 1) gy = 1;
   hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, s, x, x_f32, M, N, ld, db, scale);
 }

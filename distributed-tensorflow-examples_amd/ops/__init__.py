@@ -49,6 +49,19 @@ def split_workspace(device, splits, M, N, tile):
     return ws, ctr
 
 
+def auto_splits(M: int, N: int, K: int, tile: int) -> int:
+    """Split-K factor for an under-filled GEMM (few output tiles, long K: the small dense layers
+    of the reference models, a weight gradient reducing over T*B rows) so the grid reaches
+    ~256 workgroups; the last-arriving split runs the fused epilogue (deterministic order).
+    Uses the shared per-device workspace: GEMMs issued concurrently on several streams must not
+    rely on it (pass splits / workspace explicitly)."""
+    bm, bn = TILE_DIMS[tile]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    if tiles >= 128 or K < 4 * GEMM_KTILE:
+        return 1
+    return max(1, min(math.ceil(256 / tiles), K // (2 * GEMM_KTILE), 16))
+
+
 def pick_tile(M: int, N: int) -> int:
     """Largest MFMA tile that still yields >= one workgroup per CU (256 CUs)."""
     if M <= 32 and N <= 32:
@@ -56,7 +69,8 @@ def pick_tile(M: int, N: int) -> int:
     for tid, bm, bn in _TILES:
         if math.ceil(M / bm) * math.ceil(N / bn) >= 256:
             return tid
-    return 0
+    # small outputs: 32x32 tiles quadruple the workgroups of 64x64 (split-K adds more if K allows)
+    return 4 if math.ceil(M / 64) * math.ceil(N / 64) < 64 else 0
 
 
 # --------------------------------------------------------------- references
@@ -127,6 +141,8 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
     if out.is_cuda:
         if tile is None:
             tile = pick_tile(M, N)
+            if splits == 1 and not atomic and workspace is None:
+                splits = auto_splits(M, N, K, tile)
         ws = ctr = None
         if splits > 1 and not atomic:
             ws, ctr = workspace if workspace is not None else split_workspace(out.device, splits, M, N, tile)
