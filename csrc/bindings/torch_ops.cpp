@@ -15,6 +15,7 @@
 #include "../kernels/elementwise.h"
 #include "../kernels/gemm_dense.h"
 #include "../kernels/head.h"
+#include "../kernels/lstm_seq.h"
 #include "../kernels/optim.h"
 
 using at::Tensor;
@@ -454,6 +455,35 @@ void lstm_cell_bwd(const Tensor& act, const optional<Tensor>& c_prev, const Tens
   dtfe::launch_lstm_cell_bwd(a, cur_stream());
 }
 
+// whole-sequence LSTM (lstm_seq.hip): returns false when the shape needs the per-step path
+bool lstm_seq_fwd(const Tensor& xh, const Tensor& K, const Tensor& bias, double forget_bias, const Tensor& act,
+                  const Tensor& c, const Tensor& hT) {
+  check_cuda(xh, "xh");
+  TORCH_CHECK(xh.dim() == 3 && xh.scalar_type() == at::kFloat && xh.is_contiguous(), "lstm_seq_fwd: xh [T][B][I+H] f32");
+  dtfe::LstmSeqArgs a{};
+  a.T = (int)xh.size(0); a.B = (int)xh.size(1); a.H = (int)hT.size(1); a.I = (int)xh.size(2) - a.H;
+  TORCH_CHECK(K.numel() == (int64_t)(a.I + a.H) * 4 * a.H && bias.numel() == 4 * a.H, "lstm_seq_fwd: K/bias shape");
+  TORCH_CHECK(act.numel() == (int64_t)a.T * a.B * 4 * a.H && c.numel() == (int64_t)a.T * a.B * a.H &&
+              hT.numel() == (int64_t)a.B * a.H, "lstm_seq_fwd: output shapes");
+  a.xh = xh.data_ptr<float>(); a.K = K.data_ptr<float>(); a.bias = bias.data_ptr<float>();
+  a.forget_bias = (float)forget_bias; a.act = act.data_ptr<float>(); a.c = c.data_ptr<float>();
+  a.hT = hT.data_ptr<float>();
+  return dtfe::launch_lstm_seq_fwd(a, cur_stream());
+}
+
+bool lstm_seq_bwd(const Tensor& K, const Tensor& act, const Tensor& c, const Tensor& dhT, const Tensor& dg,
+                  int64_t I) {
+  check_cuda(act, "act");
+  dtfe::LstmSeqArgs a{};
+  a.T = (int)c.size(0); a.B = (int)c.size(1); a.H = (int)c.size(2); a.I = (int)I;
+  TORCH_CHECK(K.numel() == (int64_t)(a.I + a.H) * 4 * a.H, "lstm_seq_bwd: K shape");
+  TORCH_CHECK(act.numel() == (int64_t)a.T * a.B * 4 * a.H && dg.numel() == act.numel() &&
+              dhT.numel() == (int64_t)a.B * a.H, "lstm_seq_bwd: shapes");
+  a.K = K.data_ptr<float>(); a.act = act.data_ptr<float>(); a.c = c.data_ptr<float>();
+  a.dhT = dhT.data_ptr<float>(); a.dg = dg.data_ptr<float>();
+  return dtfe::launch_lstm_seq_bwd(a, cur_stream());
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------- norm
@@ -566,6 +596,9 @@ void maxpool3_bwd(const Tensor& dy, const Tensor& am, const Tensor& dx) {
 }
 
 TORCH_LIBRARY(dtfe, m) {
+  m.def("lstm_seq_fwd(Tensor(a!) xh, Tensor K, Tensor bias, float forget_bias, Tensor(b!) act, Tensor(c!) c,"
+        " Tensor(d!) hT) -> bool");
+  m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I) -> bool");
   m.def("bn_stats(Tensor x, Tensor(a!) stats) -> ()");
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
@@ -633,6 +666,8 @@ TORCH_LIBRARY(dtfe, m) {
 }
 
 TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
+  m.impl("lstm_seq_fwd", &lstm_seq_fwd);
+  m.impl("lstm_seq_bwd", &lstm_seq_bwd);
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
   m.impl("bn_bwd_stats", &bn_bwd_stats);

@@ -1,0 +1,24 @@
+// Persistent whole-sequence LSTM forward / BPTT.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dtfe {
+
+struct LstmSeqArgs {
+  int T, B, I, H;
+  float* xh;          // [T][B][I+H]: x_t rows given; h_{t-1} columns of steps 1..T-1 written by the forward
+  const float* K;     // [I+H][4H] (TF kernel layout: rows x then h; columns gates i, j, f, o)
+  const float* bias;  // [4H]
+  float forget_bias;
+  float* act;         // [T][B][4H] activated gates (forward out, backward in)
+  float* c;           // [T][B][H]
+  float* hT;          // [B][H] last hidden state
+  const float* dhT;   // [B][H] d loss / d h_T (backward in)
+  float* dg;          // [T][B][4H] gate pre-activation grads (backward out)
+};
+
+// false when the shape is not supported (H != 128, B % 16, (I+H) % 4): callers fall back
+bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s);
+bool launch_lstm_seq_bwd(const LstmSeqArgs& a, hipStream_t s);
+
+}  // namespace dtfe

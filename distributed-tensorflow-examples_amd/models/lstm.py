@@ -11,9 +11,14 @@ row buffer (h_{t-1} is written straight into it by the previous cell kernel),
 so each timestep is one exact-fp32 MFMA GEMM + one fused cell kernel; BPTT is
 one fused cell-backward kernel + one dgrad GEMM per step, and the kernel
 gradient is a single [156 x 512] GEMM reducing over all T*B rows at the end
-(TF accumulates 28 separate MatMul grads).
+(TF accumulates 28 separate MatMul grads).  On the GPU the whole forward
+recurrence and the whole BPTT recurrence are each ONE persistent kernel
+(csrc/kernels/lstm_seq.hip); the per-step path remains for the
+CPU reference and unsupported shapes (DTFE_LSTM_PERSIST=0 forces it).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -79,8 +84,15 @@ class LstmProgram(StepProgram):
         self.xh[0, :, I:].zero_()
         self.y.copy_(y.reshape(B, NC))
 
+    def _persistent(self):
+        return self.device.type == "cuda" and os.environ.get("DTFE_LSTM_PERSIST", "1") != "0"
+
     def forward(self):
         B = self.batch_size
+        if self._persistent() and ops.require().lstm_seq_fwd(self.xh, self.K, self.b, 1.0, self.act, self.c,
+                                                               self.hT):
+            ops.gemm(self.hT, self.Wo, self.logits, M=B, N=NC, K=H, bmode=ops.RMAJ, ldb=NC, bias=self.bo)
+            return
         for t in range(T):
             ops.gemm(self.xh[t], self.K, self.gates[t], M=B, N=4 * H, K=I + H, bmode=ops.RMAJ, ldb=4 * H,
                      bias=self.b)
@@ -103,6 +115,19 @@ class LstmProgram(StepProgram):
         ops.gemm(self.hT, self.dlogits, self.gWo, M=H, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ, ldb=NC)
         ops.colsum(self.dlogits, B, NC, NC, self.gbo)
         ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
+        if self._persistent() and ops.require().lstm_seq_bwd(self.K, self.act, self.c, self.dh, self.dg, I):
+            pass  # whole BPTT recurrence in one launch (dc / dh stay on chip)
+        else:
+            self._bptt_steps()
+        ops.gemm(self.xh, self.dg, self.gK, M=I + H, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H, bmode=ops.RMAJ,
+                 ldb=4 * H)
+        ops.colsum(self.dg, T * B, 4 * H, 4 * H, self.gb)
+        return {"loss": self.loss / B}
+
+    def _bptt_steps(self):
+        """Per-step BPTT: fused cell-backward kernel + dgrad GEMM per timestep (CPU reference /
+        shapes the persistent kernel does not cover)."""
+        B = self.batch_size
         self.dc.zero_()
         Kh = self.K[I:]  # recurrent rows [H][4H]
         for t in range(T - 1, -1, -1):
@@ -110,10 +135,6 @@ class LstmProgram(StepProgram):
                               self.dg[t], self.dc)
             if t > 0:
                 ops.gemm(self.dg[t], Kh, self.dh, M=B, N=H, K=4 * H, bmode=ops.KMAJ, ldb=4 * H)
-        ops.gemm(self.xh, self.dg, self.gK, M=I + H, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H, bmode=ops.RMAJ,
-                 ldb=4 * H)
-        ops.colsum(self.dg, T * B, 4 * H, 4 * H, self.gb)
-        return {"loss": self.loss / B}
 
     def evaluate(self, images, labels) -> float:
         """accuracy = mean(argmax(softmax(logits)) == argmax(Y)) (LSTM:98-100, 134-138)."""

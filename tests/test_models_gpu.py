@@ -89,3 +89,26 @@ def test_lstm_trains_on_gpu_with_graph():
     last = float(prog.loss.item()) / 128
     assert run.graph is not None, run.capture_error
     assert last < 0.5 * first, (first, last)
+
+
+@pytest.mark.parametrize("batch", [128, 48])
+def test_lstm_persistent_matches_per_step(batch, monkeypatch):
+    """Persistent whole-sequence kernels (lstm_seq.hip) vs the per-step cell kernels + GEMMs:
+    forward activations, cell states, logits, and every gradient."""
+    model = LstmModel()
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(batch, 784, generator=g)
+    y = F.one_hot(torch.randint(0, 10, (batch,), generator=g), 10).float()
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DTFE_LSTM_PERSIST", mode)
+        prog = model.program("cuda", batch, seed=11)
+        prog.load_batch((x.cuda(), y.cuda()))
+        prog.compute_grads()
+        torch.cuda.synchronize()
+        out[mode] = {k: v.detach().cpu().clone() for k, v in
+                     dict(act=prog.act, c=prog.c, xh=prog.xh, logits=prog.logits, dg=prog.dg, grad=prog.P.grad).items()}
+    for k in out["0"]:
+        a, b = out["1"][k], out["0"][k]
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-5, (k, err)
