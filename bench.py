@@ -50,6 +50,16 @@ def _baseline(n_gpus, batch, model="mnist_cnn"):
         return None
 
 
+def replicas_identical(params, device, backend):
+    """After the timed steps (outside the timing): every replica trained on different data
+    but applied the same all-reduced gradients, so all parameter copies must be bitwise equal."""
+    ref = params.detach().clone() if backend == "nccl" else params.detach().cpu()
+    dist.broadcast(ref, src=0)
+    d = (params.detach().to(ref.device) - ref).abs().max().reshape(1).double()
+    dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    return bool(float(d.item()) == 0.0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,7 +92,7 @@ def main():
     device = torch.device("cuda", local_rank)
 
     allreduce = None
-    trainer = MnistCnnTrainer(args.batch_size, device, seed=0, world_size=world)
+    trainer = MnistCnnTrainer(args.batch_size, device, seed=0, world_size=world, rank=rank)
     comm = None
     if world > 1:
         if args.comm != "pg" and (args.backend == "nccl" or args.comm == "ipc"):
@@ -124,6 +134,7 @@ def main():
         elapsed = float(t.item())
 
     loss = float(trainer.loss_sum.item()) / args.batch_size
+    consistent = replicas_identical(trainer.P.master, device, args.backend) if world > 1 else None
     global_batch = args.batch_size * world
     value = global_batch * args.steps / elapsed
     base = _baseline(world, args.batch_size)
@@ -154,6 +165,7 @@ def main():
                 if world > 1 else "none (1 rank)",
                 "hip_graph": runner.graph is not None,
                 "last_loss": round(loss, 4),
+                "replicas_identical": consistent,
             },
         }), flush=True)
     if world > 1:

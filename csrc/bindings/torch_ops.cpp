@@ -204,9 +204,10 @@ void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
 void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
-              int64_t pad, double scale, const optional<Tensor>& ws) {
+              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks) {
   check_cuda(src, "src");
   dtfe::ImgWgradArgs a{};
+  a.max_blocks = (int)max_blocks;
   if (ws.has_value() && ws->defined()) {
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= 256 * (N * KH * KW * CS + N),
                 "imgwgrad: workspace too small");
@@ -635,7 +636,8 @@ TORCH_LIBRARY(dtfe, m) {
       " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1) -> ()");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
-      " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None) -> ()");
+      " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"
+      " int max_blocks=0) -> ()");
   m.def("conv1_wgrad_pooled(Tensor x, Tensor dp, Tensor argmax, Tensor(a!) dw, Tensor(b!)? db, float scale) -> ()");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"

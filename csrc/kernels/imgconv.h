@@ -49,6 +49,10 @@ struct ImgWgradArgs {
   // per-workgroup partials are stored plainly and summed by a second kernel (cheaper than
   // 256-way contended fp32 atomics on every dW element); null -> atomics
   float* ws;
+  // persistent-kernel grid cap (0: 256 = one workgroup per CU).  Fewer workgroups accumulate
+  // more images each and halve the partial-sum traffic - the better trade when the launch
+  // runs beside other work (MNIST conv2's weight grad on its own graph branch)
+  int max_blocks;
 };
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);

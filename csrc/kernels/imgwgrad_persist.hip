@@ -298,7 +298,8 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   if (lds > 150 * 1024) return false;
   if ((G.ctiles + CTW - 1) / CTW > 8) return false;
   const int npfs = (G.schunks + 511) / 512, npfd = (G.dchunks + 511) / 512;
-  const int grid = a.B < 256 ? a.B : 256;
+  const int gcap = a.max_blocks > 0 && a.max_blocks < 256 ? a.max_blocks : 256;
+  const int grid = a.B < gcap ? a.B : gcap;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a, G);

@@ -132,7 +132,7 @@ class MnistCnnTrainer:
 
     def __init__(self, batch: int, device, lr: float = 1e-3, keep_prob: float = 0.75, seed: int = 0,
                  data: SyntheticMnist | None = None, allreduce=None, world_size: int = 1, P: FlatParams | None = None,
-                 standalone: bool = True):
+                 standalone: bool = True, rank: int = 0):
         """standalone: own optimizer + HBM dataset (bench / smoke).  With standalone=False the
         caller supplies P and the batches (``CnnProgram``: ps / all-reduce roles of train.py)."""
         self.B = batch
@@ -140,7 +140,9 @@ class MnistCnnTrainer:
         if self.device.type == "cuda":
             ops.require()  # GPU buffers always take the HIP kernels; fail loudly without them
         self.keep = keep_prob
-        self.seed = seed
+        # weights come from `seed` (identical on every replica); batch sampling and dropout
+        # streams are offset by `rank` so data-parallel replicas train on different data
+        self.seed = seed + 7919 * rank
         self.world = world_size
         self.allreduce = allreduce
         specs, self.names = var_specs()
@@ -149,7 +151,7 @@ class MnistCnnTrainer:
         self.opt = self.data = None
         if standalone:
             self.opt = Optimizer(OptimizerConfig(kind="adam", lr=lr), self.P, global_step=self.global_step)
-            self.data = data or SyntheticMnist(60000, self.device, seed=seed + 17)
+            self.data = data or SyntheticMnist(60000, self.device, seed=self.seed + 17)
         d = self.device
         B = batch
         bf = torch.bfloat16
@@ -239,7 +241,8 @@ class MnistCnnTrainer:
         with self._branch(self.s_c2 if self.br_c2 else None, main):
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                         workspace=self.ws_c2 if self.br_c2 else None, **self.ic2)
+                         workspace=self.ws_c2 if self.br_c2 else None, max_blocks=128 if self.br_c2 else 0,
+                         **self.ic2)
         # conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)
         ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
                     flip_taps=True, **self.ic2_dgrad)

@@ -320,7 +320,7 @@ def wgrad_workspace(device, numel):
 
 
 def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
-             dy_argmax=None, scale=1.0, workspace=None):
+             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0):
     """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY.
     On the GPU the persistent kernel stores per-workgroup partials in `workspace`
     (default: a cached per-device buffer) and a second kernel sums them."""
@@ -328,7 +328,7 @@ def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, 
         if workspace is None and (CS % 16 == 0 or CS == 1):
             workspace = wgrad_workspace(dw.device, 256 * (N * KH * KW * CS + N))
         require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
-                           scale, workspace)
+                           scale, workspace, max_blocks)
         return
     d = dy.float().view(B, OH, OW, N) if dy is not None else _unpooled_nhwc(dy_pooled, dy_argmax, B, OH, OW, N)
     gw = torch.nn.grad.conv2d_weight(src.float().view(B, SH, SW, CS).permute(0, 3, 1, 2), (N, CS, KH, KW),
