@@ -327,7 +327,8 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         # all-reduce included, replays as one hipGraph); gloo / CPU keeps ProcessGroup collectives
         bks = _buckets(prog.P)
         comm = None
-        if device.type == "cuda" and dist.get_backend(group) != "gloo" and flags.comm != "pg":
+        # (gloo + --comm=ipc: several ranks sharing one GPU rehearse the in-graph IPC path)
+        if device.type == "cuda" and flags.comm != "pg" and (dist.get_backend(group) != "gloo" or flags.comm == "ipc"):
             cdt = torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32
             comm = make_comm(device, group, [(hi - lo) * (2 if cdt == torch.bfloat16 else 4) for lo, hi in bks], cdt,
                              mode=flags.comm, log=log if is_chief else None)
@@ -341,7 +342,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
     metrics_log = MetricsLog(flags.metrics_jsonl)
 
     state = {}
-    timer = PhaseTimer(device) if flags.phase_timers else None
+    trace = flags.trace_json if world == 1 or not flags.trace_json else \
+        flags.trace_json.replace(".json", "") + ".rank%d.json" % rank
+    timer = PhaseTimer(device, trace_path=trace or None, rank=rank) \
+        if (flags.phase_timers or flags.trace_json) else None
     phase = timer.phase if timer else (lambda _n: contextlib.nullcontext())
     faults = FaultInjector("worker", rank, log=log)
 
@@ -384,12 +388,16 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                               images_per_sec=prog.batch_size * world / max(elapsed, 1e-9))
             local_step += 1
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
+        if world > 1 and flags.check_pull:  # synchronous replicas: identical parameters on every worker
+            log("params checksum %.12e" % float(prog.P.master.double().sum().item()))
         if model.name == "lstm" and is_chief:
             test_len = 128
             acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
                                 torch.from_numpy(data.test.labels[:test_len]).to(device))
             log("Test-Accuracy: %2.4f" % acc)
     finally:
+        if timer is not None:
+            timer.close()
         sv.stop()
     return prog, opts, gstep
 

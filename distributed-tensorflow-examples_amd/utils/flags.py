@@ -73,7 +73,10 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     ap.add_argument("--heartbeat_timeout", type=float, default=30.0,
                     help="ps: count a worker silent for this long as lost (with --heartbeat_secs)")
     add_bool(ap, "phase_timers", False, "time fwd+bwd / comm / apply per step with hipEvents (no hipGraph)")
-    add_bool(ap, "check_pull", False, "debug: checksum the pulled parameters every step (ps mode)")
+    add_bool(ap, "check_pull", False, "debug: checksum the pulled parameters every step (ps mode) / the "
+                                      "replicas' parameters at the end (all-reduce mode)")
+    ap.add_argument("--trace_json", default="", help="write the per-step phase timings as a Chrome trace "
+                                                     "(chrome://tracing / Perfetto); implies --phase_timers")
     return ap
 
 

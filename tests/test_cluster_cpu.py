@@ -185,3 +185,15 @@ def test_phase_timers_and_check_pull(tmp_path):
         "--check_pull"], timeout=240, stream=False)
     assert all(c == 0 for c in codes.values()), out
     assert any(l.startswith("pull checksum gs=") for l in out[("worker", 0)])
+
+
+def test_chrome_trace_of_phases(tmp_path):
+    import json
+    tr = str(tmp_path / "trace.json")
+    codes, out, _ = local_cluster.launch("encoder", 0, 1, COMMON + [
+        "--mode=local", "--num_steps=3", "--model_dir=" + str(tmp_path / "ck"), "--save_model_secs=0",
+        "--batch_size=16", "--trace_json=" + tr], timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    ev = json.load(open(tr))["traceEvents"]
+    assert {e["name"] for e in ev} >= {"fwd+bwd", "apply"} and all(e["ph"] == "X" and e["dur"] >= 0 for e in ev)
+    assert len([e for e in ev if e["name"] == "apply"]) == 3

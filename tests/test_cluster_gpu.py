@@ -33,3 +33,22 @@ def test_cnn_ps_on_gpu(tmp_path, sync):
     assert max(gs) >= 8
     t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
     assert tuple(t["Variable_1"].shape) == (5, 5, 32, 64) and "Variable_1/Adam" in t
+
+
+def test_cnn_allreduce_two_workers_ipc_in_graph(tmp_path):
+    """--mode=allreduce with the reference CLI, 2 workers sharing cuda:0: the IPC all-reduce
+    engine inside the captured step graph (gloo only carries the control traffic)."""
+    md = str(tmp_path / "ck")
+    extra = ["--mode=allreduce", "--device=cuda", "--backend=gloo", "--comm=ipc", "--comm_dtype=bf16",
+             "--synthetic", "--num_steps=12", "--batch_size=128", "--model_dir=" + md, "--save_model_secs=0.2",
+             "--check_pull"]
+    codes, out, _ = local_cluster.launch("cnn", 0, 2, extra, timeout=600, stream=False, gpus=1)
+    assert all(c == 0 for c in codes.values()), "%s\n%s" % (codes, "\n".join(
+        "---- %s\n%s" % (k, "\n".join(v[-40:])) for k, v in out.items()))
+    for w in (0, 1):
+        assert any(l.startswith("Total Time: ") for l in out[("worker", w)])
+        assert max(_gs(out[("worker", w)])) == 12
+    sums = [[l for l in out[("worker", w)] if l.startswith("params checksum")] for w in (0, 1)]
+    assert sums[0] and sums[0] == sums[1], sums
+    t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
+    assert "Variable_1/Adam" in t
