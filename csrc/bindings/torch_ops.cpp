@@ -201,6 +201,39 @@ void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
   dtfe::launch_imgconv(a, cur_stream());
 }
 
+// MNIST conv1 forward with the step's batch sampling fused in (imgconv1_copies.hip): samples B rows
+// of the uint8 dataset, writes the bf16 images to x (the weight gradient's input) and the labels,
+// clears the accumulators in `zero`, and runs conv1 + bias + ReLU + 2x2 max-pool(+argmax).
+void conv1_gather_fwd(const Tensor& images, const Tensor& labels_src, int64_t seed, const Tensor& counter,
+                      const Tensor& done, const Tensor& labels_dst, const Tensor& x, const Tensor& w,
+                      const optional<Tensor>& bias, const Tensor& y, const Tensor& argmax, at::TensorList zero) {
+  check_cuda(images, "images");
+  TORCH_CHECK(images.scalar_type() == at::kByte && images.dim() == 2 && images.size(1) == 784,
+              "conv1_gather_fwd: uint8 [rows][784] dataset");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.numel() % 784 == 0, "conv1_gather_fwd: bf16 x [B][28][28]");
+  dtfe::ImgConvArgs a{};
+  a.B = (int)(x.numel() / 784); a.SH = a.SW = 28; a.CS = 1; a.OH = a.OW = 28; a.N = 32;
+  a.KH = a.KW = 5; a.stride = 1; a.pad = 2; a.dil = 1;
+  a.src = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
+  a.bias = ptr_or_null<float>(bias);
+  a.act = dtfe::ACT_RELU; a.pool = 1;
+  a.y = reinterpret_cast<dtfe::bf16*>(y.data_ptr());
+  a.argmax = reinterpret_cast<uint8_t*>(argmax.data_ptr());
+  TORCH_CHECK(w.numel() == 32 * 25 && y.numel() == (int64_t)a.B * 14 * 14 * 32 && argmax.numel() == y.numel(),
+              "conv1_gather_fwd: MNIST conv1 shapes");
+  a.g_src = images.data_ptr<uint8_t>(); a.g_rows = images.size(0); a.g_seed = (uint64_t)seed;
+  a.g_counter = counter.data_ptr<int64_t>(); a.g_done = reinterpret_cast<uint32_t*>(done.data_ptr());
+  a.g_labels_src = labels_src.data_ptr<int32_t>(); a.g_labels_dst = labels_dst.data_ptr<int32_t>();
+  TORCH_CHECK(zero.size() <= 4, "conv1_gather_fwd: at most 4 zero ranges");
+  for (const Tensor& z : zero) {
+    TORCH_CHECK(z.is_contiguous() && (z.numel() * z.element_size()) % 4 == 0, "conv1_gather_fwd: zero ranges");
+    a.zptr[a.nz] = reinterpret_cast<uint32_t*>(z.data_ptr());
+    a.zlen[a.nz++] = (long)(z.numel() * z.element_size() / 4);
+  }
+  TORCH_CHECK(dtfe::launch_conv1_copies_fwd(a, cur_stream()), "conv1_gather_fwd: needs B >= 256");
+}
+
 void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
@@ -597,6 +630,9 @@ void maxpool3_bwd(const Tensor& dy, const Tensor& am, const Tensor& dx) {
 }
 
 TORCH_LIBRARY(dtfe, m) {
+  m.def("conv1_gather_fwd(Tensor images, Tensor labels_src, int seed, Tensor(a!) counter, Tensor(b!) done,"
+        " Tensor(c!) labels_dst, Tensor(d!) x, Tensor w, Tensor? bias, Tensor(e!) y, Tensor(f!) argmax,"
+        " Tensor(g!)[] zero) -> ()");
   m.def("lstm_seq_fwd(Tensor(a!) xh, Tensor K, Tensor bias, float forget_bias, Tensor(b!) act, Tensor(c!) c,"
         " Tensor(d!) hT) -> bool");
   m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I) -> bool");
@@ -668,6 +704,7 @@ TORCH_LIBRARY(dtfe, m) {
 }
 
 TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
+  m.impl("conv1_gather_fwd", &conv1_gather_fwd);
   m.impl("lstm_seq_fwd", &lstm_seq_fwd);
   m.impl("lstm_seq_bwd", &lstm_seq_bwd);
   m.impl("bn_stats", &bn_stats);

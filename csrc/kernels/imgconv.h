@@ -33,6 +33,21 @@ struct ImgConvArgs {
   bf16* y;                  // [B][OH'][OW'][N]  (OH' = OH/2 when pooling)
   uint8_t* argmax;          // pool argmax out (optional)
   const bf16* relu_mask;    // dgrad epilogue: y = mask > 0 ? y : 0 (same indexing as y)
+  // optional batch sampling fused into the network-input conv (MNIST conv1 forward): image b is
+  // row hash(g_seed, step * B + b) % g_rows of the HBM-resident uint8 dataset g_src (step =
+  // *g_counter, advanced by the last workgroup), converted to bf16 on load and also stored to
+  // src (the weight gradient's input) with its label; zptr/zlen: the step's accumulators,
+  // cleared by the same launch (replaces the separate gather kernel of the step)
+  const uint8_t* g_src;
+  long g_rows;
+  uint64_t g_seed;
+  int64_t* g_counter;
+  uint32_t* g_done;
+  const int32_t* g_labels_src;
+  int32_t* g_labels_dst;
+  uint32_t* zptr[4];
+  long zlen[4];
+  int nz;
 };
 
 // Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]

@@ -83,14 +83,34 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
     }
   }
 
+  // fused batch sampling (a.g_src): the sampled uint8 row is converted here and the bf16
+  // image written out for the weight gradient - no separate gather launch per step
+  const int64_t gstep = a.g_src ? *a.g_counter : 0;
+  for (int z = 0; z < a.nz; ++z)
+    for (long i = (long)blockIdx.x * TH + threadIdx.x; i < a.zlen[z]; i += (long)gridDim.x * TH) a.zptr[z][i] = 0u;
+  auto load = [&](long bb, u32x2_t& v) {
+    if (!a.g_src) {
+      load_img(a.src, bb, v);
+      return;
+    }
+    const long r = (long)(hash_u32(a.g_seed, (uint64_t)gstep * a.B + bb) % (uint32_t)a.g_rows);
+    if (threadIdx.x < XCH) {
+      const uint32_t px = *reinterpret_cast<const uint32_t*>(a.g_src + r * (HI * HI) + threadIdx.x * 4);
+      const float k = 1.f / 255.f;
+      v = u32x2_t{pack_bf16x2((float)(px & 0xffu) * k, (float)((px >> 8) & 0xffu) * k),
+                  pack_bf16x2((float)((px >> 16) & 0xffu) * k, (float)(px >> 24) * k)};
+      *reinterpret_cast<u32x2_t*>(const_cast<bf16*>(a.src) + bb * (HI * HI) + threadIdx.x * 4) = v;
+    }
+    if (threadIdx.x == 0 && a.g_labels_dst) a.g_labels_dst[bb] = a.g_labels_src[r];
+  };
   u32x2_t xv = {0u, 0u};
   long b = blockIdx.x;
-  if (b < a.B) load_img(a.src, b, xv);
+  if (b < a.B) load(b, xv);
   __syncthreads();
   for (; b < a.B; b += gridDim.x) {
     write_img(P, xv);
     __syncthreads();
-    if (b + gridDim.x < a.B) load_img(a.src, b + gridDim.x, xv);
+    if (b + gridDim.x < a.B) load(b + gridDim.x, xv);
     build_copies<8>(P, C);
     __syncthreads();
     // 49 tiles of 16 output pixels in 2x2-window order (4 windows per tile)
@@ -122,6 +142,13 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
       }
     }
     __syncthreads();
+  }
+  if (a.g_src && a.g_done && threadIdx.x == 0) {  // the last workgroup advances the sampling step
+    const uint32_t prev = __hip_atomic_fetch_add(a.g_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_fetch_add((unsigned long long*)a.g_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.g_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

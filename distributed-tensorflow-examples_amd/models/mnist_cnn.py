@@ -197,6 +197,7 @@ class MnistCnnTrainer:
         # weight grad) run on their own streams: inside the captured hipGraph they become
         # parallel branches that fill the CUs the dgrad chain leaves idle.  conv2's weight
         # grad gets its own partial-sum workspace (conv1's runs concurrently on the main stream).
+        self.fused_gather = os.environ.get("DTFE_CNN_FUSED_GATHER", "1") != "0"
         br = os.environ.get("DTFE_CNN_BRANCHES", "fc,c2").split(",")
         self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2"})
         self.br_fc = self.par and "fc" in br
@@ -209,14 +210,20 @@ class MnistCnnTrainer:
     # ------------------------------------------------------------------
     def forward_backward(self):
         B = self.B
-        if self.data is not None:  # standalone: sample the batch on device (advances data_ctr) and clear
-            ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
-                            seed=self.seed + 1, counter=self.data_ctr, done=self.data_done, zero=self.accum)
+        if self.data is not None and self.device.type == "cuda" and B >= 256 and self.fused_gather:
+            # standalone: batch sampling (advances data_ctr), accumulator clearing and conv1 in ONE launch
+            ops.require().conv1_gather_fwd(self.data.images, self.data.labels, self.seed + 1, self.data_ctr,
+                                           self.data_done, self.labels, self.x, self.w["wc1"], self.b["bc1"],
+                                           self.p1, self.a1, self.accum)
         else:
-            for t in self.accum:
-                t.zero_()
-        ops.imgconv(self.w["wc1"], self.p1, src=self.x, bias=self.b["bc1"], argmax=self.a1, act=ops.ACT_RELU,
-                    pool=True, **self.ic1)
+            if self.data is not None:  # sample the batch on device (advances data_ctr) and clear
+                ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
+                                seed=self.seed + 1, counter=self.data_ctr, done=self.data_done, zero=self.accum)
+            else:
+                for t in self.accum:
+                    t.zero_()
+            ops.imgconv(self.w["wc1"], self.p1, src=self.x, bias=self.b["bc1"], argmax=self.a1, act=ops.ACT_RELU,
+                        pool=True, **self.ic1)
         ops.imgconv(self.w["wc2"], self.p2, src=self.p1, bias=self.b["bc2"], argmax=self.a2, act=ops.ACT_RELU,
                     pool=True, **self.ic2)
         K1 = 7 * 7 * C2

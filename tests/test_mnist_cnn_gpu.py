@@ -113,3 +113,25 @@ def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
     for k, gref in grads.items():
         got = tr.gw[k].detach().cpu()
         assert ((got - gref).norm() / (gref.norm() + 1e-12)).item() < 3e-2, k
+
+
+def test_cnn_fused_sampling_conv1_matches_separate_gather(monkeypatch):
+    """B >= 256: batch sampling + accumulator clearing fused into conv1's forward launch must
+    give the same batch, labels, activations and gradients as gather kernel + conv1."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DTFE_CNN_FUSED_GATHER", fused)
+        tr = MnistCnnTrainer(256, "cuda", keep_prob=1.0, seed=7)
+        tr.P.grad.fill_(5.0)
+        for _ in range(2):            # second step: counter advanced once, stale accumulators cleared
+            tr.forward_backward()
+        torch.cuda.synchronize()
+        res[fused] = dict(x=tr.x.clone(), lab=tr.labels.clone(), p1=tr.p1.clone(), g=tr.P.grad.clone(),
+                          ctr=int(tr.data_ctr.item()), loss=tr.loss_sum.clone())
+    a, b = res["1"], res["0"]
+    assert a["ctr"] == b["ctr"] == 2
+    assert torch.equal(a["x"], b["x"]) and torch.equal(a["lab"], b["lab"]) and torch.equal(a["p1"], b["p1"])
+    assert torch.allclose(a["g"], b["g"], rtol=1e-4, atol=1e-6)
+    assert torch.allclose(a["loss"], b["loss"], rtol=1e-5)
