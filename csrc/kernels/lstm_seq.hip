@@ -7,14 +7,14 @@
 // workgroup ever waits on another) and keeps everything the next step needs on-chip:
 //
 //   forward, per step t:  A = [x_t | h_{t-1}] (16 x 156, LDS; h written there by the
-//     previous step's cell update) . K (156 x 512, streamed from L2 - every workgroup reads
-//     the same 320 KB) on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, 16 waves x 32 gate
-//     columns) -> +bias, sigma/tanh (forget_bias folded in) -> gate tile in LDS -> cell
+//     previous step's cell update) . K (156 x 512: each wave's 32-column slice is loaded once
+//     into 78 VGPRs per lane and reused for all T steps) on exact-fp32 MFMA
+//     (v_mfma_f32_16x16x4_f32, 16 waves x 32 gate columns) -> +bias, sigma/tanh (forget_bias folded in) -> gate tile in LDS -> cell
 //     update c = c_prev * f + i * j, h = tanh(c) * o with c in registers.  act / c / h go to
 //     HBM for the backward pass and the kernel-gradient GEMM.
 //   backward, per step t = T-1..0: cell backward (dc carried in registers, dh from LDS) ->
 //     dgates (LDS + HBM) -> dh_{t-1} = dgates . K_h^T (16 x 512 x 128 MFMA, k split over
-//     two wave halves, partials summed through LDS).
+//     two wave halves, partials summed through LDS; K_h^T fragments register-resident too).
 //
 // Gate order i, j, f, o and the formulas are those of the per-step kernels in
 // elementwise.hip (lstm_cell_fwd / lstm_cell_bwd), which the tests compare against.
@@ -29,7 +29,7 @@ namespace {
 constexpr int LR = 16;        // batch rows per workgroup (one MFMA row tile)
 constexpr int LWAVES = 16;    // 1024 threads
 
-template <int H>
+template <int H, int KT4>
 __global__ __launch_bounds__(1024) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
   constexpr int G4 = 4 * H;
   constexpr int CPW = G4 / LWAVES;  // gate columns per wave
@@ -48,6 +48,16 @@ __global__ __launch_bounds__(1024) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     As[r * AP + k] = a.xh[(long)(r0 + r) * rowKT + k];   // t = 0: x_0 and the initial h (zeros)
   }
   const int c0 = w * CPW, mrow = lane & 15, g = lane >> 4;
+  // this wave's 32 gate columns of K as MFMA B fragments, loaded ONCE and kept in VGPRs for all
+  // T steps (KT4 x TPW floats per lane): no per-step L2 traffic or load latency on the chain
+  float kreg[KT4][TPW];
+  {
+    const float* kcol = a.K + c0 + mrow;
+#pragma unroll
+    for (int kk = 0; kk < KT4; ++kk)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) kreg[kk][j] = kcol[(long)(4 * kk + g) * G4 + 16 * j];
+  }
   float creg[LR * H / 1024];
 #pragma unroll
   for (int q = 0; q < LR * H / 1024; ++q) creg[q] = 0.f;
@@ -63,14 +73,11 @@ __global__ __launch_bounds__(1024) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     f32x4_t acc[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const float* kcol = a.K + c0 + mrow;
-#pragma unroll 13
-    for (int kk = 0; kk < KT / 4; ++kk) {
-      const int k = 4 * kk + g;
-      const float av = As[mrow * AP + k];
 #pragma unroll
-      for (int j = 0; j < TPW; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, kcol[(long)k * G4 + 16 * j], acc[j], 0, 0, 0);
+    for (int kk = 0; kk < KT4; ++kk) {
+      const float av = As[mrow * AP + 4 * kk + g];
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, kreg[kk][j], acc[j], 0, 0, 0);
     }
     float* act_t = a.act + ((long)t * B + r0) * G4;
 #pragma unroll
@@ -128,6 +135,13 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
   for (int q = 0; q < LR * H / 1024; ++q) dcreg[q] = 0.f;
   __syncthreads();
   const int tile = w % NT, half = w / NT, mrow = lane & 15, g = lane >> 4;
+  // this wave's K_h^T fragments (16 hidden units x its k half) in VGPRs for all T steps
+  f32x4_t kb[KH / 16];
+  {
+    const float* krow = a.K + (long)(a.I + tile * 16 + mrow) * G4 + half * KH;
+#pragma unroll
+    for (int q = 0; q < KH / 16; ++q) kb[q] = *reinterpret_cast<const f32x4_t*>(krow + 16 * q + 4 * g);
+  }
   for (int t = a.T - 1; t >= 0; --t) {
     const float* act_t = a.act + ((long)t * B + r0) * G4;
     float* dg_t = a.dg + ((long)t * B + r0) * G4;
@@ -155,16 +169,13 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
     __syncthreads();
     if (t > 0 && half < 2) {
       // dh_{t-1}[r][u] = sum_c DG[r][c] * K[I + u][c]; lane group g supplies k = kb + 16q + 4g + e
-      const int u = tile * 16 + mrow;
-      const float* krow = a.K + (long)(a.I + u) * G4 + half * KH;
       const float* drow = DG + mrow * GP + half * KH;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+#pragma unroll
       for (int q = 0; q < KH / 16; ++q) {
-        const f32x4_t bv = *reinterpret_cast<const f32x4_t*>(krow + 16 * q + 4 * g);
         const f32x4_t av = *reinterpret_cast<const f32x4_t*>(drow + 16 * q + 4 * g);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc, 0, 0, 0);
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], kb[q][e], acc, 0, 0, 0);
       }
       float* P = half == 0 ? P0 : P1;
 #pragma unroll
@@ -178,9 +189,10 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
 }  // namespace
 
 bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
-  if (a.H != 128 || a.B % LR || (a.I + a.H) % 4) return false;
+  // register-resident K slice: instantiated for the MNIST row-LSTM (I = 28, H = 128)
+  if (a.H != 128 || a.I != 28 || a.B % LR) return false;
   const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * a.H + 4)) * sizeof(float);
-  auto k = lstm_seq_fwd_kernel<128>;
+  auto k = lstm_seq_fwd_kernel<128, (28 + 128) / 4>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, dim3(a.B / LR), dim3(1024), lds, s, a);
   return true;
