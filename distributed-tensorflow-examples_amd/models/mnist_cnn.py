@@ -199,9 +199,11 @@ class MnistCnnTrainer:
         # grad gets its own partial-sum workspace (conv1's runs concurrently on the main stream).
         self.fused_gather = os.environ.get("DTFE_CNN_FUSED_GATHER", "1") != "0"
         br = os.environ.get("DTFE_CNN_BRANCHES", "fc,c2").split(",")
-        self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2"})
-        self.br_fc = self.par and "fc" in br
-        self.br_c2 = self.par and "c2" in br
+        self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2", "side1"})
+        self.br_one = self.par and "side1" in br   # ONE weight-grad branch forked after fc1 dgrad
+        self.br_fc = self.par and not self.br_one and "fc" in br
+        self.br_c2 = self.par and (self.br_one or "c2" in br)
+        self.c2_blocks = int(os.environ.get("DTFE_CNN_C2_BLOCKS", "128"))
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
@@ -232,6 +234,9 @@ class MnistCnnTrainer:
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
         main = torch.cuda.current_stream(self.device) if self.par else None
+        if self.br_one:
+            self._backward_one_branch(main)
+            return
         with self._branch(self.s_fc if self.br_fc else None, main):
             # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
             ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
@@ -248,8 +253,8 @@ class MnistCnnTrainer:
         with self._branch(self.s_c2 if self.br_c2 else None, main):
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                         workspace=self.ws_c2 if self.br_c2 else None, max_blocks=128 if self.br_c2 else 0,
-                         **self.ic2)
+                         workspace=self.ws_c2 if self.br_c2 else None,
+                         max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
         # conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)
         ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
                     flip_taps=True, **self.ic2_dgrad)
@@ -258,6 +263,31 @@ class MnistCnnTrainer:
             main.wait_stream(self.s_fc)
         if self.br_c2:
             main.wait_stream(self.s_c2)
+        if self.allreduce is not None:
+            self.allreduce.launch(1)
+            self.allreduce.wait()
+
+    def _backward_one_branch(self, main):
+        """Backward with a single fork/join pair (every cross-stream edge of a hipGraph costs a few
+        microseconds of dependency latency): the dgrad chain stays on the main stream, all weight
+        gradients that feed nothing but the optimizer run on one side stream."""
+        B, K1 = self.B, 7 * 7 * C2
+        ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
+                 aux_act=ops.ACT_RELU)
+        with self._branch(self.s_fc, main):
+            ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
+                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
+                     splits=max(1, min(16, B // 128)), tile=4)
+            ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
+                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
+            if self.allreduce is not None:
+                self.allreduce.launch(0)
+            ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
+                         workspace=self.ws_c2, max_blocks=self.c2_blocks, **self.ic2)
+        ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
+                    flip_taps=True, **self.ic2_dgrad)
+        ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
+        main.wait_stream(self.s_fc)
         if self.allreduce is not None:
             self.allreduce.launch(1)
             self.allreduce.wait()

@@ -88,7 +88,7 @@ def test_cnn_trains_and_graph_replays():
     assert int(tr.global_step.item()) == 60
 
 
-@pytest.mark.parametrize("branches", ["fc,c2", "fc", "none"])
+@pytest.mark.parametrize("branches", ["fc,c2", "fc", "side1", "none"])
 def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
     """Only the atomically-accumulated grads are cleared per step (fused into the batch gather);
     every other gradient must be fully overwritten: the same batch twice -> the same grads,
