@@ -106,8 +106,7 @@ def main():
 
     if allreduce is not None and allreduce.grad16 is not None:
         def step():
-            trainer.forward_backward()
-            trainer.opt.step(grad16=allreduce.grad16, gscale=1.0 / world)
+            trainer.step(grad16=allreduce.grad16, gscale=1.0 / world)
     else:
         step = trainer.step
     # the whole step (with the overlapped RCCL all-reduce at world > 1) is one hipGraph replay

@@ -204,6 +204,23 @@ class MnistCnnTrainer:
         self.br_fc = self.par and not self.br_one and "fc" in br
         self.br_c2 = self.par and (self.br_one or "c2" in br)
         self.c2_blocks = int(os.environ.get("DTFE_CNN_C2_BLOCKS", "128"))
+        # early apply (DTFE_CNN_EARLY_APPLY=1; off by default - measured 313-325 vs 293 us/step on
+        # one MI355X: the HBM-bound Adam slows the concurrent conv backward more than it hides):
+        # when step() runs the whole step, the fc/head variables (98% of the
+        # parameters, ~21 us of HBM-bound Adam) are updated on the fc branch as soon as their
+        # gradients are final (all-reduced), concurrently with the conv backward; the conv
+        # variables are applied at the end.  Split optimizers share the slot buffers; each keeps
+        # its own beta powers (both advance once per step).
+        self.opt_fc = self.opt_conv = None
+        self._early = None
+        if self.opt is not None and self.par and os.environ.get("DTFE_CNN_EARLY_APPLY", "0") != "0":
+            n_ = self.names
+            cfg = self.opt.cfg
+            self.opt_fc = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("out", "bout", "bd1", "wd1")],
+                                    global_step=self.global_step)
+            self.opt_conv = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2", "wc1", "bc1")],
+                                      global_step=self.global_step)
+            self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
@@ -250,6 +267,13 @@ class MnistCnnTrainer:
         # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
                  aux_act=ops.ACT_RELU)
+        if self._early is not None:
+            # fc/head Adam as soon as their (reduced) gradients are final - and after fc1 dgrad, the
+            # last reader of the fc1 weights this step (the branch re-joins main's progress here)
+            with self._branch(self.s_fc, main):
+                if self.allreduce is not None:
+                    self.allreduce.wait_launched()
+                self.opt_fc.step(grad16=self._early[0], gscale=self._early[1], gs_inc=0)
         with self._branch(self.s_c2 if self.br_c2 else None, main):
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
@@ -266,6 +290,8 @@ class MnistCnnTrainer:
         if self.allreduce is not None:
             self.allreduce.launch(1)
             self.allreduce.wait()
+        if self._early is not None:
+            self.opt_conv.step(grad16=self._early[0], gscale=self._early[1], gs_inc=1)
 
     def _backward_one_branch(self, main):
         """Backward with a single fork/join pair (every cross-stream edge of a hipGraph costs a few
@@ -303,9 +329,19 @@ class MnistCnnTrainer:
     def apply(self):
         self.opt.step(gscale=1.0 / self.world)
 
-    def step(self):
-        self.forward_backward()
-        self.apply()
+    def step(self, grad16=None, gscale=None):
+        """One training step: forward, backward (+ all-reduce), Adam.  ``grad16``: the all-reduced
+        bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
+        gscale = 1.0 / self.world if gscale is None else gscale
+        if self.opt_fc is None or self.br_one or not self.br_fc:
+            self.forward_backward()
+            self.opt.step(grad16=grad16, gscale=gscale)
+            return
+        self._early = (grad16, gscale)
+        try:
+            self.forward_backward()
+        finally:
+            self._early = None
 
     def flops_per_image(self) -> float:
         """Training FLOPs per image (fwd + dgrad + wgrad of every GEMM-shaped op)."""

@@ -82,6 +82,14 @@ class BucketAllReduce:
             self.launch(self._next)
             self._next += 1
 
+    def wait_launched(self):
+        """Make the current stream wait for every bucket launched so far (the step goes on;
+        ``wait()`` still closes the step)."""
+        if self._forked:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.side)
+        for w in self._works:
+            w.wait()
+
     def wait(self):
         if self._forked:  # join the side stream back into the compute stream
             torch.cuda.current_stream(self.flat.device).wait_stream(self.side)

@@ -135,3 +135,21 @@ def test_cnn_fused_sampling_conv1_matches_separate_gather(monkeypatch):
     assert torch.equal(a["x"], b["x"]) and torch.equal(a["lab"], b["lab"]) and torch.equal(a["p1"], b["p1"])
     assert torch.allclose(a["g"], b["g"], rtol=1e-4, atol=1e-6)
     assert torch.allclose(a["loss"], b["loss"], rtol=1e-5)
+
+
+def test_cnn_early_fc_apply_matches_sequential(monkeypatch):
+    """step() with the fc/head Adam issued on the fc branch (split optimizers, shared slots) must
+    train exactly like forward_backward() + one whole-model Adam."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    out = {}
+    for early in ("1", "0"):
+        monkeypatch.setenv("DTFE_CNN_EARLY_APPLY", early)
+        tr = MnistCnnTrainer(256, "cuda", seed=9)
+        assert (tr.opt_fc is not None) == (early == "1")
+        for _ in range(4):
+            tr.step()
+        torch.cuda.synchronize()
+        out[early] = (tr.P.master.clone(), int(tr.global_step.item()))
+    assert out["1"][1] == out["0"][1] == 4
+    assert torch.allclose(out["1"][0], out["0"][0], rtol=1e-4, atol=1e-6)
