@@ -211,16 +211,13 @@ class MnistCnnTrainer:
         # gradients are final (all-reduced), concurrently with the conv backward; the conv
         # variables are applied at the end.  Split optimizers share the slot buffers; each keeps
         # its own beta powers (both advance once per step).
+        # Data-parallel "late split" (default whenever an all-reduce is attached): the fc/head Adam
+        # (bucket 0, already reduced during the conv backward) runs while the small conv bucket's
+        # all-reduce is still in flight, so that collective's latency hides behind ~20 us of Adam.
         self.opt_fc = self.opt_conv = None
-        self._early = None
-        if self.opt is not None and self.par and os.environ.get("DTFE_CNN_EARLY_APPLY", "0") != "0":
-            n_ = self.names
-            cfg = self.opt.cfg
-            self.opt_fc = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("out", "bout", "bd1", "wd1")],
-                                    global_step=self.global_step)
-            self.opt_conv = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2", "wc1", "bc1")],
-                                      global_step=self.global_step)
-            self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
+        self._apply = None
+        self.early_apply = os.environ.get("DTFE_CNN_EARLY_APPLY", "0") != "0"
+        self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
@@ -267,13 +264,13 @@ class MnistCnnTrainer:
         # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
                  aux_act=ops.ACT_RELU)
-        if self._early is not None:
+        if self._apply is not None and self._apply[0] == "early":
             # fc/head Adam as soon as their (reduced) gradients are final - and after fc1 dgrad, the
             # last reader of the fc1 weights this step (the branch re-joins main's progress here)
             with self._branch(self.s_fc, main):
                 if self.allreduce is not None:
                     self.allreduce.wait_launched()
-                self.opt_fc.step(grad16=self._early[0], gscale=self._early[1], gs_inc=0)
+                self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
         with self._branch(self.s_c2 if self.br_c2 else None, main):
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
@@ -289,9 +286,22 @@ class MnistCnnTrainer:
             main.wait_stream(self.s_c2)
         if self.allreduce is not None:
             self.allreduce.launch(1)
+            if self._apply is not None and self._apply[0] == "late":
+                self.allreduce.wait_bucket(0)   # fc/head Adam overlaps the conv bucket's all-reduce
+                self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
             self.allreduce.wait()
-        if self._early is not None:
-            self.opt_conv.step(grad16=self._early[0], gscale=self._early[1], gs_inc=1)
+        if self._apply is not None:
+            self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
+
+    def _ensure_split(self):
+        """fc/head and conv optimizers over disjoint var lists, sharing one set of slot buffers."""
+        if self.opt_fc is None:
+            n_, cfg = self.names, self.opt.cfg
+            self.opt_fc = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("out", "bout", "bd1", "wd1")],
+                                    global_step=self.global_step)
+            self.opt_conv = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2", "wc1", "bc1")],
+                                      global_step=self.global_step)
+            self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
 
     def _backward_one_branch(self, main):
         """Backward with a single fork/join pair (every cross-stream edge of a hipGraph costs a few
@@ -333,15 +343,28 @@ class MnistCnnTrainer:
         """One training step: forward, backward (+ all-reduce), Adam.  ``grad16``: the all-reduced
         bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
         gscale = 1.0 / self.world if gscale is None else gscale
-        if self.opt_fc is None or self.br_one or not self.br_fc:
+        mode = None
+        if self.par and not self.br_one and self.br_fc:
+            if self.early_apply:
+                mode = "early"
+            elif self.late_split and self.allreduce is not None:
+                mode = "late"
+        if mode is None or (self.opt_fc is None and self.global_step_started()):
             self.forward_backward()
             self.opt.step(grad16=grad16, gscale=gscale)
+            self._whole_steps = getattr(self, "_whole_steps", 0) + 1
             return
-        self._early = (grad16, gscale)
+        self._ensure_split()
+        self._apply = (mode, grad16, gscale)
         try:
             self.forward_backward()
         finally:
-            self._early = None
+            self._apply = None
+
+    def global_step_started(self) -> bool:
+        """True once the whole-model optimizer has applied a step (its slots then hold the state,
+        so the schedule must not switch to the split optimizers)."""
+        return getattr(self, "_whole_steps", 0) > 0
 
     def flops_per_image(self) -> float:
         """Training FLOPs per image (fwd + dgrad + wgrad of every GEMM-shaped op)."""

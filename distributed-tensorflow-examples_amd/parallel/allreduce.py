@@ -44,6 +44,8 @@ class BucketAllReduce:
         if comm_dtype == torch.bfloat16:
             self.shadow = torch.empty(flat_grad.numel(), dtype=torch.bfloat16, device=flat_grad.device)
         self._works = []
+        self._work_of = {}
+        self._done_ev = [torch.cuda.Event() for _ in self.buckets] if comm is not None else []
         self._next = 0  # next bucket (in launch order) not yet launched this step
 
     @property
@@ -62,11 +64,21 @@ class BucketAllReduce:
             self.side.wait_stream(torch.cuda.current_stream(self.flat.device))
             with torch.cuda.stream(self.side):
                 self.comm.all_reduce(buf)
+                self._done_ev[i].record(self.side)
             self._forked = True
             return
         if self.world == 1:
             return
         self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        self._work_of[i] = self._works[-1]
+
+    def wait_bucket(self, i: int):
+        """Make the current stream wait for bucket i's all-reduce only (later buckets may still
+        be in flight)."""
+        if self.comm is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(self._done_ev[i])
+        elif i in self._work_of:
+            self._work_of[i].wait()
 
     def ready(self, lo: int):
         """Backward progress hook: every gradient at flat offset >= lo is final.  Launches the
@@ -97,4 +109,5 @@ class BucketAllReduce:
         for w in self._works:
             w.wait()
         self._works.clear()
+        self._work_of.clear()
         self._next = 0

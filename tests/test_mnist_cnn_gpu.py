@@ -146,9 +146,9 @@ def test_cnn_early_fc_apply_matches_sequential(monkeypatch):
     for early in ("1", "0"):
         monkeypatch.setenv("DTFE_CNN_EARLY_APPLY", early)
         tr = MnistCnnTrainer(256, "cuda", seed=9)
-        assert (tr.opt_fc is not None) == (early == "1")
         for _ in range(4):
             tr.step()
+        assert (tr.opt_fc is not None) == (early == "1")
         torch.cuda.synchronize()
         out[early] = (tr.P.master.clone(), int(tr.global_step.item()))
     assert out["1"][1] == out["0"][1] == 4

@@ -141,3 +141,35 @@ def test_make_comm_routes(pg, mode):
             assert "rccl" not in d
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_cnn_late_split_apply_with_allreduce(pg, split, monkeypatch):
+    """With an all-reduce attached, step() applies the fc/head bucket while the conv bucket is
+    still being reduced (split optimizers, per-bucket completion events); the trajectory must
+    equal the whole-model apply."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    monkeypatch.setenv("DTFE_CNN_SPLIT_APPLY", split)
+    dev = torch.device("cuda", 0)
+    comm = RcclComm(dev)
+    try:
+        tr = MnistCnnTrainer(256, dev, seed=4)
+        ar = BucketAllReduce(tr.P.grad, tr.buckets, comm=comm, comm_dtype=torch.bfloat16)
+        tr.allreduce = ar
+        runner = StepGraph(lambda: tr.step(grad16=ar.grad16, gscale=1.0), warmup=2, enabled=True,
+                           capture_error_mode="thread_local")
+        for _ in range(6):
+            runner()
+        torch.cuda.synchronize()
+        assert runner.graph is not None, runner.capture_error
+        assert (tr.opt_fc is not None) == (split == "1")
+        assert int(tr.global_step.item()) == 6
+        _LATE[split] = tr.P.master.clone()
+        if len(_LATE) == 2:
+            assert torch.allclose(_LATE["1"], _LATE["0"], rtol=1e-4, atol=1e-6)
+    finally:
+        comm.close()
+
+
+_LATE = {}
