@@ -197,3 +197,17 @@ def test_chrome_trace_of_phases(tmp_path):
     ev = json.load(open(tr))["traceEvents"]
     assert {e["name"] for e in ev} >= {"fwd+bwd", "apply"} and all(e["ph"] == "X" and e["dur"] >= 0 for e in ev)
     assert len([e for e in ev if e["name"] == "apply"]) == 3
+
+
+def test_killed_ps_makes_workers_error_out(tmp_path):
+    """when the ps dies, workers error out on their next exchange and exit
+    non-zero (no hang); the reference gives the same outcome through failing RecvTensor RPCs."""
+    env = dict(os.environ, DTFE_FAULT="crash@ps:0:step=10")
+    codes, out, _ = local_cluster.launch("softmax", 1, 2, COMMON + [
+        "--num_steps=100000", "--workers=2", "--model_dir=" + str(tmp_path / "ck"), "--save_model_secs=0"],
+        env=env, timeout=240, stream=False)
+    assert codes[("ps", 0)] == 17, out[("ps", 0)]
+    assert any("fault injection: ps 0 crashes" in l for l in out[("ps", 0)])
+    for w in (0, 1):
+        assert codes[("worker", w)] != 0, out[("worker", w)][-5:]
+        assert not any(l.startswith("Total Time") for l in out[("worker", w)])
