@@ -47,7 +47,8 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
           const optional<Tensor>& aux, int64_t ld_aux, int64_t aux_act, int64_t b_ones_row, double keep, int64_t seed,
           const optional<Tensor>& counter, const optional<Tensor>& pooled, const optional<Tensor>& argmax,
           int64_t PH, int64_t PW, int64_t PC, const optional<Tensor>& out2, int64_t ldc2, bool out2_trans,
-          const optional<Tensor>& bias_out, const optional<Tensor>& ws, const optional<Tensor>& tile_ctr) {
+          const optional<Tensor>& bias_out, const optional<Tensor>& ws, const optional<Tensor>& tile_ctr,
+          int64_t a_ones_row) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(out, "out");
@@ -58,6 +59,8 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   a.A = A.data_ptr(); a.lda = lda;
   a.B = B.data_ptr(); a.ldb = ldb;
   a.b_ones_row = (int)b_ones_row;
+  a.a_ones_row = (int)a_ones_row;
+  TORCH_CHECK(a_ones_row < 0 || b_ones_row < 0, "gemm: at most one of a_ones_row / b_ones_row");
   if (splits < 1) splits = 1;
   int bm = 0, bn = 0;
   const int kt = dtfe::gemm_dense_tile_dims((int)tile, bm, bn);
@@ -96,7 +99,7 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   }
   a.keep = (float)keep; a.seed = (uint64_t)seed; a.counter = ptr_or_null<int64_t>(counter);
   a.bias_out = ptr_or_null<float>(bias_out);
-  TORCH_CHECK(!a.bias_out || b_ones_row >= 0, "gemm: bias_out needs b_ones_row");
+  TORCH_CHECK(!a.bias_out || b_ones_row >= 0 || a_ones_row >= 0, "gemm: bias_out needs a ones row");
   dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
 }
 
@@ -658,7 +661,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor? bias, int bias_axis, int act, float alpha, float beta, bool atomic, int splits, int tile,"
       " Tensor? aux, int ld_aux, int aux_act, int b_ones_row, float keep, int seed, Tensor? counter,"
       " Tensor? pooled, Tensor? argmax, int PH, int PW, int PC, Tensor(b!)? out2, int ldc2, bool out2_trans,"
-      " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr) -> ()");
+      " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr, int a_ones_row=-1) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");

@@ -13,6 +13,7 @@ struct DenseGemmArgs {
   const void* A; long lda;     // A(m,k): KMAJ a[m*lda+k], RMAJ a[k*lda+m]
   const void* B; long ldb;     // B(n,k): KMAJ b[n*ldb+k], RMAJ b[k*ldb+n]
   int b_ones_row;              // >=0: B row that reads as 1.0 (bias column)
+  int a_ones_row;              // >=0: A row that reads as 1.0 (bias row: out[a_ones_row][n] -> bias_out[n])
   int k_chunk;                 // split-K chunk (multiple of BK); gridDim.z splits
   // epilogue
   void* out; long ldc; int out_f32;
@@ -41,6 +42,11 @@ struct DenseGemmArgs {
 __device__ __forceinline__ bool dense_epi(const DenseGemmArgs& a, int row, int col, float& x, int64_t drop_step,
                                           float inv_keep) {
   const long o = (long)row * a.ldc + col;
+  if (a.bias_out && row == a.a_ones_row) {  // the ones row = this layer's bias gradient (per column)
+    if (a.atomic) atomicAdd(a.bias_out + col, a.alpha * x);
+    else a.bias_out[col] = a.alpha * x;
+    return false;
+  }
   if (a.bias_out && col == a.b_ones_row) {  // the ones column = this layer's bias gradient
     if (a.atomic) atomicAdd(a.bias_out + row, a.alpha * x);
     else a.bias_out[row] = a.alpha * x;
@@ -92,7 +98,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
   const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
   const int k_begin = blockIdx.z * a.k_chunk;
   const int k_end = min(a.K, k_begin + a.k_chunk);
-  LA la((const T*)a.A, a.lda, a.M, a.K, m_base, -1);
+  LA la((const T*)a.A, a.lda, a.M, a.K, m_base, a.a_ones_row);
   LB lb((const T*)a.B, a.ldb, a.N, a.K, n_base, a.b_ones_row);
   f32x4_t acc[Cfg::TM][Cfg::TN];
   gemm_mainloop<T, Cfg, AMODE, BMODE>(la, lb, k_begin, k_end, smem, acc);  // ends with a barrier
@@ -163,7 +169,8 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
   const int64_t drop_step = (a.keep < 1.f && a.counter) ? *a.counter : 0;
   const float inv_keep = 1.f / a.keep;
   // plain-store fast path: no per-element side outputs, 16 B aligned rows
-  const bool vec_store = !a.atomic && !a.unpool && !a.out2 && !a.bias_out && a.beta == 0.f &&
+  // (a weight-gradient GEMM's bias row / column only takes the per-element path in its own chunks)
+  const bool vec_store = !a.atomic && !a.unpool && !a.out2 && a.beta == 0.f &&
                          (a.ldc % 8) == 0 && ((((uintptr_t)a.out) & 15) == 0);
   for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
     const int r = ch / CPR, c = (ch % CPR) * 8;
@@ -172,7 +179,8 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
     float x[8];
     *reinterpret_cast<f32x4_t*>(x) = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c);
     *reinterpret_cast<f32x4_t*>(x + 4) = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c + 4);
-    if (vec_store && col0 + 8 <= a.N) {
+    const bool side = a.bias_out && (row == a.a_ones_row || (a.b_ones_row >= col0 && a.b_ones_row < col0 + 8));
+    if (vec_store && !side && col0 + 8 <= a.N) {
       const long o = (long)row * a.ldc + col0;
       float g[8];  // act'(aux) factors, one 16 B load when aux is bf16 and aligned
       if (a.aux && !a.aux_f32 && (a.ld_aux % 8) == 0) {

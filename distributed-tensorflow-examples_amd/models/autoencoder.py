@@ -83,10 +83,9 @@ class AutoencoderProgram(StepProgram):
         ops.mse_sigmoid(y, self.x, self.loss, self.dz[3])
         for i in range(3, -1, -1):
             inp = self.x if i == 0 else self.a[i - 1]
-            # dW_i[K][N] = inp^T . dz_i ; db_i = colsum(dz_i)
-            ops.gemm(inp, self.dz[i], self.gW[i], M=DIMS[i], N=DIMS[i + 1], K=B, amode=ops.RMAJ, lda=DIMS[i],
-                     bmode=ops.RMAJ, ldb=DIMS[i + 1])
-            ops.colsum(self.dz[i], B, DIMS[i + 1], DIMS[i + 1], self.gb[i])
+            # dW_i[K][N] = inp^T . dz_i ; db_i = sum_b dz_i through the GEMM's ones row (no colsum launch)
+            ops.gemm(inp, self.dz[i], self.gW[i], M=DIMS[i] + 1, N=DIMS[i + 1], K=B, amode=ops.RMAJ, lda=DIMS[i],
+                     bmode=ops.RMAJ, ldb=DIMS[i + 1], a_ones_row=DIMS[i], bias_out=self.gb[i])
             if i > 0:
                 # dz_{i-1} = (dz_i . W_i^T) * sigmoid'(a_{i-1})
                 ops.gemm(self.dz[i], self.W[i], self.dz[i - 1], M=B, N=DIMS[i], K=DIMS[i + 1],

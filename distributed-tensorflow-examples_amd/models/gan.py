@@ -111,21 +111,22 @@ class GanProgram(StepProgram):
         ops.gan_loss(self.p[:B], self.p[B:], self.gen_loss, self.disc_loss, self.dlog[:B], self.dlog[B:],
                      self.dlog_g)
         # ---- discriminator: d disc_loss over the stacked batch
-        ops.gemm(self.d1, self.dlog, G["Wd2"], M=DH, N=1, K=2 * B, amode=R, lda=DH, bmode=R, ldb=1)
-        ops.colsum(self.dlog, 2 * B, 1, 1, G["bd2"])
+        # weight grads carry their bias grads in a ones row of A (no separate column-sum launches)
+        ops.gemm(self.d1, self.dlog, G["Wd2"], M=DH + 1, N=1, K=2 * B, amode=R, lda=DH, bmode=R, ldb=1,
+                 a_ones_row=DH, bias_out=G["bd2"])
         ops.gemm(self.dlog, W["Wd2"], self.dd1, M=2 * B, N=DH, K=1, amode=K, lda=1, bmode=K, ldb=1,
                  aux=self.d1, aux_act=ops.ACT_RELU)
-        ops.gemm(self.xx, self.dd1, G["Wd1"], M=IMG, N=DH, K=2 * B, amode=R, lda=IMG, bmode=R, ldb=DH)
-        ops.colsum(self.dd1, 2 * B, DH, DH, G["bd1"])
+        ops.gemm(self.xx, self.dd1, G["Wd1"], M=IMG + 1, N=DH, K=2 * B, amode=R, lda=IMG, bmode=R, ldb=DH,
+                 a_ones_row=IMG, bias_out=G["bd1"])
         # ---- generator: d gen_loss through D (same parameter snapshot)
         ops.gemm(self.dlog_g, W["Wd2"], self.ddf, M=B, N=DH, K=1, amode=K, lda=1, bmode=K, ldb=1,
                  aux=self.d1[B:], aux_act=ops.ACT_RELU)
         ops.gemm(self.ddf, W["Wd1"], self.dg, M=B, N=IMG, K=DH, amode=K, lda=DH, bmode=K, ldb=DH,
                  aux=self.xx[B:], aux_act=ops.ACT_SIGMOID)
-        ops.gemm(self.h1, self.dg, G["Wg2"], M=GH, N=IMG, K=B, amode=R, lda=GH, bmode=R, ldb=IMG)
-        ops.colsum(self.dg, B, IMG, IMG, G["bg2"])
+        ops.gemm(self.h1, self.dg, G["Wg2"], M=GH + 1, N=IMG, K=B, amode=R, lda=GH, bmode=R, ldb=IMG,
+                 a_ones_row=GH, bias_out=G["bg2"])
         ops.gemm(self.dg, W["Wg2"], self.dh1, M=B, N=GH, K=IMG, amode=K, lda=IMG, bmode=K, ldb=IMG,
                  aux=self.h1, aux_act=ops.ACT_RELU)
-        ops.gemm(self.z, self.dh1, G["Wg1"], M=NOISE, N=GH, K=B, amode=R, lda=NOISE, bmode=R, ldb=GH)
-        ops.colsum(self.dh1, B, GH, GH, G["bg1"])
+        ops.gemm(self.z, self.dh1, G["Wg1"], M=NOISE + 1, N=GH, K=B, amode=R, lda=NOISE, bmode=R, ldb=GH,
+                 a_ones_row=NOISE, bias_out=G["bg1"])
         return {"gen_loss": self.gen_loss, "disc_loss": self.disc_loss}

@@ -112,16 +112,15 @@ class LstmProgram(StepProgram):
         self.forward()
         ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
                          correct=self.correct)
-        ops.gemm(self.hT, self.dlogits, self.gWo, M=H, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ, ldb=NC)
-        ops.colsum(self.dlogits, B, NC, NC, self.gbo)
+        ops.gemm(self.hT, self.dlogits, self.gWo, M=H + 1, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ,
+                 ldb=NC, a_ones_row=H, bias_out=self.gbo)
         ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
         if self._persistent() and ops.require().lstm_seq_bwd(self.K, self.act, self.c, self.dh, self.dg, I):
             pass  # whole BPTT recurrence in one launch (dc / dh stay on chip)
         else:
             self._bptt_steps()
-        ops.gemm(self.xh, self.dg, self.gK, M=I + H, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H, bmode=ops.RMAJ,
-                 ldb=4 * H)
-        ops.colsum(self.dg, T * B, 4 * H, 4 * H, self.gb)
+        ops.gemm(self.xh, self.dg, self.gK, M=I + H + 1, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H,
+                 bmode=ops.RMAJ, ldb=4 * H, a_ones_row=I + H, bias_out=self.gb)
         return {"loss": self.loss / B}
 
     def _bptt_steps(self):

@@ -58,8 +58,8 @@ class SoftmaxProgram(StepProgram):
         ops.gemm(self.x, self.W, self.logits, M=B, N=NC, K=IMG, bmode=ops.RMAJ, ldb=NC, bias=self.b)
         ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
                          correct=self.correct)
-        ops.gemm(self.x, self.dlogits, self.gW, M=IMG, N=NC, K=B, amode=ops.RMAJ, lda=IMG, bmode=ops.RMAJ, ldb=NC)
-        ops.colsum(self.dlogits, B, NC, NC, self.gb)
+        ops.gemm(self.x, self.dlogits, self.gW, M=IMG + 1, N=NC, K=B, amode=ops.RMAJ, lda=IMG, bmode=ops.RMAJ,
+                 ldb=NC, a_ones_row=IMG, bias_out=self.gb)
         return {"loss": self.loss / B}
 
     def evaluate(self, images, labels) -> float:

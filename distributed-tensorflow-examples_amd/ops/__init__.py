@@ -120,13 +120,15 @@ def _mat(t, mode, rows, K, ld):
 def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=None, bias=None, bias_axis=0,
          act=ACT_NONE, alpha=1.0, beta=0.0, atomic=False, splits=1, tile=None, aux=None, ld_aux=None, aux_act=0,
          b_ones_row=-1, keep=1.0, seed=0, counter=None, pooled=None, argmax=None, PH=0, PW=0, PC=0, out2=None,
-         ldc2=0, out2_trans=False, bias_out=None, workspace=None):
+         ldc2=0, out2_trans=False, bias_out=None, workspace=None, a_ones_row=-1):
     """out[M,N] = epilogue( A(m,k) . B(n,k) ).
 
     A(m,k) = A[m*lda+k] (KMAJ) or A[k*lda+m] (RMAJ); likewise B(n,k).
     Epilogue order: alpha*acc, +bias, act, dropout(keep), *act'(aux), [unpool | +beta*out], store.
     b_ones_row >= 0 makes B row n=b_ones_row all ones; with bias_out that output
     column goes to bias_out[m] (a weight-gradient GEMM producing the bias gradient).
+    a_ones_row = M-1 is the transpose: A's last row reads as ones and output row M-1 goes to
+    bias_out[n] (W[in][out] weight gradients: the bias gradient without a column-sum launch).
     splits > 1 without atomic: split-K whose last-arriving split runs the fused
     epilogue (workspace = (ws, tile_ctr), default: a per-device cached one).
     """
@@ -148,17 +150,28 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
             ws, ctr = workspace if workspace is not None else split_workspace(out.device, splits, M, N, tile)
         require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
                        splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
-                       PC, out2, ldc2, out2_trans, bias_out, ws, ctr)
+                       PC, out2, ldc2, out2_trans, bias_out, ws, ctr, a_ones_row)
         return out
     # CPU reference
-    a = _mat(A, amode, M, K, lda)
+    if a_ones_row >= 0:
+        assert a_ones_row == M - 1, "CPU reference: a_ones_row must be the last row"
+        a = torch.cat([_mat(A, amode, M - 1, K, lda), torch.ones(1, K)], 0)
+    else:
+        a = _mat(A, amode, M, K, lda)
     if b_ones_row >= 0:
         b = _mat(B, bmode, b_ones_row, K, ldb) if b_ones_row > 0 else torch.zeros(0, K)
         b = torch.cat([b, torch.ones(1, K), _mat_tail(B, bmode, b_ones_row + 1, N, K, ldb)], 0)
     else:
         b = _mat(B, bmode, N, K, ldb)
     acc = a @ b.t()
-    if bias_out is not None:
+    if bias_out is not None and a_ones_row >= 0:
+        if atomic:
+            bias_out += alpha * acc[a_ones_row]
+        else:
+            bias_out.copy_(alpha * acc[a_ones_row])
+        acc = acc[:a_ones_row]
+        M = a_ones_row
+    elif bias_out is not None:
         if atomic:
             bias_out += alpha * acc[:, b_ones_row]
         else:

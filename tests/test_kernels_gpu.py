@@ -113,6 +113,23 @@ def test_gemm_ones_row_bias_column():
     assert _rel(out.cpu(), exp) < 1e-5
 
 
+@pytest.mark.parametrize("dtype,splits", [(torch.float32, 1), (torch.float32, 4), (torch.bfloat16, 1),
+                                          (torch.bfloat16, 3)])
+def test_gemm_ones_row_bias_row(dtype, splits):
+    """a_ones_row: W[in][out] weight gradient X^T . dZ with the bias gradient sum_b dZ[b][:] routed from
+    the ones row of A to bias_out - RMAJ operands as the reference models' wgrads use them."""
+    Bn, IN, OUT = 200, 100, 70
+    X = torch.randn(Bn, IN, device=DEV).to(dtype)
+    dZ = torch.randn(Bn, OUT, device=DEV).to(dtype)
+    gW = torch.zeros(IN, OUT, device=DEV)
+    gb = torch.full((OUT,), 9.0, device=DEV)
+    ops.gemm(X, dZ, gW, M=IN + 1, N=OUT, K=Bn, amode=ops.RMAJ, lda=IN, bmode=ops.RMAJ, ldb=OUT,
+             a_ones_row=IN, bias_out=gb, splits=splits)
+    exp = X.float().cpu().t() @ dZ.float().cpu()
+    assert _rel(gW.cpu(), exp) < 1e-5
+    assert _rel(gb.cpu(), dZ.float().cpu().sum(0)) < 1e-5
+
+
 def _geom(B, H, W, C, Cout, KH, KW, stride, pad):
     OH = (H + 2 * pad - KH) // stride + 1
     OW = (W + 2 * pad - KW) // stride + 1
