@@ -126,6 +126,7 @@ struct IpcComm {
   char* base[dtfe::IPC_MAXW] = {};
   bool opened[dtfe::IPC_MAXW] = {};
   uint32_t* epoch = nullptr;
+  uint32_t* calls = nullptr;
   int* err = nullptr;
   double timeout_s = 30.0;
 };
@@ -160,6 +161,7 @@ int64_t ipc_create(int64_t cap_bytes, int64_t rank, int64_t world, int64_t devic
   hip_check(hipMalloc(reinterpret_cast<void**>(&c->epoch), dtfe::IPC_MAXB * sizeof(uint32_t) + 64), "hipMalloc");
   hip_check(hipMemset(c->epoch, 0, dtfe::IPC_MAXB * sizeof(uint32_t) + 64), "hipMemset");
   c->err = reinterpret_cast<int*>(c->epoch + dtfe::IPC_MAXB);
+  c->calls = c->epoch + dtfe::IPC_MAXB + 4;
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   std::lock_guard<std::mutex> lk(g_mu);
   g_ipc.push_back(c);
@@ -215,6 +217,7 @@ void ipc_all_reduce(Tensor buf, int64_t h) {
   a.buf = buf.data_ptr();
   a.n = buf.numel();
   a.epoch = c->epoch;
+  a.calls = c->calls;
   a.err = c->err;
   a.timeout = (unsigned long long)(c->timeout_s * 1e8);  // wall_clock64: 100 MHz
   // the block count must be identical on every rank: a function of (n, world) only

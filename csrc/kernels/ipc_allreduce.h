@@ -19,6 +19,7 @@ struct IpcAllReduceArgs {
   void* buf;             // in/out tensor (in place)
   long n;                // elements
   uint32_t* epoch;       // [IPC_MAXB] per-block call counters (local memory)
+  uint32_t* calls;       // [2] {launches completed, blocks finished in the current launch} (local memory)
   int* err;              // set to 1 when a barrier timed out
   unsigned long long timeout;  // wall_clock64 ticks (100 MHz)
   int blocks;

@@ -58,6 +58,15 @@ __device__ __forceinline__ bool ipc_barrier(const IpcAllReduceArgs& a, int ph, u
   return *s_ok != 0;
 }
 
+// The last block of a launch to finish advances the launch counter (every block read it at its
+// start; the next launch on this stream only begins after this one completed).
+__device__ __forceinline__ void ipc_block_done(const IpcAllReduceArgs& a) {
+  if (threadIdx.x == 0 && atomicAdd(a.calls + 1, 1u) == (uint32_t)a.blocks - 1) {
+    a.calls[1] = 0;
+    atomicAdd(a.calls, 1u);
+  }
+}
+
 template <typename T> struct Vec16;
 template <> struct Vec16<bf16> {
   static constexpr int N = 8;
@@ -94,16 +103,21 @@ template <> struct Vec16<float> {
 template <typename T, int W>
 __global__ __launch_bounds__(IPC_THREADS) void ipc_allreduce_kernel(IpcAllReduceArgs a) {
   using V = Vec16<T>;
-  __shared__ uint32_t s_ep;
+  __shared__ uint32_t s_ep, s_par;
   __shared__ int s_ok;
   const int tid = threadIdx.x, b = blockIdx.x, r = a.rank;
   if (tid == 0) {
     s_ep = a.epoch[b] + 1;
+    s_par = a.calls[0] & 1u;
     s_ok = 1;
   }
   __syncthreads();
   const uint32_t ep = s_ep;
-  const long off = IPC_DATA_OFF + (long)(ep & 1u) * a.cap;
+  // The staging parity flips once per LAUNCH, identically for every block and rank.  (A
+  // per-block parity would not do: launches of different sizes run different block counts,
+  // so block b's slice and its epoch differ between calls, and a fast rank's next-call
+  // staging could land on the parity a slow peer is still gathering from.)
+  const long off = IPC_DATA_OFF + (long)s_par * a.cap;
   // 16-B body plus up to 2*(V::N-1) scalar elements (the unaligned head before the first
   // 16-B boundary and the tail) that block 0 of every rank reduces on its own
   T* const x = reinterpret_cast<T*>(a.buf);
@@ -127,7 +141,10 @@ __global__ __launch_bounds__(IPC_THREADS) void ipc_allreduce_kernel(IpcAllReduce
     for (long i = p * seg + i0; i < hi; i += step) mine[i] = io[i];
   }
   if (sx) reinterpret_cast<T*>(mine + nvec)[tid] = *sx;
-  if (!ipc_barrier(a, 0, ep, &s_ok)) return;
+  if (!ipc_barrier(a, 0, ep, &s_ok)) {
+    ipc_block_done(a);
+    return;
+  }
 
   // B: reduce this block's slice of segment r over every rank's staging buffer
   {
@@ -153,7 +170,10 @@ __global__ __launch_bounds__(IPC_THREADS) void ipc_allreduce_kernel(IpcAllReduce
       V::st(sx, s);
     }
   }
-  if (!ipc_barrier(a, 1, ep, &s_ok)) return;
+  if (!ipc_barrier(a, 1, ep, &s_ok)) {
+    ipc_block_done(a);
+    return;
+  }
 
   // C: gather the other ranks' reduced segments
 #pragma unroll
@@ -164,6 +184,7 @@ __global__ __launch_bounds__(IPC_THREADS) void ipc_allreduce_kernel(IpcAllReduce
     for (long i = p * seg + i0; i < hi; i += step) io[i] = src[i];
   }
   if (tid == 0) a.epoch[b] = ep;
+  ipc_block_done(a);
 }
 
 template <typename T>

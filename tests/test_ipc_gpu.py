@@ -73,6 +73,20 @@ def _worker(rank, world, port, q):
             if not torch.equal(buf.cpu(), exp):
                 errs.append(("graph", it))
         errs.append(("graph_captured", runner.graph is not None))
+        # alternating bucket sizes (different block counts per launch), as the CNN step issues
+        # its fc bucket then its conv bucket: staging parity must flip per launch on every block
+        big = torch.zeros(3 << 20, device=dev, dtype=torch.bfloat16)
+        small = torch.zeros(53000, device=dev, dtype=torch.bfloat16)
+        for it in range(6):
+            for j, t in enumerate((big, small)):
+                t.copy_(_inputs(rank, t.numel(), torch.bfloat16, 200 + 2 * it + j).to(dev))
+                comm.all_reduce(t)
+            torch.cuda.synchronize()
+            for j, t in enumerate((big, small)):
+                exp = sum(_inputs(r, t.numel(), torch.bfloat16, 200 + 2 * it + j).float()
+                          for r in range(world)).to(torch.bfloat16)
+                if not torch.equal(t.cpu(), exp):
+                    errs.append(("mixed", it, j))
         st = comm.status()
         comm.close()
         dist.barrier()
