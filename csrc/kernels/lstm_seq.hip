@@ -61,15 +61,23 @@ __global__ __launch_bounds__(1024) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
   float creg[LR * H / 1024];
 #pragma unroll
   for (int q = 0; q < LR * H / 1024; ++q) creg[q] = 0.f;
+  // per-column gate bias (forget_bias folded in), hoisted out of the recurrence
+  float bias_r[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int col = c0 + 16 * j + mrow;
+    bias_r[j] = a.bias[col] + (col / H == 2 ? a.forget_bias : 0.f);
+  }
+  // x_{t+1} does not depend on the recurrence: each thread prefetches its element (LR * I <= 1024,
+  // checked at launch) right after step t's first barrier, so its HBM latency hides under step
+  // t's MFMA + cell update instead of heading step t+1's critical path
+  const bool xl = tid < LR * a.I;
+  const int xr = xl ? tid / a.I : 0, xk = xl ? tid - xr * a.I : 0;
+  float xnext = 0.f;
   for (int t = 0; t < a.T; ++t) {
-    if (t > 0) {
-      const float* xt = a.xh + (long)t * B * rowKT;
-      for (int e = tid; e < LR * a.I; e += 1024) {
-        const int r = e / a.I, k = e - r * a.I;
-        As[r * AP + k] = xt[(long)(r0 + r) * rowKT + k];
-      }
-    }
+    if (t > 0 && xl) As[xr * AP + xk] = xnext;
     __syncthreads();
+    if (t + 1 < a.T && xl) xnext = a.xh[((long)(t + 1) * B + r0 + xr) * rowKT + xk];
     f32x4_t acc[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -84,7 +92,7 @@ __global__ __launch_bounds__(1024) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     for (int j = 0; j < TPW; ++j) {
       const int col = c0 + 16 * j + mrow;
       const int gt = col / H;  // 0 i, 1 j, 2 f, 3 o
-      const float bias = a.bias[col] + (gt == 2 ? a.forget_bias : 0.f);
+      const float bias = bias_r[j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
@@ -142,17 +150,36 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
 #pragma unroll
     for (int q = 0; q < KH / 16; ++q) kb[q] = *reinterpret_cast<const f32x4_t*>(krow + 16 * q + 4 * g);
   }
+  // step t's saved gates and cells do not depend on the recurrence: registers hold step t's
+  // (i, j, f, o, c_t, c_{t-1}) and step t-1's are loaded as soon as step t has read them, so
+  // their HBM latency hides under step t's dgate stores and dh MFMA
+  constexpr int NQ = LR * H / 1024;
+  float pa[NQ][4], pc[NQ], pcp[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int p = tid + 1024 * q, r = p / H, u = p - r * H;
+    const int t = a.T - 1;
+    const float* ac = a.act + ((long)t * B + r0 + r) * G4;
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) pa[q][gi] = ac[gi * H + u];
+    const long ci = ((long)t * B + r0 + r) * H + u;
+    pc[q] = a.c[ci];
+    pcp[q] = t > 0 ? a.c[ci - (long)B * H] : 0.f;
+  }
   for (int t = a.T - 1; t >= 0; --t) {
-    const float* act_t = a.act + ((long)t * B + r0) * G4;
     float* dg_t = a.dg + ((long)t * B + r0) * G4;
 #pragma unroll
-    for (int q = 0; q < LR * H / 1024; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int p = tid + 1024 * q, r = p / H, u = p - r * H;
-      const float* ac = act_t + (long)r * G4;
-      const float si = ac[u], tj = ac[H + u], sf = ac[2 * H + u], so = ac[3 * H + u];
-      const long ci = ((long)t * B + r0 + r) * H + u;
-      const float c = a.c[ci];
-      const float cp = t > 0 ? a.c[ci - (long)B * H] : 0.f;
+      const float si = pa[q][0], tj = pa[q][1], sf = pa[q][2], so = pa[q][3];
+      const float c = pc[q], cp = pcp[q];
+      if (t > 0) {  // prefetch step t-1
+        const float* an = a.act + ((long)(t - 1) * B + r0 + r) * G4;
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) pa[q][gi] = an[gi * H + u];
+        pc[q] = cp;
+        pcp[q] = t > 1 ? a.c[((long)(t - 2) * B + r0 + r) * H + u] : 0.f;
+      }
       const float dh = P0[r * H + u] + P1[r * H + u];
       const float tc = tanhf(c);
       const float dc = dcreg[q] + dh * so * (1.f - tc * tc);
@@ -190,7 +217,7 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
 
 bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
   // register-resident K slice: instantiated for the MNIST row-LSTM (I = 28, H = 128)
-  if (a.H != 128 || a.I != 28 || a.B % LR) return false;
+  if (a.H != 128 || a.I != 28 || a.B % LR || LR * a.I > 1024) return false;
   const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * a.H + 4)) * sizeof(float);
   auto k = lstm_seq_fwd_kernel<128, (28 + 128) / 4>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
