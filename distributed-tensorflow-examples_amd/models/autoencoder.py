@@ -78,7 +78,7 @@ class AutoencoderProgram(StepProgram):
 
     def compute_grads(self):
         B = self.batch_size
-        self.P.grad.zero_()
+        # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
         y = self.forward()
         ops.mse_sigmoid(y, self.x, self.loss, self.dz[3])
         for i in range(3, -1, -1):

@@ -106,7 +106,7 @@ class GanProgram(StepProgram):
     def compute_grads(self):
         B, W, G = self.batch_size, self.W, self.G
         R, K = ops.RMAJ, ops.KMAJ
-        self.P.grad.zero_()
+        # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
         self.forward()
         ops.gan_loss(self.p[:B], self.p[B:], self.gen_loss, self.disc_loss, self.dlog[:B], self.dlog[B:],
                      self.dlog_g)

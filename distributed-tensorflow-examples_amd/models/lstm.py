@@ -106,7 +106,7 @@ class LstmProgram(StepProgram):
 
     def compute_grads(self):
         B = self.batch_size
-        self.P.grad.zero_()
+        # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
         self.loss.zero_()
         self.correct.zero_()
         self.forward()

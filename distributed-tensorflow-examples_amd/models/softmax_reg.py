@@ -52,7 +52,7 @@ class SoftmaxProgram(StepProgram):
 
     def compute_grads(self):
         B = self.batch_size
-        self.P.grad.zero_()
+        # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
         self.loss.zero_()
         self.correct.zero_()
         ops.gemm(self.x, self.W, self.logits, M=B, N=NC, K=IMG, bmode=ops.RMAJ, ldb=NC, bias=self.b)

@@ -26,12 +26,19 @@ def _cmp(cpu, gpu, tol):
         assert rel < tol, (s.name, rel)
 
 
+def _poison(*progs):
+    """NaN-fill the gradient buffers: compute_grads must store every element (it does not zero)."""
+    for p in progs:
+        p.P.grad.fill_(float("nan"))
+
+
+@pytest.mark.parametrize("B", [32, 256])
 @pytest.mark.parametrize("name", ["softmax", "encoder", "lstm"])
-def test_supervised_models_gpu_match_cpu(name):
+def test_supervised_models_gpu_match_cpu(name, B):
     torch.manual_seed(0)
     model = {"softmax": SoftmaxRegressionModel, "encoder": AutoencoderModel, "lstm": LstmModel}[name]()
-    B = 32
     cpu, gpu = _pair(model, B)
+    _poison(cpu, gpu)
     x = torch.rand(B, 784)
     y = F.one_hot(torch.randint(0, 10, (B,)), 10).float()
     batch = x if name == "encoder" else (x, y)
@@ -43,11 +50,12 @@ def test_supervised_models_gpu_match_cpu(name):
     assert abs(float(mc["loss"]) - float(mg["loss"])) < 1e-4 * max(1.0, abs(float(mc["loss"])))
 
 
-def test_gan_gpu_matches_cpu():
+@pytest.mark.parametrize("B", [64, 128])
+def test_gan_gpu_matches_cpu(B):
     torch.manual_seed(1)
     model = GanModel()
-    B = 64
     cpu, gpu = _pair(model, B)
+    _poison(cpu, gpu)
     x = torch.rand(B, 784)
     gpu.load_batch(x.cuda())
     cpu.load_batch(x)
