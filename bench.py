@@ -2,268 +2,385 @@
 """Headline benchmark: MNIST 2-layer CNN, sync all-reduce data parallel, bf16,
 images/sec for the whole job (BASELINE.json metric).
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W        (self-launches N ranks)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
-    python bench.py --model resnet20 | resnet50     (BASELINE.json configs 3 and 5)
+    python bench.py --model resnet20 | resnet50          (BASELINE.json configs 3 and 5)
+    python bench.py --mode ps --gpus N                   (config 4: 1 ps + N workers, async)
+
+Launching: under torchrun (``WORLD_SIZE`` set) each process is one rank.  Without
+``WORLD_SIZE`` and with ``--gpus N > 1`` this process is a pure launcher: it starts N
+child ranks of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 in their
+environment) BEFORE touching the GPU, waits for them, and exits with the worst exit
+code; rank 0's JSON line is the result.  Every rank asserts WORLD_SIZE == --gpus.
 
 Weak scaling: every rank trains --batch_size images per step (global batch =
 batch_size * N).  Synthetic MNIST-shaped data resident in HBM, random-init
 weights.  The timed region is exactly K full training steps (device-side batch
-sampling, forward, backward, RCCL gradient all-reduce, fused Adam), bracketed
-by barrier + device synchronize on both sides; the reported time is the MAX
-over ranks.  Rank 0 prints one JSON line.
+sampling, forward, backward, gradient all-reduce, fused Adam), bracketed by
+barrier + device synchronize on both sides; the reported time is the MAX over
+ranks.  The K steps are also cut into up to 5 windows by hipEvents recorded
+between replays (no sync inside the timed region) so the JSON carries its own
+spread.  Rank 0 prints one JSON line.
+
+Reference: the reference's only performance output is its per-step wall-clock
+print (gan/distributed_gan.py:195-196, encoder/distributed_encoder.py:166-167).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
-import dtfe  # noqa: E402,F401
-from dtfe.models.mnist_cnn import MnistCnnTrainer, num_params  # noqa: E402
-from dtfe.parallel.allreduce import BucketAllReduce  # noqa: E402
-from dtfe.parallel.comm import make_comm  # noqa: E402
-from dtfe.utils.graphs import StepGraph, graphs_enabled  # noqa: E402
-
-DEFAULT_BATCH = 1024  # per GPU
+DEFAULT_BATCH = 1024  # per GPU, MNIST CNN
+MODEL_BATCH = {"mnist_cnn": 1024, "resnet20": 256, "resnet50": 256}
 
 
-def _baseline(n_gpus, batch, model="mnist_cnn"):
-    """Stock-PyTorch (DDP + MIOpen/hipBLASLt, bf16) images/sec measured on the same MI355X
-    box and config by bench/stock_torch_cnn.py (bench/stock_torch_resnet.py for the
-    ResNets); see BASELINE.md."""
-    p = os.path.join(ROOT, "bench", "stock_baseline.json")
-    try:
-        with open(p) as f:
-            tab = json.load(f)
-        key = f"{n_gpus}x{batch}" if model == "mnist_cnn" else f"{model}_{n_gpus}x{batch}"
-        return tab.get(key)
-    except (OSError, ValueError):
-        return None
-
-
-def replicas_identical(params, device, backend):
-    """After the timed steps (outside the timing): every replica trained on different data
-    but applied the same all-reduced gradients, so all parameter copies must be bitwise equal."""
-    ref = params.detach().clone() if backend == "nccl" else params.detach().cpu()
-    dist.broadcast(ref, src=0)
-    d = (params.detach().to(ref.device) - ref).abs().max().reshape(1).double()
-    dist.all_reduce(d, op=dist.ReduceOp.MAX)
-    return bool(float(d.item()) == 0.0)
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="number of ranks (one per GPU); default 1 "
+                    "or WORLD_SIZE under torchrun")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch_size", type=int, default=DEFAULT_BATCH, help="per-GPU batch")
+    ap.add_argument("--batch_size", type=int, default=None, help="per-GPU batch (default: per model)")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
+    ap.add_argument("--mode", choices=["allreduce", "ps"], default="allreduce",
+                    help="allreduce: sync data parallel (headline).  ps: async parameter server, "
+                         "1 ps service + --gpus workers (BASELINE.json config 4)")
     ap.add_argument("--comm", choices=["auto", "rccl", "ipc", "pg"], default="auto",
                     help="auto: per bucket size the faster of dtfe's RCCL communicator and the hipIpc two-shot "
                          "kernel (timed at setup); rccl / ipc: force one; all three run on a side stream with the "
                          "whole step captured in one hipGraph.  pg: torch.distributed ProcessGroupNCCL, eager steps")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
-    args = ap.parse_args()
-    if args.model != "mnist_cnn":
-        return bench_resnet(args)
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        local_rank %= torch.cuda.device_count()
-        torch.cuda.set_device(local_rank)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group("gloo")
-    device = torch.device("cuda", local_rank)
 
-    allreduce = None
-    trainer = MnistCnnTrainer(args.batch_size, device, seed=0, world_size=world, rank=rank)
-    comm = None
-    if world > 1:
-        if args.comm != "pg" and (args.backend == "nccl" or args.comm == "ipc"):
-            esz = 2 if args.comm_dtype == "bf16" else 4
-            comm = make_comm(device, None, [(hi - lo) * esz for lo, hi in trainer.buckets],
-                             torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, mode=args.comm,
-                             log=(lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None)
-        allreduce = BucketAllReduce(trainer.P.grad, trainer.buckets, comm=comm,
-                                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start ``n`` child ranks of this script (no GPU call has been made in this process) and
+    return the worst exit code.  If one rank fails the others are stopped (by PID)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DTFE_BENCH_CHILD="1")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in live:  # a failed rank would leave its peers blocked in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+        if p.returncode not in (0, None) and rc == 0:
+            rc = p.returncode
+    return rc if rc >= 0 else 128 - rc
+
+
+# ----------------------------------------------------------------------------- per rank
+class Dist:
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        want = args.gpus if args.gpus is not None else self.world
+        if want != self.world:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (want, self.world))
+        self.backend = args.backend
+        if self.world > 1:
+            ndev = torch.cuda.device_count()
+            if args.backend == "nccl" and self.local_rank >= ndev:
+                raise SystemExit("bench.py: rank %d needs GPU %d but only %d are visible (RCCL needs one GPU "
+                                 "per rank; use --backend gloo --comm ipc to rehearse on fewer GPUs)"
+                                 % (self.rank, self.local_rank, ndev))
+            self.local_rank %= max(1, ndev)
+            torch.cuda.set_device(self.local_rank)
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            else:
+                dist.init_process_group("gloo")
+        self.device = torch.device("cuda", self.local_rank)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def distinct_devices(self) -> int:
+        """Distinct physical GPUs behind the ranks (a gloo rehearsal may share one)."""
+        me = "%s:%d" % (socket.gethostname(), self.local_rank)
+        if self.world == 1:
+            return 1
+        allv = [None] * self.world
+        dist.all_gather_object(allv, me)
+        return len(set(allv))
+
+    def close(self):
+        if self.world > 1:
+            dist.destroy_process_group()
+
+
+def replicas_identical(params, d: Dist):
+    """After the timed steps (outside the timing): every replica trained on different data
+    but applied the same all-reduced gradients, so all parameter copies must be bitwise equal."""
+    ref = params.detach().clone() if d.backend == "nccl" else params.detach().cpu()
+    dist.broadcast(ref, src=0)
+    diff = (params.detach().to(ref.device) - ref).abs().max().reshape(1).double()
+    dist.all_reduce(diff, op=dist.ReduceOp.MAX)
+    return bool(float(diff.item()) == 0.0)
+
+
+def timed(runner, steps: int, warmup: int, d: Dist):
+    """W untimed steps, then exactly K steps between barrier+sync brackets.  Returns
+    (elapsed_s max over ranks, per-window ms/step list measured on this rank)."""
+    for _ in range(warmup):
+        runner()
+    torch.cuda.synchronize()
+    d.barrier()
+    torch.cuda.synchronize()
+    nwin = max(1, min(5, steps))
+    cuts = [round(i * steps / nwin) for i in range(nwin + 1)]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in cuts]
+    t0 = time.perf_counter()
+    evs[0].record()
+    w = 1
+    for i in range(steps):
+        runner()
+        if i + 1 == cuts[w]:
+            evs[w].record()
+            w += 1
+    torch.cuda.synchronize()
+    d.barrier()
+    torch.cuda.synchronize()
+    elapsed = d.max(time.perf_counter() - t0)
+    win = [evs[i].elapsed_time(evs[i + 1]) / max(1, cuts[i + 1] - cuts[i]) for i in range(nwin)]
+    return elapsed, win
+
+
+def _baseline(n_gpus, batch, model="mnist_cnn"):
+    """Faster of the stock-PyTorch rows (eager DDP, and graph-captured + fused Adam/SGD) measured on
+    the same MI355X box and config by bench/stock_torch_cnn.py / stock_torch_resnet.py; BASELINE.md."""
+    p = os.path.join(ROOT, "bench", "stock_baseline.json")
+    try:
+        with open(p) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return None
+    key = f"{n_gpus}x{batch}" if model == "mnist_cnn" else f"{model}_{n_gpus}x{batch}"
+    vals = [v for k, v in tab.items() if k == key or k.startswith(key + "_")]
+    vals = [v for v in vals if isinstance(v, (int, float))]
+    return max(vals) if vals else None
+
+
+def _make_comm(args, d: Dist, bucket_bytes):
+    from dtfe.parallel.comm import make_comm
+
+    if d.world == 1 or args.comm == "pg" or not (args.backend == "nccl" or args.comm == "ipc"):
+        return None
+    return make_comm(d.device, None, bucket_bytes,
+                     torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, mode=args.comm,
+                     log=(lambda m: print(m, file=sys.stderr, flush=True)) if d.rank == 0 else None)
+
+
+def _comm_info(args, d: Dist, comm):
+    if d.world == 1:
+        return {"grad_allreduce": "none (1 rank)", "ranks_seen_by_comm": 1}
+    if comm is not None:
+        eng = "in-graph [%s]" % comm.describe()
+        seen = comm.world
+    else:
+        eng = "ProcessGroupNCCL (RCCL)" if args.backend == "nccl" else "gloo"
+        seen = dist.get_world_size()
+    return {"grad_allreduce": "%s bucketed %s" % (eng, args.comm_dtype), "ranks_seen_by_comm": seen}
+
+
+def _emit(d: Dist, args, metric, value, elapsed, win, model_desc, B, extra, data_desc):
+    base = _baseline(d.world, B, args.model)
+    rec = {
+        "metric": metric,
+        "value": round(value, 1),
+        "unit": "images/sec",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1000, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / base, 3) if base else None,
+        "dtype": "bf16",
+        "data": data_desc,
+        "config": dict({"model": model_desc, "global_batch": B * d.world, "seq_len": None,
+                        "parallelism": "dp%d" % d.world, "per_gpu_batch": B}, **extra),
+        "window_ms_per_step": [round(x, 4) for x in win],
+        "median_window_ms_per_step": round(statistics.median(win), 4),
+    }
+    if d.rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
+def bench_cnn(args, d: Dist):
+    import dtfe  # noqa: F401
+    from dtfe.models.mnist_cnn import MnistCnnTrainer, num_params
+    from dtfe.parallel.allreduce import BucketAllReduce
+    from dtfe.utils.graphs import StepGraph, graphs_enabled
+
+    B = args.batch_size or MODEL_BATCH["mnist_cnn"]
+    trainer = MnistCnnTrainer(B, d.device, seed=0, world_size=d.world, rank=d.rank)
+    comm = allreduce = None
+    cdt = torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32
+    if d.world > 1:
+        esz = 2 if args.comm_dtype == "bf16" else 4
+        comm = _make_comm(args, d, [(hi - lo) * esz for lo, hi in trainer.buckets])
+        allreduce = BucketAllReduce(trainer.P.grad, trainer.buckets, comm=comm, comm_dtype=cdt)
         trainer.allreduce = allreduce
 
     if allreduce is not None and allreduce.grad16 is not None:
         def step():
-            trainer.step(grad16=allreduce.grad16, gscale=1.0 / world)
+            trainer.step(grad16=allreduce.grad16, gscale=1.0 / d.world)
     else:
         step = trainer.step
-    # the whole step (with the overlapped RCCL all-reduce at world > 1) is one hipGraph replay
-    runner = StepGraph(step, warmup=2, enabled=((world == 1 or comm is not None) and not args.no_graph
+    # the whole step (with the overlapped all-reduce at world > 1) is one hipGraph replay
+    runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
                                                 and graphs_enabled()), capture_error_mode="thread_local")
-
-    for _ in range(args.warmup):
-        runner()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    loss = float(trainer.loss_sum.item()) / args.batch_size
-    consistent = replicas_identical(trainer.P.master, device, args.backend) if world > 1 else None
-    global_batch = args.batch_size * world
-    value = global_batch * args.steps / elapsed
-    base = _baseline(world, args.batch_size)
-    if rank == 0:
-        print(json.dumps({
-            "metric": "images/sec (whole node), MNIST CNN sync all-reduce",
-            "value": round(value, 1),
-            "unit": "images/sec",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1000, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / base, 3) if base else None,
-            "dtype": "bf16",
-            "data": "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)",
-            "config": {
-                "model": "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(),
-                "global_batch": global_batch,
-                "seq_len": None,
-                "parallelism": "dp%d" % world,
-                "per_gpu_batch": args.batch_size,
-                "optimizer": "adam (TF1)",
-                "grad_allreduce": ("%s bucketed %s" % ("in-graph [%s]" % comm.describe() if comm is not None else
-                                                       "rccl (ProcessGroupNCCL)" if args.backend == "nccl" else "gloo",
-                                                       args.comm_dtype))
-                if world > 1 else "none (1 rank)",
-                "hip_graph": runner.graph is not None,
-                "last_loss": round(loss, 4),
-                "replicas_identical": consistent,
-            },
-        }), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    elapsed, win = timed(runner, args.steps, args.warmup, d)
+    if comm is not None and hasattr(comm, "check_health"):
+        comm.check_health()
+    loss = float(trainer.loss_sum.item()) / B
+    same = replicas_identical(trainer.P.master, d) if d.world > 1 else None
+    ndev = d.distinct_devices()
+    extra = {"optimizer": "adam (TF1)", "hip_graph": runner.graph is not None, "last_loss": round(loss, 4),
+             "replicas_identical": same, "distinct_gpus": ndev}
+    extra.update(_comm_info(args, d, comm))
+    _emit(d, args, "images/sec (whole node), MNIST CNN sync all-reduce", B * d.world * args.steps / elapsed,
+          elapsed, win, "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(),
+          B, extra, "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)")
+    if comm is not None:
+        comm.close()
 
 
-def bench_resnet(args):
+def bench_resnet(args, d: Dist):
     """ResNet-20 (CIFAR-10 shape) / ResNet-50 (ImageNet shape) sync all-reduce step: device-side
-    batch sampling from an HBM-resident synthetic set, fwd+bwd, RCCL all-reduce, Momentum apply."""
+    batch sampling (+ one-hot labels) from an HBM-resident synthetic set, fwd+bwd, all-reduce,
+    Momentum apply."""
+    import dtfe  # noqa: F401
     from dtfe import ops
     from dtfe.models.resnet import ResNetModel
     from dtfe.optim import Optimizer
+    from dtfe.parallel.allreduce import BucketAllReduce
     from dtfe.train import _buckets
+    from dtfe.utils.graphs import StepGraph, graphs_enabled
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
     model = ResNetModel(arch=args.model)
-    B = args.batch_size if args.batch_size != DEFAULT_BATCH else (256 if args.model == "resnet20" else 64)
-    prog = model.program(device, B, seed=0)
-    gstep = torch.zeros(1, dtype=torch.int32, device=device)
+    B = args.batch_size or MODEL_BATCH[args.model]
+    prog = model.program(d.device, B, seed=0)
+    gstep = torch.zeros(1, dtype=torch.int32, device=d.device)
     cfg, names, bp = model.opt_groups[0]
     opt = Optimizer(cfg, prog.P, var_list=names, global_step=gstep, beta_power_names=bp)
     ar = comm = None
-    if world > 1:
-        dist.broadcast(prog.P.master, src=0)
+    cdt = torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32
+    if d.world > 1:
+        if d.backend == "nccl":
+            dist.broadcast(prog.P.master, src=0)
+        else:
+            m = prog.P.master.detach().cpu()
+            dist.broadcast(m, src=0)
+            prog.P.master.copy_(m)
         prog.P.refresh_copies()
         bks = _buckets(prog.P)
         esz = 2 if args.comm_dtype == "bf16" else 4
-        comm = make_comm(device, None, [(hi - lo) * esz for lo, hi in bks],
-                         torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, mode=args.comm,
-                         log=(lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None) \
-            if args.comm != "pg" else None
-        ar = BucketAllReduce(prog.P.grad, bks, comm=comm,
-                             comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
-        prog.grad_ready = ar.ready  # buckets launch during backward (overlap on RCCL's stream)
+        comm = _make_comm(args, d, [(hi - lo) * esz for lo, hi in bks])
+        ar = BucketAllReduce(prog.P.grad, bks, comm=comm, comm_dtype=cdt)
+        prog.grad_ready = ar.ready  # buckets launch during backward (overlap on the side stream)
     n_pool = 4096 if args.model == "resnet20" else 512
-    g = torch.Generator().manual_seed(rank + 11)
+    g = torch.Generator().manual_seed(d.rank + 11)
     pix = model.image * model.image * model.channels
-    images = torch.randint(0, 256, (n_pool, pix), generator=g, dtype=torch.uint8).to(device)
-    labels = torch.randint(0, model.num_classes, (n_pool,), generator=g, dtype=torch.int32).to(device)
-    lab = torch.empty(B, dtype=torch.int32, device=device)
-    ctr = torch.zeros(1, dtype=torch.int64, device=device)
-    done = torch.zeros(1, dtype=torch.int32, device=device)
+    images = torch.randint(0, 256, (n_pool, pix), generator=g, dtype=torch.uint8).to(d.device)
+    labels = torch.randint(0, model.num_classes, (n_pool,), generator=g, dtype=torch.int32).to(d.device)
+    lab = torch.empty(B, dtype=torch.int32, device=d.device)
+    ctr = torch.zeros(1, dtype=torch.int64, device=d.device)
+    done = torch.zeros(1, dtype=torch.int32, device=d.device)
 
     def step():
-        ops.gather_rows(images, prog.x.view(B, -1), None, labels, lab, seed=rank + 1, counter=ctr, done=done)
-        prog.y.zero_()
-        prog.y.scatter_(1, lab.long().unsqueeze(1), 1.0)
-        prog.compute_grads()
+        # batch rows + their one-hot label rows in ONE launch (no per-step fill / scatter kernels)
+        ops.gather_rows(images, prog.x.view(B, -1), None, labels, lab, seed=d.rank + 1, counter=ctr, done=done,
+                        zero=prog.step_accumulators(), onehot=prog.y)
+        prog.compute_grads(zeroed=True)
         g16 = None
         if ar is not None:
             ar.flush()
             ar.wait()
             g16 = ar.grad16
-        opt.step(grad16=g16, gscale=1.0 / world) if g16 is not None else opt.step(gscale=1.0 / world)
+        opt.step(grad16=g16, gscale=1.0 / d.world) if g16 is not None else opt.step(gscale=1.0 / d.world)
 
-    runner = StepGraph(step, warmup=2, enabled=((world == 1 or comm is not None) and not args.no_graph
+    runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
                                                 and graphs_enabled()), capture_error_mode="thread_local")
-    for _ in range(args.warmup):
-        runner()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    value = B * world * args.steps / elapsed
-    base = _baseline(world, B, args.model)
-    if rank == 0:
-        print(json.dumps({
-            "metric": "images/sec (whole node), %s sync all-reduce" % args.model,
-            "value": round(value, 1), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": round(value / base, 3) if base else None, "dtype": "bf16",
-            "data": "synthetic (HBM-resident %dx%dx%d uint8 images, random labels; random-init weights)"
-                    % (model.image, model.image, model.channels),
-            "config": {"model": "%s (%d params)" % (args.model, model.num_params()), "global_batch": B * world,
-                       "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_batch": B,
-                       "optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None,
-                       "last_loss": round(float(prog.loss.item()) / B, 4)},
-        }), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    elapsed, win = timed(runner, args.steps, args.warmup, d)
+    same = replicas_identical(prog.P.master, d) if d.world > 1 else None
+    extra = {"optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None,
+             "last_loss": round(float(prog.loss.item()) / B, 4), "replicas_identical": same,
+             "distinct_gpus": d.distinct_devices()}
+    extra.update(_comm_info(args, d, comm))
+    _emit(d, args, "images/sec (whole node), %s sync all-reduce" % args.model, B * d.world * args.steps / elapsed,
+          elapsed, win, "%s (%d params)" % (args.model, model.num_params()), B, extra,
+          "synthetic (HBM-resident %dx%dx%d uint8 images, random labels; random-init weights)"
+          % (model.image, model.image, model.channels))
+    if comm is not None:
+        comm.close()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.mode == "ps":
+        from bench_ps import main as ps_main  # noqa: E402  (bench/ps harness; launches its own ranks)
+
+        return ps_main(args)
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        return launch_ranks(args.gpus, argv)
+    d = Dist(args)
+    try:
+        if args.model == "mnist_cnn":
+            bench_cnn(args, d)
+        else:
+            bench_resnet(args, d)
+    finally:
+        d.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

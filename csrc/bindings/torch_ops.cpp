@@ -371,9 +371,17 @@ int data_code(const Tensor& t) {
 
 void gather_rows(const Tensor& src, const Tensor& dst, const optional<Tensor>& idx, const optional<Tensor>& labels_src,
                  const optional<Tensor>& labels_dst, int64_t seed, const optional<Tensor>& counter,
-                 const optional<Tensor>& done, at::TensorList zero) {
+                 const optional<Tensor>& done, at::TensorList zero, const optional<Tensor>& onehot) {
   check_cuda(src, "src");
   dtfe::GatherArgs a{};
+  if (onehot.has_value()) {
+    check_cuda(*onehot, "onehot");
+    TORCH_CHECK(onehot->scalar_type() == at::kFloat && onehot->is_contiguous() && onehot->dim() == 2 &&
+                onehot->size(0) == dst.size(0) && labels_src.has_value(),
+                "gather_rows: onehot must be contiguous f32 [B][ncls] and needs labels_src");
+    a.onehot = onehot->data_ptr<float>();
+    a.ncls = (int)onehot->size(1);
+  }
   TORCH_CHECK(zero.size() <= 4, "gather_rows: at most 4 zero ranges");
   for (const Tensor& z : zero) {
     check_cuda(z, "zero");
@@ -691,7 +699,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork) -> ()");
   m.def(
       "gather_rows(Tensor src, Tensor(a!) dst, Tensor? idx, Tensor? labels_src, Tensor(b!)? labels_dst, int seed,"
-      " Tensor(c!)? counter, Tensor(d!)? done, Tensor(e!)[] zero) -> ()");
+      " Tensor(c!)? counter, Tensor(d!)? done, Tensor(e!)[] zero, Tensor(f!)? onehot=None) -> ()");
   m.def("uniform_fill(Tensor(a!) out, float lo, float hi, int seed, Tensor(b!)? counter, Tensor(c!)? done) -> ()");
   m.def("cast_(Tensor src, Tensor(a!) dst) -> ()");
   m.def(

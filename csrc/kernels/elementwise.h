@@ -17,6 +17,8 @@ struct GatherArgs {
   // step-prologue zeroing fused into the same launch: up to 4 word ranges (accumulators the
   // step's atomics add into - loss / hit counters, atomically reduced weight grads)
   uint32_t* zptr[4]; long zlen[4]; int nz;
+  // optional one-hot label rows [B][ncls] fp32 written in the same launch (softmax-xent input)
+  float* onehot; int ncls;
 };
 void launch_gather_rows(const GatherArgs& a, hipStream_t s);
 

@@ -88,6 +88,14 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
       }
     }
   }
+  if (a.onehot) {
+    const long n = (long)a.B * a.ncls;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+      const int b = (int)(i / a.ncls);
+      const int c = (int)(i - (long)b * a.ncls);
+      a.onehot[i] = a.labels_src[gather_src_row(a, b, step)] == c ? 1.f : 0.f;
+    }
+  }
   for (int z = 0; z < a.nz; ++z)
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < a.zlen[z]; i += (long)gridDim.x * 256) a.zptr[z][i] = 0u;
   advance_counter_last_block(a.counter, a.done, 1);

@@ -136,11 +136,22 @@ class LstmProgram(StepProgram):
                 ops.gemm(self.dg[t], Kh, self.dh, M=B, N=H, K=4 * H, bmode=ops.KMAJ, ldb=4 * H)
 
     def evaluate(self, images, labels) -> float:
-        """accuracy = mean(argmax(softmax(logits)) == argmax(Y)) (LSTM:98-100, 134-138)."""
-        n = images.shape[0]
-        assert n == self.batch_size, "evaluation batch must equal the program batch"
-        self.load_batch((images, labels))
-        self.forward()
-        self.correct.zero_()
-        ops.softmax_xent(self.logits, labels_oh=self.y, correct=self.correct)
-        return int(self.correct.item()) / n
+        """accuracy = mean(argmax(softmax(logits)) == argmax(Y)) (LSTM:98-100, 134-138).  Any number
+        of images: evaluated in program-batch chunks, the last one padded by repeating rows (only
+        the real rows are counted)."""
+        n, B = images.shape[0], self.batch_size
+        if n == B:
+            self.load_batch((images, labels))
+            self.forward()
+            self.correct.zero_()
+            ops.softmax_xent(self.logits, labels_oh=self.y, correct=self.correct)
+            return int(self.correct.item()) / n
+        hits = 0
+        for lo in range(0, n, B):
+            m = min(B, n - lo)
+            idx = torch.arange(lo, lo + B, device=images.device).clamp_max(n - 1)
+            xb, yb = images[idx], labels[idx]
+            self.load_batch((xb, yb))
+            self.forward()
+            hits += int((self.logits[:m].argmax(1) == self.y[:m].argmax(1)).sum().item())
+        return hits / n

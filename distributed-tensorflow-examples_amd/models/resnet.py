@@ -494,11 +494,17 @@ class ResNetProgram(StepProgram):
         st.wgrad(self.dc_stem, self.x)
         self._ready(0)
 
-    def compute_grads(self):
-        self.P.grad.zero_()
-        self.arena.buf.zero_()
-        self.loss.zero_()
-        self.correct.zero_()
+    def step_accumulators(self):
+        """The buffers a step accumulates into (cleared at its start): gradients, BN statistics,
+        loss and hit counters.  ``ops.gather_rows(zero=...)`` clears them inside the batch gather."""
+        return [self.P.grad, self.arena.buf, self.loss, self.correct]
+
+    def compute_grads(self, zeroed: bool = False):
+        """Forward + backward.  ``zeroed``: the caller already cleared ``step_accumulators()``
+        (bench.py does it in the fused gather launch, so no fill kernel runs per step)."""
+        if not zeroed:
+            for t in self.step_accumulators():
+                t.zero_()
         self.forward()
         self.backward()
         return {"loss": self.loss / self.batch_size, "correct": self.correct}

@@ -446,14 +446,19 @@ def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, mome
 
 
 # ------------------------------------------------------------- elementwise
-def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, counter=None, done=None, zero=()):
+def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, counter=None, done=None, zero=(),
+                onehot=None):
     """dst[b] = src[row(b)] (+ labels); ``zero``: up to 4 contiguous tensors cleared in the same
-    launch (a step's accumulators), saving one fill kernel each."""
+    launch (a step's accumulators), saving one fill kernel each; ``onehot``: f32 [B][ncls] one-hot
+    rows of the gathered labels, also written in the same launch."""
     if dst.is_cuda:
-        require().gather_rows(src, dst, idx, labels_src, labels_dst, seed, counter, done, list(zero))
+        require().gather_rows(src, dst, idx, labels_src, labels_dst, seed, counter, done, list(zero), onehot)
         return dst
     for z in zero:
         z.zero_()
+    if onehot is not None:
+        onehot.zero_()
+        onehot.scatter_(1, labels_src[idx.long()].long().unsqueeze(1), 1.0)
     assert idx is not None, "CPU gather needs explicit indices"
     rows = src[idx.long()]
     if src.dtype == torch.uint8:

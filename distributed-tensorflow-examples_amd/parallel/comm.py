@@ -22,11 +22,34 @@ from .rccl import RcclComm
 class RoutedComm:
     """``all_reduce`` dispatching on the tensor's byte size (decided once, at setup)."""
 
-    def __init__(self, default, routes=None, names=None):
+    def __init__(self, default, routes=None, names=None, group=None, device=None):
         self.default = default
         self.routes = dict(routes or {})
         self.names = dict(names or {})
         self.comms = [default] + [c for c in self.routes.values() if c is not default]
+        self.group = group
+        self.device = device
+
+    @property
+    def world(self) -> int:
+        """Ranks the collective engine spans (reported by bench.py as ranks_seen_by_comm)."""
+        return int(self.default.world)
+
+    def check_health(self):
+        """Raise on EVERY rank if any rank's IPC kernel hit a barrier timeout since setup.
+
+        The IPC all-reduce runs inside replayed hipGraphs; a peer that misses a barrier for longer
+        than the timeout makes the kernel set its error word and leave the bucket half reduced, and
+        nothing else would notice.  Reading the word synchronizes the device, so callers do it every
+        ``log_every`` steps and once at the end; the decision is agreed over the group so all ranks
+        stop together instead of training on diverged replicas."""
+        bad = 0.0
+        for c in self.comms:
+            if hasattr(c, "status"):
+                bad = max(bad, float(c.status()))
+        if _agree(bad, self.group, self.device) > 0:
+            raise RuntimeError("IPC all-reduce barrier timeout on %s rank: gradients of that step were not "
+                               "fully reduced; replicas may have diverged" % ("this" if bad else "another"))
 
     def all_reduce(self, t: torch.Tensor, *args):
         self.routes.get(t.numel() * t.element_size(), self.default).all_reduce(t, *args)
@@ -75,10 +98,11 @@ def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: s
     cap = max([int(b) for b in bucket_bytes] + [1 << 20]) + 4096
     if mode == "ipc":  # IPC only (no RCCL communicator: also works for several ranks sharing one GPU)
         ipc = IpcComm(device, group, cap_bytes=cap)
-        return RoutedComm(ipc, {int(b): ipc for b in bucket_bytes}, {int(b): "ipc" for b in bucket_bytes})
+        return RoutedComm(ipc, {int(b): ipc for b in bucket_bytes}, {int(b): "ipc" for b in bucket_bytes},
+                          group=group, device=device)
     rccl = RcclComm(device, group)
     if mode == "rccl":
-        return RoutedComm(rccl)
+        return RoutedComm(rccl, group=group, device=device)
     ipc = None
     try:
         ipc = IpcComm(device, group, cap_bytes=cap, fallback=rccl)
@@ -90,7 +114,7 @@ def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: s
     if _agree(1.0 - ok, group, device) > 0:   # one rank failed: nobody uses IPC
         if ipc is not None:
             ipc.close()
-        return RoutedComm(rccl)
+        return RoutedComm(rccl, group=group, device=device)
     routes, names = {}, {}
     esz = torch.tensor([], dtype=dtype).element_size()
     for b in sorted(set(int(x) for x in bucket_bytes)):
@@ -104,5 +128,5 @@ def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: s
                 % (b / 1e6, dtype, t_r * 1e3, t_i * 1e3, names[b]))
     if _agree(float(ipc.status()), group, device) != 0:   # a timing run tripped a barrier timeout somewhere
         ipc.close()
-        return RoutedComm(rccl)
-    return RoutedComm(rccl, routes, names)
+        return RoutedComm(rccl, group=group, device=device)
+    return RoutedComm(rccl, routes, names, group=group, device=device)

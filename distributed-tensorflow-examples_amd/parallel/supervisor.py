@@ -49,6 +49,7 @@ class Supervisor:
         self.exception = None
         self._last_gs = None
         self.saves = 0
+        self._ev_lock = threading.Lock()  # the step-counter thread and summary() share the writer
 
     # ---------------------------------------------------------------- setup
     def prepare(self):
@@ -104,7 +105,8 @@ class Supervisor:
             now = time.time()
             if last_gs is not None and now > last_t:
                 rate = (gs - last_gs) / (now - last_t)
-                self.events.add_scalars(gs, {"global_step/sec": rate})
+                with self._ev_lock:
+                    self.events.add_scalars(gs, {"global_step/sec": rate})
             last_t, last_gs = now, gs
 
     # ------------------------------------------------------------ control
@@ -115,8 +117,11 @@ class Supervisor:
         self._stop.set()
 
     def summary(self, step, scalars: dict):
-        if self.events is not None:
-            self.events.add_scalars(step, scalars)
+        """Append scalar summaries (losses, images/sec) to the chief's events file; a no-op on
+        non-chief tasks (TF: only the chief's Supervisor owns a summary writer)."""
+        if self.events is not None and scalars:
+            with self._ev_lock:
+                self.events.add_scalars(step, scalars)
 
     def stop(self):
         self._stop.set()
@@ -124,6 +129,8 @@ class Supervisor:
             t.join(timeout=60)
         self._threads.clear()
         if self.events is not None:
-            self.events.close()
+            with self._ev_lock:
+                self.events.close()
+            self.events = None
         if self.exception is not None:
             raise self.exception

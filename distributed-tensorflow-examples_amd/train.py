@@ -95,6 +95,16 @@ def step_line(step, local_step, ms, py2=False):
     return repr(parts) if py2 else " ".join(parts)
 
 
+def scalar_metrics(metrics) -> dict:
+    """Float scalars of a step's metrics (``loss``; GAN ``gen_loss`` / ``disc_loss``) as Python
+    floats - the loss values written to the events file and the --metrics_jsonl stream."""
+    out = {}
+    for k, v in (metrics or {}).items():
+        if torch.is_tensor(v) and v.numel() == 1 and v.is_floating_point():
+            out[k] = float(v.item())
+    return out
+
+
 def model_step_hook(model, step, metrics, log):
     if model.name == "gan" and (step % 1000 == 0 or step == 1):
         log("Step %i: Generator Loss: %f, Discriminator Loss: %f"
@@ -276,11 +286,13 @@ def run_worker_ps(flags, model, server, device, log):
                 log("pull checksum gs=%d: %.9e" % (step, float(prog.P.master.double().sum().item())))
             faults.step(step)
             elapsed = time.time() - t0
+            ips = prog.batch_size / max(elapsed, 1e-9)
+            sc = scalar_metrics(metrics)
             if local_step % flags.log_every == 0:
                 log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
+                sv.summary(step, dict(sc, **{"images/sec": ips}))
             model_step_hook(model, step, metrics, log)
-            metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000,
-                              images_per_sec=prog.batch_size / max(elapsed, 1e-9))
+            metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000, images_per_sec=ips, **sc)
             local_step += 1
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
         if model.name == "lstm":
@@ -378,19 +390,25 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
             step = int(gstep.item())
             faults.step(step)
             elapsed = time.time() - t0
+            ips = prog.batch_size * world / max(elapsed, 1e-9)
+            sc = scalar_metrics(state.get("m"))
             if local_step % flags.log_every == 0:
                 log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
                 if timer is not None:
                     log(PhaseTimer.format(timer.summary()))
+                sv.summary(step, dict(sc, **{"images/sec": ips}))
+                if ar is not None and ar.comm is not None:
+                    ar.comm.check_health()  # IPC barrier timeouts fail the job on every rank
             if "m" in state:
                 model_step_hook(model, step, state["m"], log)
-            metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000,
-                              images_per_sec=prog.batch_size * world / max(elapsed, 1e-9))
+            metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000, images_per_sec=ips, **sc)
             local_step += 1
+        if ar is not None and ar.comm is not None:
+            ar.comm.check_health()
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
         if world > 1 and flags.check_pull:  # synchronous replicas: identical parameters on every worker
             log("params checksum %.12e" % float(prog.P.master.double().sum().item()))
-        if model.name == "lstm" and is_chief:
+        if model.name == "lstm":  # every worker evaluates and prints, as LSTM:134-138
             test_len = 128
             acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
                                 torch.from_numpy(data.test.labels[:test_len]).to(device))
