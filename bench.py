@@ -349,7 +349,9 @@ def bench_resnet(args, d: Dist):
     runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
                                                 and graphs_enabled()), capture_error_mode="thread_local")
     elapsed, win = timed(runner, args.steps, args.warmup, d)
-    same = replicas_identical(prog.P.master, d) if d.world > 1 else None
+    # trainable variables only: BN moving statistics are per-replica (each rank's own batches)
+    train_vals = torch.cat([prog.P.view(n).reshape(-1) for n in names])
+    same = replicas_identical(train_vals, d) if d.world > 1 else None
     extra = {"optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None,
              "last_loss": round(float(prog.loss.item()) / B, 4), "replicas_identical": same,
              "distinct_gpus": d.distinct_devices()}

@@ -57,19 +57,23 @@ def main():
                       lambda: torch.mm(dz, w1), 2.0 * B * FC * K1),
         "fc1_wgrad": (lambda t, s: ops.gemm(dz, p2, gw, M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
                                             ldb=K1, ldc=K1, b_ones_row=K1, bias_out=gb, tile=t, splits=s,
-                                            atomic=s > 1),
+                                            atomic=s > 1 and t < 5),
                       lambda: torch.mm(dz.t(), p2), 2.0 * B * FC * K1),
     }
     for name, (fn, ref, fl) in shapes.items():
         tr = timeit(ref, a.iters)
         print(f"{name:10s} torch.mm {tr:8.1f} us {fl / tr / 1e6:7.1f} TFLOP/s", flush=True)
-        for tile in (0, 1, 2, 3):
+        for tile in (0, 2, 5, 6, 8, 10, 12):
             row = []
-            for s in (1, 2, 4, 8):
-                t = timeit(lambda: fn(tile, s), a.iters)
+            for s in (1, 2, 4):
+                try:
+                    t = timeit(lambda: fn(tile, s), a.iters)
+                except RuntimeError:
+                    row.append(f"s{s}:      n/a        ")
+                    continue
                 row.append(f"s{s}:{t:7.1f}us/{fl / t / 1e6:6.1f}TF")
             bm, bn = ops.TILE_DIMS[tile]
-            print(f"{name:10s} {bm:3d}x{bn:<3d} " + "  ".join(row), flush=True)
+            print(f"{name:10s} {bm:3d}x{bn:<3d}{'g' if tile >= 5 else ' '} " + "  ".join(row), flush=True)
 
 
 if __name__ == "__main__":

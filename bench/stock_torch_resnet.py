@@ -95,7 +95,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch_size", type=int, default=None)
     ap.add_argument("--write", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="capture the whole step (fwd, bwd, fused optimizer) in one "
+                    "CUDA/HIP graph (1 GPU); implies --fused")
+    ap.add_argument("--fused", action="store_true", help="torch.optim fused=True optimizer kernels")
     a = ap.parse_args()
+    a.fused = a.fused or a.graph
     B = a.batch_size or (256 if a.arch == "resnet20" else 64)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,11 +111,17 @@ def main():
     net, (C, H, W), ncls = resnet20() if a.arch == "resnet20" else resnet50()
     net = net.to(dev).to(memory_format=torch.channels_last)
     model = nn.parallel.DistributedDataParallel(net, device_ids=[lr_]) if world > 1 else net
-    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, fused=True) if a.fused \
+        else torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
     g = torch.Generator(device=dev).manual_seed(rank)
     n_pool = 4096 if a.arch == "resnet20" else 512
     data = torch.randint(0, 256, (n_pool, H, W, C), device=dev, dtype=torch.uint8, generator=g)
     labels = torch.randint(0, ncls, (n_pool,), device=dev, generator=g)
+
+    n_pool_, B_ = n_pool, B
+
+    def xform(idx):
+        return (data[idx].float() / 255).permute(0, 3, 1, 2)
 
     def step():
         idx = torch.randint(0, n_pool, (B,), device=dev, generator=g)
@@ -123,14 +133,39 @@ def main():
         opt.step()
         return loss
 
+    runner = step
+    if a.graph:
+        assert world == 1, "--graph is the 1-GPU stock row (DDP steps stay eager)"
+
+        def gstep():  # the captured step: backward ASSIGNS fresh grads (set to None before capture)
+            idx = torch.randint(0, n_pool_, (B_,), device=dev)
+            x = xform(idx)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(model(x), labels[idx])
+            loss.backward()
+            opt.step()
+            return loss
+
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                opt.zero_grad(set_to_none=True)
+                gstep()
+        torch.cuda.current_stream().wait_stream(s)
+        G = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(G):
+            gstep()
+        runner = G.replay
     for _ in range(a.warmup):
-        step()
+        runner()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step()
+        runner()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -142,11 +177,12 @@ def main():
     v = B * world * a.steps / el
     if rank == 0:
         print(json.dumps({"arch": a.arch, "stock_torch_images_per_sec": round(v, 1), "n_gpus": world,
-                          "batch_size": B, "ms_per_step": round(el / a.steps * 1000, 3)}), flush=True)
+                          "batch_size": B, "ms_per_step": round(el / a.steps * 1000, 3), "graph": a.graph,
+                          "fused_optimizer": a.fused}), flush=True)
         if a.write:
             p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stock_baseline.json")
             tab = json.load(open(p)) if os.path.exists(p) else {}
-            tab[f"{a.arch}_{world}x{B}"] = round(v, 1)
+            tab[f"{a.arch}_{world}x{B}" + ("_graph_fused" if a.graph else "_fused" if a.fused else "")] = round(v, 1)
             json.dump(tab, open(p, "w"), indent=1, sort_keys=True)
     if world > 1:
         dist.destroy_process_group()

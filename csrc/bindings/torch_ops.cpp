@@ -48,7 +48,7 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
           const optional<Tensor>& counter, const optional<Tensor>& pooled, const optional<Tensor>& argmax,
           int64_t PH, int64_t PW, int64_t PC, const optional<Tensor>& out2, int64_t ldc2, bool out2_trans,
           const optional<Tensor>& bias_out, const optional<Tensor>& ws, const optional<Tensor>& tile_ctr,
-          int64_t a_ones_row) {
+          int64_t a_ones_row, const optional<Tensor>& ones) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(out, "out");
@@ -100,6 +100,10 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   a.keep = (float)keep; a.seed = (uint64_t)seed; a.counter = ptr_or_null<int64_t>(counter);
   a.bias_out = ptr_or_null<float>(bias_out);
   TORCH_CHECK(!a.bias_out || b_ones_row >= 0 || a_ones_row >= 0, "gemm: bias_out needs a ones row");
+  a.ones = ptr_or_null<dtfe::bf16>(ones);
+  if (tile >= 5)
+    TORCH_CHECK(dtfe::gemm_glds_eligible(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, a),
+                "gemm: shape / layout not eligible for the global_load_lds tile ", tile);
   dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
 }
 
@@ -669,7 +673,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor? bias, int bias_axis, int act, float alpha, float beta, bool atomic, int splits, int tile,"
       " Tensor? aux, int ld_aux, int aux_act, int b_ones_row, float keep, int seed, Tensor? counter,"
       " Tensor? pooled, Tensor? argmax, int PH, int PW, int PC, Tensor(b!)? out2, int ldc2, bool out2_trans,"
-      " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr, int a_ones_row=-1) -> ()");
+      " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr, int a_ones_row=-1, Tensor? ones=None) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");

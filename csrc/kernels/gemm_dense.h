@@ -35,6 +35,9 @@ struct DenseGemmArgs {
   // tile to ws[split][tile]; the last split to arrive (tile_ctr) sums them in
   // fixed split order (deterministic), resets the counter and runs the epilogue
   float* ws; int* tile_ctr;
+  // global_load_lds kernel (tiles 5..8): a 1 KB page of bf16 ones, read by the whole n-tile that
+  // starts at b_ones_row (the bias column of a weight-gradient GEMM sits past the operand's rows)
+  const bf16* ones;
 };
 
 // Epilogue of one output element (row < M, col < N); returns false when the
@@ -82,29 +85,16 @@ __device__ __forceinline__ bool dense_epi(const DenseGemmArgs& a, int row, int c
   return true;
 }
 
-template <typename T, typename Cfg, int AMODE, int BMODE>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs a) {
-  using LA = DenseLoader<T, Cfg::BM, AMODE, Cfg::BK>;
-  using LB = DenseLoader<T, Cfg::BN, BMODE, Cfg::BK>;
+// Everything after the k-loop: accumulators -> f32 C tile in LDS (the operand buffers are dead,
+// the caller has passed a barrier), optional deterministic split-K combine (last arriver), then
+// the fused epilogue walking 8-column chunks (coalesced 16-32 B stores).  Shared by the
+// register-staged kernel below and the global_load_lds kernel of gemm_glds.h.
+template <typename Cfg>
+__device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* smem_raw, f32x4_t (&acc)[Cfg::TM][Cfg::TN],
+                                               int tm, int tn, int tiles_m, int tiles_n) {
   constexpr int CLD = Cfg::BN + 4;  // f32 C tile row stride: 16*(odd) bytes, conflict-free quad writes
-  constexpr int SMEM_BYTES = SmemSize<T, Cfg, LA, LB>::BYTES > Cfg::BM * CLD * 4 ? SmemSize<T, Cfg, LA, LB>::BYTES
-                                                                                   : Cfg::BM * CLD * 4;
-  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM_BYTES];
-  T* smem = reinterpret_cast<T*>(smem_raw);
   float* Cs = reinterpret_cast<float*>(smem_raw);
-  const int tiles_m = (a.M + Cfg::BM - 1) / Cfg::BM, tiles_n = (a.N + Cfg::BN - 1) / Cfg::BN;
-  int tm, tn;
-  tile_coords(tiles_m, tiles_n, tm, tn);
   const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
-  const int k_begin = blockIdx.z * a.k_chunk;
-  const int k_end = min(a.K, k_begin + a.k_chunk);
-  LA la((const T*)a.A, a.lda, a.M, a.K, m_base, a.a_ones_row);
-  LB lb((const T*)a.B, a.ldb, a.N, a.K, n_base, a.b_ones_row);
-  f32x4_t acc[Cfg::TM][Cfg::TN];
-  gemm_mainloop<T, Cfg, AMODE, BMODE>(la, lb, k_begin, k_end, smem, acc);  // ends with a barrier
-
-  // accumulators -> f32 C tile in LDS (the operand buffers are dead), so the
-  // epilogue walks 8-column chunks: coalesced 16-32 B stores, no register-array indexing
   {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid / Cfg::WARPS_N, wn = wid % Cfg::WARPS_N;
@@ -234,11 +224,39 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
   }
 }
 
+template <typename Cfg> struct DenseCBytes { static constexpr int VALUE = Cfg::BM * (Cfg::BN + 4) * 4; };
+
+template <typename T, typename Cfg, int AMODE, int BMODE>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs a) {
+  using LA = DenseLoader<T, Cfg::BM, AMODE, Cfg::BK>;
+  using LB = DenseLoader<T, Cfg::BN, BMODE, Cfg::BK>;
+  constexpr int SMEM_BYTES = SmemSize<T, Cfg, LA, LB>::BYTES > DenseCBytes<Cfg>::VALUE ? SmemSize<T, Cfg, LA, LB>::BYTES
+                                                                                      : DenseCBytes<Cfg>::VALUE;
+  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM_BYTES];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+  const int tiles_m = (a.M + Cfg::BM - 1) / Cfg::BM, tiles_n = (a.N + Cfg::BN - 1) / Cfg::BN;
+  int tm, tn;
+  tile_coords(tiles_m, tiles_n, tm, tn);
+  const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
+  const int k_begin = blockIdx.z * a.k_chunk;
+  const int k_end = min(a.K, k_begin + a.k_chunk);
+  LA la((const T*)a.A, a.lda, a.M, a.K, m_base, a.a_ones_row);
+  LB lb((const T*)a.B, a.ldb, a.N, a.K, n_base, a.b_ones_row);
+  f32x4_t acc[Cfg::TM][Cfg::TN];
+  gemm_mainloop<T, Cfg, AMODE, BMODE>(la, lb, k_begin, k_end, smem, acc);  // ends with a barrier
+  dense_epilogue<Cfg>(a, smem_raw, acc, tm, tn, tiles_m, tiles_n);
+}
+
 // host-side launcher (defined in gemm_dense.hip)
 // dtype: 0 = bf16, 1 = f32.  tile: 0 = 64x64, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 32x32
+// (register-staged engine of gemm_core.h); 5 = 128x128, 6 = 128x64, 7 = 64x128, 8 = 64x64 with
+// direct global->LDS staging, 3 stages (gemm_glds.h: bf16, K % 64 == 0, whole tiles - see
+// gemm_glds_eligible); 9..12 the same tiles with 2 stages
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream);
 // block tile of a tile id; returns the k-tile depth (split-K chunks are multiples of it)
 int gemm_dense_tile_dims(int tile, int& bm, int& bn);
+// whether the global_load_lds kernel family can run this GEMM with tile `tile` (5..8)
+bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGemmArgs& a);
 
 }  // namespace dtfe

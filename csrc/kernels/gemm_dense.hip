@@ -1,5 +1,7 @@
 // Instantiation + dispatch of the dense GEMM kernel family.
 #include "gemm_dense.h"
+#include "gemm_glds.h"
+
 #include <stdexcept>
 
 namespace dtfe {
@@ -15,11 +17,53 @@ static void launch_one(int splits, const DenseGemmArgs& args, hipStream_t s) {
 }
 
 int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
-  static const int dims[5][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32}};
-  if (tile < 0 || tile > 4) return -1;
+  static const int dims[13][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
+                                  {128, 128}, {128, 64}, {64, 128}, {64, 64},
+                                  {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  if (tile < 0 || tile > 12) return -1;
   bm = dims[tile][0];
   bn = dims[tile][1];
-  return GEMM_KTILE;
+  return tile >= 5 ? GL_BK : GEMM_KTILE;
+}
+
+bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGemmArgs& a) {
+  int bm = 0, bn = 0;
+  if (tile < 5 || gemm_dense_tile_dims(tile, bm, bn) < 0) return false;
+  if (dtype != 0 || a.a_ones_row >= 0 || a.K % GL_BK || a.k_chunk % GL_BK || a.M % bm) return false;
+  if ((a.lda % 8) || (a.ldb % 8) || (((uintptr_t)a.A) & 15) || (((uintptr_t)a.B) & 15)) return false;
+  // n-tiles: whole tiles of real rows, plus at most one trailing tile that starts at the ones row
+  if (a.b_ones_row >= 0) {
+    if (a.b_ones_row != a.N - 1 || a.b_ones_row % bn || !a.ones || (((uintptr_t)a.ones) & 15)) return false;
+  } else if (a.N % bn) {
+    return false;
+  }
+  (void)amode;
+  (void)bmode;
+  return true;
+}
+
+// tiles 5..8: 3 k-tiles in flight (one workgroup per CU streams deeper);
+// tiles 9..12: 2 stages, half the LDS, so more workgroups share a CU (grids of many tiles)
+template <int BM, int BN, int AM, int BMD, int STAGES>
+static void launch_glds(int splits, const DenseGemmArgs& a, hipStream_t s) {
+  const int tiles = (a.M / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, 1, splits);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, AM, BMD, STAGES>), grid, dim3(GEMM_THREADS), 0, s, a);
+}
+
+template <int AM, int BMD>
+static void glds_by_tile(int tile, int splits, const DenseGemmArgs& a, hipStream_t s) {
+  switch (tile) {
+    case 5: launch_glds<128, 128, AM, BMD, 3>(splits, a, s); break;
+    case 6: launch_glds<128, 64, AM, BMD, 3>(splits, a, s); break;
+    case 7: launch_glds<64, 128, AM, BMD, 3>(splits, a, s); break;
+    case 8: launch_glds<64, 64, AM, BMD, 3>(splits, a, s); break;
+    case 9: launch_glds<128, 128, AM, BMD, 2>(splits, a, s); break;
+    case 10: launch_glds<128, 64, AM, BMD, 2>(splits, a, s); break;
+    case 11: launch_glds<64, 128, AM, BMD, 2>(splits, a, s); break;
+    case 12: launch_glds<64, 64, AM, BMD, 2>(splits, a, s); break;
+    default: throw std::runtime_error("gemm_dense: bad glds tile id");
+  }
 }
 
 template <typename T, int AM, int BMD>
@@ -45,6 +89,17 @@ static void by_mode(int am, int bm, int tile, int splits, const DenseGemmArgs& a
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream) {
   if (splits < 1) splits = 1;
+  if (tile >= 5) {
+    if (!gemm_glds_eligible(dtype, amode, bmode, tile, args))
+      throw std::runtime_error("gemm_dense: this GEMM is not eligible for the global_load_lds tiles");
+    if (splits > 1 && !args.atomic && (!args.ws || !args.tile_ctr))
+      throw std::runtime_error("gemm_dense: split-K with a fused epilogue needs a workspace");
+    if (amode == KMAJ && bmode == KMAJ) glds_by_tile<KMAJ, KMAJ>(tile, splits, args, stream);
+    else if (amode == KMAJ && bmode == RMAJ) glds_by_tile<KMAJ, RMAJ>(tile, splits, args, stream);
+    else if (amode == RMAJ && bmode == KMAJ) glds_by_tile<RMAJ, KMAJ>(tile, splits, args, stream);
+    else glds_by_tile<RMAJ, RMAJ>(tile, splits, args, stream);
+    return;
+  }
   if (dtype == 0) by_mode<bf16>(amode, bmode, tile, splits, args, stream);
   else by_mode<float>(amode, bmode, tile, splits, args, stream);
 }

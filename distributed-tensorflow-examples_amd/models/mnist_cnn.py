@@ -218,10 +218,23 @@ class MnistCnnTrainer:
         self._apply = None
         self.early_apply = os.environ.get("DTFE_CNN_EARLY_APPLY", "0") != "0"
         self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
+        # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
+        # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
+        # 2-stage variant (784 / 800 tiles, several workgroups per CU)
+        self.glds = self.device.type == "cuda" and os.environ.get("DTFE_CNN_GLDS", "1") != "0"
+        K1 = 7 * 7 * C2
+        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 8)
+        self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
+        self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
             self.ws_c2 = torch.empty(256 * (C2 * KS * KS * C1 + C2), device=d, dtype=torch.float32)
+
+    def _glds_tile(self, A, Bm, M, N, K, lda, ldb, tile, b_ones_row=-1):
+        if self.glds and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row):
+            return tile
+        return None
 
     # ------------------------------------------------------------------
     def forward_backward(self):
@@ -244,7 +257,7 @@ class MnistCnnTrainer:
                     pool=True, **self.ic2)
         K1 = 7 * 7 * C2
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
-                 keep=self.keep, seed=self.seed + 2, counter=self.data_ctr)
+                 keep=self.keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd)
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
         main = torch.cuda.current_stream(self.device) if self.par else None
@@ -258,12 +271,12 @@ class MnistCnnTrainer:
                      splits=max(1, min(16, B // 128)), tile=4)
             # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
-                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
+                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
             if self.allreduce is not None:  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
                 self.allreduce.launch(0)
         # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
-                 aux_act=ops.ACT_RELU)
+                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
         if self._apply is not None and self._apply[0] == "early":
             # fc/head Adam as soon as their (reduced) gradients are final - and after fc1 dgrad, the
             # last reader of the fc1 weights this step (the branch re-joins main's progress here)
@@ -309,13 +322,13 @@ class MnistCnnTrainer:
         gradients that feed nothing but the optimizer run on one side stream."""
         B, K1 = self.B, 7 * 7 * C2
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
-                 aux_act=ops.ACT_RELU)
+                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
         with self._branch(self.s_fc, main):
             ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
                      bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
                      splits=max(1, min(16, B // 128)), tile=4)
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
-                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
+                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
             if self.allreduce is not None:
                 self.allreduce.launch(0)
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,

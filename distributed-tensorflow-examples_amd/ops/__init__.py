@@ -22,12 +22,39 @@ __all__ = [
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
-    "TILE_DIMS", "GEMM_KTILE", "bn_stats", "bn_apply", "bn_bwd_stats", "bn_bwd_apply", "shortcut_grad_add",
+    "TILE_DIMS", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
+    "bn_bwd_apply", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
-TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)}
+TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32),
+             # global_load_lds kernel family (csrc/kernels/gemm_glds.h): bf16, K % 64 == 0, whole tiles
+             5: (128, 128), 6: (128, 64), 7: (64, 128), 8: (64, 64),      # 3 k-tiles in flight
+             9: (128, 128), 10: (128, 64), 11: (64, 128), 12: (64, 64)}   # 2 stages (more WGs per CU)
+GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12)
+_ONES = {}
+
+
+def ones_page(device):
+    """1 KB of bf16 ones (the bias column of a glds weight-gradient GEMM reads it)."""
+    key = torch.device(device)
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones(512, dtype=torch.bfloat16, device=key)
+    return t
+
+
+def glds_ok(A, B, M, N, K, tile, lda, ldb, b_ones_row=-1, a_ones_row=-1):
+    """Host mirror of gemm_glds_eligible: can the global_load_lds tile `tile` run this GEMM?"""
+    bm, bn = TILE_DIMS[tile]
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16 or a_ones_row >= 0 or K % 64 or M % bm:
+        return False
+    if lda % 8 or ldb % 8 or A.data_ptr() % 16 or B.data_ptr() % 16:
+        return False
+    if b_ones_row >= 0:
+        return b_ones_row == N - 1 and b_ones_row % bn == 0
+    return N % bn == 0
 GEMM_KTILE = 64  # k-tile depth of the dense GEMM kernels (split-K chunks are multiples of it)
 _WS = {}
 
@@ -150,7 +177,8 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
             ws, ctr = workspace if workspace is not None else split_workspace(out.device, splits, M, N, tile)
         require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
                        splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
-                       PC, out2, ldc2, out2_trans, bias_out, ws, ctr, a_ones_row)
+                       PC, out2, ldc2, out2_trans, bias_out, ws, ctr, a_ones_row,
+                       ones_page(out.device) if tile in GLDS_TILES else None)
         return out
     # CPU reference
     if a_ones_row >= 0:

@@ -153,3 +153,86 @@ def test_cnn_early_fc_apply_matches_sequential(monkeypatch):
         out[early] = (tr.P.master.clone(), int(tr.global_step.item()))
     assert out["1"][1] == out["0"][1] == 4
     assert torch.allclose(out["1"][0], out["0"][0], rtol=1e-4, atol=1e-6)
+
+
+def _reference_grads_on(trainer, device):
+    """_reference_grads with the fp32 oracle on ``device`` (the bench-sized batches)."""
+    P, n = trainer.P, trainer.names
+    x = trainer.x.float().permute(0, 3, 1, 2).to(device)
+    y = trainer.labels.long().to(device)
+
+    def w(k):
+        return P.view(n[k]).detach().to(device).to(torch.bfloat16).float().requires_grad_(True)
+
+    def b(k):
+        return P.view(n[k]).detach().to(device).float().requires_grad_(True)
+
+    wc1, wc2, wd1, wo = w("wc1"), w("wc2"), w("wd1"), w("out")
+    bc1, bc2, bd1, bo = b("bc1"), b("bc2"), b("bd1"), b("bout")
+    with torch.backends.cudnn.flags(enabled=True, allow_tf32=False):
+        z = F.conv2d(x, wc1.permute(0, 3, 1, 2), bc1, padding=2)
+        z = q(F.max_pool2d(F.relu(z), 2))
+        z = F.conv2d(z, wc2.permute(0, 3, 1, 2), bc2, padding=2)
+        z = q(F.max_pool2d(F.relu(z), 2))
+        z = z.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+        h = F.relu(q(z @ wd1.t() + bd1))
+        logits = h @ wo.t() + bo
+        loss = F.cross_entropy(logits, y)
+        loss.backward()
+    return loss.item(), {"wc1": wc1.grad, "wc2": wc2.grad, "wd1": wd1.grad, "out": wo.grad,
+                         "bc1": bc1.grad, "bc2": bc2.grad, "bd1": bd1.grad, "bout": bo.grad}
+
+
+@pytest.mark.parametrize("B", [512, 1024])
+def test_cnn_bench_shaped_step_matches_autograd(B):
+    """The headline configuration itself (bench.py: B=1024 per GPU, fused gather+conv1 launch,
+    split-K head wgrad with splits=8, conv2 blocks=128 on the side branch), dropout off, against
+    fp32 autograd of the same bf16-rounded network."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    tr = MnistCnnTrainer(B, "cuda", keep_prob=1.0, seed=11)
+    assert tr.fused_gather and tr.br_c2 and tr.br_fc
+    tr.P.grad.fill_(3.0)               # stale values: every gradient must be overwritten / cleared
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    loss_ref, grads = _reference_grads_on(tr, "cuda")
+    loss = tr.loss_sum.item() / tr.B
+    assert abs(loss - loss_ref) < 2e-2 * max(1.0, abs(loss_ref)), (loss, loss_ref)
+    errs = {k: ((tr.gw[k].detach().float() - g).norm() / (g.norm() + 1e-12)).item() for k, g in grads.items()}
+    assert all(e < 3e-2 for e in errs.values()), sorted(errs.items(), key=lambda kv: -kv[1])
+
+
+def test_cnn_adam_step_matches_torch_adam_tf1_form():
+    """One fused apply_gradients launch over all 3.27 M parameters (master, Adam slots, bf16 and
+    transposed bf16 copies) against torch.optim.Adam on the same gradients.  TF1 Adam
+    (lr_t = lr*sqrt(1-b2^t)/(1-b1^t), v -= lr_t*m/(sqrt(v)+eps)) is torch's Adam with
+    eps_torch = eps / sqrt(1 - b2^t)."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    tr = MnistCnnTrainer(1024, "cuda", keep_prob=0.75, seed=13)
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    p0 = tr.P.master.detach().clone()
+    g = tr.P.grad.detach().clone()
+    tr.opt.step(gscale=1.0)
+    torch.cuda.synchronize()
+    ref = p0.clone().requires_grad_(True)
+    ref.grad = g.clone()
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    opt = torch.optim.Adam([ref], lr=1e-3, betas=(b1, b2), eps=eps / (1 - b2) ** 0.5)
+    opt.step()
+    got = tr.P.master.detach()
+    mask = g != 0   # padding between variables stays untouched
+    err = (got - ref.detach())[mask].abs().max().item()
+    assert err < 2e-6, err
+    assert torch.equal(got[~mask], p0[~mask])
+    # beta powers and global step advanced once
+    assert torch.allclose(tr.opt.beta_pow.cpu(), torch.tensor([b1 * b1, b2 * b2]))
+    assert int(tr.global_step.item()) == 1
+    # bf16 working copies written by the same launch
+    P, n = tr.P, tr.names
+    for k in ("wc1", "wc2", "wd1", "out"):
+        assert torch.equal(P.w16[n[k]], P.view(n[k]).to(torch.bfloat16)), k
+    R, T, C = P.spec(n["wc2"]).transpose
+    wt = P.view(n["wc2"]).reshape(R, T, C).permute(2, 1, 0).reshape(-1).to(torch.bfloat16)
+    assert torch.equal(P.wt16[n["wc2"]], wt)
