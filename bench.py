@@ -63,6 +63,7 @@ def parse_args(argv=None):
                     help="auto: per bucket size the faster of dtfe's RCCL communicator and the hipIpc two-shot "
                          "kernel (timed at setup); rccl / ipc: force one; all three run on a side stream with the "
                          "whole step captured in one hipGraph.  pg: torch.distributed ProcessGroupNCCL, eager steps")
+    ap.add_argument("--hogwild", action="store_true", help="--mode ps: lock-free concurrent applies")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
     return ap.parse_args(argv)
@@ -192,18 +193,26 @@ def timed(runner, steps: int, warmup: int, d: Dist):
 
 
 def _baseline(n_gpus, batch, model="mnist_cnn"):
-    """Faster of the stock-PyTorch rows (eager DDP, and graph-captured + fused Adam/SGD) measured on
-    the same MI355X box and config by bench/stock_torch_cnn.py / stock_torch_resnet.py; BASELINE.md."""
+    """Faster of the stock-PyTorch rows (eager DDP; graph-captured + fused Adam/SGD) measured on
+    the same MI355X and config by bench/stock_torch_cnn.py / stock_torch_resnet.py.
+    Without a measured N-GPU stock row the bar is N x the best 1-GPU stock row (stock with ideal
+    scaling - never easier than the real stock DDP curve)."""
     p = os.path.join(ROOT, "bench", "stock_baseline.json")
     try:
         with open(p) as f:
             tab = json.load(f)
     except (OSError, ValueError):
         return None
-    key = f"{n_gpus}x{batch}" if model == "mnist_cnn" else f"{model}_{n_gpus}x{batch}"
-    vals = [v for k, v in tab.items() if k == key or k.startswith(key + "_")]
-    vals = [v for v in vals if isinstance(v, (int, float))]
-    return max(vals) if vals else None
+
+    def best(n):
+        key = f"{n}x{batch}" if model == "mnist_cnn" else f"{model}_{n}x{batch}"
+        vals = [v for k, v in tab.items() if (k == key or k.startswith(key + "_")) and isinstance(v, (int, float))]
+        return max(vals) if vals else None
+
+    b = best(n_gpus)
+    if b is None and n_gpus > 1 and best(1) is not None:
+        b = n_gpus * best(1)
+    return b
 
 
 def _make_comm(args, d: Dist, bucket_bytes):
@@ -364,13 +373,131 @@ def bench_resnet(args, d: Dist):
         comm.close()
 
 
+def bench_ps(args):
+    """BASELINE.json config 4: MNIST CNN async parameter-server SGD, 1 ps + N workers on one node.
+
+    Rank 0 is the ps task (its shard of every variable + the TF1 Adam slots on GPU 0, served by
+    the native C++ progress thread of ``parallel/ps_native.py``); ranks 1..N are workers on GPUs
+    0..N-1.  A worker step = HBM batch sampling fused into conv1, forward, backward with the
+    gradient buckets pushed into the ps's hipIpc mailboxes on a side stream while backward
+    continues (bf16 over xGMI), a device-side request / wait for the ps's apply, and the pull of
+    the fresh bf16 working copies - one hipGraph replay, no host round trip.  Every push is
+    applied (async: one at a time in arrival order; --hogwild: concurrently).  Timed: K steps
+    per worker between worker barriers + device syncs, MAX over workers; images/sec counts
+    every worker's images.  Reference: gan/distributed_gan.py:119-121,193 (push/pull per
+    sess.run), :195-196 (its per-step timing print)."""
+    import dtfe  # noqa: F401
+    from dtfe.models.mnist_cnn import MnistCnnModel, MnistCnnTrainer, num_params
+    from dtfe.parallel import ps_native
+    from dtfe.parallel.cluster import ClusterSpec, Server
+    from dtfe.parallel.ps import PSClient, PSServer, Shard, wait_for_init
+    from dtfe.train import _shard_layout
+    from dtfe.utils.graphs import StepGraph, graphs_enabled
+
+    N = args.gpus or 1
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    if world != N + 1:
+        raise SystemExit("bench.py --mode ps: expected %d processes (1 ps + %d workers), got %d" % (N + 1, N, world))
+    ndev = max(1, torch.cuda.device_count())
+    port = int(os.environ["MASTER_PORT"])
+    cluster = ClusterSpec(["127.0.0.1:%d" % port], ["127.0.0.1:%d" % (port + 1 + i) for i in range(N)])
+    job, idx = cluster.task_of(rank)
+    gpu = 0 if job == "ps" else idx % ndev
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    server = Server(cluster, job, idx, backend="nccl", device=dev)
+    model = MnistCnnModel()
+    placement, shard_specs = _shard_layout(model, 1)
+    B = args.batch_size or MODEL_BATCH["mnist_cnn"]
+    if job == "ps":
+        shard = Shard(shard_specs[0], model.opt_groups, dev, True, model.gs_increments)
+        ps = PSServer(server, shard, num_workers=N, comm_device="cpu", log=lambda *_: None)
+        ps.native = ps_native.NativeShardService(server, shard, N, hogwild=args.hogwild)
+        ps.serve_forever()
+        st = ps.native.stats()
+        ps.native.stop()
+        server.store.set("dtfe/bench/ps_stats", json.dumps(dict(st, global_step=shard.global_step())))
+        print("ps: %s" % json.dumps(st), file=sys.stderr, flush=True)
+        server.shutdown()
+        sys.stdout.flush()
+        os._exit(0)
+
+    def wsum(x: float, op=dist.ReduceOp.SUM) -> float:
+        t = torch.tensor([x], dtype=torch.float64)  # CPU tensor: the gloo half of the worker group
+        dist.all_reduce(t, op=op, group=server.worker_group)
+        return float(t.item())
+
+    tr = MnistCnnTrainer(B, dev, seed=0, rank=idx)
+    client = PSClient(server, tr.P, placement, shard_specs, cluster.rank_of("ps", 0), model.opt_groups,
+                      comm_device="cpu")
+    if idx == 0:
+        client.init_variables()   # the chief's global_variables_initializer
+    else:
+        wait_for_init(client, poll_s=0.05)
+    link = ps_native.NativePSLink(server, tr.P, placement, shard_specs, placement[model.gs_name], dev,
+                                  buckets=tr.buckets)
+    tr.allreduce = link           # bucket pushes fork off backward (MnistCnnTrainer.forward_backward)
+    link.pull()
+
+    def step():
+        tr.forward_backward()
+        link.end_step()
+
+    runner = StepGraph(step, warmup=2, enabled=not args.no_graph and graphs_enabled(),
+                       capture_error_mode="thread_local")
+
+    def run1():
+        runner()
+        link.note_request()
+
+    class _D:  # the timed() bracket over the workers only (the ps is serving)
+        world = N
+
+        @staticmethod
+        def barrier():
+            wsum(0.0)
+
+        @staticmethod
+        def max(x):
+            return wsum(x, dist.ReduceOp.MAX)
+
+    elapsed, win = timed(run1, args.steps, args.warmup, _D)
+    gs = link.host_reply()
+    link.check()
+    loss = float(tr.loss_sum.item()) / B
+    link.close()
+    client.done()
+    stats = json.loads(server.store.get("dtfe/bench/ps_stats").decode()) if idx == 0 else None
+    if idx == 0:
+        pushes = N * (args.steps + args.warmup)  # every runner() call is exactly one step (one push)
+        rec_extra = {"optimizer": "adam (TF1), applied on the ps", "hip_graph": runner.graph is not None,
+                     "last_loss": round(loss, 4), "global_step": gs, "ps_applies": stats.get("applies"),
+                     "ps_global_step": stats.get("global_step"),
+                     "pushes_issued": pushes, "transport": "hipIpc mailboxes + C++ ps service (bf16 push, bf16 pull)",
+                     "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": 0}
+
+        class _R:
+            rank = 0
+            world = N
+        args_ps = argparse.Namespace(**vars(args))
+        args_ps.model = "mnist_cnn_ps"
+        _emit(_R, args_ps, "images/sec (whole node), MNIST CNN async parameter server (1 ps + %d workers)" % N,
+              B * N * args.steps / elapsed, elapsed, win,
+              "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(), B,
+              dict(rec_extra, parallelism="ps1+w%d" % N),
+              "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)")
+    sys.stdout.flush()
+    os._exit(0)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
     if args.mode == "ps":
-        from bench_ps import main as ps_main  # noqa: E402  (bench/ps harness; launches its own ranks)
-
-        return ps_main(args)
+        if os.environ.get("DTFE_BENCH_CHILD") != "1":
+            # 1 ps + N workers = N + 1 processes on N GPUs (the ps shares GPU 0 with worker 0)
+            return launch_ranks((args.gpus or 1) + 1, argv)
+        return bench_ps(args)
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         return launch_ranks(args.gpus, argv)
     d = Dist(args)

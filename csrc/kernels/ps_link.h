@@ -1,0 +1,75 @@
+// Parameter-server data plane over hipIpc-mapped device memory.
+//
+// Every (ps shard, worker) pair owns a gradient mailbox and a parameter reply buffer in the
+// ps GPU's memory (uncached, exported with hipIpcGetMemHandle, mapped by the worker); a push
+// is the worker's GPU writing its gradients straight into the mailbox over xGMI (or locally
+// when the worker shares the ps's GPU), a pull is its GPU reading the reply buffer.  The
+// request / reply handshake lives in a small shared-memory page mapped into both processes and
+// registered for device access: the worker's GPU publishes "request s" with a system-scope
+// release store after its push, the ps's native service thread polls the page, enqueues the
+// fused apply and the reply snapshot on its own stream and a reply store; the worker's GPU waits
+// for the reply in a bounded spin kernel, then pulls.  No host round trip on the worker side,
+// so the whole worker step (compute, push, request, wait, pull) replays as one hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace dtfe {
+
+// One copy segment (element counts; pointers may be local or peer-mapped device memory).
+// mode: 0 f32->f32, 1 f32->bf16, 2 bf16->bf16, 3 bf16->f32, 4 f32 += f32, 5 f32 += bf16
+struct PsSeg {
+  const void* src;
+  void* dst;
+  long n;
+  int mode;
+  int pad;
+};
+struct PsWork {
+  int seg;
+  int pad;
+  long start, count;
+};
+
+constexpr int PS_MAX_WORKERS = 64;
+constexpr int PS_SLOT_WORDS = 16;  // 128 B per worker slot (own cache lines)
+
+// shared page layout (uint64 words): [worker w][PS_SLOT_WORDS] of
+enum PsWord : int {
+  PS_REQ_SEQ = 0,   // written last by the worker's GPU (request number, 1, 2, ...)
+  PS_REQ_KIND = 1,  // 1 = push (apply the mailbox), 2 = pull only
+  PS_REQ_TAG = 2,   // sync mode: shard version the gradient was computed from
+  PS_REP_SEQ = 8,   // written last by the ps's GPU: the request number answered
+  PS_REP_GS = 9,    // global step after the apply (the gs shard; -1 elsewhere)
+  PS_REP_VER = 10,  // shard version after the apply
+  PS_REP_STALE = 11 // 1 when a sync-mode gradient was dropped as stale
+};
+enum PsKind : int { PS_PUSH = 1, PS_PULL = 2 };
+
+// the copy plan: nwork items over the segments (one launch)
+void launch_ps_copy(const PsSeg* segs, const PsWork* work, int nwork, hipStream_t s);
+
+// worker GPU: ctr += 1; slot[KIND] = kind; slot[TAG] = *ver; slot[REQ_SEQ] = ctr (release)
+void launch_ps_request(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, hipStream_t s);
+
+// worker GPU: spin (bounded by timeout_ticks of the 100 MHz wall clock) until every slot's
+// REP_SEQ >= *ctr; then gs_out = slot[gs_slot][REP_GS], ver_out = slot[0][REP_VER].  On a
+// timeout *err = 1 and the kernel returns.
+constexpr int PS_MAX_SHARDS = 8;
+struct PsWaitArgs {
+  uint64_t* slot[PS_MAX_SHARDS];  // this worker's slot in every ps shard's shared page
+  int nslots, gs_slot;
+  const int64_t* ctr;
+  int32_t* gs_out;
+  int64_t* ver_out;
+  int* err;
+  unsigned long long timeout_ticks;
+};
+void launch_ps_wait(const PsWaitArgs& a, hipStream_t s);
+
+// ps GPU: slot[REP_GS] = gs ? *gs : -1; slot[REP_VER] = ver; slot[REP_STALE] = stale; slot[REP_SEQ] = seq
+void launch_ps_reply(uint64_t* slot, const int32_t* gs, uint64_t seq, uint64_t ver, int stale, hipStream_t s);
+
+}  // namespace dtfe

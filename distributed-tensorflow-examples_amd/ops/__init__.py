@@ -57,6 +57,9 @@ def glds_ok(A, B, M, N, K, tile, lda, ldb, b_ones_row=-1, a_ones_row=-1):
     return N % bn == 0
 GEMM_KTILE = 64  # k-tile depth of the dense GEMM kernels (split-K chunks are multiples of it)
 _WS = {}
+# Every workspace ever handed out stays alive: a hipGraph captured with an older (smaller)
+# buffer keeps its device pointers, and the caching allocator must never recycle that memory.
+_WS_RETIRED = []
 
 
 def split_workspace(device, splits, M, N, tile):
@@ -70,6 +73,8 @@ def split_workspace(device, splits, M, N, tile):
     key = torch.device(device)
     ws, ctr = _WS.get(key, (None, None))
     if ws is None or ws.numel() < need or ctr.numel() < ntiles:
+        if ws is not None:
+            _WS_RETIRED.append((ws, ctr))
         ws = torch.empty(max(need, 0 if ws is None else ws.numel()), device=key, dtype=torch.float32)
         ctr = torch.zeros(max(ntiles, 0 if ctr is None else ctr.numel()), device=key, dtype=torch.int32)
         _WS[key] = (ws, ctr)
@@ -355,6 +360,8 @@ def wgrad_workspace(device, numel):
     key = torch.device(device)
     ws = _WG_WS.get(key)
     if ws is None or ws.numel() < numel:
+        if ws is not None:
+            _WS_RETIRED.append((ws,))  # may be referenced by a captured graph
         ws = torch.empty(numel, device=key, dtype=torch.float32)
         _WG_WS[key] = ws
     return ws

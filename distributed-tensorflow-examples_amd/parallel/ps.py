@@ -64,9 +64,12 @@ class Shard:
         return self.P.total
 
     def apply(self, grad: torch.Tensor, scale: float = 1.0):
-        self.P.grad.copy_(grad)
+        """Apply one gradient payload (this shard's flat layout).  The payload goes to the
+        optimizer kernels directly - never staged in a shared buffer - so concurrent (hogwild)
+        applies race only on the variables and slots, as TF's use_locking=False does, and every
+        pushed gradient is applied exactly once."""
         for o in self.opts:
-            o.step(gscale=scale, gs_inc=0)
+            o.step(grad=grad, gscale=scale, gs_inc=0)
         if self.gs is not None:
             self.gs += self.gs_increments
         self.version += 1
@@ -149,6 +152,26 @@ class PSServer:
         self.faults = faults          # utils.faults.FaultInjector of this ps task
         self.done_ranks = set()
         self.lost = set()
+        self.native = None            # ps_native.NativeShardService when PUSH/PULL use the native plane
+
+    def _guard(self):
+        """Exclusive access to the shard for a control handler (the native service pauses)."""
+        if self.native is None:
+            return self.shard.lock
+        nat, lock = self.native, self.shard.lock
+
+        class _G:
+            def __enter__(self_):
+                lock.acquire()
+                self_.cm = nat.paused()
+                self_.cm.__enter__()
+
+            def __exit__(self_, *exc):
+                try:
+                    self_.cm.__exit__(*exc)
+                finally:
+                    lock.release()
+        return _G()
 
     # ---- per-worker service thread
     def _serve(self, worker_rank: int):
@@ -168,6 +191,7 @@ class PSServer:
                         self.done_ranks.add(worker_rank)
                         self.log("ps %d received done %d" % (self.server.task_index, i))
                         self._done_cv.notify_all()
+                    self._membership_changed()
                     return
                 if typ == STATUS:
                     self._reply_hdr(worker_rank, g)
@@ -176,7 +200,7 @@ class PSServer:
                     # global_variables_initializer: params from the chief, slots / beta powers /
                     # global_step back to their initial values
                     dist.recv(pay, src=worker_rank, group=g)
-                    with sh.lock:
+                    with self._guard():
                         sh.P.master.copy_(pay.to(sh.device))
                         sh.P.refresh_copies()
                         sh.reset_optimizer_state()
@@ -188,7 +212,7 @@ class PSServer:
                     gsv = torch.zeros(1, dtype=torch.int64)
                     dist.recv(st, src=worker_rank, group=g)
                     dist.recv(gsv, src=worker_rank, group=g)
-                    with sh.lock:
+                    with self._guard():
                         sh.load_state_payload(st.to(sh.device))
                         if sh.gs is not None:
                             sh.gs.fill_(int(gsv.item()))
@@ -196,7 +220,7 @@ class PSServer:
                     self._reply_hdr(worker_rank, g)
                     continue
                 if typ == SAVE:
-                    with sh.lock:
+                    with self._guard():
                         st = sh.state_payload().to(cdev)
                     self._reply_hdr(worker_rank, g)
                     dist.send(st, dst=worker_rank, group=g)
@@ -213,7 +237,7 @@ class PSServer:
                     if self.faults:
                         self.faults.step(sh.global_step())
                 # PULL and PUSH both answer with fresh parameters
-                with sh.lock:
+                with self._guard():
                     params = sh.P.master.to(cdev, copy=True)
                 self._reply_hdr(worker_rank, g)
                 dist.send(params, dst=worker_rank, group=g)
@@ -225,6 +249,32 @@ class PSServer:
         r = torch.tensor([sh.global_step(), int(sh.initialized), sh.version, 0], dtype=torch.int64)
         dist.send(r, dst=worker_rank, group=g)
 
+    def _active_workers(self) -> int:
+        return self.num_workers - self.done_count - len(self.lost)
+
+    def _apply_accumulated(self):
+        """Apply the mean of the accumulated gradients, release the waiters (caller holds _acc_cv)."""
+        sh = self.shard
+        with sh.lock:
+            sh.apply(self._acc.to(sh.device), scale=1.0 / self._acc_n)
+        self._acc.zero_()
+        self._acc_n = 0
+        self._acc_cv.notify_all()
+
+    def _membership_changed(self):
+        """A worker finished or was lost: in sync mode a round that can no longer reach
+        replicas_to_aggregate fresh gradients is applied with the ones it has (else the workers
+        waiting on it would block forever), and the native service's target shrinks."""
+        if not self.sync:
+            return
+        with self._acc_cv:
+            if self._acc_n > 0 and self._acc_n >= min(self.R, self._active_workers()):
+                self._apply_accumulated()
+            self._acc_cv.notify_all()
+        if self.native is not None:
+            with self.native.paused():
+                torch.ops.dtfe.ps_service_set_replicas(self.native.svc, max(1, min(self.R, self._active_workers())))
+
     def _sync_push(self, pay, tag):
         sh = self.shard
         with self._acc_cv:
@@ -234,16 +284,14 @@ class PSServer:
                 self._acc = torch.zeros_like(pay)
             self._acc += pay
             self._acc_n += 1
-            if self._acc_n >= self.R:
-                with sh.lock:
-                    sh.apply(self._acc.to(sh.device), scale=1.0 / self._acc_n)
-                self._acc.zero_()
-                self._acc_n = 0
-                self._acc_cv.notify_all()
+            if self._acc_n >= min(self.R, max(1, self._active_workers())):
+                self._apply_accumulated()
             else:
                 v = sh.version
                 while sh.version == v:
                     self._acc_cv.wait(timeout=1.0)
+                    if sh.version == v and self._acc_n > 0 and self._acc_n >= min(self.R, max(1, self._active_workers())):
+                        self._apply_accumulated()
 
     def serve_forever(self):
         for w in self.server.cluster.worker_ranks()[: len(self.server.cluster.worker)]:
@@ -257,10 +305,15 @@ class PSServer:
                 if self.watchdog is None:
                     continue
                 for _job, task, age in self.watchdog.poll():
-                    if cl.rank_of("worker", task) in self.done_ranks:
+                    if cl.rank_of("worker", task) in self.done_ranks or task in self.lost:
                         continue  # finished normally, then exited
                     self.lost.add(task)
                     self.log("ps %d: worker %d lost (no heartbeat for %.0fs)" % (self.server.task_index, task, age))
+                    self._done_cv.release()
+                    try:
+                        self._membership_changed()
+                    finally:
+                        self._done_cv.acquire()
         self.log("ps %d: quitting" % self.server.task_index)
 
 

@@ -43,6 +43,7 @@ from .parallel.health import Heartbeat, Watchdog
 from .utils.faults import FaultInjector
 from .utils.timers import PhaseTimer
 from .parallel.placement import round_robin
+from .parallel import ps_native
 from .parallel.ps import PSClient, PSServer, Shard, wait_for_init
 from .parallel.supervisor import Supervisor
 from .utils import flags as flagmod
@@ -203,7 +204,16 @@ def run_ps(flags, model, server, device, log):
     ps = PSServer(server, shard, num_workers=flags.workers, sync=flags.sync,
                   replicas_to_aggregate=flags.replicas_to_aggregate, hogwild=flags.hogwild, comm_device=comm,
                   log=log, watchdog=wd, faults=FaultInjector("ps", k, log=log))
+    if _native_ps(flags, server, device):
+        ps.native = ps_native.NativeShardService(server, shard, len(server.cluster.worker), sync=flags.sync,
+                                                 replicas_to_aggregate=flags.replicas_to_aggregate,
+                                                 hogwild=flags.hogwild)
     ps.serve_forever()
+    if ps.native is not None:
+        st = ps.native.stats()
+        log("ps %d: native data plane: %d requests, %d applies, %d stale" % (k, st["requests"], st["applies"],
+                                                                             st["stale"]))
+        ps.native.stop()
     hb.stop()
     if ps.lost:
         # service threads of lost workers are blocked in recv: leave without the collective teardown
@@ -217,6 +227,16 @@ def run_ps(flags, model, server, device, log):
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(0)
+
+
+def _native_ps(flags, server, device) -> bool:
+    """Whether the ps roles move PUSH / PULL over the native single-node data plane."""
+    if flags.ps_transport == "pg":
+        return False
+    ok = ps_native.eligible(server, device)
+    if flags.ps_transport == "native" and not ok:
+        raise SystemExit("--ps_transport=native needs every task on this host, on GPUs")
+    return ok
 
 
 def ps_state(client, model, shard_specs, placement):
@@ -273,15 +293,44 @@ def run_worker_ps(flags, model, server, device, log):
         # GAN:181 / ENC:160: every worker re-runs init, clobbering restore + progress
         prog.P.initialize(flags.seed)
         client.init_variables()
-    client.pull()
+    link = None
+    if _native_ps(flags, server, device):
+        # gradient buckets in backward-completion order (flat order = the order backward produces them)
+        link = ps_native.NativePSLink(server, prog.P, placement, shard_specs, placement[model.gs_name], device,
+                                      buckets=_ps_buckets(prog))
+        core = getattr(prog, "core", None)
+        if core is not None and hasattr(core, "allreduce"):
+            core.allreduce = link       # the CNN program pushes its buckets from inside backward
+        elif hasattr(prog, "grad_ready"):
+            prog.grad_ready = link.ready
+    state = {}
+
+    def native_step():
+        state["m"] = prog.compute_grads()
+        link.end_step()    # push what backward has not pushed yet, request / wait / pull
+
+    runner = StepGraph(native_step, warmup=2, capture_error_mode="thread_local",
+                       enabled=link is not None and flags.hip_graph) if link is not None else None
+    if link is not None:
+        link.pull()
+    else:
+        client.pull()
     step = 0
     local_step = 0
     try:
         while not sv.should_stop() and step < flags.num_steps:
             t0 = time.time()
             prog.load_batch(feeder.next())
-            metrics = prog.compute_grads()
-            step = client.push_pull(prog.P.grad)
+            if link is not None:
+                runner()
+                link.note_request()
+                step = link.host_reply()
+                metrics = state.get("m")
+                if local_step % flags.log_every == 0:
+                    link.check()
+            else:
+                metrics = prog.compute_grads()
+                step = client.push_pull(prog.P.grad)
             if flags.check_pull:
                 log("pull checksum gs=%d: %.9e" % (step, float(prog.P.master.double().sum().item())))
             faults.step(step)
@@ -296,7 +345,7 @@ def run_worker_ps(flags, model, server, device, log):
             local_step += 1
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
         if model.name == "lstm":
-            client.pull()
+            link.pull() if link is not None else client.pull()
             test_len = 128
             acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
                                 torch.from_numpy(data.test.labels[:test_len]).to(device))
@@ -305,6 +354,8 @@ def run_worker_ps(flags, model, server, device, log):
     finally:
         hb.stop()
         sv.stop()
+        if link is not None:
+            link.close()
 
 
 # --------------------------------------------------------------- allreduce
@@ -418,6 +469,15 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
             timer.close()
         sv.stop()
     return prog, opts, gstep
+
+
+def _ps_buckets(prog):
+    """Push buckets of a ps-mode worker: the program's own (the CNN's [head + fc1], [convs]) or
+    ~16 MB ranges of the flat buffer, back to front."""
+    core = getattr(prog, "core", None)
+    if core is not None and getattr(core, "buckets", None):
+        return core.buckets
+    return _buckets(prog.P)
 
 
 def _buckets(P, bucket_elems: int = 4 << 20):

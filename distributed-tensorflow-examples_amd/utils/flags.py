@@ -67,6 +67,9 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     ap.add_argument("--comm", choices=["auto", "rccl", "ipc", "pg"], default="auto",
                     help="all-reduce engine on GPUs: auto = faster of RCCL / hipIpc two-shot per bucket size "
                          "(both in-graph); pg = torch.distributed ProcessGroupNCCL (eager)")
+    ap.add_argument("--ps_transport", choices=["auto", "native", "pg"], default="auto",
+                    help="--mode=ps data plane: native = hipIpc mailboxes + C++ service thread (one node, GPUs; "
+                         "parallel/ps_native.py), pg = torch.distributed send/recv; auto = native when eligible")
     ap.add_argument("--metrics_jsonl", default="", help="append {step, gs, ms, images/sec, loss} lines here")
     ap.add_argument("--heartbeat_secs", type=float, default=0.0,
                     help="publish a TCPStore heartbeat every N s (0: off, the reference has none)")

@@ -1,7 +1,8 @@
 """Multi-process cluster roles on the GPU (one MI355X box): the MNIST CNN through the
 parameter-server path with the ps and both workers on cuda:0 (BASELINE.json config 4 in
-miniature).  Every (ps, worker) pair shares the GPU, so the pairs exchange payloads through
-host memory (Server.pair_comm_device); compute and the optimizer apply run on the GPU kernels."""
+miniature).  Every task drives a GPU of this host, so PUSH / PULL take the native data plane
+(parallel/ps_native.py: hipIpc mailboxes written by the workers' GPUs, a C++ service thread on
+the ps applying them) and only control messages use gloo; compute and the apply are HIP kernels."""
 import os
 import re
 import sys
@@ -28,7 +29,9 @@ def test_cnn_ps_on_gpu(tmp_path, sync):
     codes, out, _ = local_cluster.launch("cnn", 1, 2, extra, timeout=600, stream=False, gpus=1)
     assert all(c == 0 for c in codes.values()), "%s\n%s" % (codes, "\n".join(
         "---- %s\n%s" % (k, "\n".join(v[-40:])) for k, v in out.items()))
-    assert out[("ps", 0)][-1] == "ps 0: quitting"
+    assert "ps 0: quitting" in out[("ps", 0)]
+    # every worker task is on this host's GPU: PUSH / PULL take the native hipIpc data plane
+    assert any(l.startswith("ps 0: native data plane:") for l in out[("ps", 0)]), out[("ps", 0)][-10:]
     gs = _gs(out[("worker", 0)]) + _gs(out[("worker", 1)])
     assert max(gs) >= 8
     t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
@@ -52,3 +55,23 @@ def test_cnn_allreduce_two_workers_ipc_in_graph(tmp_path):
     assert sums[0] and sums[0] == sums[1], sums
     t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
     assert "Variable_1/Adam" in t
+
+
+@pytest.mark.parametrize("hogwild", [False, True])
+def test_bench_ps_native_plane(hogwild):
+    """bench.py --mode ps: 1 ps + 2 workers sharing cuda:0 over the native hipIpc data plane; every
+    pushed gradient is applied exactly once and the JSON line reports the whole job's images/sec."""
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--mode", "ps", "--gpus", "2", "--steps", "30",
+           "--warmup", "4", "--batch_size", "256"] + (["--hogwild"] if hogwild else [])
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    rec = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0
+    c = rec["config"]
+    assert c["ps_applies"] == c["pushes_issued"] == 2 * 34
+    assert c["ps_global_step"] == 2 * 34 and 0 < c["global_step"] <= 2 * 34
+    assert 0.0 < c["last_loss"] < 10.0
