@@ -211,3 +211,53 @@ def test_killed_ps_makes_workers_error_out(tmp_path):
     for w in (0, 1):
         assert codes[("worker", w)] != 0, out[("worker", w)][-5:]
         assert not any(l.startswith("Total Time") for l in out[("worker", w)])
+
+
+def test_sync_three_workers_two_replicas_terminates(tmp_path):
+    """--replicas_to_aggregate below the worker count: the last round may be left with fewer
+    fresh gradients than R once workers finish; the ps must release it and the job must end."""
+    codes, out, _ = local_cluster.launch("softmax", 1, 3, COMMON + ["--num_steps=15", "--workers=3", "--sync",
+                                                                     "--replicas_to_aggregate=2",
+                                                                     "--save_model_secs=0",
+                                                                     "--model_dir=" + str(tmp_path)],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), {k: v[-15:] for k, v in out.items()}
+    assert "ps 0: quitting" in out[("ps", 0)]
+    assert max(max(_gs_lines(out[("worker", w)]) or [0]) for w in range(3)) >= 15
+
+
+def test_lstm_non_default_batch_evaluates(tmp_path):
+    """Test-Accuracy over the reference's 128 test images with a 64-image program batch."""
+    codes, out, _ = local_cluster.launch("lstm", 1, 1, COMMON + ["--num_steps=3", "--workers=1", "--batch_size=64",
+                                                                  "--save_model_secs=0", "--model_dir=" + str(tmp_path)],
+                                         timeout=240, stream=False)
+    assert all(c == 0 for c in codes.values()), out
+    assert any(re.match(r"Test-Accuracy: \d\.\d{4}$", l) for l in out[("worker", 0)])
+    assert "ps 0: quitting" in out[("ps", 0)]
+
+
+def test_shard_apply_takes_the_payload_not_a_shared_buffer():
+    """Hogwild applies run without the shard lock: each one must read its own payload (never a
+    gradient staged in the shard's shared P.grad, which a concurrent push could overwrite)."""
+    import threading
+
+    from dtfe.models.softmax_reg import SoftmaxRegressionModel
+    from dtfe.parallel.ps import Shard
+
+    m = SoftmaxRegressionModel()
+    specs = [s for s in m.specs]
+    sh = Shard(specs, m.opt_groups, "cpu", True, m.gs_increments)
+    sh.P.master.zero_()
+    sh.P.refresh_copies()
+    sh.P.grad.fill_(float("nan"))            # anything read from here would poison the params
+    lr = m.opt_groups[0][0].lr
+    ga = torch.full((sh.P.total,), 1.0)
+    gb = torch.full((sh.P.total,), 2.0)
+    ths = [threading.Thread(target=lambda g=g: [sh.apply(g) for _ in range(5)]) for g in (ga, gb)]
+    for t in ths:  # one after the other: lock-free applies may legitimately race on the params
+        t.start()
+        t.join()
+    v = sh.P.view(specs[0].name)
+    assert torch.isfinite(v).all()
+    assert torch.allclose(v, torch.full_like(v, -lr * 15.0), rtol=1e-5)
+    assert sh.global_step() == 10
