@@ -87,6 +87,9 @@ def main():
                   timeit(lambda: torch.ops.aten.convolution_backward(dyn, xn, wn, None, (s, s), (pad, pad), (1, 1),
                                                                      False, (0, 0), 1, (False, True, False)), a.reps)]
             line += "  || torch " + " ".join("%7.1f" % u for u in tt)
+            if k == 1 and s == 1:  # a 1x1 conv is a plain GEMM: hipBLASLt via torch.mm for the bar
+                a2, w2 = x.view(-1, C), w.view(Cout, C)
+                line += "  || mm %7.1f (%7.1f)" % ((lambda u: (u, fl / u * 1e-6))(timeit(lambda: torch.mm(a2, w2.t()), a.reps)))
             for i in range(3):
                 tot["torch"][i] += n * tt[i]
         print(line, flush=True)

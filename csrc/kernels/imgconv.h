@@ -48,6 +48,7 @@ struct ImgConvArgs {
   uint32_t* zptr[4];
   long zlen[4];
   int nz;
+  int diag;                 // ablation bits for kernel experiments (DTFE_IC_DIAG; 0 in production)
 };
 
 // Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]
@@ -84,5 +85,13 @@ bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s);
 // (imgconv1_copies.hip); false when the shape is not that layer
 bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s);
 bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s);
+
+
+// dw[k] += scale * sum_{p < nblk} ws[p * len + k]   (k >= nw: db[k - nw]), len % 4 == 0.
+// Fixed summation order (each thread a strided subset of the partials in order, then the 16
+// subsets in order through LDS): bitwise reproducible gradients, no atomics.  One workgroup per
+// 64 elements.
+void launch_partials_reduce(const float* ws, int nblk, int len, int nw, float* dw, float* db, float scale,
+                            hipStream_t s);
 
 }  // namespace dtfe

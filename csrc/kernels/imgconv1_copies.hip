@@ -127,7 +127,9 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw[nt][0], f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw[nt][1], acc[nt], 0, 0, 0);
       }
-      // lane holds rows (lane>>4)*4 + j = one 2x2 window, column lane & 15 of each n-tile
+      // lane holds rows (lane>>4)*4 + j = one 2x2 window, column lane & 15 of each n-tile.
+      // Direct scattered stores: at 4-6 workgroups per CU they hide behind the other
+      // workgroups' MFMAs (an LDS-staged 16-B store epilogue measured 15 -> 19 us here)
       const int wq = t * 4 + g, py = wq / 14, px = wq - py * 14;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
@@ -159,12 +161,12 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 P[PRW * PWD];
   __shared__ __attribute__((aligned(16))) bf16 C[5 * CSZ];
   __shared__ __attribute__((aligned(16))) bf16 D[HI * 32 * DP];  // dY [oy][ox < 32][n]
-  __shared__ float red[32 * 32 + 32];
+  constexpr int RL = 32 * 32 + 32;      // one wave's partial dW[n][tap < 32] + db[n]
+  __shared__ float red[4 * RL];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
   const int q4 = i16 >> 2, p4 = i16 & 3;
   for (int i = threadIdx.x; i < PRW * PWD / 8; i += TH) reinterpret_cast<u32x4_t*>(P)[i] = u32x4_t{0u, 0u, 0u, 0u};
   for (int i = threadIdx.x; i < HI * 32 * DP / 8; i += TH) reinterpret_cast<u32x4_t*>(D)[i] = u32x4_t{0u, 0u, 0u, 0u};
-  for (int i = threadIdx.x; i < 32 * 32 + 32; i += TH) red[i] = 0.f;
 
   // B fragment addresses: tap ti = tt*16 + i16 -> (kh, kw); taps >= 25 read tap 24 (dropped)
   int boff[2];
@@ -258,19 +260,21 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
     }
     __syncthreads();
   }
-  // cross-wave reduction in LDS: red[n][tap] (+ db[n])
+  // cross-wave reduction in LDS: every wave stores its own partial (no LDS float atomics), the
+  // flush sums the 4 in wave order - the weight gradient is bitwise reproducible
+  float* mine = red + wid * RL;
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(red + (nt * 16 + g * 4 + j) * 32 + tt * 16 + i16, acc[nt][tt][j]);
+      for (int j = 0; j < 4; ++j) mine[(nt * 16 + g * 4 + j) * 32 + tt * 16 + i16] = acc[nt][tt][j];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     float v = dbacc[nt];
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
-    if (lane < 16) atomicAdd(red + 32 * 32 + nt * 16 + lane, v);
+    if (lane < 16) mine[32 * 32 + nt * 16 + lane] = v;
   }
   __syncthreads();
   // flush: dW[n][tap] (tap < 25) and db[n]; one partial per workgroup (summed by the reduce
@@ -278,29 +282,12 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
   constexpr int KC = 25, LEN = NCH * KC + NCH;
   float* part = a.ws ? a.ws + (long)blockIdx.x * LEN : nullptr;
   for (int i = threadIdx.x; i < LEN; i += TH) {
-    const float v = i < NCH * KC ? red[(i / KC) * 32 + (i % KC)] : red[32 * 32 + (i - NCH * KC)];
+    const int r = i < NCH * KC ? (i / KC) * 32 + (i % KC) : 32 * 32 + (i - NCH * KC);
+    const float v = ((red[r] + red[RL + r]) + red[2 * RL + r]) + red[3 * RL + r];
     if (part) part[i] = v;
     else if (i < NCH * KC) atomicAdd(a.dw + i, v * a.scale);
     else if (a.db) atomicAdd(a.db + (i - NCH * KC), v * a.scale);
   }
-}
-
-// dw[i] += scale * sum_p part[p][i] (tail -> db): one thread per element, 16 partials per
-// y-block with all loads in flight, one atomic per element and y-block
-constexpr int RP = 16;
-__global__ __launch_bounds__(256) void conv1c_reduce_kernel(const float* __restrict__ ws, int parts, int len, int nw,
-                                                            float* dw, float* db, float scale) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= len) return;
-  const int p0 = blockIdx.y * RP;
-  float v[RP];
-#pragma unroll
-  for (int j = 0; j < RP; ++j) v[j] = p0 + j < parts ? ws[(long)(p0 + j) * len + i] : 0.f;
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < RP; ++j) s += v[j];
-  if (i < nw) atomicAdd(dw + i, scale * s);
-  else if (db) atomicAdd(db + i - nw, scale * s);
 }
 
 bool mnist_conv1_shape(int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad) {
@@ -325,8 +312,7 @@ bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a);
   if (a.ws) {
     constexpr int LEN = NCH * 25 + NCH;
-    hipLaunchKernelGGL(conv1c_reduce_kernel, dim3((LEN + 255) / 256, (grid + RP - 1) / RP), dim3(256), 0, s, a.ws,
-                       grid, LEN, NCH * 25, a.dw, a.db, a.scale);
+    launch_partials_reduce(a.ws, grid, LEN, NCH * 25, a.dw, a.db, a.scale, s);
   }
   return true;
 }

@@ -401,6 +401,7 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
 
   const int g = lane >> 4;
   const int M = a.OH * a.OW, tiles = (M + 15) >> 4;
+  const int nout = (POOLED ? M : (M >> 2)) * a.N / 8;  // 16-B chunks of one image's output
   const bf16* wlane = wl + (lane & 15) * KP + 8 * g;
   float biasv[NT];  // loaded once, not once per image in the epilogue
 #pragma unroll
@@ -410,9 +411,9 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
   if (b < a.B) load_src(b);
   __syncthreads();
   for (; b < a.B; b += gridDim.x) {
-    write_src();
+    if (!(a.diag & 2) || b == blockIdx.x) write_src();
     __syncthreads();
-    if (b + gridDim.x < a.B) load_src(b + gridDim.x);
+    if (b + gridDim.x < a.B && !(a.diag & 2)) load_src(b + gridDim.x);
     // tiles past the image (a wave's last r) multiply pixel 0 and are dropped by the epilogue:
     // no lane-divergent guards inside the k loop
     const bf16* abase[RT];
@@ -422,20 +423,10 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
       row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
       abase[r] = img + (oy * LWP + ox) * PS + 8 * g;
     }
-    // data-gradient epilogue mask: loads issued now, in flight during the k loop
-    bf16 mask[RT][NT][4];
-    if (!a.pool && a.relu_mask) {
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int oy = 0, ox = 0;
-            row_pixel((wm + WM * r) * 16 + (lane >> 4) * 4 + j, a.OH, a.OW, G.blocked, oy, ox);
-            mask[r][n][j] = a.relu_mask[((b * a.OH + oy) * a.OW + ox) * a.N + n * 16 + (lane & 15)];
-          }
-    }
+    // data-gradient ReLU mask: this thread's 16-B chunk of the image's [OH*OW][N] output, in
+    // flight during the k loop (host: M * N / 8 <= THREADS)
+    u32x4_t mk = {0u, 0u, 0u, 0u};
+    if (POOLED && a.relu_mask && tid < nout) mk = *reinterpret_cast<const u32x4_t*>(a.relu_mask + b * M * a.N + tid * 8);
     f32x4_t acc[RT][NT];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -458,7 +449,7 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
     static_for<0, PF>([&](auto sc) {
       if constexpr (decltype(sc)::value < NK) fetch(sc);
     });
-    static_for<0, NK>([&](auto sc) {
+    if (!(a.diag & 4)) static_for<0, NK>([&](auto sc) {
       constexpr int st = decltype(sc)::value;
       if constexpr (st + PF < NK) fetch(std::integral_constant<int, st + PF>{});
       constexpr int buf = st % (PF + 1);
@@ -471,41 +462,81 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
                                                               0, 0, 0);
       }
     });
+    // Epilogue through LDS: the per-lane results are scattered 2-byte (and 1-byte argmax) values,
+    // so they are staged in LDS in the output's own layout and leave as 16-B row-contiguous
+    // stores (each image's output is one contiguous block).  rocprof ablation of the direct
+    // scattered stores: ~2 us per image per CU, a quarter of the forward kernel.
+    if constexpr (!POOLED) {
+      // forward (+bias, act, 2x2 max-pool, argmax): stage [M/4][N] values + [M/4][N] argmax bytes
+      // in the dedicated region after the image; the next image's staging is two barriers away
+      bf16* sy = img + G.LH * LWP * PS;
+      uint8_t* sa = reinterpret_cast<uint8_t*>(sy + (M >> 2) * a.N);
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int tile = wm + WM * r;
-      if (tile >= tiles) break;
-      const int m0 = tile * 16 + (lane >> 4) * 4;
+      for (int r = 0; r < RT; ++r) {
+        const int tile = wm + WM * r;
+        if (tile >= tiles || (a.diag & 1)) break;
+        int oy, ox;
+        if (!row_pixel(tile * 16 + (lane >> 4) * 4, a.OH, a.OW, 1, oy, ox)) continue;
+        const int pp = (oy >> 1) * (a.OW >> 1) + (ox >> 1);
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const int col = n * 16 + (lane & 15);
-        if (col >= a.N) continue;
-        const float bias = biasv[n];
-        const f32x4_t v = acc[r][n];
-        if (a.pool) {
-          int oy, ox;
-          if (!row_pixel(m0, a.OH, a.OW, 1, oy, ox)) continue;
+        for (int n = 0; n < NT; ++n) {
+          const int col = n * 16 + (lane & 15);
+          const f32x4_t v = acc[r][n];
           int am = 0;
           float mx = v[0];
 #pragma unroll
           for (int j = 1; j < 4; ++j) if (v[j] > mx) { mx = v[j]; am = j; }
-          const long o = ((b * (a.OH >> 1) + (oy >> 1)) * (a.OW >> 1) + (ox >> 1)) * a.N + col;
-          a.y[o] = f2bf(apply_act(mx + bias, a.act));
-          if (a.argmax) a.argmax[o] = (uint8_t)am;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int oy, ox;
-            if (!row_pixel(m0 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
-            const long o = ((b * a.OH + oy) * a.OW + ox) * a.N + col;
-            float x = apply_act(v[j] + bias, a.act);
-            if (a.relu_mask && !(bf2f(mask[r][n][j]) > 0.f)) x = 0.f;
-            a.y[o] = f2bf(x);
-          }
+          sy[pp * a.N + col] = f2bf(apply_act(mx + biasv[n], a.act));
+          sa[pp * a.N + col] = (uint8_t)am;
         }
       }
+      __syncthreads();
+      const int ny = nout, na = nout / 2;  // 16-B chunks of values / argmax bytes
+      const long pb = b * (M >> 2) * a.N;
+      for (int i = tid; i < ny + na; i += THREADS) {
+        if (i < ny) {
+          *reinterpret_cast<u32x4_t*>(a.y + pb + i * 8) = *reinterpret_cast<const u32x4_t*>(sy + i * 8);
+        } else if (a.argmax) {
+          const int k = i - ny;
+          *reinterpret_cast<u32x4_t*>(a.argmax + pb + k * 16) = *reinterpret_cast<const u32x4_t*>(sa + k * 16);
+        }
+      }
+    } else {
+      // data gradient (ReLU'-masked, no pool): stage [pixel][N] in the image interior once every
+      // wave is done reading the image, then masked 16-B stores
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int tile = wm + WM * r;
+        if (tile >= tiles || (a.diag & 1)) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int oy, ox;
+          if (!row_pixel(tile * 16 + (lane >> 4) * 4 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
+          bf16* d = img + ((oy + a.pad) * LWP + ox + a.pad) * PS + (lane & 15);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) d[n * 16] = f2bf(apply_act(acc[r][n][j] + biasv[n], a.act));
+        }
+      }
+      __syncthreads();
+      constexpr int CPX = NT * 2;  // 16-B chunks per output pixel
+      for (int i = tid; i < nout; i += THREADS) {
+        const int p = i / CPX, c = i - p * CPX;
+        const int oy = p / a.OW, ox = p - oy * a.OW;
+        u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + ((oy + a.pad) * LWP + ox + a.pad) * PS + c * 8);
+        if (a.relu_mask) {
+          const u32x4_t m = i == tid ? mk : *reinterpret_cast<const u32x4_t*>(a.relu_mask + b * M * a.N + i * 8);
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {  // keep element e where mask e > 0 (bf16 bits: positive, non-zero, not NaN)
+            const uint32_t lo = m[w] & 0xffffu, hi = m[w] >> 16;
+            const uint32_t keep = ((lo - 1u) < 0x7f80u ? 0x0000ffffu : 0u) | ((hi - 1u) < 0x7f80u ? 0xffff0000u : 0u);
+            v[w] &= keep;
+          }
+        }
+        *reinterpret_cast<u32x4_t*>(a.y + (b * M + p) * (long)a.N + c * 8) = v;
+      }
+      __syncthreads();  // the interior is read before the next image is written into it
     }
-    __syncthreads();
   }
 }
 
@@ -606,16 +637,25 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
   constexpr int K = KH * KW * CS, KP = (K + 31) / 32 * 32 + 16;
   if (a.CS != CS || a.KH != KH || a.KW != KW || a.N != NT * 16 || a.stride != 1 || a.dil > 1) return false;
   if ((a.src == nullptr) != POOLED) return false;
+  // the LDS-staged epilogues: forward = pooled (+ argmax), data gradient = un-pooled
+  if (POOLED ? a.pool != 0 : a.pool == 0) return false;
   PGeom G = persist_geom(a, 1, NT, 64 * WM);
   if (G.LWP != LWP || G.PS != PS || G.KP != KP || G.slack != 0) return false;
   const int tiles = (a.OH * a.OW + 15) / 16;
   if (tiles > WM * RT) return false;
-  const size_t lds = persist_lds(G);
+  // forward staging region after the image: [M/4][N] bf16 values + [M/4][N] argmax bytes
+  const size_t lds = persist_lds(G) + (POOLED ? 0 : (size_t)(a.OH * a.OW / 4) * a.N * 3);
   if (lds > 160 * 1024 || (a.pool && !G.blocked)) return false;
   const int grid = a.B < 256 ? a.B : 256;
+  static const int diag = [] {
+    const char* e = getenv("DTFE_IC_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  ImgConvArgs ad = a;
+  ad.diag = diag;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM), lds, s, a, G);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM), lds, s, ad, G);
   };
   switch (G.npf) {
     case 1: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 1, POOLED>); return true;
@@ -631,6 +671,18 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
     return !(e && atoi(e) == 0);
   }();
   if (fixed_ok && a.OH == 14 && a.OW == 14 && a.B >= 256) {
+    // DTFE_IC_RT: 16-row tiles per wave (1: 13 waves, 2: 7 waves, 4: 4 waves) - experiments
+    static const int rt = [] {
+      const char* e = getenv("DTFE_IC_RT");
+      return e ? atoi(e) : 1;
+    }();
+    if (rt == 2) {
+      if (launch_fixed<32, 5, 5, 20, 48, 4, 2, 7, false>(a, s)) return true;
+      if (launch_fixed<64, 5, 5, 20, 80, 2, 2, 7, true>(a, s)) return true;
+    } else if (rt == 4) {
+      if (launch_fixed<32, 5, 5, 20, 48, 4, 4, 4, false>(a, s)) return true;
+      if (launch_fixed<64, 5, 5, 20, 80, 2, 4, 4, true>(a, s)) return true;
+    }
     if (launch_fixed<32, 5, 5, 20, 48, 4, 1, 13, false>(a, s)) return true;  // conv2 forward
     if (launch_fixed<64, 5, 5, 20, 80, 2, 1, 13, true>(a, s)) return true;   // conv2 data gradient
   }

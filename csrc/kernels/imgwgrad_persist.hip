@@ -246,30 +246,47 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
   }
 }
 
-// dw[i] += scale * sum_b part[b][i] (and the bias tail into db).  blockIdx.y picks a
-// chunk of RCH partials (all loads of a thread in flight together), then one
-// atomic per element and chunk: 256 partials -> 16-way contention.
-constexpr int RCH = 16;
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int nblk, int len, int nw,
-                                                           float* dw, float* db, float scale) {
-  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= len) return;
-  const int b0 = blockIdx.y * RCH;
-  f32x4_t v[RCH];
+}  // namespace
+
+__global__ __launch_bounds__(256) void partials_reduce_kernel(const float* __restrict__ ws, int nblk, int len, int nw,
+                                                              float* dw, float* db, float scale) {
+  __shared__ f32x4_t red[16][17];
+  const int c = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const int i = (blockIdx.x * 16 + c) * 4;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < len) {
+    for (int p0 = pg; p0 < nblk; p0 += 16 * 8) {
+      f32x4_t v[8];
 #pragma unroll
-  for (int j = 0; j < RCH; ++j)
-    v[j] = b0 + j < nblk ? *reinterpret_cast<const f32x4_t*>(ws + (long)(b0 + j) * len + i) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 8; ++j) {
+        const int p = p0 + 16 * j;
+        v[j] = p < nblk ? *reinterpret_cast<const f32x4_t*>(ws + (long)p * len + i) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
-  for (int w = RCH / 2; w >= 1; w /= 2)
+      for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+  }
+  red[pg][c] = acc;
+  __syncthreads();
+  if (pg == 0 && i < len) {
+    f32x4_t t = red[0][c];
 #pragma unroll
-    for (int j = 0; j < w; ++j) v[j] += v[j + w];
+    for (int q = 1; q < 16; ++q) t += red[q][c];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int k = i + e;
-    if (k < nw) atomicAdd(dw + k, scale * v[0][e]);
-    else if (k < len && db) atomicAdd(db + k - nw, scale * v[0][e]);
+    for (int e = 0; e < 4; ++e) {
+      const int k = i + e;
+      if (k < nw) dw[k] += scale * t[e];
+      else if (db) db[k - nw] += scale * t[e];
+    }
   }
 }
+
+void launch_partials_reduce(const float* ws, int nblk, int len, int nw, float* dw, float* db, float scale,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(partials_reduce_kernel, dim3((len + 63) / 64), dim3(256), 0, s, ws, nblk, len, nw, dw, db, scale);
+}
+
+namespace {
 
 WPGeom wp_geom(const ImgWgradArgs& a) {
   WPGeom G;
@@ -305,8 +322,7 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a, G);
     if (a.ws) {
       const int nw = a.N * a.KH * a.KW * a.CS, len = nw + a.N;  // len % 4 == 0: N % 8 == 0
-      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len / 4 + 255) / 256, (grid + RCH - 1) / RCH), dim3(256), 0, s,
-                         a.ws, grid, len, nw, a.dw, a.db, a.scale);
+      launch_partials_reduce(a.ws, grid, len, nw, a.dw, a.db, a.scale, s);
     }
     return true;
   };

@@ -200,6 +200,9 @@ class MnistCnnTrainer:
         self.fused_gather = os.environ.get("DTFE_CNN_FUSED_GATHER", "1") != "0"
         br = os.environ.get("DTFE_CNN_BRANCHES", "fc,c2").split(",")
         self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2", "side1"})
+        # capture order of the branched backward (DTFE_CNN_ORDER): "branch" = each branch's work
+        # captured before the critical chain continues, "crit" = the critical chain first
+        self.crit_first = os.environ.get("DTFE_CNN_ORDER", "branch") == "crit"
         self.br_one = self.par and "side1" in br   # ONE weight-grad branch forked after fc1 dgrad
         self.br_fc = self.par and not self.br_one and "fc" in br
         self.br_c2 = self.par and (self.br_one or "c2" in br)
@@ -226,6 +229,14 @@ class MnistCnnTrainer:
         self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 8)
         self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
         self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
+        # head weight gradient: split-K over the batch with the deterministic last-arriver combine
+        # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
+        # workspace, since it runs on the fc branch beside other GEMMs
+        self.head_splits = max(1, min(16, B // 128))
+        bm, bn = ops.TILE_DIMS[4]
+        ntiles = -(-NCLS // bm) * -(-(FC + 1) // bn)
+        self.ws_head = (torch.empty(self.head_splits * ntiles * bm * bn, device=d, dtype=torch.float32),
+                        torch.zeros(ntiles, device=d, dtype=torch.int32)) if self.head_splits > 1 else None
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
@@ -264,19 +275,28 @@ class MnistCnnTrainer:
         if self.br_one:
             self._backward_one_branch(main)
             return
-        with self._branch(self.s_fc if self.br_fc else None, main):
+        # Capture order changes how the hipGraph runtime maps the branches onto hardware queues (every
+        # edge between queues costs ~5-10 us of dependency latency on this step's timeline): with
+        # crit_first the fork point is recorded on the branch stream and the critical chain is
+        # captured before the branch work; otherwise the branch work comes first.
+        crit = self.crit_first
+        if self.br_fc and crit:
+            self.s_fc.wait_stream(main)        # fork: the weight-grad branch depends on head_xent only
+        if crit:
+            self._fc1_dgrad(B, K1)
+        with (self._branch(self.s_fc, main) if (self.br_fc and not crit) else
+              torch.cuda.stream(self.s_fc) if self.br_fc else contextlib.nullcontext()):
             # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
             ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
-                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
-                     splits=max(1, min(16, B // 128)), tile=4)
+                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],
+                     splits=self.head_splits, tile=4, workspace=self.ws_head)
             # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
                      bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
             if self.allreduce is not None:  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
                 self.allreduce.launch(0)
-        # fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)
-        ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
-                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
+        if not crit:
+            self._fc1_dgrad(B, K1)
         if self._apply is not None and self._apply[0] == "early":
             # fc/head Adam as soon as their (reduced) gradients are final - and after fc1 dgrad, the
             # last reader of the fc1 weights this step (the branch re-joins main's progress here)
@@ -284,14 +304,18 @@ class MnistCnnTrainer:
                 if self.allreduce is not None:
                     self.allreduce.wait_launched()
                 self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
-        with self._branch(self.s_c2 if self.br_c2 else None, main):
+        if self.br_c2 and crit:
+            self.s_c2.wait_stream(main)        # fork after fc1 dgrad (dP2 final)
+        if crit:
+            self._conv2_dgrad()
+        with (self._branch(self.s_c2, main) if (self.br_c2 and not crit) else
+              torch.cuda.stream(self.s_c2) if self.br_c2 else contextlib.nullcontext()):
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
                          workspace=self.ws_c2 if self.br_c2 else None,
                          max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
-        # conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)
-        ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
-                    flip_taps=True, **self.ic2_dgrad)
+        if not crit:
+            self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
         if self.br_fc:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
@@ -305,6 +329,16 @@ class MnistCnnTrainer:
             self.allreduce.wait()
         if self._apply is not None:
             self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
+
+    def _fc1_dgrad(self, B, K1):
+        """fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)."""
+        ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
+                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
+
+    def _conv2_dgrad(self):
+        """conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)."""
+        ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
+                    flip_taps=True, **self.ic2_dgrad)
 
     def _ensure_split(self):
         """fc/head and conv optimizers over disjoint var lists, sharing one set of slot buffers."""
@@ -325,8 +359,8 @@ class MnistCnnTrainer:
                  aux_act=ops.ACT_RELU, tile=self.t_dgrad)
         with self._branch(self.s_fc, main):
             ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
-                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"], atomic=True,
-                     splits=max(1, min(16, B // 128)), tile=4)
+                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],
+                     splits=self.head_splits, tile=4, workspace=self.ws_head)
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
                      bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
             if self.allreduce is not None:

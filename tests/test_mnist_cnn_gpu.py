@@ -236,3 +236,21 @@ def test_cnn_adam_step_matches_torch_adam_tf1_form():
     R, T, C = P.spec(n["wc2"]).transpose
     wt = P.view(n["wc2"]).reshape(R, T, C).permute(2, 1, 0).reshape(-1).to(torch.bfloat16)
     assert torch.equal(P.wt16[n["wc2"]], wt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [256, 1024])
+def test_cnn_training_is_bitwise_reproducible(B):
+    """Two trainers with the same seed follow the same trajectory bit for bit: every reduction of
+    the step (split-K combines, conv weight-gradient partial sums) runs in a fixed order, no
+    float atomics - the property the data-parallel replicas_identical check builds on."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+
+    outs = []
+    for _ in range(2):
+        tr = MnistCnnTrainer(B, "cuda", seed=5)
+        for _ in range(5):
+            tr.step()
+        torch.cuda.synchronize()
+        outs.append(tr.P.master.clone())
+    assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
