@@ -249,8 +249,8 @@ void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tens
   dtfe::ImgWgradArgs a{};
   a.max_blocks = (int)max_blocks;
   if (ws.has_value() && ws->defined()) {
-    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= 256 * (N * KH * KW * CS + N),
-                "imgwgrad: workspace too small");
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= dtfe::imgwgrad_ws_floats((int)N, (int)(KH * KW * CS)),
+                "imgwgrad: workspace too small (ops.wgrad_ws_floats)");
     a.ws = ws->data_ptr<float>();
   }
   a.B = (int)B; a.SH = (int)SH; a.SW = (int)SW; a.CS = (int)CS; a.OH = (int)OH; a.OW = (int)OW; a.N = (int)N;

@@ -69,6 +69,7 @@ struct ImgWgradArgs {
   // more images each and halve the partial-sum traffic - the better trade when the launch
   // runs beside other work (MNIST conv2's weight grad on its own graph branch)
   int max_blocks;
+  int diag;                 // ablation bits for kernel experiments (DTFE_IW_DIAG; 0 in production)
 };
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
@@ -77,6 +78,9 @@ void launch_imgconv(const ImgConvArgs& a, hipStream_t s);
 // returns false when the shape does not fit it (launch_imgconv then uses the per-image kernel)
 bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s);
 bool imgwgrad_supported(const ImgWgradArgs& a);
+// floats of the partial-sum workspace the weight-gradient kernels need (256 workgroup slabs);
+// mirrored by ops.wgrad_ws_floats
+long imgwgrad_ws_floats(int N, int KC);
 void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s);
 // persistent variant (dW accumulated in registers across a workgroup's images);
 // returns false when the shape does not fit it

@@ -49,6 +49,9 @@ __host__ __device__ inline int odd16(int e) {  // round up to 16 * odd elements
   return 16 * (u | 1);
 }
 
+// floats per workgroup slab of the register-layout partials (tiles + db, rounded to 16 B)
+__host__ __device__ inline int wp_part_len(int MT, int CTW, int N) { return 8 * CTW * MT * 256 + (N + 3) / 4 * 4; }
+
 template <int MT, int CTW, int NPFS, int NPFD, bool POOLED>
 __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, WPGeom G) {
   constexpr int THREADS = 512;
@@ -176,10 +179,10 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
   if (b < a.B) load_img(b);
   __syncthreads();
   for (; b < a.B; b += gridDim.x) {
-    write_img();
+    if (!(a.diag & 2) || b == blockIdx.x) write_img();
     __syncthreads();
-    if (b + gridDim.x < a.B) load_img(b + gridDim.x);
-    for (int s = 0; s < G.nk; ++s) {
+    if (b + gridDim.x < a.B && !(a.diag & 2)) load_img(b + gridDim.x);
+    for (int s = 0; s < ((a.diag & 4) ? 0 : G.nk); ++s) {
       bf16x8_t af[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -215,8 +218,30 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     }
     __syncthreads();
   }
-  // ---- flush: row n = mt*16 + (lane>>4)*4 + j, column = (ct0 + c)*16 + (lane&15)
-  float* part = a.ws ? a.ws + (long)blockIdx.x * ((long)a.N * KC + a.N) : nullptr;
+  // ---- flush.  With a workspace: the accumulators in their REGISTER layout - slab
+  // [wave][c][mt][lane] of f32x4, one coalesced 16-B store per lane and tile (the (n, col)
+  // scatter happens once, in the reduce kernel) - then db[N] after the 8 * CTW * MT tiles.
+  // Without: scaled atomics into dw / db.
+  if (a.diag & 1) return;
+  if (a.ws) {
+    float* part = a.ws + (long)blockIdx.x * wp_part_len(MT, CTW, a.N);
+    f32x4_t* pv = reinterpret_cast<f32x4_t*>(part) + (long)wid * CTW * MT * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) pv[(c * MT + mt) * 64] = acc[mt][c];  // dead tiles: ignored
+    if (wid == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float v = dbacc[mt];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int n = mt * 16 + i16;
+        if (lane < 16 && n < a.N) part[8 * CTW * MT * 256 + n] = v;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int c = 0; c < CTW; ++c) {
     if (c >= nct) break;
@@ -226,22 +251,63 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = mt * 16 + g * 4 + j;
-        if (n >= a.N) continue;
-        if (part) part[(long)n * KC + col] = acc[mt][c][j];
-        else atomicAdd(a.dw + (long)n * KC + col, acc[mt][c][j] * a.scale);
+        if (n < a.N) atomicAdd(a.dw + (long)n * KC + col, acc[mt][c][j] * a.scale);
       }
   }
-  if (wid == 0 && (a.db || part)) {
+  if (wid == 0 && a.db) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       float v = dbacc[mt];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       const int n = mt * 16 + i16;
-      if (lane < 16 && n < a.N) {
-        if (part) part[(long)a.N * KC + n] = v;
-        else atomicAdd(a.db + n, v * a.scale);
+      if (lane < 16 && n < a.N) atomicAdd(a.db + n, v * a.scale);
+    }
+  }
+}
+
+// sum of the register-layout partial slabs over the nblk workgroups in a fixed order (16
+// strided subsets, then the subsets in order through LDS: bitwise reproducible, no atomics),
+// scattered once into dw[n][col] / db[n]
+__global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict__ ws, int nblk, int plen, int MT,
+                                                        int CTW, int KC, int N, float* dw, float* db, float scale) {
+  __shared__ f32x4_t red[16][17];
+  const int c16 = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const int v = blockIdx.x * 16 + c16;  // f32x4 index within a slab
+  const int nv = (plen + 3) / 4;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (v < nv) {
+    for (int p0 = pg; p0 < nblk; p0 += 16 * 8) {
+      f32x4_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = p0 + 16 * j;
+        x[j] = p < nblk ? *reinterpret_cast<const f32x4_t*>(ws + (long)p * plen + 4 * v) : f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j];
+    }
+  }
+  red[pg][c16] = acc;
+  __syncthreads();
+  if (pg != 0 || v >= nv) return;
+  f32x4_t t = red[0][c16];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) t += red[q][c16];
+  const int ntile = 8 * CTW * MT * 64;  // f32x4 of the tile region
+  if (v < ntile) {
+    const int lane = v & 63, r = v >> 6, mt = r % MT, rc = r / MT, c = rc % CTW, w = rc / CTW;
+    const int col = (w * CTW + c) * 16 + (lane & 15), n0 = mt * 16 + (lane >> 4) * 4;
+    if (col < KC) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n0 + j < N) dw[(long)(n0 + j) * KC + col] += scale * t[j];
+    }
+  } else if (db) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = (v - ntile) * 4 + j;
+      if (n < N) db[n] += scale * t[j];
     }
   }
 }
@@ -319,10 +385,17 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   const int grid = a.B < gcap ? a.B : gcap;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, a, G);
+    static const int diag = [] {
+      const char* e = getenv("DTFE_IW_DIAG");
+      return e ? atoi(e) : 0;
+    }();
+    ImgWgradArgs ad = a;
+    ad.diag = diag;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, ad, G);
     if (a.ws) {
-      const int nw = a.N * a.KH * a.KW * a.CS, len = nw + a.N;  // len % 4 == 0: N % 8 == 0
-      launch_partials_reduce(a.ws, grid, len, nw, a.dw, a.db, a.scale, s);
+      const int plen = wp_part_len(MT, CTW, a.N), KC = a.KH * a.KW * a.CS;
+      hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW, KC,
+                         a.N, a.dw, a.db, a.scale);
     }
     return true;
   };
@@ -343,6 +416,13 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
 }
 
 }  // namespace
+
+long imgwgrad_ws_floats(int N, int KC) {
+  const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 8;  // the wp_launch instances below
+  const long plain = (long)N * KC + N;                   // imgconv1_copies / per-image kernels
+  const long reg = wp_part_len(MT, CTW, N);
+  return 256L * (plain > reg ? plain : reg);
+}
 
 bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s) {
   if (a.CS % 16 || a.N % 8 || a.N > 64 || a.OW > 32 || a.B < 128) return false;

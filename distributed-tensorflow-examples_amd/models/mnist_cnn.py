@@ -240,7 +240,7 @@ class MnistCnnTrainer:
         if self.par:
             self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
-            self.ws_c2 = torch.empty(256 * (C2 * KS * KS * C1 + C2), device=d, dtype=torch.float32)
+            self.ws_c2 = torch.empty(ops.wgrad_ws_floats(C2, KS * KS * C1), device=d, dtype=torch.float32)
 
     def _glds_tile(self, A, Bm, M, N, K, lda, ldb, tile, b_ones_row=-1):
         if self.glds and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row):

@@ -354,6 +354,14 @@ def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None
 _WG_WS = {}
 
 
+def wgrad_ws_floats(N: int, KC: int) -> int:
+    """Floats of the weight-gradient partial-sum workspace (256 workgroup slabs) - mirrors
+    imgwgrad_ws_floats in csrc/kernels/imgwgrad_persist.hip (the register-layout slabs of the
+    persistent kernel: 8 waves x CTW column tiles x MT row tiles x 64 lanes x 4, + db)."""
+    MT, CTW = (4, 7) if N > 32 else (2, 8)
+    return 256 * max(N * KC + N, 8 * CTW * MT * 256 + (N + 3) // 4 * 4)
+
+
 def wgrad_workspace(device, numel):
     """Cached fp32 partial-sum buffer for the persistent weight-gradient kernel
     (per device, grown on demand; single-stream use)."""
@@ -374,7 +382,7 @@ def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, 
     (default: a cached per-device buffer) and a second kernel sums them."""
     if dw.is_cuda:
         if workspace is None and (CS % 16 == 0 or CS == 1):
-            workspace = wgrad_workspace(dw.device, 256 * (N * KH * KW * CS + N))
+            workspace = wgrad_workspace(dw.device, wgrad_ws_floats(N, KH * KW * CS))
         require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
                            scale, workspace, max_blocks)
         return
