@@ -379,7 +379,8 @@ template <typename Cfg> struct FwdK { static constexpr auto fn = conv_fwd_kernel
 template <typename Cfg> struct DgradK { static constexpr auto fn = conv_dgrad_kernel<Cfg>; };
 
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
-  if (launch_igemm_fwd(a, s)) return;  // wide layers: DMA-staged 64-deep k-tiles
+  if (launch_stem_fwd(a, s)) return;   // ImageNet 7x7/2 stem
+  if (launch_igemm_fwd(a, s)) return;  // wide layers: DMA-staged 64-deep k-tiles  // wide layers: DMA-staged 64-deep k-tiles
   const ConvGeom& g = a.g;
   if (g.pool_order && ((g.OH | g.OW) & 1)) throw std::runtime_error("conv_fwd: pool needs even output dims");
   launch_skinny<FwdK>(a, g.B * g.OH * g.OW, g.Cout, s);
@@ -407,6 +408,7 @@ static void wgrad_launch(const ConvWgradArgs& a0, int target_blocks, hipStream_t
 }
 
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
+  if (launch_stem_wgrad(a, s, true)) return;
   if (launch_igemm_wgrad(a, s)) return;
   const ConvGeom& g = a.g;
   const int M = g.Cout, N = g.KH * g.KW * g.C + (a.db ? 1 : 0);

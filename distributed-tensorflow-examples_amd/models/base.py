@@ -24,6 +24,19 @@ import torch
 from ..optim import FlatParams
 
 
+
+class ScaledScalar:
+    """A step metric kept as (device scalar, host scale): ``.item()`` reads and scales it on the
+    host, so a captured step issues no extra kernel just to divide a loss sum by the batch."""
+
+    def __init__(self, t, scale: float):
+        self.t, self.scale = t, float(scale)
+
+    def item(self) -> float:
+        return float(self.t.item()) * self.scale
+
+    __float__ = item
+
 class StepProgram:
     batch_size: int
 

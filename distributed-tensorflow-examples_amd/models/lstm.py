@@ -24,7 +24,7 @@ import torch
 
 from .. import ops
 from ..optim import OptimizerConfig, VarSpec
-from .base import ModelDef, StepProgram, glorot_uniform_init, normal_init, zeros_init
+from .base import ModelDef, ScaledScalar, StepProgram, glorot_uniform_init, normal_init, zeros_init
 
 T, I, H, NC = 28, 28, 128, 10
 LR = 0.001
@@ -121,7 +121,7 @@ class LstmProgram(StepProgram):
             self._bptt_steps()
         ops.gemm(self.xh, self.dg, self.gK, M=I + H + 1, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H,
                  bmode=ops.RMAJ, ldb=4 * H, a_ones_row=I + H, bias_out=self.gb)
-        return {"loss": self.loss / B}
+        return {"loss": ScaledScalar(self.loss, 1.0 / B)}
 
     def _bptt_steps(self):
         """Per-step BPTT: fused cell-backward kernel + dgrad GEMM per timestep (CPU reference /

@@ -43,7 +43,7 @@ import torch
 
 from .. import ops
 from ..optim import FlatParams, Optimizer, OptimizerConfig, VarSpec
-from .base import ModelDef, StepProgram
+from .base import ModelDef, ScaledScalar, StepProgram
 
 IMG, C1, C2, FC, NCLS = 28, 32, 64, 1024, 10
 KS = 5
@@ -468,7 +468,7 @@ class CnnProgram(StepProgram):
 
     def compute_grads(self):
         self.core.forward_backward()
-        return {"loss": self.core.loss_sum / self.batch_size, "correct": self.core.correct}
+        return {"loss": ScaledScalar(self.core.loss_sum, 1.0 / self.batch_size), "correct": self.core.correct}
 
     def evaluate(self, images, labels) -> float:
         raise NotImplementedError("the CNN example has no evaluation step")

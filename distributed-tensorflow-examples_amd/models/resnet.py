@@ -40,7 +40,7 @@ import torch
 
 from .. import ops
 from ..optim import OptimizerConfig, VarSpec
-from .base import ModelDef, StepProgram
+from .base import ModelDef, ScaledScalar, StepProgram
 
 BN_EPS, BN_MOMENTUM = 1e-3, 0.99
 # activation / activation-gradient storage dtype: bf16 on the GPU kernels; the CPU reference
@@ -507,7 +507,7 @@ class ResNetProgram(StepProgram):
                 t.zero_()
         self.forward()
         self.backward()
-        return {"loss": self.loss / self.batch_size, "correct": self.correct}
+        return {"loss": ScaledScalar(self.loss, 1.0 / self.batch_size), "correct": self.correct}
 
     def evaluate(self, images, labels) -> float:
         raise NotImplementedError("training-mode BN only; no evaluation step in this example")

@@ -10,7 +10,7 @@ import torch
 
 from .. import ops
 from ..optim import OptimizerConfig, VarSpec
-from .base import ModelDef, StepProgram, zeros_init
+from .base import ModelDef, ScaledScalar, StepProgram, zeros_init
 
 IMG, NC = 784, 10
 
@@ -60,7 +60,7 @@ class SoftmaxProgram(StepProgram):
                          correct=self.correct)
         ops.gemm(self.x, self.dlogits, self.gW, M=IMG + 1, N=NC, K=B, amode=ops.RMAJ, lda=IMG, bmode=ops.RMAJ,
                  ldb=NC, a_ones_row=IMG, bias_out=self.gb)
-        return {"loss": self.loss / B}
+        return {"loss": ScaledScalar(self.loss, 1.0 / B)}
 
     def evaluate(self, images, labels) -> float:
         n = images.shape[0]

@@ -29,6 +29,7 @@ from . import ckpt
 from .data import cifar, imagenet_synth
 from .data.mnist import DeviceBatcher, read_data_sets as read_mnist
 from .models.autoencoder import AutoencoderModel
+from .models.base import ScaledScalar
 from .models.gan import LR as GAN_LR, GanModel
 from .models.lstm import LR as LSTM_LR, LstmModel
 from .models.mnist_cnn import MnistCnnModel
@@ -101,7 +102,7 @@ def scalar_metrics(metrics) -> dict:
     floats - the loss values written to the events file and the --metrics_jsonl stream."""
     out = {}
     for k, v in (metrics or {}).items():
-        if torch.is_tensor(v) and v.numel() == 1 and v.is_floating_point():
+        if isinstance(v, ScaledScalar) or (torch.is_tensor(v) and v.numel() == 1 and v.is_floating_point()):
             out[k] = float(v.item())
     return out
 
