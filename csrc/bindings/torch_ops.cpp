@@ -230,7 +230,9 @@ void conv1_gather_fwd(const Tensor& images, const Tensor& labels_src, int64_t se
   TORCH_CHECK(w.numel() == 32 * 25 && y.numel() == (int64_t)a.B * 14 * 14 * 32 && argmax.numel() == y.numel(),
               "conv1_gather_fwd: MNIST conv1 shapes");
   a.g_src = images.data_ptr<uint8_t>(); a.g_rows = images.size(0); a.g_seed = (uint64_t)seed;
-  a.g_counter = counter.data_ptr<int64_t>(); a.g_done = reinterpret_cast<uint32_t*>(done.data_ptr());
+  // an empty `done` leaves the counter alone (the caller advances it later in the step)
+  a.g_counter = counter.data_ptr<int64_t>();
+  a.g_done = done.numel() ? reinterpret_cast<uint32_t*>(done.data_ptr()) : nullptr;
   a.g_labels_src = labels_src.data_ptr<int32_t>(); a.g_labels_dst = labels_dst.data_ptr<int32_t>();
   TORCH_CHECK(zero.size() <= 4, "conv1_gather_fwd: at most 4 zero ranges");
   for (const Tensor& z : zero) {
@@ -285,7 +287,7 @@ void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optio
 // ------------------------------------------------------------------- head
 void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, const Tensor& labels, const Tensor& dz,
                const Tensor& dl, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
-               const optional<Tensor>& logits, double scale, double inv_keep) {
+               const optional<Tensor>& logits, double scale, double inv_keep, const optional<Tensor>& step_counter) {
   check_cuda(h, "h");
   TORCH_CHECK(dl.scalar_type() == at::kBFloat16 && dl.dim() == 2, "head_xent: dl must be bf16 [B][ld]");
   dtfe::HeadArgs a{};
@@ -300,6 +302,10 @@ void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, cons
   a.dl = reinterpret_cast<dtfe::bf16*>(dl.data_ptr()); a.ld_dl = (int)dl.size(1);
   a.loss_sum = ptr_or_null<float>(loss_sum); a.correct = ptr_or_null<int32_t>(correct);
   a.logits_out = ptr_or_null<float>(logits);
+  if (step_counter.has_value() && step_counter->defined()) {
+    TORCH_CHECK(step_counter->scalar_type() == at::kLong && step_counter->is_cuda(), "head_xent: int64 step_counter");
+    a.step_counter = step_counter->data_ptr<int64_t>();
+  }
   dtfe::launch_head_xent(a, cur_stream());
 }
 
@@ -695,7 +701,8 @@ TORCH_LIBRARY(dtfe, m) {
       " int OW, int KH, int KW, int stride, int pad, float scale) -> ()");
   m.def(
       "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl,"
-      " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep) -> ()");
+      " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep,"
+      " Tensor(f!)? step_counter=None) -> ()");
   m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
   m.def(
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"

@@ -103,7 +103,9 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
 
 void launch_gather_rows(const GatherArgs& a, hipStream_t s) {
   long blocks = (a.D % 8) == 0 ? ((long)a.B * (a.D / 8) + 255) / 256 : (a.B + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
+  // the step counter's last-arriver ticket is one same-address atomic per workgroup (~88 per us
+  // on one word): with a counter to advance, stay at one workgroup per CU
+  if (blocks > (a.done ? 256 : 2048)) blocks = a.done ? 256 : 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(256) void uniform_fill_kernel(float* out, long n, f
 void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, int64_t* counter, uint32_t* done,
                          hipStream_t s) {
   long blocks = (n + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > (done ? 256 : 1024)) blocks = done ? 256 : 1024;  // see launch_gather_rows
   hipLaunchKernelGGL(uniform_fill_kernel, dim3(blocks), dim3(256), 0, s, out, n, lo, hi, seed, counter, done);
 }
 

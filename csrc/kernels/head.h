@@ -12,6 +12,10 @@ struct HeadArgs {
   bf16* dz;           // [B][K]
   bf16* dl; int ld_dl;  // d(loss)/d(logit) rows, bf16 [B][ld_dl]
   float* loss_sum; int32_t* correct; float* logits_out;
+  // optional: advanced by one (one thread of workgroup 0) - the per-step sampling / dropout
+  // counter of the fused MNIST step, whose readers (the conv1 gather, fc1 dropout) all run
+  // before this kernel: one plain increment instead of a grid-wide last-arriver atomic
+  int64_t* step_counter;
 };
 
 void launch_head_xent(const HeadArgs& a, hipStream_t s);

@@ -30,6 +30,7 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __shared__ float red_loss[4];
   __shared__ int red_correct[4];
+  if (a.step_counter && blockIdx.x == 0 && threadIdx.x == 0) *a.step_counter += 1;
   const int row = min(blockIdx.x * 4 + wid, a.B - 1);  // a surplus wave recomputes the last row, unstored
   const bool live = blockIdx.x * 4 + wid < a.B;
   u32x4_t wv[NC][E / 8], hv[E / 8];

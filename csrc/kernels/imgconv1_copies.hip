@@ -86,7 +86,7 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
   // fused batch sampling (a.g_src): the sampled uint8 row is converted here and the bf16
   // image written out for the weight gradient - no separate gather launch per step
   const int64_t gstep = a.g_src ? *a.g_counter : 0;
-  for (int z = 0; z < a.nz; ++z)
+  for (int z = 0; z < ((a.diag & 8) ? 0 : a.nz); ++z)
     for (long i = (long)blockIdx.x * TH + threadIdx.x; i < a.zlen[z]; i += (long)gridDim.x * TH) a.zptr[z][i] = 0u;
   auto load = [&](long bb, u32x2_t& v) {
     if (!a.g_src) {
@@ -111,10 +111,10 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
     write_img(P, xv);
     __syncthreads();
     if (b + gridDim.x < a.B) load(b + gridDim.x, xv);
-    build_copies<8>(P, C);
+    if (!(a.diag & 2)) build_copies<8>(P, C);
     __syncthreads();
     // 49 tiles of 16 output pixels in 2x2-window order (4 windows per tile)
-    for (int t = wid; t < 49; t += 4) {
+    for (int t = wid; t < ((a.diag & 4) ? 0 : 49); t += 4) {
       const int m = t * 16 + (lane & 15), q = m & 3, w = m >> 2;
       const int oy = 2 * (w / 14) + (q >> 1), ox = 2 * (w % 14) + (q & 1);
       const int s = ox & 7;
@@ -139,6 +139,7 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
 #pragma unroll
         for (int j = 1; j < 4; ++j) if (v[j] > mx) { mx = v[j]; am = j; }
         const long o = ((b * 14 + py) * 14 + px) * NCH + nt * 16 + (lane & 15);
+        if (a.diag & 1) continue;
         a.y[o] = f2bf(apply_act(mx + biasv[nt], a.act));
         if (a.argmax) a.argmax[o] = (uint8_t)am;
       }
@@ -301,7 +302,13 @@ bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s) {
   if (!mnist_conv1_shape(a.B, a.SH, a.SW, a.CS, a.OH, a.OW, a.N, a.KH, a.KW, a.stride, a.pad)) return false;
   if (!a.src || !a.pool || a.flip_taps || a.dil > 1 || a.relu_mask) return false;
   const int grid = a.B < 1024 ? a.B : 1024;
-  hipLaunchKernelGGL(conv1c_fwd_kernel, dim3(grid), dim3(TH), 0, s, a);
+  static const int diag = [] {
+    const char* e = getenv("DTFE_C1_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  ImgConvArgs ad = a;
+  ad.diag = diag;
+  hipLaunchKernelGGL(conv1c_fwd_kernel, dim3(grid), dim3(TH), 0, s, ad);
   return true;
 }
 

@@ -170,6 +170,7 @@ class MnistCnnTrainer:
         self.correct = torch.zeros(1, dtype=torch.int32, device=d)
         self.data_ctr = torch.zeros(1, dtype=torch.int64, device=d)
         self.data_done = torch.zeros(1, dtype=torch.int32, device=d)
+        self.no_done = torch.zeros(0, dtype=torch.int32, device=d)
         self.g1 = dict(B=B, H=IMG, W=IMG, C=1, Cout=C1, OH=IMG, OW=IMG, KH=KS, KW=KS, stride=1, pad=2)
         self.g2 = dict(B=B, H=14, W=14, C=C1, Cout=C2, OH=14, OW=14, KH=KS, KW=KS, stride=1, pad=2)
         # whole-image LDS conv geometry: conv1 (1-channel tap-packed kernels), conv2 (forward /
@@ -250,11 +251,15 @@ class MnistCnnTrainer:
     # ------------------------------------------------------------------
     def forward_backward(self):
         B = self.B
+        fused = False
         if self.data is not None and self.device.type == "cuda" and B >= 256 and self.fused_gather:
             # standalone: batch sampling (advances data_ctr), accumulator clearing and conv1 in ONE launch
+            # (the sampling counter is advanced by head_xent, after its last reader: fc1's dropout -
+            # a grid-wide last-arriver atomic here serialised ~10 us of the launch)
             ops.require().conv1_gather_fwd(self.data.images, self.data.labels, self.seed + 1, self.data_ctr,
-                                           self.data_done, self.labels, self.x, self.w["wc1"], self.b["bc1"],
+                                           self.no_done, self.labels, self.x, self.w["wc1"], self.b["bc1"],
                                            self.p1, self.a1, self.accum)
+            fused = True
         else:
             if self.data is not None:  # sample the batch on device (advances data_ctr) and clear
                 ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
@@ -270,7 +275,8 @@ class MnistCnnTrainer:
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
                  keep=self.keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd)
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
-                      self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep)
+                      self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep,
+                      step_counter=self.data_ctr if fused else None)
         main = torch.cuda.current_stream(self.device) if self.par else None
         if self.br_one:
             self._backward_one_branch(main)

@@ -452,12 +452,15 @@ def conv_wgrad(dz, x, dw, db, g, scale=1.0):
 
 
 # -------------------------------------------------------------------- head
-def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0):
+def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0, step_counter=None):
     """Per-row classifier head: logits, softmax-xent (loss/correct sums), dlogit rows (bf16 [B][ld] into
-    ``dl``) and dZ = (dlogit . W) * inv_keep * (h > 0).  dW/db come from a wgrad GEMM over ``dl``."""
+    ``dl``) and dZ = (dlogit . W) * inv_keep * (h > 0).  dW/db come from a wgrad GEMM over ``dl``.
+    ``step_counter`` (int64 [1], optional) is advanced by one."""
     if h.is_cuda:
-        require().head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits, scale, inv_keep)
+        require().head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits, scale, inv_keep, step_counter)
         return
+    if step_counter is not None:
+        step_counter += 1
     hf, wf = h.float(), w.float()
     lg = hf @ wf.t() + (b.float() if b is not None else 0)
     if logits is not None:
