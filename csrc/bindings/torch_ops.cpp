@@ -134,9 +134,11 @@ void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, co
 
 void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B, int64_t H, int64_t W, int64_t C,
                 int64_t Cout, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                const optional<Tensor>& pooled, const optional<Tensor>& argmax, const optional<Tensor>& relu_mask) {
+                const optional<Tensor>& pooled, const optional<Tensor>& argmax, const optional<Tensor>& relu_mask,
+                bool accumulate) {
   check_cuda(dy, "dy");
   dtfe::ConvDgradArgs a{};
+  a.accumulate = accumulate ? 1 : 0;
   a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
   a.wt = reinterpret_cast<const dtfe::bf16*>(wt.data_ptr());
@@ -685,7 +687,7 @@ TORCH_LIBRARY(dtfe, m) {
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");
   m.def(
       "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
-      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask) -> ()");
+      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask, bool accumulate=False) -> ()");
   m.def("conv1_fwd_pool(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!) argmax) -> ()");
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"

@@ -48,6 +48,7 @@ struct ConvDgradArgs {
   const bf16* dy; const bf16* wt;   // wt: [C][KH][KW][Cout]
   bf16* dx; int unpool; UnpoolArgs up;
   const bf16* relu_mask;            // optional: dx = mask > 0 ? dx : 0 (ReLU' of a pooled output)
+  int accumulate;                   // dx += dgrad (implicit-GEMM path only)
 };
 struct ConvWgradArgs {
   ConvGeom g;

@@ -388,6 +388,7 @@ void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
 
 void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s) {
   if (launch_igemm_dgrad(a, s)) return;
+  if (a.accumulate) throw std::runtime_error("conv_dgrad: accumulate needs the implicit-GEMM path (C, Cout % 64 == 0)");
   const ConvGeom& g = a.g;
   launch_skinny<DgradK>(a, g.B * g.H * g.W, g.C, s);
 }

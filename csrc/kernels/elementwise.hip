@@ -103,9 +103,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
 
 void launch_gather_rows(const GatherArgs& a, hipStream_t s) {
   long blocks = (a.D % 8) == 0 ? ((long)a.B * (a.D / 8) + 255) / 256 : (a.B + 3) / 4;
-  // the step counter's last-arriver ticket is one same-address atomic per workgroup (~88 per us
-  // on one word): with a counter to advance, stay at one workgroup per CU
-  if (blocks > (a.done ? 256 : 2048)) blocks = a.done ? 256 : 2048;
+  if (blocks > 2048) blocks = 2048;  // (its tail of counter tickets overlaps the grid's drain)
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, s, a);
 }

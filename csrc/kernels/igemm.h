@@ -33,6 +33,7 @@ struct IgemmArgs {
   int N, Ktot;            // output channels; weight row length = taps * SC
   int istr, OHf, OWf, ostr;
   int nphase, splits, tiles_m;
+  int accum;              // out += result (bf16 read-modify-write in the epilogue)
   IgPhase ph[4];
 };
 

@@ -173,9 +173,14 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
         Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
   __syncthreads();
   constexpr int CPR = BN / 8;
-  for (int q = tid; q < BM * CPR; q += IG_THREADS) {
-    const int r = q / CPR, c8 = q - r * CPR;
+  constexpr int PER = BM * CPR / IG_THREADS;  // 16-B chunks per thread
+  static_assert(PER * IG_THREADS == BM * CPR, "whole chunks per thread");
+  bf16* dst[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
     const int m = m_base + r;
+    dst[j] = nullptr;
     if (m >= Mp) continue;
     long opix = m;
     if (a.nphase > 1) {
@@ -183,18 +188,43 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
       const int i = t % P.RH, b = t / P.RH;
       opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
     }
-    *reinterpret_cast<u32x4_t*>(a.out + opix * a.N + n_base + c8 * 8) =
-        *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c8 * 8);
+    dst[j] = a.out + opix * a.N + n_base + c8 * 8;
+  }
+  u32x4_t old[PER];
+  if (a.accum) {  // e.g. a block's input gradient: the shortcut branch's share is already there;
+                  // every load is issued before the first add (no per-chunk latency chain)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (!dst[j]) continue;
+    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
+    u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c8 * 8);
+    if (a.accum) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f((bf16)(v[e] & 0xffffu)) + bf2f((bf16)(old[j][e] & 0xffffu));
+        const float hi = bf2f((bf16)(v[e] >> 16)) + bf2f((bf16)(old[j][e] >> 16));
+        v[e] = pack_bf16x2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4_t*>(dst[j]) = v;
   }
 }
 
-// out[i] = bf16(sum_s ws[s][i])
+// out[i] = bf16(sum_s ws[s][i])   (accum: out[i] = bf16(out[i] + sum_s ws[s][i]))
 __global__ __launch_bounds__(256) void splitk_to_bf16_kernel(const float* __restrict__ ws, int splits, long len,
-                                                             bf16* __restrict__ out) {
+                                                             bf16* __restrict__ out, int accum) {
   const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= len) return;
   f32x4_t v = *reinterpret_cast<const f32x4_t*>(ws + i);
   for (int s = 1; s < splits; ++s) v += *reinterpret_cast<const f32x4_t*>(ws + (long)s * len + i);
+  if (accum) {
+    const u32x2_t o = *reinterpret_cast<const u32x2_t*>(out + i);
+    v[0] += bf2f((bf16)(o[0] & 0xffffu)); v[1] += bf2f((bf16)(o[0] >> 16));
+    v[2] += bf2f((bf16)(o[1] & 0xffffu)); v[3] += bf2f((bf16)(o[1] >> 16));
+  }
   u32x2_t o = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
   *reinterpret_cast<u32x2_t*>(out + i) = o;
 }
@@ -462,7 +492,7 @@ void run_igemm(IgemmArgs& a, hipStream_t s) {
   if (a.splits > 1) {
     const long len = Mmax * a.N;
     hipLaunchKernelGGL(splitk_to_bf16_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws,
-                       a.splits, len, a.out);
+                       a.splits, len, a.out, a.accum);
   }
 }
 
@@ -501,6 +531,7 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
   a.B = g.B; a.SH = g.OH; a.SW = g.OW; a.SC = g.Cout;
   a.N = g.C; a.Ktot = g.KH * g.KW * g.Cout;
   a.istr = 1; a.OHf = g.H; a.OWf = g.W; a.ostr = g.stride;
+  a.accum = d.accumulate;
   const int st = g.stride;
   a.nphase = st * st;
   for (int py = 0; py < st; ++py)

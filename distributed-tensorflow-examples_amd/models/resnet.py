@@ -35,6 +35,7 @@ contract).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -43,6 +44,9 @@ from ..optim import OptimizerConfig, VarSpec
 from .base import ModelDef, ScaledScalar, StepProgram
 
 BN_EPS, BN_MOMENTUM = 1e-3, 0.99
+# bottleneck input gradient: shortcut share written into dx, conv1's data gradient accumulated on
+# top (DTFE_R50_SHORTCUT_FUSE=0: separate buffer + add pass, for A/B)
+_SHORTCUT_FUSE = os.environ.get("DTFE_R50_SHORTCUT_FUSE", "1") != "0"
 # activation / activation-gradient storage dtype: bf16 on the GPU kernels; the CPU reference
 # path also runs with fp32 storage (exactness tests of the program logic)
 ACT_DTYPE = torch.bfloat16
@@ -122,6 +126,9 @@ class Conv:
         self.img_dgrad = (self.dil > 0 and (self.stride == 1 or B >= 64) and self.cout % 8 == 0 and self.cin <= 64
                           and (self.H + self.k - 1) * (self.W + self.k - 1) * self.cout * 2 <= 150 * 1024)
         self.img_wgrad = (self.cin % 8 == 0 or few) and self.cout <= 64 and self.OW <= 32 and self.cout % 8 == 0
+        # the implicit-GEMM data gradient can accumulate into dx (a block's input gradient gets its
+        # shortcut share first, then the conv's on top: no separate add pass)
+        self.can_accum = not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0
 
     def fwd(self, x):
         if self.img_fwd:
@@ -136,13 +143,14 @@ class Conv:
         else:
             ops.conv_wgrad(dy, x, self.gw, None, self.g)
 
-    def dgrad(self, dy, dx):
+    def dgrad(self, dy, dx, accumulate=False):
         if self.img_dgrad:
+            assert not accumulate
             ops.imgconv(self.wt, dx, src=dy, flip_taps=True, B=self.B, SH=self.OH, SW=self.OW, CS=self.cout,
                         OH=self.H, OW=self.W, N=self.cin, KH=self.k, KW=self.k, stride=1,
                         pad=self.k - 1 - self.pad, dil=self.dil)
         else:
-            ops.conv_dgrad(dy, self.wt, dx, self.g)
+            ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate)
 
 
 class BN:
@@ -280,7 +288,11 @@ class Bottleneck:
         return self.bn3.fwd(self.conv3.fwd(h2), res=res, rstride=1)
 
     def bwd(self, dout, dx):
-        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=self.dres)
+        # shortcut gradient straight into dx, the conv1 data gradient accumulated on top
+        fuse = (dx is not None and self.conv1.can_accum and (not self.proj or self.convs.can_accum)
+                and _SHORTCUT_FUSE)
+        dres = dx if (fuse and not self.proj) else self.dres
+        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres)
         self.conv3.wgrad(self.dc3, self.bn2.y)
         self.conv3.dgrad(self.dc3, self.dh2)
         self.bn2.bwd(self.dh2, self.conv2.y, self.dc2)
@@ -292,12 +304,19 @@ class Bottleneck:
             self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
             self.convs.wgrad(self.dsc, self.x)
         if dx is not None:
-            self.conv1.dgrad(self.dc1, dx)
-            if self.proj:
-                self.convs.dgrad(self.dsc, self.dxs)
-                ops.shortcut_grad_add(self.dxs, dx, 1)
+            if fuse:
+                if self.proj:
+                    self.conv1.dgrad(self.dc1, dx)
+                    self.convs.dgrad(self.dsc, dx, accumulate=True)
+                else:
+                    self.conv1.dgrad(self.dc1, dx, accumulate=True)
             else:
-                ops.shortcut_grad_add(self.dres, dx, 1)
+                self.conv1.dgrad(self.dc1, dx)
+                if self.proj:
+                    self.convs.dgrad(self.dsc, self.dxs)
+                    ops.shortcut_grad_add(self.dxs, dx, 1)
+                else:
+                    ops.shortcut_grad_add(self.dres, dx, 1)
 
 
 class Dense:

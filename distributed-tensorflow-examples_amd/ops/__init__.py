@@ -417,11 +417,17 @@ def conv1_wgrad_pooled(x, dp, argmax, dw, db, scale=1.0):
     conv_wgrad(dz, x, dw, db, g, scale)
 
 
-def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None):
+def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None, accumulate=False):
     """dX of an NHWC conv (wt = W laid out [C][KH][KW][Cout]); optional un-pool epilogue, or a
-    ReLU mask (dx = mask > 0 ? dx : 0) when the consumer un-pools itself."""
+    ReLU mask (dx = mask > 0 ? dx : 0) when the consumer un-pools itself.  ``accumulate``:
+    dx += dX (implicit-GEMM path: C and Cout multiples of 64)."""
     if dx.is_cuda:
-        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask)
+        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask, accumulate)
+        return dx
+    if accumulate:
+        old = dx.float().clone()
+        conv_dgrad(dy, wt, dx, g, pooled, argmax, relu_mask)
+        dx.copy_((dx.float() + old).to(dx.dtype))
         return dx
     dyt = dy.float().view(g["B"], g["OH"], g["OW"], g["Cout"]).permute(0, 3, 1, 2)
     w = wt.float().view(g["C"], g["KH"], g["KW"], g["Cout"]).permute(3, 0, 1, 2)
