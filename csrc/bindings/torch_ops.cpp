@@ -118,10 +118,16 @@ dtfe::ConvGeom geom(int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, in
 
 void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
               const optional<Tensor>& argmax, int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, int64_t OH,
-              int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool pool, int64_t act) {
+              int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool pool, int64_t act,
+              const optional<Tensor>& bn_stats) {
   check_cuda(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv_fwd: bf16 only");
   dtfe::ConvFwdArgs a{};
+  if (bn_stats.has_value() && bn_stats->defined()) {
+    TORCH_CHECK(bn_stats->scalar_type() == at::kFloat && bn_stats->is_contiguous() && bn_stats->numel() >= 2 * Cout,
+                "conv_fwd: bn_stats must be f32 [2][Cout]");
+    a.bn_stats = bn_stats->data_ptr<float>();
+  }
   a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, pool);
   a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
   a.w = reinterpret_cast<const dtfe::bf16*>(w.data_ptr());
@@ -684,7 +690,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr, int a_ones_row=-1, Tensor? ones=None) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
-      " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act) -> ()");
+      " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act, Tensor(c!)? bn_stats=None) -> ()");
   m.def(
       "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
       " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask, bool accumulate=False) -> ()");

@@ -42,6 +42,7 @@ struct ConvFwdArgs {
   ConvGeom g;
   const bf16* x; const bf16* w; const float* bias;
   bf16* y; uint8_t* argmax; int act;
+  float* bn_stats;   // optional [2][Cout] (zeroed): BatchNorm statistics of y, as bn_stats computes them
 };
 struct ConvDgradArgs {
   ConvGeom g;

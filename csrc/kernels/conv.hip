@@ -16,6 +16,7 @@
 // (BASELINE.json configs 2-5).
 #include "gemm_core.h"
 #include "conv.h"
+#include "norm.h"
 #include "igemm.h"
 #include <stdexcept>
 
@@ -378,12 +379,32 @@ static void launch_skinny(const ARGS& a, int M, int N, hipStream_t s) {
 template <typename Cfg> struct FwdK { static constexpr auto fn = conv_fwd_kernel<Cfg>; };
 template <typename Cfg> struct DgradK { static constexpr auto fn = conv_dgrad_kernel<Cfg>; };
 
+// BatchNorm statistics of a conv output by the separate pass (paths without fused partials)
+static void bn_stats_of(const ConvFwdArgs& a, hipStream_t s) {
+  if (!a.bn_stats) return;
+  if (a.g.pool_order) throw std::runtime_error("conv_fwd: bn_stats with a fused pool");
+  BnArgs b{};
+  b.R = (long)a.g.B * a.g.OH * a.g.OW;
+  b.C = a.g.Cout;
+  b.x = a.y;
+  b.stats = a.bn_stats;
+  launch_bn_stats(b, s);
+}
+
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
-  if (launch_stem_fwd(a, s)) return;   // ImageNet 7x7/2 stem
-  if (launch_igemm_fwd(a, s)) return;  // wide layers: DMA-staged 64-deep k-tiles  // wide layers: DMA-staged 64-deep k-tiles
+  if (launch_stem_fwd(a, s)) {  // ImageNet 7x7/2 stem
+    bn_stats_of(a, s);
+    return;
+  }
+  bool fused = false;
+  if (launch_igemm_fwd(a, s, &fused)) {  // wide layers: DMA-staged 64-deep k-tiles (+ BN partials)
+    if (!fused) bn_stats_of(a, s);
+    return;
+  }
   const ConvGeom& g = a.g;
   if (g.pool_order && ((g.OH | g.OW) & 1)) throw std::runtime_error("conv_fwd: pool needs even output dims");
   launch_skinny<FwdK>(a, g.B * g.OH * g.OW, g.Cout, s);
+  bn_stats_of(a, s);
 }
 
 void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s) {

@@ -34,6 +34,9 @@ struct IgemmArgs {
   int istr, OHf, OWf, ostr;
   int nphase, splits, tiles_m;
   int accum;              // out += result (bf16 read-modify-write in the epilogue)
+  // forward only: per output tile and channel the BatchNorm partials of the stored (bf16) output,
+  // [tiles_m][3][N] = (K_t = the tile's first row, sum (y - K_t), sum (y - K_t)^2)
+  float* bn_part;
   IgPhase ph[4];
 };
 
@@ -44,7 +47,8 @@ struct IgWgradArgs {
 };
 
 // true when the igemm path handles the conv (and launches it)
-bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s);
+// stats_done (optional): set when f.bn_stats was produced by the fused epilogue partials
+bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nullptr);
 bool launch_igemm_dgrad(const ConvDgradArgs& a, hipStream_t s);
 bool launch_igemm_wgrad(const ConvWgradArgs& a, hipStream_t s);
 

@@ -172,6 +172,48 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
       for (int q = 0; q < 4; ++q)
         Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
   __syncthreads();
+  if (a.bn_part) {
+    // BatchNorm statistics of this tile's stored values (replaces a separate pass over y):
+    // thread = (8-channel chunk, row group); sums around the tile's first row, then the row
+    // groups in order through the LDS past the C tile (deterministic)
+    constexpr int CH = BN / 8, RG = IG_THREADS / CH;
+    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= 2 * (A_EL + B_EL) * 2, "stats scratch fits");
+    float* red = reinterpret_cast<float*>(smem + BM * CLD);
+    const int ch = tid % CH, rg = tid / CH, rows = min(BM, Mp - m_base);
+    float k[8], sm[8] = {}, sq[8] = {};
+    const u32x4_t kv = *reinterpret_cast<const u32x4_t*>(Cs + ch * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      k[2 * e] = bf2f((bf16)(kv[e] & 0xffffu));
+      k[2 * e + 1] = bf2f((bf16)(kv[e] >> 16));
+    }
+    for (int r = rg; r < rows; r += RG) {
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + ch * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d0 = bf2f((bf16)(v[e] & 0xffffu)) - k[2 * e], d1 = bf2f((bf16)(v[e] >> 16)) - k[2 * e + 1];
+        sm[2 * e] += d0; sq[2 * e] += d0 * d0;
+        sm[2 * e + 1] += d1; sq[2 * e + 1] += d1 * d1;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 2) * BN + ch * 8 + e] = sm[e];
+      red[(rg * 2 + 1) * BN + ch * 8 + e] = sq[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += IG_THREADS) {
+      float S = 0.f, Q = 0.f;
+      for (int g2 = 0; g2 < RG; ++g2) {
+        S += red[(g2 * 2) * BN + c];
+        Q += red[(g2 * 2 + 1) * BN + c];
+      }
+      float* pp = a.bn_part + (long)tm * 3 * a.N + n_base + c;
+      pp[0] = bf2f(Cs[c]);
+      pp[a.N] = S;
+      pp[2 * a.N] = Q;
+    }
+  }
   constexpr int CPR = BN / 8;
   constexpr int PER = BM * CPR / IG_THREADS;  // 16-B chunks per thread
   static_assert(PER * IG_THREADS == BM * CPR, "whole chunks per thread");
@@ -387,6 +429,93 @@ __global__ __launch_bounds__(256) void wgrad_splits_reduce_kernel(const float* _
   *reinterpret_cast<f32x4_t*>(dw + i) = d + scale * acc;
 }
 
+// ------------------------------------------------- BatchNorm partial-statistics reduction
+// Tile t carries (K_t, s_t = sum (y - K_t), q_t = sum (y - K_t)^2) over its n_t rows; moving to
+// another shift K:  s = s_t + n_t d,  q = q_t + 2 d s_t + n_t d^2  with d = K_t - K.  Stage 1 folds
+// chunks of BN_TCH tiles onto the chunk's first K, stage 2 folds the chunks onto row 0's value
+// (the shift bn_apply reads back from y) and adds (sum, sumsq) into stats[2][N].  Fixed order.
+constexpr int BN_TCH = 64;
+
+__device__ __forceinline__ void shift_fold(float Kt, float st, float qt, float nt, float K, float& S, float& Q) {
+  const float d = Kt - K;
+  S += st + nt * d;
+  Q += qt + 2.f * d * st + nt * d * d;
+}
+
+// part [tiles][3][N] -> chunk [P][3][N] (+ rows per chunk implied); grid (ceil(N/64), P)
+__global__ __launch_bounds__(256) void bn_part_stage1(const float* __restrict__ part, int tiles, int N, long Mp,
+                                                      int BMr, float* __restrict__ chunk) {
+  __shared__ float red[4][2][64];
+  const int cl = threadIdx.x & 63, ln = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, p = blockIdx.y;
+  const int t0 = p * BN_TCH, t1 = min(tiles, t0 + BN_TCH);
+  float S = 0.f, Q = 0.f, K = 0.f;
+  if (c < N) {
+    K = part[(long)t0 * 3 * N + c];
+    // all of this lane's tiles (<= BN_TCH / 4) loaded before the first fold: one latency, not 16
+    constexpr int PT = BN_TCH / 4;
+    float kt[PT], st[PT], qt[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int t = t0 + ln + 4 * i;
+      const float* pt = part + (long)(t < t1 ? t : t0) * 3 * N + c;
+      kt[i] = pt[0];
+      st[i] = pt[N];
+      qt[i] = pt[2 * N];
+    }
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int t = t0 + ln + 4 * i;
+      if (t < t1) shift_fold(kt[i], st[i], qt[i], (float)min((long)BMr, Mp - (long)t * BMr), K, S, Q);
+    }
+  }
+  red[ln][0][cl] = S;
+  red[ln][1][cl] = Q;
+  __syncthreads();
+  if (ln == 0 && c < N) {
+    S = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
+    Q = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+    float* o = chunk + (long)p * 3 * N + c;
+    o[0] = K;
+    o[N] = S;
+    o[2 * N] = Q;
+  }
+}
+
+// chunk [P][3][N] -> stats[c] += S, stats[N + c] += Q around chunk 0's K; grid ceil(N/64)
+__global__ __launch_bounds__(256) void bn_part_stage2(const float* __restrict__ chunk, int P, int N, long Mp, int BMr,
+                                                      float* __restrict__ stats) {
+  __shared__ float red[4][2][64];
+  const int cl = threadIdx.x & 63, ln = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  float S = 0.f, Q = 0.f;
+  if (c < N) {
+    const float K = chunk[c];
+    const long rows_chunk = (long)BN_TCH * BMr;
+    for (int p0 = ln; p0 < P; p0 += 4 * 8) {  // 8 chunks per lane in flight
+      float kp[8], sp[8], qp[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = p0 + 4 * i;
+        const float* pc = chunk + (long)(p < P ? p : 0) * 3 * N + c;
+        kp[i] = pc[0];
+        sp[i] = pc[N];
+        qp[i] = pc[2 * N];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = p0 + 4 * i;
+        if (p < P) shift_fold(kp[i], sp[i], qp[i], (float)min(rows_chunk, Mp - (long)p * rows_chunk), K, S, Q);
+      }
+    }
+  }
+  red[ln][0][cl] = S;
+  red[ln][1][cl] = Q;
+  __syncthreads();
+  if (ln == 0 && c < N) {
+    stats[c] += ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
+    stats[N + c] += ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+  }
+}
+
 // ------------------------------------------------------------ host helpers
 struct DevScratch {
   void* zeros = nullptr;
@@ -432,6 +561,29 @@ float* workspace(size_t bytes, hipStream_t s) {
   return reinterpret_cast<float*>(d.ws);
 }
 
+DevScratch g_bn[64];
+
+float* bn_workspace(size_t bytes, hipStream_t s) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_mu);
+  DevScratch& d = g_bn[dev];
+  if (d.ws_bytes < bytes) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &st);
+    if (st != hipStreamCaptureStatusNone)
+      throw std::runtime_error("igemm: BN partial workspace growth inside a graph capture (run the step eagerly first)");
+    if (d.ws) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(d.ws);
+    }
+    const size_t nb = std::max(bytes, d.ws_bytes * 3 / 2);
+    if (hipMalloc(&d.ws, nb) != hipSuccess) throw std::runtime_error("igemm: BN partial workspace alloc");
+    d.ws_bytes = nb;
+  }
+  return reinterpret_cast<float*>(d.ws);
+}
+
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
@@ -463,7 +615,8 @@ void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
   hipLaunchKernelGGL((igemm_kernel<BM, BN>), grid, dim3(IG_THREADS), 0, s, a);
 }
 
-void run_igemm(IgemmArgs& a, hipStream_t s) {
+// returns true when BatchNorm statistics into bn_stats were produced (fused epilogue partials)
+bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
   long Mmax = 0;
   for (int p = 0; p < a.nphase; ++p) Mmax = std::max(Mmax, (long)a.B * a.ph[p].RH * a.ph[p].RW);
   Tile t = pick_tile(Mmax, a.N, a.nphase);
@@ -485,6 +638,10 @@ void run_igemm(IgemmArgs& a, hipStream_t s) {
       a.ws = workspace((size_t)sp * Mmax * a.N * sizeof(float), s);
     }
   }
+  const bool fuse_bn = bn_stats && a.splits == 1 && a.nphase == 1 && !a.accum;
+  const int tiles_m = (int)((Mmax + t.bm - 1) / t.bm), nchunk = (tiles_m + BN_TCH - 1) / BN_TCH;
+  a.bn_part = nullptr;
+  if (fuse_bn) a.bn_part = bn_workspace(((size_t)tiles_m + nchunk) * 3 * a.N * sizeof(float), s);
   if (t.bm == 128 && t.bn == 128) launch_ig<128, 128>(a, Mmax, s);
   else if (t.bm == 128 && t.bn == 64) launch_ig<128, 64>(a, Mmax, s);
   else if (t.bm == 64 && t.bn == 128) launch_ig<64, 128>(a, Mmax, s);
@@ -494,11 +651,17 @@ void run_igemm(IgemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(splitk_to_bf16_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws,
                        a.splits, len, a.out, a.accum);
   }
+  if (!fuse_bn) return false;
+  float* chunk = a.bn_part + (size_t)tiles_m * 3 * a.N;
+  const unsigned cg = (unsigned)((a.N + 63) / 64);
+  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_m, a.N, Mmax, t.bm, chunk);
+  hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, a.N, Mmax, t.bm, bn_stats);
+  return true;
 }
 
 }  // namespace
 
-bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s) {
+bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
   const ConvGeom& g = f.g;
   if (g.C % IG_BK || g.Cout % 64 || g.KH * g.KW > IG_MAX_TAPS || g.pool_order || f.bias || f.act != 0) return false;
   if (env_int("DTFE_IG_OFF", 0)) return false;
@@ -517,7 +680,8 @@ bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s) {
       const int t = kh * g.KW + kw;
       P.dy[t] = kh - g.pad; P.dx[t] = kw - g.pad; P.kt[t] = t;
     }
-  run_igemm(a, s);
+  const bool st = run_igemm(a, s, f.bn_stats);
+  if (stats_done) *stats_done = st;
   return true;
 }
 

@@ -130,12 +130,14 @@ class Conv:
         # shortcut share first, then the conv's on top: no separate add pass)
         self.can_accum = not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0
 
-    def fwd(self, x):
+    def fwd(self, x, stats=None):
+        """Forward; ``stats``: the following BatchNorm's [2][C] accumulators, filled by the conv
+        launch itself where it can (returns True then; the BN skips its statistics pass)."""
         if self.img_fwd:
             ops.imgconv(self.w, self.y, src=x, **self.ic)
-        else:
-            ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE)
-        return self.y
+            return self.y, False
+        ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats)
+        return self.y, stats is not None
 
     def wgrad(self, dy, x):
         if self.img_wgrad:
@@ -169,10 +171,13 @@ class BN:
             arena.take(self.C), arena.take(self.C)
 
     def fwd(self, x, act=ops.ACT_RELU, res=None, rstride=1):
+        """``x``: the conv output, or (conv output, statistics already accumulated by the conv)."""
         P = self.P
+        x, have_stats = x if isinstance(x, tuple) else (x, False)
         # backward recomputes the ReLU mask from x unless a shortcut was added before the ReLU
         self.mask_from_x = act == ops.ACT_RELU and res is None
-        ops.bn_stats(x, self.stats)
+        if not have_stats:
+            ops.bn_stats(x, self.stats)
         ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
                      invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
                      momentum=BN_MOMENTUM, act=act, res=res, rstride=rstride)
@@ -224,10 +229,8 @@ class BasicBlock:
 
     def fwd(self, x):
         self.x = x
-        c1 = self.conv1.fwd(x)
-        h1 = self.bn1.fwd(c1)
-        c2 = self.conv2.fwd(h1)
-        return self.bn2.fwd(c2, res=x, rstride=self.stride)
+        h1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats))
+        return self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats), res=x, rstride=self.stride)
 
     def bwd(self, dout, dx):
         self.bn2.bwd(dout, self.conv2.y, self.dc2, dres=self.dres)
@@ -282,10 +285,10 @@ class Bottleneck:
         self.x = x
         res = x
         if self.proj:
-            res = self.bns.fwd(self.convs.fwd(x), act=ops.ACT_NONE)
-        h1 = self.bn1.fwd(self.conv1.fwd(x))
-        h2 = self.bn2.fwd(self.conv2.fwd(h1))
-        return self.bn3.fwd(self.conv3.fwd(h2), res=res, rstride=1)
+            res = self.bns.fwd(self.convs.fwd(x, self.bns.stats), act=ops.ACT_NONE)
+        h1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats))
+        h2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats))
+        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats), res=res, rstride=1)
 
     def bwd(self, dout, dx):
         # shortcut gradient straight into dx, the conv1 data gradient accumulated on top
@@ -476,7 +479,7 @@ class ResNetProgram(StepProgram):
 
     def forward(self):
         L = self.L
-        h = L["stem_bn"].fwd(L["stem"].fwd(self.x))
+        h = L["stem_bn"].fwd(L["stem"].fwd(self.x, L["stem_bn"].stats))
         if "pool_hw" in L:
             ops.maxpool3_fwd(h, self.pool, self.pool_am)
             h = self.pool

@@ -279,10 +279,16 @@ def _conv_geom_args(g):
     return (g["B"], g["H"], g["W"], g["C"], g["Cout"], g["OH"], g["OW"], g["KH"], g["KW"], g["stride"], g["pad"])
 
 
-def conv_fwd(x, w, bias, y, argmax, g, pool=False, act=ACT_RELU):
-    """NHWC conv (+bias, act, optional fused 2x2 max-pool writing argmax)."""
+def conv_fwd(x, w, bias, y, argmax, g, pool=False, act=ACT_RELU, stats=None):
+    """NHWC conv (+bias, act, optional fused 2x2 max-pool writing argmax).  ``stats`` (f32 [2][Cout],
+    zeroed): also accumulate the BatchNorm statistics of y exactly as ``bn_stats`` does (the
+    implicit-GEMM path computes them from its epilogue tiles: no separate pass over y)."""
     if y.is_cuda:
-        require().conv_fwd(x, w, bias, y, argmax, *_conv_geom_args(g), pool, act)
+        require().conv_fwd(x, w, bias, y, argmax, *_conv_geom_args(g), pool, act, stats)
+        return y
+    if stats is not None:
+        conv_fwd(x, w, bias, y, argmax, g, pool, act)
+        bn_stats(y, stats)
         return y
     xt = x.float().view(g["B"], g["H"], g["W"], g["C"]).permute(0, 3, 1, 2)
     wt = w.float().view(g["Cout"], g["KH"], g["KW"], g["C"]).permute(0, 3, 1, 2)

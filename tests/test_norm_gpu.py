@@ -90,3 +90,30 @@ def test_maxpool3():
     assert torch.equal(ys[0], ys[1])
     assert (ams[0] == ams[1]).float().mean() > 0.999
     assert _rel(dxs[1], dxs[0]) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,C,Cout,k", [(3, 14, 64, 128, 3), (64, 56, 64, 64, 1), (16, 28, 128, 256, 3)])
+def test_conv_fwd_fused_bn_stats_match_separate_pass(B, H, C, Cout, k):
+    """The implicit-GEMM forward's epilogue BatchNorm partials (per tile, two-stage fixed-order
+    reduction) give the statistics the separate bn_stats pass computes from the stored output."""
+    from dtfe import ops
+
+    torch.manual_seed(3)
+    x = torch.randn(B, H, H, C, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Cout, k, k, C, device="cuda") * 0.05).to(torch.bfloat16)
+    g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=H, OW=H, KH=k, KW=k, stride=1, pad=(k - 1) // 2)
+    y1 = torch.empty(B, H, H, Cout, device="cuda", dtype=torch.bfloat16)
+    y2 = torch.empty_like(y1)
+    s1 = torch.zeros(2 * Cout, device="cuda")
+    s2 = torch.zeros(2 * Cout, device="cuda")
+    ops.conv_fwd(x, w, None, y1, None, g, act=ops.ACT_NONE, stats=s1)
+    ops.conv_fwd(x, w, None, y2, None, g, act=ops.ACT_NONE)
+    ops.bn_stats(y2, s2)
+    assert torch.equal(y1, y2)
+    R = B * H * H
+    # compare the derived mean / variance (the raw shifted sums are tiny when the shift is close)
+    m1, m2 = s1[:Cout] / R, s2[:Cout] / R
+    v1, v2 = s1[Cout:] / R - m1 * m1, s2[Cout:] / R - m2 * m2
+    assert torch.allclose(m1, m2, rtol=1e-3, atol=1e-5)
+    assert torch.allclose(v1, v2, rtol=1e-3, atol=1e-6)
