@@ -22,6 +22,8 @@
 
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dtfe {
 
 namespace {
@@ -213,11 +215,289 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
   (void)KT;
 }
 
+// ------------------------------------------------------------------ 4-way split recurrence
+// The kernels above run each 16-row group on ONE CU, and the exact-fp32 MFMA (1/16 of the bf16
+// rate) makes every timestep ~10k cycles of matrix work on that CU: 8 CUs busy, 248 idle.  Here
+// each row group is split over NS = 4 workgroups (4 CUs) by HIDDEN UNIT: workgroup sp owns units
+// [32 sp, 32 sp + 32) and therefore the 128 gate columns {i, j, f, o} x those units - so the cell
+// update (which couples the four gates of a unit) stays inside the workgroup and a timestep does
+// a quarter of the MFMA work.  The only coupling is the recurrent operand: the forward needs all
+// 128 units of h_{t-1}, the backward all 512 dgate columns of step t.
+//
+// Exchange: a flag-per-word ("low latency") protocol.  Every exchanged fp32 travels as one 64-bit
+// word {value, tag} stored with a single agent-scope atomic store, tag = epoch * 256 + step + 1
+// (never 0, the zero-filled buffer's tag); the reader polls the words it needs with agent-scope
+// atomic loads until every tag matches.  A
+// separate flag would cost a second memory round trip and a release fence (L2 write-back on the
+// multi-L2 gfx950) per step; here a step costs one store->load propagation.  Buffers are double
+// (step parity): slot t&1 is rewritten at step t+2 only after its writer has read the step-t+1
+// words of every peer, which those peers produce after they finished reading slot t&1.  The epoch
+// (advanced by the last workgroup of each launch) makes stale words of earlier launches - and
+// graph replays - never match, so nothing is reset between launches.  Polls are bounded by a
+// wall-clock timeout that sets an error word instead of hanging.  All 4 * B/16 workgroups must
+// be co-resident (one 512-thread workgroup per CU, <= 256): checked at launch.
+constexpr int NS = 4;
+constexpr int SPT = 512;  // 8 waves
+constexpr int MAX_GROUPS = 64;
+
+struct SplitSync {
+  unsigned long long* llf;  // [MAX_GROUPS][2][16][H]   forward h exchange
+  unsigned long long* llb;  // [MAX_GROUPS][2][NS][16][H] backward dh-partial exchange
+  int* epoch;
+  int* done;
+  int* err;
+};
+
+__device__ __forceinline__ void ll_put(unsigned long long* p, float v, unsigned tag) {
+  const unsigned long long w = ((unsigned long long)tag << 32) | __float_as_uint(v);
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// N words per thread at p[k * stride]; returns when every tag equals `tag` (or on timeout)
+template <int N>
+__device__ __forceinline__ void ll_get(const unsigned long long* p, long stride, unsigned tag, float (&v)[N], int* err) {
+  unsigned long long w[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = __hip_atomic_load(p + k * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long t0 = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) ok &= (unsigned)(w[k] >> 32) == tag;
+    if (ok) break;
+    if (!t0) t0 = wall_clock64();
+    else if (wall_clock64() - t0 > 2000000000ull) {  // 20 s at 100 MHz: a peer never ran - fail, do not hang
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if ((unsigned)(w[k] >> 32) != tag) w[k] = __hip_atomic_load(p + k * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = __uint_as_float((unsigned)w[k]);
+}
+
+__device__ __forceinline__ void finish_launch(const SplitSync& y) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(y.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (int)gridDim.x - 1) {
+      __hip_atomic_store(y.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(y.epoch, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned launch_base(const SplitSync& y) {
+  return (unsigned)__hip_atomic_load(y.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * 256u;
+}
+
+// forward: A = [x_t | h_{t-1}] (16 x 156, LDS) . K[:, my 128 gate columns] (each wave one 16-column
+// tile, its 39 k-steps of B fragments in VGPRs for all T steps) on v_mfma_f32_16x16x4_f32.
+template <int H, int KT4>
+__global__ __launch_bounds__(SPT) void lstm_split_fwd_kernel(LstmSeqArgs a, SplitSync y) {
+  constexpr int G4 = 4 * H, UPW = H / NS;  // units per workgroup (32)
+  constexpr int GC = 4 * UPW;              // gate columns per workgroup (128)
+  constexpr int GP = GC + 4;
+  constexpr int HW = LR * H / SPT;         // exchanged h words per thread (4)
+  extern __shared__ float lds[];
+  const int I = a.I, KT = I + H, AP = KT + 1;
+  float* As = lds;            // [16][AP]
+  float* Gs = lds + 16 * AP;  // [16][GP] activated gates of my columns (gate-major: gi * UPW + u)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rg = blockIdx.x / NS, sp = blockIdx.x % NS, r0 = rg * LR, B = a.B;
+  const unsigned base = launch_base(y);
+  const long rowKT = KT;
+  unsigned long long* llg = y.llf + (long)rg * 2 * LR * H;
+  const int mrow = lane & 15, g = lane >> 4;
+  // wave w: gate gi = w / 2, units 16 * (w & 1) .. +16 of my slice
+  const int gi = w >> 1, ul = 16 * (w & 1) + mrow, col = gi * H + sp * UPW + ul;  // global gate column
+  float kreg[KT4];
+#pragma unroll
+  for (int kk = 0; kk < KT4; ++kk) kreg[kk] = a.K[(long)(4 * kk + g) * G4 + col];
+  const float bias = a.bias[col] + (gi == 2 ? a.forget_bias : 0.f);
+  // cell update ownership: thread -> (row, unit) of my 16 x 32 slice
+  const int cr = tid / UPW, cu = tid - cr * UPW;
+  float creg = 0.f;
+  // x_t: one element per thread (LR * I = 448 <= 512), prefetched a step ahead so its load latency
+  // is off the recurrence's critical path
+  const int xr = tid / I, xk = tid - xr * I;
+  const bool xo = tid < LR * I;
+  float xv = xo ? a.xh[((long)r0 + xr) * rowKT + xk] : 0.f;
+  for (int t = 0; t < a.T; ++t) {
+    if (xo) As[xr * AP + xk] = xv;
+    if (xo && t + 1 < a.T) xv = a.xh[((long)(t + 1) * B + r0 + xr) * rowKT + xk];
+    if (t == 0) {
+      for (int e = tid; e < LR * H; e += SPT) As[(e / H) * AP + I + e % H] = a.xh[((long)r0 + e / H) * rowKT + I + e % H];
+    } else {
+      float hv[HW];
+      ll_get<HW>(llg + ((t - 1) & 1) * LR * H + tid, SPT, base + t, hv, y.err);
+#pragma unroll
+      for (int k = 0; k < HW; ++k) {
+        const int e = tid + k * SPT;
+        As[(e / H) * AP + I + e % H] = hv[k];
+      }
+    }
+    __syncthreads();
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KT4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[mrow * AP + 4 * kk + g], kreg[kk], acc, 0, 0, 0);
+    float* act_t = a.act + ((long)t * B + r0) * G4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = 4 * g + e;
+      const float z = acc[e] + bias;
+      const float v = gi == 1 ? tanhf(z) : sigmoidf_(z);
+      Gs[r * GP + gi * UPW + ul] = v;
+      act_t[(long)r * G4 + col] = v;
+    }
+    __syncthreads();
+    {
+      const float* gr = Gs + cr * GP;
+      const float si = gr[cu], tj = gr[UPW + cu], sf = gr[2 * UPW + cu], so = gr[3 * UPW + cu];
+      const float c = creg * sf + si * tj;
+      creg = c;
+      const float h = tanhf(c) * so;
+      const int u = sp * UPW + cu;
+      a.c[((long)t * B + r0 + cr) * H + u] = c;
+      if (t + 1 < a.T) {
+        ll_put(llg + (t & 1) * LR * H + cr * H + u, h, base + t + 1);
+        a.xh[((long)(t + 1) * B + r0 + cr) * rowKT + I + u] = h;  // for the kernel-gradient GEMM
+      } else {
+        a.hT[(long)(r0 + cr) * H + u] = h;
+      }
+    }
+    // no barrier needed here: the next As writes come after this step's post-MFMA barrier, the
+    // next Gs writes after the next step's post-exchange barrier (which every reader of Gs passes)
+  }
+  finish_launch(y);
+}
+
+// backward, per step t = T-1..0: cell backward of my 16 x 32 units (dh of my units from the
+// exchange, dc in a register; act / c of the next step prefetched) -> my 128 dgate columns ->
+// dg[t] and LDS; then this workgroup's PARTIAL dh_{t-1}[16][all 128 units] = dg_t[:, my columns]
+// . K_h[:, my columns]^T (8 waves = 8 unit tiles, 32 k4-steps) goes to the exchange, and each
+// thread sums the 4 partials of its (row, unit) in a fixed order - 4 words per thread per step
+// instead of gathering all 512 dgate columns.
+template <int H>
+__global__ __launch_bounds__(SPT) void lstm_split_bwd_kernel(LstmSeqArgs a, SplitSync y) {
+  constexpr int G4 = 4 * H, UPW = H / NS, GC = 4 * UPW;  // my gate columns (128) = 32 k4-steps
+  constexpr int DP = GC + 4;
+  extern __shared__ float lds[];
+  float* DG = lds;  // [2][16][DP] my dgates of step t (parity-double-buffered: one barrier per step)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rg = blockIdx.x / NS, sp = blockIdx.x % NS, r0 = rg * LR, B = a.B;
+  const unsigned base = launch_base(y);
+  unsigned long long* llg = y.llb + (long)rg * 2 * NS * LR * H;  // [2][NS src][16][H]
+  const int mrow = lane & 15, g = lane >> 4;
+  // B fragments: B[k = j][n = u] = K[I + u][col(j)], j = my gate column q * UPW + v -> q * H + sp * UPW + v,
+  // u = 16 w + mrow (wave w = unit tile w)
+  float kb[GC / 4];
+  {
+    const float* krow = a.K + (long)(a.I + 16 * w + mrow) * G4 + sp * UPW;
+#pragma unroll
+    for (int kk = 0; kk < GC / 4; ++kk) {
+      const int j = 4 * kk + g;
+      kb[kk] = krow[(j / UPW) * H + j % UPW];
+    }
+  }
+  const int cr = tid / UPW, cu = tid - cr * UPW, u = sp * UPW + cu;
+  float dh = a.dhT[(long)(r0 + cr) * H + u];
+  float dc = 0.f;
+  auto fetch = [&](int t, float (&v)[6]) {
+    const long ri = (long)t * B + r0 + cr;
+    const float* ac = a.act + ri * G4;
+    v[0] = ac[u];
+    v[1] = ac[H + u];
+    v[2] = ac[2 * H + u];
+    v[3] = ac[3 * H + u];
+    v[4] = a.c[ri * H + u];
+    v[5] = t > 0 ? a.c[(ri - B) * H + u] : 0.f;
+  };
+  float nx[6];
+  fetch(a.T - 1, nx);
+  for (int t = a.T - 1; t >= 0; --t) {
+    const float si = nx[0], tj = nx[1], sf = nx[2], so = nx[3], c = nx[4], cp = nx[5];
+    if (t > 0) fetch(t - 1, nx);
+    float* D = DG + (t & 1) * 16 * DP;
+    {
+      const float tc = tanhf(c);
+      const float dct = dc + dh * so * (1.f - tc * tc);
+      const float d4[4] = {dct * tj * si * (1.f - si), dct * si * (1.f - tj * tj), dct * cp * sf * (1.f - sf),
+                           dh * tc * so * (1.f - so)};
+      float* dgr = a.dg + ((long)t * B + r0 + cr) * G4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dgr[q * H + u] = d4[q];
+        D[cr * DP + q * UPW + cu] = d4[q];
+      }
+      dc = dct * sf;
+    }
+    if (t == 0) break;
+    __syncthreads();
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    const float* drow = D + mrow * DP;
+#pragma unroll
+    for (int kk = 0; kk < GC / 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(drow[4 * kk + g], kb[kk], acc, 0, 0, 0);
+    unsigned long long* slot = llg + (long)(t & 1) * NS * LR * H;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ll_put(slot + ((long)sp * LR + 4 * g + e) * H + 16 * w + mrow, acc[e], base + t + 1);
+    float pv[NS];
+    ll_get<NS>(slot + (long)cr * H + u, (long)LR * H, base + t + 1, pv, y.err);
+    dh = ((pv[0] + pv[1]) + pv[2]) + pv[3];
+  }
+  finish_launch(y);
+}
+
+SplitSync split_sync(hipStream_t s, int H) {
+  static char* buf[64] = {};
+  constexpr size_t CTL = 4096;
+  const size_t fw = (size_t)MAX_GROUPS * 2 * LR * 128, bw = fw * NS;  // words, H = 128
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (H != 128 || dev < 0 || dev >= 64) return SplitSync{};
+  if (!buf[dev]) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &st);
+    if (st != hipStreamCaptureStatusNone) return SplitSync{};  // first use inside a capture: fall back
+    const size_t bytes = CTL + (fw + bw) * 8;
+    char* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return SplitSync{};
+    if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return SplitSync{};
+    }
+    buf[dev] = p;
+  }
+  int* c = reinterpret_cast<int*>(buf[dev]);
+  auto* ll = reinterpret_cast<unsigned long long*>(buf[dev] + CTL);
+  return SplitSync{ll, ll + fw, c, c + 4, c + 8};
+}
+
+bool split_ok(const LstmSeqArgs& a) {
+  const char* e = getenv("DTFE_LSTM_SPLIT");  // read per launch (tests A/B both paths in one process)
+  const bool on = !(e && atoi(e) == 0);
+  // one workgroup per CU, all co-resident: <= 256 workgroups; exchange buffers sized for MAX_GROUPS
+  return on && a.H == 128 && a.I == 28 && a.B % LR == 0 && a.B / LR <= MAX_GROUPS && (a.B / LR) * NS <= 256 &&
+         a.T < 255;
+}
+
 }  // namespace
 
 bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
   // register-resident K slice: instantiated for the MNIST row-LSTM (I = 28, H = 128)
   if (a.H != 128 || a.I != 28 || a.B % LR || LR * a.I > 1024) return false;
+  if (split_ok(a)) {
+    const SplitSync y = split_sync(s, a.H);
+    if (y.llf) {
+      const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (a.H + 4)) * sizeof(float);
+      auto k = lstm_split_fwd_kernel<128, (28 + 128) / 4>;
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
+      return true;
+    }
+  }
   const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * a.H + 4)) * sizeof(float);
   auto k = lstm_seq_fwd_kernel<128, (28 + 128) / 4>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -227,6 +507,16 @@ bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
 
 bool launch_lstm_seq_bwd(const LstmSeqArgs& a, hipStream_t s) {
   if (a.H != 128 || a.B % LR || (a.I + a.H) % 4) return false;
+  if (split_ok(a)) {
+    const SplitSync y = split_sync(s, a.H);
+    if (y.llf) {
+      const size_t lds = (size_t)2 * 16 * (4 * (a.H / NS) + 4) * sizeof(float);
+      auto k = lstm_split_bwd_kernel<128>;
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
+      return true;
+    }
+  }
   const size_t lds = ((size_t)LR * (4 * a.H + 4) + 2 * (size_t)LR * a.H) * sizeof(float);
   auto k = lstm_seq_bwd_kernel<128>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -99,15 +99,18 @@ def test_lstm_trains_on_gpu_with_graph():
     assert last < 0.5 * first, (first, last)
 
 
-@pytest.mark.parametrize("batch", [128, 48])
-def test_lstm_persistent_matches_per_step(batch, monkeypatch):
-    """Persistent whole-sequence kernels (lstm_seq.hip) vs the per-step cell kernels + GEMMs:
+@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("batch", [128, 48, 1024])
+def test_lstm_persistent_matches_per_step(batch, split, monkeypatch):
+    """Persistent whole-sequence kernels (lstm_seq.hip; split=1: each row group over 4 CUs with a
+    per-step flag exchange, split=0: one CU per row group) vs the per-step cell kernels + GEMMs:
     forward activations, cell states, logits, and every gradient."""
     model = LstmModel()
     g = torch.Generator().manual_seed(3)
     x = torch.rand(batch, 784, generator=g)
     y = F.one_hot(torch.randint(0, 10, (batch,), generator=g), 10).float()
     out = {}
+    monkeypatch.setenv("DTFE_LSTM_SPLIT", split)
     for mode in ("1", "0"):
         monkeypatch.setenv("DTFE_LSTM_PERSIST", mode)
         prog = model.program("cuda", batch, seed=11)
@@ -120,3 +123,24 @@ def test_lstm_persistent_matches_per_step(batch, monkeypatch):
         a, b = out["1"][k], out["0"][k]
         err = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert err < 1e-5, (k, err)
+
+
+def test_lstm_split_kernels_replay_in_a_graph(monkeypatch):
+    """The split kernels' step flags are epoch-stamped: replaying a captured step many times
+    (fwd and bwd share the flag words) must keep giving the eager result."""
+    from dtfe.utils.graphs import StepGraph
+    monkeypatch.setenv("DTFE_LSTM_SPLIT", "1")
+    model = LstmModel()
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(256, 784, generator=g).cuda()
+    y = F.one_hot(torch.randint(0, 10, (256,), generator=g), 10).float().cuda()
+    prog = model.program("cuda", 256, seed=2)
+    prog.load_batch((x, y))
+    prog.compute_grads()
+    ref = prog.P.grad.clone()
+    run = StepGraph(prog.compute_grads, warmup=1)
+    for _ in range(40):
+        run()
+    torch.cuda.synchronize()
+    assert run.graph is not None, run.capture_error
+    assert torch.equal(prog.P.grad, ref)
