@@ -44,8 +44,8 @@ def time_model(name, steps, warmup, graph=True):
     def step():
         prog.load_batch((x, y))
         prog.compute_grads()
-        for i, o in enumerate(opts):
-            o.step(gs_inc=model.gs_increments if i == len(opts) - 1 else 0)
+        # all of the step's optimizers in one launch (TF: the minimize ops of one sess.run)
+        Optimizer.step_all(opts, [model.gs_increments if i == len(opts) - 1 else 0 for i in range(len(opts))])
 
     run = StepGraph(step, warmup=2, enabled=graph)
     for _ in range(warmup):

@@ -101,9 +101,13 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   a.bias_out = ptr_or_null<float>(bias_out);
   TORCH_CHECK(!a.bias_out || b_ones_row >= 0 || a_ones_row >= 0, "gemm: bias_out needs a ones row");
   a.ones = ptr_or_null<dtfe::bf16>(ones);
-  if (tile >= 5)
+  if (tile == dtfe::GEMM_TILE_SMALL) {
+    TORCH_CHECK(real_splits == 1 && dtfe::gemm_small_eligible(dt == 0 ? 0 : 1, a),
+                "gemm: the small-tile kernel takes fp32 operands, one split, no un-pool epilogue");
+  } else if (tile >= 5) {
     TORCH_CHECK(dtfe::gemm_glds_eligible(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, a),
                 "gemm: shape / layout not eligible for the global_load_lds tile ", tile);
+  }
   dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
 }
 
@@ -317,6 +321,29 @@ void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, cons
   dtfe::launch_head_xent(a, cur_stream());
 }
 
+void head_wgrad(const Tensor& dl, const Tensor& h, const Tensor& dw, const optional<Tensor>& db, int64_t nc,
+                double scale) {
+  check_cuda(h, "h");
+  TORCH_CHECK(dl.scalar_type() == at::kBFloat16 && h.scalar_type() == at::kBFloat16 && dl.dim() == 2 && h.dim() == 2,
+              "head_wgrad: bf16 dl [B][ld] and h [B][K]");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.size(0) == nc && dw.stride(1) == 1,
+              "head_wgrad: fp32 dw [NC][>=K]");
+  TORCH_CHECK(dl.size(0) == h.size(0) && dl.stride(1) == 1 && h.stride(1) == 1 && dl.size(1) >= nc,
+              "head_wgrad: batch / layout mismatch");
+  dtfe::HeadWgradArgs a{};
+  a.B = (int)h.size(0); a.K = (int)h.size(1); a.NC = (int)nc;
+  TORCH_CHECK(dw.size(1) >= a.K, "head_wgrad: dw rows shorter than K");
+  a.dl = reinterpret_cast<const dtfe::bf16*>(dl.data_ptr()); a.ld_dl = (int)dl.stride(0);
+  a.h = reinterpret_cast<const dtfe::bf16*>(h.data_ptr()); a.ldh = (int)h.stride(0);
+  a.dw = dw.data_ptr<float>(); a.ldw = (int)dw.stride(0);
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() >= nc, "head_wgrad: fp32 db [NC]");
+    a.db = db->data_ptr<float>();
+  }
+  a.scale = (float)scale;
+  dtfe::launch_head_wgrad(a, cur_stream());
+}
+
 // -------------------------------------------------------------- optimizer
 // segs: int64 [nseg, 6] = (off, R, T, C, w16_ptr, wt16_ptr)
 // work: int64 [nwork, 7] = (kind, seg, t, r0, c0, start, count)
@@ -352,8 +379,11 @@ void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, c
                      double gscale, const optional<Tensor>& s1, const optional<Tensor>& s2, double lr, double beta1,
                      double beta2, double eps, double momentum, double rho, const optional<Tensor>& beta_pow,
                      const optional<Tensor>& global_step, int64_t gs_inc, const Tensor& done, const Tensor& blob,
-                     int64_t nseg, int64_t nwork) {
+                     int64_t nseg, int64_t nwork, int64_t group) {
   check_cuda(p, "p");
+  // group: 0 = launch now; 1 = queue these args; 2 = queue and launch every queued optimizer in
+  // ONE grouped launch (same kind, disjoint var lists: e.g. the GAN's two Adams)
+  thread_local std::vector<dtfe::OptArgs> pending;
   dtfe::OptArgs a{};
   a.kind = (int)kind;
   a.p = p.data_ptr<float>();
@@ -376,7 +406,17 @@ void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, c
   if (kind == dtfe::OPT_ADAM) TORCH_CHECK(a.beta_pow && a.s1 && a.s2, "adam needs slots and beta powers");
   if (kind == dtfe::OPT_RMSPROP) TORCH_CHECK(a.s1 && a.s2, "rmsprop needs slots");
   if (kind == dtfe::OPT_MOMENTUM) TORCH_CHECK(a.s1, "momentum needs a slot");
-  dtfe::launch_apply_gradients(a, cur_stream());
+  if (group == 0) {
+    TORCH_CHECK(pending.empty(), "apply_gradients: a queued group was never launched");
+    dtfe::launch_apply_gradients(a, cur_stream());
+    return;
+  }
+  pending.push_back(a);
+  if (group == 2) {
+    std::vector<dtfe::OptArgs> q;
+    q.swap(pending);
+    dtfe::launch_apply_gradients_group(q.data(), (int)q.size(), cur_stream());
+  }
 }
 
 // ---------------------------------------------------------- elementwise
@@ -418,10 +458,24 @@ void gather_rows(const Tensor& src, const Tensor& dst, const optional<Tensor>& i
 }
 
 void uniform_fill(const Tensor& out, double lo, double hi, int64_t seed, const optional<Tensor>& counter,
-                  const optional<Tensor>& done) {
+                  const optional<Tensor>& done, const optional<Tensor>& copy_src, const optional<Tensor>& copy_dst) {
   check_cuda(out, "out");
+  const float* cs = nullptr;
+  float* cd = nullptr;
+  long nc = 0;
+  if (copy_src.has_value() && copy_src->defined()) {
+    TORCH_CHECK(copy_dst.has_value() && copy_dst->defined(), "uniform_fill: copy_src without copy_dst");
+    TORCH_CHECK(copy_src->scalar_type() == at::kFloat && copy_dst->scalar_type() == at::kFloat &&
+                    copy_src->is_contiguous() && copy_dst->is_contiguous() && copy_src->numel() == copy_dst->numel() &&
+                    copy_src->numel() % 4 == 0 && ((uintptr_t)copy_src->data_ptr() & 15) == 0 &&
+                    ((uintptr_t)copy_dst->data_ptr() & 15) == 0,
+                "uniform_fill: the fused copy takes equal-size contiguous 16-B aligned fp32 tensors (numel % 4 == 0)");
+    cs = copy_src->data_ptr<float>();
+    cd = copy_dst->data_ptr<float>();
+    nc = copy_src->numel();
+  }
   dtfe::launch_uniform_fill(out.data_ptr<float>(), out.numel(), (float)lo, (float)hi, (uint64_t)seed,
-                            ptr_or_null<int64_t>(counter), ptr_or_null<uint32_t>(done), cur_stream());
+                            ptr_or_null<int64_t>(counter), ptr_or_null<uint32_t>(done), cur_stream(), cs, cd, nc);
 }
 
 void cast_(const Tensor& src, const Tensor& dst) {
@@ -711,15 +765,17 @@ TORCH_LIBRARY(dtfe, m) {
       "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl,"
       " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep,"
       " Tensor(f!)? step_counter=None) -> ()");
+  m.def("head_wgrad(Tensor dl, Tensor h, Tensor(a!) dw, Tensor(b!)? db, int nc, float scale) -> ()");
   m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
   m.def(
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
       " float lr, float beta1, float beta2, float eps, float momentum, float rho, Tensor(d!)? beta_pow,"
-      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork) -> ()");
+      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0) -> ()");
   m.def(
       "gather_rows(Tensor src, Tensor(a!) dst, Tensor? idx, Tensor? labels_src, Tensor(b!)? labels_dst, int seed,"
       " Tensor(c!)? counter, Tensor(d!)? done, Tensor(e!)[] zero, Tensor(f!)? onehot=None) -> ()");
-  m.def("uniform_fill(Tensor(a!) out, float lo, float hi, int seed, Tensor(b!)? counter, Tensor(c!)? done) -> ()");
+  m.def("uniform_fill(Tensor(a!) out, float lo, float hi, int seed, Tensor(b!)? counter, Tensor(c!)? done,"
+        " Tensor? copy_src=None, Tensor(d!)? copy_dst=None) -> ()");
   m.def("cast_(Tensor src, Tensor(a!) dst) -> ()");
   m.def(
       "softmax_xent(Tensor logits, Tensor? labels_i, Tensor? labels_oh, float scale, Tensor(a!)? dlogits,"
@@ -751,6 +807,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("conv_dgrad", &conv_dgrad);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("head_xent", &head_xent);
+  m.impl("head_wgrad", &head_wgrad);
   m.impl("apply_gradients", &apply_gradients);
   m.impl("gather_rows", &gather_rows);
   m.impl("uniform_fill", &uniform_fill);

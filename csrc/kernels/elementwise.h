@@ -24,7 +24,8 @@ void launch_gather_rows(const GatherArgs& a, hipStream_t s);
 
 // uniform noise U(lo, hi) from a counter-based hash; *counter advanced per call
 void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, int64_t* counter,
-                         uint32_t* done, hipStream_t s);
+                         uint32_t* done, hipStream_t s, const float* csrc = nullptr, float* cdst = nullptr,
+                         long ncopy = 0);
 
 // dtype casts
 void launch_cast_f32_bf16(const float* src, bf16* dst, long n, hipStream_t s);

@@ -108,19 +108,26 @@ void launch_gather_rows(const GatherArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
 
+// Optionally also copies ncopy floats (16-B aligned, ncopy % 4 == 0) from csrc to cdst in the same
+// launch: the GAN's batch staging (real images into the stacked [real; fake] buffer + the noise).
 __global__ __launch_bounds__(256) void uniform_fill_kernel(float* out, long n, float lo, float hi, uint64_t seed,
-                                                          int64_t* counter, uint32_t* done) {
+                                                          int64_t* counter, uint32_t* done, const float* csrc,
+                                                          float* cdst, long ncopy) {
   const int64_t step = counter ? *counter : 0;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     out[i] = lo + (hi - lo) * hash_uniform(seed ^ 0xA5A5A5A5ull, (uint64_t)step * n + i);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < ncopy / 4; i += (long)gridDim.x * 256)
+    reinterpret_cast<f32x4_t*>(cdst)[i] = reinterpret_cast<const f32x4_t*>(csrc)[i];
   advance_counter_last_block(counter, done, 1);
 }
 
 void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, int64_t* counter, uint32_t* done,
-                         hipStream_t s) {
-  long blocks = (n + 255) / 256;
+                         hipStream_t s, const float* csrc, float* cdst, long ncopy) {
+  const long work = n > ncopy / 4 ? n : ncopy / 4;
+  long blocks = (work + 255) / 256;
   if (blocks > (done ? 256 : 1024)) blocks = done ? 256 : 1024;  // see launch_gather_rows
-  hipLaunchKernelGGL(uniform_fill_kernel, dim3(blocks), dim3(256), 0, s, out, n, lo, hi, seed, counter, done);
+  hipLaunchKernelGGL(uniform_fill_kernel, dim3(blocks), dim3(256), 0, s, out, n, lo, hi, seed, counter, done, csrc,
+                     cdst, ncopy);
 }
 
 __global__ void cast_f32_bf16_kernel(const float* src, bf16* dst, long n) {

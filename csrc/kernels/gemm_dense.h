@@ -254,6 +254,11 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
 // gemm_glds_eligible); 9..12 the same tiles with 2 stages
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream);
+// tile 13: exact-fp32 16x16 tiles, one workgroup per tile with an in-workgroup 4-way K split and
+// register-direct operands (gemm_small.hip) - the small layers of the reference workloads
+constexpr int GEMM_TILE_SMALL = 13;
+bool gemm_small_eligible(int dtype, const DenseGemmArgs& a);
+void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s);
 // block tile of a tile id; returns the k-tile depth (split-K chunks are multiples of it)
 int gemm_dense_tile_dims(int tile, int& bm, int& bn);
 // whether the global_load_lds kernel family can run this GEMM with tile `tile` (5..8)

@@ -17,12 +17,13 @@ static void launch_one(int splits, const DenseGemmArgs& args, hipStream_t s) {
 }
 
 int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
-  static const int dims[13][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
+  static const int dims[14][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64},
-                                  {128, 128}, {128, 64}, {64, 128}, {64, 64}};
-  if (tile < 0 || tile > 12) return -1;
+                                  {128, 128}, {128, 64}, {64, 128}, {64, 64}, {16, 16}};
+  if (tile < 0 || tile > 13) return -1;
   bm = dims[tile][0];
   bn = dims[tile][1];
+  if (tile == GEMM_TILE_SMALL) return 16;
   return tile >= 5 ? GL_BK : GEMM_KTILE;
 }
 
@@ -89,6 +90,12 @@ static void by_mode(int am, int bm, int tile, int splits, const DenseGemmArgs& a
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream) {
   if (splits < 1) splits = 1;
+  if (tile == GEMM_TILE_SMALL) {
+    if (!gemm_small_eligible(dtype, args) || splits != 1)
+      throw std::runtime_error("gemm_dense: the small-tile kernel takes fp32, one split, no un-pool epilogue");
+    launch_gemm_small(amode, bmode, args, stream);
+    return;
+  }
   if (tile >= 5) {
     if (!gemm_glds_eligible(dtype, amode, bmode, tile, args))
       throw std::runtime_error("gemm_dense: this GEMM is not eligible for the global_load_lds tiles");

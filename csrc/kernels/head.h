@@ -20,4 +20,16 @@ struct HeadArgs {
 
 void launch_head_xent(const HeadArgs& a, hipStream_t s);
 
+// dW[c][k] = scale * sum_b dl[b][c] h[b][k] (row stride ldw), db[c] = scale * sum_b dl[b][c];
+// stored, not accumulated (one workgroup per 16 columns, fixed summation order)
+struct HeadWgradArgs {
+  int B, NC, K;
+  const bf16* dl; int ld_dl;   // [B][ld_dl]
+  const bf16* h; int ldh;      // [B][ldh]
+  float* dw; int ldw;          // [NC][ldw]
+  float* db;                   // [NC] (optional)
+  float scale;
+};
+void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s);
+
 }  // namespace dtfe

@@ -120,3 +120,74 @@ void launch_head_xent(const HeadArgs& a, hipStream_t s) {
 }
 
 }  // namespace dtfe
+
+namespace dtfe {
+
+// Classifier-head weight / bias gradient: dW[c][k] = sum_b dl[b][c] h[b][k], db[c] = sum_b dl[b][c].
+// The layer is 10 x 1024 over a 1024-row batch (21 MFLOP): a split-K MFMA GEMM spends ~16 us on
+// 32 x 32 tiles (a 10-row M padded to 32) and the fixed-order combine of 8 K-splits.  Here one
+// 1024-thread workgroup owns 16 columns of dW for the WHOLE batch (no cross-workgroup
+// reduction): the batch's dlogit rows are staged in LDS (32 KB, 16-B loads) while every thread
+// has its 16 h values in flight (thread (column c = t & 15, row group r = t >> 4) takes rows
+// r, r + 64, ...), so the launch pays about two memory latencies; the 64 row groups are then
+// summed through LDS in a fixed order - bitwise reproducible, no atomics.  Workgroup K/16
+// produces the bias gradient (h read as ones).
+template <int NC>
+__global__ __launch_bounds__(1024) void head_wgrad_kernel(HeadWgradArgs a) {
+  constexpr int RG = 64, PER = 16;  // row groups, rows per thread (B <= RG * PER)
+  // one LDS buffer: the staged dlogit rows, then (after a barrier) the per-row-group partials
+  constexpr int DL_BYTES = RG * PER * 16 * 2, PART_BYTES = RG * 16 * (NC + 1) * 4;
+  __shared__ __attribute__((aligned(16))) char smem[DL_BYTES > PART_BYTES ? DL_BYTES : PART_BYTES];
+  auto dls = reinterpret_cast<bf16(*)[16]>(smem);
+  auto part = reinterpret_cast<float(*)[16][NC + 1]>(smem);
+  const int t = threadIdx.x, c = t & 15, rg = t >> 4;
+  const bool bias_blk = blockIdx.x * 16 >= a.K;
+  const int col = blockIdx.x * 16 + c;
+  float hv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int b = rg + RG * i;
+    hv[i] = b < a.B ? (bias_blk ? 1.f : bf2f(a.h[(long)b * a.ldh + col])) : 0.f;
+  }
+  for (int i = t; i < RG * PER * 2; i += 1024) {  // 16-B halves of the 32-B dlogit rows
+    const int b = i >> 1;
+    u32x4_t v = {0u, 0u, 0u, 0u};
+    if (b < a.B) v = *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl + (i & 1) * 8);
+    *reinterpret_cast<u32x4_t*>(&dls[b][(i & 1) * 8]) = v;
+  }
+  __syncthreads();
+  float acc[NC];
+#pragma unroll
+  for (int n = 0; n < NC; ++n) acc[n] = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int b = rg + RG * i;
+    const u32x4_t d0 = *reinterpret_cast<const u32x4_t*>(&dls[b][0]);
+    const u32x4_t d1 = *reinterpret_cast<const u32x4_t*>(&dls[b][8]);
+#pragma unroll
+    for (int n = 0; n < NC; ++n) {
+      const uint32_t w = n < 8 ? d0[n >> 1] : d1[(n - 8) >> 1];
+      acc[n] = fmaf(bf2f((bf16)(w >> (16 * (n & 1)))), hv[i], acc[n]);
+    }
+  }
+  __syncthreads();  // every thread is done with the staged rows
+#pragma unroll
+  for (int n = 0; n < NC; ++n) part[rg][c][n] = acc[n];
+  __syncthreads();
+  if (t < 16 * NC) {
+    const int cc = t % 16, n = t / 16;
+    float s = 0.f;
+    for (int r = 0; r < RG; ++r) s += part[r][cc][n];
+    if (!bias_blk) a.dw[(long)n * a.ldw + blockIdx.x * 16 + cc] = s * a.scale;
+    else if (cc == 0) a.db[n] = s * a.scale;
+  }
+}
+
+void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s) {
+  if (a.NC != 10 || a.K % 16 || a.ld_dl < 16 || a.ld_dl % 8 || a.B > 1024)
+    throw std::runtime_error("head_wgrad: needs NC=10, K % 16 == 0, 16-B aligned dl rows of >= 16, B <= 1024");
+  const int blocks = a.K / 16 + (a.db ? 1 : 0);
+  hipLaunchKernelGGL(head_wgrad_kernel<10>, dim3(blocks), dim3(1024), 0, s, a);
+}
+
+}  // namespace dtfe

@@ -423,10 +423,28 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
       row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
       abase[r] = img + (oy * LWP + ox) * PS + 8 * g;
     }
-    // data-gradient ReLU mask: this thread's 16-B chunk of the image's [OH*OW][N] output, in
-    // flight during the k loop (host: M * N / 8 <= THREADS)
-    u32x4_t mk = {0u, 0u, 0u, 0u};
-    if (POOLED && a.relu_mask && tid < nout) mk = *reinterpret_cast<const u32x4_t*>(a.relu_mask + b * M * a.N + tid * 8);
+    // Data gradient (POOLED source): the MFMA operands are swapped, D = W . patch^T, so a lane's
+    // accumulator holds 4 consecutive channels (4g..4g+3 of each n-tile) of ONE output pixel
+    // (column lane & 15): the epilogue is one 8-B masked store per n-tile straight to HBM - no
+    // LDS staging, no scattered 2-byte writes, no extra barriers (rocprof ablation of the staged
+    // version: ~14 us of the 47 us B=1024 launch).  The lane's ReLU-mask words are in flight
+    // during the k loop.
+    int opix[RT];
+    u32x2_t mk[RT][NT];
+    if constexpr (POOLED) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        int oy = 0, ox = 0;
+        const bool ok = row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
+        opix[r] = ok ? oy * a.OW + ox : -1;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          mk[r][n] = u32x2_t{0x3f803f80u, 0x3f803f80u};  // bf16 1.0: no mask
+          if (ok && a.relu_mask)
+            mk[r][n] = *reinterpret_cast<const u32x2_t*>(a.relu_mask + (b * M + opix[r]) * (long)a.N + n * 16 + 4 * g);
+        }
+      }
+    }
     f32x4_t acc[RT][NT];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -456,10 +474,16 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[buf][r]),
-                                                              __builtin_bit_cast(bf16x8_t, fb[buf][n]), acc[r][n],
-                                                              0, 0, 0);
+        for (int n = 0; n < NT; ++n) {
+          if constexpr (POOLED)  // D[channel][pixel]
+            acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fb[buf][n]),
+                                                                __builtin_bit_cast(bf16x8_t, fa[buf][r]), acc[r][n],
+                                                                0, 0, 0);
+          else  // D[pixel][channel]
+            acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[buf][r]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[buf][n]), acc[r][n],
+                                                                0, 0, 0);
+        }
       }
     });
     // Epilogue through LDS: the per-lane results are scattered 2-byte (and 1-byte argmax) values,
@@ -502,40 +526,26 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
         }
       }
     } else {
-      // data gradient (ReLU'-masked, no pool): stage [pixel][N] in the image interior once every
-      // wave is done reading the image, then masked 16-B stores
-      __syncthreads();
+      // data gradient (ReLU'-masked, no pool): lane = one pixel, 4 consecutive channels per n-tile
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        const int tile = wm + WM * r;
-        if (tile >= tiles || (a.diag & 1)) break;
+        if (opix[r] < 0 || (a.diag & 1)) continue;
+        bf16* yp = a.y + (b * M + opix[r]) * (long)a.N + 4 * g;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int oy, ox;
-          if (!row_pixel(tile * 16 + (lane >> 4) * 4 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
-          bf16* d = img + ((oy + a.pad) * LWP + ox + a.pad) * PS + (lane & 15);
+        for (int n = 0; n < NT; ++n) {
+          uint32_t w2[2];
 #pragma unroll
-          for (int n = 0; n < NT; ++n) d[n * 16] = f2bf(apply_act(acc[r][n][j] + biasv[n], a.act));
-        }
-      }
-      __syncthreads();
-      constexpr int CPX = NT * 2;  // 16-B chunks per output pixel
-      for (int i = tid; i < nout; i += THREADS) {
-        const int p = i / CPX, c = i - p * CPX;
-        const int oy = p / a.OW, ox = p - oy * a.OW;
-        u32x4_t v = *reinterpret_cast<const u32x4_t*>(img + ((oy + a.pad) * LWP + ox + a.pad) * PS + c * 8);
-        if (a.relu_mask) {
-          const u32x4_t m = i == tid ? mk : *reinterpret_cast<const u32x4_t*>(a.relu_mask + b * M * a.N + i * 8);
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {  // keep element e where mask e > 0 (bf16 bits: positive, non-zero, not NaN)
-            const uint32_t lo = m[w] & 0xffffu, hi = m[w] >> 16;
-            const uint32_t keep = ((lo - 1u) < 0x7f80u ? 0x0000ffffu : 0u) | ((hi - 1u) < 0x7f80u ? 0xffff0000u : 0u);
-            v[w] &= keep;
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t lo = f2bf(apply_act(acc[r][n][2 * h] + biasv[n], a.act));
+            const uint32_t hi = f2bf(apply_act(acc[r][n][2 * h + 1] + biasv[n], a.act));
+            // keep element e where mask e > 0 (bf16 bits: positive, non-zero, not NaN)
+            const uint32_t m = mk[r][n][h], ml = m & 0xffffu, mh = m >> 16;
+            w2[h] = (((ml - 1u) < 0x7f80u) ? lo : 0u) | (((mh - 1u) < 0x7f80u) ? (hi << 16) : 0u);
           }
+          *reinterpret_cast<u32x2_t*>(yp + n * 16) = u32x2_t{w2[0], w2[1]};
         }
-        *reinterpret_cast<u32x4_t*>(a.y + (b * M + p) * (long)a.N + c * 8) = v;
       }
-      __syncthreads();  // the interior is read before the next image is written into it
+      __syncthreads();  // every wave is done reading the image before the next one is written
     }
   }
 }

@@ -1,6 +1,8 @@
 #pragma once
 #include "common.h"
 
+#include <stdexcept>
+
 namespace dtfe {
 
 enum OptKind : int { OPT_SGD = 0, OPT_MOMENTUM = 1, OPT_ADAM = 2, OPT_RMSPROP = 3 };
@@ -35,5 +37,14 @@ struct OptArgs {
 };
 
 void launch_apply_gradients(const OptArgs& a, hipStream_t s);
+
+// up to OPT_GROUP_MAX optimizers of one kind in a single launch (contiguous workgroup ranges)
+constexpr int OPT_GROUP_MAX = 4;
+struct OptGroup {
+  OptArgs o[OPT_GROUP_MAX];
+  int first[OPT_GROUP_MAX + 1];
+  int n;
+};
+void launch_apply_gradients_group(const OptArgs* o, int n, hipStream_t s);
 
 }  // namespace dtfe

@@ -117,15 +117,16 @@ __device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long 
   }
 }
 
+// One optimizer's share of a launch: workgroups bid = 0..nblk-1 of the grid (the whole grid for a
+// plain launch, a contiguous range of it for a grouped one).
 template <int KIND>
-__global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
-  __shared__ bf16 tile[64][66];
+__device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, bf16 (&tile)[64][66]) {
   float lr_t = a.lr;
   if (KIND == OPT_ADAM) {
     const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
     lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   }
-  for (int wi = blockIdx.x; wi < a.nwork; wi += gridDim.x) {
+  for (int wi = bid; wi < a.nwork; wi += nblk) {
     const OptWork w = a.work[wi];
     const OptSeg sg = a.segs[w.seg];
     if (w.kind == 0) {
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(a.done_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
+    if (prev == (uint32_t)nblk - 1) {
       if (KIND == OPT_ADAM) {
         a.beta_pow[0] *= a.beta1;
         a.beta_pow[1] *= a.beta2;
@@ -179,9 +180,49 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
   }
 }
 
-void launch_apply_gradients(const OptArgs& a, hipStream_t s) {
+template <int KIND>
+__global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
+  __shared__ bf16 tile[64][66];
+  apply_body<KIND>(a, blockIdx.x, gridDim.x, tile);
+}
+
+// Several optimizers of one kind in ONE launch (the GAN's two Adams over disjoint var lists):
+// workgroup ranges [first[i], first[i + 1]) run optimizer i; each keeps its own done counter,
+// beta powers and global-step increment, exactly as separate launches would.
+template <int KIND>
+__global__ __launch_bounds__(256) void apply_gradients_group_kernel(OptGroup g) {
+  __shared__ bf16 tile[64][66];
+  int i = 0;
+  while (i + 1 < g.n && (int)blockIdx.x >= g.first[i + 1]) ++i;
+  apply_body<KIND>(g.o[i], blockIdx.x - g.first[i], g.first[i + 1] - g.first[i], tile);
+}
+
+static int apply_blocks(const OptArgs& a) {
   int blocks = a.nwork < 2048 ? a.nwork : 2048;
-  if (blocks < 1) blocks = 1;
+  return blocks < 1 ? 1 : blocks;
+}
+
+void launch_apply_gradients_group(const OptArgs* o, int n, hipStream_t s) {
+  if (n < 1 || n > OPT_GROUP_MAX) throw std::runtime_error("apply_gradients_group: 1..4 optimizers");
+  OptGroup g{};
+  g.n = n;
+  g.first[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (o[i].kind != o[0].kind) throw std::runtime_error("apply_gradients_group: one optimizer kind per launch");
+    g.o[i] = o[i];
+    g.first[i + 1] = g.first[i] + apply_blocks(o[i]);
+  }
+  const dim3 grid(g.first[n]);
+  switch (o[0].kind) {
+    case OPT_SGD: hipLaunchKernelGGL(apply_gradients_group_kernel<OPT_SGD>, grid, dim3(256), 0, s, g); break;
+    case OPT_MOMENTUM: hipLaunchKernelGGL(apply_gradients_group_kernel<OPT_MOMENTUM>, grid, dim3(256), 0, s, g); break;
+    case OPT_ADAM: hipLaunchKernelGGL(apply_gradients_group_kernel<OPT_ADAM>, grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL(apply_gradients_group_kernel<OPT_RMSPROP>, grid, dim3(256), 0, s, g); break;
+  }
+}
+
+void launch_apply_gradients(const OptArgs& a, hipStream_t s) {
+  const int blocks = apply_blocks(a);
   switch (a.kind) {
     case OPT_SGD: hipLaunchKernelGGL(apply_gradients_kernel<OPT_SGD>, dim3(blocks), dim3(256), 0, s, a); break;
     case OPT_MOMENTUM:

@@ -88,9 +88,15 @@ class GanProgram(StepProgram):
 
     def load_batch(self, batch):
         x = batch[0] if isinstance(batch, (tuple, list)) else batch
-        self.xx[: self.batch_size].copy_(x.reshape(self.batch_size, IMG))
-        # z ~ U(-1, 1) (GAN:189); device hash RNG on GPU, torch RNG on CPU
-        ops.uniform_fill(self.z, -1.0, 1.0, seed=self.seed, counter=self.noise_ctr, done=self.noise_done)
+        x = x.reshape(self.batch_size, IMG)
+        real = self.xx[: self.batch_size]
+        # z ~ U(-1, 1) (GAN:189); device hash RNG on GPU, torch RNG on CPU.  On the GPU the real batch
+        # is staged into the stacked [real; fake] buffer by the same launch.
+        fused = x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.data_ptr() % 16 == 0
+        if not fused:
+            real.copy_(x)
+        ops.uniform_fill(self.z, -1.0, 1.0, seed=self.seed, counter=self.noise_ctr, done=self.noise_done,
+                         copy=(x, real) if fused else None)
 
     def forward(self):
         B, W = self.batch_size, self.W

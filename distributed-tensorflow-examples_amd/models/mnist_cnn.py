@@ -233,6 +233,7 @@ class MnistCnnTrainer:
         # head weight gradient: split-K over the batch with the deterministic last-arriver combine
         # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
         # workspace, since it runs on the fc branch beside other GEMMs
+        self.head_gemm = os.environ.get("DTFE_CNN_HEAD_GEMM", "0") == "1" or batch > 1024
         self.head_splits = max(1, min(16, B // 128))
         bm, bn = ops.TILE_DIMS[4]
         ntiles = -(-NCLS // bm) * -(-(FC + 1) // bn)
@@ -292,10 +293,7 @@ class MnistCnnTrainer:
             self._fc1_dgrad(B, K1)
         with (self._branch(self.s_fc, main) if (self.br_fc and not crit) else
               torch.cuda.stream(self.s_fc) if self.br_fc else contextlib.nullcontext()):
-            # head wgrad: dW[10][1024] = dlogit^T . H ; db via the ones column (split-K over the batch)
-            ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
-                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],
-                     splits=self.head_splits, tile=4, workspace=self.ws_head)
+            self._head_wgrad()
             # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
                      bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
@@ -336,6 +334,16 @@ class MnistCnnTrainer:
         if self._apply is not None:
             self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
 
+    def _head_wgrad(self):
+        """head wgrad: dW[10][1024] = dlogit^T . H, db = sum dlogit (dedicated whole-batch kernel; the
+        split-K GEMM path is kept behind DTFE_CNN_HEAD_GEMM=1)"""
+        if self.head_gemm:
+            ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=self.B, amode=ops.RMAJ,
+                     lda=self.dl.shape[1], bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],
+                     splits=self.head_splits, tile=4, workspace=self.ws_head)
+        else:
+            ops.head_wgrad(self.dl, self.h, self.gw["out"], self.gw["bout"], NCLS)  # B <= 1024
+
     def _fc1_dgrad(self, B, K1):
         """fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)."""
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
@@ -364,9 +372,7 @@ class MnistCnnTrainer:
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
                  aux_act=ops.ACT_RELU, tile=self.t_dgrad)
         with self._branch(self.s_fc, main):
-            ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=self.dl.shape[1],
-                     bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],
-                     splits=self.head_splits, tile=4, workspace=self.ws_head)
+            self._head_wgrad()
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
                      bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
             if self.allreduce is not None:

@@ -10,6 +10,7 @@ distributed machinery, and as the fp32 oracle the kernel tests compare to.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -22,7 +23,7 @@ __all__ = [
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
-    "TILE_DIMS", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
+    "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
@@ -31,8 +32,10 @@ _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
 TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32),
              # global_load_lds kernel family (csrc/kernels/gemm_glds.h): bf16, K % 64 == 0, whole tiles
              5: (128, 128), 6: (128, 64), 7: (64, 128), 8: (64, 64),      # 3 k-tiles in flight
-             9: (128, 128), 10: (128, 64), 11: (64, 128), 12: (64, 64)}   # 2 stages (more WGs per CU)
+             9: (128, 128), 10: (128, 64), 11: (64, 128), 12: (64, 64),   # 2 stages (more WGs per CU)
+             13: (16, 16)}   # exact-fp32 small-layer kernel (gemm_small.hip): no split-K, in-WG K split
 GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12)
+TILE_SMALL = 13
 _ONES = {}
 
 
@@ -87,11 +90,23 @@ def auto_splits(M: int, N: int, K: int, tile: int) -> int:
     ~256 workgroups; the last-arriving split runs the fused epilogue (deterministic order).
     Uses the shared per-device workspace: GEMMs issued concurrently on several streams must not
     rely on it (pass splits / workspace explicitly)."""
+    if tile == TILE_SMALL:
+        return 1
     bm, bn = TILE_DIMS[tile]
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     if tiles >= 128 or K < 4 * GEMM_KTILE:
         return 1
     return max(1, min(math.ceil(256 / tiles), K // (2 * GEMM_KTILE), 16))
+
+
+def small_f32_ok(M: int, N: int, K: int) -> bool:
+    """The small-layer fp32 kernel wins where the output has at most ~1M elements (<= 4096
+    16x16 tiles) and K is short enough for register-direct operands (reference GAN /
+    autoencoder layers: 1.7-10 us -> ~2-3 us each); DTFE_GEMM_SMALL=0 disables it."""
+    return _SMALL_ON and math.ceil(M / 16) * math.ceil(N / 16) <= 4096 and K <= 2048
+
+
+_SMALL_ON = os.environ.get("DTFE_GEMM_SMALL", "1") != "0"
 
 
 def pick_tile(M: int, N: int) -> int:
@@ -173,6 +188,9 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
     if ld_aux is None:
         ld_aux = ldc
     if out.is_cuda:
+        if tile is None and A.dtype == torch.float32 and pooled is None and splits == 1 and \
+                small_f32_ok(M, N, K):
+            tile = TILE_SMALL
         if tile is None:
             tile = pick_tile(M, N)
             if splits == 1 and not atomic and workspace is None:
@@ -492,15 +510,28 @@ def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0
     dz.copy_(g.to(dz.dtype))
 
 
+def head_wgrad(dl, h, dw, db, nc, scale=1.0):
+    """Classifier-head weight / bias gradient, stored: dw[c][:K] = scale * sum_b dl[b][c] h[b][:],
+    db[c] = scale * sum_b dl[b][c] (one workgroup per 16 columns over the whole batch, fixed order)."""
+    if h.is_cuda:
+        require().head_wgrad(dl, h, dw, db, nc, scale)
+        return
+    d = dl[:, :nc].float()
+    dw[:, : h.shape[1]] = (scale * (d.t() @ h.float())).to(dw.dtype)
+    if db is not None:
+        db.copy_((scale * d.sum(0)).to(db.dtype))
+
+
 # --------------------------------------------------------------- optimizer
 def opt_pack(segs, work, device_like):
     return require().opt_pack(segs, work, device_like)
 
 
 def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow, global_step,
-                    gs_inc, done, blob, nseg, nwork):
+                    gs_inc, done, blob, nseg, nwork, group=0):
+    """group: 0 launch now, 1 queue, 2 queue + launch all queued optimizers as one grouped launch."""
     require().apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow,
-                              global_step, gs_inc, done, blob, nseg, nwork)
+                              global_step, gs_inc, done, blob, nseg, nwork, group)
 
 
 # ------------------------------------------------------------- elementwise
@@ -527,10 +558,15 @@ def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, co
     return dst
 
 
-def uniform_fill(out, lo, hi, seed=0, counter=None, done=None):
+def uniform_fill(out, lo, hi, seed=0, counter=None, done=None, copy=None):
+    """out ~ U(lo, hi) from the device hash RNG (advances ``counter``); ``copy=(src, dst)``: an fp32
+    copy issued in the same launch (batch staging next to the noise)."""
     if out.is_cuda:
-        require().uniform_fill(out, lo, hi, seed, counter, done)
+        src, dst = copy if copy is not None else (None, None)
+        require().uniform_fill(out, lo, hi, seed, counter, done, src, dst)
         return out
+    if copy is not None:
+        copy[1].copy_(copy[0])
     out.uniform_(lo, hi)
     return out
 

@@ -201,17 +201,32 @@ class Optimizer:
         self._blob = ops.opt_pack(torch.tensor(segs, dtype=torch.int64), torch.tensor(work, dtype=torch.int64),
                                   self.P.master)
 
-    def step(self, grad=None, grad16=None, gscale: float = 1.0, gs_inc: int = 1):
-        """Apply gradients (default: the FlatParams grad buffer) to var_list."""
+    def step(self, grad=None, grad16=None, gscale: float = 1.0, gs_inc: int = 1, group: int = 0):
+        """Apply gradients (default: the FlatParams grad buffer) to var_list.  ``group`` (GPU):
+        1 queues this apply, 2 queues it and launches every queued one together (``step_all``)."""
         c = self.cfg
         if grad is None and grad16 is None:
             grad = self.P.grad
         if self.device.type == "cuda":
             ops.apply_gradients(self.kind, self.P.master, grad, grad16, gscale, self.s1, self.s2, c.lr, c.beta1,
                                 c.beta2, c.resolved_eps(), c.momentum, c.rho, self.beta_pow, self.global_step, gs_inc,
-                                self.done, self._blob, self.nseg, self.nwork)
+                                self.done, self._blob, self.nseg, self.nwork, group)
             return
         self._step_cpu(grad if grad is not None else grad16.float(), gscale, gs_inc)
+
+    @staticmethod
+    def step_all(opts, gs_incs, grad=None, grad16=None, gscale: float = 1.0):
+        """Apply several optimizers over disjoint var lists of one FlatParams (the reference's
+        several ``minimize`` calls per step).  On the GPU, optimizers of one kind share ONE grouped
+        launch (each keeps its own beta powers / global-step increment); the math equals
+        calling ``step`` on each in order."""
+        kinds = {o.kind for o in opts}
+        if len(opts) > 1 and len(opts) <= 4 and len(kinds) == 1 and all(o.device.type == "cuda" for o in opts):
+            for i, (o, inc) in enumerate(zip(opts, gs_incs)):
+                o.step(grad=grad, grad16=grad16, gscale=gscale, gs_inc=inc, group=2 if i == len(opts) - 1 else 1)
+            return
+        for o, inc in zip(opts, gs_incs):
+            o.step(grad=grad, grad16=grad16, gscale=gscale, gs_inc=inc)
 
     @torch.no_grad()
     def _step_cpu(self, grad, gscale, gs_inc):

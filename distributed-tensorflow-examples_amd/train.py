@@ -423,10 +423,9 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                 ar.wait()
             g16 = ar.grad16
         with phase("apply"):
-            for i, o in enumerate(opts):
-                last = i == len(opts) - 1
-                o.step(grad16=g16, gscale=1.0 / world, gs_inc=model.gs_increments if last else 0) if g16 is not None \
-                    else o.step(gscale=1.0 / world, gs_inc=model.gs_increments if last else 0)
+            # every minimize op of the step in one (grouped) launch; gs advances once per step by gs_increments
+            Optimizer.step_all(opts, [model.gs_increments if i == len(opts) - 1 else 0 for i in range(len(opts))],
+                               grad16=g16, gscale=1.0 / world)
 
     runner = StepGraph(train_step, warmup=2, capture_error_mode="thread_local",
                        enabled=(device.type == "cuda" and (world == 1 or ar.comm is not None) and flags.hip_graph

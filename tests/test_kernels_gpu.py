@@ -46,6 +46,43 @@ def test_gemm_modes_tiles(dtype, amode, bmode, tile):
     assert _rel(out.cpu(), exp) < tol
 
 
+@pytest.mark.parametrize("amode,bmode", list(itertools.product([0, 1], [0, 1])))
+@pytest.mark.parametrize("M,N,K", [(200, 136, 264), (257, 1, 256), (128, 784, 100), (17, 33, 1), (785, 256, 2049)])
+def test_gemm_small_tile_exact_fp32(amode, bmode, M, N, K):
+    """Small-layer fp32 kernel (tile 13): odd shapes, K not a multiple of 4/16, N = 1, K = 1."""
+    torch.manual_seed(3)
+    A = torch.randn(M, K)
+    B = torch.randn(N, K)
+    At, lda = _operand(A, amode, torch.float32)
+    Bt, ldb = _operand(B, bmode, torch.float32)
+    out = torch.full((M, N), float("nan"), device=DEV)
+    ops.gemm(At, Bt, out, M=M, N=N, K=K, amode=amode, lda=lda, bmode=bmode, ldb=ldb, tile=ops.TILE_SMALL)
+    exp = A.double() @ B.double().t()
+    assert _rel(out.cpu().double(), exp) < 1e-5
+
+
+def test_gemm_small_tile_ones_rows_and_aux():
+    """Weight-gradient form: bias gradient through a ones row (A side and B side), act' epilogue."""
+    torch.manual_seed(4)
+    X, D = torch.randn(256, 100, device=DEV), torch.randn(256, 64, device=DEV)
+    dw = torch.empty(100, 64, device=DEV)
+    db = torch.empty(64, device=DEV)
+    ops.gemm(X, D, dw, M=101, N=64, K=256, amode=ops.RMAJ, lda=100, bmode=ops.RMAJ, ldb=64, a_ones_row=100,
+             bias_out=db, tile=ops.TILE_SMALL)
+    assert _rel(dw.cpu(), X.cpu().t() @ D.cpu()) < 1e-5 and _rel(db.cpu(), D.cpu().sum(0)) < 1e-5
+    dw2 = torch.empty(64, 100, device=DEV)
+    db2 = torch.empty(64, device=DEV)
+    ops.gemm(D, X, dw2, M=64, N=101, K=256, amode=ops.RMAJ, lda=64, bmode=ops.RMAJ, ldb=100, ldc=100,
+             b_ones_row=100, bias_out=db2, tile=ops.TILE_SMALL)
+    assert _rel(dw2.cpu(), D.cpu().t() @ X.cpu()) < 1e-5 and _rel(db2.cpu(), D.cpu().sum(0)) < 1e-5
+    y = torch.sigmoid(torch.randn(256, 64, device=DEV))
+    g = torch.empty(256, 64, device=DEV)
+    W = torch.randn(64, 100, device=DEV)
+    ops.gemm(X, W, g, M=256, N=64, K=100, aux=y, aux_act=ops.ACT_SIGMOID, tile=ops.TILE_SMALL)
+    exp = (X.cpu() @ W.cpu().t()) * y.cpu() * (1 - y.cpu())
+    assert _rel(g.cpu(), exp) < 1e-5
+
+
 def test_gemm_identity_asymmetric():
     M = N = K = 64
     A = torch.eye(M)
@@ -280,6 +317,26 @@ def test_head_xent():
     assert abs(int(got[6]) - int(exp[6])) <= 2
 
 
+@pytest.mark.parametrize("B", [1024, 300])
+def test_head_wgrad_matches_fp32(B):
+    """Dedicated head weight/bias-gradient kernel vs an fp32 reference of the same product."""
+    torch.manual_seed(11)
+    K, NC = 1024, 10
+    h = torch.relu(torch.randn(B, K)).to(DEV, torch.bfloat16)
+    dl = torch.zeros(B, 16, dtype=torch.bfloat16, device=DEV)
+    dl[:, :NC] = (torch.randn(B, NC) / B).to(DEV, torch.bfloat16)
+    dw = torch.full((NC, K), float("nan"), device=DEV)   # every element must be stored
+    db = torch.full((NC,), float("nan"), device=DEV)
+    ops.head_wgrad(dl, h, dw, db, NC, scale=0.5)
+    ref_w = 0.5 * dl[:, :NC].float().t().cpu() @ h.float().cpu()
+    ref_b = 0.5 * dl[:, :NC].float().sum(0).cpu()
+    assert _rel(dw.cpu(), ref_w) < 1e-5 and _rel(db.cpu(), ref_b) < 1e-5
+    dw2 = torch.empty_like(dw)
+    db2 = torch.empty_like(db)
+    ops.head_wgrad(dl, h, dw2, db2, NC, scale=0.5)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)   # fixed summation order
+
+
 def _plan(n, dev):
     segs = torch.tensor([[0, n, 1, 1, 0, 0]], dtype=torch.int64)
     work = torch.tensor([[0, 0, 0, 0, 0, 0, n]], dtype=torch.int64)
@@ -330,6 +387,49 @@ def test_optimizers_tf1_math(kind):
     assert int(gs.item()) == reps
     if kind == 2:
         assert abs(bp[0].item() - 0.9 ** (reps + 1)) < 1e-6
+
+
+def test_grouped_apply_equals_separate_launches():
+    """Optimizer.step_all (one grouped launch of the GAN's two Adams) == two separate steps,
+    bitwise, including each optimizer's beta powers and the global step."""
+    from dtfe.models.gan import GanModel
+    from dtfe.optim import Optimizer
+    model = GanModel()
+    res = []
+    for grouped in (False, True):
+        prog = model.program(DEV, 32, seed=3)
+        torch.manual_seed(5)
+        prog.P.grad.copy_(torch.randn(prog.P.total))
+        gs = torch.zeros(1, dtype=torch.int32, device=DEV)
+        opts = [Optimizer(c, prog.P, var_list=vl, global_step=gs, beta_power_names=bp) for c, vl, bp in model.opt_groups]
+        for _ in range(3):
+            if grouped:
+                Optimizer.step_all(opts, [0, 2])
+            else:
+                opts[0].step(gs_inc=0)
+                opts[1].step(gs_inc=2)
+        torch.cuda.synchronize()
+        res.append((prog.P.master.cpu(), opts[0].s1.cpu(), opts[1].s2.cpu(), opts[0].beta_pow.cpu(),
+                    opts[1].beta_pow.cpu(), int(gs.item())))
+    for a, b in zip(*res):
+        assert torch.equal(a, b) if torch.is_tensor(a) else a == b
+    assert res[1][5] == 6
+
+
+def test_uniform_fill_fused_copy():
+    x = torch.randn(128, 784, device=DEV)
+    dst = torch.zeros(256, 784, device=DEV)
+    z = torch.empty(128, 100, device=DEV)
+    z2 = torch.empty(128, 100, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    ctr2 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    done2 = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops.uniform_fill(z, -1.0, 1.0, seed=9, counter=ctr, done=done, copy=(x, dst[:128]))
+    ops.uniform_fill(z2, -1.0, 1.0, seed=9, counter=ctr2, done=done2)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:128], x) and float(dst[128:].abs().max()) == 0.0
+    assert torch.equal(z, z2) and int(ctr.item()) == 1 and float(z.abs().max()) <= 1.0
 
 
 def test_optimizer_transposed_copies():
