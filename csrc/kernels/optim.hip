@@ -21,6 +21,10 @@ namespace dtfe {
 
 template <int KIND>
 __device__ __forceinline__ float upd(const OptArgs& a, float lr_t, float v, float g, float& s1, float& s2) {
+  // no multiply-add contraction: the rounding of every update must not depend on how a kernel
+  // instantiation's instruction selection happened to fuse it (a grouped launch of several
+  // optimizers and separate launches must agree bitwise)
+#pragma clang fp contract(off)
   if constexpr (KIND == OPT_SGD) {
     return v - a.lr * g;
   } else if constexpr (KIND == OPT_MOMENTUM) {
