@@ -427,6 +427,34 @@ int data_code(const Tensor& t) {
   TORCH_CHECK(false, "gather_rows: unsupported dtype");
 }
 
+void seq_stage(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Tensor& ysrc, const Tensor& ydst,
+               at::TensorList zero) {
+  check_cuda(x, "x");
+  check_cuda(xh, "xh");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && xh.scalar_type() == at::kFloat && x.is_contiguous() &&
+                  xh.is_contiguous() && xh.dim() == 3 && xh.size(0) == T && xh.size(2) > I,
+              "seq_stage: x f32 [B][T*I], xh f32 [T][B][ld > I] contiguous");
+  const int64_t B = xh.size(1);
+  TORCH_CHECK(x.numel() == B * T * I, "seq_stage: x holds B*T*I floats");
+  TORCH_CHECK(ysrc.scalar_type() == at::kFloat && ydst.scalar_type() == at::kFloat && ysrc.is_contiguous() &&
+                  ydst.is_contiguous() && ysrc.numel() == ydst.numel(),
+              "seq_stage: label rows f32, same size, contiguous");
+  dtfe::SeqStageArgs a{};
+  a.x = x.data_ptr<float>();
+  a.xh = xh.data_ptr<float>();
+  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.ld = (int)xh.size(2);
+  a.ysrc = ysrc.data_ptr<float>(); a.ydst = ydst.data_ptr<float>(); a.ny = ysrc.numel();
+  TORCH_CHECK(zero.size() <= 4, "seq_stage: at most 4 zero ranges");
+  for (const Tensor& z : zero) {
+    check_cuda(z, "zero");
+    TORCH_CHECK(z.is_contiguous() && (z.numel() * z.element_size()) % 4 == 0, "seq_stage: zero ranges must be "
+                "contiguous whole 32-bit words");
+    a.zptr[a.nz] = reinterpret_cast<uint32_t*>(z.data_ptr());
+    a.zlen[a.nz++] = z.numel() * z.element_size() / 4;
+  }
+  dtfe::launch_seq_stage(a, cur_stream());
+}
+
 void gather_rows(const Tensor& src, const Tensor& dst, const optional<Tensor>& idx, const optional<Tensor>& labels_src,
                  const optional<Tensor>& labels_dst, int64_t seed, const optional<Tensor>& counter,
                  const optional<Tensor>& done, at::TensorList zero, const optional<Tensor>& onehot) {
@@ -771,6 +799,7 @@ TORCH_LIBRARY(dtfe, m) {
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
       " float lr, float beta1, float beta2, float eps, float momentum, float rho, Tensor(d!)? beta_pow,"
       " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0) -> ()");
+  m.def("seq_stage(Tensor x, Tensor(a!) xh, int T, int I, Tensor ysrc, Tensor(b!) ydst, Tensor(c!)[] zero) -> ()");
   m.def(
       "gather_rows(Tensor src, Tensor(a!) dst, Tensor? idx, Tensor? labels_src, Tensor(b!)? labels_dst, int seed,"
       " Tensor(c!)? counter, Tensor(d!)? done, Tensor(e!)[] zero, Tensor(f!)? onehot=None) -> ()");
@@ -810,6 +839,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("head_wgrad", &head_wgrad);
   m.impl("apply_gradients", &apply_gradients);
   m.impl("gather_rows", &gather_rows);
+  m.impl("seq_stage", &seq_stage);
   m.impl("uniform_fill", &uniform_fill);
   m.impl("cast_", &cast_);
   m.impl("softmax_xent", &softmax_xent);

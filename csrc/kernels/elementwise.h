@@ -27,6 +27,17 @@ void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, 
                          uint32_t* done, hipStream_t s, const float* csrc = nullptr, float* cdst = nullptr,
                          long ncopy = 0);
 
+// LSTM batch staging in ONE launch (reference lstm/distributed_lstm.py:127 reshape): image rows
+// x[B][T][I] -> the x part of the per-step [x_t, h_{t-1}] rows xh[T][B][ld] (ld = I + H), the h_{-1}
+// part of step 0 zeroed, ny label floats copied, up to 4 word ranges (loss / hit accumulators)
+// cleared.
+struct SeqStageArgs {
+  const float* x; float* xh; int B, T, I, ld;
+  const float* ysrc; float* ydst; long ny;
+  uint32_t* zptr[4]; long zlen[4]; int nz;
+};
+void launch_seq_stage(const SeqStageArgs& a, hipStream_t s);
+
 // dtype casts
 void launch_cast_f32_bf16(const float* src, bf16* dst, long n, hipStream_t s);
 void launch_cast_bf16_f32(const bf16* src, float* dst, long n, hipStream_t s);

@@ -130,6 +130,34 @@ void launch_uniform_fill(float* out, long n, float lo, float hi, uint64_t seed, 
                      cdst, ncopy);
 }
 
+__global__ __launch_bounds__(256) void seq_stage_kernel(SeqStageArgs a) {
+  const long tid = blockIdx.x * 256L + threadIdx.x, nth = (long)gridDim.x * 256;
+  // x part: one (t, b) row of I floats per I consecutive work items (coalesced reads of image b's
+  // row t, coalesced writes of xh row (t, b))
+  const long nx = (long)a.T * a.B * a.I;
+  for (long i = tid; i < nx; i += nth) {
+    const long row = i / a.I, c = i - row * a.I;  // row = t * B + b
+    const long t = row / a.B, b = row - t * a.B;
+    a.xh[row * a.ld + c] = a.x[(b * a.T + t) * a.I + c];
+  }
+  const int hw = a.ld - a.I;  // h_{-1} = 0 (step 0 only; later steps are written by the recurrence)
+  for (long i = tid; i < (long)a.B * hw; i += nth) {
+    const long b = i / hw;
+    a.xh[b * a.ld + a.I + (i - b * hw)] = 0.f;
+  }
+  for (long i = tid; i < a.ny; i += nth) a.ydst[i] = a.ysrc[i];
+  for (int z = 0; z < a.nz; ++z)
+    for (long i = tid; i < a.zlen[z]; i += nth) a.zptr[z][i] = 0u;
+}
+
+void launch_seq_stage(const SeqStageArgs& a, hipStream_t s) {
+  long work = (long)a.T * a.B * a.I;
+  long blocks = (work + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(seq_stage_kernel, dim3(blocks), dim3(256), 0, s, a);
+}
+
 __global__ void cast_f32_bf16_kernel(const float* src, bf16* dst, long n) {
   const long n4 = n / 4;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {

@@ -79,7 +79,13 @@ class LstmProgram(StepProgram):
     def load_batch(self, batch):
         x, y = batch
         B = self.batch_size
-        # batch_x.reshape((B, timesteps, num_input)) (LSTM:127): row t of the image is step t
+        # batch_x.reshape((B, timesteps, num_input)) (LSTM:127): row t of the image is step t.
+        # One launch stages x, zeroes h_{-1}, copies the labels and clears the step's loss / hit
+        # accumulators (compute_grads then skips its own clearing).
+        if x.dtype == torch.float32 and y.dtype == torch.float32 and x.numel() == B * T * I and y.numel() == B * NC:
+            ops.seq_stage(x, self.xh, T, I, y, self.y, zero=(self.loss, self.correct))
+            self._acc_cleared = True
+            return
         self.xh[:, :, :I].copy_(x.reshape(B, T, I).transpose(0, 1))
         self.xh[0, :, I:].zero_()
         self.y.copy_(y.reshape(B, NC))
@@ -107,8 +113,10 @@ class LstmProgram(StepProgram):
     def compute_grads(self):
         B = self.batch_size
         # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
-        self.loss.zero_()
-        self.correct.zero_()
+        if not getattr(self, "_acc_cleared", False):
+            self.loss.zero_()
+            self.correct.zero_()
+        self._acc_cleared = False
         self.forward()
         ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
                          correct=self.correct)
@@ -142,6 +150,7 @@ class LstmProgram(StepProgram):
         n, B = images.shape[0], self.batch_size
         if n == B:
             self.load_batch((images, labels))
+            self._acc_cleared = False
             self.forward()
             self.correct.zero_()
             ops.softmax_xent(self.logits, labels_oh=self.y, correct=self.correct)
@@ -152,6 +161,7 @@ class LstmProgram(StepProgram):
             idx = torch.arange(lo, lo + B, device=images.device).clamp_max(n - 1)
             xb, yb = images[idx], labels[idx]
             self.load_batch((xb, yb))
+            self._acc_cleared = False
             self.forward()
             hits += int((self.logits[:m].argmax(1) == self.y[:m].argmax(1)).sum().item())
         return hits / n

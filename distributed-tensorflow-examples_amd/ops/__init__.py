@@ -25,7 +25,7 @@ __all__ = [
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "shortcut_grad_add",
-    "gap_fwd", "gap_bwd", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
+    "gap_fwd", "gap_bwd", "seq_stage", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -535,6 +535,22 @@ def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, mome
 
 
 # ------------------------------------------------------------- elementwise
+def seq_stage(x, xh, T, I, y_src, y_dst, zero=()):
+    """LSTM batch staging (one launch on the GPU): xh[t, b, :I] = x[b, t*I:(t+1)*I] (image row t
+    is timestep t), xh[0, :, I:] = 0 (h_{-1}), y_dst = y_src, and the tensors in ``zero`` (up to 4
+    accumulators) cleared."""
+    if xh.is_cuda:
+        require().seq_stage(x.reshape(-1).contiguous(), xh, int(T), int(I), y_src.reshape(-1).contiguous(),
+                            y_dst, list(zero))
+        return
+    B = xh.shape[1]
+    xh[:, :, :I].copy_(x.reshape(B, T, I).transpose(0, 1))
+    xh[0, :, I:].zero_()
+    y_dst.copy_(y_src.reshape(y_dst.shape))
+    for z in zero:
+        z.zero_()
+
+
 def gather_rows(src, dst, idx=None, labels_src=None, labels_dst=None, seed=0, counter=None, done=None, zero=(),
                 onehot=None):
     """dst[b] = src[row(b)] (+ labels); ``zero``: up to 4 contiguous tensors cleared in the same

@@ -519,3 +519,24 @@ def test_softmax_xent_and_losses():
     l2, d2 = torch.empty(1), torch.empty(256, 784)
     ops.mse_sigmoid(y.cpu(), tt.cpu(), l2, d2)
     assert _rel(l1.cpu(), l2) < 1e-4 and _rel(d1.cpu(), d2) < 1e-4
+
+
+@pytest.mark.parametrize("B", [128, 37])
+def test_seq_stage_matches_reference(B):
+    """seq_stage (LSTM batch staging in one launch) == the CPU reference: x rows transposed into
+    the [T][B][I+H] step rows, h_{-1} zeroed, labels copied, accumulators cleared."""
+    T, I, H, NC = 28, 28, 128, 10
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(B, T * I, generator=g)
+    y = torch.rand(B, NC, generator=g)
+    xh_ref = torch.randn(T, B, I + H, generator=g)
+    xh = xh_ref.to(DEV)
+    y_dst = torch.full((B, NC), 7.0, device=DEV)
+    acc_f, acc_i = torch.ones(1, device=DEV), torch.ones(3, dtype=torch.int32, device=DEV)
+    ops.seq_stage(x.to(DEV), xh, T, I, y.to(DEV), y_dst, zero=(acc_f, acc_i))
+    y_ref, zf, zi = torch.empty(B, NC), torch.ones(1), torch.ones(3, dtype=torch.int32)
+    ops.seq_stage(x, xh_ref, T, I, y, y_ref, zero=(zf, zi))
+    torch.cuda.synchronize()
+    assert torch.equal(xh.cpu(), xh_ref)
+    assert torch.equal(y_dst.cpu(), y_ref)
+    assert acc_f.item() == 0.0 and int(acc_i.abs().sum().item()) == 0
