@@ -30,3 +30,16 @@ for tile, splits in [(None, 1), (13, 1), (4, 1), (4, 4), (4, 8), (4, 16), (0, 1)
     for _ in range(50): run()
     e.record(); torch.cuda.synchronize()
     print("tile", tile, "splits", splits, "us %.1f" % (s.elapsed_time(e) / 50 * 1e3), "maxerr %.2e" % err, flush=True)
+
+for splits in (8, 16, 32, 56, 112):
+    ws = torch.empty(ops.tallk_ws_floats(I + H, 4 * H, splits), device=dev)
+    def run():
+        ops.wgrad_tallk(xh, I + H, dg, 4 * H, I + H, 4 * H, T * B, gK, bias=gb, splits=splits, workspace=ws)
+    run(); torch.cuda.synchronize()
+    err = max((gK.double() - ref[:-1]).abs().max().item(), (gb.double() - ref[-1]).abs().max().item())
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(5): run()
+    s.record()
+    for _ in range(50): run()
+    e.record(); torch.cuda.synchronize()
+    print("tallk splits", splits, "us %.1f" % (s.elapsed_time(e) / 50 * 1e3), "maxerr %.2e" % err, flush=True)

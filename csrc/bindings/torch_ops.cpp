@@ -427,6 +427,30 @@ int data_code(const Tensor& t) {
   TORCH_CHECK(false, "gather_rows: unsupported dtype");
 }
 
+void wgrad_tallk(const Tensor& A, int64_t lda, const Tensor& B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                 const Tensor& out, int64_t ldc, const optional<Tensor>& bias, const Tensor& ws, int64_t splits,
+                 double scale) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  check_cuda(out, "out");
+  TORCH_CHECK(A.scalar_type() == at::kFloat && B.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat &&
+                  ws.scalar_type() == at::kFloat,
+              "wgrad_tallk: fp32 operands / output / workspace");
+  TORCH_CHECK(A.numel() >= (K - 1) * lda + M && B.numel() >= (K - 1) * ldb + N && out.numel() >= (M - 1) * ldc + N,
+              "wgrad_tallk: operand / output extents");
+  TORCH_CHECK(ws.numel() >= dtfe::tallk_ws_floats((int)M, (int)N, (int)splits), "wgrad_tallk: workspace too small");
+  if (bias) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "wgrad_tallk: bias [N] fp32");
+  dtfe::TallKArgs a{};
+  a.A = A.data_ptr<float>(); a.lda = (int)lda;
+  a.B = B.data_ptr<float>(); a.ldb = (int)ldb;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.out = out.data_ptr<float>(); a.ldc = (int)ldc;
+  a.bias = bias ? bias->data_ptr<float>() : nullptr;
+  a.ws = ws.data_ptr<float>(); a.splits = (int)splits;
+  a.scale = (float)scale;
+  dtfe::launch_wgrad_tallk(a, cur_stream());
+}
+
 void seq_stage(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Tensor& ysrc, const Tensor& ydst,
                at::TensorList zero) {
   check_cuda(x, "x");
@@ -799,6 +823,8 @@ TORCH_LIBRARY(dtfe, m) {
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
       " float lr, float beta1, float beta2, float eps, float momentum, float rho, Tensor(d!)? beta_pow,"
       " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0) -> ()");
+  m.def("wgrad_tallk(Tensor A, int lda, Tensor B, int ldb, int M, int N, int K, Tensor(a!) out, int ldc,"
+        " Tensor(b!)? bias, Tensor(c!) ws, int splits, float scale) -> ()");
   m.def("seq_stage(Tensor x, Tensor(a!) xh, int T, int I, Tensor ysrc, Tensor(b!) ydst, Tensor(c!)[] zero) -> ()");
   m.def(
       "gather_rows(Tensor src, Tensor(a!) dst, Tensor? idx, Tensor? labels_src, Tensor(b!)? labels_dst, int seed,"
@@ -840,6 +866,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("apply_gradients", &apply_gradients);
   m.impl("gather_rows", &gather_rows);
   m.impl("seq_stage", &seq_stage);
+  m.impl("wgrad_tallk", &wgrad_tallk);
   m.impl("uniform_fill", &uniform_fill);
   m.impl("cast_", &cast_);
   m.impl("softmax_xent", &softmax_xent);

@@ -158,12 +158,14 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
 // ------------------------------------------------------------ weight grad
 constexpr int DP = NCH;  // dY image pitch (elements per pixel)
 
-__global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
+__global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int diag) {
   __shared__ __attribute__((aligned(16))) bf16 P[PRW * PWD];
   __shared__ __attribute__((aligned(16))) bf16 C[5 * CSZ];
   __shared__ __attribute__((aligned(16))) bf16 D[HI * 32 * DP];  // dY [oy][ox < 32][n]
   constexpr int RL = 32 * 32 + 32;      // one wave's partial dW[n][tap < 32] + db[n]
-  __shared__ float red[4 * RL];
+  // the cross-wave partials reuse D (dead after the image loop): ~73 KB of LDS, two workgroups per CU
+  static_assert(4 * RL * 4 <= HI * 32 * DP * 2, "partials must fit in the dY image");
+  float* red = reinterpret_cast<float*>(D);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
   const int q4 = i16 >> 2, p4 = i16 & 3;
   for (int i = threadIdx.x; i < PRW * PWD / 8; i += TH) reinterpret_cast<u32x4_t*>(P)[i] = u32x4_t{0u, 0u, 0u, 0u};
@@ -233,12 +235,12 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
   __syncthreads();
   for (; b < a.B; b += gridDim.x) {
     write_img(P, xv);
-    write_dy();
+    if (!(diag & 1)) write_dy();
     __syncthreads();
     if (b + gridDim.x < a.B) load_all(b + gridDim.x);
-    build_copies<5>(P, C);
+    if (!(diag & 2)) build_copies<5>(P, C);
     __syncthreads();
-    for (int oy = wid; oy < HI; oy += 4) {
+    for (int oy = wid; oy < ((diag & 4) ? 0 : HI); oy += 4) {
       bf16x8_t af[2];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
@@ -260,6 +262,10 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a) {
       }
     }
     __syncthreads();
+  }
+  if (diag & 8) {  // ablation: keep the loads live without the flush
+    if (a.ws && acc[0][0][0] == 12345.f) a.ws[blockIdx.x] = dbacc[0];
+    return;
   }
   // cross-wave reduction in LDS: every wave stores its own partial (no LDS float atomics), the
   // flush sums the 4 in wave order - the weight gradient is bitwise reproducible
@@ -315,8 +321,20 @@ bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s) {
 bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s) {
   if (!mnist_conv1_shape(a.B, a.SH, a.SW, a.CS, a.OH, a.OW, a.N, a.KH, a.KW, a.stride, a.pad)) return false;
   if (!a.src || a.dy || !a.dy_pooled) return false;
-  const int grid = a.B < 256 ? a.B : 256;
-  hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a);
+  // DTFE_C1W_GRID: workgroups (images per workgroup = B / grid); DTFE_C1W_DIAG: ablation bits
+  // (1 skip the un-pooled dY image, 2 skip the shifted copies, 4 skip the MFMA tiles, 8 skip the flush)
+  static const int want = [] {
+    const char* e = getenv("DTFE_C1W_GRID");
+    return e ? atoi(e) : 256;
+  }();
+  static const int diag = [] {
+    const char* e = getenv("DTFE_C1W_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  const int grid = a.B < want ? a.B : (want < 1 ? 1 : want);
+  if (a.ws && (long)grid * (NCH * 25 + NCH) > imgwgrad_ws_floats(NCH, 25))
+    throw std::runtime_error("conv1 wgrad: partials exceed the workspace");
+  hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a, diag);
   if (a.ws) {
     constexpr int LEN = NCH * 25 + NCH;
     launch_partials_reduce(a.ws, grid, LEN, NCH * 25, a.dw, a.db, a.scale, s);

@@ -22,3 +22,20 @@ bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s);
 bool launch_lstm_seq_bwd(const LstmSeqArgs& a, hipStream_t s);
 
 }  // namespace dtfe
+
+namespace dtfe {
+// tall-K exact-fp32 weight gradient (csrc/kernels/wgrad_tallk.hip): out[m][n] = scale * sum_k
+// A[k*lda+m] B[k*ldb+n] (stored, m < M), bias[n] = scale * sum_k B[k*ldb+n] (optional)
+struct TallKArgs {
+  const float* A; int lda;
+  const float* B; int ldb;
+  int M, N, K;
+  float* out; int ldc;
+  float* bias;
+  float* ws; int splits;
+  float scale;
+  int MP, kchunk;  // set by the launcher
+};
+long tallk_ws_floats(int M, int N, int splits);
+void launch_wgrad_tallk(const TallKArgs& a, hipStream_t s);
+}  // namespace dtfe

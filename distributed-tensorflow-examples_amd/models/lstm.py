@@ -75,6 +75,11 @@ class LstmProgram(StepProgram):
         self.K, self.b = self.P.view(m.kname), self.P.view(m.bname)
         self.gWo, self.gbo = self.P.gview("Variable"), self.P.gview("Variable_1")
         self.gK, self.gb = self.P.gview(m.kname), self.P.gview(m.bname)
+        # the kernel gradient's own split-K workspace (DTFE_LSTM_TALLK=0: the generic GEMM instead)
+        self.k_splits = int(os.environ.get("DTFE_LSTM_KSPLITS", "32"))
+        self.ws_k = None
+        if self.device.type == "cuda" and os.environ.get("DTFE_LSTM_TALLK", "1") != "0":
+            self.ws_k = torch.empty(ops.tallk_ws_floats(I + H, 4 * H, self.k_splits), **f)
 
     def load_batch(self, batch):
         x, y = batch
@@ -127,8 +132,12 @@ class LstmProgram(StepProgram):
             pass  # whole BPTT recurrence in one launch (dc / dh stay on chip)
         else:
             self._bptt_steps()
-        ops.gemm(self.xh, self.dg, self.gK, M=I + H + 1, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H,
-                 bmode=ops.RMAJ, ldb=4 * H, a_ones_row=I + H, bias_out=self.gb)
+        if self.ws_k is not None:  # kernel + bias gradient over all T*B rows: split-K slabs (wgrad_tallk.hip)
+            ops.wgrad_tallk(self.xh, I + H, self.dg, 4 * H, I + H, 4 * H, T * B, self.gK, bias=self.gb,
+                            splits=self.k_splits, workspace=self.ws_k)
+        else:
+            ops.gemm(self.xh, self.dg, self.gK, M=I + H + 1, N=4 * H, K=T * B, amode=ops.RMAJ, lda=I + H,
+                     bmode=ops.RMAJ, ldb=4 * H, a_ones_row=I + H, bias_out=self.gb)
         return {"loss": ScaledScalar(self.loss, 1.0 / B)}
 
     def _bptt_steps(self):

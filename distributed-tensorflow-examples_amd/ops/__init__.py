@@ -25,7 +25,7 @@ __all__ = [
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "shortcut_grad_add",
-    "gap_fwd", "gap_bwd", "seq_stage", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
+    "gap_fwd", "gap_bwd", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -535,6 +535,28 @@ def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, mome
 
 
 # ------------------------------------------------------------- elementwise
+def tallk_ws_floats(M: int, N: int, splits: int) -> int:
+    """Partial-slab floats of wgrad_tallk (mirrors tallk_ws_floats in csrc/kernels/wgrad_tallk.hip)."""
+    return splits * ((M + 1 + 15) // 16 * 16) * N
+
+
+def wgrad_tallk(A, lda, B, ldb, M, N, K, out, ldc=None, bias=None, splits=32, scale=1.0, workspace=None):
+    """Exact-fp32 weight gradient of a long reduction: out[m][n] = scale * sum_k A[k*lda+m] B[k*ldb+n]
+    (stored), bias[n] = scale * sum_k B[k*ldb+n] (the LSTM kernel / bias gradient over T*B rows).
+    GPU: K split over `splits` workgroups per 64-column slab + a fixed-order partial reduce."""
+    ldc = N if ldc is None else ldc
+    if out.is_cuda:
+        ws = workspace if workspace is not None else wgrad_workspace(out.device, tallk_ws_floats(M, N, splits))
+        require().wgrad_tallk(A, lda, B, ldb, M, N, K, out, ldc, bias, ws, splits, scale)
+        return out
+    a = torch.as_strided(A.reshape(-1), (K, M), (lda, 1)).double()
+    b = torch.as_strided(B.reshape(-1), (K, N), (ldb, 1)).double()
+    torch.as_strided(out.view(-1), (M, N), (ldc, 1)).copy_((scale * (a.t() @ b)).float())
+    if bias is not None:
+        bias.copy_((scale * b.sum(0)).float())
+    return out
+
+
 def seq_stage(x, xh, T, I, y_src, y_dst, zero=()):
     """LSTM batch staging (one launch on the GPU): xh[t, b, :I] = x[b, t*I:(t+1)*I] (image row t
     is timestep t), xh[0, :, I:] = 0 (h_{-1}), y_dst = y_src, and the tensors in ``zero`` (up to 4

@@ -11,6 +11,7 @@ exact PyTorch path with the same formulas.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -176,7 +177,10 @@ class Optimizer:
             self._build_plan()
 
     # ---- plan of work items for the fused kernel
-    def _build_plan(self, chunk: int = 8192):
+    def _build_plan(self, chunk: int = 0):
+        # flat work items of `chunk` elements (DTFE_OPT_CHUNK; multiple of 1024): one workgroup
+        # each, up to 2048 workgroups per launch
+        chunk = chunk or int(os.environ.get("DTFE_OPT_CHUNK", "8192"))
         segs, work = [], []
         for si, name in enumerate(self.var_list):
             s = self.P.spec(name)

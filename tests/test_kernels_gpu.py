@@ -540,3 +540,22 @@ def test_seq_stage_matches_reference(B):
     assert torch.equal(xh.cpu(), xh_ref)
     assert torch.equal(y_dst.cpu(), y_ref)
     assert acc_f.item() == 0.0 and int(acc_i.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(156, 512, 3584, 32), (156, 512, 3584, 7), (30, 64, 101, 4), (100, 128, 5, 32)])
+def test_wgrad_tallk_matches_fp64(M, N, K, splits):
+    """Tall-K fp32 weight gradient (LSTM kernel/bias grads) vs a float64 reference, strided rows."""
+    g = torch.Generator().manual_seed(M + K)
+    lda, ldb = M + 3, N + 8
+    A = torch.randn(K, lda, generator=g)
+    Bm = torch.randn(K, ldb, generator=g)
+    out = torch.full((M, N + 5), 9.0, device=DEV)
+    bias = torch.full((N,), 9.0, device=DEV)
+    ops.wgrad_tallk(A.to(DEV), lda, Bm.to(DEV), ldb, M, N, K, out, ldc=N + 5, bias=bias, splits=splits, scale=0.5)
+    ref = 0.5 * (A[:, :M].double().t() @ Bm[:, :N].double())
+    rb = 0.5 * Bm[:, :N].double().sum(0)
+    torch.cuda.synchronize()
+    o = out.cpu().double()
+    assert (o[:, :N] - ref).abs().max().item() <= 1e-4 * (ref.abs().max().item() + 1)
+    assert (o[:, N:] == 9.0).all()  # columns past N untouched
+    assert (bias.cpu().double() - rb).abs().max().item() <= 1e-4 * (rb.abs().max().item() + 1)
