@@ -4,12 +4,9 @@
 // Layout: NHWC bf16 viewed as [R][C] rows with C % 8 == 0 and C/8 a power of
 // two; every thread owns one 16-byte chunk (8 channels) of a row, so loads and
 // stores are 16 B vectors and a warp-wide load covers whole 128 B lines.
-// Channel statistics are reduced per workgroup through LDS into a per-workgroup partial slot;
-// a second launch sums the slots in workgroup order into the [2][C] accumulators.  (The former
-// one-atomic-per-channel-and-workgroup flush serialised up to 256 same-address float atomics
-// per channel: ~10 us of the 13-15 us statistics passes of the small ResNet-20 layers.)
+// Channel statistics are reduced per workgroup through LDS and then added to
+// the [2][C] accumulators with one atomic per channel and workgroup.
 #include "norm.h"
-#include "imgconv.h"  // launch_partials_reduce (fixed-order slot sum)
 
 #include <stdexcept>
 
@@ -47,12 +44,8 @@ struct Slots {
   }
 };
 
-__constant__ int bn_legacy_flush;  // DTFE_BN_LEGACY=1 (A/B only)
-
-// block-reduce s[8], q[8] of every thread onto channels: part[0..C) = sum s, part[C..2C) = sum q
-// (fixed summation order within the workgroup).  slots: plain stores into this workgroup's slot
-// (summed by a second launch); otherwise one atomic add per value into part = the accumulators.
-__device__ void reduce_stats(const float (&s)[8], const float (&q)[8], int C, float* part, bool slots) {
+// block-reduce s[8], q[8] of every thread onto channels and add them to stats[0..C), stats[C..2C)
+__device__ void reduce_stats(const float (&s)[8], const float (&q)[8], int C, float* stats) {
   extern __shared__ float red[];  // [rpp][2][C]
   const Slots S(C);
   float* mine = red + S.slot * 2 * C;
@@ -62,31 +55,10 @@ __device__ void reduce_stats(const float (&s)[8], const float (&q)[8], int C, fl
     mine[C + S.chunk * 8 + e] = q[e];
   }
   __syncthreads();
-  const int V = 2 * C;
-  if (!slots && bn_legacy_flush) {  // A/B: one thread per value sums every row slot
-    for (int c = threadIdx.x; c < V; c += NT) {
-      float v = 0.f;
-      for (int r = 0; r < S.rpp; ++r) v += red[r * V + c];
-      atomicAdd(part + c, v);
-    }
-    return;
-  }
-  if (V <= NT) {  // T threads per value (a power of two <= 16), each summing every T-th row slot
-    const int T = NT / V, v = threadIdx.x / T, j = threadIdx.x % T;
-    float t = 0.f;
-    for (int r = j; r < S.rpp; r += T) t += red[r * V + v];
-    for (int o = T / 2; o > 0; o >>= 1) t += __shfl_down(t, o, T);
-    if (j == 0) {
-      if (slots) part[v] = t;
-      else atomicAdd(part + v, t);
-    }
-  } else {
-    for (int c = threadIdx.x; c < V; c += NT) {
-      float v = 0.f;
-      for (int r = 0; r < S.rpp; ++r) v += red[r * V + c];
-      if (slots) part[c] = v;
-      else atomicAdd(part + c, v);
-    }
+  for (int c = threadIdx.x; c < 2 * C; c += NT) {
+    float v = 0.f;
+    for (int r = 0; r < S.rpp; ++r) v += red[r * 2 * C + c];
+    atomicAdd(stats + c, v);
   }
 }
 
@@ -100,7 +72,7 @@ __device__ __forceinline__ u32x4_t ld16(const bf16* p) { return *reinterpret_cas
 // Statistics are accumulated around a per-channel shift K = x[row 0][c] (sum (x-K), sum (x-K)^2):
 // the one-pass E[x^2] - E[x]^2 form loses the variance to cancellation when |mean| >> std.
 // Rows past the end re-read row 0 (= K), which contributes exactly zero.
-__global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a, float* part, int slots) {
+__global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   const Slots S(a.C);
   float k[8];
   unpack8(ld16(a.x + S.chunk * 8), k);
@@ -125,7 +97,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a, float* part, int
       }
     }
   }
-  reduce_stats(s, q, a.C, slots ? part + (long)blockIdx.x * 2 * a.C : a.stats, slots);
+  reduce_stats(s, q, a.C, a.stats);
 }
 
 __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean, float& invstd) {
@@ -235,7 +207,7 @@ __device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, c
   }
 }
 
-__global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a, float* part, int slots) {
+__global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   const Slots S(a.C);
   const BwdMask M(a, S.chunk);
   const bool need_y = a.act != ACT_NONE && !M.from_x;
@@ -271,7 +243,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a, float* part,
       }
     }
   }
-  reduce_stats(s, q, a.C, slots ? part + (long)blockIdx.x * 2 * a.C : a.stats, slots);
+  reduce_stats(s, q, a.C, a.stats);
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
@@ -325,8 +297,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
   }
 }
 
-// Statistics kernels: at most 512 workgroups (one partial slot each), each looping over
-// U_STATS-row batches.  Apply kernels: one U_APPLY-row
+// Statistics kernels: few enough workgroups that the per-channel atomics stay cheap
+// (about 2 per CU), each looping over U_STATS-row batches.  Apply kernels: one U_APPLY-row
 // batch per thread, as many workgroups as that takes (no atomics to amortise).
 int stats_grid(long R, int C) {
   const long rows_per_block = (long)(NT / (C / 8)) * U_STATS;
@@ -490,43 +462,10 @@ int ew_grid(long n) {
 
 }  // namespace
 
-// per-device partial-slot workspace of the statistics kernels: 512 slots x 2C <= 4096 floats,
-// allocated once (a captured hipGraph keeps the pointer); single-stream use like the other
-// cached workspaces
-constexpr long BN_PART_FLOATS = 512L * 4096;
-// DTFE_BN_SLOTS=1: per-workgroup slots + a fixed-order reduce launch (bitwise reproducible);
-// default: one float atomic per value and workgroup (no second launch in the graph)
-bool bn_slots() {
-  static const bool legacy_set = [] {
-    const char* e = getenv("DTFE_BN_LEGACY");
-    const int v = e ? atoi(e) : 0;
-    return hipMemcpyToSymbol(HIP_SYMBOL(bn_legacy_flush), &v, sizeof(int)) == hipSuccess;
-  }();
-  (void)legacy_set;
-  static const int v = [] {
-    const char* e = getenv("DTFE_BN_SLOTS");
-    return e ? atoi(e) : 0;
-  }();
-  return v != 0;
-}
-
-float* bn_part_ws() {
-  static float* ws[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw std::runtime_error("bn: hipGetDevice");
-  if (!ws[dev] && hipMalloc(&ws[dev], BN_PART_FLOATS * sizeof(float)) != hipSuccess)
-    throw std::runtime_error("bn: workspace allocation failed");
-  return ws[dev];
-}
-
 void launch_bn_stats(const BnArgs& a, hipStream_t s) {
   check(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  const int grid = stats_grid(a.R, a.C);
-  const bool slots = bn_slots();
-  float* part = slots ? bn_part_ws() : nullptr;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(grid), dim3(NT), lds, s, a, part, (int)slots);
-  if (slots) launch_partials_reduce(part, grid, 2 * a.C, 2 * a.C, a.stats, nullptr, 1.f, s);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(stats_grid(a.R, a.C)), dim3(NT), lds, s, a);
 }
 
 void launch_bn_apply(const BnArgs& a, hipStream_t s) {
@@ -544,11 +483,7 @@ void check_bwd(const BnArgs& a) {
 void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s) {
   check_bwd(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  const int grid = stats_grid(a.R, a.C);
-  const bool slots = bn_slots();
-  float* part = slots ? bn_part_ws() : nullptr;
-  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(grid), dim3(NT), lds, s, a, part, (int)slots);
-  if (slots) launch_partials_reduce(part, grid, 2 * a.C, 2 * a.C, a.stats, nullptr, 1.f, s);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(stats_grid(a.R, a.C)), dim3(NT), lds, s, a);
 }
 
 void launch_bn_bwd_apply(const BnArgs& a, hipStream_t s) {
