@@ -41,6 +41,34 @@ int dtype_code(const Tensor& t) {
 }
 
 // ------------------------------------------------------------------- gemm
+// A head weight gradient queued by head_wgrad_fuse() rides in the NEXT gemm() launch of this
+// thread (global_load_lds tiles only): ops.gemm(..., head=...) issues the two back to back.
+thread_local dtfe::HeadFuse g_pending_head{};
+
+void head_wgrad_fuse(const Tensor& dl, const Tensor& h, const Tensor& dw, const optional<Tensor>& db, int64_t nc,
+                     double scale) {
+  TORCH_CHECK(g_pending_head.blocks == 0, "head_wgrad_fuse: a queued head gradient was never launched");
+  TORCH_CHECK(nc == 10, "head_wgrad_fuse: 10 classes");
+  TORCH_CHECK(dl.scalar_type() == at::kBFloat16 && h.scalar_type() == at::kBFloat16 && dl.dim() == 2 && h.dim() == 2 &&
+                  dl.size(0) == h.size(0) && dl.stride(1) == 1 && h.stride(1) == 1 && dl.size(1) >= 16,
+              "head_wgrad_fuse: bf16 dl [B][>=16] and h [B][K]");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.size(0) == nc && dw.stride(1) == 1 &&
+                  dw.size(1) >= h.size(1),
+              "head_wgrad_fuse: fp32 dw [10][>=K]");
+  dtfe::HeadFuse f{};
+  f.dl = reinterpret_cast<const dtfe::bf16*>(dl.data_ptr()); f.ld_dl = (int)dl.stride(0);
+  f.h = reinterpret_cast<const dtfe::bf16*>(h.data_ptr()); f.ldh = (int)h.stride(0);
+  f.dw = dw.data_ptr<float>(); f.ldw = (int)dw.stride(0);
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() >= nc, "head_wgrad_fuse: fp32 db [10]");
+    f.db = db->data_ptr<float>();
+  }
+  f.B = (int)h.size(0); f.K = (int)h.size(1); f.scale = (float)scale;
+  TORCH_CHECK(f.K % 16 == 0 && f.B <= 1024, "head_wgrad_fuse: K % 16 == 0, B <= 1024");
+  f.blocks = (f.K / 16 + (f.db ? 1 : 0) + 7) / 8 * 8;
+  g_pending_head = f;
+}
+
 void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t bmode, int64_t ldb, int64_t M,
           int64_t N, int64_t K, const Tensor& out, int64_t ldc, const optional<Tensor>& bias, int64_t bias_axis,
           int64_t act, double alpha, double beta, bool atomic, int64_t splits, int64_t tile,
@@ -101,6 +129,12 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   a.bias_out = ptr_or_null<float>(bias_out);
   TORCH_CHECK(!a.bias_out || b_ones_row >= 0 || a_ones_row >= 0, "gemm: bias_out needs a ones row");
   a.ones = ptr_or_null<dtfe::bf16>(ones);
+  if (g_pending_head.blocks) {
+    a.hw = g_pending_head;
+    g_pending_head = dtfe::HeadFuse{};
+    TORCH_CHECK(tile >= 5 && tile != dtfe::GEMM_TILE_SMALL && real_splits == 1,
+                "gemm: a fused head weight gradient needs a global_load_lds tile and one split");
+  }
   if (tile == dtfe::GEMM_TILE_SMALL) {
     TORCH_CHECK(real_splits == 1 && dtfe::gemm_small_eligible(dt == 0 ? 0 : 1, a),
                 "gemm: the small-tile kernel takes fp32 operands, one split, no un-pool epilogue");
@@ -817,6 +851,7 @@ TORCH_LIBRARY(dtfe, m) {
       "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl,"
       " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep,"
       " Tensor(f!)? step_counter=None) -> ()");
+  m.def("head_wgrad_fuse(Tensor dl, Tensor h, Tensor(a!) dw, Tensor(b!)? db, int nc, float scale) -> ()");
   m.def("head_wgrad(Tensor dl, Tensor h, Tensor(a!) dw, Tensor(b!)? db, int nc, float scale) -> ()");
   m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
   m.def(
@@ -866,6 +901,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("apply_gradients", &apply_gradients);
   m.impl("gather_rows", &gather_rows);
   m.impl("seq_stage", &seq_stage);
+  m.impl("head_wgrad_fuse", &head_wgrad_fuse);
   m.impl("wgrad_tallk", &wgrad_tallk);
   m.impl("uniform_fill", &uniform_fill);
   m.impl("cast_", &cast_);

@@ -409,11 +409,14 @@ __device__ __forceinline__ void for_each_quad(int m_base, int n_base, f32x4_t (&
 
 // Map a flat block id to (tile_m, tile_n) with XCD-aware grouping so blocks
 // sharing an A panel (same tile_m) run on one XCD's L2.
-__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int nwg = tiles_m * tiles_n;
-  const int id = xcd_remap(blockIdx.x, nwg);
+  const int id = xcd_remap(bid, nwg);
   tm = id / tiles_n;
   tn = id % tiles_n;
+}
+__device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
+  tile_coords(blockIdx.x, tiles_m, tiles_n, tm, tn);
 }
 
 }  // namespace dtfe

@@ -8,6 +8,18 @@ namespace dtfe {
 
 constexpr int GEMM_KTILE = 64;  // k-tile depth of the dense GEMMs (2 MFMA k-steps per barrier)
 
+// A classifier-head weight gradient riding in the same launch as a global_load_lds GEMM (the MNIST
+// CNN's fc1 data gradient): dw[n][k] = scale * sum_b dl[b][n] h[b][k], db[n] = scale * sum_b dl[b][n]
+// for n < 10, computed by `blocks` extra workgroups placed before the GEMM tiles (see gemm_glds.h)
+struct HeadFuse {
+  const bf16* dl; int ld_dl;   // [B][ld_dl] bf16 dlogit rows (>= 16 wide, 16-B aligned)
+  const bf16* h; int ldh;      // [B][ldh] bf16 activations
+  float* dw; int ldw;          // [10][ldw]
+  float* db;                   // [10] (optional)
+  int B, K, blocks;            // blocks: K/16 (+1 with db), rounded up to a multiple of 8 (0 = none)
+  float scale;
+};
+
 struct DenseGemmArgs {
   int M, N, K;
   const void* A; long lda;     // A(m,k): KMAJ a[m*lda+k], RMAJ a[k*lda+m]
@@ -38,6 +50,7 @@ struct DenseGemmArgs {
   // global_load_lds kernel (tiles 5..8): a 1 KB page of bf16 ones, read by the whole n-tile that
   // starts at b_ones_row (the bias column of a weight-gradient GEMM sits past the operand's rows)
   const bf16* ones;
+  HeadFuse hw;                 // optional fused head weight gradient (glds tiles, one split)
 };
 
 // Epilogue of one output element (row < M, col < N); returns false when the

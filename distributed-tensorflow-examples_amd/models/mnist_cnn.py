@@ -204,6 +204,11 @@ class MnistCnnTrainer:
         # capture order of the branched backward (DTFE_CNN_ORDER): "branch" = each branch's work
         # captured before the critical chain continues, "crit" = the critical chain first
         self.crit_first = os.environ.get("DTFE_CNN_ORDER", "branch") == "crit"
+        # DTFE_CNN_FC1W_SPLIT=2: fc1's weight gradient as two launches of half the rows.  The hipGraph
+        # runtime executes dependency level by level: with the head gradient fused into fc1 dgrad, a
+        # single fc1 wgrad node sits on fc1 dgrad's level and holds the conv2 stage back; split, its
+        # second half lands on the conv2 stage's level
+        self.fc1w_split = int(os.environ.get("DTFE_CNN_FC1W_SPLIT", "1"))
         self.br_one = self.par and "side1" in br   # ONE weight-grad branch forked after fc1 dgrad
         self.br_fc = self.par and not self.br_one and "fc" in br
         self.br_c2 = self.par and (self.br_one or "c2" in br)
@@ -234,6 +239,12 @@ class MnistCnnTrainer:
         # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
         # workspace, since it runs on the fc branch beside other GEMMs
         self.head_gemm = os.environ.get("DTFE_CNN_HEAD_GEMM", "0") == "1" or batch > 1024
+        # DTFE_CNN_HEAD_FUSE=1: the head weight gradient rides in the fc1 data-gradient launch (extra
+        # workgroups of the glds GEMM, no graph node of its own).  Off by default: the hipGraph
+        # runtime's queue / level schedule of the resulting graph measured 8-10 us slower per step
+        # (profiles/r2_cnn_head_fuse_ab.txt); the head gradient keeps its own kernel on the fc branch.
+        self.head_fused = (not self.head_gemm and self.device.type == "cuda" and self.t_dgrad is not None
+                           and os.environ.get("DTFE_CNN_HEAD_FUSE", "0") != "0")
         self.head_splits = max(1, min(16, B // 128))
         bm, bn = ops.TILE_DIMS[4]
         ntiles = -(-NCLS // bm) * -(-(FC + 1) // bn)
@@ -293,14 +304,25 @@ class MnistCnnTrainer:
             self._fc1_dgrad(B, K1)
         with (self._branch(self.s_fc, main) if (self.br_fc and not crit) else
               torch.cuda.stream(self.s_fc) if self.br_fc else contextlib.nullcontext()):
-            self._head_wgrad()
+            if not self.head_fused:
+                self._head_wgrad()
             # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
-            ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
-                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
-            if self.allreduce is not None:  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
-                self.allreduce.launch(0)
+            parts = self.fc1w_split if (self.t_wgrad is not None and FC % (64 * self.fc1w_split) == 0) else 1
+            rows = FC // parts
+            for i in range(parts):
+                r0 = i * rows
+                ops.gemm(self.dzf.view(-1)[r0:], self.p2, self.gw["wd1"][r0:], M=rows, N=K1 + 1, K=B,
+                         amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1,
+                         bias_out=self.gw["bd1"][r0:], tile=self.t_wgrad)
+            if self.allreduce is not None and not self.head_fused:
+                self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
         if not crit:
             self._fc1_dgrad(B, K1)
+        if self.allreduce is not None and self.head_fused:
+            # the head gradient (in bucket 0) is written by the fc1 dgrad launch: bucket 0 forks
+            # once both the fc branch (fc1 wgrad) and that launch are done
+            with (self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext()):
+                self.allreduce.launch(0)
         if self._apply is not None and self._apply[0] == "early":
             # fc/head Adam as soon as their (reduced) gradients are final - and after fc1 dgrad, the
             # last reader of the fc1 weights this step (the branch re-joins main's progress here)
@@ -347,7 +369,8 @@ class MnistCnnTrainer:
     def _fc1_dgrad(self, B, K1):
         """fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)."""
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
-                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
+                 aux_act=ops.ACT_RELU, tile=self.t_dgrad,
+                 head=(self.dl, self.h, self.gw["out"], self.gw["bout"]) if self.head_fused else None)
 
     def _conv2_dgrad(self):
         """conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)."""

@@ -167,7 +167,7 @@ def _mat(t, mode, rows, K, ld):
 def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=None, bias=None, bias_axis=0,
          act=ACT_NONE, alpha=1.0, beta=0.0, atomic=False, splits=1, tile=None, aux=None, ld_aux=None, aux_act=0,
          b_ones_row=-1, keep=1.0, seed=0, counter=None, pooled=None, argmax=None, PH=0, PW=0, PC=0, out2=None,
-         ldc2=0, out2_trans=False, bias_out=None, workspace=None, a_ones_row=-1):
+         ldc2=0, out2_trans=False, bias_out=None, workspace=None, a_ones_row=-1, head=None):
     """out[M,N] = epilogue( A(m,k) . B(n,k) ).
 
     A(m,k) = A[m*lda+k] (KMAJ) or A[k*lda+m] (RMAJ); likewise B(n,k).
@@ -178,6 +178,8 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
     bias_out[n] (W[in][out] weight gradients: the bias gradient without a column-sum launch).
     splits > 1 without atomic: split-K whose last-arriving split runs the fused
     epilogue (workspace = (ws, tile_ctr), default: a per-device cached one).
+    head = (dl, h, dw, db): a 10-class head weight gradient (``head_wgrad``) computed by extra
+    workgroups of the same launch (global_load_lds tiles, one split) - no graph node of its own.
     """
     if lda is None:
         lda = K if amode == KMAJ else M
@@ -198,12 +200,16 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
         ws = ctr = None
         if splits > 1 and not atomic:
             ws, ctr = workspace if workspace is not None else split_workspace(out.device, splits, M, N, tile)
+        if head is not None:
+            require().head_wgrad_fuse(head[0], head[1], head[2], head[3], 10, 1.0)
         require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
                        splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
                        PC, out2, ldc2, out2_trans, bias_out, ws, ctr, a_ones_row,
                        ones_page(out.device) if tile in GLDS_TILES else None)
         return out
     # CPU reference
+    if head is not None:
+        head_wgrad(head[0], head[1], head[2], head[3], 10)
     if a_ones_row >= 0:
         assert a_ones_row == M - 1, "CPU reference: a_ones_row must be the last row"
         a = torch.cat([_mat(A, amode, M - 1, K, lda), torch.ones(1, K)], 0)

@@ -88,15 +88,18 @@ def test_cnn_trains_and_graph_replays():
     assert int(tr.global_step.item()) == 60
 
 
-@pytest.mark.parametrize("branches", ["fc,c2", "fc", "side1", "none"])
+@pytest.mark.parametrize("branches", ["fc,c2", "fc", "side1", "none", "fc,c2:headfuse", "none:headfuse"])
 def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
     """Only the atomically-accumulated grads are cleared per step (fused into the batch gather);
     every other gradient must be fully overwritten: the same batch twice -> the same grads,
     and the result matches autograd after a previous step left garbage behind."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
+    branches, _, fuse = branches.partition(":")
     monkeypatch.setenv("DTFE_CNN_BRANCHES", branches)
+    monkeypatch.setenv("DTFE_CNN_HEAD_FUSE", "1" if fuse else "0")  # head wgrad inside the fc1 dgrad launch
     tr = MnistCnnTrainer(64, "cuda", keep_prob=1.0, seed=5)
+    assert tr.head_fused == bool(fuse)
     tr.P.grad.fill_(7.0)            # stale values everywhere
     tr.loss_sum.fill_(3.0)
     ctr0 = int(tr.data_ctr.item())
