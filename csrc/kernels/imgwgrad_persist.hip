@@ -227,9 +227,11 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     float* part = a.ws + (long)blockIdx.x * wp_part_len(MT, CTW, a.N);
     f32x4_t* pv = reinterpret_cast<f32x4_t*>(part) + (long)wid * CTW * MT * 64 + lane;
 #pragma unroll
-    for (int c = 0; c < CTW; ++c)
+    for (int c = 0; c < CTW; ++c) {
+      if (c >= nct) break;  // dead tiles (past the weight's columns) are neither stored nor reduced
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) pv[(c * MT + mt) * 64] = acc[mt][c];  // dead tiles: ignored
+      for (int mt = 0; mt < MT; ++mt) pv[(c * MT + mt) * 64] = acc[mt][c];
+    }
     if (wid == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -275,8 +277,12 @@ __global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict_
   const int c16 = threadIdx.x & 15, pg = threadIdx.x >> 4;
   const int v = blockIdx.x * 16 + c16;  // f32x4 index within a slab
   const int nv = (plen + 3) / 4;
+  const int ntile = 8 * CTW * MT * 64;  // f32x4 of the tile region
+  // live entries only: a tile past the weight's KC columns was never stored (small convs such as
+  // ResNet-20's 3x3x16 use 9 of the 64 tile slots: the slab traffic shrinks with them)
+  const bool live = v < nv && (v >= ntile || ((v >> 6) / MT / CTW * CTW + (v >> 6) / MT % CTW) * 16 < KC);
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  if (v < nv) {
+  if (live) {
     for (int p0 = pg; p0 < nblk; p0 += 16 * 8) {
       f32x4_t x[8];
 #pragma unroll
@@ -290,11 +296,10 @@ __global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict_
   }
   red[pg][c16] = acc;
   __syncthreads();
-  if (pg != 0 || v >= nv) return;
+  if (pg != 0 || !live) return;
   f32x4_t t = red[0][c16];
 #pragma unroll
   for (int q = 1; q < 16; ++q) t += red[q][c16];
-  const int ntile = 8 * CTW * MT * 64;  // f32x4 of the tile region
   if (v < ntile) {
     const int lane = v & 63, r = v >> 6, mt = r % MT, rc = r / MT, c = rc % CTW, w = rc / CTW;
     const int col = (w * CTW + c) * 16 + (lane & 15), n0 = mt * 16 + (lane >> 4) * 4;
