@@ -628,9 +628,10 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
     const long blocks = ((Mmax + t.bm - 1) / t.bm) * (a.N / t.bn);
     const int nk = a.ph[0].ntaps * (a.SC / IG_BK);
     int sp = env_int("DTFE_IG_SPLIT", 0);
+    static const long ftarget = env_int("DTFE_IG_FTARGET", 200);  // split-K workgroup target (R50 sweep: 400 -> 200 saves 0.15 ms)
     if (sp <= 0) {
       sp = 1;
-      while (blocks * sp < 400 && nk / (sp * 2) >= 6) sp *= 2;
+      while (blocks * sp < ftarget && nk / (sp * 2) >= 6) sp *= 2;
     }
     sp = std::max(1, std::min(sp, nk));
     if (sp > 1) {
@@ -735,7 +736,17 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   const long tiles = (long)(g.Cout / bm) * g.KH * g.KW * (g.C / bn);
   const long M = (long)g.B * g.OH * g.OW;
   int sp = env_int("DTFE_IG_WSPLIT", 0);
-  if (sp <= 0) sp = (int)std::max(1L, std::min((768 + tiles - 1) / tiles, (M + 255) / 256));
+  // splits: enough workgroups to fill the chip (DTFE_IG_WTARGET), each split at least 256 rows, and
+  // the fp32 partial slabs (splits x weight size, written once and re-read by the reduce) bounded
+  // by DTFE_IG_WPART_MB.  ResNet-50 B=256 sweep (profiles/r2_resnet50_wgrad_splits_ab.txt):
+  // 768 WGs / unbounded 27.8 ms -> 512 WGs / 32 MB 27.0 ms per step
+  static const long target = env_int("DTFE_IG_WTARGET", 512);
+  static const long part_mb = env_int("DTFE_IG_WPART_MB", 32);
+  if (sp <= 0) {
+    sp = (int)std::max(1L, std::min((target + tiles - 1) / tiles, (M + 255) / 256));
+    const long len0 = (long)g.Cout * g.KH * g.KW * g.C;
+    if (part_mb > 0) sp = (int)std::max(1L, std::min((long)sp, (part_mb << 20) / (len0 * 4)));
+  }
   long mchunk = (M + sp - 1) / sp;
   mchunk = (mchunk + 63) / 64 * 64;
   sp = (int)((M + mchunk - 1) / mchunk);
