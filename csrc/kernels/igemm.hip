@@ -599,11 +599,12 @@ Tile pick_tile(long M, int N, int nphase) {
     if (std::sscanf(e, "%dx%d", &bm, &bn) == 2 && (bm == 64 || bm == 128) && (bn == 64 || bn == 128) && N % bn == 0)
       return {bm, bn};
   }
+  static const long min_blocks = env_int("DTFE_IG_TBLOCKS", 240);
   const Tile cands[3] = {{128, 128}, {128, 64}, {64, 64}};
   for (const Tile& t : cands) {
     if (N % t.bn) continue;
     const long blocks = ((M + t.bm - 1) / t.bm) * (N / t.bn) * nphase;
-    if (blocks >= 240) return t;
+    if (blocks >= min_blocks) return t;
   }
   return {64, 64};
 }
