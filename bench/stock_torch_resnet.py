@@ -133,7 +133,12 @@ def main():
         opt.step()
         return loss
 
-    runner = step
+    out = {}
+
+    def runner_eager():
+        out["loss"] = step()
+
+    runner = runner_eager
     if a.graph:
         assert world == 1, "--graph is the 1-GPU stock row (DDP steps stay eager)"
 
@@ -156,7 +161,7 @@ def main():
         G = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(G):
-            gstep()
+            out["loss"] = gstep()
         runner = G.replay
     for _ in range(a.warmup):
         runner()
@@ -178,7 +183,7 @@ def main():
     if rank == 0:
         print(json.dumps({"arch": a.arch, "stock_torch_images_per_sec": round(v, 1), "n_gpus": world,
                           "batch_size": B, "ms_per_step": round(el / a.steps * 1000, 3), "graph": a.graph,
-                          "fused_optimizer": a.fused}), flush=True)
+                          "fused_optimizer": a.fused, "last_loss": round(float(out["loss"]), 4)}), flush=True)
         if a.write:
             p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stock_baseline.json")
             tab = json.load(open(p)) if os.path.exists(p) else {}

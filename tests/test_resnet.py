@@ -17,16 +17,25 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-def _ref_forward(model, P, x_nhwc, y_onehot):
-    """Autograd oracle of the program's network (NCHW fp32, training-mode BN)."""
+def _ref_forward(model, P, x_nhwc, y_onehot, device="cpu", round_act=False, params=None):
+    """Autograd oracle of the program's network (NCHW fp32, training-mode BN).
+
+    ``round_act``: round the forward activations at the program's bf16 storage points (conv and
+    BN outputs, straight-through in the backward).  A randomly initialised ResNet-50 has channels
+    whose pre-BN mean is many standard deviations from zero, so x_hat = (x - mean) / std of a
+    bf16-stored conv output differs from the fp32 one by O(1): the bf16 and fp32 networks are
+    different functions there, and their gradients only agree once the oracle sees the same
+    rounded forward values."""
+    rnd = (lambda h: h + (h.to(torch.bfloat16).float() - h).detach()) if round_act else (lambda h: h)
     L = model.layers
     # conv weights as the program sees them (bf16 working copies), everything else fp32 master
-    params = {s.name: (P.w16[s.name] if s.name in P.w16 else P.view(s.name)).detach().float().cpu().clone()
-              .reshape(s.shape).requires_grad_(True) for s in model.specs}
+    if params is None:  # (a training loop passes its own leaf tensors)
+        params = {s.name: (P.w16[s.name] if s.name in P.w16 else P.view(s.name)).detach().float().to(device).clone()
+                  .reshape(s.shape).requires_grad_(True) for s in model.specs}
 
     def conv(c, h):
         w = params[c.name].permute(0, 3, 1, 2)  # [Cout][KH][KW][Cin] -> OIHW
-        return F.conv2d(h, w, stride=c.stride, padding=c.pad)
+        return rnd(F.conv2d(h, w, stride=c.stride, padding=c.pad))
 
     def bn(b, h, relu=True, res=None):
         g, be = params[b.gamma], params[b.beta]
@@ -35,7 +44,7 @@ def _ref_forward(model, P, x_nhwc, y_onehot):
         o = (h - m) / torch.sqrt(v + BN_EPS) * g.view(1, -1, 1, 1) + be.view(1, -1, 1, 1)
         if res is not None:
             o = o + res
-        return torch.relu(o) if relu else o
+        return rnd(torch.relu(o) if relu else o)
 
     def shortcut(x, stride, cout):
         r = x[:, :, ::stride, ::stride]
