@@ -540,11 +540,15 @@ const bf16* zero_page(hipStream_t s) {
   return reinterpret_cast<const bf16*>(d.zeros);
 }
 
-float* workspace(size_t bytes, hipStream_t s) {
+// Weight-gradient partial slabs live in their own buffer: the ResNet backward runs the weight
+// gradients on a side stream, concurrently with the forward/data-gradient split-K launches.
+DevScratch g_wg[64];
+
+float* workspace(size_t bytes, hipStream_t s, DevScratch* pool = g_dev) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_mu);
-  DevScratch& d = g_dev[dev];
+  DevScratch& d = pool[dev];
   if (d.ws_bytes < bytes) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &st);
@@ -754,7 +758,7 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   a.splits = sp;
   a.mchunk = (int)mchunk;
   const long len = (long)g.Cout * g.KH * g.KW * g.C;
-  if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s);
+  if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s, g_wg);
   dim3 grid((unsigned)tiles, sp);
   if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
   else if (bm == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);

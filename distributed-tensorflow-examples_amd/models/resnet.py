@@ -140,6 +140,10 @@ class Conv:
         return self.y, stats is not None
 
     def wgrad(self, dy, x):
+        side = getattr(self, "side", None)
+        if side is not None and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0:
+            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g))
+            return
         if self.img_wgrad:
             ops.imgwgrad(x, self.gw, None, dy=dy, **self.ic)
         else:
@@ -153,6 +157,40 @@ class Conv:
                         pad=self.k - 1 - self.pad, dil=self.dil)
         else:
             ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate)
+
+
+class SideStream:
+    """Weight gradients of the implicit-GEMM convs on a second HIP stream.
+
+    A conv's weight gradient needs only its output gradient and its (forward) input, and nothing
+    downstream in the backward reads it, so it runs concurrently with the data-gradient and
+    BatchNorm-backward chain on the main stream: compute-bound implicit GEMMs overlap the
+    HBM-bound BatchNorm passes.  ``run`` forks after the producer of ``dy`` (an event on the
+    current stream), ``join`` makes the current stream wait for every launch so far; inside a
+    hipGraph capture this becomes a parallel branch.  The weight-gradient split partials have
+    their own workspace (igemm.hip ``g_wg``), so the two streams never share scratch memory."""
+
+    def __init__(self, device):
+        self.stream = torch.cuda.Stream(device=device)
+        self.pending = False
+
+    def run(self, fn):
+        ev = torch.cuda.Event()
+        ev.record()
+        self.stream.wait_event(ev)
+        with torch.cuda.stream(self.stream):
+            fn()
+        self.pending = True
+
+    def join(self):
+        if self.pending:
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            torch.cuda.current_stream().wait_event(ev)
+            self.pending = False
+
+
+_WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
 
 
 class BN:
@@ -462,9 +500,19 @@ class ResNetProgram(StepProgram):
         self.block_lo = [min(P.offsets[n] for n in b.var_names) for b in L["blocks"]]
         self.dense_lo = min(P.offsets[d.kernel], P.offsets[d.bias])
         self.grad_ready = None  # optional backward-progress hook (BucketAllReduce.ready)
+        # ResNet-50 (bottleneck) weight gradients on a side stream (SideStream; DTFE_WGRAD_STREAM=0 off)
+        self.side = None
+        if self.device.type == "cuda" and _WGRAD_STREAM and model.arch == "resnet50":
+            self.side = SideStream(self.device)
+            for b in L["blocks"]:
+                for c in (b.conv1, b.conv2, b.conv3, getattr(b, "convs", None)):
+                    if c is not None:
+                        c.side = self.side
 
     def _ready(self, lo):
         if self.grad_ready is not None:
+            if self.side is not None:
+                self.side.join()  # the bucket's weight gradients were launched on the side stream
             self.grad_ready(lo)
 
     def load_batch(self, batch):
@@ -514,6 +562,8 @@ class ResNetProgram(StepProgram):
             dout = self.d_stem
         L["stem_bn"].bwd(dout, st.y, self.dc_stem)
         st.wgrad(self.dc_stem, self.x)
+        if self.side is not None:
+            self.side.join()
         self._ready(0)
 
     def step_accumulators(self):

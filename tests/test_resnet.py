@@ -192,3 +192,35 @@ def test_resnet50_conv_ops_gpu(case):
             continue
         a, b = res["cuda"][i], res["cpu"][i]
         assert _rel(a, b) < 2e-2, name
+
+
+@pytest.mark.gpu
+def test_resnet50_training_tracks_fp32_gpu():
+    """Three Momentum steps of the bf16 HIP program track an fp32 autograd model started from the
+    same weights on the same batches (the bench-scale run is profiles/r2_resnet50_b256_loss_vs_fp32.txt)."""
+    from dtfe.optim import Optimizer
+    dev = torch.device("cuda", 0)
+    model = ResNetModel(arch="resnet50")
+    B = 32
+    prog = model.program(dev, B, seed=0)
+    cfg, names, bp = model.opt_groups[0]
+    opt = Optimizer(cfg, prog.P, var_list=names, global_step=torch.zeros(1, dtype=torch.int32, device=dev),
+                    beta_power_names=bp)
+    params = {s.name: prog.P.view(s.name).detach().float().clone().reshape(s.shape).requires_grad_(True)
+              for s in model.specs}
+    bufs = {n: torch.zeros_like(params[n]) for n in names}
+    g = torch.Generator(device=dev).manual_seed(3)
+    for _ in range(3):
+        x = torch.rand(B, 224, 224, 3, device=dev, generator=g)
+        y = F.one_hot(torch.randint(0, 1000, (B,), device=dev, generator=g), 1000).float()
+        prog.load_batch((x, y))
+        ours = float(prog.compute_grads()["loss"].item())
+        opt.step()
+        for p in params.values():
+            p.grad = None
+        ref, _ = _ref_forward(model, prog.P, prog.x, y, device=dev, params=params)
+        with torch.no_grad():
+            for n in names:
+                bufs[n].mul_(0.9).add_(params[n].grad)
+                params[n].sub_(0.1 * bufs[n])
+        assert math.isfinite(ours) and abs(ours - ref.item()) < 0.03 * abs(ref.item()), (ours, ref.item())
