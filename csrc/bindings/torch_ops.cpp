@@ -179,10 +179,30 @@ void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, co
 void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B, int64_t H, int64_t W, int64_t C,
                 int64_t Cout, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                 const optional<Tensor>& pooled, const optional<Tensor>& argmax, const optional<Tensor>& relu_mask,
-                bool accumulate) {
+                bool accumulate, const optional<Tensor>& bnb_x, const optional<Tensor>& bnb_y,
+                const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_invstd, const optional<Tensor>& bnb_gamma,
+                const optional<Tensor>& bnb_beta, const optional<Tensor>& bnb_stats, int64_t bnb_act) {
   check_cuda(dy, "dy");
   dtfe::ConvDgradArgs a{};
   a.accumulate = accumulate ? 1 : 0;
+  if (bnb_stats.has_value() && bnb_stats->defined()) {
+    TORCH_CHECK(bnb_x.has_value() && bnb_x->defined() && bnb_mean.has_value() && bnb_invstd.has_value() &&
+                    bnb_gamma.has_value(), "conv_dgrad: BN-backward statistics need x, mean, invstd, gamma");
+    TORCH_CHECK(bnb_x->numel() == dx.numel() && bnb_x->scalar_type() == at::kBFloat16, "conv_dgrad: bnb_x shape/dtype");
+    TORCH_CHECK(bnb_stats->numel() >= 2 * C && bnb_stats->scalar_type() == at::kFloat, "conv_dgrad: bnb_stats [2][C] fp32");
+    TORCH_CHECK(bnb_mean->numel() >= C && bnb_invstd->numel() >= C && bnb_gamma->numel() >= C, "conv_dgrad: BN params");
+    if (bnb_y.has_value() && bnb_y->defined())
+      TORCH_CHECK(bnb_y->numel() == dx.numel() && bnb_y->scalar_type() == at::kBFloat16, "conv_dgrad: bnb_y shape/dtype");
+    if (bnb_beta.has_value() && bnb_beta->defined()) TORCH_CHECK(bnb_beta->numel() >= C, "conv_dgrad: bnb_beta");
+    a.bnb_x = reinterpret_cast<const dtfe::bf16*>(bnb_x->data_ptr());
+    a.bnb_y = ptr_or_null<dtfe::bf16>(bnb_y);
+    a.bnb_mean = bnb_mean->data_ptr<float>();
+    a.bnb_invstd = bnb_invstd->data_ptr<float>();
+    a.bnb_gamma = bnb_gamma->data_ptr<float>();
+    a.bnb_beta = ptr_or_null<float>(bnb_beta);
+    a.bnb_stats = bnb_stats->data_ptr<float>();
+    a.bnb_act = (int)bnb_act;
+  }
   a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
   a.wt = reinterpret_cast<const dtfe::bf16*>(wt.data_ptr());
@@ -833,7 +853,9 @@ TORCH_LIBRARY(dtfe, m) {
       " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act, Tensor(c!)? bn_stats=None) -> ()");
   m.def(
       "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
-      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask, bool accumulate=False) -> ()");
+      " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask, bool accumulate=False,"
+      " Tensor? bnb_x=None, Tensor? bnb_y=None, Tensor? bnb_mean=None, Tensor? bnb_invstd=None,"
+      " Tensor? bnb_gamma=None, Tensor? bnb_beta=None, Tensor(b!)? bnb_stats=None, int bnb_act=0) -> ()");
   m.def("conv1_fwd_pool(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!) argmax) -> ()");
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"

@@ -50,6 +50,11 @@ struct ConvDgradArgs {
   bf16* dx; int unpool; UnpoolArgs up;
   const bf16* relu_mask;            // optional: dx = mask > 0 ? dx : 0 (ReLU' of a pooled output)
   int accumulate;                   // dx += dgrad (implicit-GEMM path only)
+  // optional (bnb_stats != nullptr): the consuming BatchNorm's backward statistics of the final dx,
+  // bnb_stats += (sum g, sum g*xhat), g = dx * act'(.) (norm.h launch_bn_bwd_stats semantics) -
+  // from the implicit-GEMM epilogue where it can, else a separate statistics pass
+  const bf16* bnb_x; const bf16* bnb_y; const float* bnb_mean; const float* bnb_invstd;
+  const float* bnb_gamma; const float* bnb_beta; float* bnb_stats; int bnb_act;
 };
 struct ConvWgradArgs {
   ConvGeom g;
@@ -58,6 +63,8 @@ struct ConvWgradArgs {
 };
 
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
+// the separate BN-backward statistics pass over a finished dx (ConvDgradArgs::bnb_*)
+void launch_dgrad_bn_bwd_stats(const ConvDgradArgs& a, hipStream_t s);
 // dedicated ImageNet stem (7x7/2, 3 -> 64, 224 -> 112; stem.hip): true when it handled the call
 bool launch_stem_fwd(const ConvFwdArgs& a, hipStream_t s);
 bool launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t s, bool accumulate);

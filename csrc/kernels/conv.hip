@@ -407,11 +407,24 @@ void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   bn_stats_of(a, s);
 }
 
+void launch_dgrad_bn_bwd_stats(const ConvDgradArgs& a, hipStream_t s) {
+  BnArgs b{};
+  b.R = (long)a.g.B * a.g.H * a.g.W;
+  b.C = a.g.C;
+  b.x = a.bnb_x; b.y = a.bnb_y; b.dy = a.dx;
+  b.stats = a.bnb_stats;
+  b.gamma = a.bnb_gamma; b.beta = a.bnb_beta;
+  b.mean = const_cast<float*>(a.bnb_mean); b.invstd = const_cast<float*>(a.bnb_invstd);
+  b.act = a.bnb_act;
+  launch_bn_bwd_stats(b, s);
+}
+
 void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s) {
   if (launch_igemm_dgrad(a, s)) return;
   if (a.accumulate) throw std::runtime_error("conv_dgrad: accumulate needs the implicit-GEMM path (C, Cout % 64 == 0)");
   const ConvGeom& g = a.g;
   launch_skinny<DgradK>(a, g.B * g.H * g.W, g.C, s);
+  if (a.bnb_stats) launch_dgrad_bn_bwd_stats(a, s);
 }
 
 template <typename Cfg>

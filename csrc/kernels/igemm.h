@@ -37,6 +37,12 @@ struct IgemmArgs {
   // forward only: per output tile and channel the BatchNorm partials of the stored (bf16) output,
   // [tiles_m][3][N] = (K_t = the tile's first row, sum (y - K_t), sum (y - K_t)^2)
   float* bn_part;
+  // data gradient only (bb_x != nullptr): BatchNorm-backward statistics of the stored (final) output
+  // for the BN that consumes it, g = out * act'(.), into bn_part as (0, sum g, sum g*xhat) per tile
+  // (tile index = phase * tiles_m + tm; zero shift, so the forward reduce kernels fold them as is).
+  // bb_y == nullptr with ReLU: the mask is recomputed from x (norm.hip BwdMask).
+  const bf16* bb_x; const bf16* bb_y; const float* bb_mean; const float* bb_invstd;
+  const float* bb_gamma; const float* bb_beta; int bb_act;
   IgPhase ph[4];
 };
 

@@ -65,7 +65,13 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
   const IgPhase& P = a.ph[blockIdx.z];
   const int Mp = a.B * P.RH * P.RW;
   const int m_base = tm * BM, n_base = tn * BN;
-  if (m_base >= Mp) return;
+  if (m_base >= Mp) {
+    if (a.bb_x) {  // a phase with fewer tiles: its absent tiles contribute zero BN-backward partials
+      float* pp = a.bn_part + ((long)blockIdx.z * a.tiles_m + tm) * 3 * a.N + n_base;
+      for (int c = tid; c < BN; c += IG_THREADS) pp[c] = pp[a.N + c] = pp[2 * a.N + c] = 0.f;
+    }
+    return;
+  }
 
   const int cpt = a.SC / IG_BK;
   const int nk_all = P.ntaps * cpt;
@@ -159,6 +165,58 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
     return;
   }
 
+  // output addresses and every epilogue operand load (accumulation source, BN-backward x / y) are
+  // issued before the C tile is staged, so their latency hides under the LDS round trip
+  constexpr int CPR = BN / 8;
+  constexpr int PER = BM * CPR / IG_THREADS;  // 16-B chunks per thread
+  static_assert(PER * IG_THREADS == BM * CPR, "whole chunks per thread");
+  bf16* dst[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
+    const int m = m_base + r;
+    dst[j] = nullptr;
+    if (m >= Mp) continue;
+    long opix = m;
+    if (a.nphase > 1) {
+      const int jx = m % P.RW, t = m / P.RW;
+      const int i = t % P.RH, b = t / P.RH;
+      opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
+    }
+    dst[j] = a.out + opix * a.N + n_base + c8 * 8;
+  }
+  u32x4_t old[PER];
+  if (a.accum) {  // e.g. a block's input gradient: the shortcut branch's share is already there;
+                  // every load is issued before the first add (no per-chunk latency chain)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
+  }
+  // BatchNorm-backward statistics of the final values: this thread's 8 channels are the same for
+  // every j (IG_THREADS % CPR == 0); x (and y for a non-recomputable mask) at the same offsets
+  const bool bb = a.bb_x != nullptr;
+  const bool bb_from_x = bb && a.bb_y == nullptr && a.bb_act == ACT_RELU;
+  const bool bb_need_y = bb && a.bb_act != ACT_NONE && !bb_from_x;
+  u32x4_t xv[PER], yv[PER];
+  float bmean[8], binv[8], bsc[8], bsh[8], bs[8] = {}, bq[8] = {};
+  const int my_c8 = tid % CPR;
+  if (bb) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const long off = dst[j] ? (long)(dst[j] - a.out) : 0;
+      xv[j] = *reinterpret_cast<const u32x4_t*>(a.bb_x + off);
+      if (bb_need_y) yv[j] = *reinterpret_cast<const u32x4_t*>(a.bb_y + off);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = n_base + my_c8 * 8 + e;
+      bmean[e] = a.bb_mean[c];
+      binv[e] = a.bb_invstd[c];
+      if (bb_from_x) {  // = norm.hip BwdMask (bit-identical to the forward's pre-activation)
+        bsc[e] = a.bb_gamma[c] * a.bb_invstd[c];
+        bsh[e] = a.bb_beta[c] - a.bb_mean[c] * bsc[e];
+      }
+    }
+  }
   // bf16 tile through LDS, then 16-B row-contiguous stores
   constexpr int CLD = BN + 8;
   static_assert(BM * CLD <= 2 * (A_EL + B_EL), "C tile fits the staging LDS");
@@ -172,7 +230,7 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
       for (int q = 0; q < 4; ++q)
         Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
   __syncthreads();
-  if (a.bn_part) {
+  if (a.bn_part && !a.bb_x) {
     // BatchNorm statistics of this tile's stored values (replaces a separate pass over y):
     // thread = (8-channel chunk, row group); sums around the tile's first row, then the row
     // groups in order through the LDS past the C tile (deterministic)
@@ -214,30 +272,6 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
       pp[2 * a.N] = Q;
     }
   }
-  constexpr int CPR = BN / 8;
-  constexpr int PER = BM * CPR / IG_THREADS;  // 16-B chunks per thread
-  static_assert(PER * IG_THREADS == BM * CPR, "whole chunks per thread");
-  bf16* dst[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
-    const int m = m_base + r;
-    dst[j] = nullptr;
-    if (m >= Mp) continue;
-    long opix = m;
-    if (a.nphase > 1) {
-      const int jx = m % P.RW, t = m / P.RW;
-      const int i = t % P.RH, b = t / P.RH;
-      opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
-    }
-    dst[j] = a.out + opix * a.N + n_base + c8 * 8;
-  }
-  u32x4_t old[PER];
-  if (a.accum) {  // e.g. a block's input gradient: the shortcut branch's share is already there;
-                  // every load is issued before the first add (no per-chunk latency chain)
-#pragma unroll
-    for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
-  }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     if (!dst[j]) continue;
@@ -252,6 +286,44 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
       }
     }
     *reinterpret_cast<u32x4_t*>(dst[j]) = v;
+    if (bb) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g0 = bf2f((bf16)((v[e >> 1] >> (16 * (e & 1))) & 0xffffu));
+        const float x = bf2f((bf16)((xv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu));
+        float g = g0;
+        if (bb_from_x) {
+          g = (x * bsc[e] + bsh[e]) > 0.f ? g0 : 0.f;
+        } else if (a.bb_act != ACT_NONE) {
+          g = g0 * act_grad_from_out(bf2f((bf16)((yv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu)), a.bb_act);
+        }
+        bs[e] += g;
+        bq[e] += g * (x - bmean[e]) * binv[e];
+      }
+    }
+  }
+  if (bb) {  // row groups -> per-tile partial, fixed order, through the LDS past the C tile
+    constexpr int RG = IG_THREADS / CPR;
+    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= 2 * (A_EL + B_EL) * 2, "bwd stats scratch fits");
+    float* red = reinterpret_cast<float*>(smem + BM * CLD);
+    const int rg = tid / CPR;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 2) * BN + my_c8 * 8 + e] = bs[e];
+      red[(rg * 2 + 1) * BN + my_c8 * 8 + e] = bq[e];
+    }
+    __syncthreads();
+    float* pp = a.bn_part + ((long)blockIdx.z * a.tiles_m + tm) * 3 * a.N + n_base;
+    for (int c = tid; c < BN; c += IG_THREADS) {
+      float S = 0.f, Q = 0.f;
+      for (int g2 = 0; g2 < RG; ++g2) {
+        S += red[(g2 * 2) * BN + c];
+        Q += red[(g2 * 2 + 1) * BN + c];
+      }
+      pp[c] = 0.f;
+      pp[a.N + c] = S;
+      pp[2 * a.N + c] = Q;
+    }
   }
 }
 
@@ -644,10 +716,15 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
       a.ws = workspace((size_t)sp * Mmax * a.N * sizeof(float), s);
     }
   }
-  const bool fuse_bn = bn_stats && a.splits == 1 && a.nphase == 1 && !a.accum;
-  const int tiles_m = (int)((Mmax + t.bm - 1) / t.bm), nchunk = (tiles_m + BN_TCH - 1) / BN_TCH;
+  // forward: BN statistics of the output (one phase, no accumulation); data gradient (a.bb_x set by
+  // the caller): BN-backward statistics of the final, accumulated output, any phase count
+  const bool bwd_bn = a.bb_x != nullptr;
+  const bool fuse_bn = bn_stats && a.splits == 1 && (bwd_bn || (a.nphase == 1 && !a.accum));
+  if (!fuse_bn) a.bb_x = nullptr;
+  const int tiles_m = (int)((Mmax + t.bm - 1) / t.bm);
+  const int tiles_all = tiles_m * (bwd_bn ? a.nphase : 1), nchunk = (tiles_all + BN_TCH - 1) / BN_TCH;
   a.bn_part = nullptr;
-  if (fuse_bn) a.bn_part = bn_workspace(((size_t)tiles_m + nchunk) * 3 * a.N * sizeof(float), s);
+  if (fuse_bn) a.bn_part = bn_workspace(((size_t)tiles_all + nchunk) * 3 * a.N * sizeof(float), s);
   if (t.bm == 128 && t.bn == 128) launch_ig<128, 128>(a, Mmax, s);
   else if (t.bm == 128 && t.bn == 64) launch_ig<128, 64>(a, Mmax, s);
   else if (t.bm == 64 && t.bn == 128) launch_ig<64, 128>(a, Mmax, s);
@@ -658,9 +735,10 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
                        a.splits, len, a.out, a.accum);
   }
   if (!fuse_bn) return false;
-  float* chunk = a.bn_part + (size_t)tiles_m * 3 * a.N;
+  float* chunk = a.bn_part + (size_t)tiles_all * 3 * a.N;
   const unsigned cg = (unsigned)((a.N + 63) / 64);
-  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_m, a.N, Mmax, t.bm, chunk);
+  // (backward partials carry a zero shift: the row counts passed here then do not enter the fold)
+  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_all, a.N, Mmax, t.bm, chunk);
   hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, a.N, Mmax, t.bm, bn_stats);
   return true;
 }
@@ -702,6 +780,10 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
   a.N = g.C; a.Ktot = g.KH * g.KW * g.Cout;
   a.istr = 1; a.OHf = g.H; a.OWf = g.W; a.ostr = g.stride;
   a.accum = d.accumulate;
+  if (d.bnb_stats) {
+    a.bb_x = d.bnb_x; a.bb_y = d.bnb_y; a.bb_mean = d.bnb_mean; a.bb_invstd = d.bnb_invstd;
+    a.bb_gamma = d.bnb_gamma; a.bb_beta = d.bnb_beta; a.bb_act = d.bnb_act;
+  }
   const int st = g.stride;
   a.nphase = st * st;
   for (int py = 0; py < st; ++py)
@@ -723,7 +805,8 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
         }
       }
     }
-  run_igemm(a, s);
+  const bool fused = run_igemm(a, s, d.bnb_stats);
+  if (d.bnb_stats && !fused) launch_dgrad_bn_bwd_stats(d, s);
   return true;
 }
 

@@ -149,14 +149,17 @@ class Conv:
         else:
             ops.conv_wgrad(dy, x, self.gw, None, self.g)
 
-    def dgrad(self, dy, dx, accumulate=False):
+    def dgrad(self, dy, dx, accumulate=False, bn_bwd=None):
+        """``bn_bwd``: BN.bwd_stats_args of the BatchNorm that consumes dx; returns True when its
+        backward statistics were produced with dx (the BN then skips its statistics pass)."""
         if self.img_dgrad:
             assert not accumulate
             ops.imgconv(self.wt, dx, src=dy, flip_taps=True, B=self.B, SH=self.OH, SW=self.OW, CS=self.cout,
                         OH=self.H, OW=self.W, N=self.cin, KH=self.k, KW=self.k, stride=1,
                         pad=self.k - 1 - self.pad, dil=self.dil)
-        else:
-            ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate)
+            return False
+        ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate, bn_bwd=bn_bwd if _BN_BWD_FUSE else None)
+        return bn_bwd is not None and _BN_BWD_FUSE
 
 
 class SideStream:
@@ -191,6 +194,9 @@ class SideStream:
 
 
 _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
+# BN-backward statistics from the producing data-gradient launch (DTFE_BN_BWD_FUSE=1; off by default:
+# measured 0.5 ms per ResNet-50 B=256 step SLOWER than the separate pass, profiles/r2_resnet50_bn_bwd_fuse_ab.txt)
+_BN_BWD_FUSE = os.environ.get("DTFE_BN_BWD_FUSE", "0") == "1"
 
 
 class BN:
@@ -221,12 +227,22 @@ class BN:
                      momentum=BN_MOMENTUM, act=act, res=res, rstride=rstride)
         return self.y
 
-    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None):
+    def bwd_stats_args(self, x, act=ops.ACT_RELU):
+        """(x, y, mean, invstd, gamma, beta, stats, act) of this BN's backward statistics, for the
+        launch that produces its output gradient (ops.conv_dgrad(bn_bwd=...))."""
         P = self.P
         from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
         y = self.y if act != ops.ACT_NONE and not from_x else None
         beta = P.view(self.beta) if from_x else None
-        ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta)
+        return (x, y, self.mean, self.invstd, P.view(self.gamma), beta, self.dstats, act)
+
+    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None, stats_done=False):
+        P = self.P
+        from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
+        y = self.y if act != ops.ACT_NONE and not from_x else None
+        beta = P.view(self.beta) if from_x else None
+        if not stats_done:
+            ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta)
         ops.bn_bwd_apply(dy, y, x, self.mean, self.invstd, P.view(self.gamma), self.dstats, dx, act=act, dres=dres,
                          dgamma=P.gview(self.gamma), dbeta=P.gview(self.beta), beta=beta)
 
@@ -328,29 +344,32 @@ class Bottleneck:
         h2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats))
         return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats), res=res, rstride=1)
 
-    def bwd(self, dout, dx):
+    def bwd(self, dout, dx, dout_stats_done=False, next_bn=None):
+        """``next_bn``: (BN, its x) of the layer that consumes dx (the previous block's bn3): its
+        backward statistics come out of the launch that finishes dx; returns True if they did.
+        ``dout_stats_done``: bn3's statistics of dout were produced that way by the next block."""
         # shortcut gradient straight into dx, the conv1 data gradient accumulated on top
         fuse = (dx is not None and self.conv1.can_accum and (not self.proj or self.convs.can_accum)
                 and _SHORTCUT_FUSE)
         dres = dx if (fuse and not self.proj) else self.dres
-        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres)
+        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres, stats_done=dout_stats_done)
         self.conv3.wgrad(self.dc3, self.bn2.y)
-        self.conv3.dgrad(self.dc3, self.dh2)
-        self.bn2.bwd(self.dh2, self.conv2.y, self.dc2)
+        done = self.conv3.dgrad(self.dc3, self.dh2, bn_bwd=self.bn2.bwd_stats_args(self.conv2.y))
+        self.bn2.bwd(self.dh2, self.conv2.y, self.dc2, stats_done=done)
         self.conv2.wgrad(self.dc2, self.bn1.y)
-        self.conv2.dgrad(self.dc2, self.dh1)
-        self.bn1.bwd(self.dh1, self.conv1.y, self.dc1)
+        done = self.conv2.dgrad(self.dc2, self.dh1, bn_bwd=self.bn1.bwd_stats_args(self.conv1.y))
+        self.bn1.bwd(self.dh1, self.conv1.y, self.dc1, stats_done=done)
         self.conv1.wgrad(self.dc1, self.x)
         if self.proj:
             self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
             self.convs.wgrad(self.dsc, self.x)
+        nb = next_bn[0].bwd_stats_args(next_bn[1]) if next_bn is not None else None
         if dx is not None:
             if fuse:
                 if self.proj:
                     self.conv1.dgrad(self.dc1, dx)
-                    self.convs.dgrad(self.dsc, dx, accumulate=True)
-                else:
-                    self.conv1.dgrad(self.dc1, dx, accumulate=True)
+                    return self.convs.dgrad(self.dsc, dx, accumulate=True, bn_bwd=nb)
+                return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
             else:
                 self.conv1.dgrad(self.dc1, dx)
                 if self.proj:
@@ -552,8 +571,13 @@ class ResNetProgram(StepProgram):
         ops.gap_bwd(self.dfeat16, self.d_last)
         dout = self.d_last
         blocks = L["blocks"]
+        done = False
         for i in range(len(blocks) - 1, -1, -1):
-            blocks[i].bwd(dout, self.d_in[i])
+            if isinstance(blocks[i], Bottleneck):
+                nb = (blocks[i - 1].bn3, blocks[i - 1].conv3.y) if i > 0 else None
+                done = bool(blocks[i].bwd(dout, self.d_in[i], dout_stats_done=done, next_bn=nb))
+            else:
+                blocks[i].bwd(dout, self.d_in[i])
             self._ready(self.block_lo[i])
             dout = self.d_in[i]
         st = L["stem"]

@@ -447,12 +447,21 @@ def conv1_wgrad_pooled(x, dp, argmax, dw, db, scale=1.0):
     conv_wgrad(dz, x, dw, db, g, scale)
 
 
-def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None, accumulate=False):
+def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None, accumulate=False, bn_bwd=None):
     """dX of an NHWC conv (wt = W laid out [C][KH][KW][Cout]); optional un-pool epilogue, or a
     ReLU mask (dx = mask > 0 ? dx : 0) when the consumer un-pools itself.  ``accumulate``:
-    dx += dX (implicit-GEMM path: C and Cout multiples of 64)."""
+    dx += dX (implicit-GEMM path: C and Cout multiples of 64).  ``bn_bwd``: the consuming
+    BatchNorm's backward statistics of the final dx, ``(x, y, mean, invstd, gamma, beta, stats,
+    act)`` with ``bn_bwd_stats`` semantics - computed in the implicit-GEMM epilogue (no separate
+    pass over dx and x), or by a statistics pass after the launch."""
     if dx.is_cuda:
-        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask, accumulate)
+        b = bn_bwd or (None,) * 7 + (0,)
+        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask, accumulate, *b)
+        return dx
+    if bn_bwd is not None:
+        conv_dgrad(dy, wt, dx, g, pooled, argmax, relu_mask, accumulate)
+        x, y, mean, invstd, gamma, beta, stats, act = bn_bwd
+        bn_bwd_stats(dx, y, x, mean, invstd, stats, act, gamma=gamma, beta=beta)
         return dx
     if accumulate:
         old = dx.float().clone()

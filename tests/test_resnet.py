@@ -224,3 +224,46 @@ def test_resnet50_training_tracks_fp32_gpu():
                 bufs[n].mul_(0.9).add_(params[n].grad)
                 params[n].sub_(0.1 * bufs[n])
         assert math.isfinite(ours) and abs(ours - ref.item()) < 0.03 * abs(ref.item()), (ours, ref.item())
+
+
+BN_BWD_CASES = [  # (B, H, Cin, Cout, K, stride, accumulate, mask)  - dgrad shapes that feed a BN backward
+    (4, 14, 256, 256, 3, 2, False, "x"),     # 4-phase stride-2 data gradient, ReLU mask from x
+    (32, 14, 256, 1024, 1, 1, True, "y"),    # block input gradient (accumulated), ReLU mask from y
+    (4, 28, 512, 1024, 1, 2, True, "y"),     # projection data gradient (stride 2: 3 of 4 phases tapless)
+    (2, 56, 64, 64, 3, 1, False, "x"),
+    (4, 7, 512, 2048, 1, 1, False, "none"),  # no activation
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", BN_BWD_CASES)
+def test_conv_dgrad_bn_bwd_stats_gpu(case):
+    """conv_dgrad(bn_bwd=...) fills the consuming BN's backward statistics from the implicit-GEMM
+    epilogue; they must equal a separate bn_bwd_stats pass over the same finished dx."""
+    from dtfe import ops
+    B, H, C, CO, K, s, acc, mask = case
+    dev = torch.device("cuda", 0)
+    pad = (K - 1) // 2
+    OH = (H + 2 * pad - K) // s + 1
+    g = dict(B=B, H=H, W=H, C=C, Cout=CO, OH=OH, OW=OH, KH=K, KW=K, stride=s, pad=pad)
+    torch.manual_seed(0)
+    dy = torch.randn(B, OH, OH, CO, device=dev).to(torch.bfloat16)
+    wt = (torch.randn(C, K, K, CO, device=dev) / (K * K * CO) ** 0.5).to(torch.bfloat16)
+    x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+    y = torch.relu(torch.randn(B, H, H, C, device=dev)).to(torch.bfloat16)
+    mean, invstd = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    gamma, beta = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    act = ops.ACT_NONE if mask == "none" else ops.ACT_RELU
+    yy = y if mask == "y" else None
+    bb = beta if mask == "x" else None
+    base = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+    dx = base.clone()
+    st = torch.zeros(2 * C, device=dev)
+    ops.conv_dgrad(dy, wt, dx, g, accumulate=acc, bn_bwd=(x, yy, mean, invstd, gamma, bb, st, act))
+    dx2 = base.clone()
+    ops.conv_dgrad(dy, wt, dx2, g, accumulate=acc)
+    st2 = torch.zeros(2 * C, device=dev)
+    ops.bn_bwd_stats(dx2, yy, x, mean, invstd, st2, act, gamma=gamma, beta=bb)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx2)
+    assert _rel(st[:C], st2[:C]) < 1e-4 and _rel(st[C:], st2[C:]) < 1e-4
