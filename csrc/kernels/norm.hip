@@ -417,40 +417,65 @@ __global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const bf16* x, bf16* 
   }
 }
 
-// one thread per (input pixel, 8-channel chunk): sums dy over the (at most 2x2) windows whose
-// argmax is this pixel
+// one thread per (2x2 input cell, 8-channel chunk): input rows 2k, 2k+1 are covered only by window
+// rows k (both) and k+1 (the odd row), columns likewise, so the thread issues the <= 4 window loads
+// (dy 16 B + argmax 8 B each) up front and writes 4 input pixels; each pixel sums its windows in
+// (oy, ox) order, as a per-pixel gather would
 __global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H,
                                                            int W, int C, int OH, int OW) {
   const int cpr = C / 8;
-  const long n = (long)B * H * W * cpr;
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2;
+  const long n = (long)B * QH * QW * cpr;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long row = i / cpr;
-    const int ch = (int)(i - row * cpr) * 8;
-    const long hw = (long)H * W, b = row / hw;
-    const int p = (int)(row - b * hw), iy = p / W, ix = p - iy * W;
-    float g[8] = {};
-    const int oy0 = (iy + 1) / 2 - 1, ox0 = (ix + 1) / 2 - 1;
+    const long cell = i / cpr;
+    const int ch = (int)(i - cell * cpr) * 8;
+    const long qhw = (long)QH * QW, b = cell / qhw;
+    const int p = (int)(cell - b * qhw), k = p / QW, j = p - k * QW;
+    u32x4_t d[2][2];
+    u32x2_t m[2][2];
+    bool ok[2][2];
 #pragma unroll
-    for (int dyo = 0; dyo < 2; ++dyo) {
-      const int oy = oy0 + dyo;
-      if (oy < 0 || oy >= OH || iy < oy * 2 - 1 || iy > oy * 2 + 1) continue;
+    for (int a2 = 0; a2 < 2; ++a2)
 #pragma unroll
-      for (int dxo = 0; dxo < 2; ++dxo) {
-        const int ox = ox0 + dxo;
-        if (ox < 0 || ox >= OW || ix < ox * 2 - 1 || ix > ox * 2 + 1) continue;
-        const long o = ((b * OH + oy) * OW + ox) * C + ch;
-        const uint32_t t = (uint32_t)((iy - (oy * 2 - 1)) * 3 + (ix - (ox * 2 - 1)));
-        const u32x2_t m = *reinterpret_cast<const u32x2_t*>(am + o);
-        float d[8];
-        unpack8(ld16(dy + o), d);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t ae = ((e < 4 ? m[0] : m[1]) >> (8 * (e & 3))) & 0xffu;
-          if (ae == t) g[e] += d[e];
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const int oy = k + a2, ox = j + c2;
+        ok[a2][c2] = oy < OH && ox < OW;
+        if (ok[a2][c2]) {
+          const long o = ((b * OH + oy) * OW + ox) * C + ch;
+          d[a2][c2] = ld16(dy + o);
+          m[a2][c2] = *reinterpret_cast<const u32x2_t*>(am + o);
         }
       }
+#pragma unroll
+    for (int yi = 0; yi < 2; ++yi) {
+      const int iy = 2 * k + yi;
+      if (iy >= H) continue;
+#pragma unroll
+      for (int xi = 0; xi < 2; ++xi) {
+        const int ix = 2 * j + xi;
+        if (ix >= W) continue;
+        float g[8] = {};
+#pragma unroll
+        for (int a2 = 0; a2 < 2; ++a2) {
+          const int ty = yi - 2 * a2 + 1;  // tap row of (iy) in window row k + a2
+          if (ty < 0) continue;
+#pragma unroll
+          for (int c2 = 0; c2 < 2; ++c2) {
+            const int tx = xi - 2 * c2 + 1;
+            if (tx < 0 || !ok[a2][c2]) continue;
+            const uint32_t t = (uint32_t)(ty * 3 + tx);
+            float dv[8];
+            unpack8(d[a2][c2], dv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t ae = ((e < 4 ? m[a2][c2][0] : m[a2][c2][1]) >> (8 * (e & 3))) & 0xffu;
+              if (ae == t) g[e] += dv[e];
+            }
+          }
+        }
+        *reinterpret_cast<u32x4_t*>(dx + ((b * H + iy) * W + ix) * C + ch) = pack8(g);
+      }
     }
-    *reinterpret_cast<u32x4_t*>(dx + row * C + ch) = pack8(g);
   }
 }
 
@@ -519,8 +544,8 @@ void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int 
 void launch_maxpool3_bwd(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH, int OW,
                          hipStream_t s) {
   if (C % 8) throw std::runtime_error("maxpool3: C % 8");
-  hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(ew_grid((long)B * H * W * C / 8)), dim3(256), 0, s, dy, am, dx, B, H,
-                     W, C, OH, OW);
+  hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(ew_grid((long)B * ((H + 1) / 2) * ((W + 1) / 2) * C / 8)), dim3(256), 0,
+                     s, dy, am, dx, B, H, W, C, OH, OW);
 }
 
 }  // namespace dtfe
