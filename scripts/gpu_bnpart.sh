@@ -2,7 +2,7 @@
 set -o pipefail
 O=gpurun_out/bnpart
 mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest tests/test_norm_gpu.py tests/test_resnet.py -m gpu -x -q --timeout 120 \
+DTFE_BN_PART_1L=1 timeout -k 10 400 python3 -u -m pytest tests/test_norm_gpu.py tests/test_resnet.py -m gpu -x -q --timeout 120 \
   --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 &&
 DTFE_BN_PART_1L=0 timeout -k 10 200 python3 bench.py --model resnet50 --steps 20 --warmup 5 > $O/b_2l.log 2>&1 &&
 DTFE_BN_PART_1L=1 timeout -k 10 200 python3 bench.py --model resnet50 --steps 20 --warmup 5 > $O/b_1l.log 2>&1 &&
