@@ -54,6 +54,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch_size", type=int, default=None, help="per-GPU batch (default: per model)")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
+    ap.add_argument("--bucket_mb", type=float, default=None,
+                    help="ResNet gradient bucket size, MB of fp32 gradient (default parallel.comm.DEFAULT_BUCKET_MB; "
+                         "the CNN keeps its two buckets [head + fc1] / [convs])")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
     ap.add_argument("--mode", choices=["allreduce", "ps"], default="allreduce",
@@ -329,7 +332,7 @@ def bench_resnet(args, d: Dist):
             dist.broadcast(m, src=0)
             prog.P.master.copy_(m)
         prog.P.refresh_copies()
-        bks = _buckets(prog.P)
+        bks = _buckets(prog.P, args.bucket_mb)
         esz = 2 if args.comm_dtype == "bf16" else 4
         comm = _make_comm(args, d, [(hi - lo) * esz for lo, hi in bks])
         ar = BucketAllReduce(prog.P.grad, bks, comm=comm, comm_dtype=cdt)

@@ -254,11 +254,15 @@ void ps_copy(const Tensor& blob, int64_t nseg, int64_t nwork) {
 }
 
 // ------------------------------------------------------------------ worker side
-void ps_request(int64_t shm, int64_t w, Tensor ctr, const c10::optional<Tensor>& ver, int64_t kind) {
+void ps_request(int64_t shm, int64_t w, Tensor ctr, const c10::optional<Tensor>& ver, int64_t kind, int64_t shard,
+                int64_t bump) {
   Shm* s = shm_of(shm);
   TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kLong, "dtfe ps: request counter must be a GPU int64");
-  const int64_t* v = (ver.has_value() && ver->defined()) ? ver->data_ptr<int64_t>() : nullptr;
-  dtfe::launch_ps_request(slot_dev(s, (int)w), ctr.data_ptr<int64_t>(), v, (int)kind, cur_stream());
+  const bool hv = ver.has_value() && ver->defined();
+  TORCH_CHECK(!hv || (ver->scalar_type() == at::kLong && shard >= 0 && shard < ver->numel()),
+              "dtfe ps: ver must be a GPU int64 with one version per shard");
+  const int64_t* v = hv ? ver->data_ptr<int64_t>() + shard : nullptr;
+  dtfe::launch_ps_request(slot_dev(s, (int)w), ctr.data_ptr<int64_t>(), v, (int)kind, bump ? 1 : 0, cur_stream());
 }
 
 void ps_wait(std::vector<int64_t> shms, int64_t w, int64_t gs_slot, const Tensor& ctr, const c10::optional<Tensor>& gs_out,
@@ -271,6 +275,7 @@ void ps_wait(std::vector<int64_t> shms, int64_t w, int64_t gs_slot, const Tensor
   a.ctr = ctr.data_ptr<int64_t>();
   a.gs_out = (gs_out.has_value() && gs_out->defined()) ? gs_out->data_ptr<int32_t>() : nullptr;
   a.ver_out = (ver_out.has_value() && ver_out->defined()) ? ver_out->data_ptr<int64_t>() : nullptr;
+  TORCH_CHECK(!a.ver_out || ver_out->numel() >= (int64_t)shms.size(), "dtfe ps: ver_out needs one entry per shard");
   a.err = err.data_ptr<int>();
   a.timeout_ticks = (unsigned long long)(timeout_s * 1e8);
   dtfe::launch_ps_wait(a, cur_stream());
@@ -592,7 +597,7 @@ TORCH_LIBRARY_FRAGMENT(dtfe, m) {
   m.def("ps_plan(Tensor segs, int chunk, Tensor device_like) -> Tensor", &ps_plan);
   m.def("ps_plan_nwork(Tensor segs, int chunk) -> int", &plan_nwork);
   m.def("ps_copy(Tensor blob, int nseg, int nwork) -> ()", &ps_copy);
-  m.def("ps_request(int shm, int w, Tensor(a!) ctr, Tensor? ver, int kind) -> ()", &ps_request);
+  m.def("ps_request(int shm, int w, Tensor(a!) ctr, Tensor? ver, int kind, int shard=0, int bump=1) -> ()", &ps_request);
   m.def("ps_wait(int[] shms, int w, int gs_slot, Tensor ctr, Tensor(a!)? gs_out, Tensor(b!)? ver_out, Tensor(c!) err,"
         " float timeout_s) -> ()", &ps_wait);
   m.def("ps_service_create(int shm, int nworkers, int device, bool sync, int R, bool hogwild) -> int", &ps_service_create);

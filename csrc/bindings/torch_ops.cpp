@@ -694,6 +694,8 @@ bool lstm_seq_fwd(const Tensor& xh, const Tensor& K, const Tensor& bias, double 
   return dtfe::launch_lstm_seq_fwd(a, cur_stream());
 }
 
+int64_t lstm_status(bool reset) { return dtfe::lstm_split_status(reset); }
+
 bool lstm_seq_bwd(const Tensor& K, const Tensor& act, const Tensor& c, const Tensor& dhT, const Tensor& dg,
                   int64_t I) {
   check_cuda(act, "act");
@@ -825,6 +827,7 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("lstm_seq_fwd(Tensor(a!) xh, Tensor K, Tensor bias, float forget_bias, Tensor(b!) act, Tensor(c!) c,"
         " Tensor(d!) hT) -> bool");
   m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I) -> bool");
+  m.def("lstm_status(bool reset=False) -> int", &lstm_status);
   m.def("bn_stats(Tensor x, Tensor(a!) stats) -> ()");
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"

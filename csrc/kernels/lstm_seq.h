@@ -21,6 +21,11 @@ struct LstmSeqArgs {
 bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s);
 bool launch_lstm_seq_bwd(const LstmSeqArgs& a, hipStream_t s);
 
+// error word of the split (4 CUs per row group) kernels on the current device: 1 when a
+// cross-workgroup exchange timed out since the last reset (the outputs of that launch are
+// wrong).  Synchronises the device.  reset clears it.
+int lstm_split_status(bool reset);
+
 }  // namespace dtfe
 
 namespace dtfe {

@@ -450,8 +450,10 @@ __global__ __launch_bounds__(SPT) void lstm_split_bwd_kernel(LstmSeqArgs a, Spli
   finish_launch(y);
 }
 
+char* g_split_buf[64] = {};
+
 SplitSync split_sync(hipStream_t s, int H) {
-  static char* buf[64] = {};
+  char** buf = g_split_buf;
   constexpr size_t CTL = 4096;
   const size_t fw = (size_t)MAX_GROUPS * 2 * LR * 128, bw = fw * NS;  // words, H = 128
   int dev = 0;
@@ -475,6 +477,16 @@ SplitSync split_sync(hipStream_t s, int H) {
   return SplitSync{ll, ll + fw, c, c + 4, c + 8};
 }
 
+// every workgroup of a split launch must be resident at once (they exchange h every step): the
+// grid must fit the occupancy the runtime reports for this kernel and LDS size, times the CUs
+bool co_resident(const void* kern, size_t lds, int blocks) {
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SPT, lds) != hipSuccess) return false;
+  return per_cu >= 1 && (long)per_cu * cus >= blocks;
+}
+
 bool split_ok(const LstmSeqArgs& a) {
   const char* e = getenv("DTFE_LSTM_SPLIT");  // read per launch (tests A/B both paths in one process)
   const bool on = !(e && atoi(e) == 0);
@@ -485,6 +497,20 @@ bool split_ok(const LstmSeqArgs& a) {
 
 }  // namespace
 
+int lstm_split_status(bool reset) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_split_buf[dev]) return 0;
+  int* err = reinterpret_cast<int*>(g_split_buf[dev]) + 8;  // SplitSync::err (split_sync's layout)
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return 1;
+  if (reset && v) {
+    const int z = 0;
+    (void)hipMemcpy(err, &z, sizeof(int), hipMemcpyHostToDevice);
+  }
+  return v;
+}
+
 bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
   // register-resident K slice: instantiated for the MNIST row-LSTM (I = 28, H = 128)
   if (a.H != 128 || a.I != 28 || a.B % LR || LR * a.I > 1024) return false;
@@ -494,8 +520,10 @@ bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
       const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (a.H + 4)) * sizeof(float);
       auto k = lstm_split_fwd_kernel<128, (28 + 128) / 4>;
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
-      return true;
+      if (co_resident((const void*)k, lds, a.B / LR * NS)) {
+        hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
+        return true;
+      }
     }
   }
   const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * a.H + 4)) * sizeof(float);
@@ -513,8 +541,10 @@ bool launch_lstm_seq_bwd(const LstmSeqArgs& a, hipStream_t s) {
       const size_t lds = (size_t)2 * 16 * (4 * (a.H / NS) + 4) * sizeof(float);
       auto k = lstm_split_bwd_kernel<128>;
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
-      return true;
+      if (co_resident((const void*)k, lds, a.B / LR * NS)) {
+        hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
+        return true;
+      }
     }
   }
   const size_t lds = ((size_t)LR * (4 * a.H + 4) + 2 * (size_t)LR * a.H) * sizeof(float);

@@ -51,11 +51,12 @@ enum PsKind : int { PS_PUSH = 1, PS_PULL = 2 };
 // the copy plan: nwork items over the segments (one launch)
 void launch_ps_copy(const PsSeg* segs, const PsWork* work, int nwork, hipStream_t s);
 
-// worker GPU: ctr += 1; slot[KIND] = kind; slot[TAG] = *ver; slot[REQ_SEQ] = ctr (release)
-void launch_ps_request(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, hipStream_t s);
+// worker GPU: ctr += bump; slot[KIND] = kind; slot[TAG] = *ver; slot[REQ_SEQ] = ctr (release).
+// An exchange with several shards bumps once (first shard) so every shard sees the same number.
+void launch_ps_request(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, int bump, hipStream_t s);
 
 // worker GPU: spin (bounded by timeout_ticks of the 100 MHz wall clock) until every slot's
-// REP_SEQ >= *ctr; then gs_out = slot[gs_slot][REP_GS], ver_out = slot[0][REP_VER].  On a
+// REP_SEQ >= *ctr; then gs_out = slot[gs_slot][REP_GS], ver_out[k] = slot[k][REP_VER].  On a
 // timeout *err = 1 and the kernel returns.
 constexpr int PS_MAX_SHARDS = 8;
 struct PsWaitArgs {

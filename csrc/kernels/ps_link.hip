@@ -87,10 +87,12 @@ __global__ __launch_bounds__(256) void ps_copy_kernel(const PsSeg* __restrict__ 
   }
 }
 
-__global__ void ps_request_kernel(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind) {
+__global__ void ps_request_kernel(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, int bump) {
   if (threadIdx.x != 0) return;
-  const int64_t c = *ctr + 1;
-  *ctr = c;
+  // one exchange = one request number for every shard: only the first shard's request advances
+  // the counter (the others follow it on the same stream and reuse the value)
+  const int64_t c = *ctr + bump;
+  if (bump) *ctr = c;
   // every preceding kernel of this stream (the push copies) has completed; drain this
   // kernel's own view before publishing
   __threadfence_system();
@@ -114,7 +116,8 @@ __global__ void ps_wait_kernel(PsWaitArgs a) {
     }
   }
   if (a.gs_out && a.gs_slot >= 0) *a.gs_out = (int32_t)(int64_t)ld_sys(a.slot[a.gs_slot] + PS_REP_GS);
-  if (a.ver_out) *a.ver_out = (int64_t)ld_sys(a.slot[0] + PS_REP_VER);
+  if (a.ver_out)  // per shard: each shard's version is the staleness tag of that shard's next request
+    for (int k = 0; k < a.nslots; ++k) a.ver_out[k] = (int64_t)ld_sys(a.slot[k] + PS_REP_VER);
   __threadfence_system();
 }
 
@@ -136,8 +139,8 @@ void launch_ps_copy(const PsSeg* segs, const PsWork* work, int nwork, hipStream_
   hipLaunchKernelGGL(ps_copy_kernel, dim3(blocks), dim3(256), 0, s, segs, work, nwork);
 }
 
-void launch_ps_request(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, hipStream_t s) {
-  hipLaunchKernelGGL(ps_request_kernel, dim3(1), dim3(64), 0, s, slot, ctr, ver, kind);
+void launch_ps_request(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, int bump, hipStream_t s) {
+  hipLaunchKernelGGL(ps_request_kernel, dim3(1), dim3(64), 0, s, slot, ctr, ver, kind, bump);
 }
 
 void launch_ps_wait(const PsWaitArgs& a, hipStream_t s) {

@@ -55,6 +55,10 @@ class StepProgram:
     def evaluate(self, images, labels) -> float:
         raise NotImplementedError("this model has no evaluation metric")
 
+    def check_health(self):
+        """Raise if a kernel of this program reported a failure it could not surface itself (e.g.
+        a cross-workgroup exchange timeout).  Synchronises; callers do it every log step."""
+
 
 class ModelDef:
     name = "model"

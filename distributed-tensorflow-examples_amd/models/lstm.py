@@ -152,6 +152,14 @@ class LstmProgram(StepProgram):
             if t > 0:
                 ops.gemm(self.dg[t], Kh, self.dh, M=B, N=H, K=4 * H, bmode=ops.KMAJ, ldb=4 * H)
 
+    def check_health(self):
+        """The split persistent kernels (4 CUs per row group) exchange h / dh through memory; a
+        peer workgroup that never ran makes the poll time out and set an error word, after which
+        that launch's outputs are wrong.  Raise instead of training on them."""
+        if self.device.type == "cuda" and int(ops.require().lstm_status(True)) != 0:
+            raise RuntimeError("LSTM split kernel: a cross-workgroup h exchange timed out (a peer workgroup "
+                               "was not co-resident); that step's activations / gradients are invalid")
+
     def evaluate(self, images, labels) -> float:
         """accuracy = mean(argmax(softmax(logits)) == argmax(Y)) (LSTM:98-100, 134-138).  Any number
         of images: evaluated in program-batch chunks, the last one padded by repeating rows (only

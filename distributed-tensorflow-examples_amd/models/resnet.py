@@ -185,6 +185,12 @@ class SideStream:
             fn()
         self.pending = True
 
+    def mark(self):
+        """An event covering every launch on the side stream so far (the stream stays forked)."""
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
     def join(self):
         if self.pending:
             ev = torch.cuda.Event()
@@ -529,10 +535,15 @@ class ResNetProgram(StepProgram):
                         c.side = self.side
 
     def _ready(self, lo):
+        """Backward progress: every gradient at flat offset >= lo has been launched.  The bucket's
+        weight gradients may still run on the wgrad side stream: the all-reduce fork waits on an
+        event recorded there, the compute stream does not (no per-block join serialising the
+        data-gradient chain behind the weight gradients)."""
         if self.grad_ready is not None:
-            if self.side is not None:
-                self.side.join()  # the bucket's weight gradients were launched on the side stream
-            self.grad_ready(lo)
+            after = None
+            if self.side is not None and self.side.pending:
+                after = [self.side.mark()]
+            self.grad_ready(lo, after)
 
     def load_batch(self, batch):
         x, y = batch

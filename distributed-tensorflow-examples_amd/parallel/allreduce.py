@@ -52,25 +52,36 @@ class BucketAllReduce:
     def grad16(self):
         return self.shadow
 
-    def launch(self, i: int):
+    def launch(self, i: int, after=None):
+        """Start bucket i's all-reduce.  ``after``: extra hipEvents its gradients depend on beyond
+        the current stream's work so far (e.g. weight gradients computed on another stream)."""
         lo, hi = self.buckets[i]
-        if self.shadow is not None:
-            ops.cast_(self.flat[lo:hi], self.shadow[lo:hi])
-            buf = self.shadow[lo:hi]
-        else:
-            buf = self.flat[lo:hi]
         if self.comm is not None:
             # fork: the side stream waits for everything enqueued so far (the bucket's producers)
+            # plus the given events; the cast to the wire dtype runs on the side stream too, so
+            # the compute stream never waits for a producer on a third stream
             self.side.wait_stream(torch.cuda.current_stream(self.flat.device))
+            for ev in after or ():
+                self.side.wait_event(ev)
             with torch.cuda.stream(self.side):
+                buf = self._pack(lo, hi)
                 self.comm.all_reduce(buf)
                 self._done_ev[i].record(self.side)
             self._forked = True
             return
+        for ev in after or ():
+            torch.cuda.current_stream(self.flat.device).wait_event(ev)
+        buf = self._pack(lo, hi)
         if self.world == 1:
             return
         self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self._work_of[i] = self._works[-1]
+
+    def _pack(self, lo: int, hi: int):
+        if self.shadow is not None:
+            ops.cast_(self.flat[lo:hi], self.shadow[lo:hi])
+            return self.shadow[lo:hi]
+        return self.flat[lo:hi]
 
     def wait_bucket(self, i: int):
         """Make the current stream wait for bucket i's all-reduce only (later buckets may still
@@ -80,12 +91,13 @@ class BucketAllReduce:
         elif i in self._work_of:
             self._work_of[i].wait()
 
-    def ready(self, lo: int):
-        """Backward progress hook: every gradient at flat offset >= lo is final.  Launches the
-        buckets (in order) that lie entirely above lo, so their all-reduce overlaps the rest of
-        the backward pass."""
+    def ready(self, lo: int, after=None):
+        """Backward progress hook: every gradient at flat offset >= lo is final (once the
+        current stream's work so far and the events ``after`` complete).  Launches the buckets
+        (in order) that lie entirely above lo, so their all-reduce overlaps the rest of the
+        backward pass."""
         while self._next < len(self.buckets) and self.buckets[self._next][0] >= lo:
-            self.launch(self._next)
+            self.launch(self._next, after)
             self._next += 1
 
     def flush(self):

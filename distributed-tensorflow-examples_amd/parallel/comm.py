@@ -18,6 +18,16 @@ import torch.distributed as dist
 from .ipc import IpcComm
 from .rccl import RcclComm
 
+# Gradient bucket size (MB of fp32 gradient; half that on a bf16 wire).  Sizing for 8 GPUs on
+# point-to-point xGMI (7 links per GPU): the two-shot IPC kernel moves 2*(W-1)/W of a bucket per
+# rank spread over all 7 links at once, so its per-bucket time is ~latency (two cross-GPU
+# barriers, a few us) + bytes / (7 links); a ring's per-link bound does not apply.  Overlap with
+# backward wants several buckets per step for the large models (ResNet-50: 51 MB bf16 -> 13
+# buckets of 4 MB on the wire), while every extra bucket adds one barrier latency and one graph
+# node.  16 MB fp32 = 8 MB bf16 sits where the IPC staging (cap = largest bucket) stays small and
+# the per-bucket fixed cost is < 10 % of the transfer.  Override with --bucket_mb.
+DEFAULT_BUCKET_MB = 16.0
+
 
 class RoutedComm:
     """``all_reduce`` dispatching on the tensor's byte size (decided once, at setup)."""

@@ -228,7 +228,9 @@ class NativePSLink:
         self._push = [self._push_plan(lo, hi) for lo, hi in self.buckets]
         self.side = torch.cuda.Stream(device=self.device)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
-        self.ver = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # one version per shard: shard k's last reply version is the staleness tag of the next
+        # request to shard k (sync mode drops pushes computed from an older version)
+        self.ver = torch.zeros(max(1, len(self.shards)), dtype=torch.int64, device=self.device)
         self.gs_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.seq = 0          # host mirror of ctr (requests issued, eager or replayed)
@@ -261,21 +263,24 @@ class NativePSLink:
             self.lib.ps_copy(plan[0], plan[1], plan[2])
 
     # ---- BucketAllReduce interface (called by the step programs during backward)
-    def launch(self, i: int):
-        """Push bucket i (once per step) on the side stream, forked from the current stream."""
+    def launch(self, i: int, after=None):
+        """Push bucket i (once per step) on the side stream, forked from the current stream
+        (and after the events ``after``: gradients produced on another stream)."""
         if i in self._launched:
             return
         self._launched.add(i)
         self.side.wait_stream(torch.cuda.current_stream(self.device))
+        for ev in after or ():
+            self.side.wait_event(ev)
         with torch.cuda.stream(self.side):
             self._run(self._push[i])
         self._forked = True
 
-    def ready(self, lo: int):
+    def ready(self, lo: int, after=None):
         """Backward progress hook: every bucket starting at or above flat offset ``lo`` is final."""
         for i, (blo, _hi) in enumerate(self.buckets):
             if blo >= lo:
-                self.launch(i)
+                self.launch(i, after)
 
     def flush(self):
         for i in range(len(self.buckets)):
@@ -306,8 +311,10 @@ class NativePSLink:
         self._exchanged = False
 
     def _exchange(self, kind: int):
-        for sh in self.shards:
-            self.lib.ps_request(sh["shm"], self.w, self.ctr, self.ver, kind)
+        # ONE request number per exchange for every shard (the first request bumps the counter,
+        # the rest reuse it), so ps_wait's target matches what each shard answers
+        for i, sh in enumerate(self.shards):
+            self.lib.ps_request(sh["shm"], self.w, self.ctr, self.ver, kind, i, 1 if i == 0 else 0)
         self.lib.ps_wait([sh["shm"] for sh in self.shards], self.w, self.gs_slot, self.ctr, self.gs_dev, self.ver,
                          self.err, self.timeout_s)
         self._run(self._pull)

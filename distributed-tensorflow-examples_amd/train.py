@@ -298,7 +298,7 @@ def run_worker_ps(flags, model, server, device, log):
     if _native_ps(flags, server, device):
         # gradient buckets in backward-completion order (flat order = the order backward produces them)
         link = ps_native.NativePSLink(server, prog.P, placement, shard_specs, placement[model.gs_name], device,
-                                      buckets=_ps_buckets(prog))
+                                      buckets=_ps_buckets(prog, flags.bucket_mb))
         core = getattr(prog, "core", None)
         if core is not None and hasattr(core, "allreduce"):
             core.allreduce = link       # the CNN program pushes its buckets from inside backward
@@ -329,6 +329,7 @@ def run_worker_ps(flags, model, server, device, log):
                 metrics = state.get("m")
                 if local_step % flags.log_every == 0:
                     link.check()
+                    prog.check_health()
             else:
                 metrics = prog.compute_grads()
                 step = client.push_pull(prog.P.grad)
@@ -389,7 +390,7 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         prog.P.refresh_copies()
         # on GPUs the buckets go through dtfe's own RCCL communicator (capturable: the whole step,
         # all-reduce included, replays as one hipGraph); gloo / CPU keeps ProcessGroup collectives
-        bks = _buckets(prog.P)
+        bks = _buckets(prog.P, flags.bucket_mb)
         comm = None
         # (gloo + --comm=ipc: several ranks sharing one GPU rehearse the in-graph IPC path)
         if device.type == "cuda" and flags.comm != "pg" and (dist.get_backend(group) != "gloo" or flags.comm == "ipc"):
@@ -450,12 +451,14 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                 sv.summary(step, dict(sc, **{"images/sec": ips}))
                 if ar is not None and ar.comm is not None:
                     ar.comm.check_health()  # IPC barrier timeouts fail the job on every rank
+                prog.check_health()
             if "m" in state:
                 model_step_hook(model, step, state["m"], log)
             metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000, images_per_sec=ips, **sc)
             local_step += 1
         if ar is not None and ar.comm is not None:
             ar.comm.check_health()
+        prog.check_health()
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
         if world > 1 and flags.check_pull:  # synchronous replicas: identical parameters on every worker
             log("params checksum %.12e" % float(prog.P.master.double().sum().item()))
@@ -471,17 +474,24 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
     return prog, opts, gstep
 
 
-def _ps_buckets(prog):
-    """Push buckets of a ps-mode worker: the program's own (the CNN's [head + fc1], [convs]) or
-    ~16 MB ranges of the flat buffer, back to front."""
+def _ps_buckets(prog, bucket_mb=None):
+    """Push buckets of a ps-mode worker: the program's own (the CNN's [head + fc1], [convs]) unless
+    --bucket_mb is given, else ranges of the flat buffer, back to front."""
     core = getattr(prog, "core", None)
-    if core is not None and getattr(core, "buckets", None):
+    if bucket_mb is None and core is not None and getattr(core, "buckets", None):
         return core.buckets
-    return _buckets(prog.P)
+    return _buckets(prog.P, bucket_mb)
 
 
-def _buckets(P, bucket_elems: int = 4 << 20):
-    """Contiguous gradient buckets of ~16 MB fp32 (back of the flat buffer first = backward order)."""
+def _buckets(P, bucket_mb=None):
+    """Contiguous gradient buckets of ``bucket_mb`` MB of fp32 gradient (default
+    comm.DEFAULT_BUCKET_MB), back of the flat buffer first = backward-completion order."""
+    from .parallel.comm import DEFAULT_BUCKET_MB
+
+    mb = DEFAULT_BUCKET_MB if bucket_mb is None else float(bucket_mb)
+    if mb <= 0:
+        raise ValueError("--bucket_mb must be > 0")
+    bucket_elems = max(1024, int(mb * (1 << 20)) // 4)
     total = P.total
     b = []
     hi = total

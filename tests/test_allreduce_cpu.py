@@ -33,7 +33,7 @@ def _worker(rank, world, port, q):
     ar = BucketAllReduce(g, buckets)
     launched = []
     orig = ar.launch
-    ar.launch = lambda i: (launched.append(i), orig(i))
+    ar.launch = lambda i, after=None: (launched.append(i), orig(i, after))
     ar.ready(700)   # nothing lies entirely above 700
     a = list(launched)
     ar.ready(600)   # bucket 0

@@ -44,6 +44,28 @@ def test_bench_resnet20_two_ranks():
     assert r["config"]["ranks_seen_by_comm"] == 2
 
 
+def test_bench_resnet50_two_ranks():
+    """ResNet-50 at world 2: seven ~8 MB bf16 buckets launched from the backward progress hook, the
+    bottleneck weight gradients on their own stream (the all-reduce fork waits on an event of that
+    stream, the compute stream never joins it mid-backward), one hipGraph per step."""
+    r = _bench("--model", "resnet50", "--gpus", "2", "--backend", "gloo", "--comm", "ipc", "--steps", "4",
+               "--warmup", "3", "--batch_size", "32", timeout=400)
+    cfg = r["config"]
+    assert r["n_gpus"] == 2 and cfg["replicas_identical"] is True and cfg["ranks_seen_by_comm"] == 2
+    assert cfg["hip_graph"] is True and "ipc" in cfg["grad_allreduce"]
+
+
+@pytest.mark.parametrize("model,batch", [("mnist_cnn", 256), ("resnet20", 64)])
+def test_bench_eight_ranks(model, batch):
+    """The W = 8 template of the IPC all-reduce kernel (the driver's 8-GPU node): eight ranks share
+    the one GPU here, every one of them in every bucket's collective."""
+    r = _bench("--model", model, "--gpus", "8", "--backend", "gloo", "--comm", "ipc", "--steps", "4", "--warmup", "3",
+               "--batch_size", str(batch), timeout=400)
+    cfg = r["config"]
+    assert r["n_gpus"] == 8 and cfg["replicas_identical"] is True and cfg["ranks_seen_by_comm"] == 8
+    assert cfg["global_batch"] == 8 * batch and cfg["parallelism"] == "dp8"
+
+
 def test_bench_single_rank_json_contract():
     r = _bench("--steps", "10", "--warmup", "3")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",

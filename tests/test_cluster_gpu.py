@@ -21,17 +21,22 @@ def _gs(lines):
     return [int(m.group(1)) for l in lines for m in [re.match(r"Global step (\d+) Local step", l)] if m]
 
 
-@pytest.mark.parametrize("sync", [False, True])
-def test_cnn_ps_on_gpu(tmp_path, sync):
+@pytest.mark.parametrize("n_ps,sync", [(1, False), (1, True), (2, False), (2, True)])
+def test_cnn_ps_on_gpu(tmp_path, n_ps, sync):
+    """n_ps = 2: the variables are sharded round-robin over two ps tasks; every
+    exchange carries ONE request number to both shards and each shard's own version tag."""
     md = str(tmp_path / "ck")
     extra = ["--device=cuda", "--synthetic", "--num_steps=8", "--workers=2", "--batch_size=64", "--seed=3",
              "--model_dir=" + md, "--save_model_secs=0.2"] + (["--sync"] if sync else [])
-    codes, out, _ = local_cluster.launch("cnn", 1, 2, extra, timeout=600, stream=False, gpus=1)
+    codes, out, _ = local_cluster.launch("cnn", n_ps, 2, extra, timeout=600, stream=False, gpus=1)
     assert all(c == 0 for c in codes.values()), "%s\n%s" % (codes, "\n".join(
         "---- %s\n%s" % (k, "\n".join(v[-40:])) for k, v in out.items()))
-    assert "ps 0: quitting" in out[("ps", 0)]
-    # every worker task is on this host's GPU: PUSH / PULL take the native hipIpc data plane
-    assert any(l.startswith("ps 0: native data plane:") for l in out[("ps", 0)]), out[("ps", 0)][-10:]
+    for k in range(n_ps):
+        assert "ps %d: quitting" % k in out[("ps", k)]
+        # every worker task is on this host's GPU: PUSH / PULL take the native hipIpc data plane
+        assert any(l.startswith("ps %d: native data plane:" % k) for l in out[("ps", k)]), out[("ps", k)][-10:]
+    for w in (0, 1):  # a missed reply would stall 60 s and then raise from the device error word
+        assert not any("no reply" in l for l in out[("worker", w)])
     gs = _gs(out[("worker", 0)]) + _gs(out[("worker", 1)])
     assert max(gs) >= 8
     t = ckpt.load_bundle(ckpt.latest_checkpoint(md))

@@ -144,3 +144,5 @@ def test_lstm_split_kernels_replay_in_a_graph(monkeypatch):
     torch.cuda.synchronize()
     assert run.graph is not None, run.capture_error
     assert torch.equal(prog.P.grad, ref)
+    prog.check_health()  # the split kernels' exchange error word stayed clear
+    assert int(torch.ops.dtfe.lstm_status(False)) == 0
