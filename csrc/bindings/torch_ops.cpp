@@ -752,6 +752,35 @@ void bn_apply(const Tensor& x, const Tensor& stats, const Tensor& gamma, const T
   dtfe::launch_bn_apply(a, cur_stream());
 }
 
+// inference-mode BatchNorm: out = act(gamma * (x - moving_mean) * rsqrt(moving_var + eps) + beta [+ res])
+void bn_infer(const Tensor& x, const Tensor& gamma, const Tensor& beta, const Tensor& moving_mean,
+              const Tensor& moving_var, double eps, int64_t act, const optional<Tensor>& res, int64_t rstride,
+              int64_t OH, int64_t OW, const Tensor& out) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() >= 2, "bn_infer: bf16 [..., C] input");
+  dtfe::BnArgs a{};
+  a.C = (int)x.size(-1);
+  a.R = x.numel() / a.C;
+  a.x = reinterpret_cast<const dtfe::bf16*>(x.data_ptr());
+  a.act = (int)act;
+  a.infer = 1;
+  TORCH_CHECK(moving_mean.numel() == a.C && moving_var.numel() == a.C, "bn_infer: moving averages [C]");
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.moving_mean = moving_mean.data_ptr<float>();
+  a.moving_var = moving_var.data_ptr<float>();
+  a.eps = (float)eps;
+  a.res = ptr_or_null<dtfe::bf16>(res);
+  if (a.res) {
+    TORCH_CHECK(res->dim() == 4, "bn_infer: residual NHWC");
+    a.RH = (int)res->size(1); a.RW = (int)res->size(2); a.RC = (int)res->size(3);
+    a.rstride = (int)rstride; a.OH = (int)OH; a.OW = (int)OW;
+  }
+  TORCH_CHECK(out.numel() == x.numel() && out.scalar_type() == at::kBFloat16, "bn_infer: out");
+  a.out = reinterpret_cast<dtfe::bf16*>(out.data_ptr());
+  dtfe::launch_bn_apply(a, cur_stream());
+}
+
 void bn_bwd_stats(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                   const Tensor& invstd, const Tensor& stats, int64_t act, const optional<Tensor>& gamma,
                   const optional<Tensor>& beta) {
@@ -829,6 +858,8 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I) -> bool");
   m.def("lstm_status(bool reset=False) -> int", &lstm_status);
   m.def("bn_stats(Tensor x, Tensor(a!) stats) -> ()");
+  m.def("bn_infer(Tensor x, Tensor gamma, Tensor beta, Tensor moving_mean, Tensor moving_var, float eps, int act,"
+        " Tensor? res, int rstride, int OH, int OW, Tensor(a!) out) -> ()");
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
         " int rstride, int OH, int OW, Tensor(e!) out) -> ()");
@@ -910,6 +941,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("lstm_seq_bwd", &lstm_seq_bwd);
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
+  m.impl("bn_infer", &bn_infer);
   m.impl("bn_bwd_stats", &bn_bwd_stats);
   m.impl("bn_bwd_apply", &bn_bwd_apply);
   m.impl("shortcut_grad_add", &shortcut_grad_add);

@@ -50,6 +50,195 @@ __device__ __forceinline__ int qdiv(int m, int d, float inv_d) {
 }
 
 // ------------------------------------------------------------ fwd / dgrad
+// Epilogue shared by the 4- and 8-wave kernels: fp32 split-K partial tile, or the bf16 tile through
+// LDS (+ accumulation source, BatchNorm forward / backward partial statistics).  THREADS threads,
+// a 2-column wave grid (wave w owns rows (w >> 1) * WM.., columns (w & 1) * WN..).
+template <int BM, int BN, int THREADS, int SMEM_EL>
+__device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&acc)[BM / (THREADS / 128) / 16][BN / 2 / 16],
+                                            bf16* smem, int tid, int lane, int w, int m_base, int n_base,
+                                            int tm, int Mp, const IgPhase& P) {
+  constexpr int IG_THREADS = THREADS;
+  constexpr int WM = BM / (THREADS / 128), WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  const int wm = w >> 1, wn = w & 1;
+  if (a.splits > 1) {
+    // fp32 partial tile (forward only: one phase, output row == m)
+    float* ws = a.ws + (long)blockIdx.y * Mp * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n_base + wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = m_base + wm * WM + i * 16 + (lane >> 4) * 4 + q;
+          if (m < Mp) ws[(long)m * a.N + col] = acc[i][j][q];
+        }
+      }
+    return;
+  }
+
+  // output addresses and every epilogue operand load (accumulation source, BN-backward x / y) are
+  // issued before the C tile is staged, so their latency hides under the LDS round trip
+  constexpr int CPR = BN / 8;
+  constexpr int PER = BM * CPR / IG_THREADS;  // 16-B chunks per thread
+  static_assert(PER * IG_THREADS == BM * CPR, "whole chunks per thread");
+  bf16* dst[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
+    const int m = m_base + r;
+    dst[j] = nullptr;
+    if (m >= Mp) continue;
+    long opix = m;
+    if (a.nphase > 1) {
+      const int jx = m % P.RW, t = m / P.RW;
+      const int i = t % P.RH, b = t / P.RH;
+      opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
+    }
+    dst[j] = a.out + opix * a.N + n_base + c8 * 8;
+  }
+  u32x4_t old[PER];
+  if (a.accum) {  // e.g. a block's input gradient: the shortcut branch's share is already there;
+                  // every load is issued before the first add (no per-chunk latency chain)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
+  }
+  // BatchNorm-backward statistics of the final values: this thread's 8 channels are the same for
+  // every j (IG_THREADS % CPR == 0); x (and y for a non-recomputable mask) at the same offsets
+  const bool bb = a.bb_x != nullptr;
+  const bool bb_from_x = bb && a.bb_y == nullptr && a.bb_act == ACT_RELU;
+  const bool bb_need_y = bb && a.bb_act != ACT_NONE && !bb_from_x;
+  u32x4_t xv[PER], yv[PER];
+  float bmean[8], binv[8], bsc[8], bsh[8], bs[8] = {}, bq[8] = {};
+  const int my_c8 = tid % CPR;
+  if (bb) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const long off = dst[j] ? (long)(dst[j] - a.out) : 0;
+      xv[j] = *reinterpret_cast<const u32x4_t*>(a.bb_x + off);
+      if (bb_need_y) yv[j] = *reinterpret_cast<const u32x4_t*>(a.bb_y + off);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = n_base + my_c8 * 8 + e;
+      bmean[e] = a.bb_mean[c];
+      binv[e] = a.bb_invstd[c];
+      if (bb_from_x) {  // = norm.hip BwdMask (bit-identical to the forward's pre-activation)
+        bsc[e] = a.bb_gamma[c] * a.bb_invstd[c];
+        bsh[e] = a.bb_beta[c] - a.bb_mean[c] * bsc[e];
+      }
+    }
+  }
+  // bf16 tile through LDS, then 16-B row-contiguous stores
+  constexpr int CLD = BN + 8;
+  static_assert(BM * CLD <= SMEM_EL, "C tile fits the staging LDS");
+  __syncthreads();
+  bf16* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
+  __syncthreads();
+  if (a.bn_part && !a.bb_x) {
+    // BatchNorm statistics of this tile's stored values (replaces a separate pass over y):
+    // thread = (8-channel chunk, row group); sums around the tile's first row, then the row
+    // groups in order through the LDS past the C tile (deterministic)
+    constexpr int CH = BN / 8, RG = IG_THREADS / CH;
+    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= SMEM_EL * 2, "stats scratch fits");
+    float* red = reinterpret_cast<float*>(smem + BM * CLD);
+    const int ch = tid % CH, rg = tid / CH, rows = min(BM, Mp - m_base);
+    float k[8], sm[8] = {}, sq[8] = {};
+    const u32x4_t kv = *reinterpret_cast<const u32x4_t*>(Cs + ch * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      k[2 * e] = bf2f((bf16)(kv[e] & 0xffffu));
+      k[2 * e + 1] = bf2f((bf16)(kv[e] >> 16));
+    }
+    for (int r = rg; r < rows; r += RG) {
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + ch * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d0 = bf2f((bf16)(v[e] & 0xffffu)) - k[2 * e], d1 = bf2f((bf16)(v[e] >> 16)) - k[2 * e + 1];
+        sm[2 * e] += d0; sq[2 * e] += d0 * d0;
+        sm[2 * e + 1] += d1; sq[2 * e + 1] += d1 * d1;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 2) * BN + ch * 8 + e] = sm[e];
+      red[(rg * 2 + 1) * BN + ch * 8 + e] = sq[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += IG_THREADS) {
+      float S = 0.f, Q = 0.f;
+      for (int g2 = 0; g2 < RG; ++g2) {
+        S += red[(g2 * 2) * BN + c];
+        Q += red[(g2 * 2 + 1) * BN + c];
+      }
+      float* pp = a.bn_part + (long)tm * 3 * a.N + n_base + c;
+      pp[0] = bf2f(Cs[c]);
+      pp[a.N] = S;
+      pp[2 * a.N] = Q;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (!dst[j]) continue;
+    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
+    u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c8 * 8);
+    if (a.accum) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f((bf16)(v[e] & 0xffffu)) + bf2f((bf16)(old[j][e] & 0xffffu));
+        const float hi = bf2f((bf16)(v[e] >> 16)) + bf2f((bf16)(old[j][e] >> 16));
+        v[e] = pack_bf16x2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4_t*>(dst[j]) = v;
+    if (bb) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g0 = bf2f((bf16)((v[e >> 1] >> (16 * (e & 1))) & 0xffffu));
+        const float x = bf2f((bf16)((xv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu));
+        float g = g0;
+        if (bb_from_x) {
+          g = (x * bsc[e] + bsh[e]) > 0.f ? g0 : 0.f;
+        } else if (a.bb_act != ACT_NONE) {
+          g = g0 * act_grad_from_out(bf2f((bf16)((yv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu)), a.bb_act);
+        }
+        bs[e] += g;
+        bq[e] += g * (x - bmean[e]) * binv[e];
+      }
+    }
+  }
+  if (bb) {  // row groups -> per-tile partial, fixed order, through the LDS past the C tile
+    constexpr int RG = IG_THREADS / CPR;
+    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= SMEM_EL * 2, "bwd stats scratch fits");
+    float* red = reinterpret_cast<float*>(smem + BM * CLD);
+    const int rg = tid / CPR;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 2) * BN + my_c8 * 8 + e] = bs[e];
+      red[(rg * 2 + 1) * BN + my_c8 * 8 + e] = bq[e];
+    }
+    __syncthreads();
+    float* pp = a.bn_part + ((long)blockIdx.z * a.tiles_m + tm) * 3 * a.N + n_base;
+    for (int c = tid; c < BN; c += IG_THREADS) {
+      float S = 0.f, Q = 0.f;
+      for (int g2 = 0; g2 < RG; ++g2) {
+        S += red[(g2 * 2) * BN + c];
+        Q += red[(g2 * 2 + 1) * BN + c];
+      }
+      pp[c] = 0.f;
+      pp[a.N + c] = S;
+      pp[2 * a.N + c] = Q;
+    }
+  }
+}
+
 template <int BM, int BN>
 __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -148,183 +337,7 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
     }
   }
 
-  if (a.splits > 1) {
-    // fp32 partial tile (forward only: one phase, output row == m)
-    float* ws = a.ws + (long)blockIdx.y * Mp * a.N;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n_base + wn * WN + j * 16 + (lane & 15);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int m = m_base + wm * WM + i * 16 + (lane >> 4) * 4 + q;
-          if (m < Mp) ws[(long)m * a.N + col] = acc[i][j][q];
-        }
-      }
-    return;
-  }
-
-  // output addresses and every epilogue operand load (accumulation source, BN-backward x / y) are
-  // issued before the C tile is staged, so their latency hides under the LDS round trip
-  constexpr int CPR = BN / 8;
-  constexpr int PER = BM * CPR / IG_THREADS;  // 16-B chunks per thread
-  static_assert(PER * IG_THREADS == BM * CPR, "whole chunks per thread");
-  bf16* dst[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
-    const int m = m_base + r;
-    dst[j] = nullptr;
-    if (m >= Mp) continue;
-    long opix = m;
-    if (a.nphase > 1) {
-      const int jx = m % P.RW, t = m / P.RW;
-      const int i = t % P.RH, b = t / P.RH;
-      opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
-    }
-    dst[j] = a.out + opix * a.N + n_base + c8 * 8;
-  }
-  u32x4_t old[PER];
-  if (a.accum) {  // e.g. a block's input gradient: the shortcut branch's share is already there;
-                  // every load is issued before the first add (no per-chunk latency chain)
-#pragma unroll
-    for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
-  }
-  // BatchNorm-backward statistics of the final values: this thread's 8 channels are the same for
-  // every j (IG_THREADS % CPR == 0); x (and y for a non-recomputable mask) at the same offsets
-  const bool bb = a.bb_x != nullptr;
-  const bool bb_from_x = bb && a.bb_y == nullptr && a.bb_act == ACT_RELU;
-  const bool bb_need_y = bb && a.bb_act != ACT_NONE && !bb_from_x;
-  u32x4_t xv[PER], yv[PER];
-  float bmean[8], binv[8], bsc[8], bsh[8], bs[8] = {}, bq[8] = {};
-  const int my_c8 = tid % CPR;
-  if (bb) {
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const long off = dst[j] ? (long)(dst[j] - a.out) : 0;
-      xv[j] = *reinterpret_cast<const u32x4_t*>(a.bb_x + off);
-      if (bb_need_y) yv[j] = *reinterpret_cast<const u32x4_t*>(a.bb_y + off);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = n_base + my_c8 * 8 + e;
-      bmean[e] = a.bb_mean[c];
-      binv[e] = a.bb_invstd[c];
-      if (bb_from_x) {  // = norm.hip BwdMask (bit-identical to the forward's pre-activation)
-        bsc[e] = a.bb_gamma[c] * a.bb_invstd[c];
-        bsh[e] = a.bb_beta[c] - a.bb_mean[c] * bsc[e];
-      }
-    }
-  }
-  // bf16 tile through LDS, then 16-B row-contiguous stores
-  constexpr int CLD = BN + 8;
-  static_assert(BM * CLD <= 2 * (A_EL + B_EL), "C tile fits the staging LDS");
-  __syncthreads();
-  bf16* Cs = smem;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
-  __syncthreads();
-  if (a.bn_part && !a.bb_x) {
-    // BatchNorm statistics of this tile's stored values (replaces a separate pass over y):
-    // thread = (8-channel chunk, row group); sums around the tile's first row, then the row
-    // groups in order through the LDS past the C tile (deterministic)
-    constexpr int CH = BN / 8, RG = IG_THREADS / CH;
-    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= 2 * (A_EL + B_EL) * 2, "stats scratch fits");
-    float* red = reinterpret_cast<float*>(smem + BM * CLD);
-    const int ch = tid % CH, rg = tid / CH, rows = min(BM, Mp - m_base);
-    float k[8], sm[8] = {}, sq[8] = {};
-    const u32x4_t kv = *reinterpret_cast<const u32x4_t*>(Cs + ch * 8);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      k[2 * e] = bf2f((bf16)(kv[e] & 0xffffu));
-      k[2 * e + 1] = bf2f((bf16)(kv[e] >> 16));
-    }
-    for (int r = rg; r < rows; r += RG) {
-      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + ch * 8);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d0 = bf2f((bf16)(v[e] & 0xffffu)) - k[2 * e], d1 = bf2f((bf16)(v[e] >> 16)) - k[2 * e + 1];
-        sm[2 * e] += d0; sq[2 * e] += d0 * d0;
-        sm[2 * e + 1] += d1; sq[2 * e + 1] += d1 * d1;
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(rg * 2) * BN + ch * 8 + e] = sm[e];
-      red[(rg * 2 + 1) * BN + ch * 8 + e] = sq[e];
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += IG_THREADS) {
-      float S = 0.f, Q = 0.f;
-      for (int g2 = 0; g2 < RG; ++g2) {
-        S += red[(g2 * 2) * BN + c];
-        Q += red[(g2 * 2 + 1) * BN + c];
-      }
-      float* pp = a.bn_part + (long)tm * 3 * a.N + n_base + c;
-      pp[0] = bf2f(Cs[c]);
-      pp[a.N] = S;
-      pp[2 * a.N] = Q;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    if (!dst[j]) continue;
-    const int q = tid + j * IG_THREADS, r = q / CPR, c8 = q - r * CPR;
-    u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c8 * 8);
-    if (a.accum) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = bf2f((bf16)(v[e] & 0xffffu)) + bf2f((bf16)(old[j][e] & 0xffffu));
-        const float hi = bf2f((bf16)(v[e] >> 16)) + bf2f((bf16)(old[j][e] >> 16));
-        v[e] = pack_bf16x2(lo, hi);
-      }
-    }
-    *reinterpret_cast<u32x4_t*>(dst[j]) = v;
-    if (bb) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float g0 = bf2f((bf16)((v[e >> 1] >> (16 * (e & 1))) & 0xffffu));
-        const float x = bf2f((bf16)((xv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu));
-        float g = g0;
-        if (bb_from_x) {
-          g = (x * bsc[e] + bsh[e]) > 0.f ? g0 : 0.f;
-        } else if (a.bb_act != ACT_NONE) {
-          g = g0 * act_grad_from_out(bf2f((bf16)((yv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu)), a.bb_act);
-        }
-        bs[e] += g;
-        bq[e] += g * (x - bmean[e]) * binv[e];
-      }
-    }
-  }
-  if (bb) {  // row groups -> per-tile partial, fixed order, through the LDS past the C tile
-    constexpr int RG = IG_THREADS / CPR;
-    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= 2 * (A_EL + B_EL) * 2, "bwd stats scratch fits");
-    float* red = reinterpret_cast<float*>(smem + BM * CLD);
-    const int rg = tid / CPR;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(rg * 2) * BN + my_c8 * 8 + e] = bs[e];
-      red[(rg * 2 + 1) * BN + my_c8 * 8 + e] = bq[e];
-    }
-    __syncthreads();
-    float* pp = a.bn_part + ((long)blockIdx.z * a.tiles_m + tm) * 3 * a.N + n_base;
-    for (int c = tid; c < BN; c += IG_THREADS) {
-      float S = 0.f, Q = 0.f;
-      for (int g2 = 0; g2 < RG; ++g2) {
-        S += red[(g2 * 2) * BN + c];
-        Q += red[(g2 * 2 + 1) * BN + c];
-      }
-      pp[c] = 0.f;
-      pp[a.N + c] = S;
-      pp[2 * a.N + c] = Q;
-    }
-  }
+  igemm_store<BM, BN, IG_THREADS, 2 * (A_EL + B_EL)>(a, acc, smem, tid, lane, w, m_base, n_base, tm, Mp, P);
 }
 
 // out[i] = bf16(sum_s ws[s][i])   (accum: out[i] = bf16(out[i] + sum_s ws[s][i]))
@@ -772,6 +785,8 @@ int env_int(const char* name, int dflt) {
 struct Tile { int bm, bn; };
 
 // Largest tile that still gives >= ~one workgroup per CU; DTFE_IG_TILE=BMxBN overrides.
+// (An 8-wave 256-row-tile kernel with 3 LDS stages, one workgroup per CU, measured slower than
+// these 4-wave tiles at two workgroups per CU on every ResNet-50 layer: profiles/r3_igemm_8wave_ab.txt.)
 Tile pick_tile(long M, int N, int nphase) {
   const char* e = std::getenv("DTFE_IG_TILE");
   if (e && *e) {

@@ -31,6 +31,8 @@ struct BnArgs {
   const bf16* res; bf16* dres; int RH, RW, RC, rstride, OH, OW;
   bf16* out;                     // forward y / backward dx
   float* dgamma; float* dbeta;   // backward parameter gradients (+=)
+  int infer;                     // bn_apply only: normalise with the moving averages (inference mode;
+                                 // stats unused, nothing is updated or saved)
 };
 
 void launch_bn_stats(const BnArgs& a, hipStream_t s);

@@ -101,6 +101,11 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 }
 
 __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean, float& invstd) {
+  if (a.infer) {  // TF inference: (x - moving_mean) * rsqrt(moving_variance + eps)
+    mean = a.moving_mean[c];
+    invstd = rsqrtf(a.moving_var[c] + a.eps);
+    return;
+  }
   const float inv_r = 1.f / (float)a.R;
   const float d = a.stats[c] * inv_r;
   mean = bf2f(a.x[c]) + d;
@@ -117,7 +122,7 @@ __device__ __forceinline__ long res_offset(const BnArgs& a, long r, int chunk, b
 
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
   const Slots S(a.C);
-  if (blockIdx.x == 0) {  // saved statistics + moving averages (TF: unbiased batch variance)
+  if (blockIdx.x == 0 && !a.infer) {  // saved statistics + moving averages (TF: unbiased batch variance)
     for (int c = threadIdx.x; c < a.C; c += NT) {
       float mean, invstd;
       chan_params(a, c, mean, invstd);
@@ -495,6 +500,7 @@ void launch_bn_stats(const BnArgs& a, hipStream_t s) {
 
 void launch_bn_apply(const BnArgs& a, hipStream_t s) {
   check(a);
+  if (a.infer && (!a.moving_mean || !a.moving_var)) throw std::runtime_error("bn_apply: inference needs the moving averages");
   if (a.res && (a.RC % 8 || a.RC > a.C)) throw std::runtime_error("bn_apply: residual channels");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(a.R, a.C)), dim3(NT), 0, s, a);
 }

@@ -206,6 +206,8 @@ _BN_BWD_FUSE = os.environ.get("DTFE_BN_BWD_FUSE", "0") == "1"
 
 
 class BN:
+    infer = False  # set by ResNetProgram.evaluate
+
     def __init__(self, reg, C):
         self.C = C
         s = reg.scope("batch_normalization")
@@ -224,6 +226,10 @@ class BN:
         """``x``: the conv output, or (conv output, statistics already accumulated by the conv)."""
         P = self.P
         x, have_stats = x if isinstance(x, tuple) else (x, False)
+        if self.infer:  # evaluation: moving averages, nothing updated (TF training=False)
+            ops.bn_infer(x, P.view(self.gamma), P.view(self.beta), P.view(self.mm), P.view(self.mv), self.y,
+                         eps=BN_EPS, act=act, res=res, rstride=rstride)
+            return self.y
         # backward recomputes the ReLU mask from x unless a shortcut was added before the ReLU
         self.mask_from_x = act == ops.ACT_RELU and res is None
         if not have_stats:
@@ -616,5 +622,33 @@ class ResNetProgram(StepProgram):
         self.backward()
         return {"loss": ScaledScalar(self.loss, 1.0 / self.batch_size), "correct": self.correct}
 
+    def batchnorms(self):
+        L = self.L
+        out = [L["stem_bn"]]
+        for b in L["blocks"]:
+            out += [bn for bn in (getattr(b, "bns", None), b.bn1, b.bn2, getattr(b, "bn3", None)) if bn is not None]
+        return out
+
     def evaluate(self, images, labels) -> float:
-        raise NotImplementedError("training-mode BN only; no evaluation step in this example")
+        """Top-1 accuracy with inference-mode BatchNorm (the moving averages; TF ``training=False``),
+        the evaluation analog of LSTM:134-138.  Any number of images, in program-batch chunks (the
+        last one padded by repeating rows; only the real rows are counted).  Parameters and moving
+        averages are left untouched; the step accumulators the forward touched are cleared."""
+        n, B = images.shape[0], self.batch_size
+        bns = self.batchnorms()
+        for bn in bns:
+            bn.infer = True
+        hits = 0
+        try:
+            for lo in range(0, n, B):
+                m = min(B, n - lo)
+                idx = torch.arange(lo, lo + B, device=images.device).clamp_max(n - 1)
+                self.load_batch((images[idx], labels[idx]))
+                self.forward()
+                hits += int((self.logits[:m].argmax(1) == self.y[:m].argmax(1)).sum().item())
+        finally:
+            for bn in bns:
+                bn.infer = False
+            for t in self.step_accumulators()[1:]:
+                t.zero_()
+        return hits / n

@@ -796,6 +796,23 @@ def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=
     return out
 
 
+def bn_infer(x, gamma, beta, moving_mean, moving_var, out, *, eps=1e-3, act=ACT_RELU, res=None, rstride=1):
+    """Inference-mode BatchNorm (TF ``training=False``): out = act(gamma * (x - moving_mean) *
+    rsqrt(moving_var + eps) + beta [+ shortcut(res)]); nothing is updated."""
+    OH, OW = (x.shape[1], x.shape[2]) if x.dim() == 4 else (1, 1)
+    if x.is_cuda:
+        require().bn_infer(x, gamma, beta, moving_mean, moving_var, eps, act, res, rstride, OH, OW, out)
+        return out
+    r = _rows(x)
+    R, C = r.shape
+    inv = torch.rsqrt(moving_var.float() + eps)
+    y = (r - moving_mean.float()) * inv * gamma.float() + beta.float()
+    if res is not None:
+        y = y + _shortcut_view(res, OH, OW, C, rstride).reshape(R, C)
+    out.copy_(_act_ref(y, act).reshape(out.shape).to(out.dtype))
+    return out
+
+
 def _masked_grad(dy, y, act, x=None, mean=None, invstd=None, gamma=None, beta=None):
     g = _rows(dy)
     if act != ACT_NONE:

@@ -75,15 +75,18 @@ def test_shortcut_grad_add_and_gap():
     assert _rel(d2, d1) < 1e-2
 
 
-def test_maxpool3():
+@pytest.mark.parametrize("B,H,W,C", [(2, 112, 112, 64), (3, 7, 9, 64), (2, 15, 15, 32), (1, 9, 6, 128)])
+def test_maxpool3(B, H, W, C):
+    """Odd H / W exercise the backward's partial 2x2 input cells at the bottom / right edge."""
     torch.manual_seed(2)
-    x = torch.randn(2, 112, 112, 64).to(torch.bfloat16)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    x = torch.randn(B, H, W, C).to(torch.bfloat16)
     ys, ams, dxs = [], [], []
-    dy = torch.randn(2, 56, 56, 64).to(torch.bfloat16)
+    dy = torch.randn(B, OH, OW, C).to(torch.bfloat16)
     for dev in ("cpu", DEV):
-        y = torch.empty(2, 56, 56, 64, dtype=torch.bfloat16, device=dev)
-        am = torch.empty(2, 56, 56, 64, dtype=torch.uint8, device=dev)
-        dx = torch.empty(2, 112, 112, 64, dtype=torch.bfloat16, device=dev)
+        y = torch.empty(B, OH, OW, C, dtype=torch.bfloat16, device=dev)
+        am = torch.empty(B, OH, OW, C, dtype=torch.uint8, device=dev)
+        dx = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
         ops.maxpool3_fwd(x.to(dev), y, am)
         ops.maxpool3_bwd(dy.to(dev), am, dx)
         ys.append(y.cpu()), ams.append(am.cpu()), dxs.append(dx.cpu())

@@ -267,3 +267,41 @@ def test_conv_dgrad_bn_bwd_stats_gpu(case):
     torch.cuda.synchronize()
     assert torch.equal(dx, dx2)
     assert _rel(st[:C], st2[:C]) < 1e-4 and _rel(st[C:], st2[C:]) < 1e-4
+
+
+def _eval_matches_batch_stats(device, arch, B):
+    """Inference-mode BN with moving averages set to one batch's statistics reproduces the
+    training-mode forward on that batch; evaluate() leaves parameters / moving averages alone."""
+    torch.manual_seed(5)
+    model = ResNetModel(arch=arch)
+    prog = model.program(device, B, seed=2)
+    x = torch.rand(B, model.image, model.image, model.channels, device=device)
+    y = torch.randint(0, model.num_classes, (B,), device=device)
+    prog.load_batch((x, y.view(-1, 1)))
+    prog.forward()
+    train_logits = prog.logits.clone()
+    P = prog.P
+    for bn in prog.batchnorms():
+        P.view(bn.mm).copy_(bn.mean)
+        P.view(bn.mv).copy_(1.0 / (bn.invstd * bn.invstd) - BN_EPS)
+    before = P.master.clone()
+    acc = prog.evaluate(x, y.view(-1, 1))
+    assert 0.0 <= acc <= 1.0
+    eval_logits = prog.logits.clone()
+    assert _rel(eval_logits, train_logits) < 3e-2
+    # accuracy is the argmax agreement with the labels, computed on the same logits
+    assert abs(acc - (eval_logits.argmax(1) == y).float().mean().item()) < 1e-6
+    assert torch.equal(before, P.master)
+    # odd counts: chunks padded by repeating rows, only real rows counted
+    acc2 = prog.evaluate(x[:B - 1], y[:B - 1].view(-1, 1))
+    assert 0.0 <= acc2 <= 1.0
+
+
+def test_resnet20_evaluate_inference_bn_cpu():
+    _eval_matches_batch_stats("cpu", "resnet20", 4)
+
+
+@pytest.mark.gpu
+def test_resnet_evaluate_inference_bn_gpu():
+    _eval_matches_batch_stats("cuda", "resnet20", 32)
+    _eval_matches_batch_stats("cuda", "resnet50", 8)
