@@ -475,6 +475,7 @@ def bench_ps(args):
         pushes = N * (args.steps + args.warmup)  # every runner() call is exactly one step (one push)
         rec_extra = {"optimizer": "adam (TF1), applied on the ps", "hip_graph": runner.graph is not None,
                      "last_loss": round(loss, 4), "global_step": gs, "ps_applies": stats.get("applies"),
+                     "ps_bucket_applies": stats.get("bucket_applies"),
                      "ps_global_step": stats.get("global_step"),
                      "pushes_issued": pushes, "transport": "hipIpc mailboxes + C++ ps service (bf16 push, bf16 pull)",
                      "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": 0}

@@ -28,9 +28,11 @@
 #include <torch/library.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -265,6 +267,13 @@ void ps_request(int64_t shm, int64_t w, Tensor ctr, const c10::optional<Tensor>&
   dtfe::launch_ps_request(slot_dev(s, (int)w), ctr.data_ptr<int64_t>(), v, (int)kind, bump ? 1 : 0, cur_stream());
 }
 
+void ps_bucket(int64_t shm, int64_t w, const Tensor& ctr, int64_t b, int64_t lo, int64_t hi) {
+  Shm* s = shm_of(shm);
+  TORCH_CHECK(b >= 0 && b < dtfe::PS_MAX_BUCKETS, "dtfe ps: bucket index out of range");
+  TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kLong, "dtfe ps: request counter must be a GPU int64");
+  dtfe::launch_ps_bucket(slot_dev(s, (int)w), ctr.data_ptr<int64_t>(), (int)b, (long)lo, (long)hi, cur_stream());
+}
+
 void ps_wait(std::vector<int64_t> shms, int64_t w, int64_t gs_slot, const Tensor& ctr, const c10::optional<Tensor>& gs_out,
              const c10::optional<Tensor>& ver_out, Tensor err, double timeout_s) {
   TORCH_CHECK(!shms.empty() && shms.size() <= (size_t)dtfe::PS_MAX_SHARDS, "dtfe ps: 1..8 shards");
@@ -282,9 +291,18 @@ void ps_wait(std::vector<int64_t> shms, int64_t w, int64_t gs_slot, const Tensor
 }
 
 // ------------------------------------------------------------------ ps service
+// A partial plan of one optimizer group: its work items whose variable lies in a shard-flat range
+// (a push bucket), same segment table.  Built on first use, cached by range.
+struct SubPlan {
+  Tensor blob;
+  int nwork = 0;
+};
 struct Group {
   dtfe::OptArgs args;    // g / g16 and done_counter set per launch
   bool g16;
+  std::vector<dtfe::OptSeg> hsegs;   // host copies of the plan (for the bucket sub-plans)
+  std::vector<dtfe::OptWork> hwork;
+  std::map<std::pair<long, long>, SubPlan> sub;
 };
 struct WorkerCh {
   void* mailbox = nullptr;       // this worker's gradient mailbox (ps GPU)
@@ -295,6 +313,11 @@ struct WorkerCh {
   std::vector<uint32_t*> done;   // per-group done counters (this channel's launches)
   bool waiting = false;          // sync mode: accumulated, reply pending
   uint64_t wait_seq = 0;
+  // async bucket applies of the coming request: last bucket sequence applied per bucket, and the
+  // ranges applied for request `range_seq`
+  uint64_t bkt_done[dtfe::PS_MAX_BUCKETS] = {};
+  uint64_t range_seq = 0;
+  std::vector<std::pair<long, long>> ranges;
 };
 struct Service {
   Shm* shm = nullptr;
@@ -304,6 +327,7 @@ struct Service {
   std::vector<Group> groups;
   std::vector<WorkerCh> ch;
   const int32_t* gs = nullptr;
+  long total = 0;                // shard-flat elements (bucket ranges are clamped to it)
   float* acc = nullptr;          // sync mode accumulator (fp32, shard layout)
   long acc_n = 0;
   int acc_count = 0;
@@ -311,7 +335,7 @@ struct Service {
   hipStream_t stream = nullptr;
   std::thread th;
   std::atomic<bool> stop{false}, pause{false}, paused{false};
-  std::atomic<int64_t> n_req{0}, n_apply{0}, n_stale{0};
+  std::atomic<int64_t> n_req{0}, n_apply{0}, n_stale{0}, n_bucket{0};
   std::string error;
 };
 std::vector<Service*> g_svc;
@@ -360,6 +384,10 @@ void ps_service_add_group(int64_t h, int64_t kind, Tensor p, const c10::optional
   a.work = reinterpret_cast<const dtfe::OptWork*>((const char*)blob.data_ptr() + off);
   a.nwork = (int)nwork;
   g.g16 = g16;
+  g.hsegs.resize((size_t)nseg);
+  g.hwork.resize((size_t)nwork);
+  if (nseg) hchk(hipMemcpy(g.hsegs.data(), a.segs, bs, hipMemcpyDeviceToHost), "plan segs D2H");
+  if (nwork) hchk(hipMemcpy(g.hwork.data(), a.work, (size_t)nwork * sizeof(dtfe::OptWork), hipMemcpyDeviceToHost), "plan work D2H");
   s->groups.push_back(g);
 }
 
@@ -375,6 +403,8 @@ void ps_service_set_worker(int64_t h, int64_t w, int64_t mailbox_addr, const Ten
 }
 
 void ps_service_set_gs(int64_t h, const Tensor& gs) { svc_of(h)->gs = gs.data_ptr<int32_t>(); }
+
+void ps_service_set_total(int64_t h, int64_t total) { svc_of(h)->total = (long)total; }
 
 void ps_service_set_acc(int64_t h, Tensor acc) {
   Service* s = svc_of(h);
@@ -396,6 +426,68 @@ void launch_apply(Service* s, WorkerCh& c, hipStream_t st, const void* grad, boo
     a.done_counter = c.done[gi];
     dtfe::launch_apply_gradients(a, st);
   }
+}
+
+// the sub-plan of group g over shard range [lo, hi) (every variable lies wholly inside or outside)
+const SubPlan& sub_plan(Service* s, Group& g, long lo, long hi) {
+  auto key = std::make_pair(lo, hi);
+  auto it = g.sub.find(key);
+  if (it != g.sub.end()) return it->second;
+  std::vector<dtfe::OptWork> wk;
+  for (const auto& w : g.hwork) {
+    const long off = g.hsegs[(size_t)w.seg].off;
+    if (off >= lo && off < hi) wk.push_back(w);
+  }
+  SubPlan p;
+  p.nwork = (int)wk.size();
+  const size_t bs = g.hsegs.size() * sizeof(dtfe::OptSeg), off = (bs + 255) / 256 * 256;
+  std::vector<uint8_t> host(off + wk.size() * sizeof(dtfe::OptWork) + 16, 0);
+  if (bs) std::memcpy(host.data(), g.hsegs.data(), bs);
+  if (!wk.empty()) std::memcpy(host.data() + off, wk.data(), wk.size() * sizeof(dtfe::OptWork));
+  p.blob = at::empty({(int64_t)host.size()}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, s->device));
+  (void)hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice);
+  return g.sub.emplace(key, std::move(p)).first->second;
+}
+
+// apply the mailbox over shard range [lo, hi) with every group, leaving the step scalars alone
+void launch_apply_range(Service* s, WorkerCh& c, hipStream_t st, long lo, long hi) {
+  for (size_t gi = 0; gi < s->groups.size(); ++gi) {
+    Group& g = s->groups[gi];
+    const SubPlan& p = sub_plan(s, g, lo, hi);
+    if (p.nwork == 0) continue;
+    dtfe::OptArgs a = g.args;
+    if (g.g16) {
+      a.g = nullptr;
+      a.g16 = reinterpret_cast<const dtfe::bf16*>(c.mailbox);
+    } else {
+      a.g = reinterpret_cast<const float*>(c.mailbox);
+      a.g16 = nullptr;
+    }
+    const size_t bs = g.hsegs.size() * sizeof(dtfe::OptSeg), off = (bs + 255) / 256 * 256;
+    a.segs = reinterpret_cast<const dtfe::OptSeg*>(p.blob.data_ptr());
+    a.work = reinterpret_cast<const dtfe::OptWork*>((const char*)p.blob.data_ptr() + off);
+    a.nwork = p.nwork;
+    a.gscale = 1.f;
+    a.skip_advance = 1;
+    a.done_counter = c.done[gi];
+    dtfe::launch_apply_gradients(a, st);
+  }
+}
+
+// async push with buckets: apply every bucket range of request `seq` not applied yet (the gaps
+// between the ranges already applied - all of the shard when the worker sent no bucket), then
+// advance each group's step scalars once
+void finish_bucketed(Service* s, WorkerCh& c, hipStream_t st, uint64_t seq) {
+  std::vector<std::pair<long, long>> done = c.range_seq == seq ? c.ranges : std::vector<std::pair<long, long>>{};
+  std::sort(done.begin(), done.end());
+  long at = 0;
+  for (const auto& r : done) {
+    if (r.first > at) launch_apply_range(s, c, st, at, r.first);
+    at = std::max(at, r.second);
+  }
+  if (at < s->total) launch_apply_range(s, c, st, at, s->total);
+  for (const auto& g : s->groups) dtfe::launch_opt_advance(g.args, st);
+  c.ranges.clear();
 }
 
 void reply(Service* s, int w, hipStream_t st, uint64_t seq, int stale) {
@@ -467,6 +559,28 @@ void run(Service* s) {
     for (int w = 0; w < s->nworkers; ++w) {
       auto& c = s->ch[(size_t)w];
       uint64_t* sl = slot_host(s->shm, w);
+      hipStream_t bst = c.stream ? c.stream : s->stream;
+      // async: apply each pushed bucket as soon as it is announced (the worker is still in backward)
+      auto scan_buckets = [&](uint64_t floor) {  // buckets of requests after `floor`
+        for (int b = 0; b < dtfe::PS_MAX_BUCKETS; ++b) {
+          const uint64_t bseq = __atomic_load_n(sl + dtfe::PS_BKT_BASE + 3 * b, __ATOMIC_ACQUIRE);
+          if (bseq <= floor || bseq <= c.bkt_done[b]) continue;
+          const long lo = std::max(0L, (long)__atomic_load_n(sl + dtfe::PS_BKT_BASE + 3 * b + 1, __ATOMIC_ACQUIRE));
+          const long hi = std::min(s->total, (long)__atomic_load_n(sl + dtfe::PS_BKT_BASE + 3 * b + 2, __ATOMIC_ACQUIRE));
+          c.bkt_done[b] = bseq;
+          if (c.range_seq != bseq) {
+            c.range_seq = bseq;
+            c.ranges.clear();
+          }
+          if (lo < hi) {
+            launch_apply_range(s, c, bst, lo, hi);
+            c.ranges.emplace_back(lo, hi);
+            s->n_bucket++;
+          }
+          any = true;
+        }
+      };
+      if (!s->sync && s->total > 0) scan_buckets(c.handled);
       const uint64_t seq = __atomic_load_n(sl + dtfe::PS_REQ_SEQ, __ATOMIC_ACQUIRE);
       if (seq == c.handled) continue;
       c.handled = seq;
@@ -479,7 +593,12 @@ void run(Service* s) {
         continue;
       }
       if (!s->sync) {
-        launch_apply(s, c, st, c.mailbox, false, 1.f);
+        if (s->total > 0) {
+          scan_buckets(seq - 1);  // bucket words published just before this request
+          finish_bucketed(s, c, st, seq);
+        } else {
+          launch_apply(s, c, st, c.mailbox, false, 1.f);
+        }
         s->version++;
         s->n_apply++;
         reply(s, w, st, seq, 0);
@@ -553,7 +672,8 @@ void ps_service_resume(int64_t h) { svc_of(h)->pause.store(false, std::memory_or
 
 Tensor ps_service_stats(int64_t h) {
   Service* s = svc_of(h);
-  Tensor t = at::empty({4}, at::TensorOptions().dtype(at::kLong));
+  Tensor t = at::empty({5}, at::TensorOptions().dtype(at::kLong));
+  t.data_ptr<int64_t>()[4] = s->n_bucket.load();
   t.data_ptr<int64_t>()[0] = s->n_req.load();
   t.data_ptr<int64_t>()[1] = s->n_apply.load();
   t.data_ptr<int64_t>()[2] = s->n_stale.load();
@@ -606,6 +726,8 @@ TORCH_LIBRARY_FRAGMENT(dtfe, m) {
         " Tensor blob, int nseg, int nwork, bool g16) -> ()", &ps_service_add_group);
   m.def("ps_service_set_worker(int h, int w, int mailbox_addr, Tensor snap, int snap_nseg, int snap_nwork) -> ()",
         &ps_service_set_worker);
+  m.def("ps_service_set_total(int h, int total) -> ()", &ps_service_set_total);
+  m.def("ps_bucket(int shm, int w, Tensor ctr, int b, int lo, int hi) -> ()", &ps_bucket);
   m.def("ps_service_set_gs(int h, Tensor gs) -> ()", &ps_service_set_gs);
   m.def("ps_service_set_acc(int h, Tensor(a!) acc) -> ()", &ps_service_set_acc);
   m.def("ps_service_start(int h) -> ()", &ps_service_start);

@@ -48,15 +48,7 @@ bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGe
 template <int BM, int BN, int AM, int BMD, int STAGES>
 static void launch_glds(int splits, const DenseGemmArgs& a, hipStream_t s) {
   const int tiles = (a.M / BM) * ((a.N + BN - 1) / BN);
-  if (a.hw.blocks) {
-    using SM = GlSmem<BM, BN, STAGES>;
-    if (splits != 1 || a.hw.B > 1024 || a.hw.B * 32 > SM::BYTES || 16 * 16 * 11 * 4 > SM::BYTES || a.hw.K % 16 ||
-        a.hw.ld_dl < 16 || a.hw.ld_dl % 8 || (uintptr_t)a.hw.dl % 16 || a.hw.blocks % 8 ||
-        a.hw.blocks * 16 < a.hw.K + (a.hw.db ? 16 : 0))
-      throw std::runtime_error("gemm: fused head weight gradient needs one split, B <= 1024, K % 16 == 0, "
-                               "16-B aligned dlogit rows and a multiple-of-8 block count");
-  }
-  dim3 grid(tiles + a.hw.blocks, 1, splits);
+  dim3 grid(tiles, 1, splits);
   hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, AM, BMD, STAGES>), grid, dim3(GEMM_THREADS), 0, s, a);
 }
 

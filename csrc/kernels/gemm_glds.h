@@ -89,60 +89,6 @@ struct GlOperand {
   }
 };
 
-// Fused head weight gradient (HeadFuse), one 256-thread workgroup per 16 columns of h (the last
-// one: the bias, reading h as ones).  Thread (c = t & 15, rg = t >> 4) accumulates column c over
-// rows rg, rg + 16, ... with the batch's dlogit rows staged in LDS; the 16 row-group partials are
-// summed in order (deterministic).  LDS: B x 32 B of dlogits, then 16 x 16 x 11 floats.
-__device__ __forceinline__ void head_wgrad_tile(const HeadFuse& f, int blk, char* smem) {
-  constexpr int NC = 10;
-  if (blk * 16 > f.K || (blk * 16 == f.K && !f.db)) return;  // padding workgroups (uniform exit)
-  const int t = threadIdx.x, c = t & 15, rg = t >> 4;
-  const bool bias_blk = blk * 16 == f.K;
-  bf16(*dls)[16] = reinterpret_cast<bf16(*)[16]>(smem);
-  for (int i = t; i < f.B * 2; i += 256) {
-    const int b = i >> 1;
-    *reinterpret_cast<u32x4_t*>(&dls[b][(i & 1) * 8]) =
-        *reinterpret_cast<const u32x4_t*>(f.dl + (long)b * f.ld_dl + (i & 1) * 8);
-  }
-  __syncthreads();
-  float acc[NC];
-#pragma unroll
-  for (int n = 0; n < NC; ++n) acc[n] = 0.f;
-  const int col = blk * 16 + c;
-  for (int b0 = rg; b0 < f.B; b0 += 16 * 8) {
-    float hv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + 16 * u;
-      hv[u] = b < f.B ? (bias_blk ? 1.f : bf2f(f.h[(long)b * f.ldh + col])) : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + 16 * u;
-      if (b >= f.B) break;
-      const u32x4_t d0 = *reinterpret_cast<const u32x4_t*>(&dls[b][0]);
-      const u32x4_t d1 = *reinterpret_cast<const u32x4_t*>(&dls[b][8]);
-#pragma unroll
-      for (int n = 0; n < NC; ++n) {
-        const uint32_t w = n < 8 ? d0[n >> 1] : d1[(n - 8) >> 1];
-        acc[n] = fmaf(bf2f((bf16)(w >> (16 * (n & 1)))), hv[u], acc[n]);
-      }
-    }
-  }
-  __syncthreads();  // every thread is done with the staged rows
-  float(*part)[16][NC + 1] = reinterpret_cast<float(*)[16][NC + 1]>(smem);
-#pragma unroll
-  for (int n = 0; n < NC; ++n) part[rg][c][n] = acc[n];
-  __syncthreads();
-  if (t < 16 * NC) {
-    const int cc = t % 16, n = t / 16;
-    float v = 0.f;
-    for (int r = 0; r < 16; ++r) v += part[r][cc][n];
-    if (!bias_blk) f.dw[(long)n * f.ldw + blk * 16 + cc] = v * f.scale;
-    else if (cc == 0) f.db[n] = v * f.scale;
-  }
-}
-
 template <int BM, int BN, int STAGES> struct GlSmem {
   static constexpr int STAGE_EL = (BM + BN) * GL_BK;
   static constexpr int STAGING = STAGES * STAGE_EL * 2;
@@ -160,14 +106,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_kernel(DenseGemmArg
   __shared__ __attribute__((aligned(16))) char smem_raw[SM::BYTES];
   bf16* smem = reinterpret_cast<bf16*>(smem_raw);
 
-  int bid = blockIdx.x;
-  if (a.hw.blocks) {  // the fused head weight gradient's workgroups come first
-    if (bid < a.hw.blocks) {
-      head_wgrad_tile(a.hw, bid, smem_raw);
-      return;
-    }
-    bid -= a.hw.blocks;
-  }
+  const int bid = blockIdx.x;
   const int tiles_m = a.M / BM, tiles_n = (a.N + BN - 1) / BN;
   int tm, tn;
   tile_coords(bid, tiles_m, tiles_n, tm, tn);

@@ -601,94 +601,6 @@ __global__ __launch_bounds__(256) void bn_part_stage2(const float* __restrict__ 
   }
 }
 
-// stage 1 + stage 2 in ONE launch (grid (ceil(N/64), P)): every workgroup folds its chunk, then the
-// last of a channel group's P workgroups to arrive (counter hand-off of gemm_dense.h: plain stores,
-// one agent-scope release + ticket, one acquire) folds the P chunks in order - same arithmetic
-// and order as the two-launch form, one graph node fewer per fused convolution
-__global__ __launch_bounds__(256) void bn_part_fused(const float* __restrict__ part, int tiles, int N, long Mp,
-                                                     int BMr, float* __restrict__ chunk, int P, int* ctr,
-                                                     float* __restrict__ stats) {
-  __shared__ float red[4][2][64];
-  __shared__ int is_last;
-  const int cl = threadIdx.x & 63, ln = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, p = blockIdx.y;
-  {
-    const int t0 = p * BN_TCH, t1 = min(tiles, t0 + BN_TCH);
-    float S = 0.f, Q = 0.f, K = 0.f;
-    if (c < N) {
-      K = part[(long)t0 * 3 * N + c];
-      constexpr int PT = BN_TCH / 4;
-      float kt[PT], st[PT], qt[PT];
-#pragma unroll
-      for (int i = 0; i < PT; ++i) {
-        const int t = t0 + ln + 4 * i;
-        const float* pt = part + (long)(t < t1 ? t : t0) * 3 * N + c;
-        kt[i] = pt[0];
-        st[i] = pt[N];
-        qt[i] = pt[2 * N];
-      }
-#pragma unroll
-      for (int i = 0; i < PT; ++i) {
-        const int t = t0 + ln + 4 * i;
-        if (t < t1) shift_fold(kt[i], st[i], qt[i], (float)min((long)BMr, Mp - (long)t * BMr), K, S, Q);
-      }
-    }
-    red[ln][0][cl] = S;
-    red[ln][1][cl] = Q;
-    __syncthreads();
-    if (ln == 0 && c < N) {
-      float* o = chunk + (long)p * 3 * N + c;
-      o[0] = K;
-      o[N] = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
-      o[2 * N] = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(ctr + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == P - 1;
-    if (last) {
-      __hip_atomic_store(ctr + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    is_last = last;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  float S = 0.f, Q = 0.f;
-  if (c < N) {
-    const float K = chunk[c];
-    const long rows_chunk = (long)BN_TCH * BMr;
-    for (int p0 = ln; p0 < P; p0 += 4 * 8) {
-      float kp[8], sp[8], qp[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int pp = p0 + 4 * i;
-        const float* pc = chunk + (long)(pp < P ? pp : 0) * 3 * N + c;
-        kp[i] = pc[0];
-        sp[i] = pc[N];
-        qp[i] = pc[2 * N];
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int pp = p0 + 4 * i;
-        if (pp < P) shift_fold(kp[i], sp[i], qp[i], (float)min(rows_chunk, Mp - (long)pp * rows_chunk), K, S, Q);
-      }
-    }
-  }
-  __syncthreads();  // red is reused
-  red[ln][0][cl] = S;
-  red[ln][1][cl] = Q;
-  __syncthreads();
-  if (ln == 0 && c < N) {
-    stats[c] += ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
-    stats[N + c] += ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
-  }
-}
-
 // ------------------------------------------------------------ host helpers
 struct DevScratch {
   void* zeros = nullptr;
@@ -739,22 +651,6 @@ float* workspace(size_t bytes, hipStream_t s, DevScratch* pool = g_dev) {
 }
 
 DevScratch g_bn[64];
-int* g_bn_ctr[64];  // per-device hand-off counters of bn_part_fused (<= 64 channel groups)
-
-int* bn_counters(hipStream_t s) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_bn_ctr[dev]) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(s, &st);
-    if (st != hipStreamCaptureStatusNone) throw std::runtime_error("igemm: first BN counter use inside a graph capture");
-    if (hipMalloc(&g_bn_ctr[dev], 64 * sizeof(int)) != hipSuccess) throw std::runtime_error("igemm: BN counter alloc");
-    if (hipMemset(g_bn_ctr[dev], 0, 64 * sizeof(int)) != hipSuccess) throw std::runtime_error("igemm: BN counter memset");
-    (void)hipDeviceSynchronize();
-  }
-  return g_bn_ctr[dev];
-}
 
 float* bn_workspace(size_t bytes, hipStream_t s) {
   int dev = 0;
@@ -857,14 +753,10 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
   float* chunk = a.bn_part + (size_t)tiles_all * 3 * a.N;
   const unsigned cg = (unsigned)((a.N + 63) / 64);
   // (backward partials carry a zero shift: the row counts passed here then do not enter the fold)
-  static const int one_launch = env_int("DTFE_BN_PART_1L", 0);  // bn_part_fused (opt-in until measured)
-  if (!one_launch || cg > 64) {
-    hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_all, a.N, Mmax, t.bm, chunk);
-    hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, a.N, Mmax, t.bm, bn_stats);
-  } else {
-    hipLaunchKernelGGL(bn_part_fused, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_all, a.N, Mmax, t.bm, chunk,
-                       nchunk, bn_counters(s), bn_stats);
-  }
+  // (a one-launch variant - last-arriving workgroup per channel group folds the chunks - saved a
+  // graph node per conv but shared one hand-off counter array per device; removed in round 3)
+  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_all, a.N, Mmax, t.bm, chunk);
+  hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, a.N, Mmax, t.bm, bn_stats);
   return true;
 }
 

@@ -676,23 +676,9 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
 
 bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
-  static const bool fixed_ok = [] {
-    const char* e = getenv("DTFE_IC_FIXED");
-    return !(e && atoi(e) == 0);
-  }();
-  if (fixed_ok && a.OH == 14 && a.OW == 14 && a.B >= 256) {
-    // DTFE_IC_RT: 16-row tiles per wave (1: 13 waves, 2: 7 waves, 4: 4 waves) - experiments
-    static const int rt = [] {
-      const char* e = getenv("DTFE_IC_RT");
-      return e ? atoi(e) : 1;
-    }();
-    if (rt == 2) {
-      if (launch_fixed<32, 5, 5, 20, 48, 4, 2, 7, false>(a, s)) return true;
-      if (launch_fixed<64, 5, 5, 20, 80, 2, 2, 7, true>(a, s)) return true;
-    } else if (rt == 4) {
-      if (launch_fixed<32, 5, 5, 20, 48, 4, 4, 4, false>(a, s)) return true;
-      if (launch_fixed<64, 5, 5, 20, 80, 2, 4, 4, true>(a, s)) return true;
-    }
+  if (a.OH == 14 && a.OW == 14 && a.B >= 256) {
+    // compile-time geometry, one 16-row tile per wave (13 waves); 2 / 4 tiles per wave (7 / 4
+    // waves) measured slower and were removed in round 3
     if (launch_fixed<32, 5, 5, 20, 48, 4, 1, 13, false>(a, s)) return true;  // conv2 forward
     if (launch_fixed<64, 5, 5, 20, 80, 2, 1, 13, true>(a, s)) return true;   // conv2 data gradient
   }
@@ -703,24 +689,11 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
     const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
     if (pooled && (a.SH + a.pad > LH || a.SW + a.pad > LW)) return false;
   }
-  // wave grid (measured on MNIST conv2, B=1024): 8 x 2 waves, 4 per SIMD (default: fwd 48 us, dgrad 68)
-  // beat 4 x 2 (48 / 74) and 4 x 1 waves holding
-  // every n-tile (fewer LDS reads, but one wave per SIMD exposes the read latency: fwd 48 vs 63 us).
-  // DTFE_IC_WAVES=4 / 8 select 4 x 1 / 4 x 2 for experiments.
-  static const int waves = [] {
-    const char* e = getenv("DTFE_IC_WAVES");
-    return e ? atoi(e) : 16;
-  }();
-  if (waves == 4) {
-    if (a.N <= 32) return pooled ? launch_cfg<2, 4, 4, 1, true>(a, s) : launch_cfg<2, 4, 4, 1, false>(a, s);
-    return pooled ? launch_cfg<4, 4, 4, 1, true>(a, s) : launch_cfg<4, 4, 4, 1, false>(a, s);
-  }
-  if (waves == 16) {  // 8 x 2 waves, 4 per SIMD
-    if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s) : launch_cfg<1, 2, 8, 2, false>(a, s);
-    return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s) : launch_cfg<2, 2, 8, 2, false>(a, s);
-  }
-  if (a.N <= 32) return pooled ? launch_cfg<1, 4, 4, 2, true>(a, s) : launch_cfg<1, 4, 4, 2, false>(a, s);
-  return pooled ? launch_cfg<2, 4, 4, 2, true>(a, s) : launch_cfg<2, 4, 4, 2, false>(a, s);
+  // wave grid (measured on MNIST conv2, B=1024): 8 x 2 waves, 4 per SIMD (fwd 48 us, dgrad 68) beat
+  // 4 x 2 (48 / 74) and 4 x 1 waves holding every n-tile (fewer LDS reads, but one wave per SIMD
+  // exposes the read latency: fwd 48 vs 63 us); the alternatives were removed in round 3
+  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s) : launch_cfg<1, 2, 8, 2, false>(a, s);
+  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s) : launch_cfg<2, 2, 8, 2, false>(a, s);
 }
 
 }  // namespace dtfe

@@ -31,9 +31,7 @@ __device__ __forceinline__ float upd(const OptArgs& a, float lr_t, float v, floa
     s1 = s1 * a.momentum + g;
     return v - a.lr * s1;
   } else if constexpr (KIND == OPT_ADAM) {
-    s1 = s1 * a.beta1 + (1.f - a.beta1) * g;
-    s2 = s2 * a.beta2 + (1.f - a.beta2) * g * g;
-    return v - lr_t * s1 / (sqrtf(s2) + a.eps);
+    return tf1_adam(v, g, s1, s2, lr_t, a.beta1, a.beta2, a.eps);
   } else {
     s1 = s1 * a.rho + (1.f - a.rho) * g * g;
     s2 = s2 * a.momentum + a.lr * g / sqrtf(s1 + a.eps);
@@ -126,10 +124,7 @@ __device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long 
 template <int KIND>
 __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, bf16 (&tile)[64][66]) {
   float lr_t = a.lr;
-  if (KIND == OPT_ADAM) {
-    const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
-    lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-  }
+  if (KIND == OPT_ADAM) lr_t = tf1_adam_lr(a.lr, a.beta_pow);
   for (int wi = bid; wi < a.nwork; wi += nblk) {
     const OptWork w = a.work[wi];
     const OptSeg sg = a.segs[w.seg];
@@ -173,14 +168,14 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(a.done_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (uint32_t)nblk - 1) {
+    if (prev == (uint32_t)nblk - 1 && !a.skip_advance) {
       if (KIND == OPT_ADAM) {
         a.beta_pow[0] *= a.beta1;
         a.beta_pow[1] *= a.beta2;
       }
       if (a.global_step && a.gs_inc) atomicAdd(a.global_step, a.gs_inc);
-      __hip_atomic_store(a.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (prev == (uint32_t)nblk - 1) __hip_atomic_store(a.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -199,6 +194,15 @@ __global__ __launch_bounds__(256) void apply_gradients_group_kernel(OptGroup g) 
   int i = 0;
   while (i + 1 < g.n && (int)blockIdx.x >= g.first[i + 1]) ++i;
   apply_body<KIND>(g.o[i], blockIdx.x - g.first[i], g.first[i + 1] - g.first[i], tile);
+}
+
+__global__ void opt_advance_kernel(OptArgs a) {
+  if (threadIdx.x != 0) return;
+  if (a.kind == OPT_ADAM && a.beta_pow) {
+    a.beta_pow[0] *= a.beta1;
+    a.beta_pow[1] *= a.beta2;
+  }
+  if (a.global_step && a.gs_inc) atomicAdd(a.global_step, a.gs_inc);
 }
 
 static int apply_blocks(const OptArgs& a) {
@@ -223,6 +227,10 @@ void launch_apply_gradients_group(const OptArgs* o, int n, hipStream_t s) {
     case OPT_ADAM: hipLaunchKernelGGL(apply_gradients_group_kernel<OPT_ADAM>, grid, dim3(256), 0, s, g); break;
     default: hipLaunchKernelGGL(apply_gradients_group_kernel<OPT_RMSPROP>, grid, dim3(256), 0, s, g); break;
   }
+}
+
+void launch_opt_advance(const OptArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(opt_advance_kernel, dim3(1), dim3(64), 0, s, a);
 }
 
 void launch_apply_gradients(const OptArgs& a, hipStream_t s) {

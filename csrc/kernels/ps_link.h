@@ -34,7 +34,8 @@ struct PsWork {
 };
 
 constexpr int PS_MAX_WORKERS = 64;
-constexpr int PS_SLOT_WORDS = 16;  // 128 B per worker slot (own cache lines)
+constexpr int PS_SLOT_WORDS = 32;  // 256 B per worker slot (own cache lines)
+constexpr int PS_MAX_BUCKETS = 4;
 
 // shared page layout (uint64 words): [worker w][PS_SLOT_WORDS] of
 enum PsWord : int {
@@ -44,9 +45,16 @@ enum PsWord : int {
   PS_REP_SEQ = 8,   // written last by the ps's GPU: the request number answered
   PS_REP_GS = 9,    // global step after the apply (the gs shard; -1 elsewhere)
   PS_REP_VER = 10,  // shard version after the apply
-  PS_REP_STALE = 11 // 1 when a sync-mode gradient was dropped as stale
+  PS_REP_STALE = 11, // 1 when a sync-mode gradient was dropped as stale
+  // bucket b (< PS_MAX_BUCKETS) of the coming push: its gradient range [LO, HI) (shard-flat
+  // elements) is in the mailbox; BKT_SEQ is written last = the request number it belongs to.
+  // The ps applies the range as soon as it sees it (async mode), overlapping the worker's backward.
+  PS_BKT_BASE = 16   // + 3b: BKT_SEQ, + 3b + 1: BKT_LO, + 3b + 2: BKT_HI
 };
 enum PsKind : int { PS_PUSH = 1, PS_PULL = 2 };
+
+// worker GPU, after bucket b's push: slot[BKT_LO/HI(b)] = lo / hi; slot[BKT_SEQ(b)] = *ctr + 1 (release)
+void launch_ps_bucket(uint64_t* slot, const int64_t* ctr, int b, long lo, long hi, hipStream_t s);
 
 // the copy plan: nwork items over the segments (one launch)
 void launch_ps_copy(const PsSeg* segs, const PsWork* work, int nwork, hipStream_t s);

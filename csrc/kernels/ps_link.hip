@@ -102,6 +102,16 @@ __global__ void ps_request_kernel(uint64_t* slot, int64_t* ctr, const int64_t* v
   __hip_atomic_store(slot + PS_REQ_SEQ, (uint64_t)c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__global__ void ps_bucket_kernel(uint64_t* slot, const int64_t* ctr, int b, long lo, long hi) {
+  if (threadIdx.x != 0) return;
+  // the bucket's push copies (earlier on this stream) have completed: publish its range
+  __threadfence_system();
+  st_sys(slot + PS_BKT_BASE + 3 * b + 1, (uint64_t)lo);
+  st_sys(slot + PS_BKT_BASE + 3 * b + 2, (uint64_t)hi);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __hip_atomic_store(slot + PS_BKT_BASE + 3 * b, (uint64_t)(*ctr + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void ps_wait_kernel(PsWaitArgs a) {
   if (threadIdx.x != 0) return;
   const uint64_t target = (uint64_t)*a.ctr;
@@ -141,6 +151,10 @@ void launch_ps_copy(const PsSeg* segs, const PsWork* work, int nwork, hipStream_
 
 void launch_ps_request(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, int bump, hipStream_t s) {
   hipLaunchKernelGGL(ps_request_kernel, dim3(1), dim3(64), 0, s, slot, ctr, ver, kind, bump);
+}
+
+void launch_ps_bucket(uint64_t* slot, const int64_t* ctr, int b, long lo, long hi, hipStream_t s) {
+  hipLaunchKernelGGL(ps_bucket_kernel, dim3(1), dim3(64), 0, s, slot, ctr, b, lo, hi);
 }
 
 void launch_ps_wait(const PsWaitArgs& a, hipStream_t s) {

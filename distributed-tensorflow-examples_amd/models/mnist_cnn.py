@@ -198,34 +198,29 @@ class MnistCnnTrainer:
         # weight grad) run on their own streams: inside the captured hipGraph they become
         # parallel branches that fill the CUs the dgrad chain leaves idle.  conv2's weight
         # grad gets its own partial-sum workspace (conv1's runs concurrently on the main stream).
+        # DTFE_CNN_BRANCHES (A/B only): "fc,c2" (default), "fc", "c2" or "none".  Measured-slower
+        # schedules were removed in round 3: the head weight gradient inside the fc1 dgrad launch
+        # (profiles/r2_cnn_head_fuse_ab.txt), one combined weight-gradient branch, the critical
+        # chain captured first (profiles/r2_cnn_branch_orders.txt), and the fc/head Adam as its own
+        # launch on the fc branch (313-325 vs 293 us; superseded by the fc1 GEMM Adam epilogue).
         self.fused_gather = os.environ.get("DTFE_CNN_FUSED_GATHER", "1") != "0"
         br = os.environ.get("DTFE_CNN_BRANCHES", "fc,c2").split(",")
-        self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2", "side1"})
-        # capture order of the branched backward (DTFE_CNN_ORDER): "branch" = each branch's work
-        # captured before the critical chain continues, "crit" = the critical chain first
-        self.crit_first = os.environ.get("DTFE_CNN_ORDER", "branch") == "crit"
-        # DTFE_CNN_FC1W_SPLIT=2: fc1's weight gradient as two launches of half the rows.  The hipGraph
-        # runtime executes dependency level by level: with the head gradient fused into fc1 dgrad, a
-        # single fc1 wgrad node sits on fc1 dgrad's level and holds the conv2 stage back; split, its
-        # second half lands on the conv2 stage's level
-        self.fc1w_split = int(os.environ.get("DTFE_CNN_FC1W_SPLIT", "1"))
-        self.br_one = self.par and "side1" in br   # ONE weight-grad branch forked after fc1 dgrad
-        self.br_fc = self.par and not self.br_one and "fc" in br
-        self.br_c2 = self.par and (self.br_one or "c2" in br)
+        self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2"})
+        self.br_fc = self.par and "fc" in br
+        self.br_c2 = self.par and "c2" in br
         self.c2_blocks = int(os.environ.get("DTFE_CNN_C2_BLOCKS", "128"))
-        # early apply (DTFE_CNN_EARLY_APPLY=1; off by default - measured 313-325 vs 293 us/step on
-        # one MI355X: the HBM-bound Adam slows the concurrent conv backward more than it hides):
-        # when step() runs the whole step, the fc/head variables (98% of the
-        # parameters, ~21 us of HBM-bound Adam) are updated on the fc branch as soon as their
-        # gradients are final (all-reduced), concurrently with the conv backward; the conv
-        # variables are applied at the end.  Split optimizers share the slot buffers; each keeps
-        # its own beta powers (both advance once per step).
         # Data-parallel "late split" (default whenever an all-reduce is attached): the fc/head Adam
         # (bucket 0, already reduced during the conv backward) runs while the small conv bucket's
         # all-reduce is still in flight, so that collective's latency hides behind ~20 us of Adam.
-        self.opt_fc = self.opt_conv = None
+        self.opt_fc = self.opt_conv = self.opt_rest = None
         self._apply = None
-        self.early_apply = os.environ.get("DTFE_CNN_EARLY_APPLY", "0") != "0"
+        # One replica (no all-reduce): fc1's weight gradient is final when its GEMM produces it, so
+        # that GEMM applies Adam to fc1's weights and bias in its epilogue (TF1 math shared with the
+        # fused optimizer kernel - bitwise the same update) instead of storing the gradient; the
+        # step's closing Adam covers only the other 62 K parameters.  98% of the Adam traffic moves
+        # off the step's tail onto the fc branch, and the fp32 fc1 gradient never touches HBM.
+        # DTFE_CNN_FUSED_ADAM=0: the separate whole-model Adam launch.
+        self.fused_adam = os.environ.get("DTFE_CNN_FUSED_ADAM", "1") != "0"
         self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
         # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
@@ -239,12 +234,6 @@ class MnistCnnTrainer:
         # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
         # workspace, since it runs on the fc branch beside other GEMMs
         self.head_gemm = os.environ.get("DTFE_CNN_HEAD_GEMM", "0") == "1" or batch > 1024
-        # DTFE_CNN_HEAD_FUSE=1: the head weight gradient rides in the fc1 data-gradient launch (extra
-        # workgroups of the glds GEMM, no graph node of its own).  Off by default: the hipGraph
-        # runtime's queue / level schedule of the resulting graph measured 8-10 us slower per step
-        # (profiles/r2_cnn_head_fuse_ab.txt); the head gradient keeps its own kernel on the fc branch.
-        self.head_fused = (not self.head_gemm and self.device.type == "cuda" and self.t_dgrad is not None
-                           and os.environ.get("DTFE_CNN_HEAD_FUSE", "0") != "0")
         self.head_splits = max(1, min(16, B // 128))
         bm, bn = ops.TILE_DIMS[4]
         ntiles = -(-NCLS // bm) * -(-(FC + 1) // bn)
@@ -290,58 +279,23 @@ class MnistCnnTrainer:
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep,
                       step_counter=self.data_ctr if fused else None)
         main = torch.cuda.current_stream(self.device) if self.par else None
-        if self.br_one:
-            self._backward_one_branch(main)
-            return
-        # Capture order changes how the hipGraph runtime maps the branches onto hardware queues (every
-        # edge between queues costs ~5-10 us of dependency latency on this step's timeline): with
-        # crit_first the fork point is recorded on the branch stream and the critical chain is
-        # captured before the branch work; otherwise the branch work comes first.
-        crit = self.crit_first
-        if self.br_fc and crit:
-            self.s_fc.wait_stream(main)        # fork: the weight-grad branch depends on head_xent only
-        if crit:
-            self._fc1_dgrad(B, K1)
-        with (self._branch(self.s_fc, main) if (self.br_fc and not crit) else
-              torch.cuda.stream(self.s_fc) if self.br_fc else contextlib.nullcontext()):
-            if not self.head_fused:
-                self._head_wgrad()
+        # weight-gradient branch of the fc layers (forked after head_xent), then the dgrad chain
+        with self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext():
+            self._head_wgrad()
             # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
-            parts = self.fc1w_split if (self.t_wgrad is not None and FC % (64 * self.fc1w_split) == 0) else 1
-            rows = FC // parts
-            for i in range(parts):
-                r0 = i * rows
-                ops.gemm(self.dzf.view(-1)[r0:], self.p2, self.gw["wd1"][r0:], M=rows, N=K1 + 1, K=B,
-                         amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1,
-                         bias_out=self.gw["bd1"][r0:], tile=self.t_wgrad)
-            if self.allreduce is not None and not self.head_fused:
+            fused_adam = self._apply is not None and self._apply[0] == "fused"
+            ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
+                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad,
+                     adam=self._fc1_adam_args() if fused_adam else None)
+            if self.allreduce is not None:
                 self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
-        if not crit:
-            self._fc1_dgrad(B, K1)
-        if self.allreduce is not None and self.head_fused:
-            # the head gradient (in bucket 0) is written by the fc1 dgrad launch: bucket 0 forks
-            # once both the fc branch (fc1 wgrad) and that launch are done
-            with (self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext()):
-                self.allreduce.launch(0)
-        if self._apply is not None and self._apply[0] == "early":
-            # fc/head Adam as soon as their (reduced) gradients are final - and after fc1 dgrad, the
-            # last reader of the fc1 weights this step (the branch re-joins main's progress here)
-            with self._branch(self.s_fc, main):
-                if self.allreduce is not None:
-                    self.allreduce.wait_launched()
-                self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
-        if self.br_c2 and crit:
-            self.s_c2.wait_stream(main)        # fork after fc1 dgrad (dP2 final)
-        if crit:
-            self._conv2_dgrad()
-        with (self._branch(self.s_c2, main) if (self.br_c2 and not crit) else
-              torch.cuda.stream(self.s_c2) if self.br_c2 else contextlib.nullcontext()):
+        self._fc1_dgrad(B, K1)
+        with self._branch(self.s_c2, main) if self.br_c2 else contextlib.nullcontext():
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
                          workspace=self.ws_c2 if self.br_c2 else None,
                          max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
-        if not crit:
-            self._conv2_dgrad()
+        self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
         if self.br_fc:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
@@ -353,7 +307,9 @@ class MnistCnnTrainer:
                 self.allreduce.wait_bucket(0)   # fc/head Adam overlaps the conv bucket's all-reduce
                 self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
             self.allreduce.wait()
-        if self._apply is not None:
+        if self._apply is not None and self._apply[0] == "fused":
+            self.opt_rest.step(gs_inc=1)   # every variable but fc1's; advances the beta powers + global step
+        elif self._apply is not None:
             self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
 
     def _head_wgrad(self):
@@ -369,8 +325,7 @@ class MnistCnnTrainer:
     def _fc1_dgrad(self, B, K1):
         """fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)."""
         ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
-                 aux_act=ops.ACT_RELU, tile=self.t_dgrad,
-                 head=(self.dl, self.h, self.gw["out"], self.gw["bout"]) if self.head_fused else None)
+                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
 
     def _conv2_dgrad(self):
         """conv2 dgrad: whole-image LDS conv over un-pool(dP2) with flipped taps -> dP1 (ReLU'(P1)-masked)."""
@@ -387,29 +342,6 @@ class MnistCnnTrainer:
                                       global_step=self.global_step)
             self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
 
-    def _backward_one_branch(self, main):
-        """Backward with a single fork/join pair (every cross-stream edge of a hipGraph costs a few
-        microseconds of dependency latency): the dgrad chain stays on the main stream, all weight
-        gradients that feed nothing but the optimizer run on one side stream."""
-        B, K1 = self.B, 7 * 7 * C2
-        ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
-                 aux_act=ops.ACT_RELU, tile=self.t_dgrad)
-        with self._branch(self.s_fc, main):
-            self._head_wgrad()
-            ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
-                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
-            if self.allreduce is not None:
-                self.allreduce.launch(0)
-            ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                         workspace=self.ws_c2, max_blocks=self.c2_blocks, **self.ic2)
-        ops.imgconv(self.wt["wc2"], self.dp1, src_pooled=self.dp2, src_argmax=self.a2, relu_mask=self.p1,
-                    flip_taps=True, **self.ic2_dgrad)
-        ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
-        main.wait_stream(self.s_fc)
-        if self.allreduce is not None:
-            self.allreduce.launch(1)
-            self.allreduce.wait()
-
     @staticmethod
     def _branch(stream, main):
         """Run the enclosed launches on ``stream`` forked from ``main`` (no-op without one)."""
@@ -425,12 +357,16 @@ class MnistCnnTrainer:
         """One training step: forward, backward (+ all-reduce), Adam.  ``grad16``: the all-reduced
         bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
         gscale = 1.0 / self.world if gscale is None else gscale
+        if self._fused_adam_ok(grad16, gscale):
+            self._apply = ("fused", None, 1.0)
+            try:
+                self.forward_backward()
+            finally:
+                self._apply = None
+            return
         mode = None
-        if self.par and not self.br_one and self.br_fc:
-            if self.early_apply:
-                mode = "early"
-            elif self.late_split and self.allreduce is not None:
-                mode = "late"
+        if self.par and self.br_fc and self.late_split and self.allreduce is not None:
+            mode = "late"
         if mode is None or (self.opt_fc is None and self.global_step_started()):
             self.forward_backward()
             self.opt.step(grad16=grad16, gscale=gscale)

@@ -34,7 +34,8 @@ import torch
 from .. import ops
 from ..optim import FlatParams
 
-SLOT_BYTES = 128
+SLOT_BYTES = 256  # ps_link.h PS_SLOT_WORDS * 8
+MAX_BUCKETS = 4   # ps_link.h PS_MAX_BUCKETS
 ALIGN = 256  # bytes: every segment of a mailbox / reply buffer starts 256-B aligned
 COPY_CHUNK = 16384
 MODE = {("f32", "f32"): 0, ("f32", "bf16"): 1, ("bf16", "bf16"): 2, ("bf16", "f32"): 3}
@@ -131,6 +132,9 @@ class NativeShardService:
                                      shard.gs_increments if gs is not None else 0, o._blob, o.nseg, o.nwork, g16)
         if shard.gs is not None:
             lib.ps_service_set_gs(self.svc, shard.gs)
+        # async: pushes arrive bucket by bucket (ranges of this shard's flat layout) and are applied
+        # as they land, while the worker is still in backward; the request applies what is left
+        lib.ps_service_set_total(self.svc, self.lay.total)
         self.acc = None
         if sync:
             self.acc = torch.zeros(self.lay.total, dtype=torch.float32, device=dev)
@@ -167,8 +171,8 @@ class NativeShardService:
             self.lib.ps_service_resume(self.svc)
 
     def stats(self):
-        r, a, s, v = [int(x) for x in self.lib.ps_service_stats(self.svc)]
-        return {"requests": r, "applies": a, "stale": s, "version": v}
+        r, a, s, v, b = [int(x) for x in self.lib.ps_service_stats(self.svc)]
+        return {"requests": r, "applies": a, "stale": s, "version": v, "bucket_applies": b}
 
     def stop(self):
         if getattr(self, "started", False):
@@ -226,6 +230,12 @@ class NativePSLink:
         self._pull = self._plan(segs)
         self.buckets = list(buckets) if buckets is not None else [(0, full.total)]
         self._push = [self._push_plan(lo, hi) for lo, hi in self.buckets]
+        # per bucket and shard: the shard-flat range the bucket's variables occupy (the shard keeps
+        # the full layout's variable order, so it is contiguous); announced after the bucket's push
+        # so the ps applies it while backward continues.  More buckets than the slot has room for:
+        # no announcements, the ps applies the whole push at the request.
+        self._bkt_ranges = [self._shard_ranges(lo, hi) for lo, hi in self.buckets] \
+            if len(self.buckets) <= MAX_BUCKETS else None
         self.side = torch.cuda.Stream(device=self.device)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
         # one version per shard: shard k's last reply version is the staleness tag of the next
@@ -258,6 +268,13 @@ class NativePSLink:
                                  s.numel, mode])
         return self._plan(segs)
 
+    def _shard_ranges(self, lo, hi):
+        out = []
+        for sh in self.shards:
+            offs = [(sh["lay"].offsets[s.name], s.numel) for s in sh["specs"] if lo <= self.full.offsets[s.name] < hi]
+            out.append((min(o for o, _ in offs), max(o + n for o, n in offs)) if offs else None)
+        return out
+
     def _run(self, plan):
         if plan is not None:
             self.lib.ps_copy(plan[0], plan[1], plan[2])
@@ -274,6 +291,10 @@ class NativePSLink:
             self.side.wait_event(ev)
         with torch.cuda.stream(self.side):
             self._run(self._push[i])
+            if self._bkt_ranges is not None:
+                for sh, r in zip(self.shards, self._bkt_ranges[i]):
+                    if r is not None:
+                        self.lib.ps_bucket(sh["shm"], self.w, self.ctr, i, r[0], r[1])
         self._forked = True
 
     def ready(self, lo: int, after=None):

@@ -212,8 +212,8 @@ def run_ps(flags, model, server, device, log):
     ps.serve_forever()
     if ps.native is not None:
         st = ps.native.stats()
-        log("ps %d: native data plane: %d requests, %d applies, %d stale" % (k, st["requests"], st["applies"],
-                                                                             st["stale"]))
+        log("ps %d: native data plane: %d requests, %d applies (%d bucket applies during backward), %d stale"
+            % (k, st["requests"], st["applies"], st["bucket_applies"], st["stale"]))
         ps.native.stop()
     hb.stop()
     if ps.lost:

@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 import dtfe  # noqa: E402,F401
 from dtfe.models.resnet import ResNetModel  # noqa: E402
-from test_resnet import _cos, _ref_forward, _rel  # noqa: E402
+from test_resnet import _cos, _ref_forward, _rel, grad_parity_table  # noqa: E402
 
 
 def main():
@@ -26,7 +26,10 @@ def main():
     ap.add_argument("--arch", default="resnet50")
     ap.add_argument("--show", type=int, default=400)
     ap.add_argument("--round", action="store_true", help="oracle rounds forward activations at the bf16 storage points")
+    ap.add_argument("--amp", action="store_true", help="per-variable cos of dtfe AND of stock autocast-bf16 vs fp32")
     a = ap.parse_args()
+    if a.amp:
+        return amp_table(a)
     model = ResNetModel(arch=a.arch)
     torch.manual_seed(0)
     B, dev = a.batch, torch.device("cuda", 0)
@@ -48,6 +51,25 @@ def main():
         print("cos %.4f rel %.4f |g| %.4e |ref| %.4e  %s" % (c, e, gn, rn, n))
     rows.sort()
     print("min cos %.4f, median cos %.4f over %d variables" % (rows[0][0], rows[len(rows) // 2][0], len(rows)))
+
+
+def amp_table(a):
+    model = ResNetModel(arch=a.arch)
+    torch.manual_seed(0)
+    B, dev = a.batch, torch.device("cuda", 0)
+    prog = model.program(dev, B, seed=1)
+    x = torch.rand(B, model.image, model.image, model.channels, device=dev)
+    y = torch.nn.functional.one_hot(torch.randint(0, model.num_classes, (B,), device=dev), model.num_classes).float()
+    rows = grad_parity_table(model, prog, x, y, dev)
+    print("# B=%d %s: gradient cosine vs the fp32 autograd model (same weights, same batch); backward order" %
+          (B, a.arch))
+    print("%-44s %9s %9s %8s" % ("variable", "cos dtfe", "cos amp", "delta"))
+    for n, cd, ca in rows:
+        print("%-44s %9.4f %9.4f %+8.4f" % (n, cd, ca, cd - ca))
+    convs = [r for r in rows if r[0].endswith("/kernel") and "conv2d" in r[0]]
+    print("conv kernels: mean cos dtfe %.4f amp %.4f; min dtfe %.4f amp %.4f; dtfe worse than amp-0.05 on %d of %d" % (
+        sum(r[1] for r in convs) / len(convs), sum(r[2] for r in convs) / len(convs), min(r[1] for r in convs),
+        min(r[2] for r in convs), sum(r[1] < r[2] - 0.05 for r in convs), len(convs)))
 
 
 if __name__ == "__main__":

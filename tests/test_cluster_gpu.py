@@ -78,5 +78,8 @@ def test_bench_ps_native_plane(hogwild):
     assert rec["n_gpus"] == 2 and rec["value"] > 0
     c = rec["config"]
     assert c["ps_applies"] == c["pushes_issued"] == 2 * 34
+    # the CNN pushes two buckets per step; the ps applies each exactly once, as it lands (during
+    # backward) or, if it noticed the announcement only with the request, right there
+    assert c["ps_bucket_applies"] == 2 * 2 * 34
     assert c["ps_global_step"] == 2 * 34 and 0 < c["global_step"] <= 2 * 34
     assert 0.0 < c["last_loss"] < 10.0

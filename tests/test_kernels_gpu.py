@@ -561,35 +561,3 @@ def test_wgrad_tallk_matches_fp64(M, N, K, splits):
     assert (bias.cpu().double() - rb).abs().max().item() <= 1e-4 * (rb.abs().max().item() + 1)
 
 
-@pytest.mark.parametrize("B", [1024, 256])
-def test_gemm_fused_head_wgrad_matches_separate(B):
-    """A glds GEMM carrying the head weight gradient (extra workgroups of the same launch) gives the
-    GEMM output and the head dW/db of the standalone kernels (bitwise: same per-column order)."""
-    g = torch.Generator().manual_seed(B)
-    K1, FC = 3136, 1024
-    dzf = (torch.randn(B, FC, generator=g) * 0.1).to(DEV, torch.bfloat16)
-    w = (torch.randn(FC, K1, generator=g) * 0.05).to(DEV, torch.bfloat16)
-    aux = torch.randn(B, K1, generator=g).to(DEV, torch.bfloat16)
-    dl = torch.zeros(B, 16, device=DEV, dtype=torch.bfloat16)
-    dl[:, :10] = (torch.randn(B, 10, generator=g) * 0.1).to(DEV, torch.bfloat16)
-    h = torch.relu(torch.randn(B, FC, generator=g)).to(DEV, torch.bfloat16)
-    tile = 12
-    assert ops.glds_ok(dzf, w, B, K1, FC, tile, FC, K1)
-    outs = []
-    for fused in (False, True):
-        out = torch.empty(B, K1, device=DEV, dtype=torch.bfloat16)
-        dw = torch.full((10, FC), 7.0, device=DEV)
-        db = torch.full((10,), 7.0, device=DEV)
-        if fused:
-            ops.gemm(dzf, w, out, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=aux, aux_act=ops.ACT_RELU, tile=tile,
-                     head=(dl, h, dw, db))
-        else:
-            ops.gemm(dzf, w, out, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=aux, aux_act=ops.ACT_RELU, tile=tile)
-            ops.head_wgrad(dl, h, dw, db, 10)
-        torch.cuda.synchronize()
-        outs.append((out.cpu(), dw.cpu(), db.cpu()))
-    assert torch.equal(outs[0][0], outs[1][0])
-    ref = (dl[:, :10].float().t() @ h.float()).cpu()
-    assert _rel(outs[1][1], ref) < 1e-5 and _rel(outs[1][2], dl[:, :10].float().sum(0).cpu()) < 1e-5
-    # same per-column accumulation order as the standalone kernel up to the row-group split
-    assert _rel(outs[1][1], outs[0][1]) < 1e-6

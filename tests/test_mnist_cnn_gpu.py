@@ -88,18 +88,15 @@ def test_cnn_trains_and_graph_replays():
     assert int(tr.global_step.item()) == 60
 
 
-@pytest.mark.parametrize("branches", ["fc,c2", "fc", "side1", "none", "fc,c2:headfuse", "none:headfuse"])
+@pytest.mark.parametrize("branches", ["fc,c2", "fc", "c2", "none"])
 def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
     """Only the atomically-accumulated grads are cleared per step (fused into the batch gather);
     every other gradient must be fully overwritten: the same batch twice -> the same grads,
     and the result matches autograd after a previous step left garbage behind."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
-    branches, _, fuse = branches.partition(":")
     monkeypatch.setenv("DTFE_CNN_BRANCHES", branches)
-    monkeypatch.setenv("DTFE_CNN_HEAD_FUSE", "1" if fuse else "0")  # head wgrad inside the fc1 dgrad launch
     tr = MnistCnnTrainer(64, "cuda", keep_prob=1.0, seed=5)
-    assert tr.head_fused == bool(fuse)
     tr.P.grad.fill_(7.0)            # stale values everywhere
     tr.loss_sum.fill_(3.0)
     ctr0 = int(tr.data_ctr.item())
@@ -140,22 +137,33 @@ def test_cnn_fused_sampling_conv1_matches_separate_gather(monkeypatch):
     assert abs(a["loss"].item() - b["loss"].item()) <= 1e-5 * abs(b["loss"].item())
 
 
-def test_cnn_early_fc_apply_matches_sequential(monkeypatch):
-    """step() with the fc/head Adam issued on the fc branch (split optimizers, shared slots) must
-    train exactly like forward_backward() + one whole-model Adam."""
+@pytest.mark.parametrize("B", [256, 1024])
+def test_cnn_fused_fc1_adam_is_bitwise_the_separate_apply(B, monkeypatch):
+    """step() on one replica applies fc1's Adam in the fc1 weight-gradient GEMM epilogue and the
+    other variables' in a closing launch (DTFE_CNN_FUSED_ADAM=1, the default): masters, both Adam
+    slots, the bf16 working copies, the beta powers and the global step must equal bit for bit the
+    schedule that stores every gradient and runs one whole-model Adam."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
     out = {}
-    for early in ("1", "0"):
-        monkeypatch.setenv("DTFE_CNN_EARLY_APPLY", early)
-        tr = MnistCnnTrainer(256, "cuda", seed=9)
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DTFE_CNN_FUSED_ADAM", fused)
+        tr = MnistCnnTrainer(B, "cuda", seed=21)
         for _ in range(4):
             tr.step()
-        assert (tr.opt_fc is not None) == (early == "1")
         torch.cuda.synchronize()
-        out[early] = (tr.P.master.clone(), int(tr.global_step.item()))
-    assert out["1"][1] == out["0"][1] == 4
-    assert torch.allclose(out["1"][0], out["0"][0], rtol=1e-4, atol=1e-6)
+        assert (tr.opt_rest is not None) == (fused == "1")
+        n = tr.names
+        out[fused] = dict(master=tr.P.master.clone(), m=tr.opt.s1.clone(), v=tr.opt.s2.clone(),
+                          bp=tr.opt.beta_pow.clone(), gs=int(tr.global_step.item()),
+                          w16={k: tr.P.w16[n[k]].clone() for k in ("wc1", "wc2", "wd1", "out")},
+                          wt16=tr.P.wt16[n["wc2"]].clone())
+    a, b = out["1"], out["0"]
+    assert a["gs"] == b["gs"] == 4
+    for k in ("master", "m", "v", "bp", "wt16"):
+        assert torch.equal(a[k], b[k]), (k, float((a[k].float() - b[k].float()).abs().max()))
+    for k in a["w16"]:
+        assert torch.equal(a["w16"][k], b["w16"][k]), k
 
 
 def _reference_grads_on(trainer, device):

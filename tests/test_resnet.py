@@ -72,6 +72,69 @@ def _ref_forward(model, P, x_nhwc, y_onehot, device="cpu", round_act=False, para
     return loss, params
 
 
+def _amp_forward(model, P, x_nhwc, y_onehot, device):
+    """Stock PyTorch mixed precision on the same network and weights: torch.autocast(bfloat16) with
+    channels_last MIOpen convolutions and F.batch_norm (fp32 statistics), fp32 parameters - the
+    independent bar for the bf16 program's gradients."""
+    L = model.layers
+    params = {s.name: P.view(s.name).detach().float().to(device).clone().reshape(s.shape).requires_grad_(True)
+              for s in model.specs}
+
+    def conv(c, h):
+        w = params[c.name].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+        return F.conv2d(h, w, stride=c.stride, padding=c.pad)
+
+    def bn(b, h, relu=True, res=None):
+        o = F.batch_norm(h, None, None, params[b.gamma], params[b.beta], training=True, momentum=0.0, eps=BN_EPS)
+        if res is not None:
+            o = o + res
+        return torch.relu(o) if relu else o
+
+    def shortcut(x, stride, cout):
+        r = x[:, :, ::stride, ::stride]
+        return F.pad(r, (0, 0, 0, 0, 0, cout - r.shape[1])) if r.shape[1] < cout else r
+
+    h = x_nhwc.float().permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        h = bn(L["stem_bn"], conv(L["stem"], h))
+        if "pool_hw" in L:
+            h = F.max_pool2d(h, 3, 2, 1)
+        for b in L["blocks"]:
+            x = h
+            if isinstance(b, BasicBlock):
+                h1 = bn(b.bn1, conv(b.conv1, x))
+                h = bn(b.bn2, conv(b.conv2, h1), res=shortcut(x, b.stride, b.cout))
+            else:
+                res = bn(b.bns, conv(b.convs, x), relu=False) if b.proj else x
+                h1 = bn(b.bn1, conv(b.conv1, x))
+                h2 = bn(b.bn2, conv(b.conv2, h1))
+                h = bn(b.bn3, conv(b.conv3, h2), res=res)
+        f = h.float().mean(dim=(2, 3))
+        d = L["dense"]
+        logits = F.linear(f, params[d.kernel], params[d.bias])
+    loss = -(y_onehot * torch.log_softmax(logits.float(), 1)).sum(1).mean()
+    loss.backward()
+    return loss, params
+
+
+def grad_parity_table(model, prog, x, y, dev):
+    """Per-variable gradient cosine against the fp32 autograd model for dtfe's bf16 program and for
+    stock autocast-bf16, same weights and batch.  Rows (name, cos_dtfe, cos_amp) in backward order."""
+    prog.load_batch((x, y))
+    prog.compute_grads()
+    torch.cuda.synchronize()
+    _, ref = _ref_forward(model, prog.P, prog.x, y, device=dev)
+    _, amp = _amp_forward(model, prog.P, prog.x, y, dev)
+    rows = []
+    for s in model.specs:
+        n = s.name
+        if n.endswith(("moving_mean", "moving_variance")):
+            continue
+        r = ref[n].grad
+        rows.append((n, _cos(prog.P.gview(n).detach().float(), r), _cos(amp[n].grad.float(), r)))
+    return rows
+
+
 def _cos(a, b):
     a, b = a.float().reshape(-1), b.float().reshape(-1)
     return (a @ b / (a.norm() * b.norm() + 1e-12)).item()
@@ -305,3 +368,24 @@ def test_resnet20_evaluate_inference_bn_cpu():
 def test_resnet_evaluate_inference_bn_gpu():
     _eval_matches_batch_stats("cuda", "resnet20", 32)
     _eval_matches_batch_stats("cuda", "resnet50", 8)
+
+
+@pytest.mark.gpu
+def test_resnet50_bf16_grads_vs_stock_amp_gpu():
+    """dtfe's bf16 ResNet-50 gradients are at least as close to the fp32 model's as stock PyTorch
+    autocast-bf16 (MIOpen) gradients are, per conv kernel: cos_dtfe >= cos_amp - 0.05 for the ten
+    conv kernels deepest in the backward (nearest the input) and for every conv kernel on average."""
+    model = ResNetModel(arch="resnet50")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    B = 32
+    prog = model.program(dev, B, seed=1)
+    x = torch.rand(B, 224, 224, 3, device=dev)
+    y = F.one_hot(torch.randint(0, 1000, (B,), device=dev), 1000).float()
+    rows = [r for r in grad_parity_table(model, prog, x, y, dev) if r[0].endswith("/kernel") and "conv2d" in r[0]]
+    deepest = rows[-10:]
+    bad = [(n, round(cd, 4), round(ca, 4)) for n, cd, ca in deepest if cd < ca - 0.05]
+    assert not bad, bad
+    md = sum(cd for _, cd, _ in rows) / len(rows)
+    ma = sum(ca for _, _, ca in rows) / len(rows)
+    assert md >= ma - 0.02, (md, ma)
