@@ -422,8 +422,7 @@ def bench_ps(args):
         server.store.set("dtfe/bench/ps_stats", json.dumps(dict(st, global_step=shard.global_step())))
         print("ps: %s" % json.dumps(st), file=sys.stderr, flush=True)
         server.shutdown()
-        sys.stdout.flush()
-        os._exit(0)
+        _rank_exit()
 
     def wsum(x: float, op=dist.ReduceOp.SUM) -> float:
         t = torch.tensor([x], dtype=torch.float64)  # CPU tensor: the gloo half of the worker group
@@ -490,7 +489,18 @@ def bench_ps(args):
               "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(), B,
               dict(rec_extra, parallelism="ps1+w%d" % N),
               "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)")
+    _rank_exit()
+
+
+def _rank_exit() -> None:
+    """End a ps-mode rank.  os._exit skips interpreter teardown (the peer-mapped mailboxes and the
+    ps service thread need no orderly unwinding); DTFE_PROFILE_EXIT=1 exits normally instead so a
+    profiler's exit handlers (rocprofv3 writes its trace at exit) run in every rank."""
     sys.stdout.flush()
+    sys.stderr.flush()
+    if os.environ.get("DTFE_PROFILE_EXIT") == "1":
+        torch.cuda.synchronize()
+        sys.exit(0)
     os._exit(0)
 
 

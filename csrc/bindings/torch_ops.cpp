@@ -41,29 +41,6 @@ int dtype_code(const Tensor& t) {
 }
 
 // ------------------------------------------------------------------- gemm
-// Adam queued by gemm_adam_epilogue() replaces the gradient store of the NEXT gemm() launch of this
-// thread (world size 1 weight gradients: ops.gemm(..., adam=...) issues the two back to back).
-thread_local dtfe::AdamEpi g_pending_adam{};
-
-void gemm_adam_epilogue(const Tensor& p, const Tensor& m, const Tensor& v, const optional<Tensor>& w16,
-                        const optional<Tensor>& bp, const optional<Tensor>& bm, const optional<Tensor>& bv,
-                        const Tensor& beta_pow, double lr, double beta1, double beta2, double eps, double gscale) {
-  TORCH_CHECK(g_pending_adam.p == nullptr, "gemm_adam_epilogue: a queued Adam epilogue was never launched");
-  for (const Tensor* t : {&p, &m, &v})
-    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == p.numel(),
-                "gemm_adam_epilogue: fp32 p / m / v of one shape");
-  TORCH_CHECK(beta_pow.scalar_type() == at::kFloat && beta_pow.numel() == 2, "gemm_adam_epilogue: beta powers [2]");
-  dtfe::AdamEpi e{};
-  e.p = p.data_ptr<float>(); e.m = m.data_ptr<float>(); e.v = v.data_ptr<float>();
-  e.w16 = ptr_or_null<dtfe::bf16>(w16);
-  e.bp = ptr_or_null<float>(bp); e.bm = ptr_or_null<float>(bm); e.bv = ptr_or_null<float>(bv);
-  TORCH_CHECK((e.bp != nullptr) == (e.bm != nullptr) && (e.bm != nullptr) == (e.bv != nullptr),
-              "gemm_adam_epilogue: bias master and both slots together");
-  e.beta_pow = beta_pow.data_ptr<float>();
-  e.lr = (float)lr; e.beta1 = (float)beta1; e.beta2 = (float)beta2; e.eps = (float)eps; e.gscale = (float)gscale;
-  g_pending_adam = e;
-}
-
 void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t bmode, int64_t ldb, int64_t M,
           int64_t N, int64_t K, const Tensor& out, int64_t ldc, const optional<Tensor>& bias, int64_t bias_axis,
           int64_t act, double alpha, double beta, bool atomic, int64_t splits, int64_t tile,
@@ -124,15 +101,6 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   a.bias_out = ptr_or_null<float>(bias_out);
   TORCH_CHECK(!a.bias_out || b_ones_row >= 0 || a_ones_row >= 0, "gemm: bias_out needs a ones row");
   a.ones = ptr_or_null<dtfe::bf16>(ones);
-  if (g_pending_adam.p) {
-    a.adam = g_pending_adam;
-    g_pending_adam = dtfe::AdamEpi{};
-    TORCH_CHECK(tile != dtfe::GEMM_TILE_SMALL && !atomic && a.out_f32 && !a.unpool && !a.out2 && beta == 0.0,
-                "gemm: the Adam epilogue takes a plain fp32 (weight-gradient) output");
-    TORCH_CHECK(out.numel() >= M * ldc && (uintptr_t)a.adam.p % 16 == 0 && ldc % 8 == 0,
-                "gemm: the Adam epilogue needs 16-B aligned rows matching out");
-    TORCH_CHECK(!a.bias_out || a.adam.bp, "gemm: bias gradient column without the bias Adam state");
-  }
   if (tile == dtfe::GEMM_TILE_SMALL) {
     TORCH_CHECK(real_splits == 1 && dtfe::gemm_small_eligible(dt == 0 ? 0 : 1, a),
                 "gemm: the small-tile kernel takes fp32 operands, one split, no un-pool epilogue");
@@ -874,8 +842,6 @@ TORCH_LIBRARY(dtfe, m) {
         " float forget_bias) -> ()");
   m.def("lstm_cell_bwd(Tensor act, Tensor? c_prev, Tensor c, Tensor? dh, Tensor? dh2, Tensor? dc_next,"
         " Tensor(a!) dgates, Tensor(b!) dc_prev) -> ()");
-  m.def("gemm_adam_epilogue(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? w16, Tensor(e!)? bp, Tensor(f!)? bm,"
-        " Tensor(g!)? bv, Tensor beta_pow, float lr, float beta1, float beta2, float eps, float gscale) -> ()");
   m.def(
       "gemm(Tensor A, int amode, int lda, Tensor B, int bmode, int ldb, int M, int N, int K, Tensor(a!) out, int ldc,"
       " Tensor? bias, int bias_axis, int act, float alpha, float beta, bool atomic, int splits, int tile,"
@@ -955,7 +921,6 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("head_xent", &head_xent);
   m.impl("head_wgrad", &head_wgrad);
   m.impl("apply_gradients", &apply_gradients);
-  m.impl("gemm_adam_epilogue", &gemm_adam_epilogue);
   m.impl("gather_rows", &gather_rows);
   m.impl("seq_stage", &seq_stage);
   m.impl("wgrad_tallk", &wgrad_tallk);

@@ -22,16 +22,16 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf2f(bf16 v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// round-to-nearest-even fp32 -> bf16 (NaN preserved as quiet NaN)
-__device__ __forceinline__ bf16 f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16)0x7fc0;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16)(u >> 16);
-}
+// round-to-nearest-even fp32 -> bf16 on the gfx950 converter (v_cvt_pk_bf16_f32; NaN stays a quiet
+// NaN).  The software rounding it replaces (bit test, add, select: ~5 VALU per value) was a third of
+// the implicit-GEMM epilogue's vector instructions.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16 f2bf(float f) { return __builtin_bit_cast(bf16, (__bf16)f); }
 
+// two values, one instruction
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 // Activation codes shared with the host side (ops/_lib.py mirrors these).

@@ -66,7 +66,7 @@ void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
 // the separate BN-backward statistics pass over a finished dx (ConvDgradArgs::bnb_*)
 void launch_dgrad_bn_bwd_stats(const ConvDgradArgs& a, hipStream_t s);
 // dedicated ImageNet stem (7x7/2, 3 -> 64, 224 -> 112; stem.hip): true when it handled the call
-bool launch_stem_fwd(const ConvFwdArgs& a, hipStream_t s);
+bool launch_stem_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nullptr);
 bool launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t s, bool accumulate);
 void launch_conv_dgrad(const ConvDgradArgs& a, hipStream_t s);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);

@@ -392,8 +392,9 @@ static void bn_stats_of(const ConvFwdArgs& a, hipStream_t s) {
 }
 
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
-  if (launch_stem_fwd(a, s)) {  // ImageNet 7x7/2 stem
-    bn_stats_of(a, s);
+  bool stem_stats = false;
+  if (launch_stem_fwd(a, s, &stem_stats)) {  // ImageNet 7x7/2 stem (+ BN partials in its epilogue)
+    if (!stem_stats) bn_stats_of(a, s);
     return;
   }
   bool fused = false;

@@ -3,7 +3,6 @@
 #pragma once
 #include "gemm_core.h"
 #include "conv.h"
-#include "optim.h"
 
 namespace dtfe {
 
@@ -40,41 +39,7 @@ struct DenseGemmArgs {
   // global_load_lds kernel (tiles 5..8): a 1 KB page of bf16 ones, read by the whole n-tile that
   // starts at b_ones_row (the bias column of a weight-gradient GEMM sits past the operand's rows)
   const bf16* ones;
-  AdamEpi adam;                // optional: Adam instead of storing the (weight / bias) gradient
 };
-
-// Adam epilogue (AdamEpi, optim.h): one element, and 8 consecutive ones with 16-B accesses
-__device__ __forceinline__ void adam_one(const AdamEpi& e, float* p, float* m, float* v, bf16* w16, float g) {
-  float mm = *m, vv = *v;
-  const float np = tf1_adam(*p, g * e.gscale, mm, vv, tf1_adam_lr(e.lr, e.beta_pow), e.beta1, e.beta2, e.eps);
-  *p = np; *m = mm; *v = vv;
-  if (w16) *w16 = f2bf(np);
-}
-__device__ __forceinline__ void adam_chunk8(const AdamEpi& e, long o, const float (&g)[8], float lr_t) {
-  f32x4_t p[2], m[2], v[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    p[h] = *reinterpret_cast<const f32x4_t*>(e.p + o + 4 * h);
-    m[h] = *reinterpret_cast<const f32x4_t*>(e.m + o + 4 * h);
-    v[h] = *reinterpret_cast<const f32x4_t*>(e.v + o + 4 * h);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float mm = m[j >> 2][j & 3], vv = v[j >> 2][j & 3];
-    p[j >> 2][j & 3] = tf1_adam(p[j >> 2][j & 3], g[j] * e.gscale, mm, vv, lr_t, e.beta1, e.beta2, e.eps);
-    m[j >> 2][j & 3] = mm;
-    v[j >> 2][j & 3] = vv;
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    *reinterpret_cast<f32x4_t*>(e.p + o + 4 * h) = p[h];
-    *reinterpret_cast<f32x4_t*>(e.m + o + 4 * h) = m[h];
-    *reinterpret_cast<f32x4_t*>(e.v + o + 4 * h) = v[h];
-  }
-  if (e.w16)
-    *reinterpret_cast<u32x4_t*>(e.w16 + o) = u32x4_t{pack_bf16x2(p[0][0], p[0][1]), pack_bf16x2(p[0][2], p[0][3]),
-                                                     pack_bf16x2(p[1][0], p[1][1]), pack_bf16x2(p[1][2], p[1][3])};
-}
 
 // Epilogue of one output element (row < M, col < N); returns false when the
 // element was fully handled (atomic / bias column / unpool) and x must not be stored.
@@ -87,13 +52,8 @@ __device__ __forceinline__ bool dense_epi(const DenseGemmArgs& a, int row, int c
     return false;
   }
   if (a.bias_out && col == a.b_ones_row) {  // the ones column = this layer's bias gradient
-    if (a.adam.bp) {
-      adam_one(a.adam, a.adam.bp + row, a.adam.bm + row, a.adam.bv + row, nullptr, a.alpha * x);
-    } else if (a.atomic) {
-      atomicAdd(a.bias_out + row, a.alpha * x);
-    } else {
-      a.bias_out[row] = a.alpha * x;
-    }
+    if (a.atomic) atomicAdd(a.bias_out + row, a.alpha * x);
+    else a.bias_out[row] = a.alpha * x;
     return false;
   }
   if (a.atomic) {
@@ -199,7 +159,6 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
   }
   const int64_t drop_step = (a.keep < 1.f && a.counter) ? *a.counter : 0;
   const float inv_keep = 1.f / a.keep;
-  const float adam_lr = a.adam.p ? tf1_adam_lr(a.adam.lr, a.adam.beta_pow) : 0.f;
   // plain-store fast path: no per-element side outputs, 16 B aligned rows
   // (a weight-gradient GEMM's bias row / column only takes the per-element path in its own chunks)
   const bool vec_store = !a.atomic && !a.unpool && !a.out2 && a.beta == 0.f &&
@@ -242,9 +201,7 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
                                                                                                          : 0.f;
         x[e] = v * g[e];
       }
-      if (a.adam.p) {
-        adam_chunk8(a.adam, o, x, adam_lr);
-      } else if (a.out_f32) {
+      if (a.out_f32) {
         reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + o)[0] = *reinterpret_cast<f32x4_t*>(x);
         reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(a.out) + o)[1] = *reinterpret_cast<f32x4_t*>(x + 4);
       } else {
@@ -261,8 +218,7 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
         float xe = x[e];
         if (!dense_epi(a, row, col, xe, drop_step, inv_keep)) continue;
         const long o = (long)row * a.ldc + col;
-        if (a.adam.p) adam_one(a.adam, a.adam.p + o, a.adam.m + o, a.adam.v + o, a.adam.w16 ? a.adam.w16 + o : nullptr, xe);
-        else if (a.out_f32) reinterpret_cast<float*>(a.out)[o] = xe;
+        if (a.out_f32) reinterpret_cast<float*>(a.out)[o] = xe;
         else reinterpret_cast<bf16*>(a.out)[o] = f2bf(xe);
       }
     }

@@ -52,6 +52,14 @@ struct IgWgradArgs {
   int splits, mchunk;
 };
 
+// BatchNorm statistics from per-tile shifted partials (any producer's epilogue): part holds
+// [tiles][3][N] = (K_t = the tile's first row, sum (y - K_t), sum (y - K_t)^2) of tiles of BMr rows
+// (the last one Mp - (tiles-1)*BMr); two fixed-order fold launches add (sum, sumsq) around row 0's
+// value into stats[2][N], as bn_stats would.  bn_part_buffer: the device scratch for `tiles`
+// tiles plus the fold's chunk table (valid until the next call on this device).
+float* bn_part_buffer(long tiles, int N, hipStream_t s);
+void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s);
+
 // true when the igemm path handles the conv (and launches it)
 // stats_done (optional): set when f.bn_stats was produced by the fused epilogue partials
 bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nullptr);

@@ -53,7 +53,7 @@ __device__ __forceinline__ int qdiv(int m, int d, float inv_d) {
 // Epilogue shared by the 4- and 8-wave kernels: fp32 split-K partial tile, or the bf16 tile through
 // LDS (+ accumulation source, BatchNorm forward / backward partial statistics).  THREADS threads,
 // a 2-column wave grid (wave w owns rows (w >> 1) * WM.., columns (w & 1) * WN..).
-template <int BM, int BN, int THREADS, int SMEM_EL>
+template <int BM, int BN, int THREADS, int SMEM_EL, bool BB>
 __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&acc)[BM / (THREADS / 128) / 16][BN / 2 / 16],
                                             bf16* smem, int tid, int lane, int w, int m_base, int n_base,
                                             int tm, int Mp, const IgPhase& P) {
@@ -90,7 +90,7 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
     dst[j] = nullptr;
     if (m >= Mp) continue;
     long opix = m;
-    if (a.nphase > 1) {
+    if (a.ostr > 1) {  // data gradient of a strided conv: phase pixel grid -> output pixel
       const int jx = m % P.RW, t = m / P.RW;
       const int i = t % P.RH, b = t / P.RH;
       opix = ((long)b * a.OHf + i * a.ostr + P.oy) * a.OWf + jx * a.ostr + P.ox;
@@ -105,7 +105,7 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
   }
   // BatchNorm-backward statistics of the final values: this thread's 8 channels are the same for
   // every j (IG_THREADS % CPR == 0); x (and y for a non-recomputable mask) at the same offsets
-  const bool bb = a.bb_x != nullptr;
+  const bool bb = BB && a.bb_x != nullptr;  // compiled out of the instances without a BN-backward epilogue
   const bool bb_from_x = bb && a.bb_y == nullptr && a.bb_act == ACT_RELU;
   const bool bb_need_y = bb && a.bb_act != ACT_NONE && !bb_from_x;
   u32x4_t xv[PER], yv[PER];
@@ -239,12 +239,24 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
   }
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a) {
+// NST: LDS stages (1 only for launches whose every workgroup has ONE k-tile: the 64-channel 1x1
+// convs - half the LDS, so three workgroups share a CU instead of two); BB: with the BN-backward
+// statistics epilogue (its registers are compiled out of the other instances); MINB: workgroups
+// per CU the register allocation must allow
+template <int BM, int BN, int NST, bool BB>
+constexpr int ig_smem_el() {
+  constexpr int stage = NST * (BM + BN) * IG_BK, cld = BN + 8, rg = IG_THREADS / (BN / 8);
+  constexpr int epi = (BM * cld * 2 + rg * 2 * BN * 4 + 3) / 4 * 2;  // C tile + statistics scratch, in bf16 units
+  return stage > epi ? stage : epi;
+}
+
+template <int BM, int BN, int NST, bool BB, int MINB>
+__global__ __launch_bounds__(IG_THREADS, MINB) void igemm_kernel(const IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_EL = BM * IG_BK, B_EL = BN * IG_BK;
   constexpr int NA = BM / 32, NB = BN / 32;  // 1-KB glds pieces per thread and k-tile
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
+  constexpr int SMEM_EL = ig_smem_el<BM, BN, NST, BB>();
+  __shared__ __attribute__((aligned(16))) bf16 smem[SMEM_EL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -316,8 +328,8 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
   for (int t = 0; t < nk; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t + 1 < nk) issue(kt0 + t + 1, (t + 1) & 1);
-    const bf16* As = smem + (t & 1) * (A_EL + B_EL);
+    if (NST > 1 && t + 1 < nk) issue(kt0 + t + 1, (t + 1) & 1);
+    const bf16* As = smem + (NST > 1 ? (t & 1) : 0) * (A_EL + B_EL);
     const bf16* Bs = As + A_EL;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -337,7 +349,7 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_kernel(const IgemmArgs a)
     }
   }
 
-  igemm_store<BM, BN, IG_THREADS, 2 * (A_EL + B_EL)>(a, acc, smem, tid, lane, w, m_base, n_base, tm, Mp, P);
+  igemm_store<BM, BN, IG_THREADS, SMEM_EL, BB>(a, acc, smem, tid, lane, w, m_base, n_base, tm, Mp, P);
 }
 
 // out[i] = bf16(sum_s ws[s][i])   (accum: out[i] = bf16(out[i] + sum_s ws[s][i]))
@@ -492,6 +504,147 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgra
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         ws[(long)(row_base + i * 16 + (lane >> 4) * 4 + q) * Kw + col_base + j * 16 + (lane & 15)] = acc[i][j][q];
+}
+
+// ------------------------------------------------------- 3x3 / stride-1 weight gradient, all taps
+// dW[co][tap][c] for a 64-channel (co) x 64-channel (c) tile and ALL 9 taps in one workgroup: a
+// k-tile is R = 64 / W whole output rows (R*W <= 64 pixels, the rest zero), the dY rows are staged
+// once ([64 k][64 co]) and the source rows they need ONCE as a halo'd patch [(R+2) x (W+2) pixels]
+// [64 c]; the 9 taps' B fragments are the same patch read at 9 pixel shifts.  Against the per-tap
+// kernel (9 workgroups each staging their own shifted source tile and re-staging dY, 2 fragment
+// reads per MFMA) this stages 2.6x fewer bytes and reads 0.72 fragments per MFMA.
+// Wave w owns c = 16w..16w+15 of the tile for every co (4 tiles) and tap: 36 accumulators.
+constexpr int W3_PATCH = 192;  // patch pixels staged per k-tile (>= (R+2)(W+2) for every W <= 64)
+
+// chunk XOR of patch pixel `pix` ([pixel][64 c] image, 128-B rows): the 8 pixels one 32-lane half of
+// a transposing read covers (pix..pix+3, pix+8..pix+11 between row wraps) land on distinct
+// (bank-row half, 32-B segment) pairs - the 64-column form of wg_swz
+__device__ __forceinline__ int w3_swz(int pix) { return wg_swz<64>(pix); }
+
+__global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgradArgs a, float* dw, float scale,
+                                                                    int R, int ktiles_per_img) {
+  constexpr int A_EL = 64 * 64, P_EL = W3_PATCH * 64, ST_EL = A_EL + P_EL;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * ST_EL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, W = a.W, PW = W + 2;
+  const int npix = (R + 2) * PW, kvalid = R * W;
+  const int cblocks = a.C / 64;
+  const int id = xcd_remap(blockIdx.x, (a.Cout / 64) * cblocks);
+  const int tco = id / cblocks, tc = id - tco * cblocks;
+  const int T = a.B * ktiles_per_img;
+  const int t0 = (int)((long)T * blockIdx.y / a.splits), nk = (int)((long)T * (blockIdx.y + 1) / a.splits) - t0;
+
+  // A rows (2 pieces per thread): k = row -> (r, x) of the k-tile
+  int a_r[2], a_x[2], a_chk[2];
+  bool a_ok[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (j * 4 + w) * 8 + (lane >> 3);
+    a_ok[j] = row < kvalid;
+    a_r[j] = a_ok[j] ? row / W : 0;
+    a_x[j] = a_ok[j] ? row - a_r[j] * W : 0;
+    a_chk[j] = (lane & 7) ^ wg_swz<64>(row);
+  }
+  // patch pixels (6 pieces per thread): pixel -> (pr, pc) of the halo'd patch
+  int p_r[6], p_c[6], p_chk[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int pix = (j * 4 + w) * 8 + (lane >> 3);
+    p_r[j] = pix < npix ? pix / PW : -(1 << 20);
+    p_c[j] = pix < npix ? pix - (pix / PW) * PW : 0;
+    p_chk[j] = (lane & 7) ^ w3_swz(pix);
+  }
+  const bf16* dy_col = a.dy + tco * 64;
+  const bf16* x_col = a.x + tc * 64;
+  auto issue = [&](int t, int buf) {
+    const int kt = t0 + t, b = kt / ktiles_per_img, oy0 = (kt - b * ktiles_per_img) * R;
+    bf16* As = smem + buf * ST_EL;
+    bf16* Ps = As + A_EL;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int oy = oy0 + a_r[j];
+      const bf16* p = (a_ok[j] && oy < H) ? dy_col + ((long)(b * H + oy) * W + a_x[j]) * a.Cout + a_chk[j] * 8 : a.zeros;
+      glds16(p, As + (j * 4 + w) * 512);
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int sy = oy0 - 1 + p_r[j], sx = p_c[j] - 1;
+      const bf16* p = ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W)
+                          ? x_col + ((long)(b * H + sy) * W + sx) * a.C + p_chk[j] * 8
+                          : a.zeros;
+      glds16(p, Ps + (j * 4 + w) * 512);
+    }
+  };
+
+  // B fragment read offsets: lane (g, q, p4) of read half h covers k = kk + 8g + 4h + q at columns
+  // 16w + 4p4 .. +3; the patch pixel of k for tap (kh, kw) is pix(k) + kh * PW + kw
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int ccol = 16 * w + 4 * p4;
+  int boff[2][2][9];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = kk * 32 + 8 * g + 4 * h + q;
+      const int r = k / W, x = k - r * W;
+      const int base = (k < kvalid) ? r * PW + x : 0;  // dead rows (dY is 0): any staged, finite pixel
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int pix = base + (tap / 3) * PW + (tap % 3);
+        boff[kk][h][tap] = pix * 64 + (ccol ^ (w3_swz(pix) * 8));
+      }
+    }
+
+  f32x4_t acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+    const bf16* As = smem + (t & 1) * ST_EL;
+    const bf16* Ps = As + A_EL;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = wg_frag<64>(As, i * 16, kk * 32, lane);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        bf16x8_t bfr[3];
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, Ps + boff[kk][0][kh * 3 + kw]));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, Ps + boff[kk][1][kh * 3 + kw]));
+          const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[kw] = __builtin_bit_cast(bf16x8_t, v);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw)
+            acc[i][kh * 3 + kw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[kw], acc[i][kh * 3 + kw], 0, 0, 0);
+      }
+    }
+  }
+
+  // dW[co][tap][c]: rows co = 16i + 4(lane>>4) + e, column tap*C + c
+  const int Kw = 9 * a.C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long o = (long)(tco * 64 + i * 16 + (lane >> 4) * 4 + e) * Kw + tap * a.C + tc * 64 + 16 * w + (lane & 15);
+        if (a.splits == 1) dw[o] += scale * acc[i][tap][e];
+        else a.ws[(long)blockIdx.y * a.Cout * Kw + o] = acc[i][tap][e];
+      }
 }
 
 // dw[i] += scale * sum_s ws[s][i]
@@ -704,7 +857,15 @@ template <int BM, int BN>
 void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
   a.tiles_m = (int)((Mmax + BM - 1) / BM);
   dim3 grid(a.tiles_m * (a.N / BN), a.splits, a.nphase);
-  hipLaunchKernelGGL((igemm_kernel<BM, BN>), grid, dim3(IG_THREADS), 0, s, a);
+  int nk_max = 0;
+  for (int p = 0; p < a.nphase; ++p) nk_max = std::max(nk_max, a.ph[p].ntaps * (a.SC / IG_BK));
+  // (a 1-stage, 3-workgroups-per-CU instance for the one-k-tile 1x1 convs measured 15-25 % slower
+  // than this one: profiles/r3_resnet50_b256_kernels.txt)
+  (void)nk_max;
+  if (a.bb_x)
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, 2, true, 2>), grid, dim3(IG_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, 2, false, 2>), grid, dim3(IG_THREADS), 0, s, a);
 }
 
 // returns true when BatchNorm statistics into bn_stats were produced (fused epilogue partials)
@@ -761,6 +922,19 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
 }
 
 }  // namespace
+
+float* bn_part_buffer(long tiles, int N, hipStream_t s) {
+  const long nchunk = (tiles + BN_TCH - 1) / BN_TCH;
+  return bn_workspace(((size_t)tiles + nchunk) * 3 * N * sizeof(float), s);
+}
+
+void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s) {
+  const int nchunk = (tiles + BN_TCH - 1) / BN_TCH;
+  float* chunk = part + (size_t)tiles * 3 * N;
+  const unsigned cg = (unsigned)((N + 63) / 64);
+  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, part, tiles, N, Mp, BMr, chunk);
+  hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, N, Mp, BMr, stats);
+}
 
 bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
   const ConvGeom& g = f.g;
@@ -822,9 +996,28 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
         }
       }
     }
+  // Accumulating into dx (a bottleneck's input gradient on top of its shortcut share), a phase no
+  // tap reaches contributes nothing: drop it instead of re-reading and re-writing its pixels (3 of
+  // the 4 phases of a 1x1 / stride-2 projection - 617 MB of dead traffic per step at the ResNet-50
+  // 56x56 layer).  BN-backward statistics need every phase's pixels, so they keep all phases.
+  if (a.accum && !d.bnb_stats) {
+    int n = 0;
+    for (int p = 0; p < a.nphase; ++p)
+      if (a.ph[p].ntaps > 0) a.ph[n++] = a.ph[p];
+    if (n == 0) return true;
+    a.nphase = n;
+  }
   const bool fused = run_igemm(a, s, d.bnb_stats);
   if (d.bnb_stats && !fused) launch_dgrad_bn_bwd_stats(d, s);
   return true;
+}
+
+// DTFE_IG_W3: 0 off, 1 every eligible shape, 2 (default) only 64->64: measured 218 -> 143 us at
+// 56x56 (B=256), equal at 28x28 128->128, slower at 14x14 / 7x7 where the per-tap kernel's
+// 128x128 tiles fill the chip (profiles/r3_resnet50_wgrad3_ab.txt)
+static bool use_wgrad3(const ConvGeom& g) {
+  const int m = env_int("DTFE_IG_W3", 2);
+  return m == 1 || (m == 2 && g.C <= 64 && g.Cout <= 64);
 }
 
 bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
@@ -837,6 +1030,32 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   a.B = g.B; a.H = g.H; a.W = g.W; a.C = g.C; a.OH = g.OH; a.OW = g.OW; a.Cout = g.Cout;
   a.KH = g.KH; a.KW = g.KW; a.stride = g.stride; a.pad = g.pad;
   a.zeros = zero_page(s);
+  if (g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 && g.OH == g.H && g.OW == g.W && g.W <= 62 &&
+      (64 / g.W + 2) * (g.W + 2) <= W3_PATCH && use_wgrad3(g)) {
+    // all 9 taps per workgroup from one staged patch (igemm_wgrad3_kernel)
+    const int R = 64 / g.W;
+    const int kpi = (g.H + R - 1) / R;
+    const long tiles = (long)(g.Cout / 64) * (g.C / 64);
+    const long T = (long)g.B * kpi;
+    const long len = (long)g.Cout * 9 * g.C;
+    // one workgroup per CU (the 36 accumulator tiles take the whole register file): aim for one
+    // wave of 256 workgroups, at least 4 k-tiles each, fp32 partial slabs up to 40 MB
+    static const long target = env_int("DTFE_IG_W3TARGET", 256);
+    long sp = env_int("DTFE_IG_WSPLIT", 0);
+    if (sp <= 0) {
+      sp = std::max(1L, std::min((target + tiles - 1) / tiles, T / 4));
+      sp = std::max(1L, std::min(sp, (40L << 20) / (len * 4)));
+    }
+    sp = std::min(sp, T);
+    a.splits = (int)sp;
+    if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s, g_wg);
+    hipLaunchKernelGGL(igemm_wgrad3_kernel, dim3((unsigned)tiles, (unsigned)sp), dim3(IG_THREADS), 0, s, a, f.dw,
+                       f.scale, R, kpi);
+    if (sp > 1)
+      hipLaunchKernelGGL(wgrad_splits_reduce_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws,
+                         (int)sp, len, f.dw, f.scale);
+    return true;
+  }
   const int bm = g.Cout % 128 == 0 ? 128 : 64, bn = g.C % 128 == 0 ? 128 : 64;
   const long tiles = (long)(g.Cout / bm) * g.KH * g.KW * (g.C / bn);
   const long M = (long)g.B * g.OH * g.OW;

@@ -42,8 +42,7 @@ void launch_apply_gradients(const OptArgs& a, hipStream_t s);
 // the non-slot scalars of one optimizer step: beta powers (Adam) and global_step += gs_inc
 void launch_opt_advance(const OptArgs& a, hipStream_t s);
 
-// TF1 Adam step of one element (optim.hip and the GEMM Adam epilogue share it, so the two paths
-// agree bitwise): m = b1 m + (1-b1) g; v2 = b2 v2 + (1-b2) g^2; p -= lr_t m / (sqrt(v2) + eps).
+// TF1 Adam step of one element: m = b1 m + (1-b1) g; v2 = b2 v2 + (1-b2) g^2; p -= lr_t m / (sqrt(v2) + eps).
 // No multiply-add contraction: the rounding must not depend on a kernel's instruction selection.
 __device__ __forceinline__ float tf1_adam(float p, float g, float& m, float& v2, float lr_t, float beta1, float beta2,
                                           float eps) {
@@ -56,17 +55,6 @@ __device__ __forceinline__ float tf1_adam_lr(float lr, const float* beta_pow) {
 #pragma clang fp contract(off)
   return lr * sqrtf(1.f - beta_pow[1]) / (1.f - beta_pow[0]);
 }
-
-// Adam applied in a weight-gradient GEMM's epilogue (world size 1: the gradient is final when the
-// GEMM produces it): the f32 result at out offset o is the gradient of p[o] (p / m / v / w16 share
-// out's [row][ldc] layout), the bias column's result the gradient of bp[row].  Nothing advances the
-// beta powers here: the step's last optimizer launch over the remaining variables does.
-struct AdamEpi {
-  float* p; float* m; float* v; bf16* w16;   // weight master / slots / bf16 working copy
-  float* bp; float* bm; float* bv;           // bias master / slots (the ones column)
-  const float* beta_pow;
-  float lr, beta1, beta2, eps, gscale;
-};
 
 // up to OPT_GROUP_MAX optimizers of one kind in a single launch (contiguous workgroup ranges)
 constexpr int OPT_GROUP_MAX = 4;

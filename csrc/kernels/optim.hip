@@ -143,12 +143,31 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
       }
     } else {
       // 64x64 tile of tap t: rows r0.., cols c0.. of the [R][C] slice; transposed copy via LDS
+      // the 16 elements of a thread are loaded together before any update (the update's stores may
+      // alias later loads, so a per-element loop ran 16 dependent HBM round trips per workgroup)
       const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-      for (int rr = ty; rr < 64; rr += 4) {
-        const int r = w.r0 + rr, c = w.c0 + tx;
+      const int c = w.c0 + tx;
+      float gv[16], pv[16], s1v[16], s2v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int r = w.r0 + ty + 4 * u;
+        const bool ok = r < sg.R && c < sg.C;
+        const long i = sg.off + (ok ? ((long)r * sg.T + w.t) * sg.C + c : 0);
+        gv[u] = ok ? load_grad(a, i) : 0.f;
+        pv[u] = ok ? a.p[i] : 0.f;
+        s1v[u] = (ok && KIND != OPT_SGD) ? a.s1[i] : 0.f;
+        s2v[u] = (ok && (KIND == OPT_ADAM || KIND == OPT_RMSPROP)) ? a.s2[i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int rr = ty + 4 * u, r = w.r0 + rr;
         if (r < sg.R && c < sg.C) {
           const long li = ((long)r * sg.T + w.t) * sg.C + c, i = sg.off + li;
-          const float v = update_one<KIND>(a, lr_t, i, load_grad(a, i));
+          float x1 = s1v[u], x2 = s2v[u];
+          const float v = upd<KIND>(a, lr_t, pv[u], gv[u], x1, x2);
+          a.p[i] = v;
+          if (KIND != OPT_SGD) a.s1[i] = x1;
+          if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) a.s2[i] = x2;
           const bf16 b = f2bf(v);
           if (sg.w16) sg.w16[li] = b;
           tile[rr][tx] = b;

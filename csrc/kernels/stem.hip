@@ -24,6 +24,7 @@
 #include <stdexcept>
 
 #include "conv.h"
+#include "igemm.h"
 
 namespace dtfe {
 
@@ -41,10 +42,13 @@ constexpr int F_IR = 2 * F_RPI + 5;   // input rows per item (13)
 constexpr int F_T = 896;              // 14 waves
 constexpr int F_NPF = (F_IR * NCH_ROW + F_T - 1) / F_T;  // 2
 
+// part (optional): BatchNorm partials of each work item's stored (bf16) output block, the igemm
+// epilogue's [items][3][64] layout (K = the block's first pixel, shifted sum, shifted sum of squares)
 __global__ __launch_bounds__(F_T) void stem_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                        bf16* __restrict__ y, int B) {
+                                                        bf16* __restrict__ y, int B, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) bf16 rows[F_IR * RW];
   __shared__ __attribute__((aligned(16))) bf16 ost[F_RPI * SOUT * SN];
+  __shared__ float red[F_T / SN][2][SN];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ct = wid % 7, hf = wid / 7;  // 16-pixel column tile, 32-channel half
   const int g = lane >> 4, i16 = lane & 15;
@@ -138,6 +142,33 @@ __global__ __launch_bounds__(F_T) void stem_fwd_kernel(const bf16* __restrict__ 
     const long base = ((long)(it / (SOUT / F_RPI)) * SOUT + (it % (SOUT / F_RPI)) * F_RPI) * SOUT * SN;
     for (int c = tid; c < F_RPI * SOUT * SN / 8; c += F_T)
       *reinterpret_cast<u32x4_t*>(y + base + c * 8) = *reinterpret_cast<const u32x4_t*>(ost + c * 8);
+    if (part) {
+      // thread (channel c, row group rg) sums pixels rg, rg + 14, ... around the block's first
+      // pixel; the 14 row groups are folded in order (deterministic)
+      constexpr int RG = F_T / SN, NPIX = F_RPI * SOUT;
+      const int c = tid % SN, rg = tid / SN;
+      const float k = bf2f(ost[c]);
+      float sm = 0.f, sq = 0.f;
+      for (int p = rg; p < NPIX; p += RG) {
+        const float d = bf2f(ost[p * SN + c]) - k;
+        sm += d;
+        sq += d * d;
+      }
+      red[rg][0][c] = sm;
+      red[rg][1][c] = sq;
+      __syncthreads();
+      if (tid < SN) {
+        float S = 0.f, Q = 0.f;
+        for (int r = 0; r < RG; ++r) {
+          S += red[r][0][tid];
+          Q += red[r][1][tid];
+        }
+        float* pp = part + (long)it * 3 * SN + tid;
+        pp[0] = k;
+        pp[SN] = S;
+        pp[2 * SN] = Q;
+      }
+    }
   }
 }
 
@@ -337,11 +368,16 @@ float* stem_workspace(size_t bytes, hipStream_t s) {
 
 }  // namespace
 
-bool launch_stem_fwd(const ConvFwdArgs& a, hipStream_t s) {
+bool launch_stem_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done) {
   if (!stem_shape(a.g) || a.bias || a.act != ACT_NONE || a.argmax) return false;
   const int items = a.g.B * (SOUT / F_RPI);
   const int grid = items < 256 ? items : 256;
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(F_T), 0, s, a.x, a.w, a.y, a.g.B);
+  // BatchNorm statistics from the epilogue's per-block partials (2 small fold launches instead of
+  // a 411 MB re-read of y at B = 256)
+  float* part = a.bn_stats ? bn_part_buffer(items, SN, s) : nullptr;
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(F_T), 0, s, a.x, a.w, a.y, a.g.B, part);
+  if (part) launch_bn_part_reduce(part, items, SN, (long)a.g.B * SOUT * SOUT, F_RPI * SOUT, a.bn_stats, s);
+  if (stats_done) *stats_done = part != nullptr;
   return true;
 }
 

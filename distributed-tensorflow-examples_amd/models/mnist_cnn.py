@@ -212,15 +212,11 @@ class MnistCnnTrainer:
         # Data-parallel "late split" (default whenever an all-reduce is attached): the fc/head Adam
         # (bucket 0, already reduced during the conv backward) runs while the small conv bucket's
         # all-reduce is still in flight, so that collective's latency hides behind ~20 us of Adam.
-        self.opt_fc = self.opt_conv = self.opt_rest = None
+        self.opt_fc = self.opt_conv = None
         self._apply = None
-        # One replica (no all-reduce): fc1's weight gradient is final when its GEMM produces it, so
-        # that GEMM applies Adam to fc1's weights and bias in its epilogue (TF1 math shared with the
-        # fused optimizer kernel - bitwise the same update) instead of storing the gradient; the
-        # step's closing Adam covers only the other 62 K parameters.  98% of the Adam traffic moves
-        # off the step's tail onto the fc branch, and the fp32 fc1 gradient never touches HBM.
-        # DTFE_CNN_FUSED_ADAM=0: the separate whole-model Adam launch.
-        self.fused_adam = os.environ.get("DTFE_CNN_FUSED_ADAM", "1") != "0"
+        # (Adam for fc1 applied in the fc1 weight-gradient GEMM epilogue on one replica measured
+        # ~45 us/step slower - its traffic contends with the persistent conv2 backward kernels -
+        # and was removed: profiles/r3_cnn_fused_adam_ab.txt)
         self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
         # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
@@ -283,18 +279,21 @@ class MnistCnnTrainer:
         with self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext():
             self._head_wgrad()
             # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
-            fused_adam = self._apply is not None and self._apply[0] == "fused"
             ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
-                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad,
-                     adam=self._fc1_adam_args() if fused_adam else None)
+                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
             if self.allreduce is not None:
                 self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
         self._fc1_dgrad(B, K1)
-        with self._branch(self.s_c2, main) if self.br_c2 else contextlib.nullcontext():
-            # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
-            ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                         workspace=self.ws_c2 if self.br_c2 else None,
-                         max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
+        def conv2_wgrad():
+            with self._branch(self.s_c2, main) if self.br_c2 else contextlib.nullcontext():
+                # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
+                ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
+                             workspace=self.ws_c2 if self.br_c2 else None,
+                             max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
+
+        # (forking conv2's weight gradient after its data gradient, beside conv1's weight gradient,
+        # measured 0.242 vs 0.233 ms/step: profiles/r3_cnn_c2_after_ab.txt)
+        conv2_wgrad()
         self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
         if self.br_fc:  # join the weight-grad branches
@@ -307,9 +306,7 @@ class MnistCnnTrainer:
                 self.allreduce.wait_bucket(0)   # fc/head Adam overlaps the conv bucket's all-reduce
                 self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
             self.allreduce.wait()
-        if self._apply is not None and self._apply[0] == "fused":
-            self.opt_rest.step(gs_inc=1)   # every variable but fc1's; advances the beta powers + global step
-        elif self._apply is not None:
+        if self._apply is not None:
             self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
 
     def _head_wgrad(self):
@@ -357,13 +354,6 @@ class MnistCnnTrainer:
         """One training step: forward, backward (+ all-reduce), Adam.  ``grad16``: the all-reduced
         bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
         gscale = 1.0 / self.world if gscale is None else gscale
-        if self._fused_adam_ok(grad16, gscale):
-            self._apply = ("fused", None, 1.0)
-            try:
-                self.forward_backward()
-            finally:
-                self._apply = None
-            return
         mode = None
         if self.par and self.br_fc and self.late_split and self.allreduce is not None:
             mode = "late"

@@ -167,7 +167,7 @@ def _mat(t, mode, rows, K, ld):
 def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=None, bias=None, bias_axis=0,
          act=ACT_NONE, alpha=1.0, beta=0.0, atomic=False, splits=1, tile=None, aux=None, ld_aux=None, aux_act=0,
          b_ones_row=-1, keep=1.0, seed=0, counter=None, pooled=None, argmax=None, PH=0, PW=0, PC=0, out2=None,
-         ldc2=0, out2_trans=False, bias_out=None, workspace=None, a_ones_row=-1, adam=None):
+         ldc2=0, out2_trans=False, bias_out=None, workspace=None, a_ones_row=-1):
     """out[M,N] = epilogue( A(m,k) . B(n,k) ).
 
     A(m,k) = A[m*lda+k] (KMAJ) or A[k*lda+m] (RMAJ); likewise B(n,k).
@@ -178,9 +178,6 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
     bias_out[n] (W[in][out] weight gradients: the bias gradient without a column-sum launch).
     splits > 1 without atomic: split-K whose last-arriving split runs the fused
     epilogue (workspace = (ws, tile_ctr), default: a per-device cached one).
-    adam = (p, m, v, w16, bp, bm, bv, beta_pow, lr, beta1, beta2, eps, gscale): the fp32 result is a
-    final weight gradient - apply TF1 Adam to (p, m, v) [and the bf16 copy w16] (the bias column's
-    to (bp, bm, bv)) in the epilogue instead of storing it; the beta powers are not advanced.
     """
     if lda is None:
         lda = K if amode == KMAJ else M
@@ -201,19 +198,12 @@ def gemm(A, B, out, *, M, N, K, amode=KMAJ, lda=None, bmode=KMAJ, ldb=None, ldc=
         ws = ctr = None
         if splits > 1 and not atomic:
             ws, ctr = workspace if workspace is not None else split_workspace(out.device, splits, M, N, tile)
-        if adam is not None:
-            require().gemm_adam_epilogue(*adam)
         require().gemm(A, amode, lda, B, bmode, ldb, M, N, K, out, ldc, bias, bias_axis, act, alpha, beta, atomic,
                        splits, tile, aux, ld_aux, aux_act, b_ones_row, keep, seed, counter, pooled, argmax, PH, PW,
                        PC, out2, ldc2, out2_trans, bias_out, ws, ctr, a_ones_row,
                        ones_page(out.device) if tile in GLDS_TILES else None)
         return out
     # CPU reference
-    if adam is not None:  # gradient -> TF1 Adam of (p, m, v [, w16]) and the bias column's (bp, bm, bv)
-        gemm(A, B, out, M=M, N=N, K=K, amode=amode, lda=lda, bmode=bmode, ldb=ldb, ldc=ldc, alpha=alpha,
-             b_ones_row=b_ones_row, bias_out=bias_out, a_ones_row=a_ones_row)
-        _adam_ref(out, bias_out, *adam)
-        return out
     if a_ones_row >= 0:
         assert a_ones_row == M - 1, "CPU reference: a_ones_row must be the last row"
         a = torch.cat([_mat(A, amode, M - 1, K, lda), torch.ones(1, K)], 0)
@@ -798,22 +788,6 @@ def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=
         y = y + _shortcut_view(res, OH, OW, C, rstride).reshape(R, C)
     out.copy_(_act_ref(y, act).reshape(out.shape).to(out.dtype))
     return out
-
-
-@torch.no_grad()
-def _adam_ref(g, gb, p, m, v, w16, bp, bm, bv, beta_pow, lr, beta1, beta2, eps, gscale):
-    """CPU reference of the GEMM Adam epilogue (TF1 Adam; the beta powers are not advanced)."""
-    b1p, b2p = beta_pow.tolist()
-    lr_t = lr * math.sqrt(1 - b2p) / (1 - b1p)
-    for (pp, mm, vv, gg, ww) in ((p, m, v, g, w16), (bp, bm, bv, gb, None)):
-        if pp is None:
-            continue
-        gg = gg.reshape(-1)[:pp.numel()].view_as(pp) * gscale
-        mm.mul_(beta1).add_((1 - beta1) * gg)
-        vv.mul_(beta2).add_((1 - beta2) * gg * gg)
-        pp.sub_(lr_t * mm / (vv.sqrt() + eps))
-        if ww is not None:
-            ww.copy_(pp.reshape(ww.shape).to(ww.dtype))
 
 
 def bn_infer(x, gamma, beta, moving_mean, moving_var, out, *, eps=1e-3, act=ACT_RELU, res=None, rstride=1):

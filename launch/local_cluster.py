@@ -42,7 +42,22 @@ def task_argv(model, ps_hosts, worker_hosts, job, idx, extra):
             "--job_name=" + job, "--task_index=%d" % idx] + list(extra)
 
 
-def launch(model, n_ps, n_workers, extra=(), env=None, timeout=None, stream=True, gpus=0):
+def _port_clash(codes, outputs):
+    """A task failed because another process took one of the probed ports between free_ports()
+    and the task's bind (parallel test runs)."""
+    return any(c != 0 for c in codes.values()) and any(
+        "address already in use" in l.lower() or "eaddrinuse" in l.lower() for ls in outputs.values() for l in ls)
+
+
+def launch(model, n_ps, n_workers, extra=(), env=None, timeout=None, stream=True, gpus=0, attempts=3):
+    for attempt in range(attempts):
+        res = _launch_once(model, n_ps, n_workers, extra, env, timeout, stream, gpus)
+        if not _port_clash(res[0], res[1]) or attempt == attempts - 1:
+            return res
+        print("local_cluster: port clash, relaunching on fresh ports", file=sys.stderr, flush=True)
+
+
+def _launch_once(model, n_ps, n_workers, extra, env, timeout, stream, gpus):
     ports = free_ports(n_ps + n_workers)
     ps_hosts = ",".join("127.0.0.1:%d" % p for p in ports[:n_ps])
     worker_hosts = ",".join("127.0.0.1:%d" % p for p in ports[n_ps:])

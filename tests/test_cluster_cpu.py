@@ -70,7 +70,7 @@ def test_reinit_on_join_quirk(tmp_path):
     local_cluster.launch("softmax", 1, 1, args + ["--num_steps=30"], timeout=240, stream=False)
     codes, out, _ = local_cluster.launch("softmax", 1, 1, args + ["--num_steps=10", "--reinit_on_join"],
                                          timeout=240, stream=False)
-    assert all(c == 0 for c in codes.values())
+    assert all(c == 0 for c in codes.values()), (codes, {k: v[-15:] for k, v in out.items()})
     # GAN:181 / ENC:160 behaviour: the re-init clobbers the restored step counter
     assert _gs_lines(out[("worker", 0)])[0] == 1
 

@@ -126,3 +126,46 @@ def test_igemm_tiles_bn_bwd_stats(tile):
     torch.cuda.synchronize()
     assert _rel(st[:C], st2[:C]) < 1e-4 and _rel(st[C:], st2[C:]) < 1e-4
 
+
+
+W3_CASES = [  # (B, H, Cin, Cout): 3x3 / stride 1 weight gradients on the all-taps kernel
+    (2, 56, 64, 64),
+    (3, 28, 128, 128),
+    (4, 14, 256, 64),
+    (5, 7, 64, 128),
+    (2, 13, 64, 64),     # W does not divide 64: partial k-tiles, ragged last row block
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", W3_CASES)
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_igemm_wgrad_all_taps_kernel(case, split):
+    """igemm_wgrad3_kernel (9 taps from one staged patch) against the fp32 CPU reference and the
+    per-tap kernel (DTFE_IG_W3=0); split '1' = one workgroup per tile, '0' = the automatic m-split."""
+    from dtfe import ops
+    B, H, C, CO = case
+    g = _geom(B, H, C, CO, 3, 1)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    x = torch.randn(B, H, H, C).to(torch.bfloat16)
+    dy = torch.randn(B, H, H, CO).to(torch.bfloat16)
+    ref = torch.zeros(CO, 3, 3, C)
+    ops.conv_wgrad(dy, x, ref, None, g, 0.5)
+    out = {}
+    for w3 in ("1", "0"):
+        old = {k: os.environ.get(k) for k in ("DTFE_IG_W3", "DTFE_IG_WSPLIT")}
+        os.environ["DTFE_IG_W3"], os.environ["DTFE_IG_WSPLIT"] = w3, split
+        try:
+            dw = torch.full((CO, 3, 3, C), 0.25, device=dev)
+            ops.conv_wgrad(dy.to(dev), x.to(dev), dw, None, g, 0.5)
+            torch.cuda.synchronize()
+            out[w3] = dw.cpu() - 0.25
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    assert _rel(out["1"], ref) < 1e-2
+    assert _rel(out["1"], out["0"]) < 1e-3

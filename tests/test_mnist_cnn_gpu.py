@@ -137,35 +137,6 @@ def test_cnn_fused_sampling_conv1_matches_separate_gather(monkeypatch):
     assert abs(a["loss"].item() - b["loss"].item()) <= 1e-5 * abs(b["loss"].item())
 
 
-@pytest.mark.parametrize("B", [256, 1024])
-def test_cnn_fused_fc1_adam_is_bitwise_the_separate_apply(B, monkeypatch):
-    """step() on one replica applies fc1's Adam in the fc1 weight-gradient GEMM epilogue and the
-    other variables' in a closing launch (DTFE_CNN_FUSED_ADAM=1, the default): masters, both Adam
-    slots, the bf16 working copies, the beta powers and the global step must equal bit for bit the
-    schedule that stores every gradient and runs one whole-model Adam."""
-    from dtfe.models.mnist_cnn import MnistCnnTrainer
-
-    out = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("DTFE_CNN_FUSED_ADAM", fused)
-        tr = MnistCnnTrainer(B, "cuda", seed=21)
-        for _ in range(4):
-            tr.step()
-        torch.cuda.synchronize()
-        assert (tr.opt_rest is not None) == (fused == "1")
-        n = tr.names
-        out[fused] = dict(master=tr.P.master.clone(), m=tr.opt.s1.clone(), v=tr.opt.s2.clone(),
-                          bp=tr.opt.beta_pow.clone(), gs=int(tr.global_step.item()),
-                          w16={k: tr.P.w16[n[k]].clone() for k in ("wc1", "wc2", "wd1", "out")},
-                          wt16=tr.P.wt16[n["wc2"]].clone())
-    a, b = out["1"], out["0"]
-    assert a["gs"] == b["gs"] == 4
-    for k in ("master", "m", "v", "bp", "wt16"):
-        assert torch.equal(a[k], b[k]), (k, float((a[k].float() - b[k].float()).abs().max()))
-    for k in a["w16"]:
-        assert torch.equal(a["w16"][k], b["w16"][k]), k
-
-
 def _reference_grads_on(trainer, device):
     """_reference_grads with the fp32 oracle on ``device`` (the bench-sized batches)."""
     P, n = trainer.P, trainer.names

@@ -120,3 +120,26 @@ def test_conv_fwd_fused_bn_stats_match_separate_pass(B, H, C, Cout, k):
     v1, v2 = s1[Cout:] / R - m1 * m1, s2[Cout:] / R - m2 * m2
     assert torch.allclose(m1, m2, rtol=1e-3, atol=1e-5)
     assert torch.allclose(v1, v2, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [2, 5])
+def test_stem_fwd_fused_bn_stats_match_separate_pass(B):
+    """The ImageNet stem (7x7/2, 3->64) forward emits per-block BatchNorm partials from its epilogue
+    (two fold launches instead of a pass over y): the statistics equal the separate bn_stats pass."""
+    torch.manual_seed(4)
+    x = (torch.rand(B, 224, 224, 3, device="cuda") * 2 - 0.5).to(torch.bfloat16)
+    w = (torch.randn(64, 7, 7, 3, device="cuda") * 0.1).to(torch.bfloat16)
+    g = dict(B=B, H=224, W=224, C=3, Cout=64, OH=112, OW=112, KH=7, KW=7, stride=2, pad=3)
+    y1 = torch.empty(B, 112, 112, 64, device="cuda", dtype=torch.bfloat16)
+    y2 = torch.empty_like(y1)
+    s1, s2 = torch.zeros(128, device="cuda"), torch.zeros(128, device="cuda")
+    ops.conv_fwd(x, w, None, y1, None, g, act=ops.ACT_NONE, stats=s1)
+    ops.conv_fwd(x, w, None, y2, None, g, act=ops.ACT_NONE)
+    ops.bn_stats(y2, s2)
+    assert torch.equal(y1, y2)
+    R = B * 112 * 112
+    m1, m2 = s1[:64] / R, s2[:64] / R
+    v1, v2 = s1[64:] / R - m1 * m1, s2[64:] / R - m2 * m2
+    assert torch.allclose(m1, m2, rtol=1e-3, atol=1e-5)
+    assert torch.allclose(v1, v2, rtol=1e-3, atol=1e-6)
