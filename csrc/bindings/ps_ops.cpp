@@ -308,6 +308,12 @@ struct WorkerCh {
   void* mailbox = nullptr;       // this worker's gradient mailbox (ps GPU)
   Tensor snap;                   // reply snapshot plan (ps params -> reply buffer)
   int64_t snap_nseg = 0, snap_nwork = 0;
+  // per-range snapshots (async bucketed pushes): host copy of the snapshot segments with each
+  // one's shard-flat variable offset; a bucket's variables are copied into the reply buffer right
+  // after its apply, so the reply itself only waits for the last bucket's copy
+  std::vector<dtfe::PsSeg> snap_hsegs;
+  std::vector<long> snap_off;
+  std::map<std::pair<long, long>, SubPlan> snap_sub;
   uint64_t handled = 0;
   hipStream_t stream = nullptr;  // hogwild: per-worker stream
   std::vector<uint32_t*> done;   // per-group done counters (this channel's launches)
@@ -402,6 +408,22 @@ void ps_service_set_worker(int64_t h, int64_t w, int64_t mailbox_addr, const Ten
   c.snap_nwork = snap_nwork;
 }
 
+// shard-flat offset of each snapshot segment's variable (enables the per-bucket snapshots)
+void ps_service_set_snap_offsets(int64_t h, int64_t w, const Tensor& offs) {
+  Service* s = svc_of(h);
+  TORCH_CHECK(w >= 0 && w < s->nworkers, "dtfe ps: worker index out of range");
+  auto& c = s->ch[(size_t)w];
+  TORCH_CHECK(offs.device().is_cpu() && offs.scalar_type() == at::kLong && offs.numel() == c.snap_nseg,
+              "dtfe ps: one CPU int64 offset per snapshot segment");
+  c.snap_hsegs.resize((size_t)c.snap_nseg);
+  if (c.snap_nseg)
+    hchk(hipMemcpy(c.snap_hsegs.data(), plan_segs(c.snap), (size_t)c.snap_nseg * sizeof(dtfe::PsSeg),
+                   hipMemcpyDeviceToHost), "snap segs D2H");
+  auto o = offs.contiguous();
+  c.snap_off.assign(o.data_ptr<int64_t>(), o.data_ptr<int64_t>() + o.numel());
+  c.snap_sub.clear();
+}
+
 void ps_service_set_gs(int64_t h, const Tensor& gs) { svc_of(h)->gs = gs.data_ptr<int32_t>(); }
 
 void ps_service_set_total(int64_t h, int64_t total) { svc_of(h)->total = (long)total; }
@@ -474,25 +496,61 @@ void launch_apply_range(Service* s, WorkerCh& c, hipStream_t st, long lo, long h
   }
 }
 
+constexpr long SNAP_CHUNK = 16384;  // elements per copy work item (= ps_native.COPY_CHUNK)
+
+// copy the variables of shard range [lo, hi) into worker c's reply buffer (sub-plan cached by range)
+void snap_range(Service* s, WorkerCh& c, hipStream_t st, long lo, long hi) {
+  auto key = std::make_pair(lo, hi);
+  auto it = c.snap_sub.find(key);
+  if (it == c.snap_sub.end()) {
+    std::vector<dtfe::PsWork> wk;
+    for (size_t i = 0; i < c.snap_hsegs.size(); ++i) {
+      if (c.snap_off[i] < lo || c.snap_off[i] >= hi) continue;
+      for (long e = 0; e < c.snap_hsegs[i].n; e += SNAP_CHUNK)
+        wk.push_back({(int)i, 0, e, std::min<long>(SNAP_CHUNK, c.snap_hsegs[i].n - e)});
+    }
+    SubPlan p;
+    p.nwork = (int)wk.size();
+    const size_t bs = c.snap_hsegs.size() * sizeof(dtfe::PsSeg), off = (bs + 255) / 256 * 256;
+    std::vector<uint8_t> host(off + wk.size() * sizeof(dtfe::PsWork) + 16, 0);
+    if (bs) std::memcpy(host.data(), c.snap_hsegs.data(), bs);
+    if (!wk.empty()) std::memcpy(host.data() + off, wk.data(), wk.size() * sizeof(dtfe::PsWork));
+    p.blob = at::empty({(int64_t)host.size()}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, s->device));
+    hchk(hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice), "snap plan H2D");
+    it = c.snap_sub.emplace(key, std::move(p)).first;
+  }
+  const SubPlan& p = it->second;
+  if (p.nwork > 0)
+    dtfe::launch_ps_copy(plan_segs(p.blob), plan_work(p.blob, (int64_t)c.snap_hsegs.size()), p.nwork, st);
+}
+
+// a bucket's apply (and, with per-range snapshots, its reply copy)
+void apply_bucket(Service* s, WorkerCh& c, hipStream_t st, long lo, long hi) {
+  launch_apply_range(s, c, st, lo, hi);
+  if (!c.snap_off.empty()) snap_range(s, c, st, lo, hi);
+}
+
 // async push with buckets: apply every bucket range of request `seq` not applied yet (the gaps
 // between the ranges already applied - all of the shard when the worker sent no bucket), then
-// advance each group's step scalars once
-void finish_bucketed(Service* s, WorkerCh& c, hipStream_t st, uint64_t seq) {
+// advance each group's step scalars once.  Returns true when the reply buffer is already current.
+bool finish_bucketed(Service* s, WorkerCh& c, hipStream_t st, uint64_t seq) {
   std::vector<std::pair<long, long>> done = c.range_seq == seq ? c.ranges : std::vector<std::pair<long, long>>{};
   std::sort(done.begin(), done.end());
   long at = 0;
   for (const auto& r : done) {
-    if (r.first > at) launch_apply_range(s, c, st, at, r.first);
+    if (r.first > at) apply_bucket(s, c, st, at, r.first);
     at = std::max(at, r.second);
   }
-  if (at < s->total) launch_apply_range(s, c, st, at, s->total);
+  if (at < s->total) apply_bucket(s, c, st, at, s->total);
   for (const auto& g : s->groups) dtfe::launch_opt_advance(g.args, st);
   c.ranges.clear();
+  return !c.snap_off.empty();
 }
 
-void reply(Service* s, int w, hipStream_t st, uint64_t seq, int stale) {
+void reply(Service* s, int w, hipStream_t st, uint64_t seq, int stale, bool snapped = false) {
   auto& c = s->ch[(size_t)w];
-  if (c.snap_nwork > 0) dtfe::launch_ps_copy(plan_segs(c.snap), plan_work(c.snap, c.snap_nseg), (int)c.snap_nwork, st);
+  if (!snapped && c.snap_nwork > 0)
+    dtfe::launch_ps_copy(plan_segs(c.snap), plan_work(c.snap, c.snap_nseg), (int)c.snap_nwork, st);
   dtfe::launch_ps_reply(slot_dev(s->shm, w), s->gs, seq, s->version, stale, st);
 }
 
@@ -573,7 +631,7 @@ void run(Service* s) {
             c.ranges.clear();
           }
           if (lo < hi) {
-            launch_apply_range(s, c, bst, lo, hi);
+            apply_bucket(s, c, bst, lo, hi);
             c.ranges.emplace_back(lo, hi);
             s->n_bucket++;
           }
@@ -593,15 +651,16 @@ void run(Service* s) {
         continue;
       }
       if (!s->sync) {
+        bool snapped = false;
         if (s->total > 0) {
           scan_buckets(seq - 1);  // bucket words published just before this request
-          finish_bucketed(s, c, st, seq);
+          snapped = finish_bucketed(s, c, st, seq);
         } else {
           launch_apply(s, c, st, c.mailbox, false, 1.f);
         }
         s->version++;
         s->n_apply++;
-        reply(s, w, st, seq, 0);
+        reply(s, w, st, seq, 0, snapped);
         continue;
       }
       // sync: drop stale, accumulate fresh, apply the mean after R contributions
@@ -727,6 +786,7 @@ TORCH_LIBRARY_FRAGMENT(dtfe, m) {
   m.def("ps_service_set_worker(int h, int w, int mailbox_addr, Tensor snap, int snap_nseg, int snap_nwork) -> ()",
         &ps_service_set_worker);
   m.def("ps_service_set_total(int h, int total) -> ()", &ps_service_set_total);
+  m.def("ps_service_set_snap_offsets(int h, int w, Tensor offs) -> ()", &ps_service_set_snap_offsets);
   m.def("ps_bucket(int shm, int w, Tensor ctr, int b, int lo, int hi) -> ()", &ps_bucket);
   m.def("ps_service_set_gs(int h, Tensor gs) -> ()", &ps_service_set_gs);
   m.def("ps_service_set_acc(int h, Tensor(a!) acc) -> ()", &ps_service_set_acc);

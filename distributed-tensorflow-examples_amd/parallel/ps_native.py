@@ -152,6 +152,10 @@ class NativeShardService:
             self._plans.append(blob)
             lib.ps_service_set_worker(self.svc, w, base + w * (self.mb + self.rb), blob, len(segs),
                                       lib.ps_plan_nwork(st, COPY_CHUNK))
+            # each segment's shard-flat variable offset: a bucket's variables are snapshotted into
+            # the reply buffer right after the bucket's apply (async), not all at the reply
+            lib.ps_service_set_snap_offsets(self.svc, w, torch.tensor(
+                [self.lay.offsets[name] for name, _, _, _, _ in layout], dtype=torch.int64))
         torch.cuda.synchronize(dev)
         st = server.store
         st.set(_key(server, self.k, "shm"), self.shm_name)
