@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch_size", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default="", help="comma-separated op names (default: all)")
     a = ap.parse_args()
     B = a.batch_size
     t = MnistCnnTrainer(B, "cuda")
@@ -63,6 +64,8 @@ def main():
         "adam": (lambda: t.opt.step(), 0),
         "grad_zero": (lambda: t.P.grad.zero_(), 0),
     }
+    if a.only:
+        opsd = {k: v for k, v in opsd.items() if k in a.only.split(",")}
     times = {k: [] for k in opsd}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(a.iters):
