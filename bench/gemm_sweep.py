@@ -37,6 +37,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--tiles", type=lambda v: [int(t) for t in v.split(",")], default=[0, 2, 5, 6, 8, 10, 12],
+                    help="tile ids (ops.TILE_DIMS)")
     a = ap.parse_args()
     B, K1, FC = a.batch, 3136, 1024
     d, bf = "cuda", torch.bfloat16
@@ -63,9 +65,9 @@ def main():
     for name, (fn, ref, fl) in shapes.items():
         tr = timeit(ref, a.iters)
         print(f"{name:10s} torch.mm {tr:8.1f} us {fl / tr / 1e6:7.1f} TFLOP/s", flush=True)
-        for tile in (0, 2, 5, 6, 8, 10, 12):
+        for tile in a.tiles:
             row = []
-            for s in (1, 2, 4):
+            for s in ((1, 2, 4) if tile < 14 else (1,)):
                 try:
                     t = timeit(lambda: fn(tile, s), a.iters)
                 except RuntimeError:
@@ -73,7 +75,7 @@ def main():
                     continue
                 row.append(f"s{s}:{t:7.1f}us/{fl / t / 1e6:6.1f}TF")
             bm, bn = ops.TILE_DIMS[tile]
-            print(f"{name:10s} {bm:3d}x{bn:<3d}{'g' if tile >= 5 else ' '} " + "  ".join(row), flush=True)
+            print(f"{name:10s} {bm:3d}x{bn:<3d}{'g' if tile >= 5 else ' '}{tile:<3d} " + "  ".join(row), flush=True)
 
 
 if __name__ == "__main__":

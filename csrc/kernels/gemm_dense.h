@@ -252,7 +252,8 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
 // dtype: 0 = bf16, 1 = f32.  tile: 0 = 64x64, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 32x32
 // (register-staged engine of gemm_core.h); 5 = 128x128, 6 = 128x64, 7 = 64x128, 8 = 64x64 with
 // direct global->LDS staging, 3 stages (gemm_glds.h: bf16, K % 64 == 0, whole tiles - see
-// gemm_glds_eligible); 9..12 the same tiles with 2 stages
+// gemm_glds_eligible); 9..12 the same tiles with 2 stages; 14..16 64x64 with 4 / 6 / 8 stages,
+// 17..18 128x64 with 4 / 6 stages
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream);
 // tile 13: exact-fp32 16x16 tiles, one workgroup per tile with an in-workgroup 4-way K split and

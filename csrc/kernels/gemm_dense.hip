@@ -17,10 +17,11 @@ static void launch_one(int splits, const DenseGemmArgs& args, hipStream_t s) {
 }
 
 int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
-  static const int dims[14][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
+  static const int dims[19][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64},
-                                  {128, 128}, {128, 64}, {64, 128}, {64, 64}, {16, 16}};
-  if (tile < 0 || tile > 13) return -1;
+                                  {128, 128}, {128, 64}, {64, 128}, {64, 64}, {16, 16},
+                                  {64, 64}, {64, 64}, {64, 64}, {128, 64}, {128, 64}};
+  if (tile < 0 || tile > 18) return -1;
   bm = dims[tile][0];
   bn = dims[tile][1];
   if (tile == GEMM_TILE_SMALL) return 16;
@@ -44,7 +45,9 @@ bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGe
 }
 
 // tiles 5..8: 3 k-tiles in flight (one workgroup per CU streams deeper);
-// tiles 9..12: 2 stages, half the LDS, so more workgroups share a CU (grids of many tiles)
+// tiles 9..12: 2 stages, half the LDS, so more workgroups share a CU (grids of many tiles);
+// tiles 14..18: deeper pipelines (64x64 with 4 / 6 / 8 stages, 128x64 with 4 / 6) for long-K grids
+// of about one workgroup per CU, where 3 stages leave the k-loop waiting on the load latency
 template <int BM, int BN, int AM, int BMD, int STAGES>
 static void launch_glds(int splits, const DenseGemmArgs& a, hipStream_t s) {
   const int tiles = (a.M / BM) * ((a.N + BN - 1) / BN);
@@ -63,6 +66,11 @@ static void glds_by_tile(int tile, int splits, const DenseGemmArgs& a, hipStream
     case 10: launch_glds<128, 64, AM, BMD, 2>(splits, a, s); break;
     case 11: launch_glds<64, 128, AM, BMD, 2>(splits, a, s); break;
     case 12: launch_glds<64, 64, AM, BMD, 2>(splits, a, s); break;
+    case 14: launch_glds<64, 64, AM, BMD, 4>(splits, a, s); break;
+    case 15: launch_glds<64, 64, AM, BMD, 6>(splits, a, s); break;
+    case 16: launch_glds<64, 64, AM, BMD, 8>(splits, a, s); break;
+    case 17: launch_glds<128, 64, AM, BMD, 4>(splits, a, s); break;
+    case 18: launch_glds<128, 64, AM, BMD, 6>(splits, a, s); break;
     default: throw std::runtime_error("gemm_dense: bad glds tile id");
   }
 }

@@ -223,9 +223,11 @@ class MnistCnnTrainer:
         # 2-stage variant (784 / 800 tiles, several workgroups per CU)
         self.glds = self.device.type == "cuda" and os.environ.get("DTFE_CNN_GLDS", "1") != "0"
         K1 = 7 * 7 * C2
-        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 8)
-        self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
-        self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
+        # DTFE_CNN_TILES=fwd,dgrad,wgrad overrides the glds tile ids (A/B sweeps)
+        tiles = [int(t) for t in os.environ.get("DTFE_CNN_TILES", "8,12,12").split(",")]
+        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, tiles[0])
+        self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, tiles[1])
+        self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, tiles[2], b_ones_row=K1)
         # head weight gradient: split-K over the batch with the deterministic last-arriver combine
         # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
         # workspace, since it runs on the fc branch beside other GEMMs

@@ -33,8 +33,10 @@ TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)
              # global_load_lds kernel family (csrc/kernels/gemm_glds.h): bf16, K % 64 == 0, whole tiles
              5: (128, 128), 6: (128, 64), 7: (64, 128), 8: (64, 64),      # 3 k-tiles in flight
              9: (128, 128), 10: (128, 64), 11: (64, 128), 12: (64, 64),   # 2 stages (more WGs per CU)
-             13: (16, 16)}   # exact-fp32 small-layer kernel (gemm_small.hip): no split-K, in-WG K split
-GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12)
+             13: (16, 16),   # exact-fp32 small-layer kernel (gemm_small.hip): no split-K, in-WG K split
+             14: (64, 64), 15: (64, 64), 16: (64, 64),  # 4 / 6 / 8 stages (long-K grids, ~1 WG per CU)
+             17: (128, 64), 18: (128, 64)}              # 4 / 6 stages
+GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18)
 TILE_SMALL = 13
 _ONES = {}
 

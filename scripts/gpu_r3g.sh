@@ -25,4 +25,5 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLI
   done
 done
 for f in $O/pmc_*_d*.csv; do echo "== $f"; cat $f; done
+timeout -k 10 400 python3 bench/resnet50_convs.py --batch 256 --reps 10 > $O/r50_convs.log 2>&1; cat $O/r50_convs.log
 exit 0
