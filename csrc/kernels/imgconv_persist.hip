@@ -300,7 +300,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
 // offsets are constants), the double-buffered fragment registers alternate by step parity
 // at compile time, and a step costs RT + NT reads, RT x NT MFMAs and no VALU.
 // One wave per RT 16-row tiles x all N columns (NT = N/16), WM waves cover the image.
-template <int CS, int KH, int KW, int LWP, int PS, int KP, int NT, int RT, int WM, int NPF, bool POOLED>
+template <int CS, int KH, int KW, int LWP, int PS, int KP, int NT, int RT, int WM, int NPF, bool POOLED, int ACT>
 __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, PGeom G) {
   constexpr int THREADS = 64 * WM;
   constexpr int T = KH * KW, K = T * CS, NK = K / 32, CPP = CS / 8;
@@ -407,6 +407,26 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
 #pragma unroll
   for (int n = 0; n < NT; ++n) biasv[n] = a.bias ? a.bias[n * 16 + (lane & 15)] : 0.f;
 
+  // per-lane geometry is the same for every image: the row -> pixel decode (integer divisions by
+  // the runtime OW), the A-fragment bases, the data gradient's output pixels and the forward's
+  // pooled staging slots are computed once, not once per image
+  const bf16* abase[RT];
+  int opix[RT];   // data gradient: output pixel of this lane's column (-1: padding row)
+  int ppix[RT];   // forward: pooled pixel of this lane's 2x2 window (-1: padding / past the image)
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    int oy = 0, ox = 0;
+    // tiles past the image (a wave's last r) multiply pixel 0 and are dropped by the epilogue:
+    // no lane-divergent guards inside the k loop
+    const bool ok = row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
+    abase[r] = img + (ok ? (oy * LWP + ox) * PS : 0) + 8 * g;
+    opix[r] = ok ? oy * a.OW + ox : -1;
+    const int tile = wm + WM * r;
+    int py = 0, px = 0;
+    const bool pok = tile < tiles && row_pixel(tile * 16 + (lane >> 4) * 4, a.OH, a.OW, 1, py, px);
+    ppix[r] = pok ? (py >> 1) * (a.OW >> 1) + (px >> 1) : -1;
+  }
+
   long b = blockIdx.x;
   if (b < a.B) load_src(b);
   __syncthreads();
@@ -414,33 +434,20 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
     if (!(a.diag & 2) || b == blockIdx.x) write_src();
     __syncthreads();
     if (b + gridDim.x < a.B && !(a.diag & 2)) load_src(b + gridDim.x);
-    // tiles past the image (a wave's last r) multiply pixel 0 and are dropped by the epilogue:
-    // no lane-divergent guards inside the k loop
-    const bf16* abase[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      int oy = 0, ox = 0;
-      row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
-      abase[r] = img + (oy * LWP + ox) * PS + 8 * g;
-    }
     // Data gradient (POOLED source): the MFMA operands are swapped, D = W . patch^T, so a lane's
     // accumulator holds 4 consecutive channels (4g..4g+3 of each n-tile) of ONE output pixel
     // (column lane & 15): the epilogue is one 8-B masked store per n-tile straight to HBM - no
     // LDS staging, no scattered 2-byte writes, no extra barriers (rocprof ablation of the staged
     // version: ~14 us of the 47 us B=1024 launch).  The lane's ReLU-mask words are in flight
     // during the k loop.
-    int opix[RT];
     u32x2_t mk[RT][NT];
     if constexpr (POOLED) {
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        int oy = 0, ox = 0;
-        const bool ok = row_pixel((wm + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
-        opix[r] = ok ? oy * a.OW + ox : -1;
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           mk[r][n] = u32x2_t{0x3f803f80u, 0x3f803f80u};  // bf16 1.0: no mask
-          if (ok && a.relu_mask)
+          if (opix[r] >= 0 && a.relu_mask)
             mk[r][n] = *reinterpret_cast<const u32x2_t*>(a.relu_mask + (b * M + opix[r]) * (long)a.N + n * 16 + 4 * g);
         }
       }
@@ -485,6 +492,15 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
                                                                 0, 0, 0);
         }
       }
+      // Pin the interleave: the RT + NT reads of step st + PF spread between step st's MFMAs.
+      // Without it the scheduler sinks every read to just before its consumer (one lgkmcnt wait
+      // per MFMA pair), leaving the MFMA pipe ~38 % busy (rocprof SQ_VALU_MFMA_BUSY_CYCLES).
+      constexpr int nm = RT * NT, nr = (st + PF < NK) ? RT + NT : 0;
+      static_for<0, nm>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, r0 = i * nr / nm, r1 = (i + 1) * nr / nm;
+        if constexpr (r1 > r0) __builtin_amdgcn_sched_group_barrier(0x100, r1 - r0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      });
     });
     // Epilogue through LDS: the per-lane results are scattered 2-byte (and 1-byte argmax) values,
     // so they are staged in LDS in the output's own layout and leave as 16-B row-contiguous
@@ -497,11 +513,8 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
       uint8_t* sa = reinterpret_cast<uint8_t*>(sy + (M >> 2) * a.N);
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        const int tile = wm + WM * r;
-        if (tile >= tiles || (a.diag & 1)) break;
-        int oy, ox;
-        if (!row_pixel(tile * 16 + (lane >> 4) * 4, a.OH, a.OW, 1, oy, ox)) continue;
-        const int pp = (oy >> 1) * (a.OW >> 1) + (ox >> 1);
+        if (ppix[r] < 0 || (a.diag & 1)) continue;
+        const int pp = ppix[r];
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           const int col = n * 16 + (lane & 15);
@@ -510,7 +523,7 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
           float mx = v[0];
 #pragma unroll
           for (int j = 1; j < 4; ++j) if (v[j] > mx) { mx = v[j]; am = j; }
-          sy[pp * a.N + col] = f2bf(apply_act(mx + biasv[n], a.act));
+          sy[pp * a.N + col] = f2bf(apply_act(mx + biasv[n], ACT));
           sa[pp * a.N + col] = (uint8_t)am;
         }
       }
@@ -536,8 +549,8 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
           uint32_t w2[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const uint32_t lo = f2bf(apply_act(acc[r][n][2 * h] + biasv[n], a.act));
-            const uint32_t hi = f2bf(apply_act(acc[r][n][2 * h + 1] + biasv[n], a.act));
+            const uint32_t lo = f2bf(apply_act(acc[r][n][2 * h] + biasv[n], ACT));
+            const uint32_t hi = f2bf(apply_act(acc[r][n][2 * h + 1] + biasv[n], ACT));
             // keep element e where mask e > 0 (bf16 bits: positive, non-zero, not NaN)
             const uint32_t m = mk[r][n][h], ml = m & 0xffffu, mh = m >> 16;
             w2[h] = (((ml - 1u) < 0x7f80u) ? lo : 0u) | (((mh - 1u) < 0x7f80u) ? (hi << 16) : 0u);
@@ -642,10 +655,11 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s) {
 }  // namespace
 
 // compile-time-geometry instances (MNIST conv2 forward / data gradient); false if `a` is not one
-template <int CS, int KH, int KW, int LWP, int PS, int NT, int RT, int WM, bool POOLED>
+template <int CS, int KH, int KW, int LWP, int PS, int NT, int RT, int WM, bool POOLED, int ACT>
 bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
   constexpr int K = KH * KW * CS, KP = (K + 31) / 32 * 32 + 16;
   if (a.CS != CS || a.KH != KH || a.KW != KW || a.N != NT * 16 || a.stride != 1 || a.dil > 1) return false;
+  if (a.act != ACT) return false;  // the activation is a compile-time constant of the epilogue
   if ((a.src == nullptr) != POOLED) return false;
   // the LDS-staged epilogues: forward = pooled (+ argmax), data gradient = un-pooled
   if (POOLED ? a.pool != 0 : a.pool == 0) return false;
@@ -668,8 +682,8 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM), lds, s, ad, G);
   };
   switch (G.npf) {
-    case 1: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 1, POOLED>); return true;
-    case 2: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 2, POOLED>); return true;
+    case 1: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 1, POOLED, ACT>); return true;
+    case 2: go(imgconv_fixed_kernel<CS, KH, KW, LWP, PS, KP, NT, RT, WM, 2, POOLED, ACT>); return true;
     default: return false;
   }
 }
@@ -679,8 +693,8 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
   if (a.OH == 14 && a.OW == 14 && a.B >= 256) {
     // compile-time geometry, one 16-row tile per wave (13 waves); 2 / 4 tiles per wave (7 / 4
     // waves) measured slower and were removed in round 3
-    if (launch_fixed<32, 5, 5, 20, 48, 4, 1, 13, false>(a, s)) return true;  // conv2 forward
-    if (launch_fixed<64, 5, 5, 20, 80, 2, 1, 13, true>(a, s)) return true;   // conv2 data gradient
+    if (launch_fixed<32, 5, 5, 20, 48, 4, 1, 13, false, ACT_RELU>(a, s)) return true;  // conv2 forward
+    if (launch_fixed<64, 5, 5, 20, 80, 2, 1, 13, true, ACT_NONE>(a, s)) return true;   // conv2 data gradient
   }
   const bool pooled = a.src == nullptr;
   if (pooled && ((a.SH | a.SW) & 1)) return false;
