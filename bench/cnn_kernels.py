@@ -48,6 +48,7 @@ def main():
         "head_wgrad": (lambda: ops.gemm(t.dl, t.h, t.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=16,
                                         bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=t.gw["bout"],
                                         atomic=True, splits=max(1, min(16, B // 128)), tile=4), 0),
+        "head_wgrad_k": (lambda: ops.head_wgrad(t.dl, t.h, t.gw["out"], t.gw["bout"], NCLS), 0),
         "fc1_dgrad": (lambda: ops.gemm(t.dzf, t.w["wd1"], t.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1,
                                        aux=t.p2, aux_act=ops.ACT_RELU), fc1_flops),
         "fc1_wgrad": (lambda: ops.gemm(t.dzf, t.p2, t.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,

@@ -16,6 +16,8 @@
 #include "common.h"
 #include "head.h"
 
+#include <type_traits>
+
 namespace dtfe {
 
 // One wave per batch row (K/64 features per lane).  The wave's slice of W (NC x K/64 bf16,
@@ -124,70 +126,90 @@ void launch_head_xent(const HeadArgs& a, hipStream_t s) {
 namespace dtfe {
 
 // Classifier-head weight / bias gradient: dW[c][k] = sum_b dl[b][c] h[b][k], db[c] = sum_b dl[b][c].
-// The layer is 10 x 1024 over a 1024-row batch (21 MFLOP): a split-K MFMA GEMM spends ~16 us on
-// 32 x 32 tiles (a 10-row M padded to 32) and the fixed-order combine of 8 K-splits.  Here one
-// 1024-thread workgroup owns 16 columns of dW for the WHOLE batch (no cross-workgroup
-// reduction): the batch's dlogit rows are staged in LDS (32 KB, 16-B loads) while every thread
-// has its 16 h values in flight (thread (column c = t & 15, row group r = t >> 4) takes rows
-// r, r + 64, ...), so the launch pays about two memory latencies; the 64 row groups are then
-// summed through LDS in a fixed order - bitwise reproducible, no atomics.  Workgroup K/16
-// produces the bias gradient (h read as ones).
-template <int NC>
-__global__ __launch_bounds__(1024) void head_wgrad_kernel(HeadWgradArgs a) {
-  constexpr int RG = 64, PER = 16;  // row groups, rows per thread (B <= RG * PER)
-  // one LDS buffer: the staged dlogit rows, then (after a barrier) the per-row-group partials
-  constexpr int DL_BYTES = RG * PER * 16 * 2, PART_BYTES = RG * 16 * (NC + 1) * 4;
-  __shared__ __attribute__((aligned(16))) char smem[DL_BYTES > PART_BYTES ? DL_BYTES : PART_BYTES];
-  auto dls = reinterpret_cast<bf16(*)[16]>(smem);
-  auto part = reinterpret_cast<float(*)[16][NC + 1]>(smem);
-  const int t = threadIdx.x, c = t & 15, rg = t >> 4;
-  const bool bias_blk = blockIdx.x * 16 >= a.K;
-  const int col = blockIdx.x * 16 + c;
-  float hv[PER];
+// The layer is 10 x 1024 over a 1024-row batch (21 MFLOP, 2 MB of h).  One 256-thread workgroup
+// owns 8 columns of dW for the whole batch (128 workgroups + one for the bias): a thread loads
+// the 16-B h chunk and the dlogit row of each of its rows (all loads in flight at once),
+// accumulates 10 x 8 partial sums, and the wave reduces them with a halving butterfly - each
+// exchange step sends half of the lane's remaining values, 85 shuffles instead of 80 x 6 - to
+// 16 lanes holding 5 totals each; the 4 waves are summed in order through LDS.  Fixed
+// summation order (bitwise reproducible), no atomics, no cross-workgroup reduction.  (The
+// previous form - 64 workgroups of 1024 threads, 16 columns each, a 64-step serial LDS sum per
+// output - took ~11 us on the MNIST step's critical path.)
+template <int NC, int ROWS>
+__global__ __launch_bounds__(256) void head_wgrad_kernel(HeadWgradArgs a) {
+  static_assert(NC * 8 == 80, "the butterfly below is laid out for 10 classes x 8 columns");
+  constexpr int V = NC * 8;
+  __shared__ float red[4][V];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool bias_blk = blockIdx.x * 8 >= a.K;
+  const int col0 = blockIdx.x * 8;
+  u32x4_t hv[ROWS], d0[ROWS], d1[ROWS];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int b = rg + RG * i;
-    hv[i] = b < a.B ? (bias_blk ? 1.f : bf2f(a.h[(long)b * a.ldh + col])) : 0.f;
+  for (int i = 0; i < ROWS; ++i) {
+    const int b = t + 256 * i;
+    const bool ok = b < a.B;
+    hv[i] = (ok && !bias_blk) ? *reinterpret_cast<const u32x4_t*>(a.h + (long)b * a.ldh + col0) : u32x4_t{0u, 0u, 0u, 0u};
+    d0[i] = ok ? *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl) : u32x4_t{0u, 0u, 0u, 0u};
+    d1[i] = ok ? *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl + 8) : u32x4_t{0u, 0u, 0u, 0u};
   }
-  for (int i = t; i < RG * PER * 2; i += 1024) {  // 16-B halves of the 32-B dlogit rows
-    const int b = i >> 1;
-    u32x4_t v = {0u, 0u, 0u, 0u};
-    if (b < a.B) v = *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl + (i & 1) * 8);
-    *reinterpret_cast<u32x4_t*>(&dls[b][(i & 1) * 8]) = v;
-  }
-  __syncthreads();
-  float acc[NC];
+  float v[V];
 #pragma unroll
-  for (int n = 0; n < NC; ++n) acc[n] = 0.f;
+  for (int j = 0; j < V; ++j) v[j] = 0.f;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int b = rg + RG * i;
-    const u32x4_t d0 = *reinterpret_cast<const u32x4_t*>(&dls[b][0]);
-    const u32x4_t d1 = *reinterpret_cast<const u32x4_t*>(&dls[b][8]);
+  for (int i = 0; i < ROWS; ++i) {
+    float h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = bias_blk ? ((t + 256 * i) < a.B ? 1.f : 0.f) : bf2f((bf16)(hv[i][e >> 1] >> (16 * (e & 1))));
 #pragma unroll
     for (int n = 0; n < NC; ++n) {
-      const uint32_t w = n < 8 ? d0[n >> 1] : d1[(n - 8) >> 1];
-      acc[n] = fmaf(bf2f((bf16)(w >> (16 * (n & 1)))), hv[i], acc[n]);
+      const uint32_t w = n < 8 ? d0[i][n >> 1] : d1[i][(n - 8) >> 1];
+      const float d = bf2f((bf16)(w >> (16 * (n & 1))));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[n * 8 + e] = fmaf(d, h[e], v[n * 8 + e]);
     }
   }
-  __syncthreads();  // every thread is done with the staged rows
+  // halving butterfly over lane bits 5..2: 80 -> 40 -> 20 -> 10 -> 5 values per lane
+  auto halve = [&](auto half_c, int mask) {
+    constexpr int H = decltype(half_c)::value;
+    const bool hi = (lane & mask) != 0;
 #pragma unroll
-  for (int n = 0; n < NC; ++n) part[rg][c][n] = acc[n];
+    for (int j = 0; j < H; ++j) {
+      const float send = hi ? v[j] : v[H + j];
+      const float keep = hi ? v[H + j] : v[j];
+      v[j] = keep + __shfl_xor(send, mask, 64);
+    }
+  };
+  halve(std::integral_constant<int, 40>{}, 32);
+  halve(std::integral_constant<int, 20>{}, 16);
+  halve(std::integral_constant<int, 10>{}, 8);
+  halve(std::integral_constant<int, 5>{}, 4);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    v[j] += __shfl_xor(v[j], 2, 64);
+    v[j] += __shfl_xor(v[j], 1, 64);
+  }
+  // lane holds values ((b5 ? 40 : 0) + (b4 ? 20 : 0) + (b3 ? 10 : 0) + (b2 ? 5 : 0) + j)
+  if ((lane & 3) == 0) {
+    const int base = ((lane >> 5) & 1) * 40 + ((lane >> 4) & 1) * 20 + ((lane >> 3) & 1) * 10 + ((lane >> 2) & 1) * 5;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) red[wid][base + j] = v[j];
+  }
   __syncthreads();
-  if (t < 16 * NC) {
-    const int cc = t % 16, n = t / 16;
-    float s = 0.f;
-    for (int r = 0; r < RG; ++r) s += part[r][cc][n];
-    if (!bias_blk) a.dw[(long)n * a.ldw + blockIdx.x * 16 + cc] = s * a.scale;
-    else if (cc == 0) a.db[n] = s * a.scale;
+  if (t < V) {
+    const float s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    const int n = t >> 3, e = t & 7;
+    if (!bias_blk) a.dw[(long)n * a.ldw + col0 + e] = s * a.scale;
+    else if (e == 0) a.db[n] = s * a.scale;
   }
 }
 
 void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s) {
-  if (a.NC != 10 || a.K % 16 || a.ld_dl < 16 || a.ld_dl % 8 || a.B > 1024)
-    throw std::runtime_error("head_wgrad: needs NC=10, K % 16 == 0, 16-B aligned dl rows of >= 16, B <= 1024");
-  const int blocks = a.K / 16 + (a.db ? 1 : 0);
-  hipLaunchKernelGGL(head_wgrad_kernel<10>, dim3(blocks), dim3(1024), 0, s, a);
+  if (a.NC != 10 || a.K % 8 || a.ld_dl < 16 || a.ld_dl % 8 || a.ldh % 8 || a.B > 1024)
+    throw std::runtime_error("head_wgrad: needs NC=10, K % 8 == 0, 16-B aligned dl rows of >= 16 and h rows, B <= 1024");
+  const int blocks = a.K / 8 + (a.db ? 1 : 0);
+  if (a.B <= 256) hipLaunchKernelGGL((head_wgrad_kernel<10, 1>), dim3(blocks), dim3(256), 0, s, a);
+  else if (a.B <= 512) hipLaunchKernelGGL((head_wgrad_kernel<10, 2>), dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((head_wgrad_kernel<10, 4>), dim3(blocks), dim3(256), 0, s, a);
 }
 
 }  // namespace dtfe

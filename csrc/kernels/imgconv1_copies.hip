@@ -59,6 +59,8 @@ __device__ __forceinline__ void build_copies(const bf16* P, bf16* C) {
 }
 
 // ------------------------------------------------------------------ forward
+template <int ACT>  // the epilogue activation is a compile-time constant (a runtime switch per value
+                    // was ~a fifth of the kernel's VALU)
 __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 P[PRW * PWD];
   __shared__ __attribute__((aligned(16))) bf16 C[8 * CSZ];
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
         for (int j = 1; j < 4; ++j) if (v[j] > mx) { mx = v[j]; am = j; }
         const long o = ((b * 14 + py) * 14 + px) * NCH + nt * 16 + (lane & 15);
         if (a.diag & 1) continue;
-        a.y[o] = f2bf(apply_act(mx + biasv[nt], a.act));
+        a.y[o] = f2bf(apply_act(mx + biasv[nt], ACT));
         if (a.argmax) a.argmax[o] = (uint8_t)am;
       }
     }
@@ -314,7 +316,11 @@ bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s) {
   }();
   ImgConvArgs ad = a;
   ad.diag = diag;
-  hipLaunchKernelGGL(conv1c_fwd_kernel, dim3(grid), dim3(TH), 0, s, ad);
+  switch (a.act) {
+    case ACT_RELU: hipLaunchKernelGGL(conv1c_fwd_kernel<ACT_RELU>, dim3(grid), dim3(TH), 0, s, ad); break;
+    case ACT_NONE: hipLaunchKernelGGL(conv1c_fwd_kernel<ACT_NONE>, dim3(grid), dim3(TH), 0, s, ad); break;
+    default: return false;  // sigmoid / tanh: the generic few-channel kernel
+  }
   return true;
 }
 
