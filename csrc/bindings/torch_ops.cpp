@@ -111,6 +111,14 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
 }
 
+// gemm_group(anchor, begin): begin / end a grouped launch on the current stream (gemm_dense.h);
+// `anchor` is any tensor on the launch device (dispatch only)
+void gemm_group(const Tensor& anchor, bool begin) {
+  check_cuda(anchor, "anchor");
+  if (begin) dtfe::glds_group_begin();
+  else dtfe::glds_group_end(cur_stream());
+}
+
 // ------------------------------------------------------------------- conv
 dtfe::ConvGeom geom(int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, int64_t OH, int64_t OW, int64_t KH,
                     int64_t KW, int64_t stride, int64_t pad, int64_t pool) {
@@ -874,6 +882,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep,"
       " Tensor(f!)? step_counter=None) -> ()");
   m.def("head_wgrad(Tensor dl, Tensor h, Tensor(a!) dw, Tensor(b!)? db, int nc, float scale) -> ()");
+  m.def("gemm_group(Tensor anchor, bool begin) -> ()");
   m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
   m.def(
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
@@ -920,6 +929,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("head_xent", &head_xent);
   m.impl("head_wgrad", &head_wgrad);
+  m.impl("gemm_group", &gemm_group);
   m.impl("apply_gradients", &apply_gradients);
   m.impl("gather_rows", &gather_rows);
   m.impl("seq_stage", &seq_stage);

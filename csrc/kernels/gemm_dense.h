@@ -261,6 +261,15 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
 constexpr int GEMM_TILE_SMALL = 13;
 bool gemm_small_eligible(int dtype, const DenseGemmArgs& a);
 void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s);
+// Grouped launch (gemm_dense.hip): between begin and end, launch_gemm_dense calls with glds tile 12
+// and one split, and launch_head_wgrad calls, are recorded instead of launched (record functions
+// return false when a call does not fit the group); end launches the recorded pieces as one grid
+// (head weight gradient, then a (KMAJ, RMAJ) and a (RMAJ, RMAJ) GEMM), or one by one otherwise.
+struct HeadWgradArgs;
+void glds_group_begin();
+bool glds_group_record(int amode, int bmode, const DenseGemmArgs& a);
+bool glds_group_record_head(const HeadWgradArgs& a);
+void glds_group_end(hipStream_t s);
 // block tile of a tile id; returns the k-tile depth (split-K chunks are multiples of it)
 int gemm_dense_tile_dims(int tile, int& bm, int& bn);
 // whether the global_load_lds kernel family can run this GEMM with tile `tile` (5..8)

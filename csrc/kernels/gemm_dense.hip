@@ -1,7 +1,9 @@
 // Instantiation + dispatch of the dense GEMM kernel family.
 #include "gemm_dense.h"
 #include "gemm_glds.h"
+#include "head.h"
 
+#include <cstring>
 #include <stdexcept>
 
 namespace dtfe {
@@ -104,6 +106,7 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
     launch_gemm_small(amode, bmode, args, stream);
     return;
   }
+  if (tile == 12 && splits == 1 && dtype == 0 && glds_group_record(amode, bmode, args)) return;  // inside a group
   if (tile >= 5) {
     if (!gemm_glds_eligible(dtype, amode, bmode, tile, args))
       throw std::runtime_error("gemm_dense: this GEMM is not eligible for the global_load_lds tiles");
@@ -117,6 +120,101 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
   }
   if (dtype == 0) by_mode<bf16>(amode, bmode, tile, splits, args, stream);
   else by_mode<float>(amode, bmode, tile, splits, args, stream);
+}
+
+// ------------------------------------------------------------ grouped launch
+// Independent GEMMs of one step phase in ONE launch (horizontal fusion): workgroup ranges of the grid
+// run different pieces - the head weight gradient's 129 workgroups, then two 64x64 2-stage glds
+// GEMMs (the MNIST-CNN fc1 data and weight gradients).  One launch instead of a fork onto a side
+// stream: no cross-queue dependency inside the captured graph (each such edge cost 5-11 us of idle
+// time in the step timeline, profiles/r3_cnn_kernel_tuning.txt), and the dispatcher hands out the
+// lower workgroup ranges first, so the pieces listed first start first.  Piece ranges are padded to
+// multiples of 8 so every piece keeps its own XCD-aware tile order.
+struct GlGroupArgs {
+  DenseGemmArgs g0, g1;
+  HeadWgradArgs h;
+  int nh, n0, n1;      // padded workgroup ranges
+  int th, t0, t1;      // real workgroups of each piece
+};
+
+template <int AM0, int BM0, int AM1, int BM1>
+__global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_group_kernel(GlGroupArgs ga) {
+  constexpr int HEAD_BYTES = 4 * 80 * 4;
+  constexpr int BYTES = GlSmem<64, 64, 2>::BYTES > HEAD_BYTES ? GlSmem<64, 64, 2>::BYTES : HEAD_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem_raw[BYTES];
+  int bid = blockIdx.x;
+  if (bid < ga.nh) {
+    if (bid < ga.th) head_wgrad_body<10, 4>(ga.h, bid, reinterpret_cast<float(*)[80]>(smem_raw));
+    return;
+  }
+  bid -= ga.nh;
+  if (bid < ga.n0) {
+    if (bid < ga.t0) gemm_glds_body<64, 64, AM0, BM0, 2>(ga.g0, bid, smem_raw);
+    return;
+  }
+  bid -= ga.n0;
+  if (bid < ga.t1) gemm_glds_body<64, 64, AM1, BM1, 2>(ga.g1, bid, smem_raw);
+}
+
+namespace {
+struct GlGroupRec {
+  bool active = false;
+  int ng = 0, am[2] = {0, 0}, bm[2] = {0, 0};
+  DenseGemmArgs g[2];
+  bool has_h = false;
+  HeadWgradArgs h;
+};
+thread_local GlGroupRec g_group;
+int pad8(int n) { return (n + 7) / 8 * 8; }
+}  // namespace
+
+void glds_group_begin() {
+  if (g_group.active) throw std::runtime_error("gemm group: already recording");
+  g_group = GlGroupRec();
+  g_group.active = true;
+}
+
+bool glds_group_record(int amode, int bmode, const DenseGemmArgs& a) {
+  if (!g_group.active || g_group.ng == 2) return false;
+  if (!gemm_glds_eligible(0, amode, bmode, 12, a)) return false;
+  g_group.am[g_group.ng] = amode;
+  g_group.bm[g_group.ng] = bmode;
+  g_group.g[g_group.ng++] = a;
+  return true;
+}
+
+bool glds_group_record_head(const HeadWgradArgs& a) {
+  if (!g_group.active || g_group.has_h || a.B > 1024) return false;
+  g_group.has_h = true;
+  g_group.h = a;
+  return true;
+}
+
+void glds_group_end(hipStream_t s) {
+  if (!g_group.active) throw std::runtime_error("gemm group: not recording");
+  GlGroupRec r = g_group;
+  g_group = GlGroupRec();
+  const bool fused = r.ng == 2 && r.am[0] == KMAJ && r.bm[0] == RMAJ && r.am[1] == RMAJ && r.bm[1] == RMAJ;
+  if (!fused) {  // any other combination: the pieces as separate launches, in recording order
+    if (r.has_h) launch_head_wgrad(r.h, s);
+    for (int i = 0; i < r.ng; ++i) launch_gemm_dense(0, r.am[i], r.bm[i], 12, 1, r.g[i], s);
+    return;
+  }
+  GlGroupArgs ga;
+  std::memset(&ga, 0, sizeof(ga));
+  ga.g0 = r.g[0];
+  ga.g1 = r.g[1];
+  if (r.has_h) {
+    ga.h = r.h;
+    ga.th = r.h.K / 8 + (r.h.db ? 1 : 0);
+    ga.nh = pad8(ga.th);
+  }
+  ga.t0 = (ga.g0.M / 64) * ((ga.g0.N + 63) / 64);
+  ga.t1 = (ga.g1.M / 64) * ((ga.g1.N + 63) / 64);
+  ga.n0 = pad8(ga.t0);
+  ga.n1 = ga.t1;
+  hipLaunchKernelGGL((gemm_glds_group_kernel<KMAJ, RMAJ, RMAJ, RMAJ>), dim3(ga.nh + ga.n0 + ga.n1), dim3(GEMM_THREADS), 0,
+                     s, ga);
 }
 
 }  // namespace dtfe

@@ -96,17 +96,17 @@ template <int BM, int BN, int STAGES> struct GlSmem {
   static constexpr int BYTES = STAGING > CTILE ? STAGING : CTILE;
 };
 
+// One output tile (workgroup `bid` of this GEMM's grid); smem_raw: GlSmem<BM, BN, STAGES>::BYTES of LDS.
+// Shared by the plain launch below and the grouped launch (gemm_glds_group_kernel).
 template <int BM, int BN, int AMODE, int BMODE, int STAGES>
-__global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_kernel(DenseGemmArgs a) {
+__device__ __forceinline__ void gemm_glds_body(const DenseGemmArgs& a, int bid, char* smem_raw) {
   using Cfg = TileCfg<bf16, BM, BN, 2, 2, GL_BK>;
   using OA = GlOperand<BM, AMODE>;
   using OB = GlOperand<BN, BMODE>;
   constexpr int NPT = OA::NP + OB::NP;  // DMA instructions per thread and k-tile
   using SM = GlSmem<BM, BN, STAGES>;
-  __shared__ __attribute__((aligned(16))) char smem_raw[SM::BYTES];
   bf16* smem = reinterpret_cast<bf16*>(smem_raw);
 
-  const int bid = blockIdx.x;
   const int tiles_m = a.M / BM, tiles_n = (a.N + BN - 1) / BN;
   int tm, tn;
   tile_coords(bid, tiles_m, tiles_n, tm, tn);
@@ -175,6 +175,12 @@ __global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_kernel(DenseGemmArg
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the staging LDS for the C tile
   dense_epilogue<Cfg>(a, smem_raw, acc, tm, tn, tiles_m, tiles_n);
+}
+
+template <int BM, int BN, int AMODE, int BMODE, int STAGES>
+__global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_kernel(DenseGemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[GlSmem<BM, BN, STAGES>::BYTES];
+  gemm_glds_body<BM, BN, AMODE, BMODE, STAGES>(a, blockIdx.x, smem_raw);
 }
 
 }  // namespace dtfe

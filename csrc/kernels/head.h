@@ -1,6 +1,7 @@
 #pragma once
 #include "common.h"
 #include <stdexcept>
+#include <type_traits>
 
 namespace dtfe {
 
@@ -31,5 +32,75 @@ struct HeadWgradArgs {
   float scale;
 };
 void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s);
+
+// Workgroup `bid` (256 threads) of the head weight gradient: columns 8*bid..+7 of dW for the whole
+// batch (bid == K/8: the bias); red: 4 x 80 floats of LDS.  See head.hip.
+template <int NC, int ROWS>
+__device__ __forceinline__ void head_wgrad_body(const HeadWgradArgs& a, int bid, float (*red)[NC * 8]) {
+  static_assert(NC * 8 == 80, "the butterfly below is laid out for 10 classes x 8 columns");
+  constexpr int V = NC * 8;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool bias_blk = bid * 8 >= a.K;
+  const int col0 = bid * 8;
+  u32x4_t hv[ROWS], d0[ROWS], d1[ROWS];
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) {
+    const int b = t + 256 * i;
+    const bool ok = b < a.B;
+    hv[i] = (ok && !bias_blk) ? *reinterpret_cast<const u32x4_t*>(a.h + (long)b * a.ldh + col0) : u32x4_t{0u, 0u, 0u, 0u};
+    d0[i] = ok ? *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl) : u32x4_t{0u, 0u, 0u, 0u};
+    d1[i] = ok ? *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl + 8) : u32x4_t{0u, 0u, 0u, 0u};
+  }
+  float v[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) v[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) {
+    float h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = bias_blk ? ((t + 256 * i) < a.B ? 1.f : 0.f) : bf2f((bf16)(hv[i][e >> 1] >> (16 * (e & 1))));
+#pragma unroll
+    for (int n = 0; n < NC; ++n) {
+      const uint32_t w = n < 8 ? d0[i][n >> 1] : d1[i][(n - 8) >> 1];
+      const float d = bf2f((bf16)(w >> (16 * (n & 1))));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[n * 8 + e] = fmaf(d, h[e], v[n * 8 + e]);
+    }
+  }
+  // halving butterfly over lane bits 5..2: 80 -> 40 -> 20 -> 10 -> 5 values per lane
+  auto halve = [&](auto half_c, int mask) {
+    constexpr int H = decltype(half_c)::value;
+    const bool hi = (lane & mask) != 0;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const float send = hi ? v[j] : v[H + j];
+      const float keep = hi ? v[H + j] : v[j];
+      v[j] = keep + __shfl_xor(send, mask, 64);
+    }
+  };
+  halve(std::integral_constant<int, 40>{}, 32);
+  halve(std::integral_constant<int, 20>{}, 16);
+  halve(std::integral_constant<int, 10>{}, 8);
+  halve(std::integral_constant<int, 5>{}, 4);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    v[j] += __shfl_xor(v[j], 2, 64);
+    v[j] += __shfl_xor(v[j], 1, 64);
+  }
+  // lane holds values ((b5 ? 40 : 0) + (b4 ? 20 : 0) + (b3 ? 10 : 0) + (b2 ? 5 : 0) + j)
+  if ((lane & 3) == 0) {
+    const int base = ((lane >> 5) & 1) * 40 + ((lane >> 4) & 1) * 20 + ((lane >> 3) & 1) * 10 + ((lane >> 2) & 1) * 5;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) red[wid][base + j] = v[j];
+  }
+  __syncthreads();
+  if (t < V) {
+    const float s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    const int n = t >> 3, e = t & 7;
+    if (!bias_blk) a.dw[(long)n * a.ldw + col0 + e] = s * a.scale;
+    else if (e == 0) a.db[n] = s * a.scale;
+  }
+}
+
 
 }  // namespace dtfe

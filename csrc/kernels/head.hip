@@ -15,6 +15,7 @@
 // (SURVEY K01/K02/K07).
 #include "common.h"
 #include "head.h"
+#include "gemm_dense.h"
 
 #include <type_traits>
 
@@ -137,75 +138,14 @@ namespace dtfe {
 // output - took ~11 us on the MNIST step's critical path.)
 template <int NC, int ROWS>
 __global__ __launch_bounds__(256) void head_wgrad_kernel(HeadWgradArgs a) {
-  static_assert(NC * 8 == 80, "the butterfly below is laid out for 10 classes x 8 columns");
-  constexpr int V = NC * 8;
-  __shared__ float red[4][V];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const bool bias_blk = blockIdx.x * 8 >= a.K;
-  const int col0 = blockIdx.x * 8;
-  u32x4_t hv[ROWS], d0[ROWS], d1[ROWS];
-#pragma unroll
-  for (int i = 0; i < ROWS; ++i) {
-    const int b = t + 256 * i;
-    const bool ok = b < a.B;
-    hv[i] = (ok && !bias_blk) ? *reinterpret_cast<const u32x4_t*>(a.h + (long)b * a.ldh + col0) : u32x4_t{0u, 0u, 0u, 0u};
-    d0[i] = ok ? *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl) : u32x4_t{0u, 0u, 0u, 0u};
-    d1[i] = ok ? *reinterpret_cast<const u32x4_t*>(a.dl + (long)b * a.ld_dl + 8) : u32x4_t{0u, 0u, 0u, 0u};
-  }
-  float v[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) v[j] = 0.f;
-#pragma unroll
-  for (int i = 0; i < ROWS; ++i) {
-    float h[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = bias_blk ? ((t + 256 * i) < a.B ? 1.f : 0.f) : bf2f((bf16)(hv[i][e >> 1] >> (16 * (e & 1))));
-#pragma unroll
-    for (int n = 0; n < NC; ++n) {
-      const uint32_t w = n < 8 ? d0[i][n >> 1] : d1[i][(n - 8) >> 1];
-      const float d = bf2f((bf16)(w >> (16 * (n & 1))));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[n * 8 + e] = fmaf(d, h[e], v[n * 8 + e]);
-    }
-  }
-  // halving butterfly over lane bits 5..2: 80 -> 40 -> 20 -> 10 -> 5 values per lane
-  auto halve = [&](auto half_c, int mask) {
-    constexpr int H = decltype(half_c)::value;
-    const bool hi = (lane & mask) != 0;
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const float send = hi ? v[j] : v[H + j];
-      const float keep = hi ? v[H + j] : v[j];
-      v[j] = keep + __shfl_xor(send, mask, 64);
-    }
-  };
-  halve(std::integral_constant<int, 40>{}, 32);
-  halve(std::integral_constant<int, 20>{}, 16);
-  halve(std::integral_constant<int, 10>{}, 8);
-  halve(std::integral_constant<int, 5>{}, 4);
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    v[j] += __shfl_xor(v[j], 2, 64);
-    v[j] += __shfl_xor(v[j], 1, 64);
-  }
-  // lane holds values ((b5 ? 40 : 0) + (b4 ? 20 : 0) + (b3 ? 10 : 0) + (b2 ? 5 : 0) + j)
-  if ((lane & 3) == 0) {
-    const int base = ((lane >> 5) & 1) * 40 + ((lane >> 4) & 1) * 20 + ((lane >> 3) & 1) * 10 + ((lane >> 2) & 1) * 5;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) red[wid][base + j] = v[j];
-  }
-  __syncthreads();
-  if (t < V) {
-    const float s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-    const int n = t >> 3, e = t & 7;
-    if (!bias_blk) a.dw[(long)n * a.ldw + col0 + e] = s * a.scale;
-    else if (e == 0) a.db[n] = s * a.scale;
-  }
+  __shared__ float red[4][NC * 8];
+  head_wgrad_body<NC, ROWS>(a, blockIdx.x, red);
 }
 
 void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s) {
   if (a.NC != 10 || a.K % 8 || a.ld_dl < 16 || a.ld_dl % 8 || a.ldh % 8 || a.B > 1024)
     throw std::runtime_error("head_wgrad: needs NC=10, K % 8 == 0, 16-B aligned dl rows of >= 16 and h rows, B <= 1024");
+  if (glds_group_record_head(a)) return;  // recorded into a grouped launch (gemm_dense.hip)
   const int blocks = a.K / 8 + (a.db ? 1 : 0);
   if (a.B <= 256) hipLaunchKernelGGL((head_wgrad_kernel<10, 1>), dim3(blocks), dim3(256), 0, s, a);
   else if (a.B <= 512) hipLaunchKernelGGL((head_wgrad_kernel<10, 2>), dim3(blocks), dim3(256), 0, s, a);

@@ -222,6 +222,8 @@ class MnistCnnTrainer:
         # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
         # 2-stage variant (784 / 800 tiles, several workgroups per CU)
         self.glds = self.device.type == "cuda" and os.environ.get("DTFE_CNN_GLDS", "1") != "0"
+        # DTFE_CNN_FC_GROUP=0: the fc backward as a forked side branch instead of one grouped launch
+        self.fc_group = self.par and os.environ.get("DTFE_CNN_FC_GROUP", "1") != "0"
         K1 = 7 * 7 * C2
         # DTFE_CNN_TILES=fwd,dgrad,wgrad overrides the glds tile ids (A/B sweeps)
         tiles = [int(t) for t in os.environ.get("DTFE_CNN_TILES", "8,12,12").split(",")]
@@ -277,15 +279,25 @@ class MnistCnnTrainer:
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep,
                       step_counter=self.data_ctr if fused else None)
         main = torch.cuda.current_stream(self.device) if self.par else None
-        # weight-gradient branch of the fc layers (forked after head_xent), then the dgrad chain
-        with self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext():
-            self._head_wgrad()
-            # fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column
-            ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
-                     bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
+        if self.fc_group:
+            # head weight gradient + fc1 data gradient + fc1 weight gradient as ONE launch on the main
+            # stream (ops.gemm_group): no fork / join of an fc side branch, whose cross-queue edges
+            # cost 5-11 us of idle time each in the captured graph; the dispatcher starts the head and
+            # data-gradient workgroups first (lower grid ranges)
+            with ops.gemm_group(self.dzf):
+                self._head_wgrad()
+                self._fc1_dgrad(B, K1)
+                self._fc1_wgrad(B, K1)
             if self.allreduce is not None:
-                self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
-        self._fc1_dgrad(B, K1)
+                self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes)
+        else:
+            # weight-gradient branch of the fc layers (forked after head_xent), then the dgrad chain
+            with self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext():
+                self._head_wgrad()
+                self._fc1_wgrad(B, K1)
+                if self.allreduce is not None:
+                    self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
+            self._fc1_dgrad(B, K1)
         def conv2_wgrad():
             with self._branch(self.s_c2, main) if self.br_c2 else contextlib.nullcontext():
                 # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
@@ -298,7 +310,7 @@ class MnistCnnTrainer:
         conv2_wgrad()
         self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
-        if self.br_fc:  # join the weight-grad branches
+        if self.br_fc and not self.fc_group:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
         if self.br_c2:
             main.wait_stream(self.s_c2)
@@ -320,6 +332,11 @@ class MnistCnnTrainer:
                      splits=self.head_splits, tile=4, workspace=self.ws_head)
         else:
             ops.head_wgrad(self.dl, self.h, self.gw["out"], self.gw["bout"], NCLS)  # B <= 1024
+
+    def _fc1_wgrad(self, B, K1):
+        """fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column."""
+        ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC,
+                 bmode=ops.RMAJ, ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"], tile=self.t_wgrad)
 
     def _fc1_dgrad(self, B, K1):
         """fc1 dgrad -> dP2 at pooled resolution, ReLU'(P2)-masked (consumers un-pool on load)."""

@@ -9,6 +9,7 @@ distributed machinery, and as the fp32 oracle the kernel tests compare to.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -25,7 +26,7 @@ __all__ = [
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "shortcut_grad_add",
-    "gap_fwd", "gap_bwd", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
+    "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -523,7 +524,7 @@ def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0
 
 def head_wgrad(dl, h, dw, db, nc, scale=1.0):
     """Classifier-head weight / bias gradient, stored: dw[c][:K] = scale * sum_b dl[b][c] h[b][:],
-    db[c] = scale * sum_b dl[b][c] (one workgroup per 16 columns over the whole batch, fixed order)."""
+    db[c] = scale * sum_b dl[b][c] (one workgroup per 8 columns over the whole batch, fixed order)."""
     if h.is_cuda:
         require().head_wgrad(dl, h, dw, db, nc, scale)
         return
@@ -531,6 +532,23 @@ def head_wgrad(dl, h, dw, db, nc, scale=1.0):
     dw[:, : h.shape[1]] = (scale * (d.t() @ h.float())).to(dw.dtype)
     if db is not None:
         db.copy_((scale * d.sum(0)).to(db.dtype))
+
+
+@contextlib.contextmanager
+def gemm_group(anchor):
+    """Grouped launch: the head_wgrad and glds-tile-12 one-split gemm calls inside the block are
+    recorded and leave as ONE kernel launch at its end (head weight gradient, then the
+    (KMAJ, RMAJ) and (RMAJ, RMAJ) GEMMs in recording order; any other mix launches one by one).
+    CPU tensors: a no-op (the ops run eagerly)."""
+    if not anchor.is_cuda:
+        yield
+        return
+    lib = require()
+    lib.gemm_group(anchor, True)
+    try:
+        yield
+    finally:
+        lib.gemm_group(anchor, False)
 
 
 # --------------------------------------------------------------- optimizer

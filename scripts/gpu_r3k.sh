@@ -1,6 +1,6 @@
 # fc1 GEMM memory-path PMC: TLB (UTCL1) hit/miss, L2 read latency, TA/TCP stalls.
 set -o pipefail
-O=gpurun_out/r3k
+O=${O:-gpurun_out/r3k}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 i=0
