@@ -58,6 +58,8 @@ def main():
                                             relu_mask=t.p1, flip_taps=True, **t.ic2_dgrad), conv2_flops),
         "conv2_wgrad": (lambda: ops.imgwgrad(t.p1, t.gw["wc2"], t.gw["bc2"], dy_pooled=t.dp2, dy_argmax=t.a2,
                                              **t.ic2), conv2_flops),
+        "conv2_wgrad_ws": (lambda: ops.imgwgrad(t.p1, t.gw["wc2"], t.gw["bc2"], dy_pooled=t.dp2, dy_argmax=t.a2,
+                                                workspace=t.ws_c2, max_blocks=t.c2_blocks, **t.ic2), conv2_flops),
         "conv1_wgrad": (lambda: ops.imgwgrad(t.x, t.gw["wc1"], t.gw["bc1"], dy_pooled=t.dp1, dy_argmax=t.a1,
                                              **t.ic1), 2.0 * B * 784 * 32 * 25),
         "conv1_wgrad_old": (lambda: ops.conv1_wgrad_pooled(t.x, t.dp1, t.a1, t.gw["wc1"], t.gw["bc1"]),
