@@ -16,7 +16,7 @@ def _mat(t, mode, rows, K):
     return t.float() if mode == ops.KMAJ else t.float().t()
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7, 8, 9, 12])
+@pytest.mark.parametrize("tile", [5, 6, 7, 8, 9, 12, 14, 15, 16, 17, 18])
 @pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("splits", [1, 3])
 def test_glds_gemm_layouts(tile, modes, splits):
@@ -82,3 +82,38 @@ def test_glds_fc1_dgrad_and_wgrad():
         ref_b = dz.float().sum(0)
         assert (gw - ref_w).abs().max().item() < 1e-4 * ref_w.abs().max().item() + 1e-3, (tile, splits)
         assert (gb - ref_b).abs().max().item() < 1e-4 * ref_b.abs().max().item() + 1e-3, (tile, splits)
+
+
+def test_gemm_group_matches_separate_launches():
+    """ops.gemm_group: the head weight gradient + fc1 data gradient + fc1 weight gradient recorded
+    and launched as ONE grid give bitwise the results of the three separate launches."""
+    B_, K1, FC, NC = 1024, 3136, 1024, 10
+    g = torch.Generator(device="cuda").manual_seed(3)
+    dz = torch.randn(B_, FC, device="cuda", generator=g).to(bf)
+    w1 = (torch.randn(FC, K1, device="cuda", generator=g) * 0.02).to(bf)
+    p2 = torch.relu(torch.randn(B_, K1, device="cuda", generator=g)).to(bf)
+    h = torch.relu(torch.randn(B_, FC, device="cuda", generator=g)).to(bf)
+    dl = torch.zeros(B_, 16, device="cuda", dtype=bf)
+    dl[:, :NC] = (torch.randn(B_, NC, device="cuda", generator=g) / B_).to(bf)
+
+    def run(grouped):
+        dp2 = torch.full((B_, K1), float("nan"), device="cuda").to(bf)
+        gw = torch.full((FC, K1), float("nan"), device="cuda")
+        gb = torch.full((FC,), float("nan"), device="cuda")
+        hw = torch.full((NC, FC), float("nan"), device="cuda")
+        hb = torch.full((NC,), float("nan"), device="cuda")
+        ctx = ops.gemm_group(dz) if grouped else __import__("contextlib").nullcontext()
+        with ctx:
+            ops.head_wgrad(dl, h, hw, hb, NC)
+            ops.gemm(dz, w1, dp2, M=B_, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=p2, aux_act=ops.ACT_RELU, tile=12)
+            ops.gemm(dz, p2, gw, M=FC, N=K1 + 1, K=B_, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ, ldb=K1, ldc=K1,
+                     b_ones_row=K1, bias_out=gb, tile=12)
+        torch.cuda.synchronize()
+        return dp2, gw, gb, hw, hb
+
+    sep, grp = run(False), run(True)
+    for a, b in zip(sep, grp):
+        assert not torch.isnan(b.float()).any()
+        assert torch.equal(a, b)
+    ref = (dz.float() @ w1.float()) * (p2.float() > 0)
+    assert (grp[0].float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
