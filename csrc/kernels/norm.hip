@@ -118,7 +118,10 @@ __device__ __forceinline__ long res_offset(const BnArgs& a, long r, int chunk, b
 // INFER: TF inference mode - (x - moving_mean) * rsqrt(moving_variance + eps), nothing updated.
 // (A runtime flag in the training kernel's channel setup made hipcc unswitch and re-shape the row
 // loop: bn_apply 53 -> 123 us per ResNet-50 call.  The two modes are separate instantiations.)
-template <bool INFER>
+// ACTC: the activation as a compile-time constant (ACT_NONE / ACT_RELU), or -1 for the runtime a.act;
+// RES: a residual source is given.  (The runtime forms of both put a branch on every value of the
+// row loop: 2.4k static VALU instructions against ~0.8k for the ReLU / residual instance.)
+template <bool INFER, int ACTC, bool RES>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
   const Slots S(a.C);
   if (!INFER && blockIdx.x == 0) {  // saved statistics + moving averages (TF: unbiased batch variance)
@@ -149,8 +152,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
     scale[e] = a.gamma[c] * invstd;
     shift[e] = a.beta[c] - mean * scale[e];
   }
-  const bool res_identity = a.res && a.rstride == 1 && a.RC == a.C && a.RH == a.OH && a.RW == a.OW;
-  const bool res_chunk = a.res && S.chunk * 8 < a.RC;
+  const bool res_identity = RES && a.rstride == 1 && a.RC == a.C && a.RH == a.OH && a.RW == a.OW;
+  const bool res_chunk = RES && S.chunk * 8 < a.RC;
   const long step = (long)gridDim.x * S.rpp * U_APPLY;
   for (long r0 = (long)blockIdx.x * S.rpp * U_APPLY + S.slot; r0 < a.R; r0 += step) {
     u32x4_t v[U_APPLY], w[U_APPLY];
@@ -175,21 +178,30 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
         for (int e = 0; e < 8; ++e) f[e] += g[e];
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e], a.act);
+      for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e], ACTC >= 0 ? ACTC : a.act);
       if (r < a.R) *reinterpret_cast<u32x4_t*>(a.out + r * a.C + S.chunk * 8) = pack8(f);
     }
   }
 }
 
-// Backward activation mask source.  With a.y the mask is act'(y) of the stored output; with
-// a.y == nullptr and act == ReLU (no residual was added in the forward) it is recomputed from
-// x as (gamma*invstd*x + (beta - mean*gamma*invstd)) > 0 - bit-identical to the forward's
-// pre-activation (same fma on the same saved statistics) and one tensor read cheaper.
+// Backward activation mask, as a compile-time mode MM (the runtime form branched on every value):
+//   MM_NONE  no activation: g = dy
+//   MM_X     ReLU recomputed from x as (gamma*invstd*x + (beta - mean*gamma*invstd)) > 0 - bit-identical
+//            to the forward's pre-activation (same fma on the same saved statistics), one tensor read
+//            cheaper (y == nullptr)
+//   MM_YRELU ReLU mask from the stored output y (a residual was added before the ReLU)
+//   MM_YACT  act'(y) of the stored output for the runtime a.act (sigmoid / tanh)
+enum { MM_NONE = 0, MM_X = 1, MM_YRELU = 2, MM_YACT = 3 };
+
+__host__ __device__ inline int mask_mode(const BnArgs& a) {
+  if (a.act == ACT_NONE) return MM_NONE;
+  if (a.y == nullptr && a.act == ACT_RELU) return MM_X;
+  return a.act == ACT_RELU ? MM_YRELU : MM_YACT;
+}
+
 struct BwdMask {
   float scale[8], shift[8];
-  bool from_x;
-  __device__ BwdMask(const BnArgs& a, int chunk) {
-    from_x = a.y == nullptr && a.act == ACT_RELU;
+  __device__ BwdMask(const BnArgs& a, int chunk, bool from_x) {
     if (from_x) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -202,13 +214,19 @@ struct BwdMask {
 };
 
 // g = dy * act'(.) for 8 channels, from loaded dy / y / x chunks
+template <int MM>
 __device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, const u32x4_t dyv, const u32x4_t yv,
                                             const float (&x)[8], float (&g)[8]) {
   unpack8(dyv, g);
-  if (M.from_x) {
+  if constexpr (MM == MM_X) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = (x[e] * M.scale[e] + M.shift[e]) > 0.f ? g[e] : 0.f;
-  } else if (a.act != ACT_NONE) {
+  } else if constexpr (MM == MM_YRELU) {
+    float y[8];
+    unpack8(yv, y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= y[e] > 0.f ? 1.f : 0.f;  // = act_grad_from_out(y, ReLU), bit for bit
+  } else if constexpr (MM == MM_YACT) {
     float y[8];
     unpack8(yv, y);
 #pragma unroll
@@ -216,10 +234,11 @@ __device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, c
   }
 }
 
+template <int MM>
 __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   const Slots S(a.C);
-  const BwdMask M(a, S.chunk);
-  const bool need_y = a.act != ACT_NONE && !M.from_x;
+  const BwdMask M(a, S.chunk, MM == MM_X);
+  constexpr bool need_y = MM == MM_YRELU || MM == MM_YACT;
   float mean[8], invstd[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -243,7 +262,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
       const float live = (r0 + (long)u * S.rpp) < a.R ? 1.f : 0.f;
       float g[8], x[8];
       unpack8(xv[u], x);
-      masked_grad(a, M, dv[u], yv[u], x, g);
+      masked_grad<MM>(a, M, dv[u], yv[u], x, g);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float gl = g[e] * live;
@@ -255,6 +274,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   reduce_stats(s, q, a.C, a.stats);
 }
 
+template <int MM>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
   const Slots S(a.C);
   if (blockIdx.x == 0) {
@@ -263,8 +283,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
       if (a.dgamma) a.dgamma[c] += a.stats[a.C + c];
     }
   }
-  const BwdMask M(a, S.chunk);
-  const bool need_y = a.act != ACT_NONE && !M.from_x;
+  const BwdMask M(a, S.chunk, MM == MM_X);
+  constexpr bool need_y = MM == MM_YRELU || MM == MM_YACT;
   const float inv_r = 1.f / (float)a.R;
   float mean[8], invstd[8], k[8], sg[8], sgx[8];
 #pragma unroll
@@ -294,7 +314,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
       const long off = r * a.C + S.chunk * 8;
       float g[8], x[8], dx[8];
       unpack8(xv[u], x);
-      masked_grad(a, M, dv[u], yv[u], x, g);
+      masked_grad<MM>(a, M, dv[u], yv[u], x, g);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (x[e] - mean[e]) * invstd[e];
@@ -506,8 +526,24 @@ void launch_bn_apply(const BnArgs& a, hipStream_t s) {
   check(a);
   if (a.infer && (!a.moving_mean || !a.moving_var)) throw std::runtime_error("bn_apply: inference needs the moving averages");
   if (a.res && (a.RC % 8 || a.RC > a.C)) throw std::runtime_error("bn_apply: residual channels");
-  if (a.infer) hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(a.R, a.C)), dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(a.R, a.C)), dim3(NT), 0, s, a);
+  const dim3 g(apply_grid(a.R, a.C)), b(NT);
+  const bool res = a.res != nullptr;
+  const int act = a.act == ACT_NONE || a.act == ACT_RELU ? a.act : -1;
+#define BN_APPLY(INF, ACT)                                                              \
+  do {                                                                                  \
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<INF, ACT, true>), g, b, 0, s, a);      \
+    else hipLaunchKernelGGL((bn_apply_kernel<INF, ACT, false>), g, b, 0, s, a);         \
+  } while (0)
+  if (a.infer) {
+    if (act == ACT_RELU) BN_APPLY(true, ACT_RELU);
+    else if (act == ACT_NONE) BN_APPLY(true, ACT_NONE);
+    else BN_APPLY(true, -1);
+  } else {
+    if (act == ACT_RELU) BN_APPLY(false, ACT_RELU);
+    else if (act == ACT_NONE) BN_APPLY(false, ACT_NONE);
+    else BN_APPLY(false, -1);
+  }
+#undef BN_APPLY
 }
 
 void check_bwd(const BnArgs& a) {
@@ -519,12 +555,24 @@ void check_bwd(const BnArgs& a) {
 void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s) {
   check_bwd(a);
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
-  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(stats_grid(a.R, a.C)), dim3(NT), lds, s, a);
+  const dim3 g(stats_grid(a.R, a.C)), b(NT);
+  switch (mask_mode(a)) {
+    case MM_NONE: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_NONE>, g, b, lds, s, a); break;
+    case MM_X: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_X>, g, b, lds, s, a); break;
+    case MM_YRELU: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_YRELU>, g, b, lds, s, a); break;
+    default: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_YACT>, g, b, lds, s, a); break;
+  }
 }
 
 void launch_bn_bwd_apply(const BnArgs& a, hipStream_t s) {
   check_bwd(a);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(apply_grid(a.R, a.C)), dim3(NT), 0, s, a);
+  const dim3 g(apply_grid(a.R, a.C)), b(NT);
+  switch (mask_mode(a)) {
+    case MM_NONE: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_NONE>, g, b, 0, s, a); break;
+    case MM_X: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_X>, g, b, 0, s, a); break;
+    case MM_YRELU: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_YRELU>, g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_YACT>, g, b, 0, s, a); break;
+  }
 }
 
 void launch_shortcut_grad_add(const bf16* g, bf16* dx, int B, int OH, int OW, int C, int XH, int XW, int XC,
