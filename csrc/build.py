@@ -14,6 +14,11 @@ Objects are cached under build/obj keyed by a hash of (source, headers, flags),
 so rebuilds only recompile what changed.  Usage:
 
     python csrc/build.py [--only kernels|rt] [-j N] [--verbose]
+    python csrc/build.py --ab REV FILE...    # A/B library: FILEs (csrc/kernels/*.hip) taken from git REV
+
+The A/B build writes distributed-tensorflow-examples_amd/_C/ab/libdtfe_kernels.so (same bindings, the listed kernel sources as of
+REV); DTFE_KERNEL_LIB=<that path> makes a process load it instead, so two code versions can be
+timed alternately in one process pool on one GPU box (box-to-box spread is ~3 %).
 """
 from __future__ import annotations
 
@@ -77,7 +82,7 @@ def _compile(src, flags, compiler, verbose):
     return obj
 
 
-def build_kernels(jobs: int, verbose: bool) -> str:
+def build_kernels(jobs: int, verbose: bool, ab_rev: str | None = None, ab_files=()) -> str:
     inc, libdir = _torch_paths()
     os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
@@ -86,19 +91,33 @@ def build_kernels(jobs: int, verbose: bool) -> str:
     bflags = common + ["-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__", "-DTORCH_EXTENSION_NAME=dtfe"] + ["-I" + p for p in inc]
     kern_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     bind_srcs = sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp")))
+    out_lib = KERNEL_LIB
+    if ab_rev:
+        ab_dir = os.path.join(OUT_DIR, "ab")  # in-tree (travels with the gpurun snapshot; git-ignored)
+        os.makedirs(os.path.join(ROOT, "build", "ab_src"), exist_ok=True)
+        os.makedirs(ab_dir, exist_ok=True)
+        for f in ab_files:
+            rel = os.path.relpath(os.path.abspath(f), ROOT)
+            txt = subprocess.run(["git", "-C", ROOT, "show", "%s:%s" % (ab_rev, rel)], check=True,
+                                 stdout=subprocess.PIPE).stdout
+            dst = os.path.join(ROOT, "build", "ab_src", os.path.basename(rel))
+            with open(dst, "wb") as fh:
+                fh.write(txt)
+            kern_srcs = [dst if os.path.abspath(k) == os.path.abspath(f) else k for k in kern_srcs]
+        out_lib = os.path.join(ab_dir, "libdtfe_kernels.so")
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, kflags, HIPCC, verbose) for s in kern_srcs]
         futs += [ex.submit(_compile, s, bflags + ["-x", "hip"], HIPCC, verbose) for s in bind_srcs]
         objs = [f.result() for f in futs]
-    link = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", KERNEL_LIB + ".tmp"] + objs + [
+    link = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", out_lib + ".tmp"] + objs + [
         "-L" + libdir, "-Wl,-rpath," + libdir,
         "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip",
         # RCCL: the librccl torch ships (same soname torch already loaded), for bindings/comm_ops.cpp
         "-lrccl",
     ]
     _run(link, verbose)
-    os.replace(KERNEL_LIB + ".tmp", KERNEL_LIB)
-    return KERNEL_LIB
+    os.replace(out_lib + ".tmp", out_lib)
+    return out_lib
 
 
 def build_runtime(jobs: int, verbose: bool) -> str:
@@ -131,7 +150,12 @@ def main():
     ap.add_argument("--only", choices=["kernels", "rt"], default=None)
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--ab", nargs="+", metavar=("REV", "FILE"), default=None,
+                    help="A/B library: kernel sources FILE... as of git REV -> _C/ab/libdtfe_kernels.so")
     a = ap.parse_args()
+    if a.ab:
+        print("built", build_kernels(a.j, a.verbose, a.ab[0], a.ab[1:]))
+        return
     for p in build(a.only, a.j, a.verbose):
         print("built", p)
 

@@ -115,22 +115,23 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
     // deterministic split-K: partial tile -> ws[z][tile], the last split to arrive sums in split order
     const int tile = tm * tiles_n + tn, ntiles = tiles_m * tiles_n;
     float* mine = a.ws + ((long)blockIdx.z * ntiles + tile) * (Cfg::BM * Cfg::BN);
+    // hand-off (MI355X guide, split-K counter form with write-through slabs): the slab leaves in
+    // 16-B sc1 (write-through) buffer stores, every wave drains them, barrier, ONE lane takes a
+    // ticket with a relaxed agent-scope add - no release fence (an agent-scope release writes the
+    // XCD's dirty L2 lines back; one per split workgroup made the MNIST fc1 split-K GEMMs 2-4x
+    // SLOWER than no split, profiles/r2_fc1_gemm_sweep.txt); the last arriver acquires once and
+    // reads every slab.
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(mine, (short)0, Cfg::BM * Cfg::BN * 4, 0x00020000);
     for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
       const int r = ch / CPR, c = (ch % CPR) * 8;
-      f32x4_t* dst = reinterpret_cast<f32x4_t*>(mine + ch * 8);
-      dst[0] = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c);
-      dst[1] = *reinterpret_cast<const f32x4_t*>(Cs + r * CLD + c + 4);
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c), slab, ch * 32, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c + 4), slab, ch * 32 + 16, 0,
+                                             16);
     }
-    // hand-off (MI355X guide, split-K counter form): plain slab stores -> every wave waits for
-    // them -> barrier -> ONE lane releases at agent scope and takes a ticket; the last arriver
-    // acquires once and reads every slab.  A __threadfence() in every thread instead costs
-    // microseconds per workgroup and serialises the whole grid.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem_raw);  // the one LDS array (Cs is free here)
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int prev = __hip_atomic_fetch_add(a.tile_ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == (int)gridDim.z - 1;
       if (last) {

@@ -137,15 +137,19 @@ struct GlGroupArgs {
   int th, t0, t1;      // real workgroups of each piece
 };
 
-template <int AM0, int BM0, int AM1, int BM1>
+// HEAD: the head piece is compiled in (its 10x8 accumulators per thread set the register allocation
+// to ~148 VGPRs; without it the grouped kernel keeps the GEMMs' ~68)
+template <int AM0, int BM0, int AM1, int BM1, bool HEAD>
 __global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_group_kernel(GlGroupArgs ga) {
   constexpr int HEAD_BYTES = 4 * 80 * 4;
   constexpr int BYTES = GlSmem<64, 64, 2>::BYTES > HEAD_BYTES ? GlSmem<64, 64, 2>::BYTES : HEAD_BYTES;
   __shared__ __attribute__((aligned(16))) char smem_raw[BYTES];
   int bid = blockIdx.x;
-  if (bid < ga.nh) {
-    if (bid < ga.th) head_wgrad_body<10, 4>(ga.h, bid, reinterpret_cast<float(*)[80]>(smem_raw));
-    return;
+  if constexpr (HEAD) {
+    if (bid < ga.nh) {
+      if (bid < ga.th) head_wgrad_body<10, 4>(ga.h, bid, reinterpret_cast<float(*)[80]>(smem_raw));
+      return;
+    }
   }
   bid -= ga.nh;
   if (bid < ga.n0) {
@@ -213,8 +217,12 @@ void glds_group_end(hipStream_t s) {
   ga.t1 = (ga.g1.M / 64) * ((ga.g1.N + 63) / 64);
   ga.n0 = pad8(ga.t0);
   ga.n1 = ga.t1;
-  hipLaunchKernelGGL((gemm_glds_group_kernel<KMAJ, RMAJ, RMAJ, RMAJ>), dim3(ga.nh + ga.n0 + ga.n1), dim3(GEMM_THREADS), 0,
-                     s, ga);
+  if (r.has_h)
+    hipLaunchKernelGGL((gemm_glds_group_kernel<KMAJ, RMAJ, RMAJ, RMAJ, true>), dim3(ga.nh + ga.n0 + ga.n1),
+                       dim3(GEMM_THREADS), 0, s, ga);
+  else
+    hipLaunchKernelGGL((gemm_glds_group_kernel<KMAJ, RMAJ, RMAJ, RMAJ, false>), dim3(ga.n0 + ga.n1), dim3(GEMM_THREADS),
+                       0, s, ga);
 }
 
 }  // namespace dtfe

@@ -26,10 +26,20 @@
 #include "imgconv.h"
 
 #include <stdexcept>
+#include <type_traits>
 
 namespace dtfe {
 
 namespace {
+
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for_c(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for_c<B + 1, E>(f);
+  }
+}
 
 struct WPGeom {
   int LH, LW;       // LDS source extent (pixels), row pitch = LW
@@ -175,6 +185,21 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     for (int j = 0; j < CTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float dbacc[MT] = {};
 
+  auto tr2 = [](const bf16* p0, const bf16* p1) {
+    const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p0));
+    const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p1));
+    const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  auto load_a = [&](int s, bf16x8_t (&af)[MT]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      af[mt] = tr2(dimg + s * dstep + doff[0] + mt * 16, dimg + s * dstep + doff[1] + mt * 16);
+  };
+  auto load_b = [&](int s, int c) {
+    return tr2(simg + s * sstep + koff[0] + coff[c], simg + s * sstep + koff[1] + coff[c]);
+  };
+
   long b = blockIdx.x;
   if (b < a.B) load_img(b);
   __syncthreads();
@@ -182,38 +207,46 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     if (!(a.diag & 2) || b == blockIdx.x) write_img();
     __syncthreads();
     if (b + gridDim.x < a.B && !(a.diag & 2)) load_img(b + gridDim.x);
-    for (int s = 0; s < ((a.diag & 4) ? 0 : G.nk); ++s) {
-      bf16x8_t af[MT];
+    // Software-pipelined k loop: every wave runs all CTW column tiles (a dead tile - past the
+    // weight's columns - reads a valid pixel and is never flushed; on MNIST conv2 only wave 7 has
+    // dead tiles and its SIMD partner wave 3 keeps that SIMD at the 14-tile load of the others), so
+    // the tile loop is straight-line and its reads can be pinned AHEAD of their MFMAs: column tile
+    // c+1's B fragment and step s+1's A fragments are in flight while tile c's MFMAs run.  (The
+    // data-dependent `break` at the live-tile count made the scheduler wait on each tile's two
+    // transposing reads right before its 4 MFMAs: rocprof ablation, 37.7 of the 57.7 us launch in
+    // the MFMA loop at ~56 % MFMA utilisation.)
+    const int nk = (a.diag & 4) ? 0 : G.nk;
+    if (nk > 0) {
+      bf16x8_t a_cur[MT], a_nxt[MT], b_cur = load_b(0, 0);
+      load_a(0, a_cur);
+      for (int s = 0; s < nk; ++s) {
+        const int sn = s + 1 < nk ? s + 1 : s;  // the last step re-reads its own fragments (unused)
+        static_for_c<0, CTW>([&](auto cc) {
+          constexpr int c = decltype(cc)::value;
+          bf16x8_t b_nxt;
+          if constexpr (c + 1 < CTW) b_nxt = load_b(s, c + 1);
+          else b_nxt = load_b(sn, 0);
+          if constexpr (c == 0) load_a(sn, a_nxt);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4_t, dimg + s * dstep + doff[0] + mt * 16));
-        const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4_t, dimg + s * dstep + doff[1] + mt * 16));
-        const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        af[mt] = __builtin_bit_cast(bf16x8_t, v);
-      }
-      if (wid == 0) {  // bias gradient from the dY fragments (wave-uniform branch)
+          for (int mt = 0; mt < MT; ++mt)
+            acc[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur[mt], b_cur, acc[mt][c], 0, 0, 0);
+          // reads issued ahead of this tile's MFMAs (c == 0: B of tile 1 + the next step's A)
+          __builtin_amdgcn_sched_group_barrier(0x100, c == 0 ? 2 + 2 * MT : 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x8, MT, 0);
+          b_cur = b_nxt;
+        });
+        if (wid == 0) {  // bias gradient from this step's dY fragments (wave-uniform branch)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const s16x8_t v = __builtin_bit_cast(s16x8_t, af[mt]);
-          float sum = 0.f;
+          for (int mt = 0; mt < MT; ++mt) {
+            const s16x8_t v = __builtin_bit_cast(s16x8_t, a_cur[mt]);
+            float sum = 0.f;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) sum += bf2f((bf16)v[e]);
-          dbacc[mt] += sum;
+            for (int e = 0; e < 8; ++e) sum += bf2f((bf16)v[e]);
+            dbacc[mt] += sum;
+          }
         }
-      }
 #pragma unroll
-      for (int c = 0; c < CTW; ++c) {
-        if (c >= nct) break;  // wave-uniform
-        const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4_t, simg + s * sstep + koff[0] + coff[c]));
-        const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4_t, simg + s * sstep + koff[1] + coff[c]));
-        const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr, acc[mt][c], 0, 0, 0);
+        for (int mt = 0; mt < MT; ++mt) a_cur[mt] = a_nxt[mt];
       }
     }
     __syncthreads();

@@ -230,6 +230,12 @@ class MnistCnnTrainer:
         self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, tiles[0])
         self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, tiles[1])
         self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, tiles[2], b_ones_row=K1)
+        # fc1 forward split-K (deterministic last-arriver combine, write-through slabs): more
+        # workgroups per CU keep more global->LDS loads in flight (bench/probe/glds_probe.hip)
+        self.fwd_splits = int(os.environ.get("DTFE_CNN_FWD_SPLITS", "1"))
+        self.ws_fwd = None
+        if self.fwd_splits > 1 and self.t_fwd is not None:
+            self.ws_fwd = ops.split_workspace(d, self.fwd_splits, B, FC, self.t_fwd, private=True)
         # head weight gradient: split-K over the batch with the deterministic last-arriver combine
         # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
         # workspace, since it runs on the fc branch beside other GEMMs
@@ -274,18 +280,21 @@ class MnistCnnTrainer:
                     pool=True, **self.ic2)
         K1 = 7 * 7 * C2
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
-                 keep=self.keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd)
+                 keep=self.keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd, splits=self.fwd_splits,
+                 workspace=self.ws_fwd)
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
                       self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep,
                       step_counter=self.data_ctr if fused else None)
         main = torch.cuda.current_stream(self.device) if self.par else None
         if self.fc_group:
-            # head weight gradient + fc1 data gradient + fc1 weight gradient as ONE launch on the main
+            # fc1 data gradient + fc1 weight gradient as ONE launch on the main
             # stream (ops.gemm_group): no fork / join of an fc side branch, whose cross-queue edges
             # cost 5-11 us of idle time each in the captured graph; the dispatcher starts the head and
             # data-gradient workgroups first (lower grid ranges)
+            # (the head piece stays its own launch: its 10x8 accumulators per thread would set the
+            # grouped kernel's register allocation to 148 VGPRs, 3 workgroups per CU instead of 7)
+            self._head_wgrad()
             with ops.gemm_group(self.dzf):
-                self._head_wgrad()
                 self._fc1_dgrad(B, K1)
                 self._fc1_wgrad(B, K1)
             if self.allreduce is not None:

@@ -68,14 +68,19 @@ _WS = {}
 _WS_RETIRED = []
 
 
-def split_workspace(device, splits, M, N, tile):
+def split_workspace(device, splits, M, N, tile, private=False):
     """(ws, tile_ctr) for a split-K GEMM with a fused epilogue: fp32 partial tiles
     [splits][tiles][BM*BN] + per-tile arrival counters (zeroed once; the kernel
     resets them).  Cached per device and grown on demand - callers that run
-    split-K GEMMs concurrently on several streams must pass their own."""
+    split-K GEMMs concurrently on several streams must pass their own
+    (``private=True``: a fresh pair, not the shared cache)."""
     bm, bn = TILE_DIMS[tile]
     ntiles = math.ceil(M / bm) * math.ceil(N / bn)
     need = splits * ntiles * bm * bn
+    if private:
+        key = torch.device(device)
+        return (torch.empty(need, device=key, dtype=torch.float32),
+                torch.zeros(ntiles, device=key, dtype=torch.int32))
     key = torch.device(device)
     ws, ctr = _WS.get(key, (None, None))
     if ws is None or ws.numel() < need or ctr.numel() < ntiles:

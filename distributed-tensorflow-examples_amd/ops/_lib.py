@@ -12,7 +12,9 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C")
-KERNEL_LIB = os.path.join(_LIB_DIR, "libdtfe_kernels.so")
+# DTFE_KERNEL_LIB: load another build of the kernel library (csrc/build.py --ab: A/B of two code
+# versions in one session on one GPU box)
+KERNEL_LIB = os.environ.get("DTFE_KERNEL_LIB") or os.path.join(_LIB_DIR, "libdtfe_kernels.so")
 
 _lock = threading.Lock()
 _loaded = False
