@@ -230,8 +230,8 @@ class MnistCnnTrainer:
         self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, tiles[0])
         self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, tiles[1])
         self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, tiles[2], b_ones_row=K1)
-        # fc1 forward split-K (deterministic last-arriver combine, write-through slabs): more
-        # workgroups per CU keep more global->LDS loads in flight (bench/probe/glds_probe.hip)
+        # fc1 forward split-K (deterministic last-arriver combine, write-through slabs): A/B only -
+        # 2 and 3 splits measured 1-2 % slower per step (profiles/r3_cnn_kernel_tuning.txt)
         self.fwd_splits = int(os.environ.get("DTFE_CNN_FWD_SPLITS", "1"))
         self.ws_fwd = None
         if self.fwd_splits > 1 and self.t_fwd is not None:
