@@ -98,4 +98,25 @@ bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s);
 void launch_partials_reduce(const float* ws, int nblk, int len, int nw, float* dw, float* db, float scale,
                             hipStream_t s);
 
+
+// Un-pooling of one 16-B pooled chunk (8 bf16 channels) with its 8 argmax bytes (each 0..3: the
+// position in the 2x2 window): out[q] = the chunk with every channel whose argmax != q zeroed.  The
+// 2-bit argmax codes give the four byte masks with 2 bit-ops each and v_perm_b32 widens a byte mask
+// to the two bytes of its bf16 lane - ~50 VALU for the 4 quadrants against ~160 for the per-word
+// xor / compare / select form (rocprof ablation: the un-pooled dY image was a third of the MNIST conv1
+// weight-gradient launch).
+__device__ __forceinline__ void unpool4(const u32x4_t pv, const u32x2_t am, u32x4_t (&out)[4]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t lo = am[h] & 0x01010101u, hi = (am[h] >> 1) & 0x01010101u;
+    const uint32_t m[4] = {((lo | hi) ^ 0x01010101u) * 0xFFu, (lo & ~hi) * 0xFFu, (hi & ~lo) * 0xFFu,
+                           (lo & hi) * 0xFFu};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      out[q][2 * h] = pv[2 * h] & __builtin_amdgcn_perm(0u, m[q], 0x01010000u);
+      out[q][2 * h + 1] = pv[2 * h + 1] & __builtin_amdgcn_perm(0u, m[q], 0x03030202u);
+    }
+  }
+}
+
 }  // namespace dtfe

@@ -216,18 +216,12 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
       const int i = threadIdx.x + j * TH;
       if (i >= PCH) continue;
       const int win = i >> 2, c8 = (i & 3) * 8, py = win / 14, px = win - py * 14;
+      u32x4_t v[4];
+      unpool4(pv[j], pam[j], v);
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
-        u32x4_t v;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {  // keep bf16 element e where argmax byte e == qq
-          const uint32_t x = (pam[j][w >> 1] ^ ((uint32_t)qq * 0x01010101u)) >> (16 * (w & 1));
-          const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
-          const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
-          v[w] = pv[j][w] & (lo_ok | hi_ok);
-        }
         const int oy = 2 * py + (qq >> 1), ox = 2 * px + (qq & 1);
-        *reinterpret_cast<u32x4_t*>(D + (oy * 32 + ox) * DP + c8) = v;
+        *reinterpret_cast<u32x4_t*>(D + (oy * 32 + ox) * DP + c8) = v[qq];
       }
     }
   };

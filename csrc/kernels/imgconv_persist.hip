@@ -169,18 +169,11 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
       if (!POOLED) {
         *reinterpret_cast<u32x4_t*>(img + dst[j]) = pf[j];
       } else {
+        u32x4_t v[4];
+        unpool4(pf[j], pam[j], v);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          u32x4_t v;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {  // keep bf16 element e where argmax byte e == q
-            const uint32_t x = (pam[j][w >> 1] ^ ((uint32_t)q * 0x01010101u)) >> (16 * (w & 1));
-            const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
-            const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
-            v[w] = pf[j][w] & (lo_ok | hi_ok);
-          }
-          *reinterpret_cast<u32x4_t*>(img + dst[j] + ((q >> 1) * LWP + (q & 1)) * PS) = v;
-        }
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<u32x4_t*>(img + dst[j] + ((q >> 1) * LWP + (q & 1)) * PS) = v[q];
       }
     }
   };
@@ -383,18 +376,11 @@ __global__ __launch_bounds__(64 * WM) void imgconv_fixed_kernel(ImgConvArgs a, P
       if (!POOLED) {
         *reinterpret_cast<u32x4_t*>(img + dst[j]) = pf[j];
       } else {
+        u32x4_t v[4];
+        unpool4(pf[j], pam[j], v);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          u32x4_t v;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const uint32_t x = (pam[j][w >> 1] ^ ((uint32_t)q * 0x01010101u)) >> (16 * (w & 1));
-            const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
-            const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
-            v[w] = pf[j][w] & (lo_ok | hi_ok);
-          }
-          *reinterpret_cast<u32x4_t*>(img + dst[j] + ((q >> 1) * LWP + (q & 1)) * PS) = v;
-        }
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<u32x4_t*>(img + dst[j] + ((q >> 1) * LWP + (q & 1)) * PS) = v[q];
       }
     }
   };

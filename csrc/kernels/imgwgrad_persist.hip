@@ -140,18 +140,11 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
       if (!POOLED) {
         *reinterpret_cast<u32x4_t*>(dimg + ddst[j]) = dreg[j];
       } else {
+        u32x4_t v[4];
+        unpool4(dreg[j], dam[j], v);
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          u32x4_t v;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const uint32_t x = (dam[j][w >> 1] ^ ((uint32_t)qq * 0x01010101u)) >> (16 * (w & 1));
-            const uint32_t lo_ok = (x & 0xffu) == 0u ? 0x0000ffffu : 0u;
-            const uint32_t hi_ok = (x & 0xff00u) == 0u ? 0xffff0000u : 0u;
-            v[w] = dreg[j][w] & (lo_ok | hi_ok);
-          }
-          *reinterpret_cast<u32x4_t*>(dimg + ddst[j] + ((qq >> 1) * G.OWP + (qq & 1)) * NPS) = v;
-        }
+        for (int qq = 0; qq < 4; ++qq)
+          *reinterpret_cast<u32x4_t*>(dimg + ddst[j] + ((qq >> 1) * G.OWP + (qq & 1)) * NPS) = v[qq];
       }
     }
   };
