@@ -51,14 +51,15 @@ __device__ __forceinline__ float update_one(const OptArgs& a, float lr_t, long i
   return v;
 }
 
+template <bool G16>
 __device__ __forceinline__ float load_grad(const OptArgs& a, long i) {
-  return (a.g ? a.g[i] : bf2f(a.g16[i])) * a.gscale;
+  return (G16 ? bf2f(a.g16[i]) : a.g[i]) * a.gscale;
 }
 
-template <int KIND>
+template <int KIND, bool G16>
 __device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i, bf16* w16) {
   f32x4_t g;
-  if (a.g) {
+  if constexpr (!G16) {
     g = *reinterpret_cast<const f32x4_t*>(a.g + i);
   } else {
     const u32x2_t w = *reinterpret_cast<const u32x2_t*>(a.g16 + i);
@@ -84,13 +85,13 @@ __device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i
 
 // U vec4 updates at i, i+1024, ... (one workgroup-wide stride apart): every load is issued
 // before the first update, so each thread keeps U x (3-4) 16-B loads in flight
-template <int KIND, int U>
+template <int KIND, int U, bool G16>
 __device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long i, bf16* w16) {
   f32x4_t g[U], p[U], s1[U], s2[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const long k = i + u * 1024;
-    if (a.g) {
+    if constexpr (!G16) {
       g[u] = *reinterpret_cast<const f32x4_t*>(a.g + k);
     } else {
       const u32x2_t w = *reinterpret_cast<const u32x2_t*>(a.g16 + k);
@@ -121,8 +122,8 @@ __device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long 
 
 // One optimizer's share of a launch: workgroups bid = 0..nblk-1 of the grid (the whole grid for a
 // plain launch, a contiguous range of it for a grouped one).
-template <int KIND>
-__device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, bf16 (&tile)[64][66]) {
+template <int KIND, bool G16>
+__device__ __forceinline__ void apply_items(const OptArgs& a, int bid, int nblk, bf16 (&tile)[64][66]) {
   float lr_t = a.lr;
   if (KIND == OPT_ADAM) lr_t = tf1_adam_lr(a.lr, a.beta_pow);
   for (int wi = bid; wi < a.nwork; wi += nblk) {
@@ -133,12 +134,12 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
       const long n4 = ((base & 3) == 0) ? (w.count / 4) * 4 : 0;  // segments are 64-aligned; chunks 8192
       long j = threadIdx.x * 4;
       for (; j + 3 * 1024 < n4; j += 4 * 1024)  // 4 independent vec4 updates in flight per thread
-        update_vec4x<KIND, 4>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
+        update_vec4x<KIND, 4, G16>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
       for (; j < n4; j += 256 * 4)
-        update_vec4<KIND>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
+        update_vec4<KIND, G16>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
       for (long j = n4 + threadIdx.x; j < w.count; j += 256) {
         const long li = w.start + j, i = sg.off + li;
-        const float v = update_one<KIND>(a, lr_t, i, load_grad(a, i));
+        const float v = update_one<KIND>(a, lr_t, i, load_grad<G16>(a, i));
         if (sg.w16) sg.w16[li] = f2bf(v);
       }
     } else {
@@ -151,12 +152,13 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int r = w.r0 + ty + 4 * u;
+        // out-of-tile lanes load the segment's first element (never stored): no branches here
         const bool ok = r < sg.R && c < sg.C;
         const long i = sg.off + (ok ? ((long)r * sg.T + w.t) * sg.C + c : 0);
-        gv[u] = ok ? load_grad(a, i) : 0.f;
-        pv[u] = ok ? a.p[i] : 0.f;
-        s1v[u] = (ok && KIND != OPT_SGD) ? a.s1[i] : 0.f;
-        s2v[u] = (ok && (KIND == OPT_ADAM || KIND == OPT_RMSPROP)) ? a.s2[i] : 0.f;
+        gv[u] = load_grad<G16>(a, i);
+        pv[u] = a.p[i];
+        s1v[u] = KIND != OPT_SGD ? a.s1[i] : 0.f;
+        s2v[u] = (KIND == OPT_ADAM || KIND == OPT_RMSPROP) ? a.s2[i] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -181,6 +183,12 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
       __syncthreads();
     }
   }
+}
+
+template <int KIND>
+__device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, bf16 (&tile)[64][66]) {
+  if (a.g) apply_items<KIND, false>(a, bid, nblk, tile);
+  else apply_items<KIND, true>(a, bid, nblk, tile);
   // last workgroup: advance the non-slot scalars.  Every thread read them at its start and
   // used the value; after the barrier one lane takes a ticket (relaxed agent atomics - nothing
   // is handed between workgroups, so no fences) and the last arriver updates them.

@@ -218,6 +218,11 @@ class MnistCnnTrainer:
         # ~45 us/step slower - its traffic contends with the persistent conv2 backward kernels -
         # and was removed: profiles/r3_cnn_fused_adam_ab.txt)
         self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
+        # One replica, DTFE_CNN_BRANCH_APPLY=1: no Adam after the join.  The fc/head + conv2 Adam
+        # (one grouped launch; their gradients are final once the grouped fc backward launch and
+        # conv2's weight gradient are done) ends the conv2 weight-gradient branch, beside conv1's
+        # weight gradient; conv1's Adam ends the main chain.
+        self.branch_apply = os.environ.get("DTFE_CNN_BRANCH_APPLY", "0") == "1"
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
         # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
         # 2-stage variant (784 / 800 tiles, several workgroups per CU)
@@ -313,12 +318,17 @@ class MnistCnnTrainer:
                 ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
                              workspace=self.ws_c2 if self.br_c2 else None,
                              max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
+                if self._apply is not None and self._apply[0] == "branch":
+                    Optimizer.step_all([self.opt_fc, self.opt_c2], [0, 0], grad16=self._apply[1],
+                                       gscale=self._apply[2])
 
         # (forking conv2's weight gradient after its data gradient, beside conv1's weight gradient,
         # measured 0.242 vs 0.233 ms/step: profiles/r3_cnn_c2_after_ab.txt)
         conv2_wgrad()
         self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
+        if self._apply is not None and self._apply[0] == "branch":
+            self.opt_c1.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
         if self.br_fc and not self.fc_group:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
         if self.br_c2:
@@ -329,7 +339,7 @@ class MnistCnnTrainer:
                 self.allreduce.wait_bucket(0)   # fc/head Adam overlaps the conv bucket's all-reduce
                 self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
             self.allreduce.wait()
-        if self._apply is not None:
+        if self._apply is not None and self._apply[0] == "late":
             self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
 
     def _head_wgrad(self):
@@ -366,6 +376,11 @@ class MnistCnnTrainer:
             self.opt_conv = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2", "wc1", "bc1")],
                                       global_step=self.global_step)
             self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
+            # branch-apply split of the conv optimizer: conv2 (its branch) and conv1 (main chain)
+            self.opt_c2 = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2")], global_step=self.global_step)
+            self.opt_c1 = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc1", "bc1")], global_step=self.global_step)
+            for o in (self.opt_c2, self.opt_c1):
+                o.s1, o.s2 = self.opt_fc.s1, self.opt_fc.s2
 
     @staticmethod
     def _branch(stream, main):
@@ -385,6 +400,8 @@ class MnistCnnTrainer:
         mode = None
         if self.par and self.br_fc and self.late_split and self.allreduce is not None:
             mode = "late"
+        elif self.br_c2 and self.fc_group and self.branch_apply and self.allreduce is None:
+            mode = "branch"
         if mode is None or (self.opt_fc is None and self.global_step_started()):
             self.forward_backward()
             self.opt.step(grad16=grad16, gscale=gscale)
