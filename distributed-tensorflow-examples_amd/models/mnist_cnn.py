@@ -218,10 +218,10 @@ class MnistCnnTrainer:
         # ~45 us/step slower - its traffic contends with the persistent conv2 backward kernels -
         # and was removed: profiles/r3_cnn_fused_adam_ab.txt)
         self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
-        # One replica, DTFE_CNN_BRANCH_APPLY=1: no Adam after the join.  The fc/head + conv2 Adam
-        # (one grouped launch; their gradients are final once the grouped fc backward launch and
-        # conv2's weight gradient are done) ends the conv2 weight-gradient branch, beside conv1's
-        # weight gradient; conv1's Adam ends the main chain.
+        # One replica, DTFE_CNN_BRANCH_APPLY=1 (A/B knob, measured no faster): the fc/head Adam (its
+        # gradients are final once the grouped fc backward launch is done, its weights' last reader
+        # is that launch) ends the conv2 weight-gradient branch; the conv Adam stays after the join
+        # (conv2's weights are still read by conv2's data gradient on the main chain).
         self.branch_apply = os.environ.get("DTFE_CNN_BRANCH_APPLY", "0") == "1"
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
         # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
@@ -319,16 +319,13 @@ class MnistCnnTrainer:
                              workspace=self.ws_c2 if self.br_c2 else None,
                              max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
                 if self._apply is not None and self._apply[0] == "branch":
-                    Optimizer.step_all([self.opt_fc, self.opt_c2], [0, 0], grad16=self._apply[1],
-                                       gscale=self._apply[2])
+                    self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
 
         # (forking conv2's weight gradient after its data gradient, beside conv1's weight gradient,
         # measured 0.242 vs 0.233 ms/step: profiles/r3_cnn_c2_after_ab.txt)
         conv2_wgrad()
         self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
-        if self._apply is not None and self._apply[0] == "branch":
-            self.opt_c1.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
         if self.br_fc and not self.fc_group:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
         if self.br_c2:
@@ -339,7 +336,7 @@ class MnistCnnTrainer:
                 self.allreduce.wait_bucket(0)   # fc/head Adam overlaps the conv bucket's all-reduce
                 self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
             self.allreduce.wait()
-        if self._apply is not None and self._apply[0] == "late":
+        if self._apply is not None:
             self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
 
     def _head_wgrad(self):
@@ -376,11 +373,6 @@ class MnistCnnTrainer:
             self.opt_conv = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2", "wc1", "bc1")],
                                       global_step=self.global_step)
             self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
-            # branch-apply split of the conv optimizer: conv2 (its branch) and conv1 (main chain)
-            self.opt_c2 = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2")], global_step=self.global_step)
-            self.opt_c1 = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc1", "bc1")], global_step=self.global_step)
-            for o in (self.opt_c2, self.opt_c1):
-                o.s1, o.s2 = self.opt_fc.s1, self.opt_fc.s2
 
     @staticmethod
     def _branch(stream, main):
