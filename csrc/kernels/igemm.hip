@@ -389,16 +389,13 @@ __device__ __forceinline__ bf16x8_t wg_frag(const bf16* img, int rbase, int kk, 
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// NST LDS stages: 2 = tile t+1 in flight while tile t computes; 3 = tiles t+1 and t+2 (the wait at
-// the top of an iteration leaves the newer tile's DMA outstanding - counted vmcnt)
-template <int BM, int BN, int NST, int MINB>  // BM output channels x BN input channels of one tap
-__global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgWgradArgs a, float* dw, float scale) {
+template <int BM, int BN>  // BM output channels x BN input channels of one tap
+__global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgradArgs a, float* dw, float scale) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_EL = 64 * BM, B_EL = 64 * BN;
   constexpr int CPA = BM / 8, RPA = 64 / CPA, NA = BM / 32;  // chunks per m-row, m-rows per piece
   constexpr int CPB = BN / 8, RPB = 64 / CPB, NB = BN / 32;
-  static_assert(NST == 2 || NST == 3, "2 or 3 stages");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NST * (A_EL + B_EL)];
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -463,13 +460,11 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgW
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) issue(0, 0);
-  if (NST == 3 && nk > 1) issue(1, 1);
   for (int t = 0; t < nk; ++t) {
-    if (NST == 3 && t + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile t visible to every wave; every wave is done with tile t - 1's buffer
-    if (t + NST - 1 < nk) issue(t + NST - 1, (t + NST - 1) % NST);
-    const bf16* As = smem + (t % NST) * (A_EL + B_EL);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+    const bf16* As = smem + (t & 1) * (A_EL + B_EL);
     const bf16* Bs = As + A_EL;
 #pragma unroll
     for (int kk = 0; kk < 64; kk += 32) {
@@ -1084,21 +1079,10 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   const long len = (long)g.Cout * g.KH * g.KW * g.C;
   if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s, g_wg);
   dim3 grid((unsigned)tiles, sp);
-  // DTFE_IGW_NST=3: three LDS stages (128x128: 96 KB, one workgroup per CU; the others two per CU)
-  static const int nst = env_int("DTFE_IGW_NST", 2);
-#define IGW(BM_, BN_, NST_, MINB_) hipLaunchKernelGGL((igemm_wgrad_kernel<BM_, BN_, NST_, MINB_>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale)
-  if (nst == 3) {
-    if (bm == 128 && bn == 128) IGW(128, 128, 3, 1);
-    else if (bm == 128) IGW(128, 64, 3, 2);
-    else if (bn == 128) IGW(64, 128, 3, 2);
-    else IGW(64, 64, 3, 2);
-  } else {
-    if (bm == 128 && bn == 128) IGW(128, 128, 2, 2);
-    else if (bm == 128) IGW(128, 64, 2, 2);
-    else if (bn == 128) IGW(64, 128, 2, 2);
-    else IGW(64, 64, 2, 2);
-  }
-#undef IGW
+  if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else if (bm == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else if (bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<64, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else hipLaunchKernelGGL((igemm_wgrad_kernel<64, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
   if (sp > 1)
     hipLaunchKernelGGL(wgrad_splits_reduce_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws, sp,
                        len, f.dw, f.scale);

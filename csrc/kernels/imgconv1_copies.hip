@@ -159,41 +159,8 @@ __global__ __launch_bounds__(TH) void conv1c_fwd_kernel(ImgConvArgs a) {
 
 // ------------------------------------------------------------ weight grad
 constexpr int DP = NCH;  // dY image pitch (elements per pixel)
-// fused partial-sum reduce: workgroups in groups of C1W_G; the last arriver of a group sums the
-// group's partials (in workgroup order) into a group slab, the last group to finish sums the group
-// slabs (in group order) into dW / db.  Hand-offs as the split-K GEMM combine (gemm_dense.h):
-// write-through (sc1) slab stores, drained, ONE relaxed agent-scope ticket per workgroup, an
-// acquire in the last arriver only.  Tickets reset by their last arriver (graph replays); one
-// conv1 weight-gradient launch in flight per device.
-constexpr int C1W_G = 16, C1W_MAXG = 64;
-__device__ unsigned c1w_tickets[C1W_MAXG + 1];
 
-__device__ __forceinline__ void c1w_store(float* base, int i4, const f32x4_t& v, int bytes) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, i4 * 16, 0, 16);
-}
-
-// returns true in every thread of the workgroup that took the last ticket of `ctr` (of `n`)
-__device__ __forceinline__ bool c1w_ticket(unsigned* ctr, unsigned n, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == n - 1;
-    if (last) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  const bool last = *flag != 0;
-  __syncthreads();
-  return last;
-}
-
-__global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int diag, int fused) {
+__global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int diag) {
   __shared__ __attribute__((aligned(16))) bf16 P[PRW * PWD];
   __shared__ __attribute__((aligned(16))) bf16 C[5 * CSZ];
   __shared__ __attribute__((aligned(16))) bf16 D[HI * 32 * DP];  // dY [oy][ox < 32][n]
@@ -316,41 +283,6 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
   // flush: dW[n][tap] (tap < 25) and db[n]; one partial per workgroup (summed by the reduce
   // kernel) or, without a workspace, scaled atomics
   constexpr int KC = 25, LEN = NCH * KC + NCH;
-  if (a.ws && fused) {  // two-level last-arriver reduce (launch_conv1_copies_wgrad)
-    static_assert(LEN % 4 == 0, "float4 slabs");
-    constexpr int L4 = LEN / 4;
-    __shared__ int flag;
-    const int nblk = gridDim.x, ngrp = (nblk + C1W_G - 1) / C1W_G, grp = blockIdx.x / C1W_G;
-    const int g0 = grp * C1W_G, gn = min(C1W_G, nblk - g0);
-    for (int i = threadIdx.x; i < L4; i += TH) {
-      f32x4_t v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 4 * i + e, r = k < NCH * KC ? (k / KC) * 32 + (k % KC) : 32 * 32 + (k - NCH * KC);
-        v[e] = ((red[r] + red[RL + r]) + red[2 * RL + r]) + red[3 * RL + r];
-      }
-      c1w_store(a.ws + (long)blockIdx.x * LEN, i, v, LEN * 4);
-    }
-    if (!c1w_ticket(c1w_tickets + grp, gn, &flag)) return;
-    float* gslab = a.ws + (long)(nblk + grp) * LEN;
-    for (int i = threadIdx.x; i < L4; i += TH) {
-      f32x4_t v = *reinterpret_cast<const f32x4_t*>(a.ws + (long)g0 * LEN + 4 * i);
-      for (int k = 1; k < gn; ++k) v += *reinterpret_cast<const f32x4_t*>(a.ws + (long)(g0 + k) * LEN + 4 * i);
-      c1w_store(gslab, i, v, LEN * 4);
-    }
-    if (!c1w_ticket(c1w_tickets + C1W_MAXG, ngrp, &flag)) return;
-    for (int i = threadIdx.x; i < L4; i += TH) {
-      f32x4_t t = *reinterpret_cast<const f32x4_t*>(a.ws + (long)nblk * LEN + 4 * i);
-      for (int g2 = 1; g2 < ngrp; ++g2) t += *reinterpret_cast<const f32x4_t*>(a.ws + (long)(nblk + g2) * LEN + 4 * i);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 4 * i + e;
-        if (k < NCH * KC) a.dw[k] += a.scale * t[e];
-        else if (a.db) a.db[k - NCH * KC] += a.scale * t[e];
-      }
-    }
-    return;
-  }
   float* part = a.ws ? a.ws + (long)blockIdx.x * LEN : nullptr;
   for (int i = threadIdx.x; i < LEN; i += TH) {
     const int r = i < NCH * KC ? (i / KC) * 32 + (i % KC) : 32 * 32 + (i - NCH * KC);
@@ -399,22 +331,10 @@ bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s) {
     const char* e = getenv("DTFE_C1W_DIAG");
     return e ? atoi(e) : 0;
   }();
-  // DTFE_C1W_FUSED_REDUCE=0: the partial sums by a second kernel instead of the in-kernel
-  // two-level last-arriver reduce
-  static const bool fused = [] {
-    const char* e = getenv("DTFE_C1W_FUSED_REDUCE");
-    return !e || atoi(e) != 0;
-  }();
   const int grid = a.B < want ? a.B : (want < 1 ? 1 : want);
-  constexpr long LEN = NCH * 25 + NCH;
-  if (a.ws && (long)grid * LEN > imgwgrad_ws_floats(NCH, 25))
+  if (a.ws && (long)grid * (NCH * 25 + NCH) > imgwgrad_ws_floats(NCH, 25))
     throw std::runtime_error("conv1 wgrad: partials exceed the workspace");
-  const int ngrp = (grid + C1W_G - 1) / C1W_G;
-  if (a.ws && fused && ngrp <= C1W_MAXG && (long)(grid + ngrp) * LEN <= imgwgrad_ws_floats(NCH, 25)) {
-    hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a, diag, 1);
-    return true;
-  }
-  hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a, diag, 0);
+  hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a, diag);
   if (a.ws) {
     constexpr int LEN = NCH * 25 + NCH;
     launch_partials_reduce(a.ws, grid, LEN, NCH * 25, a.dw, a.db, a.scale, s);
