@@ -208,7 +208,12 @@ class MnistCnnTrainer:
         self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2"})
         self.br_fc = self.par and "fc" in br
         self.br_c2 = self.par and "c2" in br
-        self.c2_blocks = int(os.environ.get("DTFE_CNN_C2_BLOCKS", "128"))
+        # conv2's data gradient is captured before its weight gradient (same fork point): the graph
+        # runs the data gradient -> conv1 weight-gradient chain on the launch queue, first on the
+        # CUs, and the weight gradient (192 workgroups) fills in beside it - 0.2103-0.2126 vs
+        # 0.2159-0.2181 ms/step (profiles/r3_cnn_kernel_tuning.txt, r3y / r3z)
+        self.dgrad_first = os.environ.get("DTFE_CNN_DGRAD_FIRST", "1") == "1"
+        self.c2_blocks = int(os.environ.get("DTFE_CNN_C2_BLOCKS", "192" if self.dgrad_first else "128"))
         # Data-parallel "late split" (default whenever an all-reduce is attached): the fc/head Adam
         # (bucket 0, already reduced during the conv backward) runs while the small conv bucket's
         # all-reduce is still in flight, so that collective's latency hides behind ~20 us of Adam.
@@ -218,11 +223,14 @@ class MnistCnnTrainer:
         # ~45 us/step slower - its traffic contends with the persistent conv2 backward kernels -
         # and was removed: profiles/r3_cnn_fused_adam_ab.txt)
         self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
-        # One replica, DTFE_CNN_BRANCH_APPLY=1 (A/B knob, measured no faster): the fc/head Adam (its
-        # gradients are final once the grouped fc backward launch is done, its weights' last reader
-        # is that launch) ends the conv2 weight-gradient branch; the conv Adam stays after the join
-        # (conv2's weights are still read by conv2's data gradient on the main chain).
-        self.branch_apply = os.environ.get("DTFE_CNN_BRANCH_APPLY", "0") == "1"
+        # One replica, DTFE_CNN_FC_APPLY (where the fc/head Adam runs; its gradients are final once
+        # the grouped fc backward launch is done and that launch is its weights' last reader):
+        #   "join" - the whole-model Adam after the conv2 weight-gradient branch joins;
+        #   "main" - on the main chain after conv1's weight gradient, before the join (its ~18 us
+        #            hide the join's cross-queue wait), the conv Adam after the join;
+        #   "c2"   - at the end of the conv2 weight-gradient branch, the conv Adam after the join.
+        # (conv2's Adam can not move onto the branch: conv2's data gradient still reads its weights)
+        self.fc_apply = os.environ.get("DTFE_CNN_FC_APPLY", "join")
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
         # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
         # 2-stage variant (784 / 800 tiles, several workgroups per CU)
@@ -312,20 +320,32 @@ class MnistCnnTrainer:
                 if self.allreduce is not None:
                     self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
             self._fc1_dgrad(B, K1)
-        def conv2_wgrad():
-            with self._branch(self.s_c2, main) if self.br_c2 else contextlib.nullcontext():
+        def conv2_wgrad(forked=False):
+            ctx = contextlib.nullcontext()
+            if self.br_c2:
+                ctx = torch.cuda.stream(self.s_c2) if forked else self._branch(self.s_c2, main)
+            with ctx:
                 # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
                 ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
                              workspace=self.ws_c2 if self.br_c2 else None,
                              max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
-                if self._apply is not None and self._apply[0] == "branch":
+                if self._apply is not None and self._apply[0] == "c2":
                     self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
 
         # (forking conv2's weight gradient after its data gradient, beside conv1's weight gradient,
         # measured 0.242 vs 0.233 ms/step: profiles/r3_cnn_c2_after_ab.txt)
-        conv2_wgrad()
-        self._conv2_dgrad()
+        if self.dgrad_first and self.br_c2:
+            # fork point unchanged (after the fc backward); the data gradient's graph node is
+            # captured before the weight gradient's
+            self.s_c2.wait_stream(main)
+            self._conv2_dgrad()
+            conv2_wgrad(forked=True)
+        else:
+            conv2_wgrad()
+            self._conv2_dgrad()
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
+        if self._apply is not None and self._apply[0] == "main":
+            self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
         if self.br_fc and not self.fc_group:  # join the weight-grad branches
             main.wait_stream(self.s_fc)
         if self.br_c2:
@@ -392,8 +412,8 @@ class MnistCnnTrainer:
         mode = None
         if self.par and self.br_fc and self.late_split and self.allreduce is not None:
             mode = "late"
-        elif self.br_c2 and self.fc_group and self.branch_apply and self.allreduce is None:
-            mode = "branch"
+        elif self.br_c2 and self.fc_group and self.fc_apply in ("main", "c2") and self.allreduce is None:
+            mode = self.fc_apply
         if mode is None or (self.opt_fc is None and self.global_step_started()):
             self.forward_backward()
             self.opt.step(grad16=grad16, gscale=gscale)

@@ -238,19 +238,21 @@ def test_cnn_training_is_bitwise_reproducible(B):
     assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
 
 
-def test_cnn_branch_apply_matches_whole_apply(monkeypatch):
-    """DTFE_CNN_BRANCH_APPLY=1 (one replica): the fc/head Adam on the conv2 weight-gradient branch
-    and the conv Adam after the join follow the whole-model apply's trajectory bit for bit."""
+@pytest.mark.parametrize("where", ["main", "c2"])
+def test_cnn_fc_apply_placement_matches_whole_apply(where, monkeypatch):
+    """DTFE_CNN_FC_APPLY=main|c2 (one replica): the fc/head Adam before the join (main chain or the
+    conv2 weight-gradient branch) and the conv Adam after it follow the whole-model apply's
+    trajectory bit for bit."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
     outs = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("DTFE_CNN_BRANCH_APPLY", mode)
+    for mode in ("join", where):
+        monkeypatch.setenv("DTFE_CNN_FC_APPLY", mode)
         tr = MnistCnnTrainer(1024, "cuda", seed=9)
         for _ in range(4):
             tr.step()
         torch.cuda.synchronize()
-        assert (tr.opt_fc is not None) == (mode == "1")
+        assert (tr.opt_fc is not None) == (mode != "join")
         assert int(tr.global_step.item()) == 4
         outs.append(tr.P.master.clone())
     assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
