@@ -11,11 +11,13 @@
 
 typedef __attribute__((address_space(3))) void lds_t;
 
-template <int SEG, int STAGES>
+template <int SEG, int STAGES, int THREADS = 256>
 __device__ __forceinline__ void stream_body(const unsigned short* src, int ld, int kbytes, int blocks_m,
                                                         int* sink) {
   constexpr int TILE = 64 * SEG;                 // bytes per k-tile (64 rows)
-  constexpr int PIECES = TILE / (256 * 16);      // 16-B DMA pieces per thread per k-tile
+  constexpr int NW = THREADS / 64;
+  constexpr int PIECES = TILE / (THREADS * 16);  // 16-B DMA pieces per thread per k-tile
+  static_assert(PIECES >= 1, "at least one piece per thread");
   constexpr int CPR = SEG / 16, RPP = 64 / CPR;  // chunks per row, rows per 1 KB piece
   __shared__ __attribute__((aligned(16))) unsigned char lds[STAGES * TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -24,14 +26,14 @@ __device__ __forceinline__ void stream_body(const unsigned short* src, int ld, i
   const unsigned char* p[PIECES];
 #pragma unroll
   for (int j = 0; j < PIECES; ++j) {
-    const int row = (j * 4 + w) * RPP + lane / CPR, chunk = lane % CPR;
+    const int row = (j * NW + w) * RPP + lane / CPR, chunk = lane % CPR;
     p[j] = base + (long)row * ld * 2 + chunk * 16;
   }
   const int nk = kbytes / SEG;
   auto issue = [&](int kt, int s) {
 #pragma unroll
     for (int j = 0; j < PIECES; ++j)
-      __builtin_amdgcn_global_load_lds(p[j] + (long)kt * SEG, (lds_t*)(lds + s * TILE + (j * 4 + w) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(p[j] + (long)kt * SEG, (lds_t*)(lds + s * TILE + (j * NW + w) * 1024), 16, 0, 0);
   };
   for (int s = 0; s < STAGES - 1 && s < nk; ++s) issue(s, s);
   int acc = 0;
@@ -56,26 +58,36 @@ PROBE(256, 3)
 PROBE(512, 3)
 PROBE(128, 4)
 PROBE(256, 4)
+// waves per workgroup: one workgroup of 8 / 16 waves per CU vs several 4-wave workgroups
+#define PROBET(S, T, TH) \
+  __global__ __launch_bounds__(TH, 1) void k_##S##_##T##_##TH(const unsigned short* src, int ld, int kb, int bm, int* sink) { \
+    stream_body<S, T, TH>(src, ld, kb, bm, sink); \
+  }
+PROBET(128, 3, 512)
+PROBET(256, 3, 512)
+PROBET(256, 3, 1024)
+PROBET(128, 6, 512)
 
 typedef void (*Kern)(const unsigned short*, int, int, int, int*);
 
-double run(Kern k, int SEG, int STAGES, const unsigned short* d, int rows, int ld, int grid, int* sink) {
+double run(Kern k, int SEG, int STAGES, const unsigned short* d, int rows, int ld, int grid, int* sink, int th = 256) {
   const int blocks_m = rows / 64, kbytes = (ld * 2 / SEG) * SEG;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, d, ld, kbytes, blocks_m, sink);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(k, dim3(grid), dim3(th), 0, 0, d, ld, kbytes, blocks_m, sink);
   hipEventRecord(e0);
   const int reps = 20;
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, d, ld, kbytes, blocks_m, sink);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, dim3(grid), dim3(th), 0, 0, d, ld, kbytes, blocks_m, sink);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
   const double us = ms * 1000.0 / reps;
   const double bytes = (double)grid * 64 * kbytes;
-  printf("SEG %4d B  stages %d  grid %4d : %7.1f us  %6.2f TB/s  %5.1f B/clk/CU (2.4 GHz)\n", SEG, STAGES, grid, us,
+  printf("SEG %4d B  stages %d  threads %4d  grid %4d : %7.1f us  %6.2f TB/s  %5.1f B/clk/CU (2.4 GHz)\n", SEG, STAGES, th, grid, us,
          bytes / us / 1e6, bytes / (us * 1e-6) / 2.4e9 / 256);
+  (void)th;
   return us;
 }
 
@@ -86,7 +98,14 @@ int main() {
   hipMalloc(&d, (size_t)rows * ld * 2);
   hipMalloc(&sink, 4);
   hipMemset(d, 1, (size_t)rows * ld * 2);
-  for (int grid : {256, 768}) {
+  // one workgroup per CU with 8 / 16 waves (grid 256), and 2 x 8 waves (grid 512)
+  for (int grid : {256, 512}) {
+    run(k_128_3_512, 128, 3, d, rows, ld, grid, sink, 512);
+    run(k_256_3_512, 256, 3, d, rows, ld, grid, sink, 512);
+    run(k_128_6_512, 128, 6, d, rows, ld, grid, sink, 512);
+  }
+  run(k_256_3_1024, 256, 3, d, rows, ld, 256, sink, 1024);
+  for (int grid : {256, 512, 768}) {
     run(k_128_3, 128, 3, d, rows, ld, grid, sink);
     run(k_256_3, 256, 3, d, rows, ld, grid, sink);
     run(k_512_3, 512, 3, d, rows, ld, grid, sink);
