@@ -137,17 +137,17 @@ struct GlGroupArgs {
   int th, t0, t1;      // real workgroups of each piece
 };
 
-// HEAD: the head piece is compiled in (its 10x8 accumulators per thread set the register allocation
-// to ~148 VGPRs; without it the grouped kernel keeps the GEMMs' ~68)
+// HEAD: the head piece is compiled in - the 4-column body (head_wgrad4_body, 40 accumulators per
+// thread; the 8-column one set the grouped kernel to ~148 VGPRs against the GEMMs' ~68)
 template <int AM0, int BM0, int AM1, int BM1, bool HEAD>
 __global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_group_kernel(GlGroupArgs ga) {
-  constexpr int HEAD_BYTES = 4 * 80 * 4;
+  constexpr int HEAD_BYTES = 4 * 40 * 4;
   constexpr int BYTES = GlSmem<64, 64, 2>::BYTES > HEAD_BYTES ? GlSmem<64, 64, 2>::BYTES : HEAD_BYTES;
   __shared__ __attribute__((aligned(16))) char smem_raw[BYTES];
   int bid = blockIdx.x;
   if constexpr (HEAD) {
     if (bid < ga.nh) {
-      if (bid < ga.th) head_wgrad_body<10, 4>(ga.h, bid, reinterpret_cast<float(*)[80]>(smem_raw));
+      if (bid < ga.th) head_wgrad4_body<10>(ga.h, bid, reinterpret_cast<float(*)[40]>(smem_raw));
       return;
     }
   }
@@ -210,7 +210,7 @@ void glds_group_end(hipStream_t s) {
   ga.g1 = r.g[1];
   if (r.has_h) {
     ga.h = r.h;
-    ga.th = r.h.K / 8 + (r.h.db ? 1 : 0);
+    ga.th = r.h.K / 4 + (r.h.db ? 1 : 0);
     ga.nh = pad8(ga.th);
   }
   ga.t0 = (ga.g0.M / 64) * ((ga.g0.N + 63) / 64);

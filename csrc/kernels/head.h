@@ -102,5 +102,73 @@ __device__ __forceinline__ void head_wgrad_body(const HeadWgradArgs& a, int bid,
   }
 }
 
+// The grouped fc-backward launch's head piece (gemm_dense.hip): 4 columns of dW per workgroup
+// (bid == K/4: the bias) with the rows streamed one 256-row pass at a time - 40 accumulators, so
+// the piece stays inside the GEMM pieces' register budget (the 8-column body above set the grouped
+// kernel to 148 VGPRs).  red: 4 x 40 floats of LDS.
+template <int NC>
+__device__ __forceinline__ void head_wgrad4_body(const HeadWgradArgs& a, int bid, float (*red)[NC * 4]) {
+  static_assert(NC * 4 == 40, "the butterfly below is laid out for 10 classes x 4 columns");
+  constexpr int V = NC * 4;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool bias_blk = bid * 4 >= a.K;
+  const int col0 = bias_blk ? 0 : bid * 4;
+  float v[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) v[j] = 0.f;
+#pragma unroll 1
+  for (int b0 = 0; b0 < a.B; b0 += 256) {
+    const int b = b0 + t;
+    const bool ok = b < a.B;
+    const long r = ok ? b : 0;  // clamped row: loads stay in bounds, the products are zeroed
+    const u32x2_t hv = *reinterpret_cast<const u32x2_t*>(a.h + r * a.ldh + col0);
+    const u32x4_t d0 = *reinterpret_cast<const u32x4_t*>(a.dl + r * a.ld_dl);
+    const uint32_t d1 = *reinterpret_cast<const uint32_t*>(a.dl + r * a.ld_dl + 8);
+    float h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      h[e] = !ok ? 0.f : bias_blk ? 1.f : bf2f((bf16)(hv[e >> 1] >> (16 * (e & 1))));
+#pragma unroll
+    for (int n = 0; n < NC; ++n) {
+      const uint32_t w = n < 8 ? d0[n >> 1] : d1;
+      const float d = bf2f((bf16)(w >> (16 * (n & 1))));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[n * 4 + e] = fmaf(d, h[e], v[n * 4 + e]);
+    }
+  }
+  // halving butterfly over lane bits 5..3: 40 -> 20 -> 10 -> 5 values per lane, then bits 2..0
+  auto halve = [&](auto half_c, int mask) {
+    constexpr int H = decltype(half_c)::value;
+    const bool hi = (lane & mask) != 0;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const float send = hi ? v[j] : v[H + j];
+      const float keep = hi ? v[H + j] : v[j];
+      v[j] = keep + __shfl_xor(send, mask, 64);
+    }
+  };
+  halve(std::integral_constant<int, 20>{}, 32);
+  halve(std::integral_constant<int, 10>{}, 16);
+  halve(std::integral_constant<int, 5>{}, 8);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    v[j] += __shfl_xor(v[j], 4, 64);
+    v[j] += __shfl_xor(v[j], 2, 64);
+    v[j] += __shfl_xor(v[j], 1, 64);
+  }
+  // lane holds values ((b5 ? 20 : 0) + (b4 ? 10 : 0) + (b3 ? 5 : 0) + j)
+  if ((lane & 7) == 0) {
+    const int base = ((lane >> 5) & 1) * 20 + ((lane >> 4) & 1) * 10 + ((lane >> 3) & 1) * 5;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) red[wid][base + j] = v[j];
+  }
+  __syncthreads();
+  if (t < V) {
+    const float s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    const int n = t >> 2, e = t & 3;
+    if (!bias_blk) a.dw[(long)n * a.ldw + col0 + e] = s * a.scale;
+    else if (e == 0) a.db[n] = s * a.scale;
+  }
+}
 
 }  // namespace dtfe

@@ -237,6 +237,10 @@ class MnistCnnTrainer:
         self.glds = self.device.type == "cuda" and os.environ.get("DTFE_CNN_GLDS", "1") != "0"
         # DTFE_CNN_FC_GROUP=0: the fc backward as a forked side branch instead of one grouped launch
         self.fc_group = self.par and os.environ.get("DTFE_CNN_FC_GROUP", "1") != "0"
+        # the head weight gradient as the grouped launch's first piece (4-column body, 84 VGPRs: the
+        # GEMM pieces keep 5 workgroups per CU) - 0.2033-0.2071 vs 0.2105-0.2124 ms/step as its own
+        # launch before the group (DTFE_CNN_HEAD_IN_GROUP=0; profiles/r3_cnn_kernel_tuning.txt r3ze)
+        self.head_in_group = self.fc_group and os.environ.get("DTFE_CNN_HEAD_IN_GROUP", "1") == "1"
         K1 = 7 * 7 * C2
         # DTFE_CNN_TILES=fwd,dgrad,wgrad overrides the glds tile ids (A/B sweeps)
         tiles = [int(t) for t in os.environ.get("DTFE_CNN_TILES", "8,12,12").split(",")]
@@ -306,8 +310,11 @@ class MnistCnnTrainer:
             # data-gradient workgroups first (lower grid ranges)
             # (the head piece stays its own launch: its 10x8 accumulators per thread would set the
             # grouped kernel's register allocation to 148 VGPRs, 3 workgroups per CU instead of 7)
-            self._head_wgrad()
+            if not self.head_in_group:
+                self._head_wgrad()
             with ops.gemm_group(self.dzf):
+                if self.head_in_group:
+                    self._head_wgrad()   # recorded as the grouped launch's first piece
                 self._fc1_dgrad(B, K1)
                 self._fc1_wgrad(B, K1)
             if self.allreduce is not None:
