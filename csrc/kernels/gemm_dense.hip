@@ -124,7 +124,7 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
 
 // ------------------------------------------------------------ grouped launch
 // Independent GEMMs of one step phase in ONE launch (horizontal fusion): workgroup ranges of the grid
-// run different pieces - the head weight gradient's 129 workgroups, then two 64x64 2-stage glds
+// run different pieces - the head weight gradient's 257 workgroups (4 columns each), then two 64x64 2-stage glds
 // GEMMs (the MNIST-CNN fc1 data and weight gradients).  One launch instead of a fork onto a side
 // stream: no cross-queue dependency inside the captured graph (each such edge cost 5-11 us of idle
 // time in the step timeline, profiles/r3_cnn_kernel_tuning.txt), and the dispatcher hands out the
