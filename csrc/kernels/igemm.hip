@@ -649,22 +649,55 @@ __global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgr
 
 // dw[i] += scale * sum_s ws[s][i]
 constexpr int WG_RCH = 8;
+// dw[i] += scale * sum_s ws[s][i].  A workgroup covers P = 256 / S float4 positions with S split
+// slices per position (thread = (slice, position)): a small weight with many m-splits (e.g. 64x64x1x1
+// over 100+ splits: a handful of position-only workgroups, each walking every split serially) still
+// fills the chip.  Slices sum their splits in order, then slice 0 adds the S slice sums in order
+// through LDS - a fixed summation order (bitwise reproducible).
+template <int S>
 __global__ __launch_bounds__(256) void wgrad_splits_reduce_kernel(const float* __restrict__ ws, int splits, long len,
                                                                   float* dw, float scale) {
-  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= len) return;
+  constexpr int P = 256 / S;
+  __shared__ f32x4_t red[S > 1 ? S : 1][P];
+  const int pos = threadIdx.x % P, sl = threadIdx.x / P;
+  const long i = ((long)blockIdx.x * P + pos) * 4;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  int s = 0;
-  for (; s + WG_RCH <= splits; s += WG_RCH) {
-    f32x4_t v[WG_RCH];
+  if (i < len) {
+    int s = sl;
+    for (; s + (WG_RCH - 1) * S < splits; s += WG_RCH * S) {
+      f32x4_t v[WG_RCH];
 #pragma unroll
-    for (int j = 0; j < WG_RCH; ++j) v[j] = *reinterpret_cast<const f32x4_t*>(ws + (long)(s + j) * len + i);
+      for (int j = 0; j < WG_RCH; ++j) v[j] = *reinterpret_cast<const f32x4_t*>(ws + (long)(s + j * S) * len + i);
 #pragma unroll
-    for (int j = 0; j < WG_RCH; ++j) acc += v[j];
+      for (int j = 0; j < WG_RCH; ++j) acc += v[j];
+    }
+    for (; s < splits; s += S) acc += *reinterpret_cast<const f32x4_t*>(ws + (long)s * len + i);
   }
-  for (; s < splits; ++s) acc += *reinterpret_cast<const f32x4_t*>(ws + (long)s * len + i);
+  if constexpr (S > 1) {
+    red[sl][pos] = acc;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) acc += red[k][pos];
+  }
+  if (i >= len) return;
   f32x4_t d = *reinterpret_cast<const f32x4_t*>(dw + i);
   *reinterpret_cast<f32x4_t*>(dw + i) = d + scale * acc;
+}
+
+// split slices per position: enough workgroups (~512) for the chip when the weight is small
+void launch_wgrad_splits_reduce(const float* ws, int splits, long len, float* dw, float scale, hipStream_t s) {
+  const long n4 = (len + 3) / 4;
+  int S = 1;
+  while (S < 16 && S * 2 <= splits && (n4 * S) / 256 < 512) S *= 2;
+  const unsigned grid = (unsigned)((n4 + 256 / S - 1) / (256 / S));
+  switch (S) {
+    case 1: hipLaunchKernelGGL(wgrad_splits_reduce_kernel<1>, dim3(grid), dim3(256), 0, s, ws, splits, len, dw, scale); break;
+    case 2: hipLaunchKernelGGL(wgrad_splits_reduce_kernel<2>, dim3(grid), dim3(256), 0, s, ws, splits, len, dw, scale); break;
+    case 4: hipLaunchKernelGGL(wgrad_splits_reduce_kernel<4>, dim3(grid), dim3(256), 0, s, ws, splits, len, dw, scale); break;
+    case 8: hipLaunchKernelGGL(wgrad_splits_reduce_kernel<8>, dim3(grid), dim3(256), 0, s, ws, splits, len, dw, scale); break;
+    default: hipLaunchKernelGGL(wgrad_splits_reduce_kernel<16>, dim3(grid), dim3(256), 0, s, ws, splits, len, dw, scale); break;
+  }
 }
 
 // ------------------------------------------------- BatchNorm partial-statistics reduction
@@ -1052,8 +1085,7 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
     hipLaunchKernelGGL(igemm_wgrad3_kernel, dim3((unsigned)tiles, (unsigned)sp), dim3(IG_THREADS), 0, s, a, f.dw,
                        f.scale, R, kpi);
     if (sp > 1)
-      hipLaunchKernelGGL(wgrad_splits_reduce_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws,
-                         (int)sp, len, f.dw, f.scale);
+      launch_wgrad_splits_reduce(a.ws, (int)sp, len, f.dw, f.scale, s);
     return true;
   }
   const int bm = g.Cout % 128 == 0 ? 128 : 64, bn = g.C % 128 == 0 ? 128 : 64;
@@ -1084,8 +1116,7 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   else if (bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<64, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
   else hipLaunchKernelGGL((igemm_wgrad_kernel<64, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
   if (sp > 1)
-    hipLaunchKernelGGL(wgrad_splits_reduce_kernel, dim3((unsigned)((len / 4 + 255) / 256)), dim3(256), 0, s, a.ws, sp,
-                       len, f.dw, f.scale);
+    launch_wgrad_splits_reduce(a.ws, sp, len, f.dw, f.scale, s);
   return true;
 }
 
