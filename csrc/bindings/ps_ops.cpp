@@ -467,7 +467,7 @@ const SubPlan& sub_plan(Service* s, Group& g, long lo, long hi) {
   if (bs) std::memcpy(host.data(), g.hsegs.data(), bs);
   if (!wk.empty()) std::memcpy(host.data() + off, wk.data(), wk.size() * sizeof(dtfe::OptWork));
   p.blob = at::empty({(int64_t)host.size()}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, s->device));
-  (void)hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice);
+  hchk(hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice), "apply sub-plan H2D");
   return g.sub.emplace(key, std::move(p)).first->second;
 }
 
@@ -591,7 +591,7 @@ void run(Service* s) {
     std::memcpy(host.data(), &sg, sizeof(sg));
     std::memcpy(host.data() + off, wk.data(), wk.size() * sizeof(dtfe::PsWork));
     p.blob = at::empty({(int64_t)host.size()}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, s->device));
-    (void)hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice);
+    hchk(hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice), "plan H2D");
     p.nwork = (int64_t)wk.size();
     return p;
   };

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../kernels/conv.h"
+#include "../kernels/conv_f32.h"
 #include "../kernels/conv1.h"
 #include "../kernels/imgconv.h"
 #include "../kernels/norm.h"
@@ -133,7 +134,20 @@ void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, co
               int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool pool, int64_t act,
               const optional<Tensor>& bn_stats) {
   check_cuda(x, "x");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv_fwd: bf16 only");
+  if (x.scalar_type() == at::kFloat) {  // exact-fp32 path (--dtype fp32): conv_f32.hip
+    TORCH_CHECK(w.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat && !(bn_stats.has_value() && bn_stats->defined()),
+                "conv_fwd (fp32): fp32 x / w / y, no BatchNorm statistics");
+    TORCH_CHECK(!pool || ((OH | OW) & 1) == 0, "conv_fwd (fp32): pool needs even output dims");
+    dtfe::ConvF32Args f{};
+    f.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, pool);
+    f.src = x.data_ptr<float>(); f.w = w.data_ptr<float>(); f.bias = ptr_or_null<float>(bias);
+    f.out = y.data_ptr<float>(); f.argmax = ptr_or_null<uint8_t>(argmax); f.act = (int)act;
+    TORCH_CHECK(y.numel() == B * OH * OW * Cout / (pool ? 4 : 1) && x.numel() == B * H * W * C &&
+                w.numel() == Cout * KH * KW * C, "conv_fwd (fp32): shapes");
+    dtfe::launch_conv_fwd_f32(f, cur_stream());
+    return;
+  }
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv_fwd: bf16 or fp32");
   dtfe::ConvFwdArgs a{};
   if (bn_stats.has_value() && bn_stats->defined()) {
     TORCH_CHECK(bn_stats->scalar_type() == at::kFloat && bn_stats->is_contiguous() && bn_stats->numel() >= 2 * Cout,
@@ -157,6 +171,22 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
                 const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_invstd, const optional<Tensor>& bnb_gamma,
                 const optional<Tensor>& bnb_beta, const optional<Tensor>& bnb_stats, int64_t bnb_act) {
   check_cuda(dy, "dy");
+  if (dy.scalar_type() == at::kFloat) {  // exact-fp32 path (--dtype fp32): conv_f32.hip
+    TORCH_CHECK(wt.scalar_type() == at::kFloat && dx.scalar_type() == at::kFloat && stride == 1 && !accumulate &&
+                    !(pooled.has_value() && pooled->defined()) && !(bnb_stats.has_value() && bnb_stats->defined()),
+                "conv_dgrad (fp32): fp32 tensors, stride 1, optional ReLU mask only");
+    TORCH_CHECK(dx.numel() == B * H * W * C && dy.numel() == B * OH * OW * Cout && wt.numel() == C * KH * KW * Cout,
+                "conv_dgrad (fp32): shapes");
+    dtfe::ConvF32Args f{};
+    f.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
+    f.src = dy.data_ptr<float>(); f.w = wt.data_ptr<float>(); f.out = dx.data_ptr<float>();
+    if (relu_mask.has_value() && relu_mask->defined()) {
+      TORCH_CHECK(relu_mask->scalar_type() == at::kFloat && relu_mask->numel() == dx.numel(), "conv_dgrad (fp32): mask");
+      f.relu_mask = relu_mask->data_ptr<float>();
+    }
+    dtfe::launch_conv_dgrad_f32(f, cur_stream());
+    return;
+  }
   dtfe::ConvDgradArgs a{};
   a.accumulate = accumulate ? 1 : 0;
   if (bnb_stats.has_value() && bnb_stats->defined()) {
@@ -314,6 +344,16 @@ void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optio
                 int64_t pad, double scale) {
   check_cuda(dz, "dz");
   TORCH_CHECK(dw.scalar_type() == at::kFloat, "conv_wgrad: fp32 grad buffer");
+  if (dz.scalar_type() == at::kFloat) {  // exact-fp32 path (--dtype fp32): conv_f32.hip
+    TORCH_CHECK(x.scalar_type() == at::kFloat && dz.numel() == B * OH * OW * Cout && x.numel() == B * H * W * C &&
+                    dw.numel() == Cout * KH * KW * C, "conv_wgrad (fp32): fp32 dz / x, shapes");
+    dtfe::ConvF32Args f{};
+    f.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
+    f.src = dz.data_ptr<float>(); f.x = x.data_ptr<float>(); f.dw = dw.data_ptr<float>();
+    f.db = ptr_or_null<float>(db); f.scale = (float)scale;
+    dtfe::launch_conv_wgrad_f32(f, cur_stream());
+    return;
+  }
   dtfe::ConvWgradArgs a{};
   a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
   a.dz = reinterpret_cast<const dtfe::bf16*>(dz.data_ptr());
@@ -322,6 +362,25 @@ void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optio
   a.db = ptr_or_null<float>(db);
   a.scale = (float)scale;
   dtfe::launch_conv_wgrad(a, cur_stream());
+}
+
+// 2x2 un-pool of a pooled fp32 gradient (argmax routing) and the [O][T][C] -> [C][T][O] weight
+// transpose: the two data movers of the fp32 CNN step (conv_f32.hip)
+void unpool_f32(const Tensor& g, const Tensor& argmax, const Tensor& out, int64_t B, int64_t PH, int64_t PW,
+                int64_t C) {
+  check_cuda(g, "g");
+  TORCH_CHECK(g.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && argmax.scalar_type() == at::kByte &&
+                  g.numel() == B * PH * PW * C && argmax.numel() == g.numel() && out.numel() == 4 * g.numel(),
+              "unpool_f32: fp32 g [B][PH][PW][C], uint8 argmax, fp32 out [B][2PH][2PW][C]");
+  dtfe::launch_unpool_f32(g.data_ptr<float>(), argmax.data_ptr<uint8_t>(), out.data_ptr<float>(), (int)B, (int)PH,
+                          (int)PW, (int)C, cur_stream());
+}
+
+void transpose_taps_f32(const Tensor& in, const Tensor& out, int64_t O, int64_t T, int64_t C) {
+  check_cuda(in, "in");
+  TORCH_CHECK(in.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && in.numel() == O * T * C &&
+                  out.numel() == in.numel() && in.is_contiguous() && out.is_contiguous(), "transpose_taps_f32: shapes");
+  dtfe::launch_transpose_taps_f32(in.data_ptr<float>(), out.data_ptr<float>(), (int)O, (int)T, (int)C, cur_stream());
 }
 
 // ------------------------------------------------------------------- head
@@ -905,6 +964,8 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(d!) dz_fake_disc, Tensor(e!) dz_fake_gen, float clamp_eps) -> ()");
   m.def("mse_sigmoid(Tensor y, Tensor t, Tensor(a!) loss, Tensor(b!) dz) -> ()");
   m.def("colsum(Tensor x, int M, int N, int ld, Tensor(a!) db, float scale) -> ()");
+  m.def("unpool_f32(Tensor g, Tensor argmax, Tensor(a!) out, int B, int PH, int PW, int C) -> ()");
+  m.def("transpose_taps_f32(Tensor input, Tensor(a!) out, int O, int T, int C) -> ()");
   m.def("act_grad(Tensor dy, Tensor y, Tensor(a!) dz, int act) -> ()");
   m.def("bias_act(Tensor x, Tensor? bias, Tensor(a!) out, int act, float keep, int seed, Tensor? counter) -> ()");
 }
@@ -940,6 +1001,8 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("gan_loss", &gan_loss);
   m.impl("mse_sigmoid", &mse_sigmoid);
   m.impl("colsum", &colsum);
+  m.impl("unpool_f32", &unpool_f32);
+  m.impl("transpose_taps_f32", &transpose_taps_f32);
   m.impl("act_grad", &act_grad);
   m.impl("bias_act", &bias_act);
   m.impl("conv1_fwd_pool", &conv1_fwd_pool);

@@ -96,6 +96,19 @@ def build_kernels(jobs: int, verbose: bool, ab_rev: str | None = None, ab_files=
         ab_dir = os.path.join(OUT_DIR, "ab")  # in-tree (travels with the gpurun snapshot; git-ignored)
         os.makedirs(os.path.join(ROOT, "build", "ab_src"), exist_ok=True)
         os.makedirs(ab_dir, exist_ok=True)
+        # the A/B sources compile against the headers of the SAME revision (a struct that changed
+        # between REV and HEAD would otherwise mix layouts silently): every csrc/kernels/*.h of REV
+        # goes into build/ab_src, first on the include path
+        ab_src = os.path.join(ROOT, "build", "ab_src")
+        names = subprocess.run(["git", "-C", ROOT, "ls-tree", "--name-only", ab_rev, "csrc/kernels/"], check=True,
+                               stdout=subprocess.PIPE, text=True).stdout.split()
+        for rel in names:
+            if rel.endswith(".h"):
+                txt = subprocess.run(["git", "-C", ROOT, "show", "%s:%s" % (ab_rev, rel)], check=True,
+                                     stdout=subprocess.PIPE).stdout
+                with open(os.path.join(ab_src, os.path.basename(rel)), "wb") as fh:
+                    fh.write(txt)
+        kflags = common + ["-I" + ab_src, "-I" + os.path.join(CSRC, "kernels")]
         for f in ab_files:
             rel = os.path.relpath(os.path.abspath(f), ROOT)
             txt = subprocess.run(["git", "-C", ROOT, "show", "%s:%s" % (ab_rev, rel)], check=True,

@@ -1,0 +1,328 @@
+// Exact-fp32 NHWC convolution (the reference's precision, `--dtype fp32`): forward (+bias, ReLU,
+// fused 2x2 max-pool + argmax), data gradient (+ReLU mask of a pooled consumer), weight gradient
+// (+bias gradient), plus the two small data movers the fp32 CNN step needs (2x2 un-pool of a
+// pooled gradient, [O][T][C] -> [C][T][O] weight transpose for the data gradient).
+//
+// The matrix work runs on v_mfma_f32_16x16x4_f32 through the generic LDS-tiled engine of
+// gemm_core.h (T = float: 16-B chunks of 4 k, KMAJ images [rows][32 + 4]): the same fp32-in /
+// fp32-accumulate arithmetic as an fmaf chain, so the step matches fp32 autograd to rounding.
+// The im2col operands are gathered per 16-B chunk (4 consecutive channels of one tap) when the
+// channel count is a multiple of 4, element by element otherwise (the 1-channel MNIST input).
+//
+// Replaces Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter / MaxPool(+grad) / BiasAdd(+grad)
+// / Relu(+grad) of the MNIST CNN at fp32 (TensorFlow-Examples convolutional_network, the notebook
+// family of ENC:14; fp32 as every reference script: GAN:122-135, LSTM:83-97).
+#include "gemm_core.h"
+#include "conv.h"
+#include "conv_f32.h"
+
+namespace dtfe {
+
+namespace {
+
+__device__ __forceinline__ int fdiv(int m, int d, float inv_d) {
+  int q = (int)((float)m * inv_d);
+  const int r = m - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+// row m of the output grid -> (b, y, x); pool order enumerates 2x2 windows (b, ph, pw, dy, dx)
+__device__ __forceinline__ void f32_row(int m, int RH, int RW, int pool_order, int& b, int& y, int& x) {
+  if (pool_order) {
+    const int q = m & 3, pm = m >> 2, PW = RW >> 1, PH = RH >> 1;
+    const int pw = pm % PW, t = pm / PW;
+    y = 2 * (t % PH) + (q >> 1);
+    x = 2 * pw + (q & 1);
+    b = t / PH;
+  } else {
+    x = m % RW;
+    const int t = m / RW;
+    y = t % RH;
+    b = t / RH;
+  }
+}
+
+// A operand (KMAJ): rows = pixels of the row grid, k = (kh, kw, c) of the source.
+// TRANS (data gradient): source = dY, stride-1 flipped taps: src = (y + p - kh, x + p - kw).
+template <int R, bool TRANS>
+struct Im2colF32 {
+  using Lay = LdsLayout<float, R, KMAJ>;
+  using C = Chunks<float, R, KMAJ>;
+  const float* src; ConvGeom g; int rows, K, SC, SH, SW;
+  int rb[C::NC], ry[C::NC], rx[C::NC];  // per chunk: batch (-1: out of range), tap-0 source coords
+  u32x4_t regs[C::NC];
+
+  __device__ __forceinline__ Im2colF32(const float* s, const ConvGeom& g_, int r0) : src(s), g(g_) {
+    const int RH = TRANS ? g.H : g.OH, RW = TRANS ? g.W : g.OW;
+    SC = TRANS ? g.Cout : g.C;
+    SH = TRANS ? g.OH : g.H;
+    SW = TRANS ? g.OW : g.W;
+    rows = g.B * RH * RW;
+    K = g.KH * g.KW * SC;
+#pragma unroll
+    for (int c = 0; c < C::NC; ++c) {
+      int r, k;
+      C::rk(threadIdx.x + c * GEMM_THREADS, r, k);
+      const int m = r0 + r;
+      rb[c] = -1;
+      ry[c] = rx[c] = 0;
+      if ((C::N % GEMM_THREADS == 0 || threadIdx.x + c * GEMM_THREADS < C::N) && m < rows) {
+        int b, y, x;
+        f32_row(m, RH, RW, TRANS ? 0 : g.pool_order, b, y, x);
+        rb[c] = b;
+        ry[c] = TRANS ? y + g.pad : y * g.stride - g.pad;
+        rx[c] = TRANS ? x + g.pad : x * g.stride - g.pad;
+      }
+    }
+  }
+  __device__ __forceinline__ float at(int c, int gk) const {
+    const int tap = gk / SC, ch = gk - tap * SC, kh = tap / g.KW, kw = tap - kh * g.KW;
+    const int sy = TRANS ? ry[c] - kh : ry[c] + kh, sx = TRANS ? rx[c] - kw : rx[c] + kw;
+    if (sy < 0 || sy >= SH || sx < 0 || sx >= SW) return 0.f;
+    return src[(((long)rb[c] * SH + sy) * SW + sx) * SC + ch];
+  }
+  template <bool FAST = false>
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int c = 0; c < C::NC; ++c) {
+      int r, k;
+      C::rk(threadIdx.x + c * GEMM_THREADS, r, k);
+      const int gk = k0 + k;
+      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+      if (rb[c] >= 0 && gk < K) {
+        if ((SC & 3) == 0) {  // 4 channels of one tap: one 16-B load
+          const int tap = gk / SC, ch = gk - tap * SC, kh = tap / g.KW, kw = tap - kh * g.KW;
+          const int sy = TRANS ? ry[c] - kh : ry[c] + kh, sx = TRANS ? rx[c] - kw : rx[c] + kw;
+          if (sy >= 0 && sy < SH && sx >= 0 && sx < SW)
+            v = *reinterpret_cast<const f32x4_t*>(src + (((long)rb[c] * SH + sy) * SW + sx) * SC + ch);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = gk + i < K ? at(c, gk + i) : 0.f;
+        }
+      }
+      regs[c] = __builtin_bit_cast(u32x4_t, v);
+    }
+  }
+  __device__ __forceinline__ void store(float* lds) const { stage_store<float, R, KMAJ>(lds, regs); }
+};
+
+// B operand of the weight gradient (RMAJ, transposed while staging): rows = k = (kh, kw, c) of the
+// forward conv + one ones row (the bias column), reduction = output pixel m.
+template <int R>
+struct Im2colWgradF32 {
+  using Lay = LdsLayout<float, R, RMAJ>;
+  using C = Chunks<float, R, RMAJ>;
+  const float* x; ConvGeom g; int Kw, Mred, r0;
+  float inv_ow, inv_oh;
+  u32x4_t regs[C::NC];
+
+  __device__ __forceinline__ Im2colWgradF32(const float* x_, const ConvGeom& g_, int r0_) : x(x_), g(g_), r0(r0_) {
+    Kw = g.KH * g.KW * g.C;
+    Mred = g.B * g.OH * g.OW;
+    inv_ow = 1.f / (float)g.OW;
+    inv_oh = 1.f / (float)g.OH;
+  }
+  template <bool FAST = false>
+  __device__ __forceinline__ void load(int k0) {
+#pragma unroll
+    for (int c = 0; c < C::NC; ++c) {
+      f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+      const int idx = threadIdx.x + c * GEMM_THREADS;
+      if (C::N % GEMM_THREADS == 0 || idx < C::N) {
+        int r, k;
+        C::rk(idx, r, k);
+        const int m = k0 + k, gr = r0 + r;
+        if (m < Mred) {
+          const int q1 = fdiv(m, g.OW, inv_ow);
+          const int ox = m - q1 * g.OW;
+          const int b = fdiv(q1, g.OH, inv_oh);
+          const int oy = q1 - b * g.OH;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int kk = gr + i;
+            if (kk < Kw) {
+              const int tap = kk / g.C, ch = kk - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
+              const int sy = oy * g.stride - g.pad + kh, sx = ox * g.stride - g.pad + kw;
+              if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W) v[i] = x[(((long)b * g.H + sy) * g.W + sx) * g.C + ch];
+            } else if (kk == Kw) {
+              v[i] = 1.f;  // bias column
+            }
+          }
+        }
+      }
+      regs[c] = __builtin_bit_cast(u32x4_t, v);
+    }
+  }
+  __device__ __forceinline__ void store(float* lds) const { stage_store<float, R, RMAJ>(lds, regs); }
+};
+
+template <typename Cfg>
+__global__ __launch_bounds__(GEMM_THREADS) void conv_fwd_f32_kernel(ConvF32Args a) {
+  using LA = Im2colF32<Cfg::BM, false>;
+  using LB = DenseLoader<float, Cfg::BN, KMAJ>;
+  __shared__ __attribute__((aligned(16))) float smem[SmemSize<float, Cfg, LA, LB>::ELEMS];
+  const ConvGeom& g = a.g;
+  const int M = g.B * g.OH * g.OW, N = g.Cout, K = g.KH * g.KW * g.C;
+  int tm, tn;
+  tile_coords((M + Cfg::BM - 1) / Cfg::BM, (N + Cfg::BN - 1) / Cfg::BN, tm, tn);
+  const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
+  LA la(a.src, g, m_base);
+  LB lb(a.w, K, N, K, n_base);
+  f32x4_t acc[Cfg::TM][Cfg::TN];
+  gemm_mainloop<float, Cfg, KMAJ, KMAJ>(la, lb, 0, K, smem, acc);
+  for_each_quad<Cfg>(m_base, n_base, acc, [&](int row0, int col, f32x4_t v) {
+    if (col >= N || row0 >= M) return;
+    const float bias = a.bias ? a.bias[col] : 0.f;
+    if (g.pool_order) {  // the 4 rows of a lane are one 2x2 window; first maximum wins (torch / TF)
+      int am = 0;
+      float mx = v[0];
+#pragma unroll
+      for (int j = 1; j < 4; ++j)
+        if (v[j] > mx) { mx = v[j]; am = j; }
+      const long o = (long)(row0 >> 2) * N + col;
+      a.out[o] = apply_act(mx + bias, a.act);  // act is monotone: pool(act(z)) == act(pool(z))
+      if (a.argmax) a.argmax[o] = (uint8_t)am;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (row0 + j < M) a.out[(long)(row0 + j) * N + col] = apply_act(v[j] + bias, a.act);
+    }
+  });
+}
+
+template <typename Cfg>
+__global__ __launch_bounds__(GEMM_THREADS) void conv_dgrad_f32_kernel(ConvF32Args a) {
+  using LA = Im2colF32<Cfg::BM, true>;
+  using LB = DenseLoader<float, Cfg::BN, KMAJ>;  // wt [C][KH][KW][Cout]
+  __shared__ __attribute__((aligned(16))) float smem[SmemSize<float, Cfg, LA, LB>::ELEMS];
+  const ConvGeom& g = a.g;
+  const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.Cout;
+  int tm, tn;
+  tile_coords((M + Cfg::BM - 1) / Cfg::BM, (N + Cfg::BN - 1) / Cfg::BN, tm, tn);
+  const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
+  LA la(a.src, g, m_base);
+  LB lb(a.w, K, N, K, n_base);
+  f32x4_t acc[Cfg::TM][Cfg::TN];
+  gemm_mainloop<float, Cfg, KMAJ, KMAJ>(la, lb, 0, K, smem, acc);
+  for_each_quad<Cfg>(m_base, n_base, acc, [&](int row0, int col, f32x4_t v) {
+    if (col >= N) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long o = (long)(row0 + j) * N + col;
+      if (row0 + j < M) a.out[o] = (!a.relu_mask || a.relu_mask[o] > 0.f) ? v[j] : 0.f;
+    }
+  });
+}
+
+template <typename Cfg>
+__global__ __launch_bounds__(GEMM_THREADS) void conv_wgrad_f32_kernel(ConvF32Args a) {
+  using LA = DenseLoader<float, Cfg::BM, RMAJ>;  // dZ[m][cout]
+  using LB = Im2colWgradF32<Cfg::BN>;
+  __shared__ __attribute__((aligned(16))) float smem[SmemSize<float, Cfg, LA, LB>::ELEMS];
+  const ConvGeom& g = a.g;
+  const int M = g.Cout, Kw = g.KH * g.KW * g.C, N = Kw + (a.db ? 1 : 0), Kred = g.B * g.OH * g.OW;
+  int tm, tn;
+  tile_coords((M + Cfg::BM - 1) / Cfg::BM, (N + Cfg::BN - 1) / Cfg::BN, tm, tn);
+  const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
+  const int k_begin = blockIdx.z * a.k_chunk, k_end = min(Kred, k_begin + a.k_chunk);
+  LA la(a.src, M, M, Kred, m_base);
+  LB lb(a.x, g, n_base);
+  f32x4_t acc[Cfg::TM][Cfg::TN];
+  gemm_mainloop<float, Cfg, RMAJ, RMAJ>(la, lb, k_begin, k_end, smem, acc);
+  for_each_quad<Cfg>(m_base, n_base, acc, [&](int row0, int col, f32x4_t v) {
+    if (col > Kw || (col == Kw && !a.db)) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = row0 + j;
+      if (row >= M) continue;
+      if (col < Kw) atomicAdd(a.dw + (long)row * Kw + col, v[j] * a.scale);
+      else atomicAdd(a.db + row, v[j] * a.scale);
+    }
+  });
+}
+
+template <typename Cfg> int ntiles(int M, int N) { return ((M + Cfg::BM - 1) / Cfg::BM) * ((N + Cfg::BN - 1) / Cfg::BN); }
+
+// one thread per pooled element: route g to its argmax position of the 2x2 window, zeros elsewhere
+__global__ __launch_bounds__(256) void unpool_f32_kernel(const float* __restrict__ g, const uint8_t* __restrict__ am,
+                                                         float* __restrict__ out, int PH, int PW, int C, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  long t = i / C;
+  const int pw = (int)(t % PW);
+  t /= PW;
+  const int ph = (int)(t % PH);
+  const long b = t / PH;
+  const int q0 = am[i];
+  const float v = g[i];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    out[((b * 2 * PH + 2 * ph + (q >> 1)) * 2 * PW + 2 * pw + (q & 1)) * C + c] = q == q0 ? v : 0.f;
+}
+
+// out[c][t][o] = in[o][t][c]
+__global__ __launch_bounds__(256) void transpose_taps_f32_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                 int O, int T, int C) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)O * T * C) return;
+  const int c = (int)(i % C);
+  const long r = i / C;
+  const int t = (int)(r % T), o = (int)(r / T);
+  out[((long)c * T + t) * O + o] = in[i];
+}
+
+}  // namespace
+
+void launch_conv_fwd_f32(const ConvF32Args& a, hipStream_t s) {
+  const ConvGeom& g = a.g;
+  const int M = g.B * g.OH * g.OW;
+  if (g.Cout <= 32) {
+    using Cfg = TileCfg<float, 64, 32, 4, 1>;
+    hipLaunchKernelGGL(conv_fwd_f32_kernel<Cfg>, dim3(ntiles<Cfg>(M, g.Cout)), dim3(GEMM_THREADS), 0, s, a);
+  } else {
+    using Cfg = TileCfg<float, 64, 64, 2, 2>;
+    hipLaunchKernelGGL(conv_fwd_f32_kernel<Cfg>, dim3(ntiles<Cfg>(M, g.Cout)), dim3(GEMM_THREADS), 0, s, a);
+  }
+}
+
+void launch_conv_dgrad_f32(const ConvF32Args& a, hipStream_t s) {
+  const ConvGeom& g = a.g;
+  const int M = g.B * g.H * g.W;
+  if (g.C <= 32) {
+    using Cfg = TileCfg<float, 64, 32, 4, 1>;
+    hipLaunchKernelGGL(conv_dgrad_f32_kernel<Cfg>, dim3(ntiles<Cfg>(M, g.C)), dim3(GEMM_THREADS), 0, s, a);
+  } else {
+    using Cfg = TileCfg<float, 64, 64, 2, 2>;
+    hipLaunchKernelGGL(conv_dgrad_f32_kernel<Cfg>, dim3(ntiles<Cfg>(M, g.C)), dim3(GEMM_THREADS), 0, s, a);
+  }
+}
+
+void launch_conv_wgrad_f32(const ConvF32Args& a0, hipStream_t s) {
+  ConvF32Args a = a0;
+  const ConvGeom& g = a.g;
+  using Cfg = TileCfg<float, 32, 64, 2, 2>;
+  const int M = g.Cout, N = g.KH * g.KW * g.C + (a.db ? 1 : 0), Kred = g.B * g.OH * g.OW;
+  const int tiles = ntiles<Cfg>(M, N);
+  // split the pixel reduction so ~512 workgroups fill the chip, at least 8 k-tiles each
+  int splits = (512 + tiles - 1) / tiles;
+  int chunk = (Kred + splits - 1) / splits;
+  chunk = (chunk + BK - 1) / BK * BK;
+  if (chunk < 8 * BK) chunk = 8 * BK;
+  splits = (Kred + chunk - 1) / chunk;
+  a.k_chunk = chunk;
+  hipLaunchKernelGGL(conv_wgrad_f32_kernel<Cfg>, dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, s, a);
+}
+
+void launch_unpool_f32(const float* g, const uint8_t* am, float* out, int B, int PH, int PW, int C, hipStream_t s) {
+  const long n = (long)B * PH * PW * C;
+  hipLaunchKernelGGL(unpool_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, am, out, PH, PW, C, n);
+}
+
+void launch_transpose_taps_f32(const float* in, float* out, int O, int T, int C, hipStream_t s) {
+  const long n = (long)O * T * C;
+  hipLaunchKernelGGL(transpose_taps_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, O, T, C);
+}
+
+}  // namespace dtfe

@@ -120,7 +120,10 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
     // ticket with a relaxed agent-scope add - no release fence (an agent-scope release writes the
     // XCD's dirty L2 lines back; one per split workgroup made the MNIST fc1 split-K GEMMs 2-4x
     // SLOWER than no split, profiles/r2_fc1_gemm_sweep.txt); the last arriver acquires once and
-    // reads every slab.
+    // reads every slab.  Valid on gfx950 (MI355X), the only ARCH this library builds for (csrc/build.py):
+    // sc1 buffer stores write through the XCD's L2 there, which is what makes the drained slab
+    // visible to a last arriver on another XCD without a release (MI355X_MICROARCH.md, valid forms);
+    // tests/test_kernels_gpu.py::test_splitk_combine_many_splits_deterministic pins it.
     const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(mine, (short)0, Cfg::BM * Cfg::BN * 4, 0x00020000);
     for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
       const int r = ch / CPR, c = (ch % CPR) * 8;

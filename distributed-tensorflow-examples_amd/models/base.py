@@ -70,6 +70,19 @@ class ModelDef:
     default_batch: int = 128
     default_steps: int = 1000
     needs_labels: bool = True
+    # compute dtypes the model's step program implements (--dtype); the first is the default
+    dtypes: tuple = ("fp32",)
+    dtype: str | None = None
+
+    def set_dtype(self, dt):
+        """--dtype routing: ``auto`` keeps the model's default; anything the program does not
+        implement is an error (never a silent fallback)."""
+        if dt in (None, "auto"):
+            self.dtype = self.dtypes[0]
+            return
+        if dt not in self.dtypes:
+            raise ValueError("--dtype=%s: model %r computes in %s" % (dt, self.name, "/".join(self.dtypes)))
+        self.dtype = dt
 
     def program(self, device, batch_size=None, seed: int = 0) -> StepProgram:  # pragma: no cover
         raise NotImplementedError

@@ -36,8 +36,6 @@ all-reduced over RCCL while the conv backward kernels still run.
 from __future__ import annotations
 
 import contextlib
-import math
-import os
 
 import torch
 
@@ -194,87 +192,59 @@ class MnistCnnTrainer:
         ra = P.range_of([n["out"], n["bout"]])
         rc = P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
         self.accum = [P.grad[ra[0]:ra[1]], P.grad[rc[0]:rc[1]], self.loss_sum, self.correct]
-        # backward branches that do not feed the critical path (head/fc1 weight grads, conv2
-        # weight grad) run on their own streams: inside the captured hipGraph they become
-        # parallel branches that fill the CUs the dgrad chain leaves idle.  conv2's weight
-        # grad gets its own partial-sum workspace (conv1's runs concurrently on the main stream).
-        # DTFE_CNN_BRANCHES (A/B only): "fc,c2" (default), "fc", "c2" or "none".  Measured-slower
-        # schedules were removed in round 3: the head weight gradient inside the fc1 dgrad launch
-        # (profiles/r2_cnn_head_fuse_ab.txt), one combined weight-gradient branch, the critical
-        # chain captured first (profiles/r2_cnn_branch_orders.txt), and the fc/head Adam as its own
-        # launch on the fc branch (313-325 vs 293 us; superseded by the fc1 GEMM Adam epilogue).
-        self.fused_gather = os.environ.get("DTFE_CNN_FUSED_GATHER", "1") != "0"
-        br = os.environ.get("DTFE_CNN_BRANCHES", "fc,c2").split(",")
-        self.par = self.device.type == "cuda" and bool(set(br) & {"fc", "c2"})
-        self.br_fc = self.par and "fc" in br
-        self.br_c2 = self.par and "c2" in br
-        # conv2's data gradient is captured before its weight gradient (same fork point): the graph
-        # runs the data gradient -> conv1 weight-gradient chain on the launch queue, first on the
-        # CUs, and the weight gradient (192 workgroups) fills in beside it - 0.2103-0.2126 vs
-        # 0.2159-0.2181 ms/step (profiles/r3_cnn_kernel_tuning.txt, r3y / r3z)
-        self.dgrad_first = os.environ.get("DTFE_CNN_DGRAD_FIRST", "1") == "1"
-        self.c2_blocks = int(os.environ.get("DTFE_CNN_C2_BLOCKS", "192" if self.dgrad_first else "128"))
-        # Data-parallel "late split" (default whenever an all-reduce is attached): the fc/head Adam
-        # (bucket 0, already reduced during the conv backward) runs while the small conv bucket's
-        # all-reduce is still in flight, so that collective's latency hides behind ~20 us of Adam.
-        self.opt_fc = self.opt_conv = None
-        self._apply = None
-        # (Adam for fc1 applied in the fc1 weight-gradient GEMM epilogue on one replica measured
-        # ~45 us/step slower - its traffic contends with the persistent conv2 backward kernels -
-        # and was removed: profiles/r3_cnn_fused_adam_ab.txt)
-        self.late_split = os.environ.get("DTFE_CNN_SPLIT_APPLY", "1") != "0"
-        # One replica, DTFE_CNN_FC_APPLY (where the fc/head Adam runs; its gradients are final once
-        # the grouped fc backward launch is done and that launch is its weights' last reader):
-        #   "join" - the whole-model Adam after the conv2 weight-gradient branch joins;
-        #   "main" - on the main chain after conv1's weight gradient, before the join (its ~18 us
-        #            hide the join's cross-queue wait), the conv Adam after the join;
-        #   "c2"   - at the end of the conv2 weight-gradient branch, the conv Adam after the join.
-        # (conv2's Adam can not move onto the branch: conv2's data gradient still reads its weights)
-        self.fc_apply = os.environ.get("DTFE_CNN_FC_APPLY", "join")
-        # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the
-        # forward streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the
-        # 2-stage variant (784 / 800 tiles, several workgroups per CU)
-        self.glds = self.device.type == "cuda" and os.environ.get("DTFE_CNN_GLDS", "1") != "0"
-        # DTFE_CNN_FC_GROUP=0: the fc backward as a forked side branch instead of one grouped launch
-        self.fc_group = self.par and os.environ.get("DTFE_CNN_FC_GROUP", "1") != "0"
-        # the head weight gradient as the grouped launch's first piece (4-column body, 84 VGPRs: the
-        # GEMM pieces keep 5 workgroups per CU) - 0.2033-0.2071 vs 0.2105-0.2124 ms/step as its own
-        # launch before the group (DTFE_CNN_HEAD_IN_GROUP=0; profiles/r3_cnn_kernel_tuning.txt r3ze)
-        self.head_in_group = self.fc_group and os.environ.get("DTFE_CNN_HEAD_IN_GROUP", "1") == "1"
+        # ONE schedule per world size (every measured-slower alternative was removed in round 4;
+        # their A/B tables stay in profiles/r2_cnn_branch_orders.txt, r2_cnn_head_fuse_ab.txt,
+        # r3_cnn_kernel_tuning.txt, r3_cnn_c2_after_ab.txt, r3_cnn_fused_adam_ab.txt):
+        #   * batch sampling + accumulator clearing + conv1 in one launch (standalone, B >= 256);
+        #   * the fc backward (head weight gradient, fc1 data + weight gradients) as ONE grouped
+        #     launch on the main stream;
+        #   * conv2's data gradient on the main stream, its weight gradient (192 workgroups, own
+        #     partial-sum workspace) on a forked branch captured after it, conv1's weight gradient
+        #     on the main stream beside it, then the join;
+        #   * one replica: the whole-model Adam after the join.  Data parallel: the fc/head bucket's
+        #     all-reduce is launched right after the grouped fc backward (before conv2's data
+        #     gradient), and the fc/head Adam runs while the small conv bucket is still in flight
+        #     ("late split"), then the conv Adam.
+        self.par = self.device.type == "cuda"
+        self.c2_blocks = 192
+        # (test hooks, not knobs: the separate gather launch and the whole-model apply with an
+        # all-reduce attached are the oracles the fused / split schedule is checked against)
+        self.fused_gather = True
+        self.late_split = True
+        # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the forward
+        # streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the 2-stage
+        # variant (784 / 800 tiles, several workgroups per CU)
         K1 = 7 * 7 * C2
-        # DTFE_CNN_TILES=fwd,dgrad,wgrad overrides the glds tile ids (A/B sweeps)
-        tiles = [int(t) for t in os.environ.get("DTFE_CNN_TILES", "8,12,12").split(",")]
-        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, tiles[0])
-        self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, tiles[1])
-        self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, tiles[2], b_ones_row=K1)
-        # fc1 forward split-K (deterministic last-arriver combine, write-through slabs): A/B only -
-        # 2 and 3 splits measured 1-2 % slower per step (profiles/r3_cnn_kernel_tuning.txt)
-        self.fwd_splits = int(os.environ.get("DTFE_CNN_FWD_SPLITS", "1"))
-        self.ws_fwd = None
-        if self.fwd_splits > 1 and self.t_fwd is not None:
-            self.ws_fwd = ops.split_workspace(d, self.fwd_splits, B, FC, self.t_fwd, private=True)
-        # head weight gradient: split-K over the batch with the deterministic last-arriver combine
-        # (fixed split order - no float atomics, so the step is bitwise reproducible); its own
-        # workspace, since it runs on the fc branch beside other GEMMs
-        self.head_gemm = os.environ.get("DTFE_CNN_HEAD_GEMM", "0") == "1" or batch > 1024
+        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 8)
+        self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
+        self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
+        # head weight gradient: the dedicated whole-batch kernel up to B = 1024, above that a split-K
+        # GEMM with the deterministic last-arriver combine (own workspace: it runs in the group)
+        self.head_gemm = batch > 1024
         self.head_splits = max(1, min(16, B // 128))
         bm, bn = ops.TILE_DIMS[4]
         ntiles = -(-NCLS // bm) * -(-(FC + 1) // bn)
         self.ws_head = (torch.empty(self.head_splits * ntiles * bm * bn, device=d, dtype=torch.float32),
-                        torch.zeros(ntiles, device=d, dtype=torch.int32)) if self.head_splits > 1 else None
+                        torch.zeros(ntiles, device=d, dtype=torch.int32)) if self.head_gemm else None
+        self.opt_fc = self.opt_conv = None
+        self._late = None        # (grad16, gscale) while a data-parallel step runs its split Adam
+        self.schedule = []       # launch order of the last step's milestones (host side = graph order)
+        self.logits = None
         if self.par:
-            self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
             self.ws_c2 = torch.empty(ops.wgrad_ws_floats(C2, KS * KS * C1), device=d, dtype=torch.float32)
 
     def _glds_tile(self, A, Bm, M, N, K, lda, ldb, tile, b_ones_row=-1):
-        if self.glds and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row):
+        if self.device.type == "cuda" and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row):
             return tile
         return None
 
     # ------------------------------------------------------------------
-    def forward_backward(self):
+    def forward(self, keep=None, logits=None):
+        """conv1 (+ the fused batch sampling in standalone mode), conv2, fc1 (+dropout), head.
+        ``keep=1.0`` and a ``logits`` buffer: the evaluation forward (no dropout)."""
         B = self.B
+        keep = self.keep if keep is None else keep
         fused = False
         if self.data is not None and self.device.type == "cuda" and B >= 256 and self.fused_gather:
             # standalone: batch sampling (advances data_ctr), accumulator clearing and conv1 in ONE launch
@@ -297,74 +267,52 @@ class MnistCnnTrainer:
                     pool=True, **self.ic2)
         K1 = 7 * 7 * C2
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU,
-                 keep=self.keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd, splits=self.fwd_splits,
-                 workspace=self.ws_fwd)
+                 keep=keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd)
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
-                      self.correct, None, scale=1.0 / B, inv_keep=1.0 / self.keep,
+                      self.correct, logits, scale=1.0 / B, inv_keep=1.0 / keep,
                       step_counter=self.data_ctr if fused else None)
-        main = torch.cuda.current_stream(self.device) if self.par else None
-        if self.fc_group:
-            # fc1 data gradient + fc1 weight gradient as ONE launch on the main
-            # stream (ops.gemm_group): no fork / join of an fc side branch, whose cross-queue edges
-            # cost 5-11 us of idle time each in the captured graph; the dispatcher starts the head and
-            # data-gradient workgroups first (lower grid ranges)
-            # (the head piece stays its own launch: its 10x8 accumulators per thread would set the
-            # grouped kernel's register allocation to 148 VGPRs, 3 workgroups per CU instead of 7)
-            if not self.head_in_group:
-                self._head_wgrad()
-            with ops.gemm_group(self.dzf):
-                if self.head_in_group:
-                    self._head_wgrad()   # recorded as the grouped launch's first piece
-                self._fc1_dgrad(B, K1)
-                self._fc1_wgrad(B, K1)
-            if self.allreduce is not None:
-                self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes)
-        else:
-            # weight-gradient branch of the fc layers (forked after head_xent), then the dgrad chain
-            with self._branch(self.s_fc, main) if self.br_fc else contextlib.nullcontext():
-                self._head_wgrad()
-                self._fc1_wgrad(B, K1)
-                if self.allreduce is not None:
-                    self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) forks off this branch
-            self._fc1_dgrad(B, K1)
-        def conv2_wgrad(forked=False):
-            ctx = contextlib.nullcontext()
-            if self.br_c2:
-                ctx = torch.cuda.stream(self.s_c2) if forked else self._branch(self.s_c2, main)
-            with ctx:
-                # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
-                ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                             workspace=self.ws_c2 if self.br_c2 else None,
-                             max_blocks=self.c2_blocks if self.br_c2 else 0, **self.ic2)
-                if self._apply is not None and self._apply[0] == "c2":
-                    self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
 
-        # (forking conv2's weight gradient after its data gradient, beside conv1's weight gradient,
-        # measured 0.242 vs 0.233 ms/step: profiles/r3_cnn_c2_after_ab.txt)
-        if self.dgrad_first and self.br_c2:
-            # fork point unchanged (after the fc backward); the data gradient's graph node is
-            # captured before the weight gradient's
+    def forward_backward(self):
+        B = self.B
+        K1 = 7 * 7 * C2
+        self.schedule = []
+        self.forward()
+        main = torch.cuda.current_stream(self.device) if self.par else None
+        # fc backward: head weight gradient, fc1 data gradient, fc1 weight gradient - ONE grouped
+        # launch on the GPU (ops.gemm_group; no fork / join of an fc side branch, whose cross-queue
+        # edges cost 5-11 us of idle time each in the captured graph)
+        with ops.gemm_group(self.dzf):
+            self._head_wgrad()
+            self._fc1_dgrad(B, K1)
+            self._fc1_wgrad(B, K1)
+        if self.allreduce is not None:
+            self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) overlaps the conv backward
+            self.schedule.append("allreduce:0")
+        # conv2's data gradient is captured before its weight gradient (same fork point): the graph
+        # runs the data gradient -> conv1 weight-gradient chain on the launch queue, first on the
+        # CUs, and the weight gradient (192 workgroups) fills in beside it - 0.2103-0.2126 vs
+        # 0.2159-0.2181 ms/step (profiles/r3_cnn_kernel_tuning.txt, r3y / r3z)
+        if self.par:
             self.s_c2.wait_stream(main)
-            self._conv2_dgrad()
-            conv2_wgrad(forked=True)
-        else:
-            conv2_wgrad()
-            self._conv2_dgrad()
+        self._conv2_dgrad()
+        self.schedule.append("conv2_dgrad")
+        with torch.cuda.stream(self.s_c2) if self.par else contextlib.nullcontext():
+            # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
+            ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
+                         workspace=self.ws_c2 if self.par else None,
+                         max_blocks=self.c2_blocks if self.par else 0, **self.ic2)
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
-        if self._apply is not None and self._apply[0] == "main":
-            self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
-        if self.br_fc and not self.fc_group:  # join the weight-grad branches
-            main.wait_stream(self.s_fc)
-        if self.br_c2:
+        if self.par:
             main.wait_stream(self.s_c2)
         if self.allreduce is not None:
             self.allreduce.launch(1)
-            if self._apply is not None and self._apply[0] == "late":
+            self.schedule.append("allreduce:1")
+            if self._late is not None:
                 self.allreduce.wait_bucket(0)   # fc/head Adam overlaps the conv bucket's all-reduce
-                self.opt_fc.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=0)
+                self.opt_fc.step(grad16=self._late[0], gscale=self._late[1], gs_inc=0)
             self.allreduce.wait()
-        if self._apply is not None:
-            self.opt_conv.step(grad16=self._apply[1], gscale=self._apply[2], gs_inc=1)
+        if self._late is not None:
+            self.opt_conv.step(grad16=self._late[0], gscale=self._late[1], gs_inc=1)
 
     def _head_wgrad(self):
         """head wgrad: dW[10][1024] = dlogit^T . H, db = sum dlogit (dedicated whole-batch kernel; the
@@ -392,22 +340,20 @@ class MnistCnnTrainer:
                     flip_taps=True, **self.ic2_dgrad)
 
     def _ensure_split(self):
-        """fc/head and conv optimizers over disjoint var lists, sharing one set of slot buffers."""
+        """fc/head and conv optimizers over disjoint var lists (the data-parallel "late split"),
+        sharing the whole-model optimizer's slot buffers and global step.  The conv optimizer
+        advances the whole-model optimizer's beta powers (what a checkpoint saves); the fc one
+        keeps an equal copy, advanced by itself - both apply once per step."""
         if self.opt_fc is None:
-            n_, cfg = self.names, self.opt.cfg
-            self.opt_fc = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("out", "bout", "bd1", "wd1")],
-                                    global_step=self.global_step)
-            self.opt_conv = Optimizer(cfg, self.P, var_list=[n_[k] for k in ("wc2", "bc2", "wc1", "bc1")],
-                                      global_step=self.global_step)
-            self.opt_conv.s1, self.opt_conv.s2 = self.opt_fc.s1, self.opt_fc.s2
-
-    @staticmethod
-    def _branch(stream, main):
-        """Run the enclosed launches on ``stream`` forked from ``main`` (no-op without one)."""
-        if stream is None:
-            return contextlib.nullcontext()
-        stream.wait_stream(main)
-        return torch.cuda.stream(stream)
+            n_, o = self.names, self.opt
+            lists = ([n_[k] for k in ("out", "bout", "bd1", "wd1")], [n_[k] for k in ("wc2", "bc2", "wc1", "bc1")])
+            self.opt_fc, self.opt_conv = (Optimizer(o.cfg, self.P, var_list=v, global_step=o.global_step)
+                                          for v in lists)
+            for s in (self.opt_fc, self.opt_conv):
+                s.s1, s.s2 = o.s1, o.s2
+            if o.beta_pow is not None:
+                self.opt_fc.beta_pow.copy_(o.beta_pow)
+                self.opt_conv.beta_pow = o.beta_pow
 
     def apply(self):
         self.opt.step(gscale=1.0 / self.world)
@@ -416,27 +362,16 @@ class MnistCnnTrainer:
         """One training step: forward, backward (+ all-reduce), Adam.  ``grad16``: the all-reduced
         bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
         gscale = 1.0 / self.world if gscale is None else gscale
-        mode = None
-        if self.par and self.br_fc and self.late_split and self.allreduce is not None:
-            mode = "late"
-        elif self.br_c2 and self.fc_group and self.fc_apply in ("main", "c2") and self.allreduce is None:
-            mode = self.fc_apply
-        if mode is None or (self.opt_fc is None and self.global_step_started()):
+        if self.allreduce is None or not self.par or not self.late_split:
             self.forward_backward()
             self.opt.step(grad16=grad16, gscale=gscale)
-            self._whole_steps = getattr(self, "_whole_steps", 0) + 1
             return
         self._ensure_split()
-        self._apply = (mode, grad16, gscale)
+        self._late = (grad16, gscale)
         try:
             self.forward_backward()
         finally:
-            self._apply = None
-
-    def global_step_started(self) -> bool:
-        """True once the whole-model optimizer has applied a step (its slots then hold the state,
-        so the schedule must not switch to the split optimizers)."""
-        return getattr(self, "_whole_steps", 0) > 0
+            self._late = None
 
     def flops_per_image(self) -> float:
         """Training FLOPs per image (fwd + dgrad + wgrad of every GEMM-shaped op)."""
@@ -445,6 +380,132 @@ class MnistCnnTrainer:
         f1 = 2 * 7 * 7 * C2 * FC
         f2 = 2 * FC * NCLS
         return c1 * 2 + c2 * 3 + f1 * 3 + f2 * 3  # conv1 has no dgrad
+
+
+class MnistCnnF32Trainer(MnistCnnTrainer):
+    """The same CNN step at the reference's precision (``--dtype fp32``): fp32 activations and
+    gradients, every product on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain per
+    dot product), fp32 weights read straight from the masters, the same fused TF1 Adam.
+
+      conv1 / conv2   conv_f32.hip implicit GEMM, bias + ReLU + 2x2 max-pool + argmax epilogue
+      fc1             dense fp32 GEMM, bias + ReLU + dropout epilogue
+      head            fp32 GEMM -> softmax-xent kernel (loss, hits, dlogits)
+      head / fc1 dW   fp32 GEMMs, bias gradient through a ones column
+      dH, dP2         fp32 GEMMs with the 1/keep * ReLU'(h) and ReLU'(p2) epilogues
+      un-pool         argmax routing kernel (dP2 -> dY2, dP1 -> dY1)
+      conv2 dX / dW   conv_f32.hip (ReLU'(p1) epilogue; weight grad + bias grad atomics)
+      conv1 dW        conv_f32.hip
+    A parity path, not the benchmarked one: no fused sampling, no hipGraph-specific scheduling,
+    one stream."""
+
+    def __init__(self, batch, device, lr: float = 1e-3, keep_prob: float = 0.75, seed: int = 0, data=None,
+                 allreduce=None, world_size: int = 1, P: FlatParams | None = None, standalone: bool = True,
+                 rank: int = 0):
+        self.B = batch
+        self.device = torch.device(device)
+        if self.device.type == "cuda":
+            ops.require()
+        self.keep = keep_prob
+        self.seed = seed + 7919 * rank
+        self.world = world_size
+        self.allreduce = allreduce
+        specs, self.names = var_specs()
+        self.P = P if P is not None else FlatParams(specs, self.device, seed=seed)
+        self.global_step = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.opt = self.data = None
+        if standalone:
+            self.opt = Optimizer(OptimizerConfig(kind="adam", lr=lr), self.P, global_step=self.global_step)
+            self.data = data or SyntheticMnist(60000, self.device, seed=self.seed + 17)
+        d, B, f = self.device, batch, torch.float32
+        self.x = torch.empty(B, IMG, IMG, 1, device=d, dtype=f)
+        self.labels = torch.empty(B, dtype=torch.int32, device=d)
+        self.p1 = torch.empty(B, 14, 14, C1, device=d, dtype=f)
+        self.a1 = torch.empty(B, 14, 14, C1, device=d, dtype=torch.uint8)
+        self.p2 = torch.empty(B, 7, 7, C2, device=d, dtype=f)
+        self.a2 = torch.empty(B, 7, 7, C2, device=d, dtype=torch.uint8)
+        self.h = torch.empty(B, FC, device=d, dtype=f)
+        self.logits = torch.empty(B, NCLS, device=d, dtype=f)
+        self.dlogits = torch.empty(B, NCLS, device=d, dtype=f)
+        self.dzf = torch.empty(B, FC, device=d, dtype=f)
+        self.dp2 = torch.empty(B, 7, 7, C2, device=d, dtype=f)
+        self.dy2 = torch.empty(B, 14, 14, C2, device=d, dtype=f)
+        self.dp1 = torch.empty(B, 14, 14, C1, device=d, dtype=f)
+        self.dy1 = torch.empty(B, IMG, IMG, C1, device=d, dtype=f)
+        self.wt2 = torch.empty(C1, KS * KS, C2, device=d, dtype=f)
+        self.loss_sum = torch.zeros(1, device=d)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=d)
+        self.data_ctr = torch.zeros(1, dtype=torch.int64, device=d)
+        self.data_done = torch.zeros(1, dtype=torch.int32, device=d)
+        self.g1 = dict(B=B, H=IMG, W=IMG, C=1, Cout=C1, OH=IMG, OW=IMG, KH=KS, KW=KS, stride=1, pad=2)
+        self.g2 = dict(B=B, H=14, W=14, C=C1, Cout=C2, OH=14, OW=14, KH=KS, KW=KS, stride=1, pad=2)
+        n = self.names
+        self.w = {k: self.P.view(n[k]) for k in ("wc1", "wc2", "wd1", "out")}
+        self.b = {k: self.P.view(n[k]) for k in ("bc1", "bc2", "bd1", "bout")}
+        self.gw = {k: self.P.gview(n[k]) for k in ("wc1", "wc2", "wd1", "out", "bc1", "bc2", "bd1", "bout")}
+        lo1, hi1 = self.P.range_of([n["out"], n["bout"], n["bd1"], n["wd1"]])
+        lo2, hi2 = self.P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
+        self.buckets = [(lo1, hi1), (lo2, hi2)]
+        rc = self.P.range_of([n["wc2"], n["bc2"], n["wc1"], n["bc1"]])
+        self.accum = [self.P.grad[rc[0]:rc[1]], self.loss_sum, self.correct]  # atomically accumulated
+        self.par = False
+        self.late_split = False
+        self.opt_fc = self.opt_conv = None
+        self._late = None
+        self.schedule = []
+
+    def forward(self, keep=None, logits=None):
+        B, K1 = self.B, 7 * 7 * C2
+        keep = self.keep if keep is None else keep
+        if self.data is not None:
+            ops.gather_rows(self.data.images, self.x.view(B, -1), None, self.data.labels, self.labels,
+                            seed=self.seed + 1, counter=self.data_ctr, done=self.data_done, zero=self.accum)
+        else:
+            for t in self.accum:
+                t.zero_()
+        ops.conv_fwd(self.x, self.w["wc1"], self.b["bc1"], self.p1, self.a1, self.g1, pool=True, act=ops.ACT_RELU)
+        ops.conv_fwd(self.p1, self.w["wc2"], self.b["bc2"], self.p2, self.a2, self.g2, pool=True, act=ops.ACT_RELU)
+        ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU, keep=keep,
+                 seed=self.seed + 2, counter=self.data_ctr)
+        ops.gemm(self.h, self.w["out"], self.logits, M=B, N=NCLS, K=FC, bias=self.b["bout"])
+        if logits is not None and logits is not self.logits:
+            logits.copy_(self.logits)
+        ops.softmax_xent(self.logits, labels_i=self.labels, scale=1.0 / B, dlogits=self.dlogits,
+                         loss_sum=self.loss_sum, correct=self.correct)
+        self._keep_used = keep
+
+    def forward_backward(self):
+        B, K1 = self.B, 7 * 7 * C2
+        self.schedule = []
+        self.forward()
+        if self.data is not None:
+            self.data_ctr += 1  # next step's batch / dropout stream (the bf16 path's head advances it)
+        inv_keep = 1.0 / self._keep_used
+        # head: dW = dlogits^T . h (+ bias column), dh = dlogits . W * 1/keep * ReLU'(h)
+        ops.gemm(self.dlogits, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=NCLS,
+                 bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"])
+        ops.gemm(self.dlogits, self.w["out"], self.dzf, M=B, N=FC, K=NCLS, bmode=ops.RMAJ, ldb=FC, alpha=inv_keep,
+                 aux=self.h, aux_act=ops.ACT_RELU)
+        # fc1: dW = dz^T . p2 (+ bias column), dP2 = dz . W1 * ReLU'(p2)
+        ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
+                 ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
+        ops.gemm(self.dzf, self.w["wd1"], self.dp2, M=B, N=K1, K=FC, bmode=ops.RMAJ, ldb=K1, aux=self.p2,
+                 aux_act=ops.ACT_RELU)
+        if self.allreduce is not None:
+            self.allreduce.launch(0)
+            self.schedule.append("allreduce:0")
+        # conv2: un-pool, data gradient (ReLU'(p1) epilogue), weight + bias gradient
+        ops.unpool_f32(self.dp2, self.a2, self.dy2)
+        ops.transpose_taps_f32(self.w["wc2"], self.wt2, C2, KS * KS, C1)
+        ops.conv_dgrad(self.dy2, self.wt2, self.dp1, self.g2, relu_mask=self.p1)
+        self.schedule.append("conv2_dgrad")
+        ops.conv_wgrad(self.dy2, self.p1, self.gw["wc2"], self.gw["bc2"], self.g2)
+        # conv1: un-pool, weight + bias gradient
+        ops.unpool_f32(self.dp1, self.a1, self.dy1)
+        ops.conv_wgrad(self.dy1, self.x, self.gw["wc1"], self.gw["bc1"], self.g1)
+        if self.allreduce is not None:
+            self.allreduce.launch(1)
+            self.schedule.append("allreduce:1")
+            self.allreduce.wait()
 
 
 # ----------------------------------------------------------------------------
@@ -463,6 +524,7 @@ class MnistCnnModel(ModelDef):
     default_steps = 500
     gs_increments = 1
     needs_labels = True
+    dtypes = ("bf16", "fp32")
 
     def __init__(self, lr: float = 1e-3):
         self.specs, self.names = var_specs()
@@ -480,13 +542,14 @@ class CnnProgram(StepProgram):
 
     def __init__(self, model, device, batch_size: int, seed: int = 0):
         super().__init__(model, device, batch_size, seed)
-        self.core = MnistCnnTrainer(batch_size, self.device, seed=seed, P=self.P, standalone=False)
+        cls = MnistCnnF32Trainer if getattr(model, "dtype", None) == "fp32" else MnistCnnTrainer
+        self.core = cls(batch_size, self.device, seed=seed, P=self.P, standalone=False)
 
     def load_batch(self, batch):
         x, y = batch
         B = self.batch_size
         c = self.core
-        c.x.copy_(x.reshape(B, IMG, IMG, 1).to(c.x.dtype))
+        c.x.copy_(x.reshape(B, IMG, IMG, 1).to(c.x.dtype))  # bf16 or fp32 (--dtype)
         lab = y.reshape(B, -1)
         c.labels.copy_((lab.argmax(1) if lab.shape[1] > 1 else lab[:, 0]).to(c.labels.dtype))
         c.data_ctr += 1  # dropout stream position (the HBM gather advances it in standalone mode)
@@ -495,6 +558,38 @@ class CnnProgram(StepProgram):
         self.core.forward_backward()
         return {"loss": ScaledScalar(self.core.loss_sum, 1.0 / self.batch_size), "correct": self.core.correct}
 
-    def evaluate(self, images, labels) -> float:
-        raise NotImplementedError("the CNN example has no evaluation step")
+    def attach_data_parallel(self, allreduce, opt):
+        """--mode=allreduce on the GPU: the trainer runs the benchmarked schedule (fc bucket's
+        all-reduce launched right after the fc backward, before conv2's data gradient; split Adam
+        overlapping the conv bucket) with ``opt`` - train.py's whole-model optimizer, whose slots
+        and beta powers the Supervisor checkpoints - as the owner of the optimizer state."""
+        self.core.allreduce = allreduce
+        self.core.opt = opt
 
+    def train_step(self, grad16=None, gscale=1.0):
+        """Forward, backward, all-reduce (when attached) and Adam in the trainer's own order."""
+        self.core.step(grad16=grad16, gscale=gscale)
+        return {"loss": ScaledScalar(self.core.loss_sum, 1.0 / self.batch_size), "correct": self.core.correct}
+
+    @torch.no_grad()
+    def evaluate(self, images, labels) -> float:
+        """Top-1 accuracy of the current weights (the CNN analog of LSTM:134-138): the training
+        forward without dropout (keep 1.0), logits out of the fused head, argmax against the
+        labels.  Any number of images, in program-batch chunks (the last one padded by repeating
+        rows; only the real rows count).  Parameters are untouched; the loss / hit accumulators
+        and the dropout stream position are restored."""
+        c, B, n = self.core, self.batch_size, images.shape[0]
+        if c.logits is None:
+            c.logits = torch.empty(B, NCLS, device=self.device, dtype=torch.float32)
+        ctr = c.data_ctr.clone()
+        hits = 0
+        for lo in range(0, n, B):
+            m = min(B, n - lo)
+            idx = torch.arange(lo, lo + B, device=images.device).clamp_max(n - 1)
+            self.load_batch((images[idx], labels[idx]))
+            c.forward(keep=1.0, logits=c.logits)
+            hits += int((c.logits[:m].argmax(1) == c.labels[:m].long()).sum().item())
+        c.data_ctr.copy_(ctr)
+        c.loss_sum.zero_()
+        c.correct.zero_()
+        return hits / n

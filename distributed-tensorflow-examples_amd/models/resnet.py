@@ -449,6 +449,7 @@ def build(arch, reg):
 
 class ResNetModel(ModelDef):
     default_steps = 1000
+    dtypes = ("bf16",)
 
     def __init__(self, lr: float = 0.1, arch: str = "resnet20"):
         self.name = arch

@@ -498,6 +498,26 @@ def conv_wgrad(dz, x, dw, db, g, scale=1.0):
     return dw
 
 
+def unpool_f32(g, argmax, out):
+    """out[B][2PH][2PW][C] (fp32) = g routed to the argmax position of each 2x2 window, zeros
+    elsewhere (the max-pool gradient; the ReLU mask is already in g)."""
+    B, PH, PW, C = g.shape
+    if g.is_cuda:
+        require().unpool_f32(g, argmax, out, B, PH, PW, C)
+        return out
+    _unpool_ref(g.reshape(-1).float(), torch.ones(B, PH, PW, C), argmax, PH, PW, C, out)
+    return out
+
+
+def transpose_taps_f32(w, out, O, T, C):
+    """out[C][T][O] = w[O][T][C] (a conv weight laid out for its data gradient)."""
+    if w.is_cuda:
+        require().transpose_taps_f32(w, out, O, T, C)
+        return out
+    out.view(-1)[:] = w.reshape(O, T, C).permute(2, 1, 0).reshape(-1)
+    return out
+
+
 # -------------------------------------------------------------------- head
 def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0, step_counter=None):
     """Per-row classifier head: logits, softmax-xent (loss/correct sums), dlogit rows (bf16 [B][ld] into

@@ -346,7 +346,7 @@ def run_worker_ps(flags, model, server, device, log):
             metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000, images_per_sec=ips, **sc)
             local_step += 1
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
-        if model.name == "lstm":
+        if model.name in ("lstm", "cnn"):
             link.pull() if link is not None else client.pull()
             test_len = 128
             acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
@@ -379,6 +379,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         max_to_keep=flags.max_to_keep, log=log)
     sv.prepare()
     ar = None
+    # programs with their own data-parallel schedule (the MNIST CNN: the one bench.py times) run it
+    # here too, unless --bucket_mb asks for generic flat-buffer buckets
+    native = (hasattr(prog, "attach_data_parallel") and len(opts) == 1
+              and (world == 1 or flags.bucket_mb is None))
     if world > 1:
         # chief's (possibly restored) state is the starting point of every replica
         dist.broadcast(prog.P.master, src=0, group=group)
@@ -390,7 +394,7 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         prog.P.refresh_copies()
         # on GPUs the buckets go through dtfe's own RCCL communicator (capturable: the whole step,
         # all-reduce included, replays as one hipGraph); gloo / CPU keeps ProcessGroup collectives
-        bks = _buckets(prog.P, flags.bucket_mb)
+        bks = prog.core.buckets if native else _buckets(prog.P, flags.bucket_mb)
         comm = None
         # (gloo + --comm=ipc: several ranks sharing one GPU rehearse the in-graph IPC path)
         if device.type == "cuda" and flags.comm != "pg" and (dist.get_backend(group) != "gloo" or flags.comm == "ipc"):
@@ -399,8 +403,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                              mode=flags.comm, log=log if is_chief else None)
         ar = BucketAllReduce(prog.P.grad, bks, group=group, comm=comm,
                              comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
-        if hasattr(prog, "grad_ready"):  # programs that report backward progress overlap the all-reduce
+        if not native and hasattr(prog, "grad_ready"):  # programs reporting backward progress overlap the all-reduce
             prog.grad_ready = ar.ready
+    if native:
+        prog.attach_data_parallel(ar, opts[0])
     data = read_data_sets(model, "" if flags.synthetic else flags.data_dir, one_hot=True, seed=flags.seed * 1000 + rank + 1,
                           log=log if is_chief else (lambda *_: None))
     feeder = Feeder(data, prog, device)
@@ -415,6 +421,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
     faults = FaultInjector("worker", rank, log=log)
 
     def train_step():
+        if native:  # forward, backward, overlapped all-reduce and Adam in the program's own order
+            with phase("step"):
+                state["m"] = prog.train_step(grad16=ar.grad16 if ar is not None else None, gscale=1.0 / world)
+            return
         with phase("fwd+bwd"):
             state["m"] = prog.compute_grads()
         g16 = None
@@ -444,6 +454,8 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
             elapsed = time.time() - t0
             ips = prog.batch_size * world / max(elapsed, 1e-9)
             sc = scalar_metrics(state.get("m"))
+            if local_step == 0 and native and ar is not None and is_chief:
+                log("schedule: " + " < ".join(prog.core.schedule))
             if local_step % flags.log_every == 0:
                 log(step_line(step, local_step, elapsed * 1000, flags.py2_print))
                 if timer is not None:
@@ -462,7 +474,7 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         log("Total Time: %3.2fs" % float(time.time() - begin_time))
         if world > 1 and flags.check_pull:  # synchronous replicas: identical parameters on every worker
             log("params checksum %.12e" % float(prog.P.master.double().sum().item()))
-        if model.name == "lstm":  # every worker evaluates and prints, as LSTM:134-138
+        if model.name in ("lstm", "cnn"):  # every worker evaluates and prints, as LSTM:134-138
             test_len = 128
             acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
                                 torch.from_numpy(data.test.labels[:test_len]).to(device))
@@ -509,6 +521,10 @@ def run(model_name: str, argv=None, log=_print):
     flags = flagmod.parse(argv, model_defaults=dict(batch_size=m0.default_batch, num_steps=m0.default_steps,
                                                     learning_rate=lr), prog="distributed_%s.py" % model_name)
     model = cls(lr=flags.learning_rate)
+    try:
+        model.set_dtype(flags.dtype)  # --dtype: the model's program must implement it (no silent fallback)
+    except ValueError as e:
+        raise SystemExit(str(e))
     torch.manual_seed(flags.seed)
     np.random.seed(flags.seed)
     mode = flags.mode or ("ps" if flags.ps_hosts else ("allreduce" if flags.worker_hosts else "local"))

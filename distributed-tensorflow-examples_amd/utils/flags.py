@@ -65,12 +65,12 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     ap.add_argument("--log_every", type=int, default=1, help="print the per-step line every N local steps")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--bucket_mb", type=float, default=None,
-                    help="all-reduce bucket size in MB of fp32 gradient (default: the model's own buckets, else "
-                         "%.0f MB: measured on the IPC / RCCL engines, see parallel/comm.py DEFAULT_BUCKET_MB)" % 16)
+                    help="all-reduce bucket size in MB of fp32 gradient (default: the model's own buckets - the "
+                         "MNIST CNN's [head + fc1] / [convs] - else parallel/comm.py DEFAULT_BUCKET_MB); > 0")
     ap.add_argument("--dtype", choices=["auto", "fp32", "bf16"], default="auto",
-                    help="compute dtype: fp32 = exact-fp32 kernels (the reference's precision), bf16 = bf16 MFMA "
-                         "with fp32 accumulation / masters; auto = each model's default (reference models fp32, "
-                         "CNN / ResNets bf16)")
+                    help="compute dtype: fp32 = exact-fp32 MFMA kernels and fp32 activations (the reference's "
+                         "precision), bf16 = bf16 MFMA with fp32 accumulation / masters; auto = the model's default. "
+                         "GAN / autoencoder / LSTM / softmax: fp32 only; CNN: bf16 (default) or fp32; ResNets: bf16")
     ap.add_argument("--comm", choices=["auto", "rccl", "ipc", "pg"], default="auto",
                     help="all-reduce engine on GPUs: auto = faster of RCCL / hipIpc two-shot per bucket size "
                          "(both in-graph); pg = torch.distributed ProcessGroupNCCL (eager)")

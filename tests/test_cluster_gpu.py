@@ -58,8 +58,14 @@ def test_cnn_allreduce_two_workers_ipc_in_graph(tmp_path):
         assert max(_gs(out[("worker", w)])) == 12
     sums = [[l for l in out[("worker", w)] if l.startswith("params checksum")] for w in (0, 1)]
     assert sums[0] and sums[0] == sums[1], sums
+    # the CLI runs the benchmarked schedule: the fc bucket's all-reduce is launched right after the
+    # grouped fc backward, before conv2's data gradient, the conv bucket after the conv backward
+    sched = [l for l in out[("worker", 0)] if l.startswith("schedule: ")]
+    assert sched == ["schedule: allreduce:0 < conv2_dgrad < allreduce:1"], sched
+    for w in (0, 1):  # the CNN prints the reference's Test-Accuracy line (LSTM:134-138)
+        assert any(l.startswith("Test-Accuracy: ") for l in out[("worker", w)])
     t = ckpt.load_bundle(ckpt.latest_checkpoint(md))
-    assert "Variable_1/Adam" in t
+    assert "Variable_1/Adam" in t and "beta1_power" in t
 
 
 @pytest.mark.parametrize("hogwild", [False, True])

@@ -561,3 +561,25 @@ def test_wgrad_tallk_matches_fp64(M, N, K, splits):
     assert (bias.cpu().double() - rb).abs().max().item() <= 1e-4 * (rb.abs().max().item() + 1)
 
 
+
+
+@pytest.mark.parametrize("dtype,tile", [(torch.float32, 0), (torch.bfloat16, 0), (torch.bfloat16, 2)])
+def test_splitk_combine_many_splits_deterministic(dtype, tile):
+    """Write-through split-K hand-off (gemm_dense.h): 8 split workgroups per tile on a small M x N,
+    so every tile's last arriver reads 7 slabs written by workgroups on other XCDs.  Ten launches
+    in one process must agree bit for bit, and with the fp64 oracle."""
+    torch.manual_seed(3)
+    M, N, K = 64, 96, 8 * 512
+    A = torch.randn(M, K, device=DEV).to(dtype)
+    B = torch.randn(N, K, device=DEV).to(dtype)
+    ref = (A.double() @ B.double().t()).float()
+    outs = []
+    for _ in range(10):
+        out = torch.full((M, N), 7.0, device=DEV)
+        ops.gemm(A, B, out, M=M, N=N, K=K, splits=8, tile=tile)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    err = (outs[0] - ref).abs().max().item()
+    assert err < 1e-3 * ref.abs().max().item() + 1e-3, err

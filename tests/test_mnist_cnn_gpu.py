@@ -88,14 +88,12 @@ def test_cnn_trains_and_graph_replays():
     assert int(tr.global_step.item()) == 60
 
 
-@pytest.mark.parametrize("branches", ["fc,c2", "fc", "c2", "none"])
-def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
+def test_cnn_repeated_step_grads_do_not_accumulate():
     """Only the atomically-accumulated grads are cleared per step (fused into the batch gather);
     every other gradient must be fully overwritten: the same batch twice -> the same grads,
     and the result matches autograd after a previous step left garbage behind."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
-    monkeypatch.setenv("DTFE_CNN_BRANCHES", branches)
     tr = MnistCnnTrainer(64, "cuda", keep_prob=1.0, seed=5)
     tr.P.grad.fill_(7.0)            # stale values everywhere
     tr.loss_sum.fill_(3.0)
@@ -115,15 +113,15 @@ def test_cnn_repeated_step_grads_do_not_accumulate(branches, monkeypatch):
         assert ((got - gref).norm() / (gref.norm() + 1e-12)).item() < 3e-2, k
 
 
-def test_cnn_fused_sampling_conv1_matches_separate_gather(monkeypatch):
+def test_cnn_fused_sampling_conv1_matches_separate_gather():
     """B >= 256: batch sampling + accumulator clearing fused into conv1's forward launch must
     give the same batch, labels, activations and gradients as gather kernel + conv1."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
     res = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("DTFE_CNN_FUSED_GATHER", fused)
         tr = MnistCnnTrainer(256, "cuda", keep_prob=1.0, seed=7)
+        tr.fused_gather = fused == "1"
         tr.P.grad.fill_(5.0)
         for _ in range(2):            # second step: counter advanced once, stale accumulators cleared
             tr.forward_backward()
@@ -173,7 +171,7 @@ def test_cnn_bench_shaped_step_matches_autograd(B):
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
     tr = MnistCnnTrainer(B, "cuda", keep_prob=1.0, seed=11)
-    assert tr.fused_gather and tr.br_c2 and tr.br_fc
+    assert tr.fused_gather and tr.par
     tr.P.grad.fill_(3.0)               # stale values: every gradient must be overwritten / cleared
     tr.forward_backward()
     torch.cuda.synchronize()
@@ -238,21 +236,88 @@ def test_cnn_training_is_bitwise_reproducible(B):
     assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
 
 
-@pytest.mark.parametrize("where", ["main", "c2"])
-def test_cnn_fc_apply_placement_matches_whole_apply(where, monkeypatch):
-    """DTFE_CNN_FC_APPLY=main|c2 (one replica): the fc/head Adam before the join (main chain or the
-    conv2 weight-gradient branch) and the conv Adam after it follow the whole-model apply's
-    trajectory bit for bit."""
-    from dtfe.models.mnist_cnn import MnistCnnTrainer
+def test_cnn_evaluate_matches_argmax_agreement():
+    """CnnProgram.evaluate (the Test-Accuracy line) = argmax agreement of the no-dropout forward
+    with fp32 autograd's logits on a fixed batch, including a padded last chunk."""
+    from dtfe.models.mnist_cnn import MnistCnnModel
 
-    outs = []
-    for mode in ("join", where):
-        monkeypatch.setenv("DTFE_CNN_FC_APPLY", mode)
-        tr = MnistCnnTrainer(1024, "cuda", seed=9)
-        for _ in range(4):
-            tr.step()
+    model = MnistCnnModel()
+    prog = model.program(torch.device("cuda"), 64, seed=2)
+    g = torch.Generator().manual_seed(1)
+    n = 100
+    imgs = torch.rand(n, 784, generator=g).cuda()
+    lab = torch.nn.functional.one_hot(torch.randint(0, 10, (n,), generator=g), 10).float().cuda()
+    acc = prog.evaluate(imgs, lab)
+    c = prog.core
+    assert c.loss_sum.item() == 0.0 and int(c.correct.item()) == 0
+    hits = 0
+    for lo in range(0, n, 64):
+        m = min(64, n - lo)
+        idx = torch.arange(lo, lo + 64).clamp_max(n - 1)
+        prog.load_batch((imgs[idx.cuda()], lab[idx.cuda()]))
+        c.forward(keep=1.0, logits=c.logits)
         torch.cuda.synchronize()
-        assert (tr.opt_fc is not None) == (mode != "join")
-        assert int(tr.global_step.item()) == 4
-        outs.append(tr.P.master.clone())
-    assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
+        _, logits_ref = _reference_forward(c)
+        hits += int((logits_ref[:m].argmax(1).cuda() == lab[lo:lo + m].argmax(1)).sum())
+    # the bf16 forward can flip a near-tie: allow one row of slack in 100
+    assert abs(acc * n - hits) <= 1, (acc, hits / n)
+
+
+def _reference_forward(trainer):
+    P, n = trainer.P, trainer.names
+    x = trainer.x.float().permute(0, 3, 1, 2).cpu()
+
+    def w(k):
+        return P.view(n[k]).detach().cpu().to(torch.bfloat16).float()
+
+    def b(k):
+        return P.view(n[k]).detach().cpu().float()
+
+    z = F.conv2d(x, w("wc1").permute(0, 3, 1, 2), b("bc1"), padding=2)
+    z = q(F.max_pool2d(F.relu(z), 2))
+    z = F.conv2d(z, w("wc2").permute(0, 3, 1, 2), b("bc2"), padding=2)
+    z = q(F.max_pool2d(F.relu(z), 2))
+    z = z.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+    h = q(F.relu(z @ w("wd1").t() + b("bd1")))
+    return h, h @ w("out").t() + b("bout")
+
+
+def test_cnn_fp32_step_matches_fp32_autograd():
+    """--dtype fp32: the exact-fp32 MFMA step (conv_f32.hip convs, fp32 dense GEMMs, softmax-xent)
+    against fp32 autograd of the same network on the CPU, dropout off: <= 1e-4 relative."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_cnn_cpu import _batch, autograd_f32
+    from dtfe.models.mnist_cnn import MnistCnnModel
+
+    m = MnistCnnModel()
+    m.set_dtype("fp32")
+    prog = m.program(torch.device("cuda"), 128, seed=3)
+    prog.core.keep = 1.0
+    x, y = _batch(128, seed=2)
+    prog.load_batch((x.cuda(), y.cuda()))
+    prog.P.grad.fill_(9.0)             # stale values: stored gradients overwritten, accumulated ones cleared
+    met = prog.compute_grads()
+    torch.cuda.synchronize()
+    core = prog.core
+    cpu = type("C", (), {})()
+    cpu.P = type("P", (), {"view": staticmethod(lambda k: core.P.view(k).cpu())})()
+    cpu.names, cpu.x, cpu.labels = core.names, core.x.cpu(), core.labels.cpu()
+    loss_ref, grads, _ = autograd_f32(cpu)
+    assert abs(met["loss"].item() - loss_ref) <= 1e-5 * abs(loss_ref), (met["loss"].item(), loss_ref)
+    errs = {k: ((core.gw[k].cpu() - g).norm() / (g.norm() + 1e-12)).item() for k, g in grads.items()}
+    assert all(e <= 1e-4 for e in errs.values()), sorted(errs.items(), key=lambda kv: -kv[1])
+
+
+def test_cnn_fp32_local_run_trains(capsys, tmp_path):
+    """train.run with --dtype fp32 on the GPU (local mode, hipGraph-captured step): loss lines and
+    the Test-Accuracy line print, the global step advances."""
+    from dtfe import train
+
+    rc = train.run("cnn", ["--mode=local", "--device=cuda", "--synthetic", "--num_steps=4", "--dtype=fp32",
+                           "--batch_size=64", "--save_model_secs=0", "--model_dir=" + str(tmp_path / "ck")])
+    out = capsys.readouterr().out
+    assert rc == 0
+    assert "Global step 4 Local step 3" in out and "Test-Accuracy: " in out, out[-2000:]

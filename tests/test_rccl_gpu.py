@@ -144,17 +144,17 @@ def test_make_comm_routes(pg, mode):
 
 
 @pytest.mark.parametrize("split", ["1", "0"])
-def test_cnn_late_split_apply_with_allreduce(pg, split, monkeypatch):
+def test_cnn_late_split_apply_with_allreduce(pg, split):
     """With an all-reduce attached, step() applies the fc/head bucket while the conv bucket is
     still being reduced (split optimizers, per-bucket completion events); the trajectory must
     equal the whole-model apply."""
     from dtfe.models.mnist_cnn import MnistCnnTrainer
 
-    monkeypatch.setenv("DTFE_CNN_SPLIT_APPLY", split)
     dev = torch.device("cuda", 0)
     comm = RcclComm(dev)
     try:
         tr = MnistCnnTrainer(256, dev, seed=4)
+        tr.late_split = split == "1"
         ar = BucketAllReduce(tr.P.grad, tr.buckets, comm=comm, comm_dtype=torch.bfloat16)
         tr.allreduce = ar
         runner = StepGraph(lambda: tr.step(grad16=ar.grad16, gscale=1.0), warmup=2, enabled=True,
