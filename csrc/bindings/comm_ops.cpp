@@ -105,6 +105,36 @@ void rccl_broadcast(Tensor buf, int64_t root, int64_t handle) {
              "ncclBroadcast");
 }
 
+// ncclCommGetAsyncError of the communicator: 0 = healthy, else the ncclResult_t code (a peer
+// failed, a network / remote error surfaced).  Host-only, never blocks on the device: the comm
+// watchdog (parallel/health.py CommWatchdog) polls it from its own thread.
+int64_t rccl_status(int64_t handle) {
+  ncclComm_t comm;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (handle < 0 || handle >= (int64_t)g_comms.size() || g_comms[handle] == nullptr) return -1;
+    comm = g_comms[handle];
+  }
+  ncclResult_t async = ncclSuccess;
+  const ncclResult_t r = ncclCommGetAsyncError(comm, &async);
+  if (r != ncclSuccess) return (int64_t)r;
+  return async == ncclInProgress ? 0 : (int64_t)async;
+}
+
+// ncclCommAbort: stops the communicator's in-flight collectives (a replayed graph blocked in an
+// all-reduce whose peer died) and frees it.  The caller exits right after (a failed
+// rank aborts the job; restart resumes from the checkpoint).
+void rccl_abort(int64_t handle) {
+  ncclComm_t comm;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (handle < 0 || handle >= (int64_t)g_comms.size()) return;
+    comm = g_comms[handle];
+    g_comms[handle] = nullptr;
+  }
+  if (comm != nullptr) (void)ncclCommAbort(comm);
+}
+
 void rccl_destroy(int64_t handle) {
   ncclComm_t comm;
   {
@@ -272,4 +302,6 @@ TORCH_LIBRARY_FRAGMENT(dtfe, m) {
   m.def("rccl_all_reduce(Tensor(a!) buf, int comm, int op) -> ()", &rccl_all_reduce);
   m.def("rccl_broadcast(Tensor(a!) buf, int root, int comm) -> ()", &rccl_broadcast);
   m.def("rccl_destroy(int comm) -> ()", &rccl_destroy);
+  m.def("rccl_status(int comm) -> int", &rccl_status);
+  m.def("rccl_abort(int comm) -> ()", &rccl_abort);
 }

@@ -46,6 +46,17 @@ struct IgemmArgs {
   IgPhase ph[4];
 };
 
+// Pointwise (1x1) conv as a persistent pipelined GEMM (igemm_pw.hip): GEMM row m is pixel
+// pix(m) of an RH x RW grid read from an SH x SW image with stride istr (A rows) and written to
+// an OHf x OWf image with stride ostr (output rows).
+struct PwArgs {
+  const bf16* A; const bf16* W; bf16* out;
+  int M, N, K;
+  int RH, RW, SH, SW, istr, OHf, OWf, ostr;
+  int accum, tiles_m;
+  float* bn_part;         // forward: [tiles_m][3][N] shifted BatchNorm partials of the stored output
+};
+
 struct IgWgradArgs {
   const bf16* dy; const bf16* x; const bf16* zeros; float* ws;
   int B, H, W, C, OH, OW, Cout, KH, KW, stride, pad;
@@ -65,5 +76,8 @@ void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, floa
 bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nullptr);
 bool launch_igemm_dgrad(const ConvDgradArgs& a, hipStream_t s);
 bool launch_igemm_wgrad(const ConvWgradArgs& a, hipStream_t s);
+// 1x1 convs (igemm_pw.hip): true when the pointwise path handles the call
+bool launch_pw_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done);
+bool launch_pw_dgrad(const ConvDgradArgs& a, hipStream_t s);
 
 }  // namespace dtfe

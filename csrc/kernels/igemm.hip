@@ -970,6 +970,7 @@ void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, floa
 }
 
 bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
+  if (launch_pw_fwd(f, s, stats_done)) return true;  // 1x1: persistent pipelined GEMM (igemm_pw.hip)
   const ConvGeom& g = f.g;
   if (g.C % IG_BK || g.Cout % 64 || g.KH * g.KW > IG_MAX_TAPS || g.pool_order || f.bias || f.act != 0) return false;
   if (env_int("DTFE_IG_OFF", 0)) return false;
@@ -994,6 +995,7 @@ bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
 }
 
 bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
+  if (launch_pw_dgrad(d, s)) return true;  // 1x1: persistent pipelined GEMM (igemm_pw.hip)
   const ConvGeom& g = d.g;
   if (g.Cout % IG_BK || g.C % 64 || g.KH * g.KW > IG_MAX_TAPS || g.stride > 2 || d.unpool || d.relu_mask) return false;
   if (env_int("DTFE_IG_OFF", 0)) return false;

@@ -45,21 +45,36 @@ class RoutedComm:
         """Ranks the collective engine spans (reported by bench.py as ranks_seen_by_comm)."""
         return int(self.default.world)
 
-    def check_health(self):
-        """Raise on EVERY rank if any rank's IPC kernel hit a barrier timeout since setup.
-
-        The IPC all-reduce runs inside replayed hipGraphs; a peer that misses a barrier for longer
-        than the timeout makes the kernel set its error word and leave the bucket half reduced, and
-        nothing else would notice.  Reading the word synchronizes the device, so callers do it every
-        ``log_every`` steps and once at the end; the decision is agreed over the group so all ranks
-        stop together instead of training on diverged replicas."""
-        bad = 0.0
+    def local_status(self) -> int:
+        """Non-zero when an engine of THIS rank reported a failure: the IPC kernel's barrier-timeout
+        word (reading it synchronizes the device) or RCCL's asynchronous error code."""
+        bad = 0
         for c in self.comms:
             if hasattr(c, "status"):
-                bad = max(bad, float(c.status()))
+                bad = max(bad, int(c.status()))
+        return bad
+
+    def check_health(self):
+        """Raise on EVERY rank if any rank's engine failed since setup.
+
+        The all-reduce runs inside replayed hipGraphs; a peer that misses an IPC barrier for longer
+        than the timeout makes the kernel set its error word and leave the bucket half reduced, and
+        an RCCL error only surfaces through ncclCommGetAsyncError - nothing else would notice.
+        Callers do it every ``log_every`` steps and once at the end; the decision is agreed over the
+        group so all ranks stop together instead of training on diverged replicas.  (A peer that
+        died outright is the comm watchdog's job, parallel/health.py CommWatchdog: this agreement
+        itself would need the dead peer.)"""
+        bad = float(self.local_status())
         if _agree(bad, self.group, self.device) > 0:
-            raise RuntimeError("IPC all-reduce barrier timeout on %s rank: gradients of that step were not "
+            raise RuntimeError("all-reduce engine failure on %s rank: gradients of that step were not "
                                "fully reduced; replicas may have diverged" % ("this" if bad else "another"))
+
+    def abort(self):
+        """Release collectives blocked on a dead peer (ncclCommAbort; the IPC kernel ends on its own
+        barrier timeout).  The process must exit afterwards."""
+        for c in self.comms:
+            if hasattr(c, "abort"):
+                c.abort()
 
     def all_reduce(self, t: torch.Tensor, *args):
         self.routes.get(t.numel() * t.element_size(), self.default).all_reduce(t, *args)
@@ -102,12 +117,14 @@ def _agree(x: float, group, device) -> float:
     return float(t.item())
 
 
-def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: str = "auto", log=None):
-    """Collective engine for buckets of the given byte sizes.  mode: rccl | ipc | auto."""
+def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: str = "auto", log=None,
+              timeout_s: float = 30.0):
+    """Collective engine for buckets of the given byte sizes.  mode: rccl | ipc | auto.
+    ``timeout_s``: the IPC kernel's barrier timeout (a peer that never arrives)."""
     device = torch.device(device)
     cap = max([int(b) for b in bucket_bytes] + [1 << 20]) + 4096
     if mode == "ipc":  # IPC only (no RCCL communicator: also works for several ranks sharing one GPU)
-        ipc = IpcComm(device, group, cap_bytes=cap)
+        ipc = IpcComm(device, group, cap_bytes=cap, timeout_s=timeout_s)
         return RoutedComm(ipc, {int(b): ipc for b in bucket_bytes}, {int(b): "ipc" for b in bucket_bytes},
                           group=group, device=device)
     rccl = RcclComm(device, group)
@@ -115,7 +132,7 @@ def make_comm(device, group=None, bucket_bytes=(), dtype=torch.bfloat16, mode: s
         return RoutedComm(rccl, group=group, device=device)
     ipc = None
     try:
-        ipc = IpcComm(device, group, cap_bytes=cap, fallback=rccl)
+        ipc = IpcComm(device, group, cap_bytes=cap, timeout_s=timeout_s, fallback=rccl)
         ok = 1.0
     except Exception as e:  # noqa: BLE001 - any IPC trouble (mapping, self-check, timeout) -> RCCL
         ok = 0.0

@@ -9,6 +9,8 @@ when a ps they need stops beating.  Default off: the reference semantics.
 """
 from __future__ import annotations
 
+import os
+import sys
 import threading
 import time
 
@@ -69,3 +71,72 @@ class Watchdog:
                 self.lost.add((job, task))
                 newly.append((job, task, age))
         return newly
+
+
+class CommWatchdog:
+    """Failure detection for the data-parallel collectives ("in sync / all-reduce
+    modes a failed rank aborts the job; restart resumes from the checkpoint").
+
+    The gradient all-reduce is a node of the replayed step graph: when a peer dies, the survivors'
+    host threads block in the device sync of the next step forever (RCCL has no timeout; the IPC
+    kernel gives up after its barrier timeout but the next replay waits again).  This daemon thread
+    needs neither the device nor the dead peer: every ``interval`` seconds it reads the peers'
+    TCPStore heartbeats (``Heartbeat``) and RCCL's asynchronous error code
+    (``RoutedComm.abort`` / ``RcclComm.status``, host-only).  A peer silent for ``timeout`` seconds,
+    an unreachable store (its host, rank 0, is gone) or an RCCL error -> it logs the cause, aborts
+    the communicators (ncclCommAbort releases the blocked collectives) and ends the process with
+    ``exit_code`` (``os._exit``: the main thread may be stuck inside a HIP call)."""
+
+    def __init__(self, store, job: str, rank: int, world: int, comm=None, interval: float = 1.0,
+                 timeout: float = 30.0, log=print, exit_fn=None, exit_code: int = 3):
+        self.store, self.job, self.rank, self.world = store, job, rank, world
+        self.comm, self.interval, self.timeout, self.log = comm, interval, timeout, log
+        self.exit_fn = exit_fn or (lambda code: os._exit(code))
+        self.exit_code = exit_code
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True, name="comm-watchdog")
+        self._t.start()
+
+    def check(self):
+        """One poll; returns the failure description, or None while healthy."""
+        if self.comm is not None:
+            for c in getattr(self.comm, "comms", [self.comm]):
+                st = c.status() if hasattr(c, "status") and hasattr(c, "abort") else 0
+                if st:
+                    return "collective engine error %d (%s)" % (st, type(c).__name__)
+        if self.store is None:
+            return None
+        now = time.time()
+        for r in range(self.world):
+            if r == self.rank:
+                continue
+            key = hb_key(self.job, r)
+            try:
+                if not self.store.check([key]):
+                    continue  # never beat yet (still starting)
+                age = now - float(self.store.get(key).decode())
+            except Exception as e:  # noqa: BLE001 - the store's host (rank 0) is gone
+                return "control store unreachable (%s)" % (type(e).__name__,)
+            if age > self.timeout:
+                return "%s %d silent for %.1f s" % (self.job, r, age)
+        return None
+
+    def _run(self):
+        while not self._stop.wait(self.interval):
+            why = self.check()
+            if why is None:
+                continue
+            if self._stop.is_set():
+                return
+            self.log("%s %d: %s - aborting the collectives and leaving (the job restarts from the last "
+                     "checkpoint)" % (self.job, self.rank, why))
+            try:
+                sys.stdout.flush()
+                if self.comm is not None and hasattr(self.comm, "abort"):
+                    self.comm.abort()
+            finally:
+                self.exit_fn(self.exit_code)
+            return
+
+    def stop(self):
+        self._stop.set()

@@ -51,6 +51,19 @@ class RcclComm:
     def broadcast(self, t: torch.Tensor, root: int = 0):
         torch.ops.dtfe.rccl_broadcast(t, root, self.handle)
 
+    def status(self) -> int:
+        """0 while healthy, else RCCL's asynchronous error code (ncclCommGetAsyncError; no device
+        sync - safe to poll from a watchdog thread while the step graph is blocked)."""
+        if self.handle is None:
+            return 0
+        return int(torch.ops.dtfe.rccl_status(self.handle))
+
+    def abort(self):
+        """ncclCommAbort: release collectives stuck on a dead peer; the process exits next."""
+        if self.handle is not None:
+            torch.ops.dtfe.rccl_abort(self.handle)
+            self.handle = None
+
     def close(self):
         if self.handle is not None:
             torch.ops.dtfe.rccl_destroy(self.handle)

@@ -40,7 +40,7 @@ from .optim import Optimizer
 from .parallel.allreduce import BucketAllReduce
 from .parallel.comm import make_comm
 from .parallel.cluster import ClusterSpec, Server
-from .parallel.health import Heartbeat, Watchdog
+from .parallel.health import CommWatchdog, Heartbeat, Watchdog
 from .utils.faults import FaultInjector
 from .utils.timers import PhaseTimer
 from .parallel.placement import round_robin
@@ -361,7 +361,7 @@ def run_worker_ps(flags, model, server, device, log):
 
 
 # --------------------------------------------------------------- allreduce
-def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
+def run_allreduce(flags, model, device, log, world=1, rank=0, group=None, store=None):
     prog = model.program(device, flags.batch_size, seed=flags.seed)
     gstep = torch.zeros(1, dtype=torch.int32, device=device)
     opts = []
@@ -400,7 +400,8 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         if device.type == "cuda" and flags.comm != "pg" and (dist.get_backend(group) != "gloo" or flags.comm == "ipc"):
             cdt = torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32
             comm = make_comm(device, group, [(hi - lo) * (2 if cdt == torch.bfloat16 else 4) for lo, hi in bks], cdt,
-                             mode=flags.comm, log=log if is_chief else None)
+                             mode=flags.comm, log=log if is_chief else None,
+                             timeout_s=flags.heartbeat_timeout if flags.heartbeat_secs > 0 else 30.0)
         ar = BucketAllReduce(prog.P.grad, bks, group=group, comm=comm,
                              comm_dtype=torch.bfloat16 if flags.comm_dtype == "bf16" else torch.float32)
         if not native and hasattr(prog, "grad_ready"):  # programs reporting backward progress overlap the all-reduce
@@ -419,6 +420,14 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
         if (flags.phase_timers or flags.trace_json) else None
     phase = timer.phase if timer else (lambda _n: contextlib.nullcontext())
     faults = FaultInjector("worker", rank, log=log)
+    # failure detection: with --heartbeat_secs every rank beats into the TCPStore and a
+    # watchdog thread aborts the collectives and ends this rank when a peer goes silent / the store
+    # vanishes / RCCL reports an error - the step graph itself would wait on a dead peer forever
+    hb = wd = None
+    if world > 1 and store is not None and flags.heartbeat_secs > 0:
+        hb = Heartbeat(store, "worker", rank, flags.heartbeat_secs)
+        wd = CommWatchdog(store, "worker", rank, world, comm=ar.comm if ar is not None else None,
+                          interval=min(1.0, flags.heartbeat_secs), timeout=flags.heartbeat_timeout, log=log)
 
     def train_step():
         if native:  # forward, backward, overlapped all-reduce and Adam in the program's own order
@@ -468,6 +477,8 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                 model_step_hook(model, step, state["m"], log)
             metrics_log.write(step=local_step, gs=step, ms=elapsed * 1000, images_per_sec=ips, **sc)
             local_step += 1
+        if wd is not None:  # training is over: peers may now leave at their own pace
+            wd.stop()
         if ar is not None and ar.comm is not None:
             ar.comm.check_health()
         prog.check_health()
@@ -480,6 +491,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None):
                                 torch.from_numpy(data.test.labels[:test_len]).to(device))
             log("Test-Accuracy: %2.4f" % acc)
     finally:
+        if wd is not None:
+            wd.stop()
+        if hb is not None:
+            hb.stop()
         if timer is not None:
             timer.close()
         sv.stop()
@@ -560,7 +575,7 @@ def run(model_name: str, argv=None, log=_print):
     server = Server(cluster, "worker", flags.task_index, backend=backend,
                     device=device if backend == "nccl" else None)
     try:
-        run_allreduce(flags, model, device, log, world=cluster.world_size, rank=server.rank)
+        run_allreduce(flags, model, device, log, world=cluster.world_size, rank=server.rank, store=server.store)
     finally:
         server.shutdown()
     return 0

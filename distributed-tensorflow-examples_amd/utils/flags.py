@@ -81,7 +81,8 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     ap.add_argument("--heartbeat_secs", type=float, default=0.0,
                     help="publish a TCPStore heartbeat every N s (0: off, the reference has none)")
     ap.add_argument("--heartbeat_timeout", type=float, default=30.0,
-                    help="ps: count a worker silent for this long as lost (with --heartbeat_secs)")
+                    help="ps: count a worker silent for this long as lost; all-reduce: a rank whose peer "
+                         "is silent this long aborts the collectives and exits non-zero (with --heartbeat_secs)")
     add_bool(ap, "phase_timers", False, "time fwd+bwd / comm / apply per step with hipEvents (no hipGraph)")
     add_bool(ap, "check_pull", False, "debug: checksum the pulled parameters every step (ps mode) / the "
                                       "replicas' parameters at the end (all-reduce mode)")

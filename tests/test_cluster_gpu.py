@@ -68,6 +68,25 @@ def test_cnn_allreduce_two_workers_ipc_in_graph(tmp_path):
     assert "Variable_1/Adam" in t and "beta1_power" in t
 
 
+def test_allreduce_rank_crash_ends_every_rank(tmp_path):
+    """--mode=allreduce, 2 workers sharing cuda:0 (gloo + in-graph IPC all-reduce), worker 1 crashes
+    at step 5 (DTFE_FAULT): worker 0's step graph would wait on the dead peer; its comm watchdog
+    sees the silent heartbeat, aborts the collectives and exits non-zero - no rank hangs."""
+    import time
+
+    extra = ["--mode=allreduce", "--device=cuda", "--backend=gloo", "--comm=ipc", "--comm_dtype=bf16",
+             "--synthetic", "--num_steps=400", "--batch_size=128", "--model_dir=" + str(tmp_path / "ck"),
+             "--save_model_secs=0", "--heartbeat_secs=0.5", "--heartbeat_timeout=6"]
+    env = dict(os.environ, DTFE_FAULT="crash@worker:1:step=5")
+    t0 = time.time()
+    codes, out, _ = local_cluster.launch("cnn", 0, 2, extra, env=env, timeout=240, stream=False, gpus=1)
+    assert time.time() - t0 < 200
+    assert codes[("worker", 1)] == 17, codes
+    assert codes[("worker", 0)] not in (0, None), (codes, out[("worker", 0)][-20:])
+    assert any("silent for" in l or "store unreachable" in l or "engine failure" in l
+               for l in out[("worker", 0)]), out[("worker", 0)][-20:]
+
+
 @pytest.mark.parametrize("hogwild", [False, True])
 def test_bench_ps_native_plane(hogwild):
     """bench.py --mode ps: 1 ps + 2 workers sharing cuda:0 over the native hipIpc data plane; every

@@ -1,0 +1,78 @@
+"""Failure handling of the data-parallel collectives: RoutedComm.check_health on a
+fake engine error, and the CommWatchdog thread (heartbeats in a real TCPStore, fake RCCL status)."""
+import socket
+import threading
+import time
+
+import pytest
+import torch.distributed as dist
+
+from dtfe.parallel import comm as commmod
+from dtfe.parallel.health import CommWatchdog, Heartbeat
+
+
+class FakeEngine:
+    def __init__(self, status=0):
+        self._status = status
+        self.aborted = False
+        self.world = 2
+
+    def status(self):
+        return self._status
+
+    def abort(self):
+        self.aborted = True
+
+    def close(self):
+        pass
+
+
+def test_check_health_raises_on_engine_error(monkeypatch):
+    rc = commmod.RoutedComm(FakeEngine(0))
+    monkeypatch.setattr(commmod, "_agree", lambda x, group, device: x)   # one process: agreement = own value
+    rc.check_health()                                                    # healthy
+    rc.default._status = 5                                               # e.g. ncclRemoteError surfaced async
+    with pytest.raises(RuntimeError, match="all-reduce engine failure"):
+        rc.check_health()
+    rc.abort()
+    assert rc.default.aborted
+
+
+def _store():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return dist.TCPStore("127.0.0.1", port, 1, True, wait_for_workers=False)
+
+
+def test_watchdog_aborts_when_a_peer_goes_silent():
+    store = _store()
+    hb0 = Heartbeat(store, "worker", 0, 0.1)
+    hb1 = Heartbeat(store, "worker", 1, 0.1)
+    eng = FakeEngine(0)
+    exited = threading.Event()
+    codes = []
+    wd = CommWatchdog(store, "worker", 0, 2, comm=commmod.RoutedComm(eng), interval=0.1, timeout=0.6,
+                      log=lambda m: None, exit_fn=lambda c: (codes.append(c), exited.set()))
+    time.sleep(1.0)
+    assert not exited.is_set()          # both beating: healthy
+    hb1.stop()                          # worker 1 dies (no more beats)
+    assert exited.wait(5.0)
+    assert codes == [3] and eng.aborted
+    wd.stop()
+    hb0.stop()
+
+
+def test_watchdog_aborts_on_rccl_async_error():
+    store = _store()
+    eng = FakeEngine(0)
+    codes = []
+    done = threading.Event()
+    wd = CommWatchdog(store, "worker", 0, 1, comm=commmod.RoutedComm(eng), interval=0.05, timeout=10,
+                      log=lambda m: None, exit_fn=lambda c: (codes.append(c), done.set()))
+    time.sleep(0.3)
+    assert not done.is_set()
+    eng._status = 6
+    assert done.wait(5.0) and eng.aborted
+    wd.stop()
