@@ -46,15 +46,22 @@ struct IgemmArgs {
   IgPhase ph[4];
 };
 
-// Pointwise (1x1) conv as a persistent pipelined GEMM (igemm_pw.hip): GEMM row m is pixel
-// pix(m) of an RH x RW grid read from an SH x SW image with stride istr (A rows) and written to
-// an OHf x OWf image with stride ostr (output rows).
+// Implicit-GEMM conv as a persistent pipelined GEMM (igemm_pw.hip): GEMM row m is pixel (b, i, j)
+// of an RH x RW grid; tap t reads source pixel (i*istr + dy[t], j*istr + dx[t]) of an SH x SW image
+// (out of image: zeros) and weight tap kt[t]; the result goes to pixel (i*ostr + oy, j*ostr + ox)
+// of an OHf x OWf image.  1x1: one tap (0, 0, 0).
 struct PwArgs {
-  const bf16* A; const bf16* W; bf16* out;
-  int M, N, K;
-  int RH, RW, SH, SW, istr, OHf, OWf, ostr;
+  const bf16* A; const bf16* W; bf16* out; const bf16* zeros;
+  int M, N, SC, Ktot;     // rows, output channels, source channels, weight row length (taps * SC)
+  int RH, RW, SH, SW, istr, OHf, OWf, ostr, oy, ox;
+  int ntaps;
+  int dy[IG_MAX_TAPS], dx[IG_MAX_TAPS], kt[IG_MAX_TAPS];
   int accum, tiles_m;
-  float* bn_part;         // forward: [tiles_m][3][N] shifted BatchNorm partials of the stored output
+  float* bn_part;         // [tiles_m][3][N]: forward - shifted BatchNorm partials of the stored output;
+                          // data gradient with bb_x - the consuming BN's backward partials (0, sum g,
+                          // sum g*xhat), g = out * act'(.) (the IgemmArgs bb_* semantics)
+  const bf16* bb_x; const bf16* bb_y; const float* bb_mean; const float* bb_invstd;
+  const float* bb_gamma; const float* bb_beta; int bb_act;
 };
 
 struct IgWgradArgs {
@@ -76,8 +83,8 @@ void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, floa
 bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nullptr);
 bool launch_igemm_dgrad(const ConvDgradArgs& a, hipStream_t s);
 bool launch_igemm_wgrad(const ConvWgradArgs& a, hipStream_t s);
-// 1x1 convs (igemm_pw.hip): true when the pointwise path handles the call
-bool launch_pw_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done);
-bool launch_pw_dgrad(const ConvDgradArgs& a, hipStream_t s);
+// the persistent pipelined path (igemm_pw.hip) for one-phase launches without split-K or BN-backward
+// statistics: true when it took the launch (DTFE_PW_OFF=1: never)
+bool run_igemm_pipe(const IgemmArgs& a, long Mmax, hipStream_t s);
 
 }  // namespace dtfe

@@ -389,13 +389,23 @@ __device__ __forceinline__ bf16x8_t wg_frag(const bf16* img, int rbase, int kk, 
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BM, int BN>  // BM output channels x BN input channels of one tap
-__global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgradArgs a, float* dw, float scale) {
+// BM output channels x BN input channels of one tap; k-tiles of BKW pixels (m rows), an NS-stage LDS
+// ring: NS-1 k-tiles in flight behind counted vmcnt waits and a raw barrier (the 2-stage
+// vmcnt(0)-per-k-tile loop spent 50-72 % of its wave cycles waiting: profiles/r3_pmc_resnet50_igemm.csv)
+template <int N>
+__device__ __forceinline__ void wg_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int BKW, int NS, int MINB>
+__global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgWgradArgs a, float* dw, float scale) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
-  constexpr int A_EL = 64 * BM, B_EL = 64 * BN;
-  constexpr int CPA = BM / 8, RPA = 64 / CPA, NA = BM / 32;  // chunks per m-row, m-rows per piece
-  constexpr int CPB = BN / 8, RPB = 64 / CPB, NB = BN / 32;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
+  constexpr int A_EL = BKW * BM, B_EL = BKW * BN, ST_EL = A_EL + B_EL;
+  constexpr int CPA = BM / 8, RPA = 64 / CPA, NA = BKW * BM / 2048;  // chunks per m-row, m-rows per piece
+  constexpr int CPB = BN / 8, RPB = 64 / CPB, NB = BKW * BN / 2048;
+  constexpr int P = NA + NB;
+  static_assert(NA >= 1 && NB >= 1, "one DMA piece per wave at least");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * ST_EL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -407,7 +417,7 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgra
   const int kh = tap / a.KW, kw = tap - kh * a.KW;
   const int M = a.B * a.OH * a.OW;
   const int m0 = blockIdx.y * a.mchunk, m1 = min(M, m0 + a.mchunk);
-  const int nk = (m1 - m0 + 63) / 64;
+  const int nk = (m1 - m0 + BKW - 1) / BKW;
   const float inv_ow = 1.f / (float)a.OW, inv_oh = 1.f / (float)a.OH;
 
   // this lane's m-row within each piece and the logical chunk it fetches
@@ -425,10 +435,10 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgra
   const bf16* dy_col = a.dy + tm * BM;
   const bf16* x_col = a.x + cb * BN;
 
-  auto issue = [&](int t, int buf) {
-    bf16* As = smem + buf * (A_EL + B_EL);
+  auto issue = [&](int t) {
+    bf16* As = smem + (t % NS) * ST_EL;
     bf16* Bs = As + A_EL;
-    const int mt = m0 + t * 64;
+    const int mt = m0 + t * BKW;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int m = mt + a_row[j];
@@ -459,15 +469,20 @@ __global__ __launch_bounds__(IG_THREADS, 2) void igemm_wgrad_kernel(const IgWgra
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) issue(0, 0);
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
   for (int t = 0; t < nk; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
-    const bf16* As = smem + (t & 1) * (A_EL + B_EL);
+    if (t + NS - 2 < nk) wg_wait_vm<(NS - 2) * P>();
+    else wg_wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // k-tile t landed for every wave; stage (t-1) % NS read by every wave
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    const bf16* As = smem + (t % NS) * ST_EL;
     const bf16* Bs = As + A_EL;
 #pragma unroll
-    for (int kk = 0; kk < 64; kk += 32) {
+    for (int kk = 0; kk < BKW; kk += 32) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = wg_frag<BM>(As, wm * WM + i * 16, kk, lane);
@@ -905,8 +920,23 @@ void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
 bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
   long Mmax = 0;
   for (int p = 0; p < a.nphase; ++p) Mmax = std::max(Mmax, (long)a.B * a.ph[p].RH * a.ph[p].RW);
-  Tile t = pick_tile(Mmax, a.N, a.nphase);
   a.zeros = zero_page(s);
+  if (a.nphase == 1 && (!a.bb_x || bn_stats)) {
+    // persistent pipelined kernel (igemm_pw.hip), BatchNorm partials per 128-row tile: forward
+    // statistics of the output, or (data gradient, bb_x) the consuming BN's backward statistics
+    const bool fuse = bn_stats && (a.bb_x || !a.accum);
+    const int tiles128 = (int)((Mmax + 127) / 128);
+    a.bn_part = fuse ? bn_part_buffer(tiles128, a.N, s) : nullptr;
+    a.splits = 1;
+    a.ws = nullptr;
+    if (run_igemm_pipe(a, Mmax, s)) {
+      // (backward partials carry a zero shift: the fold's row counts do not enter them)
+      if (fuse) launch_bn_part_reduce(a.bn_part, tiles128, a.N, Mmax, 128, bn_stats, s);
+      return fuse;
+    }
+    a.bn_part = nullptr;
+  }
+  Tile t = pick_tile(Mmax, a.N, a.nphase);
   a.splits = 1;
   a.ws = nullptr;
   if (a.nphase == 1 && a.ostr == 1) {
@@ -970,7 +1000,6 @@ void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, floa
 }
 
 bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
-  if (launch_pw_fwd(f, s, stats_done)) return true;  // 1x1: persistent pipelined GEMM (igemm_pw.hip)
   const ConvGeom& g = f.g;
   if (g.C % IG_BK || g.Cout % 64 || g.KH * g.KW > IG_MAX_TAPS || g.pool_order || f.bias || f.act != 0) return false;
   if (env_int("DTFE_IG_OFF", 0)) return false;
@@ -995,7 +1024,6 @@ bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
 }
 
 bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
-  if (launch_pw_dgrad(d, s)) return true;  // 1x1: persistent pipelined GEMM (igemm_pw.hip)
   const ConvGeom& g = d.g;
   if (g.Cout % IG_BK || g.C % 64 || g.KH * g.KW > IG_MAX_TAPS || g.stride > 2 || d.unpool || d.relu_mask) return false;
   if (env_int("DTFE_IG_OFF", 0)) return false;
@@ -1113,10 +1141,24 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   const long len = (long)g.Cout * g.KH * g.KW * g.C;
   if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s, g_wg);
   dim3 grid((unsigned)tiles, sp);
-  if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
-  else if (bm == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<128, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
-  else if (bn == 128) hipLaunchKernelGGL((igemm_wgrad_kernel<64, 128>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
-  else hipLaunchKernelGGL((igemm_wgrad_kernel<64, 64>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  // k-tile depth / ring (DTFE_IG_WPIPE for A/B): 0 = 64-pixel k-tiles, 2 stages (the round-3 loop
+  // shape, now with counted waits); 1 = 32-pixel k-tiles, 4 stages (3 in flight, 2 WGs per CU);
+  // 2 = 64-pixel k-tiles, 3 stages (1 WG per CU)
+  const int wpipe = env_int("DTFE_IG_WPIPE", 1);
+#define DTFE_WG_LAUNCH(BM_, BN_)                                                                                  \
+  do {                                                                                                            \
+    if (wpipe == 1)                                                                                               \
+      hipLaunchKernelGGL((igemm_wgrad_kernel<BM_, BN_, 32, 4, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale); \
+    else if (wpipe == 2)                                                                                          \
+      hipLaunchKernelGGL((igemm_wgrad_kernel<BM_, BN_, 64, 3, 1>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((igemm_wgrad_kernel<BM_, BN_, 64, 2, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale); \
+  } while (0)
+  if (bm == 128 && bn == 128) DTFE_WG_LAUNCH(128, 128);
+  else if (bm == 128) DTFE_WG_LAUNCH(128, 64);
+  else if (bn == 128) DTFE_WG_LAUNCH(64, 128);
+  else DTFE_WG_LAUNCH(64, 64);
+#undef DTFE_WG_LAUNCH
   if (sp > 1)
     launch_wgrad_splits_reduce(a.ws, sp, len, f.dw, f.scale, s);
   return true;

@@ -1,10 +1,11 @@
-// Pointwise (1x1) convolutions as persistent, pipelined GEMMs on gfx950 - the 1x1 convs are two
-// thirds of ResNet-50's conv time (profiles/r3_resnet50_convs_b256.txt: 8.3 of 12.9 ms).
+// Implicit-GEMM convolutions as persistent, pipelined GEMMs on gfx950 (every one-phase launch of
+// igemm.hip: 1x1 and 3x3 forward at any stride, stride-1 data gradients, the strided 1x1 data
+// gradient that accumulates onto the shortcut's share).  The 1x1 convs alone are two thirds of
+// ResNet-50's conv time (profiles/r3_resnet50_convs_b256.txt: 8.3 of 12.9 ms).
 //
-//   forward   Y[m][n] = sum_c X[pix(m)][c] W[n][c]         (stride 1: pix(m) = m; stride 2: the
-//             strided source pixel) + BatchNorm statistics of the stored bf16 Y per tile
-//   dgrad     dX[pix(m)][c] (+)= sum_n dY[m][n] Wt[c][n]   (stride 2 only accumulating: the three
-//             other parity phases of dX get nothing and keep the shortcut's share)
+//   rows = pixels (b, i, j) of the output grid, k = (tap, channel) over the source; tap t reads
+//   source pixel (i*istr + dy[t], j*istr + dx[t]) - a zero page outside the image - and weight
+//   tap kt[t]; + BatchNorm statistics of the stored bf16 output per tile (forward)
 //
 // Against the per-tile implicit-GEMM kernel (igemm.hip) this launch
 //   * is persistent: one (or two) workgroups per CU walk a contiguous run of output tiles, and the
@@ -13,8 +14,9 @@
 //     load latency and epilogue were most of their time);
 //   * keeps NS-1 k-tiles in flight: an NS-stage LDS ring filled by global_load_lds_dwordx4, counted
 //     `s_waitcnt vmcnt(N)` and raw s_barrier (no vmcnt(0) drain per k-tile);
-//   * has no per-k-tile address math: each row's base pointer is computed once per tile (the
-//     1x1 row is one pixel), a k-tile is a +128 B step;
+//   * has no per-k-tile im2col math: each row's pixel base pointer and 9-bit tap-validity mask
+//     are computed once per tile; a k-tile adds the (wave-uniform, scalar) tap offset and selects
+//     the zero page by one mask bit;
 //   * runs the MFMAs with the operands swapped (D = W . X^T), so a lane's accumulator holds four
 //     consecutive CHANNELS of one pixel: the epilogue stores 8-B bf16 quads straight from
 //     registers and the BatchNorm partial sums reduce across 16 lanes by shuffles - no C tile in
@@ -69,12 +71,12 @@ constexpr int pw_smem_el() {
   return NS * (BM + BN) * PW_BK + 2 * 4 * BN * 2;  // ring + per-wave-row statistics (4 floats / channel)
 }
 
-// pixel index of GEMM row m on a (RH x RW) grid with stride `str` into a (SH x SW) image
-__device__ __forceinline__ long pw_pix(int m, int str, int RH, int RW, int SH, int SW, float inv_rw, float inv_rh) {
-  if (str == 1) return m;
-  const int t = pdiv(m, RW, inv_rw), j = m - t * RW;
-  const int b = pdiv(t, RH, inv_rh), i = t - b * RH;
-  return ((long)b * SH + i * str) * SW + j * str;
+// row m of the RH x RW grid -> (b, i, j)
+__device__ __forceinline__ void pw_rc(int m, int RH, int RW, float inv_rw, float inv_rh, int& b, int& i, int& j) {
+  const int t = pdiv(m, RW, inv_rw);
+  j = m - t * RW;
+  b = pdiv(t, RH, inv_rh);
+  i = t - b * RH;
 }
 
 template <int BM, int BN, int NS, int MINB>
@@ -92,37 +94,61 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
   const int tiles_n = a.N / BN;
   const int T = a.tiles_m * tiles_n;
   const int t_lo = (int)((long)T * blockIdx.x / gridDim.x), t_hi = (int)((long)T * (blockIdx.x + 1) / gridDim.x);
-  const int nk = a.K / PW_BK;
+  const int cpt = a.SC / PW_BK;               // k-tiles per tap
+  const int nk = a.ntaps * cpt;
   const int total = (t_hi - t_lo) * nk;
   const float inv_rw = 1.f / (float)a.RW, inv_rh = 1.f / (float)a.RH;
+  // 1x1 / stride 1 / no offset: row m IS pixel m of the source (no decode, no mask)
+  const bool direct = a.ntaps == 1 && a.dy[0] == 0 && a.dx[0] == 0 && a.istr == 1 && a.SH == a.RH && a.SW == a.RW;
 
-  // ---- issue side: row pointers of the tile being streamed in (rows past M re-read row M-1:
-  // finite data whose results are neither stored nor counted)
+  // ---- issue side: per piece the row's pixel base pointer and tap-validity mask of the tile being
+  // streamed in (rows past M re-read row M-1: finite data whose results are neither stored nor counted)
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
   const bf16* a_row[NA];
+  uint32_t a_mask[NA];
   const bf16* b_row[NB];
-  int i_ti = t_lo, i_kt = 0;
+  const bf16* zpage = a.zeros + lchunk * 8;
+  int i_ti = t_lo, i_tap = 0, i_cb = 0;
   auto set_rows = [&](int ti) {
     const int tm = ti / tiles_n, tn = ti - tm * tiles_n;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int m = min(tm * BM + (j * 4 + w) * 8 + lrow, a.M - 1);
-      a_row[j] = a.A + pw_pix(m, a.istr, a.RH, a.RW, a.SH, a.SW, inv_rw, inv_rh) * a.K + lchunk * 8;
+      if (direct) {
+        a_row[j] = a.A + (long)m * a.SC + lchunk * 8;
+        a_mask[j] = 1u;
+      } else {
+        int b, i, jx;
+        pw_rc(m, a.RH, a.RW, inv_rw, inv_rh, b, i, jx);
+        const int iy = i * a.istr, ix = jx * a.istr;
+        a_row[j] = a.A + (((long)b * a.SH + iy) * a.SW + ix) * a.SC + lchunk * 8;
+        uint32_t mk = 0;
+        for (int t = 0; t < a.ntaps; ++t) {
+          const int sy = iy + a.dy[t], sx = ix + a.dx[t];
+          mk |= ((unsigned)sy < (unsigned)a.SH && (unsigned)sx < (unsigned)a.SW) ? (1u << t) : 0u;
+        }
+        a_mask[j] = mk;
+      }
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) b_row[j] = a.W + (long)(tn * BN + (j * 4 + w) * 8 + lrow) * a.K + lchunk * 8;
+    for (int j = 0; j < NB; ++j) b_row[j] = a.W + (long)(tn * BN + (j * 4 + w) * 8 + lrow) * a.Ktot + lchunk * 8;
   };
   if (total > 0) set_rows(i_ti);
-  auto issue = [&](int s) {  // k-tile (i_ti, i_kt) = stream position s, then advance
+  auto issue = [&](int s) {  // k-tile (i_ti, i_tap, i_cb) = stream position s, then advance
     bf16* As = smem + (s % NS) * ST_EL;
     bf16* Bs = As + A_EL;
+    const long toff = ((long)a.dy[i_tap] * a.SW + a.dx[i_tap]) * a.SC + i_cb * PW_BK;
+    const int woff = a.kt[i_tap] * a.SC + i_cb * PW_BK;
 #pragma unroll
-    for (int j = 0; j < NA; ++j) glds16(a_row[j] + i_kt * PW_BK, As + (j * 4 + w) * 512);
+    for (int j = 0; j < NA; ++j) glds16((a_mask[j] >> i_tap) & 1u ? a_row[j] + toff : zpage, As + (j * 4 + w) * 512);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) glds16(b_row[j] + i_kt * PW_BK, Bs + (j * 4 + w) * 512);
-    if (++i_kt == nk) {
-      i_kt = 0;
-      if (++i_ti < t_hi) set_rows(i_ti);
+    for (int j = 0; j < NB; ++j) glds16(b_row[j] + woff, Bs + (j * 4 + w) * 512);
+    if (++i_cb == cpt) {
+      i_cb = 0;
+      if (++i_tap == a.ntaps) {
+        i_tap = 0;
+        if (++i_ti < t_hi) set_rows(i_ti);
+      }
     }
   };
 
@@ -176,19 +202,48 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + i * 16 + (lane & 15);
-      orow[i] = m < a.M ? a.out + pw_pix(m, a.ostr, a.RH, a.RW, a.OHf, a.OWf, inv_rw, inv_rh) * a.N + n0 : nullptr;
+      long pix = m;
+      if (!direct || a.ostr != 1) {
+        int b, ii, jx;
+        pw_rc(m, a.RH, a.RW, inv_rw, inv_rh, b, ii, jx);
+        pix = ((long)b * a.OHf + ii * a.ostr + a.oy) * a.OWf + jx * a.ostr + a.ox;
+      }
+      orow[i] = m < a.M ? a.out + pix * a.N + n0 : nullptr;
     }
-    u32x2_t old[TN][TM];
-    if (a.accum) {  // every load before the first add (one latency, not TM*TN)
+    // epilogue operands, every load before the first use (one latency, not TM*TN): the old
+    // output (accumulate) and, for the data gradient's BatchNorm-backward statistics, the BN's input
+    // x (and its output y for a mask that cannot be recomputed from x) at the same positions
+    const bool bb = a.bb_x != nullptr;
+    const bool bb_from_x = bb && a.bb_y == nullptr && a.bb_act == ACT_RELU;
+    const bool bb_need_y = bb && a.bb_act != ACT_NONE && !bb_from_x;
+    u32x2_t old[TN][TM], xv[TN][TM], yv[TN][TM];
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          old[j][i] = orow[i] ? *reinterpret_cast<const u32x2_t*>(orow[i] + 16 * j) : u32x2_t{0u, 0u};
-    }
+      for (int i = 0; i < TM; ++i) {
+        const long off = orow[i] ? (long)(orow[i] - a.out) + 16 * j : 0;
+        if (a.accum) old[j][i] = orow[i] ? *reinterpret_cast<const u32x2_t*>(a.out + off) : u32x2_t{0u, 0u};
+        if (bb) xv[j][i] = *reinterpret_cast<const u32x2_t*>(a.bb_x + off);
+        if (bb_need_y) yv[j][i] = *reinterpret_cast<const u32x2_t*>(a.bb_y + off);
+      }
     float ssum[TN][4], ssq[TN][4], kshift[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+      float bmean[4], binv[4], bsc[4], bsh[4];
+      if (bb) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = n0 + 16 * j + q;
+          bmean[q] = a.bb_mean[c];
+          binv[q] = a.bb_invstd[c];
+          if (bb_from_x) {  // = norm.hip BwdMask: bit-identical to the forward's pre-activation
+            bsc[q] = a.bb_gamma[c] * binv[q];
+            bsh[q] = a.bb_beta[c] - bmean[q] * bsc[q];
+          }
+          ssum[j][q] = ssq[j][q] = 0.f;
+          kshift[j][q] = 0.f;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         f32x4_t v = acc[j][i];
@@ -199,11 +254,27 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
         const u32x2_t pk = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
         if (orow[i]) *reinterpret_cast<u32x2_t*>(orow[i] + 16 * j) = pk;
         acc[j][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        if (a.bn_part) {
-          // statistics of the STORED values, shifted by the wave's first row (numerically safe)
-          const float y[4] = {bf2f((bf16)(pk[0] & 0xffffu)), bf2f((bf16)(pk[0] >> 16)), bf2f((bf16)(pk[1] & 0xffffu)),
-                              bf2f((bf16)(pk[1] >> 16))};
-          const bool ok = orow[i] != nullptr;
+        const float y[4] = {bf2f((bf16)(pk[0] & 0xffffu)), bf2f((bf16)(pk[0] >> 16)), bf2f((bf16)(pk[1] & 0xffffu)),
+                            bf2f((bf16)(pk[1] >> 16))};
+        const bool ok = orow[i] != nullptr;
+        if (bb) {
+          // BatchNorm-backward statistics of the stored (final) values: g = out * act'(.)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t xw = xv[j][i][q >> 1] >> (16 * (q & 1));
+            const float x = bf2f((bf16)(xw & 0xffffu));
+            float g = y[q];
+            if (bb_from_x) {
+              g = (x * bsc[q] + bsh[q]) > 0.f ? g : 0.f;
+            } else if (bb_need_y) {
+              g *= act_grad_from_out(bf2f((bf16)((yv[j][i][q >> 1] >> (16 * (q & 1))) & 0xffffu)), a.bb_act);
+            }
+            g = ok ? g : 0.f;
+            ssum[j][q] += g;
+            ssq[j][q] += g * (x - bmean[q]) * binv[q];
+          }
+        } else if (a.bn_part) {
+          // forward statistics of the STORED values, shifted by the wave's first row (numerically safe)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (i == 0) {
@@ -298,38 +369,30 @@ void run_pw(PwArgs& a, hipStream_t s) {
 
 }  // namespace
 
-bool launch_pw_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
-  const ConvGeom& g = f.g;
-  if (g.KH != 1 || g.KW != 1 || g.pad != 0 || g.C % PW_BK || g.Cout % 64 || g.pool_order || f.bias || f.act != 0)
-    return false;
-  if (env_int("DTFE_PW_OFF", 0)) return false;
+bool run_igemm_pipe(const IgemmArgs& g, long Mmax, hipStream_t s) {
+  const int off = env_int("DTFE_PW_OFF", 0);
+  if (off || g.nphase != 1 || g.SC % PW_BK || g.N % 64) return false;
+  const IgPhase& P = g.ph[0];
+  if (P.ntaps < 1) return false;
   PwArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.A = f.x; a.W = f.w; a.out = f.y;
-  a.M = g.B * g.OH * g.OW; a.N = g.Cout; a.K = g.C;
-  a.RH = g.OH; a.RW = g.OW; a.SH = g.H; a.SW = g.W; a.istr = g.stride;
-  a.OHf = g.OH; a.OWf = g.OW; a.ostr = 1;
-  const int tiles_m = (a.M + 127) / 128;
-  if (f.bn_stats) a.bn_part = bn_part_buffer(tiles_m, a.N, s);
-  run_pw(a, s);
-  if (f.bn_stats) launch_bn_part_reduce(a.bn_part, tiles_m, a.N, a.M, 128, f.bn_stats, s);
-  if (stats_done) *stats_done = f.bn_stats != nullptr;
-  return true;
-}
-
-bool launch_pw_dgrad(const ConvDgradArgs& d, hipStream_t s) {
-  const ConvGeom& g = d.g;
-  if (g.KH != 1 || g.KW != 1 || g.pad != 0 || g.Cout % PW_BK || g.C % 64 || d.unpool || d.relu_mask || d.bnb_stats)
-    return false;
-  if (g.stride != 1 && !(g.stride == 2 && d.accumulate)) return false;
-  if (env_int("DTFE_PW_OFF", 0)) return false;
-  PwArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.A = d.dy; a.W = d.wt; a.out = d.dx;
-  a.M = g.B * g.OH * g.OW; a.N = g.C; a.K = g.Cout;
-  a.RH = g.OH; a.RW = g.OW; a.SH = g.OH; a.SW = g.OW; a.istr = 1;
-  a.OHf = g.H; a.OWf = g.W; a.ostr = g.stride;
-  a.accum = d.accumulate;
+  a.A = g.src; a.W = g.w; a.out = g.out; a.zeros = g.zeros;
+  a.M = (int)Mmax; a.N = g.N; a.SC = g.SC; a.Ktot = g.Ktot;
+  a.RH = P.RH; a.RW = P.RW; a.SH = g.SH; a.SW = g.SW; a.istr = g.istr;
+  a.OHf = g.OHf; a.OWf = g.OWf; a.ostr = g.ostr; a.oy = P.oy; a.ox = P.ox;
+  a.ntaps = P.ntaps;
+  for (int t = 0; t < P.ntaps; ++t) { a.dy[t] = P.dy[t]; a.dx[t] = P.dx[t]; a.kt[t] = P.kt[t]; }
+  a.accum = g.accum;
+  a.bn_part = g.bn_part;
+  if (g.bb_x) {
+    a.bb_x = g.bb_x; a.bb_y = g.bb_y; a.bb_mean = g.bb_mean; a.bb_invstd = g.bb_invstd;
+    a.bb_gamma = g.bb_gamma; a.bb_beta = g.bb_beta; a.bb_act = g.bb_act;
+  }
+  // too few tiles for a persistent grid: the per-tile kernel's split-K spreads them better
+  const int bn = pw_cfg(a.N) == 2 ? 64 : 128;
+  const long tiles = (Mmax + 127) / 128 * (a.N / bn);
+  const long min_tiles = env_int("DTFE_PW_MINTILES", 256);
+  if (tiles < min_tiles) return false;
   run_pw(a, s);
   return true;
 }

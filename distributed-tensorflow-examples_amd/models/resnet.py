@@ -149,6 +149,14 @@ class Conv:
         else:
             ops.conv_wgrad(dy, x, self.gw, None, self.g)
 
+    def dgrad_fuses_bn(self, accumulate=False):
+        """Whether this data gradient runs on the one-phase persistent kernel (igemm_pw.hip), whose
+        register epilogue folds the consuming BatchNorm's backward statistics in: every stride-1
+        conv.  (A strided data gradient with statistics needs all its parity phases - the per-tile
+        kernel's LDS epilogue, measured slower than the separate statistics pass,
+        profiles/r2_resnet50_bn_bwd_fuse_ab.txt.)"""
+        return not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0 and self.stride == 1
+
     def dgrad(self, dy, dx, accumulate=False, bn_bwd=None):
         """``bn_bwd``: BN.bwd_stats_args of the BatchNorm that consumes dx; returns True when its
         backward statistics were produced with dx (the BN then skips its statistics pass)."""
@@ -158,8 +166,9 @@ class Conv:
                         OH=self.H, OW=self.W, N=self.cin, KH=self.k, KW=self.k, stride=1,
                         pad=self.k - 1 - self.pad, dil=self.dil)
             return False
-        ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate, bn_bwd=bn_bwd if _BN_BWD_FUSE else None)
-        return bn_bwd is not None and _BN_BWD_FUSE
+        fuse = bn_bwd is not None and self.dgrad_fuses_bn(accumulate)
+        ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate, bn_bwd=bn_bwd if fuse else None)
+        return fuse
 
 
 class SideStream:
@@ -200,9 +209,6 @@ class SideStream:
 
 
 _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
-# BN-backward statistics from the producing data-gradient launch (DTFE_BN_BWD_FUSE=1; off by default:
-# measured 0.5 ms per ResNet-50 B=256 step SLOWER than the separate pass, profiles/r2_resnet50_bn_bwd_fuse_ab.txt)
-_BN_BWD_FUSE = os.environ.get("DTFE_BN_BWD_FUSE", "0") == "1"
 
 
 class BN:
@@ -379,8 +385,12 @@ class Bottleneck:
         if dx is not None:
             if fuse:
                 if self.proj:
-                    self.conv1.dgrad(self.dc1, dx)
-                    return self.convs.dgrad(self.dsc, dx, accumulate=True, bn_bwd=nb)
+                    # the strided shortcut's data gradient first (it covers every pixel, zeros on the
+                    # parity phases no tap reaches), conv1's (stride 1, all pixels) accumulated on top:
+                    # the LAST producer of dx covers every pixel, so it can fold the previous block's
+                    # bn3 backward statistics into its epilogue
+                    self.convs.dgrad(self.dsc, dx)
+                    return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
                 return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
             else:
                 self.conv1.dgrad(self.dc1, dx)

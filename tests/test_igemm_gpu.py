@@ -76,6 +76,25 @@ def test_igemm_fwd_dgrad_wgrad(case, tile):
     assert _rel(dw - 0.5, ref_dw) < 1e-3
 
 
+@pytest.mark.parametrize("wpipe", ["0", "1", "2"])
+@pytest.mark.parametrize("case", CASES)
+def test_igemm_wgrad_pipelines(case, wpipe, monkeypatch):
+    """Every k-tile depth / LDS ring of the weight-gradient kernel (DTFE_IG_WPIPE) against fp32."""
+    monkeypatch.setenv("DTFE_IG_WPIPE", wpipe)
+    monkeypatch.setenv("DTFE_IG_W3", "0")   # the per-tap kernel for the 3x3 shapes too
+    B, H, C, Cout, k, s = case
+    g = _geom(B, H, C, Cout, k, s)
+    torch.manual_seed(4)
+    x = torch.randn(B, H, H, C).to(torch.bfloat16)
+    dy = torch.randn(B, g["OH"], g["OW"], Cout).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Cout, C, k, k), dy.float().permute(0, 3, 1, 2),
+                                      stride=s, padding=g["pad"]).permute(0, 2, 3, 1)
+    dw = torch.zeros(Cout, k, k, C, device=DEV)
+    ops.conv_wgrad(dy.to(DEV), x.to(DEV), dw, None, g, 1.0)
+    torch.cuda.synchronize()
+    assert _rel(dw, ref) < 1e-3
+
+
 def test_igemm_wgrad_scale_and_splits(monkeypatch):
     g = _geom(16, 14, 64, 64, 3, 1)
     torch.manual_seed(2)

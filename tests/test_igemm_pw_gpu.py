@@ -1,10 +1,11 @@
-"""Pointwise (1x1) convolutions on the persistent pipelined GEMM (csrc/kernels/igemm_pw.hip) vs fp32
-references and vs the per-tile implicit-GEMM kernel (DTFE_PW_OFF=1).
+"""The persistent pipelined implicit-GEMM kernel (csrc/kernels/igemm_pw.hip) vs fp32 references and
+vs the per-tile implicit-GEMM kernel (DTFE_PW_OFF=1).
 
-Covers: stride-1 / stride-2 forward with the fused BatchNorm statistics, stride-1 data gradient,
-the stride-2 accumulating data gradient (the projection shortcut's share already in dx), M not a
-multiple of the tile, every tile / ring configuration (DTFE_PW_CFG) and small grids that make every
-workgroup stream several tiles (the k-tile stream crossing tile boundaries, DTFE_PW_GRID)."""
+Covers: 1x1 and 3x3 forward at stride 1 / 2 with the fused BatchNorm statistics, stride-1 data
+gradients (1x1, 3x3 with flipped taps), the stride-2 1x1 data gradient that accumulates onto the
+shortcut's share, M not a multiple of the tile, every tile / ring configuration (DTFE_PW_CFG) and
+small grids that make every workgroup stream several tiles (the k-tile stream crossing tile
+boundaries, DTFE_PW_GRID).  DTFE_PW_MINTILES=1 keeps these small shapes on the persistent path."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -15,13 +16,16 @@ from dtfe import ops
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-CASES = [  # B, H, C, Cout, stride
-    (2, 9, 64, 64, 1),       # M = 162: partial last tile, 1 k-tile
-    (3, 14, 256, 64, 1),     # reduce, 4 k-tiles, N = 64 (128x64 tiles)
-    (2, 14, 64, 256, 1),     # expand, N = 256
-    (2, 7, 512, 128, 1),     # 8 k-tiles
-    (2, 14, 256, 512, 2),    # strided projection (7x7 output)
-    (1, 28, 128, 512, 1),    # 784 rows
+CASES = [  # B, H, C, Cout, stride, k
+    (2, 9, 64, 64, 1, 1),       # M = 162: partial last tile, 1 k-tile
+    (3, 14, 256, 64, 1, 1),     # reduce, 4 k-tiles, N = 64 (128x64 tiles)
+    (2, 14, 64, 256, 1, 1),     # expand, N = 256
+    (2, 7, 512, 128, 1, 1),     # 8 k-tiles
+    (2, 14, 256, 512, 2, 1),    # strided projection (7x7 output)
+    (1, 28, 128, 512, 1, 1),    # 784 rows
+    (2, 14, 64, 64, 1, 3),      # 3x3: 9 taps, border taps read the zero page
+    (2, 15, 128, 128, 2, 3),    # strided 3x3 (v1.5), odd image
+    (2, 7, 256, 128, 1, 3),     # 3x3, 4 k-tiles per tap
 ]
 
 
@@ -34,6 +38,7 @@ def _stats_ref(y):
 
 @pytest.fixture(params=[None, "0", "1", "2", "3"])
 def cfg(request, monkeypatch):
+    monkeypatch.setenv("DTFE_PW_MINTILES", "1")
     if request.param is not None:
         monkeypatch.setenv("DTFE_PW_CFG", request.param)
     return request.param
@@ -42,15 +47,17 @@ def cfg(request, monkeypatch):
 @pytest.mark.parametrize("grid", [None, "5"])
 @pytest.mark.parametrize("case", CASES)
 def test_pw_fwd_with_bn_stats(case, grid, cfg, monkeypatch):
-    B, H, C, Cout, s = case
+    B, H, C, Cout, s, k = case
     if grid:
         monkeypatch.setenv("DTFE_PW_GRID", grid)
-    OH = (H - 1) // s + 1
-    g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=1, KW=1, stride=s, pad=0)
+    pad = (k - 1) // 2
+    OH = (H + 2 * pad - k) // s + 1
+    g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=k, KW=k, stride=s, pad=pad)
     torch.manual_seed(1)
     x = torch.randn(B, H, H, C).to(torch.bfloat16)
-    w = (torch.randn(Cout, 1, 1, C) / C ** 0.5).to(torch.bfloat16)
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s).permute(0, 2, 3, 1)
+    w = (torch.randn(Cout, k, k, C) / (k * C ** 0.5)).to(torch.bfloat16)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
+                   padding=pad).permute(0, 2, 3, 1)
     y = torch.full((B, OH, OH, Cout), float("nan"), device=DEV, dtype=torch.bfloat16)
     st = torch.zeros(2, Cout, device=DEV)
     ops.conv_fwd(x.to(DEV), w.to(DEV), None, y, None, g, act=ops.ACT_NONE, stats=st)
@@ -72,26 +79,29 @@ def test_pw_fwd_with_bn_stats(case, grid, cfg, monkeypatch):
 @pytest.mark.parametrize("grid", [None, "3"])
 @pytest.mark.parametrize("case", CASES)
 def test_pw_dgrad(case, grid, cfg, monkeypatch):
-    B, H, C, Cout, s = case
+    B, H, C, Cout, s, k = case
     if grid:
         monkeypatch.setenv("DTFE_PW_GRID", grid)
-    OH = (H - 1) // s + 1
-    g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=1, KW=1, stride=s, pad=0)
+    pad = (k - 1) // 2
+    OH = (H + 2 * pad - k) // s + 1
+    g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=k, KW=k, stride=s, pad=pad)
     torch.manual_seed(2)
-    w = (torch.randn(Cout, 1, 1, C) / Cout ** 0.5).to(torch.bfloat16)
+    w = (torch.randn(Cout, k, k, C) / (k * Cout ** 0.5)).to(torch.bfloat16)
     dy = torch.randn(B, OH, OH, Cout).to(torch.bfloat16)
     ref = torch.nn.grad.conv2d_input((B, C, H, H), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
-                                     stride=s).permute(0, 2, 3, 1)
+                                     stride=s, padding=pad).permute(0, 2, 3, 1)
     wt = w.permute(3, 1, 2, 0).contiguous().to(DEV)
     base = torch.randn(B, H, H, C).to(torch.bfloat16)
-    accumulate = s == 2   # the strided 1x1 data gradient always accumulates (projection shortcut)
+    # the strided 1x1 data gradient always accumulates (projection shortcut); a strided 3x3 data
+    # gradient (four parity phases) stays on the per-tile kernel - test it accumulating too
+    accumulate = s == 2
     dx = base.to(DEV) if accumulate else torch.full((B, H, H, C), float("nan"), device=DEV, dtype=torch.bfloat16)
     ops.conv_dgrad(dy.to(DEV), wt, dx, g, accumulate=accumulate)
     torch.cuda.synchronize()
     want = ref + (base.float() if accumulate else 0)
     err = (dx.float().cpu() - want).abs().max().item()
     assert err <= 2e-2 * want.abs().max().item(), err
-    if accumulate:  # phases no tap reaches keep the shortcut's share bit for bit
+    if accumulate and k == 1:  # phases no tap reaches keep the shortcut's share bit for bit
         m = torch.ones(H, H, dtype=torch.bool)
         m[::2, ::2] = False
         assert torch.equal(dx.cpu()[:, m], base[:, m])

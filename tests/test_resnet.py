@@ -299,11 +299,16 @@ BN_BWD_CASES = [  # (B, H, Cin, Cout, K, stride, accumulate, mask)  - dgrad shap
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pipe", ["1", "0"])
 @pytest.mark.parametrize("case", BN_BWD_CASES)
-def test_conv_dgrad_bn_bwd_stats_gpu(case):
+def test_conv_dgrad_bn_bwd_stats_gpu(case, pipe, monkeypatch):
     """conv_dgrad(bn_bwd=...) fills the consuming BN's backward statistics from the implicit-GEMM
-    epilogue; they must equal a separate bn_bwd_stats pass over the same finished dx."""
+    epilogue; they must equal a separate bn_bwd_stats pass over the same finished dx.  pipe=1: the
+    persistent pipelined kernel's register epilogue (igemm_pw.hip) wherever the launch has one
+    phase; pipe=0: the per-tile kernel's LDS epilogue."""
     from dtfe import ops
+    monkeypatch.setenv("DTFE_PW_MINTILES", "1")
+    monkeypatch.setenv("DTFE_PW_OFF", "0" if pipe == "1" else "1")
     B, H, C, CO, K, s, acc, mask = case
     dev = torch.device("cuda", 0)
     pad = (K - 1) // 2
@@ -326,9 +331,11 @@ def test_conv_dgrad_bn_bwd_stats_gpu(case):
     dx2 = base.clone()
     ops.conv_dgrad(dy, wt, dx2, g, accumulate=acc)
     st2 = torch.zeros(2 * C, device=dev)
-    ops.bn_bwd_stats(dx2, yy, x, mean, invstd, st2, act, gamma=gamma, beta=bb)
+    ops.bn_bwd_stats(dx, yy, x, mean, invstd, st2, act, gamma=gamma, beta=bb)
     torch.cuda.synchronize()
-    assert torch.equal(dx, dx2)
+    # (a strided launch with statistics keeps its tapless parity phases, without them it drops them:
+    # the two calls may take different kernels - equal up to bf16 rounding)
+    assert _rel(dx, dx2) < 1e-2
     assert _rel(st[:C], st2[:C]) < 1e-4 and _rel(st[C:], st2[C:]) < 1e-4
 
 
