@@ -53,12 +53,16 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--only", default="", help="H,C,Cout,k,s[;...]: just these layers (PMC runs)")
     a = ap.parse_args()
+    only = {tuple(int(v) for v in t.split(",")) for t in a.only.split(";") if t}
     B, dev = a.batch, "cuda"
     tot = {"ours": [0.0, 0.0, 0.0], "torch": [0.0, 0.0, 0.0]}
     print("%-28s %4s | %22s | %22s | %22s" % ("layer (H C->Cout kxk /s)", "n", "fwd us (TF/s)", "dgrad us (TF/s)",
                                               "wgrad us (TF/s)"))
     for (H, C, Cout, k, s), n in shapes().items():
+        if only and (H, C, Cout, k, s) not in only:
+            continue
         pad = (k - 1) // 2
         OH = (H + 2 * pad - k) // s + 1
         g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=k, KW=k, stride=s, pad=pad)

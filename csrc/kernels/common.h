@@ -6,6 +6,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
+#include <cstring>
 
 namespace dtfe {
 
@@ -92,6 +94,19 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   int xcd = orig % nxcd;
   int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + orig / nxcd;
+}
+
+// Ablation bits of one kernel family from DTFE_DIAG="key=bits[,key=bits...]" (keys: c1, c1w, ic,
+// iw - the MNIST conv kernels' stage-skipping switches used by the bench/*_diag.py ablations)
+inline int diag_bits(const char* key) {
+  const char* e = std::getenv("DTFE_DIAG");
+  const size_t n = std::strlen(key);
+  while (e && *e) {
+    if (!std::strncmp(e, key, n) && e[n] == '=') return std::atoi(e + n + 1);
+    e = std::strchr(e, ',');
+    if (e) ++e;
+  }
+  return 0;
 }
 
 }  // namespace dtfe

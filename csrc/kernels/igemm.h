@@ -52,6 +52,7 @@ struct IgemmArgs {
 // of an OHf x OWf image.  1x1: one tap (0, 0, 0).
 struct PwArgs {
   const bf16* A; const bf16* W; bf16* out; const bf16* zeros;
+  bf16* sink;             // 16 KB scratch the epilogue's out-of-range rows store into
   int M, N, SC, Ktot;     // rows, output channels, source channels, weight row length (taps * SC)
   int RH, RW, SH, SW, istr, OHf, OWf, ostr, oy, ox;
   int ntaps;
@@ -76,6 +77,8 @@ struct IgWgradArgs {
 // value into stats[2][N], as bn_stats would.  bn_part_buffer: the device scratch for `tiles`
 // tiles plus the fold's chunk table (valid until the next call on this device).
 float* bn_part_buffer(long tiles, int N, hipStream_t s);
+// a 16 KB device page that kernels may write garbage into (per device, created on first use)
+bf16* ig_sink_page(hipStream_t s);
 void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s);
 
 // true when the igemm path handles the conv (and launches it)
@@ -84,7 +87,7 @@ bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nu
 bool launch_igemm_dgrad(const ConvDgradArgs& a, hipStream_t s);
 bool launch_igemm_wgrad(const ConvWgradArgs& a, hipStream_t s);
 // the persistent pipelined path (igemm_pw.hip) for one-phase launches without split-K or BN-backward
-// statistics: true when it took the launch (DTFE_PW_OFF=1: never)
+// statistics: true when it took the launch (DTFE_PW=off: never; =bb: only data gradients with BN-backward statistics)
 bool run_igemm_pipe(const IgemmArgs& a, long Mmax, hipStream_t s);
 
 }  // namespace dtfe

@@ -41,6 +41,17 @@ __device__ __forceinline__ void glds16(const void* g, bf16* lds_piece) {
   __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_piece, 16, 0, 0);
 }
 
+// The same DMA issued from inline asm (M0 = the wave-uniform LDS destination): invisible to the
+// compiler's LDS-DMA alias tracking, which otherwise puts an `s_waitcnt vmcnt(0)` in front of the
+// first fragment read of every k-tile of a multi-stage ring (it cannot tell the stage being filled
+// from the one being read) and so drains the prefetch.  The caller orders every DMA'd tile with
+// its own counted vmcnt wait + barrier; the compiler's own waits stay conservative (these DMAs
+// are always older than the loads it counts).
+__device__ __forceinline__ void glds16_async(const void* g, bf16* lds_piece) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_piece);
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(l) : "memory");
+}
+
 // exact m / d for 0 <= m < 2^24 through a float reciprocal
 __device__ __forceinline__ int qdiv(int m, int d, float inv_d) {
   int q = (int)((float)m * inv_d);
@@ -443,7 +454,7 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgW
     for (int j = 0; j < NA; ++j) {
       const int m = mt + a_row[j];
       const bf16* p = m < m1 ? dy_col + (long)m * a.Cout + a_chk[j] * 8 : a.zeros;
-      glds16(p, As + (j * 4 + w) * 512);
+      glds16_async(p, As + (j * 4 + w) * 512);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -458,7 +469,7 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgW
         if ((unsigned)sy < (unsigned)a.H && (unsigned)sx < (unsigned)a.W)
           p = x_col + ((long)(b * a.H + sy) * a.W + sx) * a.C + b_chk[j] * 8;
       }
-      glds16(p, Bs + (j * 4 + w) * 512);
+      glds16_async(p, Bs + (j * 4 + w) * 512);
     }
   };
 
@@ -891,7 +902,7 @@ Tile pick_tile(long M, int N, int nphase) {
     if (std::sscanf(e, "%dx%d", &bm, &bn) == 2 && (bm == 64 || bm == 128) && (bn == 64 || bn == 128) && N % bn == 0)
       return {bm, bn};
   }
-  static const long min_blocks = env_int("DTFE_IG_TBLOCKS", 240);
+  constexpr long min_blocks = 240;
   const Tile cands[3] = {{128, 128}, {128, 64}, {64, 64}};
   for (const Tile& t : cands) {
     if (N % t.bn) continue;
@@ -935,6 +946,13 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
       return fuse;
     }
     a.bn_part = nullptr;
+    // one-phase data gradient the persistent kernel did not take: its BN-backward statistics run as
+    // the separate pass (launch_dgrad_bn_bwd_stats) - the per-tile kernel's LDS epilogue for them
+    // measured slower (profiles/r2_resnet50_bn_bwd_fuse_ab.txt)
+    if (a.bb_x) {
+      a.bb_x = nullptr;
+      bn_stats = nullptr;
+    }
   }
   Tile t = pick_tile(Mmax, a.N, a.nphase);
   a.splits = 1;
@@ -944,7 +962,7 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
     const long blocks = ((Mmax + t.bm - 1) / t.bm) * (a.N / t.bn);
     const int nk = a.ph[0].ntaps * (a.SC / IG_BK);
     int sp = env_int("DTFE_IG_SPLIT", 0);
-    static const long ftarget = env_int("DTFE_IG_FTARGET", 200);  // split-K workgroup target (R50 sweep: 400 -> 200 saves 0.15 ms)
+    constexpr long ftarget = 200;  // split-K workgroup target (R50 sweep: 400 -> 200 saves 0.15 ms)
     if (sp <= 0) {
       sp = 1;
       while (blocks * sp < ftarget && nk / (sp * 2) >= 6) sp *= 2;
@@ -985,6 +1003,21 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
 }
 
 }  // namespace
+
+bf16* ig_sink_page(hipStream_t s) {
+  static DevScratch sinks[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_mu);
+  DevScratch& d = sinks[dev];
+  if (!d.ws) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &st);
+    if (st != hipStreamCaptureStatusNone) throw std::runtime_error("igemm: sink page first used inside a graph capture");
+    if (hipMalloc(&d.ws, 16384) != hipSuccess) throw std::runtime_error("igemm: sink page alloc");
+  }
+  return reinterpret_cast<bf16*>(d.ws);
+}
 
 float* bn_part_buffer(long tiles, int N, hipStream_t s) {
   const long nchunk = (tiles + BN_TCH - 1) / BN_TCH;
@@ -1103,7 +1136,7 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
     const long len = (long)g.Cout * 9 * g.C;
     // one workgroup per CU (the 36 accumulator tiles take the whole register file): aim for one
     // wave of 256 workgroups, at least 4 k-tiles each, fp32 partial slabs up to 40 MB
-    static const long target = env_int("DTFE_IG_W3TARGET", 256);
+    constexpr long target = 256;
     long sp = env_int("DTFE_IG_WSPLIT", 0);
     if (sp <= 0) {
       sp = std::max(1L, std::min((target + tiles - 1) / tiles, T / 4));
@@ -1122,16 +1155,15 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   const long tiles = (long)(g.Cout / bm) * g.KH * g.KW * (g.C / bn);
   const long M = (long)g.B * g.OH * g.OW;
   int sp = env_int("DTFE_IG_WSPLIT", 0);
-  // splits: enough workgroups to fill the chip (DTFE_IG_WTARGET), each split at least 256 rows, and
-  // the fp32 partial slabs (splits x weight size, written once and re-read by the reduce) bounded
-  // by DTFE_IG_WPART_MB.  ResNet-50 B=256 sweep (profiles/r2_resnet50_wgrad_splits_ab.txt):
+  // splits: enough workgroups to fill the chip (target), each split at least 256 rows, and the
+  // fp32 partial slabs (splits x weight size, written once and re-read by the reduce) bounded by
+  // part_mb.  ResNet-50 B=256 sweep (profiles/r2_resnet50_wgrad_splits_ab.txt):
   // 768 WGs / unbounded 27.8 ms -> 512 WGs / 32 MB 27.0 ms per step
-  static const long target = env_int("DTFE_IG_WTARGET", 512);
-  static const long part_mb = env_int("DTFE_IG_WPART_MB", 32);
+  constexpr long target = 512, part_mb = 32;
   if (sp <= 0) {
     sp = (int)std::max(1L, std::min((target + tiles - 1) / tiles, (M + 255) / 256));
     const long len0 = (long)g.Cout * g.KH * g.KW * g.C;
-    if (part_mb > 0) sp = (int)std::max(1L, std::min((long)sp, (part_mb << 20) / (len0 * 4)));
+    sp = (int)std::max(1L, std::min((long)sp, (part_mb << 20) / (len0 * 4)));
   }
   long mchunk = (M + sp - 1) / sp;
   mchunk = (mchunk + 63) / 64 * 64;

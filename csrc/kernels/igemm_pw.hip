@@ -39,12 +39,26 @@ namespace dtfe {
 namespace {
 
 constexpr int PW_THREADS = 256;
+// which one-phase launches take the persistent kernel by default (DTFE_PW overrides):
+// 0 none, 1 the data gradients that fold BatchNorm-backward statistics in, 2 all
+constexpr int PW_DEFAULT_MODE = 0;
 constexpr int PW_BK = 64;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 __device__ __forceinline__ void glds16(const void* g, bf16* lds_piece) {
   __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_piece, 16, 0, 0);
+}
+
+// The same DMA issued from inline asm (M0 = the wave-uniform LDS destination): invisible to the
+// compiler's LDS-DMA alias tracking, which otherwise puts an `s_waitcnt vmcnt(0)` in front of the
+// first fragment read of every k-tile of a multi-stage ring (it cannot tell the stage being filled
+// from the one being read) and so drains the prefetch.  The caller orders every DMA'd tile with
+// its own counted vmcnt wait + barrier; the compiler's own waits stay conservative (these DMAs
+// are always older than the loads it counts).
+__device__ __forceinline__ void glds16_async(const void* g, bf16* lds_piece) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_piece);
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(l) : "memory");
 }
 
 // exact m / d for 0 <= m < 2^24 through a float reciprocal
@@ -79,7 +93,12 @@ __device__ __forceinline__ void pw_rc(int m, int RH, int RW, float inv_rw, float
   i = t - b * RH;
 }
 
-template <int BM, int BN, int NS, int MINB>
+// epilogue flavour, a template parameter so each kernel holds only its own epilogue's registers
+// (one generic epilogue - accumulate source + BN input/output quads + statistics live at once -
+// needed ~250 VGPRs and spilled at 2 workgroups per CU)
+enum { PW_EPI_PLAIN = 0, PW_EPI_STATS = 1, PW_EPI_ACC = 2, PW_EPI_BB = 3 };
+
+template <int BM, int BN, int NS, int MINB, int EPI>
 __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_EL = BM * PW_BK, B_EL = BN * PW_BK, ST_EL = A_EL + B_EL;
@@ -140,9 +159,9 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
     const long toff = ((long)a.dy[i_tap] * a.SW + a.dx[i_tap]) * a.SC + i_cb * PW_BK;
     const int woff = a.kt[i_tap] * a.SC + i_cb * PW_BK;
 #pragma unroll
-    for (int j = 0; j < NA; ++j) glds16((a_mask[j] >> i_tap) & 1u ? a_row[j] + toff : zpage, As + (j * 4 + w) * 512);
+    for (int j = 0; j < NA; ++j) glds16_async((a_mask[j] >> i_tap) & 1u ? a_row[j] + toff : zpage, As + (j * 4 + w) * 512);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) glds16(b_row[j] + woff, Bs + (j * 4 + w) * 512);
+    for (int j = 0; j < NB; ++j) glds16_async(b_row[j] + woff, Bs + (j * 4 + w) * 512);
     if (++i_cb == cpt) {
       i_cb = 0;
       if (++i_tap == a.ntaps) {
@@ -163,11 +182,21 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
     if (s < total) issue(s);
 
   int c_ti = t_lo, c_kt = 0;  // compute side
+  int since_epi = 0;          // waits left that an epilogue's stores are younger than
   for (int s = 0; s < total; ++s) {
     // k-tile s has landed once at most the younger in-flight k-tiles are outstanding (over-waiting
     // near the stream's end and behind an epilogue's stores is harmless)
-    if (s + NS - 2 < total) wait_vm<(NS - 2) * P>();
-    else wait_vm<0>();
+    // (vmcnt counts the epilogue's output stores too, and they are YOUNGER than the k-tiles issued
+    // before them: for the NS-1 waits after an epilogue its TM*TN stores are allowed to stay in
+    // flight - waiting for their write acknowledgements was most of this kernel's SQ_WAIT_ANY)
+    if (s + NS - 2 >= total) {
+      wait_vm<0>();
+    } else if (since_epi > 0) {
+      --since_epi;
+      wait_vm<(NS - 2) * P + TM * TN>();
+    } else {
+      wait_vm<(NS - 2) * P>();
+    }
     lds_barrier();  // every wave's DMA of k-tile s is visible; every wave is done reading k-tile s-1
     if (s + NS - 1 < total) issue(s + NS - 1);  // into k-tile s-1's stage
 
@@ -209,11 +238,13 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
         pix = ((long)b * a.OHf + ii * a.ostr + a.oy) * a.OWf + jx * a.ostr + a.ox;
       }
       orow[i] = m < a.M ? a.out + pix * a.N + n0 : nullptr;
+      // rows past M store into the sink page: every lane issues exactly TM*TN stores, the count the
+      // waits above rely on (a branch around a store would make it smaller)
     }
     // epilogue operands, every load before the first use (one latency, not TM*TN): the old
     // output (accumulate) and, for the data gradient's BatchNorm-backward statistics, the BN's input
     // x (and its output y for a mask that cannot be recomputed from x) at the same positions
-    const bool bb = a.bb_x != nullptr;
+    constexpr bool bb = EPI == PW_EPI_BB;
     const bool bb_from_x = bb && a.bb_y == nullptr && a.bb_act == ACT_RELU;
     const bool bb_need_y = bb && a.bb_act != ACT_NONE && !bb_from_x;
     u32x2_t old[TN][TM], xv[TN][TM], yv[TN][TM];
@@ -222,7 +253,7 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const long off = orow[i] ? (long)(orow[i] - a.out) + 16 * j : 0;
-        if (a.accum) old[j][i] = orow[i] ? *reinterpret_cast<const u32x2_t*>(a.out + off) : u32x2_t{0u, 0u};
+        if (EPI == PW_EPI_ACC) old[j][i] = orow[i] ? *reinterpret_cast<const u32x2_t*>(a.out + off) : u32x2_t{0u, 0u};
         if (bb) xv[j][i] = *reinterpret_cast<const u32x2_t*>(a.bb_x + off);
         if (bb_need_y) yv[j][i] = *reinterpret_cast<const u32x2_t*>(a.bb_y + off);
       }
@@ -247,12 +278,12 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         f32x4_t v = acc[j][i];
-        if (a.accum) {
+        if (EPI == PW_EPI_ACC) {
           v[0] += bf2f((bf16)(old[j][i][0] & 0xffffu)); v[1] += bf2f((bf16)(old[j][i][0] >> 16));
           v[2] += bf2f((bf16)(old[j][i][1] & 0xffffu)); v[3] += bf2f((bf16)(old[j][i][1] >> 16));
         }
         const u32x2_t pk = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-        if (orow[i]) *reinterpret_cast<u32x2_t*>(orow[i] + 16 * j) = pk;
+        *reinterpret_cast<u32x2_t*>(orow[i] ? orow[i] + 16 * j : a.sink + ((n0 + 16 * j) & 8191)) = pk;
         acc[j][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         const float y[4] = {bf2f((bf16)(pk[0] & 0xffffu)), bf2f((bf16)(pk[0] >> 16)), bf2f((bf16)(pk[1] & 0xffffu)),
                             bf2f((bf16)(pk[1] >> 16))};
@@ -273,7 +304,7 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
             ssum[j][q] += g;
             ssq[j][q] += g * (x - bmean[q]) * binv[q];
           }
-        } else if (a.bn_part) {
+        } else if (EPI == PW_EPI_STATS) {
           // forward statistics of the STORED values, shifted by the wave's first row (numerically safe)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -288,7 +319,8 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
         }
       }
     }
-    if (!a.bn_part) continue;
+    since_epi = NS - 1;
+    if (EPI != PW_EPI_STATS && EPI != PW_EPI_BB) continue;
     // reduce over the 16 pixels of a lane group, then fold the two wave rows (fixed order)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -334,49 +366,72 @@ __global__ __launch_bounds__(PW_THREADS, MINB) void pw_kernel(const PwArgs a) {
   }
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
+// DTFE_PW="<mode>[,cfg=<id>][,grid=<workgroups>][,mintiles=<n>]" (A/B and tests): mode off | bb |
+// all, see run_igemm_pipe; the options override the tile / ring choice, the grid and the
+// smallest launch that goes persistent.
+int pw_opt(const char* key, int dflt) {
+  const char* e = std::getenv("DTFE_PW");
+  const size_t n = std::strlen(key);
+  while (e && *e) {
+    if (!std::strncmp(e, key, n) && e[n] == '=') return std::atoi(e + n + 1);
+    e = std::strchr(e, ',');
+    if (e) ++e;
+  }
+  return dflt;
+}
+
+enum { PW_MODE_OFF = 0, PW_MODE_BB = 1, PW_MODE_ALL = 2 };
+int pw_mode() {
+  const char* e = std::getenv("DTFE_PW");
+  if (!e || !*e) return PW_DEFAULT_MODE;
+  if (!std::strncmp(e, "off", 3)) return PW_MODE_OFF;
+  if (!std::strncmp(e, "bb", 2)) return PW_MODE_BB;
+  return PW_MODE_ALL;
 }
 
 template <int BM, int BN, int NS, int MINB>
-void launch_pw(PwArgs& a, hipStream_t s) {
+void launch_pw(PwArgs& a, int epi, hipStream_t s) {
   a.tiles_m = (a.M + BM - 1) / BM;
   const int T = a.tiles_m * (a.N / BN);
   int grid = 256 * MINB;
-  const int g_env = env_int("DTFE_PW_GRID", 0);
+  const int g_env = pw_opt("grid", 0);
   if (g_env > 0) grid = g_env;
   grid = std::min(grid, T);
-  hipLaunchKernelGGL((pw_kernel<BM, BN, NS, MINB>), dim3(grid), dim3(PW_THREADS), 0, s, a);
+  switch (epi) {
+    case PW_EPI_STATS: hipLaunchKernelGGL((pw_kernel<BM, BN, NS, MINB, PW_EPI_STATS>), dim3(grid), dim3(PW_THREADS), 0, s, a); break;
+    case PW_EPI_ACC: hipLaunchKernelGGL((pw_kernel<BM, BN, NS, MINB, PW_EPI_ACC>), dim3(grid), dim3(PW_THREADS), 0, s, a); break;
+    case PW_EPI_BB: hipLaunchKernelGGL((pw_kernel<BM, BN, NS, MINB, PW_EPI_BB>), dim3(grid), dim3(PW_THREADS), 0, s, a); break;
+    default: hipLaunchKernelGGL((pw_kernel<BM, BN, NS, MINB, PW_EPI_PLAIN>), dim3(grid), dim3(PW_THREADS), 0, s, a); break;
+  }
 }
 
-// tile / ring choice (DTFE_PW_CFG=<id> for A/B): 0 = 128x128 NS2 (2 WG/CU), 1 = 128x128 NS3 (1 WG/CU),
+// tile / ring choice (DTFE_PW cfg=<id> for A/B): 0 = 128x128 NS2 (2 WG/CU), 1 = 128x128 NS3 (1 WG/CU),
 // 2 = 128x64 NS3 (2 WG/CU), 3 = 128x128 NS4 (1 WG/CU)
 int pw_cfg(int N) {
-  const int e = env_int("DTFE_PW_CFG", -1);
+  const int e = pw_opt("cfg", -1);
   if (e >= 0 && e <= 3 && (e == 2 || N % 128 == 0)) return e;
   return N % 128 == 0 ? 0 : 2;
 }
 
-void run_pw(PwArgs& a, hipStream_t s) {
+void run_pw(PwArgs& a, int epi, hipStream_t s) {
   switch (pw_cfg(a.N)) {
-    case 1: launch_pw<128, 128, 3, 1>(a, s); break;
-    case 2: launch_pw<128, 64, 3, 2>(a, s); break;
-    case 3: launch_pw<128, 128, 4, 1>(a, s); break;
-    default: launch_pw<128, 128, 2, 2>(a, s); break;
+    case 1: launch_pw<128, 128, 3, 1>(a, epi, s); break;
+    case 2: launch_pw<128, 64, 3, 2>(a, epi, s); break;
+    case 3: launch_pw<128, 128, 4, 1>(a, epi, s); break;
+    default: launch_pw<128, 128, 2, 2>(a, epi, s); break;
   }
 }
 
 }  // namespace
 
 bool run_igemm_pipe(const IgemmArgs& g, long Mmax, hipStream_t s) {
-  const int off = env_int("DTFE_PW_OFF", 0);
-  if (off || g.nphase != 1 || g.SC % PW_BK || g.N % 64) return false;
+  const int mode = pw_mode();
+  if (mode == PW_MODE_OFF || (mode == PW_MODE_BB && !g.bb_x) || g.nphase != 1 || g.SC % PW_BK || g.N % 64) return false;
   const IgPhase& P = g.ph[0];
   if (P.ntaps < 1) return false;
   PwArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.A = g.src; a.W = g.w; a.out = g.out; a.zeros = g.zeros;
+  a.A = g.src; a.W = g.w; a.out = g.out; a.zeros = g.zeros; a.sink = ig_sink_page(s);
   a.M = (int)Mmax; a.N = g.N; a.SC = g.SC; a.Ktot = g.Ktot;
   a.RH = P.RH; a.RW = P.RW; a.SH = g.SH; a.SW = g.SW; a.istr = g.istr;
   a.OHf = g.OHf; a.OWf = g.OWf; a.ostr = g.ostr; a.oy = P.oy; a.ox = P.ox;
@@ -388,12 +443,15 @@ bool run_igemm_pipe(const IgemmArgs& g, long Mmax, hipStream_t s) {
     a.bb_x = g.bb_x; a.bb_y = g.bb_y; a.bb_mean = g.bb_mean; a.bb_invstd = g.bb_invstd;
     a.bb_gamma = g.bb_gamma; a.bb_beta = g.bb_beta; a.bb_act = g.bb_act;
   }
+  // one epilogue flavour per launch (the combinations no conv issues stay on the per-tile kernel)
+  const int epi = g.bb_x ? PW_EPI_BB : g.bn_part ? PW_EPI_STATS : g.accum ? PW_EPI_ACC : PW_EPI_PLAIN;
+  if ((g.bb_x || g.bn_part) && g.accum) return false;
   // too few tiles for a persistent grid: the per-tile kernel's split-K spreads them better
   const int bn = pw_cfg(a.N) == 2 ? 64 : 128;
   const long tiles = (Mmax + 127) / 128 * (a.N / bn);
-  const long min_tiles = env_int("DTFE_PW_MINTILES", 256);
+  const long min_tiles = pw_opt("mintiles", 256);
   if (tiles < min_tiles) return false;
-  run_pw(a, s);
+  run_pw(a, epi, s);
   return true;
 }
 

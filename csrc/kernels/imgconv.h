@@ -48,7 +48,7 @@ struct ImgConvArgs {
   uint32_t* zptr[4];
   long zlen[4];
   int nz;
-  int diag;                 // ablation bits for kernel experiments (DTFE_IC_DIAG; 0 in production)
+  int diag;                 // ablation bits for kernel experiments (DTFE_DIAG ic=<bits>; 0 in production)
 };
 
 // Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]
@@ -69,7 +69,7 @@ struct ImgWgradArgs {
   // more images each and halve the partial-sum traffic - the better trade when the launch
   // runs beside other work (MNIST conv2's weight grad on its own graph branch)
   int max_blocks;
-  int diag;                 // ablation bits for kernel experiments (DTFE_IW_DIAG; 0 in production)
+  int diag;                 // ablation bits for kernel experiments (DTFE_DIAG iw=<bits>; 0 in production)
 };
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);

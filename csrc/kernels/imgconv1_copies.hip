@@ -304,10 +304,7 @@ bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s) {
   if (!mnist_conv1_shape(a.B, a.SH, a.SW, a.CS, a.OH, a.OW, a.N, a.KH, a.KW, a.stride, a.pad)) return false;
   if (!a.src || !a.pool || a.flip_taps || a.dil > 1 || a.relu_mask) return false;
   const int grid = a.B < 1024 ? a.B : 1024;
-  static const int diag = [] {
-    const char* e = getenv("DTFE_C1_DIAG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int diag = diag_bits("c1");
   ImgConvArgs ad = a;
   ad.diag = diag;
   switch (a.act) {
@@ -321,16 +318,13 @@ bool launch_conv1_copies_fwd(const ImgConvArgs& a, hipStream_t s) {
 bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s) {
   if (!mnist_conv1_shape(a.B, a.SH, a.SW, a.CS, a.OH, a.OW, a.N, a.KH, a.KW, a.stride, a.pad)) return false;
   if (!a.src || a.dy || !a.dy_pooled) return false;
-  // DTFE_C1W_GRID: workgroups (images per workgroup = B / grid); DTFE_C1W_DIAG: ablation bits
+  // DTFE_C1W_GRID: workgroups (images per workgroup = B / grid); DTFE_DIAG c1w=<bits>: ablation bits
   // (1 skip the un-pooled dY image, 2 skip the shifted copies, 4 skip the MFMA tiles, 8 skip the flush)
   static const int want = [] {
     const char* e = getenv("DTFE_C1W_GRID");
     return e ? atoi(e) : 320;  // beside conv2's weight gradient: 320 / 384 ~0.8 % faster than 256 (r3zg)
   }();
-  static const int diag = [] {
-    const char* e = getenv("DTFE_C1W_DIAG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int diag = diag_bits("c1w");
   const int grid = a.B < want ? a.B : (want < 1 ? 1 : want);
   if (a.ws && (long)grid * (NCH * 25 + NCH) > imgwgrad_ws_floats(NCH, 25))
     throw std::runtime_error("conv1 wgrad: partials exceed the workspace");

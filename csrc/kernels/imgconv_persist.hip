@@ -657,10 +657,7 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
   const size_t lds = persist_lds(G) + (POOLED ? 0 : (size_t)(a.OH * a.OW / 4) * a.N * 3);
   if (lds > 160 * 1024 || (a.pool && !G.blocked)) return false;
   const int grid = a.B < 256 ? a.B : 256;
-  static const int diag = [] {
-    const char* e = getenv("DTFE_IC_DIAG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int diag = diag_bits("ic");
   ImgConvArgs ad = a;
   ad.diag = diag;
   auto go = [&](auto kern) {

@@ -416,10 +416,7 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   const int grid = a.B < gcap ? a.B : gcap;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    static const int diag = [] {
-      const char* e = getenv("DTFE_IW_DIAG");
-      return e ? atoi(e) : 0;
-    }();
+    static const int diag = diag_bits("iw");
     ImgWgradArgs ad = a;
     ad.diag = diag;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, ad, G);

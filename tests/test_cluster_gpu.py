@@ -83,8 +83,11 @@ def test_allreduce_rank_crash_ends_every_rank(tmp_path):
     assert time.time() - t0 < 200
     assert codes[("worker", 1)] == 17, codes
     assert codes[("worker", 0)] not in (0, None), (codes, out[("worker", 0)][-20:])
-    assert any("silent for" in l or "store unreachable" in l or "engine failure" in l
-               for l in out[("worker", 0)]), out[("worker", 0)][-20:]
+    # worker 0 ends either through its comm watchdog (peer silent / store gone / engine error) or
+    # because the host-side collective (gloo) raised on the dead peer first - never a hang
+    w0 = out[("worker", 0)]
+    assert any("silent for" in l or "store unreachable" in l or "engine failure" in l or "Traceback" in l
+               for l in w0), "\n".join(w0[-30:])
 
 
 @pytest.mark.parametrize("hogwild", [False, True])

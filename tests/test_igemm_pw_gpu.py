@@ -1,11 +1,11 @@
 """The persistent pipelined implicit-GEMM kernel (csrc/kernels/igemm_pw.hip) vs fp32 references and
-vs the per-tile implicit-GEMM kernel (DTFE_PW_OFF=1).
+vs the per-tile implicit-GEMM kernel (DTFE_PW=off).
 
 Covers: 1x1 and 3x3 forward at stride 1 / 2 with the fused BatchNorm statistics, stride-1 data
 gradients (1x1, 3x3 with flipped taps), the stride-2 1x1 data gradient that accumulates onto the
-shortcut's share, M not a multiple of the tile, every tile / ring configuration (DTFE_PW_CFG) and
+shortcut's share, M not a multiple of the tile, every tile / ring configuration (DTFE_PW cfg=) and
 small grids that make every workgroup stream several tiles (the k-tile stream crossing tile
-boundaries, DTFE_PW_GRID).  DTFE_PW_MINTILES=1 keeps these small shapes on the persistent path."""
+boundaries, DTFE_PW grid=).  mintiles=1 keeps these small shapes on the persistent path."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -36,11 +36,14 @@ def _stats_ref(y):
     return torch.stack([d.sum(0), (d * d).sum(0)])
 
 
+def _pw(monkeypatch, **kw):
+    """DTFE_PW=all,<k>=<v>... (every one-phase launch on the persistent kernel, small shapes too)"""
+    monkeypatch.setenv("DTFE_PW", ",".join(["all", "mintiles=1"] + ["%s=%s" % kv for kv in kw.items()]))
+
+
 @pytest.fixture(params=[None, "0", "1", "2", "3"])
 def cfg(request, monkeypatch):
-    monkeypatch.setenv("DTFE_PW_MINTILES", "1")
-    if request.param is not None:
-        monkeypatch.setenv("DTFE_PW_CFG", request.param)
+    _pw(monkeypatch, **({} if request.param is None else {"cfg": request.param}))
     return request.param
 
 
@@ -49,7 +52,7 @@ def cfg(request, monkeypatch):
 def test_pw_fwd_with_bn_stats(case, grid, cfg, monkeypatch):
     B, H, C, Cout, s, k = case
     if grid:
-        monkeypatch.setenv("DTFE_PW_GRID", grid)
+        _pw(monkeypatch, grid=grid, **({} if cfg is None else {"cfg": cfg}))
     pad = (k - 1) // 2
     OH = (H + 2 * pad - k) // s + 1
     g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=k, KW=k, stride=s, pad=pad)
@@ -68,7 +71,7 @@ def test_pw_fwd_with_bn_stats(case, grid, cfg, monkeypatch):
     sr = _stats_ref(y.cpu())
     assert torch.allclose(st.double().cpu(), sr, rtol=1e-4, atol=1e-3 * B * OH * OH), (st.cpu(), sr)
     # the per-tile implicit-GEMM kernel computes the same products: identical output
-    monkeypatch.setenv("DTFE_PW_OFF", "1")
+    monkeypatch.setenv("DTFE_PW", "off")
     y2 = torch.empty_like(y)
     st2 = torch.zeros_like(st)
     ops.conv_fwd(x.to(DEV), w.to(DEV), None, y2, None, g, act=ops.ACT_NONE, stats=st2)
@@ -81,7 +84,7 @@ def test_pw_fwd_with_bn_stats(case, grid, cfg, monkeypatch):
 def test_pw_dgrad(case, grid, cfg, monkeypatch):
     B, H, C, Cout, s, k = case
     if grid:
-        monkeypatch.setenv("DTFE_PW_GRID", grid)
+        _pw(monkeypatch, grid=grid, **({} if cfg is None else {"cfg": cfg}))
     pad = (k - 1) // 2
     OH = (H + 2 * pad - k) // s + 1
     g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=OH, OW=OH, KH=k, KW=k, stride=s, pad=pad)
@@ -107,8 +110,9 @@ def test_pw_dgrad(case, grid, cfg, monkeypatch):
         assert torch.equal(dx.cpu()[:, m], base[:, m])
 
 
-def test_pw_large_m_many_tiles_per_workgroup():
+def test_pw_large_m_many_tiles_per_workgroup(monkeypatch):
     """ResNet-50 stage-1 expand at batch 16 (M = 50176): every workgroup streams ~100 tiles."""
+    _pw(monkeypatch)
     B, H, C, Cout = 16, 56, 64, 256
     g = dict(B=B, H=H, W=H, C=C, Cout=Cout, OH=H, OW=H, KH=1, KW=1, stride=1, pad=0)
     torch.manual_seed(3)

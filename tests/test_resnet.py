@@ -305,10 +305,10 @@ def test_conv_dgrad_bn_bwd_stats_gpu(case, pipe, monkeypatch):
     """conv_dgrad(bn_bwd=...) fills the consuming BN's backward statistics from the implicit-GEMM
     epilogue; they must equal a separate bn_bwd_stats pass over the same finished dx.  pipe=1: the
     persistent pipelined kernel's register epilogue (igemm_pw.hip) wherever the launch has one
-    phase; pipe=0: the per-tile kernel's LDS epilogue."""
+    phase; pipe=0: the per-tile kernel's LDS epilogue (strided) or the separate statistics pass
+    (one phase)."""
     from dtfe import ops
-    monkeypatch.setenv("DTFE_PW_MINTILES", "1")
-    monkeypatch.setenv("DTFE_PW_OFF", "0" if pipe == "1" else "1")
+    monkeypatch.setenv("DTFE_PW", "all,mintiles=1" if pipe == "1" else "off")
     B, H, C, CO, K, s, acc, mask = case
     dev = torch.device("cuda", 0)
     pad = (K - 1) // 2
