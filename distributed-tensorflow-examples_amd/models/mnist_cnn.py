@@ -36,7 +36,6 @@ all-reduced over RCCL while the conv backward kernels still run.
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -231,12 +230,10 @@ class MnistCnnTrainer:
         self._late = None        # (grad16, gscale) while a data-parallel step runs its split Adam
         self.schedule = []       # launch order of the last step's milestones (host side = graph order)
         self.logits = None
-        # one replica: the fc/head Adam (98 % of the parameters, ~18 us of HBM traffic) on its own
-        # stream beside the conv backward, forked right after the grouped fc backward (its last
-        # reader of the fc weights); A/B knob while measured (DTFE_CNN_FC_ADAM_SIDE=0 / 1)
-        self.fc_adam_side = self.par and os.environ.get("DTFE_CNN_FC_ADAM_SIDE", "0") == "1"
+        # (one replica runs the whole-model Adam after the backward: the fc/head Adam on a side
+        # stream beside the conv backward measured 0.204 -> 0.234-0.241 ms/step,
+        # profiles/r4_comm_rehearsal.txt)
         if self.par:
-            self.s_fc = torch.cuda.Stream(device=d)
             self.s_c2 = torch.cuda.Stream(device=d)
             self.ws_c2 = torch.empty(ops.wgrad_ws_floats(C2, KS * KS * C1), device=d, dtype=torch.float32)
 
@@ -294,10 +291,6 @@ class MnistCnnTrainer:
         if self.allreduce is not None:
             self.allreduce.launch(0)  # bucket 0 (head + fc1, 98% of the bytes) overlaps the conv backward
             self.schedule.append("allreduce:0")
-        elif self._late is not None:  # one replica: fc/head Adam beside the conv backward
-            self.s_fc.wait_stream(main)
-            with torch.cuda.stream(self.s_fc):
-                self.opt_fc.step(grad16=self._late[0], gscale=self._late[1], gs_inc=0)
         # conv2's data gradient is captured before its weight gradient (same fork point): the graph
         # runs the data gradient -> conv1 weight-gradient chain on the launch queue, first on the
         # CUs, and the weight gradient (192 workgroups) fills in beside it - 0.2103-0.2126 vs
@@ -322,8 +315,6 @@ class MnistCnnTrainer:
                 self.opt_fc.step(grad16=self._late[0], gscale=self._late[1], gs_inc=0)
             self.allreduce.wait()
         if self._late is not None:
-            if self.allreduce is None:
-                main.wait_stream(self.s_fc)
             self.opt_conv.step(grad16=self._late[0], gscale=self._late[1], gs_inc=1)
 
     def _head_wgrad(self):
@@ -374,7 +365,7 @@ class MnistCnnTrainer:
         """One training step: forward, backward (+ all-reduce), Adam.  ``grad16``: the all-reduced
         bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
         gscale = 1.0 / self.world if gscale is None else gscale
-        if not self.par or not (self.late_split and (self.allreduce is not None or self.fc_adam_side)):
+        if not self.par or not (self.late_split and self.allreduce is not None):
             self.forward_backward()
             self.opt.step(grad16=grad16, gscale=gscale)
             return

@@ -18,14 +18,13 @@ import torch.distributed as dist
 from .ipc import IpcComm
 from .rccl import RcclComm
 
-# Gradient bucket size (MB of fp32 gradient; half that on a bf16 wire).  Sizing for 8 GPUs on
-# point-to-point xGMI (7 links per GPU): the two-shot IPC kernel moves 2*(W-1)/W of a bucket per
-# rank spread over all 7 links at once, so its per-bucket time is ~latency (two cross-GPU
-# barriers, a few us) + bytes / (7 links); a ring's per-link bound does not apply.  Overlap with
-# backward wants several buckets per step for the large models (ResNet-50: 51 MB bf16 -> 13
-# buckets of 4 MB on the wire), while every extra bucket adds one barrier latency and one graph
-# node.  16 MB fp32 = 8 MB bf16 sits where the IPC staging (cap = largest bucket) stays small and
-# the per-bucket fixed cost is < 10 % of the transfer.  Override with --bucket_mb.
+# Gradient bucket size (MB of fp32 gradient; half that on a bf16 wire).  Measured, ResNet-50 B=256
+# data-parallel over the IPC engine at W=2 (two ranks sharing one MI355X, the rehearsal this pool
+# allows; profiles/r4_comm_rehearsal.txt): 2 / 4 / 8 / 16 / 32 MB -> 55.5 / 54.9 / 53.9 / 54.1 /
+# 53.6 ms per step - flat within 3.5 %, small buckets slightly worse (one barrier latency and graph
+# node each).  16 MB keeps ResNet-50's 51 MB bf16 gradient in 7 buckets so the first all-reduces
+# start while the backward still has most of its layers to run (the overlap an 8-GPU node needs),
+# at the IPC staging cap of one 8 MB bucket.  Override with --bucket_mb.
 DEFAULT_BUCKET_MB = 16.0
 
 
