@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--tiles", type=lambda v: [int(t) for t in v.split(",")], default=[0, 2, 5, 6, 8, 10, 12],
                     help="tile ids (ops.TILE_DIMS)")
+    ap.add_argument("--splits", type=lambda v: [int(t) for t in v.split(",")], default=None,
+                    help="split-K factors for every tile (default 1,2,4 below tile 14, 1 above)")
     a = ap.parse_args()
     B, K1, FC = a.batch, 3136, 1024
     d, bf = "cuda", torch.bfloat16
@@ -67,7 +69,7 @@ def main():
         print(f"{name:10s} torch.mm {tr:8.1f} us {fl / tr / 1e6:7.1f} TFLOP/s", flush=True)
         for tile in a.tiles:
             row = []
-            for s in ((1, 2, 4) if tile < 14 else (1,)):
+            for s in (a.splits or ((1, 2, 4) if tile < 14 else (1,))):
                 try:
                     t = timeit(lambda: fn(tile, s), a.iters)
                 except RuntimeError:

@@ -90,13 +90,13 @@ __device__ __forceinline__ bool dense_epi(const DenseGemmArgs& a, int row, int c
 // the caller has passed a barrier), optional deterministic split-K combine (last arriver), then
 // the fused epilogue walking 8-column chunks (coalesced 16-32 B stores).  Shared by the
 // register-staged kernel below and the global_load_lds kernel of gemm_glds.h.
-template <typename Cfg>
+template <typename Cfg, int NT = GEMM_THREADS>
 __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* smem_raw, f32x4_t (&acc)[Cfg::TM][Cfg::TN],
                                                int tm, int tn, int tiles_m, int tiles_n) {
   constexpr int CLD = Cfg::BN + 4;  // f32 C tile row stride: 16*(odd) bytes, conflict-free quad writes
   float* Cs = reinterpret_cast<float*>(smem_raw);
   const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
-  {
+  if (NT == GEMM_THREADS || threadIdx.x < GEMM_THREADS) {  // (NT > 256: the first 4 waves hold the folded tile)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid / Cfg::WARPS_N, wn = wid % Cfg::WARPS_N;
 #pragma unroll
@@ -125,7 +125,7 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
     // visible to a last arriver on another XCD without a release (MI355X_MICROARCH.md, valid forms);
     // tests/test_kernels_gpu.py::test_splitk_combine_many_splits_deterministic pins it.
     const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(mine, (short)0, Cfg::BM * Cfg::BN * 4, 0x00020000);
-    for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
+    for (int ch = threadIdx.x; ch < NCH; ch += NT) {
       const int r = ch / CPR, c = (ch % CPR) * 8;
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c), slab, ch * 32, 0, 16);
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4_t*>(Cs + r * CLD + c + 4), slab, ch * 32 + 16, 0,
@@ -148,7 +148,7 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
     const int last = *flag;
     __syncthreads();
     if (!last) return;
-    for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
+    for (int ch = threadIdx.x; ch < NCH; ch += NT) {
       const int r = ch / CPR, c = (ch % CPR) * 8;
       f32x4_t v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
       for (int z = 0; z < (int)gridDim.z; ++z) {
@@ -167,7 +167,7 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
   // (a weight-gradient GEMM's bias row / column only takes the per-element path in its own chunks)
   const bool vec_store = !a.atomic && !a.unpool && !a.out2 && a.beta == 0.f &&
                          (a.ldc % 8) == 0 && ((((uintptr_t)a.out) & 15) == 0);
-  for (int ch = threadIdx.x; ch < NCH; ch += GEMM_THREADS) {
+  for (int ch = threadIdx.x; ch < NCH; ch += NT) {
     const int r = ch / CPR, c = (ch % CPR) * 8;
     const int row = m_base + r, col0 = n_base + c;
     if (row >= a.M || col0 >= a.N) continue;
@@ -257,6 +257,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dense_kernel(DenseGemmArgs 
 // (register-staged engine of gemm_core.h); 5 = 128x128, 6 = 128x64, 7 = 64x128, 8 = 64x64 with
 // direct global->LDS staging, 3 stages (gemm_glds.h: bf16, K % 64 == 0, whole tiles - see
 // gemm_glds_eligible); 9..12 the same tiles with 2 stages; 14..16 64x64 with 4 / 6 / 8 stages,
+// 19..21 64x64 with 2 / 4 / 2 in-workgroup k-groups,
 // 17..18 128x64 with 4 / 6 stages
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream);

@@ -19,11 +19,12 @@ static void launch_one(int splits, const DenseGemmArgs& args, hipStream_t s) {
 }
 
 int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
-  static const int dims[19][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
+  static const int dims[22][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64}, {16, 16},
-                                  {64, 64}, {64, 64}, {64, 64}, {128, 64}, {128, 64}};
-  if (tile < 0 || tile > 18) return -1;
+                                  {64, 64}, {64, 64}, {64, 64}, {128, 64}, {128, 64},
+                                  {64, 64}, {64, 64}, {64, 64}};
+  if (tile < 0 || tile > 21) return -1;
   bm = dims[tile][0];
   bn = dims[tile][1];
   if (tile == GEMM_TILE_SMALL) return 16;
@@ -50,11 +51,13 @@ bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGe
 // tiles 9..12: 2 stages, half the LDS, so more workgroups share a CU (grids of many tiles);
 // tiles 14..18: deeper pipelines (64x64 with 4 / 6 / 8 stages, 128x64 with 4 / 6) for long-K grids
 // of about one workgroup per CU, where 3 stages leave the k-loop waiting on the load latency
-template <int BM, int BN, int AM, int BMD, int STAGES>
+// tiles 19..21: 64x64 with 2 / 4 k-groups of 4 waves splitting the k-tiles inside the workgroup
+// (3 / 2 / 4 stages per group): more waves issuing global->LDS DMA per CU for ~one tile per CU
+template <int BM, int BN, int AM, int BMD, int STAGES, int KG = 1>
 static void launch_glds(int splits, const DenseGemmArgs& a, hipStream_t s) {
   const int tiles = (a.M / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, AM, BMD, STAGES>), grid, dim3(GEMM_THREADS), 0, s, a);
+  hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, AM, BMD, STAGES, KG>), grid, dim3(GEMM_THREADS * KG), 0, s, a);
 }
 
 template <int AM, int BMD>
@@ -73,6 +76,9 @@ static void glds_by_tile(int tile, int splits, const DenseGemmArgs& a, hipStream
     case 16: launch_glds<64, 64, AM, BMD, 8>(splits, a, s); break;
     case 17: launch_glds<128, 64, AM, BMD, 4>(splits, a, s); break;
     case 18: launch_glds<128, 64, AM, BMD, 6>(splits, a, s); break;
+    case 19: launch_glds<64, 64, AM, BMD, 3, 2>(splits, a, s); break;
+    case 20: launch_glds<64, 64, AM, BMD, 2, 4>(splits, a, s); break;
+    case 21: launch_glds<64, 64, AM, BMD, 4, 2>(splits, a, s); break;
     default: throw std::runtime_error("gemm_dense: bad glds tile id");
   }
 }

@@ -89,32 +89,44 @@ struct GlOperand {
   }
 };
 
-template <int BM, int BN, int STAGES> struct GlSmem {
+template <int BM, int BN, int STAGES, int KG = 1> struct GlSmem {
   static constexpr int STAGE_EL = (BM + BN) * GL_BK;
-  static constexpr int STAGING = STAGES * STAGE_EL * 2;
+  static constexpr int STAGING = KG * STAGES * STAGE_EL * 2;
   static constexpr int CTILE = BM * (BN + 4) * 4;
   static constexpr int BYTES = STAGING > CTILE ? STAGING : CTILE;
 };
 
-// One output tile (workgroup `bid` of this GEMM's grid); smem_raw: GlSmem<BM, BN, STAGES>::BYTES of LDS.
+// One output tile (workgroup `bid` of this GEMM's grid); smem_raw: GlSmem<BM, BN, STAGES, KG>::BYTES of LDS.
 // Shared by the plain launch below and the grouped launch (gemm_glds_group_kernel).
-template <int BM, int BN, int AMODE, int BMODE, int STAGES>
+//
+// KG > 1: KG groups of 4 waves (256 * KG threads) split the workgroup's k-tiles round-robin, each
+// group with its own STAGES-deep ring, and fold their accumulators through LDS before the
+// epilogue.  The global -> LDS DMA rate of a CU grows with the number of waves issuing it, not
+// with the ring depth of one wave (profiles/r3_cnn_kernel_tuning.txt: 1 workgroup per CU streams
+// 20-30 B/clk whatever its depth, 3 workgroups 35-44): a long-K GEMM with ~one tile per CU (the
+// MNIST fc1 forward) gets the extra waves without splitting K across workgroups.
+template <int BM, int BN, int AMODE, int BMODE, int STAGES, int KG = 1>
 __device__ __forceinline__ void gemm_glds_body(const DenseGemmArgs& a, int bid, char* smem_raw) {
   using Cfg = TileCfg<bf16, BM, BN, 2, 2, GL_BK>;
   using OA = GlOperand<BM, AMODE>;
   using OB = GlOperand<BN, BMODE>;
   constexpr int NPT = OA::NP + OB::NP;  // DMA instructions per thread and k-tile
-  using SM = GlSmem<BM, BN, STAGES>;
+  using SM = GlSmem<BM, BN, STAGES, KG>;
   bf16* smem = reinterpret_cast<bf16*>(smem_raw);
+  const int kg = KG > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) : 0;  // k-group of this wave
 
   const int tiles_m = a.M / BM, tiles_n = (a.N + BN - 1) / BN;
   int tm, tn;
   tile_coords(bid, tiles_m, tiles_n, tm, tn);
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
   const int m_base = tm * BM, n_base = tn * BN;
   const int kt0 = blockIdx.z * (a.k_chunk / GL_BK);
-  const int nk = min(a.K, (int)(blockIdx.z + 1) * a.k_chunk) / GL_BK - kt0;
+  const int nk_all = min(a.K, (int)(blockIdx.z + 1) * a.k_chunk) / GL_BK - kt0;
+  // this group's k-tiles: kg, kg + KG, ... (local index t -> k-tile kg + t * KG); the loop runs the
+  // largest group's count so every wave meets every barrier
+  const int nk = (nk_all - kg + KG - 1) / KG;
+  const int nloop = (nk_all + KG - 1) / KG;
 
   OA oa;
   OB ob;
@@ -129,17 +141,18 @@ __device__ __forceinline__ void gemm_glds_body(const DenseGemmArgs& a, int bid, 
 #pragma unroll
     for (int j = 0; j < Cfg::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto stage_a = [&](int s) { return smem + s * SM::STAGE_EL; };
-  auto stage_b = [&](int s) { return smem + s * SM::STAGE_EL + OA::ELEMS; };
+  bf16* ring = smem + kg * STAGES * SM::STAGE_EL;
+  auto stage_a = [&](int s) { return ring + s * SM::STAGE_EL; };
+  auto stage_b = [&](int s) { return ring + s * SM::STAGE_EL + OA::ELEMS; };
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) {
-      oa.issue(s, stage_a(s), w);
-      ob.issue(s, stage_b(s), w);
+      oa.issue(kg + s * KG, stage_a(s), w);
+      ob.issue(kg + s * KG, stage_b(s), w);
     }
   const int wm = w >> 1, wn = w & 1;
   int cur = 0;
-  for (int t = 0; t < nk; ++t) {
+  for (int t = 0; t < nloop; ++t) {
     // tile t landed (this wave's pieces: counted wait leaving the younger tiles in flight),
     // then a barrier so every wave's pieces of tile t are visible and tile t-1's buffer is free
     if (t + STAGES - 2 < nk) {
@@ -152,9 +165,10 @@ __device__ __forceinline__ void gemm_glds_body(const DenseGemmArgs& a, int bid, 
     if (t + STAGES - 1 < nk) {
       int s = cur + STAGES - 1;
       if (s >= STAGES) s -= STAGES;
-      oa.issue(t + STAGES - 1, stage_a(s), w);
-      ob.issue(t + STAGES - 1, stage_b(s), w);
+      oa.issue(kg + (t + STAGES - 1) * KG, stage_a(s), w);
+      ob.issue(kg + (t + STAGES - 1) * KG, stage_b(s), w);
     }
+    if (KG > 1 && t >= nk) continue;  // (a group one k-tile short: still at every barrier)
     const bf16* As = stage_a(cur);
     const bf16* Bs = stage_b(cur);
 #pragma unroll
@@ -174,13 +188,33 @@ __device__ __forceinline__ void gemm_glds_body(const DenseGemmArgs& a, int bid, 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the staging LDS for the C tile
-  dense_epilogue<Cfg>(a, smem_raw, acc, tm, tn, tiles_m, tiles_n);
+  if constexpr (KG > 1) {
+    // groups 1.. park their accumulators lane-linearly in LDS, group 0 adds them in group order
+    constexpr int FR = Cfg::TM * Cfg::TN;
+    f32x4_t* park = reinterpret_cast<f32x4_t*>(smem_raw);
+    if (kg > 0) {
+#pragma unroll
+      for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j) park[(((kg - 1) * 4 + w) * FR + i * Cfg::TN + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (kg == 0) {
+      for (int g = 1; g < KG; ++g)
+#pragma unroll
+        for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < Cfg::TN; ++j) acc[i][j] += park[(((g - 1) * 4 + w) * FR + i * Cfg::TN + j) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  dense_epilogue<Cfg, GEMM_THREADS * KG>(a, smem_raw, acc, tm, tn, tiles_m, tiles_n);
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int STAGES>
-__global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_kernel(DenseGemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem_raw[GlSmem<BM, BN, STAGES>::BYTES];
-  gemm_glds_body<BM, BN, AMODE, BMODE, STAGES>(a, blockIdx.x, smem_raw);
+template <int BM, int BN, int AMODE, int BMODE, int STAGES, int KG = 1>
+__global__ __launch_bounds__(GEMM_THREADS * KG, 1) void gemm_glds_kernel(DenseGemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[GlSmem<BM, BN, STAGES, KG>::BYTES];
+  gemm_glds_body<BM, BN, AMODE, BMODE, STAGES, KG>(a, blockIdx.x, smem_raw);
 }
 
 }  // namespace dtfe

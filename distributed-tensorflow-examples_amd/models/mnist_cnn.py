@@ -212,10 +212,11 @@ class MnistCnnTrainer:
         self.fused_gather = True
         self.late_split = True
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the forward
-        # streams 3 k-tiles deep (one 64x64 tile per CU), data / weight gradient take the 2-stage
-        # variant (784 / 800 tiles, several workgroups per CU)
+        # (one 64x64 tile per CU, 49 k-tiles) with two 4-wave k-groups per workgroup, 3 stages each
+        # (tile 19: 15.6 us vs 19.9 for one group, torch.mm 21.3 - profiles/r4_fc1_kgroups.txt);
+        # data / weight gradient take the 2-stage variant (784 / 800 tiles, several per CU)
         K1 = 7 * 7 * C2
-        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 8)
+        self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 19)
         self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
         self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
         # head weight gradient: the dedicated whole-batch kernel up to B = 1024, above that a split-K

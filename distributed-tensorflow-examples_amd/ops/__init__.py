@@ -36,8 +36,9 @@ TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)
              9: (128, 128), 10: (128, 64), 11: (64, 128), 12: (64, 64),   # 2 stages (more WGs per CU)
              13: (16, 16),   # exact-fp32 small-layer kernel (gemm_small.hip): no split-K, in-WG K split
              14: (64, 64), 15: (64, 64), 16: (64, 64),  # 4 / 6 / 8 stages (long-K grids, ~1 WG per CU)
-             17: (128, 64), 18: (128, 64)}              # 4 / 6 stages
-GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18)
+             17: (128, 64), 18: (128, 64),              # 4 / 6 stages
+             19: (64, 64), 20: (64, 64), 21: (64, 64)}  # 2 / 4 / 2 in-workgroup k-groups (3 / 2 / 4 stages)
+GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21)
 TILE_SMALL = 13
 _ONES = {}
 

@@ -16,7 +16,7 @@ def _mat(t, mode, rows, K):
     return t.float() if mode == ops.KMAJ else t.float().t()
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7, 8, 9, 12, 14, 15, 16, 17, 18])
+@pytest.mark.parametrize("tile", [5, 6, 7, 8, 9, 12, 14, 15, 16, 17, 18, 19, 20, 21])
 @pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("splits", [1, 3])
 def test_glds_gemm_layouts(tile, modes, splits):
@@ -35,7 +35,7 @@ def test_glds_gemm_layouts(tile, modes, splits):
     assert err < 1e-5, err
 
 
-@pytest.mark.parametrize("tile,splits", [(5, 4), (6, 2), (8, 1)])
+@pytest.mark.parametrize("tile,splits", [(5, 4), (6, 2), (8, 1), (19, 1), (20, 2), (21, 1)])
 def test_glds_fc1_forward_epilogue(tile, splits):
     """fc1 forward: H = dropout(relu(P2 . W1^T + b)) at B=1024, K=3136."""
     B_, K1, FC = 1024, 3136, 1024
@@ -73,7 +73,7 @@ def test_glds_fc1_dgrad_and_wgrad():
     assert err < 1e-2, err
     gw = torch.full((FC, K1), 7.0, device="cuda")
     gb = torch.full((FC,), 7.0, device="cuda")
-    for tile, splits in ((8, 1), (8, 2), (6, 1), (12, 1)):
+    for tile, splits in ((8, 1), (8, 2), (6, 1), (12, 1), (19, 1), (20, 1)):
         if not ops.glds_ok(dz, p2, FC, K1 + 1, B_, tile, FC, K1, b_ones_row=K1):
             continue
         ops.gemm(dz, p2, gw, M=FC, N=K1 + 1, K=B_, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ, ldb=K1, ldc=K1,
