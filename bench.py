@@ -67,6 +67,9 @@ def parse_args(argv=None):
                          "kernel (timed at setup); rccl / ipc: force one; all three run on a side stream with the "
                          "whole step captured in one hipGraph.  pg: torch.distributed ProcessGroupNCCL, eager steps")
     ap.add_argument("--hogwild", action="store_true", help="--mode ps: lock-free concurrent applies")
+    ap.add_argument("--ps_overlap", choices=["auto", "on", "off"], default="auto",
+                    help="--mode ps: apply pushed buckets during backward (auto: only on a ps GPU other "
+                         "than the worker's)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
     return ap.parse_args(argv)
@@ -437,7 +440,7 @@ def bench_ps(args):
     else:
         wait_for_init(client, poll_s=0.05)
     link = ps_native.NativePSLink(server, tr.P, placement, shard_specs, placement[model.gs_name], dev,
-                                  buckets=tr.buckets)
+                                  buckets=tr.buckets, overlap={"auto": None, "on": True, "off": False}[args.ps_overlap])
     tr.allreduce = link           # bucket pushes fork off backward (MnistCnnTrainer.forward_backward)
     link.pull()
 

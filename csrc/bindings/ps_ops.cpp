@@ -324,6 +324,12 @@ struct WorkerCh {
   uint64_t bkt_done[dtfe::PS_MAX_BUCKETS] = {};
   uint64_t range_seq = 0;
   std::vector<std::pair<long, long>> ranges;
+  // fused replies: per optimizer group, this worker's copy of the group's plan segments with the
+  // second destinations (w16b / wt16b / pb) aimed at its reply buffer - the apply writes the
+  // reply itself, no snapshot copy; sub-plans by shard range.  Empty: snapshot copies instead.
+  bool fused = false;
+  std::vector<std::vector<dtfe::OptSeg>> rsegs;
+  std::vector<std::map<std::pair<long, long>, SubPlan>> rsub;
 };
 struct Service {
   Shm* shm = nullptr;
@@ -450,25 +456,87 @@ void launch_apply(Service* s, WorkerCh& c, hipStream_t st, const void* grad, boo
   }
 }
 
-// the sub-plan of group g over shard range [lo, hi) (every variable lies wholly inside or outside)
-const SubPlan& sub_plan(Service* s, Group& g, long lo, long hi) {
+// the sub-plan of group g over shard range [lo, hi) (every variable lies wholly inside or outside),
+// over segment table `segs` (the group's own, or a worker's reply-aimed copy), cached in `cache`
+const SubPlan& sub_plan_of(Service* s, const Group& g, const std::vector<dtfe::OptSeg>& segs,
+                           std::map<std::pair<long, long>, SubPlan>& cache, long lo, long hi) {
   auto key = std::make_pair(lo, hi);
-  auto it = g.sub.find(key);
-  if (it != g.sub.end()) return it->second;
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
   std::vector<dtfe::OptWork> wk;
   for (const auto& w : g.hwork) {
-    const long off = g.hsegs[(size_t)w.seg].off;
+    const long off = segs[(size_t)w.seg].off;
     if (off >= lo && off < hi) wk.push_back(w);
   }
   SubPlan p;
   p.nwork = (int)wk.size();
-  const size_t bs = g.hsegs.size() * sizeof(dtfe::OptSeg), off = (bs + 255) / 256 * 256;
+  const size_t bs = segs.size() * sizeof(dtfe::OptSeg), off = (bs + 255) / 256 * 256;
   std::vector<uint8_t> host(off + wk.size() * sizeof(dtfe::OptWork) + 16, 0);
-  if (bs) std::memcpy(host.data(), g.hsegs.data(), bs);
+  if (bs) std::memcpy(host.data(), segs.data(), bs);
   if (!wk.empty()) std::memcpy(host.data() + off, wk.data(), wk.size() * sizeof(dtfe::OptWork));
   p.blob = at::empty({(int64_t)host.size()}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, s->device));
   hchk(hipMemcpy(p.blob.data_ptr(), host.data(), host.size(), hipMemcpyHostToDevice), "apply sub-plan H2D");
-  return g.sub.emplace(key, std::move(p)).first->second;
+  return cache.emplace(key, std::move(p)).first->second;
+}
+const SubPlan& sub_plan(Service* s, Group& g, long lo, long hi) { return sub_plan_of(s, g, g.hsegs, g.sub, lo, hi); }
+
+// worker c's apply args of group gi over [lo, hi): its mailbox as the gradient, the reply-aimed
+// segment table when the channel is fused (nwork == 0: nothing of the group in the range)
+dtfe::OptArgs range_args(Service* s, WorkerCh& c, size_t gi, long lo, long hi) {
+  Group& g = s->groups[gi];
+  const SubPlan& p = c.fused ? sub_plan_of(s, g, c.rsegs[gi], c.rsub[gi], lo, hi) : sub_plan(s, g, lo, hi);
+  dtfe::OptArgs a = g.args;
+  if (g.g16) {
+    a.g = nullptr;
+    a.g16 = reinterpret_cast<const dtfe::bf16*>(c.mailbox);
+  } else {
+    a.g = reinterpret_cast<const float*>(c.mailbox);
+    a.g16 = nullptr;
+  }
+  const size_t bs = g.hsegs.size() * sizeof(dtfe::OptSeg), off = (bs + 255) / 256 * 256;
+  a.segs = reinterpret_cast<const dtfe::OptSeg*>(p.blob.data_ptr());
+  a.work = reinterpret_cast<const dtfe::OptWork*>((const char*)p.blob.data_ptr() + off);
+  a.nwork = p.nwork;
+  a.gscale = 1.f;
+  a.skip_advance = 1;
+  a.done_counter = c.done[gi];
+  return a;
+}
+
+// fused replies for worker c: every reply-buffer segment of its snapshot plan must be the second
+// destination of some apply segment (bf16 natural / transposed copy, or an fp32 variable);
+// otherwise the channel keeps the snapshot copies
+void build_fused(Service* s, WorkerCh& c) {
+  c.fused = false;
+  c.rsegs.clear();
+  c.rsub.clear();
+  if (c.snap_hsegs.empty() || c.snap_off.empty()) return;
+  std::vector<char> used(c.snap_hsegs.size(), 0);
+  std::vector<std::vector<dtfe::OptSeg>> rs;
+  for (const Group& g : s->groups) {
+    std::vector<dtfe::OptSeg> segs = g.hsegs;
+    for (auto& sg : segs) {
+      for (size_t i = 0; i < c.snap_hsegs.size(); ++i) {
+        const dtfe::PsSeg& ps = c.snap_hsegs[i];
+        if (ps.mode == 2 && sg.w16 && ps.src == sg.w16) {
+          sg.w16b = reinterpret_cast<dtfe::bf16*>(ps.dst);
+          used[i] = 1;
+        } else if (ps.mode == 2 && sg.wt16 && ps.src == sg.wt16) {
+          sg.wt16b = reinterpret_cast<dtfe::bf16*>(ps.dst);
+          used[i] = 1;
+        } else if (ps.mode == 0 && ps.src == g.args.p + sg.off) {
+          sg.pb = reinterpret_cast<float*>(ps.dst);
+          used[i] = 1;
+        }
+      }
+    }
+    rs.push_back(std::move(segs));
+  }
+  for (char u : used)
+    if (!u) return;
+  c.rsegs = std::move(rs);
+  c.rsub.resize(s->groups.size());
+  c.fused = true;
 }
 
 // apply the mailbox over shard range [lo, hi) with every group, leaving the step scalars alone
@@ -524,18 +592,78 @@ void snap_range(Service* s, WorkerCh& c, hipStream_t st, long lo, long hi) {
     dtfe::launch_ps_copy(plan_segs(p.blob), plan_work(p.blob, (int64_t)c.snap_hsegs.size()), p.nwork, st);
 }
 
-// a bucket's apply (and, with per-range snapshots, its reply copy)
+// a bucket's apply (and, with per-range snapshots, its reply copy; a fused channel's apply writes
+// the reply buffer itself)
 void apply_bucket(Service* s, WorkerCh& c, hipStream_t st, long lo, long hi) {
+  if (c.fused) {
+    for (size_t gi = 0; gi < s->groups.size(); ++gi) {
+      dtfe::OptArgs a = range_args(s, c, gi, lo, hi);
+      if (a.nwork > 0) dtfe::launch_apply_gradients(a, st);
+    }
+    return;
+  }
   launch_apply_range(s, c, st, lo, hi);
   if (!c.snap_off.empty()) snap_range(s, c, st, lo, hi);
+}
+
+// fused channel, at the request: apply the ranges not applied yet with each group's step scalars
+// advanced by its last launch and the reply words published by the last launch of all (or by one
+// small advance + reply kernel when some group has nothing left to apply)
+void finish_fused(Service* s, WorkerCh& c, int w, hipStream_t st, uint64_t seq, uint64_t ver,
+                  const std::vector<std::pair<long, long>>& todo) {
+  struct L {
+    size_t gi;
+    dtfe::OptArgs a;
+  };
+  std::vector<L> ls;
+  for (const auto& r : todo)
+    for (size_t gi = 0; gi < s->groups.size(); ++gi) {
+      dtfe::OptArgs a = range_args(s, c, gi, r.first, r.second);
+      if (a.nwork > 0) ls.push_back({gi, a});
+    }
+  std::vector<int> last(s->groups.size(), -1);
+  for (size_t i = 0; i < ls.size(); ++i) last[ls[i].gi] = (int)i;
+  bool every = true;
+  for (int l : last) every = every && l >= 0;
+  auto set_reply = [&](dtfe::OptArgs& a) {
+    a.rep_slot = slot_dev(s->shm, w);
+    a.rep_gs = s->gs;
+    a.rep_seq = seq;
+    a.rep_ver = ver;
+    a.rep_stale = 0;
+  };
+  for (size_t i = 0; i < ls.size(); ++i) {
+    dtfe::OptArgs a = ls[i].a;
+    a.skip_advance = last[ls[i].gi] == (int)i ? 0 : 1;
+    if (every && i + 1 == ls.size()) set_reply(a);
+    dtfe::launch_apply_gradients(a, st);
+  }
+  if (every) return;
+  std::vector<dtfe::OptArgs> adv;
+  for (size_t gi = 0; gi < s->groups.size(); ++gi)
+    if (last[gi] < 0) adv.push_back(s->groups[gi].args);
+  set_reply(adv.back());
+  dtfe::launch_opt_advance_reply(adv.data(), (int)adv.size(), st);
 }
 
 // async push with buckets: apply every bucket range of request `seq` not applied yet (the gaps
 // between the ranges already applied - all of the shard when the worker sent no bucket), then
 // advance each group's step scalars once.  Returns true when the reply buffer is already current.
-bool finish_bucketed(Service* s, WorkerCh& c, hipStream_t st, uint64_t seq) {
+bool finish_bucketed(Service* s, WorkerCh& c, int w, hipStream_t st, uint64_t seq) {
   std::vector<std::pair<long, long>> done = c.range_seq == seq ? c.ranges : std::vector<std::pair<long, long>>{};
   std::sort(done.begin(), done.end());
+  if (c.fused) {
+    std::vector<std::pair<long, long>> todo;
+    long at = 0;
+    for (const auto& r : done) {
+      if (r.first > at) todo.emplace_back(at, r.first);
+      at = std::max(at, r.second);
+    }
+    if (at < s->total) todo.emplace_back(at, s->total);
+    finish_fused(s, c, w, st, seq, s->version + 1, todo);
+    c.ranges.clear();
+    return true;
+  }
   long at = 0;
   for (const auto& r : done) {
     if (r.first > at) apply_bucket(s, c, st, at, r.first);
@@ -654,7 +782,13 @@ void run(Service* s) {
         bool snapped = false;
         if (s->total > 0) {
           scan_buckets(seq - 1);  // bucket words published just before this request
-          snapped = finish_bucketed(s, c, st, seq);
+          if (c.fused) {       // the apply publishes the reply itself
+            finish_bucketed(s, c, w, st, seq);
+            s->version++;
+            s->n_apply++;
+            continue;
+          }
+          snapped = finish_bucketed(s, c, w, st, seq);
         } else {
           launch_apply(s, c, st, c.mailbox, false, 1.f);
         }
@@ -717,6 +851,9 @@ void ps_service_start(int64_t h) {
   TORCH_CHECK(!s->groups.empty(), "dtfe ps: service has no optimizer group");
   for (auto& c : s->ch) TORCH_CHECK(c.mailbox != nullptr, "dtfe ps: every worker channel needs a mailbox");
   TORCH_CHECK(!s->sync || s->acc, "dtfe ps: sync mode needs an accumulator");
+  // async channels with per-variable reply segments: replies written by the applies themselves
+  if (!s->sync && (int)s->groups.size() <= dtfe::OPT_GROUP_MAX)
+    for (auto& c : s->ch) build_fused(s, c);
   s->th = std::thread(run, s);
 }
 

@@ -195,11 +195,14 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
     TORCH_CHECK(bnb_x->numel() == dx.numel() && bnb_x->scalar_type() == at::kBFloat16, "conv_dgrad: bnb_x shape/dtype");
     TORCH_CHECK(bnb_stats->numel() >= 2 * C && bnb_stats->scalar_type() == at::kFloat, "conv_dgrad: bnb_stats [2][C] fp32");
     TORCH_CHECK(bnb_mean->numel() >= C && bnb_invstd->numel() >= C && bnb_gamma->numel() >= C, "conv_dgrad: BN params");
+    const bool bits = bnb_y.has_value() && bnb_y->defined() && bnb_y->scalar_type() == at::kByte;
     if (bnb_y.has_value() && bnb_y->defined())
-      TORCH_CHECK(bnb_y->numel() == dx.numel() && bnb_y->scalar_type() == at::kBFloat16, "conv_dgrad: bnb_y shape/dtype");
+      TORCH_CHECK(bits ? bnb_y->numel() == dx.numel() / 8 : (bnb_y->numel() == dx.numel() && bnb_y->scalar_type() == at::kBFloat16),
+                  "conv_dgrad: bnb_y shape/dtype (bf16 output, or its uint8 [R][C/8] ReLU bit mask)");
     if (bnb_beta.has_value() && bnb_beta->defined()) TORCH_CHECK(bnb_beta->numel() >= C, "conv_dgrad: bnb_beta");
     a.bnb_x = reinterpret_cast<const dtfe::bf16*>(bnb_x->data_ptr());
-    a.bnb_y = ptr_or_null<dtfe::bf16>(bnb_y);
+    if (bits) a.bnb_ymask = bnb_y->data_ptr<uint8_t>();
+    else a.bnb_y = ptr_or_null<dtfe::bf16>(bnb_y);
     a.bnb_mean = bnb_mean->data_ptr<float>();
     a.bnb_invstd = bnb_invstd->data_ptr<float>();
     a.bnb_gamma = bnb_gamma->data_ptr<float>();
@@ -313,13 +316,14 @@ void conv1_gather_fwd(const Tensor& images, const Tensor& labels_src, int64_t se
   TORCH_CHECK(dtfe::launch_conv1_copies_fwd(a, cur_stream()), "conv1_gather_fwd: needs B >= 256");
 }
 
-void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
+std::vector<int64_t> imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
-              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks) {
+              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks, bool defer_reduce) {
   check_cuda(src, "src");
   dtfe::ImgWgradArgs a{};
   a.max_blocks = (int)max_blocks;
+  a.defer_reduce = defer_reduce ? 1 : 0;
   if (ws.has_value() && ws->defined()) {
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= dtfe::imgwgrad_ws_floats((int)N, (int)(KH * KW * CS)),
                 "imgwgrad: workspace too small (ops.wgrad_ws_floats)");
@@ -336,7 +340,12 @@ void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tens
   a.dw = dw.data_ptr<float>();
   a.db = ptr_or_null<float>(db);
   a.scale = (float)scale;
+  dtfe::imgwgrad_last_layout() = dtfe::WgPartLayout();
   dtfe::launch_imgwgrad(a, cur_stream());
+  // defer_reduce: the partials' layout (empty when this launch kept none: no workspace / atomics)
+  const dtfe::WgPartLayout L = dtfe::imgwgrad_last_layout();
+  if (!defer_reduce || L.layout < 0) return {};
+  return {L.layout, L.nblk, L.plen, L.MT, L.CTW, L.KC, L.N, L.nw};
 }
 
 void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t H,
@@ -462,11 +471,34 @@ Tensor opt_pack(const Tensor& segs, const Tensor& work, const Tensor& device_lik
   return host.to(device_like.device());
 }
 
+// ints: int64 [n, 11] = (ws_ptr, nblk, plen, layout, MT, CTW, KC, N, nw, wseg, bseg); scales: float64 [n]
+Tensor opt_pack_parts(const Tensor& ints, const Tensor& scales, const Tensor& device_like) {
+  TORCH_CHECK(ints.device().is_cpu() && ints.scalar_type() == at::kLong && ints.dim() == 2 && ints.size(1) == 11 &&
+                  scales.device().is_cpu() && scales.numel() == ints.size(0),
+              "opt_pack_parts: CPU int64 [n, 11] + float64 [n]");
+  auto I = ints.contiguous();
+  auto S = scales.to(at::kDouble).contiguous();
+  const int64_t n = I.size(0);
+  std::vector<dtfe::OptPart> v((size_t)n);
+  const int64_t* q = I.data_ptr<int64_t>();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t* r = q + i * 11;
+    v[i].ws = reinterpret_cast<const float*>(r[0]);
+    v[i].nblk = (int)r[1]; v[i].plen = (int)r[2]; v[i].layout = (int)r[3]; v[i].MT = (int)r[4]; v[i].CTW = (int)r[5];
+    v[i].KC = (int)r[6]; v[i].N = (int)r[7]; v[i].nw = (int)r[8]; v[i].wseg = (int)r[9]; v[i].bseg = (int)r[10];
+    v[i].scale = (float)S.data_ptr<double>()[i];
+    TORCH_CHECK(v[i].layout == 0 || v[i].layout == 1, "opt_pack_parts: layout 0 / 1");
+  }
+  Tensor host = at::empty({(int64_t)(n * sizeof(dtfe::OptPart))}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(host.data_ptr(), v.data(), n * sizeof(dtfe::OptPart));
+  return host.to(device_like.device());
+}
+
 void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, const optional<Tensor>& g16,
                      double gscale, const optional<Tensor>& s1, const optional<Tensor>& s2, double lr, double beta1,
                      double beta2, double eps, double momentum, double rho, const optional<Tensor>& beta_pow,
                      const optional<Tensor>& global_step, int64_t gs_inc, const Tensor& done, const Tensor& blob,
-                     int64_t nseg, int64_t nwork, int64_t group) {
+                     int64_t nseg, int64_t nwork, int64_t group, const optional<Tensor>& parts) {
   check_cuda(p, "p");
   // group: 0 = launch now; 1 = queue these args; 2 = queue and launch every queued optimizer in
   // ONE grouped launch (same kind, disjoint var lists: e.g. the GAN's two Adams)
@@ -490,6 +522,10 @@ void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, c
   a.segs = reinterpret_cast<const dtfe::OptSeg*>(blob.data_ptr());
   a.work = reinterpret_cast<const dtfe::OptWork*>((const char*)blob.data_ptr() + off_w);
   a.nwork = (int)nwork;
+  if (parts.has_value() && parts->defined()) {
+    TORCH_CHECK(parts->is_cuda() && a.g, "apply_gradients: partial sources need the fp32 gradient buffer");
+    a.parts = reinterpret_cast<const dtfe::OptPart*>(parts->data_ptr());
+  }
   if (kind == dtfe::OPT_ADAM) TORCH_CHECK(a.beta_pow && a.s1 && a.s2, "adam needs slots and beta powers");
   if (kind == dtfe::OPT_RMSPROP) TORCH_CHECK(a.s1 && a.s2, "rmsprop needs slots");
   if (kind == dtfe::OPT_MOMENTUM) TORCH_CHECK(a.s1, "momentum needs a slot");
@@ -765,8 +801,14 @@ void bn_stats(const Tensor& x, const Tensor& stats) {
 void bn_apply(const Tensor& x, const Tensor& stats, const Tensor& gamma, const Tensor& beta,
               const optional<Tensor>& mean, const optional<Tensor>& invstd, const optional<Tensor>& moving_mean,
               const optional<Tensor>& moving_var, double eps, double momentum, int64_t act,
-              const optional<Tensor>& res, int64_t rstride, int64_t OH, int64_t OW, const Tensor& out) {
+              const optional<Tensor>& res, int64_t rstride, int64_t OH, int64_t OW, const Tensor& out,
+              const optional<Tensor>& mask_out) {
   dtfe::BnArgs a = bn_common(x, stats, act);
+  if (mask_out.has_value() && mask_out->defined()) {
+    TORCH_CHECK(mask_out->is_cuda() && mask_out->scalar_type() == at::kByte && mask_out->numel() == x.numel() / 8 &&
+                    act == 1, "bn_apply: mask_out is a uint8 [R][C/8] ReLU bit mask");
+    a.mask_out = mask_out->data_ptr<uint8_t>();
+  }
   a.gamma = gamma.data_ptr<float>();
   a.beta = beta.data_ptr<float>();
   a.mean = ptr_or_null<float>(mean);
@@ -814,15 +856,25 @@ void bn_infer(const Tensor& x, const Tensor& gamma, const Tensor& beta, const Te
   dtfe::launch_bn_apply(a, cur_stream());
 }
 
+// the backward's ReLU-mask source: the bf16 forward output, or its uint8 [R][C/8] bit mask (ReLU only)
+void set_bwd_y(dtfe::BnArgs& a, const optional<Tensor>& y, const Tensor& x) {
+  if (y.has_value() && y->defined() && y->scalar_type() == at::kByte) {
+    TORCH_CHECK(y->is_cuda() && y->numel() == x.numel() / 8 && a.act == 1, "bn_bwd: bit mask is uint8 [R][C/8], ReLU");
+    a.ymask = y->data_ptr<uint8_t>();
+    return;
+  }
+  a.y = ptr_or_null<dtfe::bf16>(y);
+}
+
 void bn_bwd_stats(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                   const Tensor& invstd, const Tensor& stats, int64_t act, const optional<Tensor>& gamma,
                   const optional<Tensor>& beta) {
   dtfe::BnArgs a = bn_common(x, stats, act);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
-  a.y = ptr_or_null<dtfe::bf16>(y);
+  set_bwd_y(a, y, x);
   a.gamma = ptr_or_null<float>(gamma);
   a.beta = ptr_or_null<float>(beta);
-  TORCH_CHECK(act == 0 || a.y || (act == 1 && a.gamma && a.beta),
+  TORCH_CHECK(act == 0 || a.y || a.ymask || (act == 1 && a.gamma && a.beta),
               "bn_bwd: the activation gradient needs the forward output (or, for ReLU, gamma and beta)");
   a.mean = mean.data_ptr<float>();
   a.invstd = invstd.data_ptr<float>();
@@ -835,9 +887,9 @@ void bn_bwd_apply(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, 
                   const optional<Tensor>& beta) {
   dtfe::BnArgs a = bn_common(x, stats, act);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
-  a.y = ptr_or_null<dtfe::bf16>(y);
+  set_bwd_y(a, y, x);
   a.beta = ptr_or_null<float>(beta);
-  TORCH_CHECK(act == 0 || a.y || (act == 1 && a.beta),
+  TORCH_CHECK(act == 0 || a.y || a.ymask || (act == 1 && a.beta),
               "bn_bwd: the activation gradient needs the forward output (or, for ReLU, beta)");
   a.mean = mean.data_ptr<float>();
   a.invstd = invstd.data_ptr<float>();
@@ -895,7 +947,7 @@ TORCH_LIBRARY(dtfe, m) {
         " Tensor? res, int rstride, int OH, int OW, Tensor(a!) out) -> ()");
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
-        " int rstride, int OH, int OW, Tensor(e!) out) -> ()");
+        " int rstride, int OH, int OW, Tensor(e!) out, Tensor(f!)? mask_out=None) -> ()");
   m.def("bn_bwd_stats(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) stats, int act,"
         " Tensor? gamma=None, Tensor? beta=None) -> ()");
   m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor stats,"
@@ -931,7 +983,7 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"
-      " int max_blocks=0) -> ()");
+      " int max_blocks=0, bool defer_reduce=False) -> int[]");
   m.def("conv1_wgrad_pooled(Tensor x, Tensor dp, Tensor argmax, Tensor(a!) dw, Tensor(b!)? db, float scale) -> ()");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
@@ -946,7 +998,9 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
       " float lr, float beta1, float beta2, float eps, float momentum, float rho, Tensor(d!)? beta_pow,"
-      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0) -> ()");
+      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0,"
+      " Tensor? parts=None) -> ()");
+  m.def("opt_pack_parts(Tensor ints, Tensor scales, Tensor device_like) -> Tensor");
   m.def("wgrad_tallk(Tensor A, int lda, Tensor B, int ldb, int M, int N, int K, Tensor(a!) out, int ldc,"
         " Tensor(b!)? bias, Tensor(c!) ws, int splits, float scale) -> ()");
   m.def("seq_stage(Tensor x, Tensor(a!) xh, int T, int I, Tensor ysrc, Tensor(b!) ydst, Tensor(c!)[] zero) -> ()");
@@ -1013,4 +1067,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }
 
-TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) { m.impl("opt_pack", &opt_pack); }
+TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) {
+  m.impl("opt_pack", &opt_pack);
+  m.impl("opt_pack_parts", &opt_pack_parts);
+}

@@ -55,6 +55,7 @@ struct ConvDgradArgs {
   // from the implicit-GEMM epilogue where it can, else a separate statistics pass
   const bf16* bnb_x; const bf16* bnb_y; const float* bnb_mean; const float* bnb_invstd;
   const float* bnb_gamma; const float* bnb_beta; float* bnb_stats; int bnb_act;
+  const uint8_t* bnb_ymask;   // 1-bit ReLU mask instead of bnb_y (norm.h BnArgs::ymask)
 };
 struct ConvWgradArgs {
   ConvGeom g;

@@ -412,7 +412,7 @@ void launch_dgrad_bn_bwd_stats(const ConvDgradArgs& a, hipStream_t s) {
   BnArgs b{};
   b.R = (long)a.g.B * a.g.H * a.g.W;
   b.C = a.g.C;
-  b.x = a.bnb_x; b.y = a.bnb_y; b.dy = a.dx;
+  b.x = a.bnb_x; b.y = a.bnb_y; b.dy = a.dx; b.ymask = a.bnb_ymask;
   b.stats = a.bnb_stats;
   b.gamma = a.bnb_gamma; b.beta = a.bnb_beta;
   b.mean = const_cast<float*>(a.bnb_mean); b.invstd = const_cast<float*>(a.bnb_invstd);

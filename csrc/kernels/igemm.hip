@@ -1067,7 +1067,7 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
   a.N = g.C; a.Ktot = g.KH * g.KW * g.Cout;
   a.istr = 1; a.OHf = g.H; a.OWf = g.W; a.ostr = g.stride;
   a.accum = d.accumulate;
-  if (d.bnb_stats) {
+  if (d.bnb_stats && !d.bnb_ymask) {  // (a bit-mask source: the separate statistics pass)
     a.bb_x = d.bnb_x; a.bb_y = d.bnb_y; a.bb_mean = d.bnb_mean; a.bb_invstd = d.bnb_invstd;
     a.bb_gamma = d.bnb_gamma; a.bb_beta = d.bnb_beta; a.bb_act = d.bnb_act;
   }
@@ -1103,7 +1103,7 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
     if (n == 0) return true;
     a.nphase = n;
   }
-  const bool fused = run_igemm(a, s, d.bnb_stats);
+  const bool fused = run_igemm(a, s, d.bnb_ymask ? nullptr : d.bnb_stats);
   if (d.bnb_stats && !fused) launch_dgrad_bn_bwd_stats(d, s);
   return true;
 }

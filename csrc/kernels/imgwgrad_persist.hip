@@ -332,13 +332,13 @@ __global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict_
     if (col < KC) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (n0 + j < N) dw[(long)(n0 + j) * KC + col] += scale * t[j];
+        if (n0 + j < N) dw[(long)(n0 + j) * KC + col] = __builtin_fmaf(scale, t[j], dw[(long)(n0 + j) * KC + col]);
     }
   } else if (db) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = (v - ntile) * 4 + j;
-      if (n < N) db[n] += scale * t[j];
+      if (n < N) db[n] = __builtin_fmaf(scale, t[j], db[n]);
     }
   }
 }
@@ -372,8 +372,8 @@ __global__ __launch_bounds__(256) void partials_reduce_kernel(const float* __res
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = i + e;
-      if (k < nw) dw[k] += scale * t[e];
-      else if (db) db[k - nw] += scale * t[e];
+      if (k < nw) dw[k] = __builtin_fmaf(scale, t[e], dw[k]);
+      else if (db) db[k - nw] = __builtin_fmaf(scale, t[e], db[k - nw]);
     }
   }
 }
@@ -422,8 +422,13 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, ad, G);
     if (a.ws) {
       const int plen = wp_part_len(MT, CTW, a.N), KC = a.KH * a.KW * a.CS;
-      hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW, KC,
-                         a.N, a.dw, a.db, a.scale);
+      if (a.defer_reduce) {
+        WgPartLayout& L = imgwgrad_last_layout();
+        L.layout = 0; L.nblk = grid; L.plen = plen; L.MT = MT; L.CTW = CTW; L.KC = KC; L.N = a.N; L.nw = a.N * KC;
+      } else {
+        hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW, KC,
+                           a.N, a.dw, a.db, a.scale);
+      }
     }
     return true;
   };
@@ -444,6 +449,11 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
 }
 
 }  // namespace
+
+WgPartLayout& imgwgrad_last_layout() {
+  thread_local WgPartLayout L;
+  return L;
+}
 
 long imgwgrad_ws_floats(int N, int KC) {
   const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 8;  // the wp_launch instances below

@@ -33,6 +33,11 @@ struct BnArgs {
   float* dgamma; float* dbeta;   // backward parameter gradients (+=)
   int infer;                     // bn_apply only: normalise with the moving averages (inference mode;
                                  // stats unused, nothing is updated or saved)
+  // 1-bit ReLU mask [R][C/8] bytes (bit e of byte (r, c/8) = out[r][c] > 0, c = 8 * (c/8) + e):
+  // bn_apply writes it (mask_out) beside a ReLU output that had a residual added; the backward
+  // kernels read it (ymask) instead of that bf16 output - 1 byte per 8 channels instead of 16
+  uint8_t* mask_out;
+  const uint8_t* ymask;
 };
 
 void launch_bn_stats(const BnArgs& a, hipStream_t s);

@@ -179,7 +179,18 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e], ACTC >= 0 ? ACTC : a.act);
-      if (r < a.R) *reinterpret_cast<u32x4_t*>(a.out + r * a.C + S.chunk * 8) = pack8(f);
+      if (r < a.R) {
+        const u32x4_t o = pack8(f);
+        *reinterpret_cast<u32x4_t*>(a.out + r * a.C + S.chunk * 8) = o;
+        if (a.mask_out) {  // of the stored bf16 values: the backward's y > 0, bit for bit
+          uint32_t bits = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            bits |= ((o[e] & 0x7fffu) != 0 && !(o[e] & 0x8000u) ? 1u : 0u) << (2 * e) |
+                    ((o[e] & 0x7fff0000u) != 0 && !(o[e] & 0x80000000u) ? 1u : 0u) << (2 * e + 1);
+          a.mask_out[r * (a.C / 8) + S.chunk] = (uint8_t)bits;
+        }
+      }
     }
   }
 }
@@ -191,10 +202,12 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
 //            cheaper (y == nullptr)
 //   MM_YRELU ReLU mask from the stored output y (a residual was added before the ReLU)
 //   MM_YACT  act'(y) of the stored output for the runtime a.act (sigmoid / tanh)
-enum { MM_NONE = 0, MM_X = 1, MM_YRELU = 2, MM_YACT = 3 };
+//   MM_BITS  ReLU mask from the forward's 1-bit mask (ymask)
+enum { MM_NONE = 0, MM_X = 1, MM_YRELU = 2, MM_YACT = 3, MM_BITS = 4 };
 
 __host__ __device__ inline int mask_mode(const BnArgs& a) {
   if (a.act == ACT_NONE) return MM_NONE;
+  if (a.ymask && a.act == ACT_RELU) return MM_BITS;
   if (a.y == nullptr && a.act == ACT_RELU) return MM_X;
   return a.act == ACT_RELU ? MM_YRELU : MM_YACT;
 }
@@ -218,7 +231,10 @@ template <int MM>
 __device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, const u32x4_t dyv, const u32x4_t yv,
                                             const float (&x)[8], float (&g)[8]) {
   unpack8(dyv, g);
-  if constexpr (MM == MM_X) {
+  if constexpr (MM == MM_BITS) {  // (yv[0] carries the mask byte)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (yv[0] >> e) & 1u ? g[e] : 0.f;
+  } else if constexpr (MM == MM_X) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = (x[e] * M.scale[e] + M.shift[e]) > 0.f ? g[e] : 0.f;
   } else if constexpr (MM == MM_YRELU) {
@@ -256,6 +272,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
       dv[u] = ld16(a.dy + off);
       xv[u] = ld16(a.x + off);
       if (need_y) yv[u] = ld16(a.y + off);
+      if (MM == MM_BITS) yv[u][0] = a.ymask[off >> 3];
     }
 #pragma unroll
     for (int u = 0; u < U_STATS; ++u) {
@@ -306,6 +323,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
       dv[u] = ld16(a.dy + off);
       xv[u] = ld16(a.x + off);
       if (need_y) yv[u] = ld16(a.y + off);
+      if (MM == MM_BITS) yv[u][0] = a.ymask[off >> 3];
     }
 #pragma unroll
     for (int u = 0; u < U_APPLY; ++u) {
@@ -560,6 +578,7 @@ void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s) {
     case MM_NONE: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_NONE>, g, b, lds, s, a); break;
     case MM_X: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_X>, g, b, lds, s, a); break;
     case MM_YRELU: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_YRELU>, g, b, lds, s, a); break;
+    case MM_BITS: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_BITS>, g, b, lds, s, a); break;
     default: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_YACT>, g, b, lds, s, a); break;
   }
 }
@@ -571,6 +590,7 @@ void launch_bn_bwd_apply(const BnArgs& a, hipStream_t s) {
     case MM_NONE: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_NONE>, g, b, 0, s, a); break;
     case MM_X: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_X>, g, b, 0, s, a); break;
     case MM_YRELU: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_YRELU>, g, b, 0, s, a); break;
+    case MM_BITS: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_BITS>, g, b, 0, s, a); break;
     default: hipLaunchKernelGGL(bn_bwd_apply_kernel<MM_YACT>, g, b, 0, s, a); break;
   }
 }

@@ -15,13 +15,33 @@ struct OptSeg {
   int R, T, C;
   bf16* w16;   // natural-layout bf16 working copy (nullable)
   bf16* wt16;  // transposed bf16 working copy (nullable)
+  // second destinations of the updated values (nullable): a ps writes the requesting worker's
+  // reply buffer from the apply itself - bf16 natural / transposed copies, or the fp32 value of
+  // a variable without bf16 copies - instead of snapshotting its working copies afterwards
+  bf16* w16b;
+  bf16* wt16b;
+  float* pb;
 };
 
 // Work item: kind 0 = flat range [start, start+count) of segment seg;
-// kind 1 = 64x64 tile (r0, c0) of tap t of segment seg (transpose path).
+// kind 1 = 64x64 tile (r0, c0) of tap t of segment seg (transpose path);
+// kind 2 = 16 f32x4 (start = first) of partial source t (OptPart): the gradient of those
+// elements is first summed over the source's unreduced weight-gradient slabs - the fold of
+// wp_reduce_kernel / partials_reduce_kernel into the optimizer launch.
 struct OptWork {
   int kind, seg, t, r0, c0;
   long start, count;
+};
+
+// Unreduced per-workgroup weight-gradient partials (imgconv.h WgPartLayout): nblk slabs of plen
+// floats at ws; layout 0 = the persistent weight-gradient kernel's register layout (MT x CTW tiles,
+// bias tail), 1 = plain [nw weights][N biases].  The reduced value is added into the gradient
+// buffer g (dW += scale * sum, exactly as the reduce kernels do) and then applied; wseg / bseg:
+// the OptSeg of the weight [N][KC] and bias [N] variables (bseg -1: none).
+struct OptPart {
+  const float* ws;
+  int nblk, plen, layout, MT, CTW, KC, N, nw, wseg, bseg;
+  float scale;
 };
 
 struct OptArgs {
@@ -36,11 +56,22 @@ struct OptArgs {
   const OptSeg* segs; const OptWork* work; int nwork;
   int skip_advance;         // 1: leave the beta powers / global step alone (a partial apply: the
                             // ps applies a push bucket by bucket, then launch_opt_advance once)
+  // ps reply folded into the launch (rep_slot != nullptr): after every workgroup's stores have
+  // completed, the last one publishes (global step, version, stale, seq) into the worker's slot
+  // of the shared page (ps_link.h), exactly as ps_reply_kernel would after this launch
+  uint64_t* rep_slot;
+  const int32_t* rep_gs;
+  uint64_t rep_seq, rep_ver;
+  int rep_stale;
+  const OptPart* parts;     // kind-2 work items' sources (fp32 gradient path only)
 };
 
 void launch_apply_gradients(const OptArgs& a, hipStream_t s);
 // the non-slot scalars of one optimizer step: beta powers (Adam) and global_step += gs_inc
 void launch_opt_advance(const OptArgs& a, hipStream_t s);
+// the step scalars of n (<= OPT_GROUP_MAX) optimizers and then, if a[n-1].rep_slot is set, its
+// reply words - one launch (a ps request whose gradient was all applied bucket by bucket)
+void launch_opt_advance_reply(const OptArgs* a, int n, hipStream_t s);
 
 // TF1 Adam step of one element: m = b1 m + (1-b1) g; v2 = b2 v2 + (1-b2) g^2; p -= lr_t m / (sqrt(v2) + eps).
 // No multiply-add contraction: the rounding must not depend on a kernel's instruction selection.

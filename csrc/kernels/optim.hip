@@ -56,8 +56,18 @@ __device__ __forceinline__ float load_grad(const OptArgs& a, long i) {
   return (G16 ? bf2f(a.g16[i]) : a.g[i]) * a.gscale;
 }
 
+// the updated values' extra destinations: bf16 copies (w16, the ps reply's w16b) and the fp32 copy pb
+__device__ __forceinline__ void store_copies(const f32x4_t& p, bf16* w16, bf16* w16b, float* pb) {
+  if (w16 || w16b) {
+    const u32x2_t q = {pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3])};
+    if (w16) *reinterpret_cast<u32x2_t*>(w16) = q;
+    if (w16b) *reinterpret_cast<u32x2_t*>(w16b) = q;
+  }
+  if (pb) *reinterpret_cast<f32x4_t*>(pb) = p;
+}
+
 template <int KIND, bool G16>
-__device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i, bf16* w16) {
+__device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i, bf16* w16, bf16* w16b, float* pb) {
   f32x4_t g;
   if constexpr (!G16) {
     g = *reinterpret_cast<const f32x4_t*>(a.g + i);
@@ -80,13 +90,13 @@ __device__ __forceinline__ void update_vec4(const OptArgs& a, float lr_t, long i
   *reinterpret_cast<f32x4_t*>(a.p + i) = p;
   if (KIND != OPT_SGD) *reinterpret_cast<f32x4_t*>(a.s1 + i) = s1;
   if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) *reinterpret_cast<f32x4_t*>(a.s2 + i) = s2;
-  if (w16) *reinterpret_cast<u32x2_t*>(w16) = u32x2_t{pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3])};
+  store_copies(p, w16, w16b, pb);
 }
 
 // U vec4 updates at i, i+1024, ... (one workgroup-wide stride apart): every load is issued
 // before the first update, so each thread keeps U x (3-4) 16-B loads in flight
 template <int KIND, int U, bool G16>
-__device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long i, bf16* w16) {
+__device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long i, bf16* w16, bf16* w16b, float* pb) {
   f32x4_t g[U], p[U], s1[U], s2[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -116,8 +126,92 @@ __device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long 
     *reinterpret_cast<f32x4_t*>(a.p + k) = p[u];
     if (KIND != OPT_SGD) *reinterpret_cast<f32x4_t*>(a.s1 + k) = s1[u];
     if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) *reinterpret_cast<f32x4_t*>(a.s2 + k) = s2[u];
-    if (w16) *reinterpret_cast<u32x2_t*>(w16 + u * 1024) = u32x2_t{pack_bf16x2(p[u][0], p[u][1]), pack_bf16x2(p[u][2], p[u][3])};
+    store_copies(p[u], w16 ? w16 + u * 1024 : nullptr, w16b ? w16b + u * 1024 : nullptr, pb ? pb + u * 1024 : nullptr);
   }
+}
+
+// apply one element of a segment from its (just reduced) fp32 gradient dwv: the master / slots,
+// the gradient buffer (the reduced value stays observable, as after the reduce kernels) and the
+// bf16 working copies (natural, and transposed [C][T][R])
+template <int KIND>
+__device__ __forceinline__ void apply_elem(const OptArgs& a, float lr_t, const OptSeg& sg, long li, float dwv) {
+  const long i = sg.off + li;
+  const_cast<float*>(a.g)[i] = dwv;
+  const float v = update_one<KIND>(a, lr_t, i, dwv * a.gscale);
+  const bf16 b = f2bf(v);
+  if (sg.w16) sg.w16[li] = b;
+  if (sg.wt16) {
+    const long TC = (long)sg.T * sg.C;
+    const long r = li / TC, rem = li - r * TC, t = rem / sg.C, c = rem - t * sg.C;
+    sg.wt16[(c * sg.T + t) * sg.R + r] = b;
+  }
+}
+
+// kind-2 item: wp_reduce_kernel / partials_reduce_kernel's block (16 f32x4 columns c16, 16 strided
+// slab subsets pg, subsets summed in order through LDS - the same additions in the same order, so
+// the applied gradient is bit-identical to the reduce-then-apply pair), then the update of the
+// <= 64 elements those columns hold
+template <int KIND>
+__device__ void part_item(const OptArgs& a, float lr_t, const OptWork& w, f32x4_t (*red)[17]) {
+  const OptPart pa = a.parts[w.t];
+  const int c16 = threadIdx.x & 15, pg = threadIdx.x >> 4;
+  const int v = (int)w.start + c16;  // f32x4 index within a slab
+  const int nv = (pa.plen + 3) / 4;
+  const int ntile = pa.layout == 0 ? 8 * pa.CTW * pa.MT * 64 : 0;
+  bool live = v < nv;
+  if (pa.layout == 0) live = live && (v >= ntile || ((v >> 6) / pa.MT / pa.CTW * pa.CTW + (v >> 6) / pa.MT % pa.CTW) * 16 < pa.KC);
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    for (int p0 = pg; p0 < pa.nblk; p0 += 16 * 8) {
+      f32x4_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = p0 + 16 * j;
+        x[j] = p < pa.nblk ? *reinterpret_cast<const f32x4_t*>(pa.ws + (long)p * pa.plen + 4 * v) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j];
+    }
+  }
+  red[pg][c16] = acc;
+  __syncthreads();
+  if (pg == 0 && live) {
+    f32x4_t t = red[0][c16];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += red[q][c16];
+    const OptSeg& ws = a.segs[pa.wseg];
+    if (pa.layout == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * v + e;
+        if (k < pa.nw) {
+          apply_elem<KIND>(a, lr_t, ws, k, __builtin_fmaf(pa.scale, t[e], a.g[ws.off + k]));
+        } else if (k < pa.plen && pa.bseg >= 0) {
+          const OptSeg& bs = a.segs[pa.bseg];
+          apply_elem<KIND>(a, lr_t, bs, k - pa.nw, __builtin_fmaf(pa.scale, t[e], a.g[bs.off + k - pa.nw]));
+        }
+      }
+    } else if (v < ntile) {
+      const int lane = v & 63, r = v >> 6, mt = r % pa.MT, rc = r / pa.MT, c = rc % pa.CTW, wv = rc / pa.CTW;
+      const int col = (wv * pa.CTW + c) * 16 + (lane & 15), n0 = mt * 16 + (lane >> 4) * 4;
+      if (col < pa.KC) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (n0 + j >= pa.N) continue;
+          const long li = (long)(n0 + j) * pa.KC + col;
+          apply_elem<KIND>(a, lr_t, ws, li, __builtin_fmaf(pa.scale, t[j], a.g[ws.off + li]));
+        }
+      }
+    } else if (pa.bseg >= 0) {
+      const OptSeg& bs = a.segs[pa.bseg];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = (v - ntile) * 4 + j;
+        if (n < pa.N) apply_elem<KIND>(a, lr_t, bs, n, __builtin_fmaf(pa.scale, t[j], a.g[bs.off + n]));
+      }
+    }
+  }
+  __syncthreads();  // (red is reused by the next item)
 }
 
 // One optimizer's share of a launch: workgroups bid = 0..nblk-1 of the grid (the whole grid for a
@@ -133,15 +227,21 @@ __device__ __forceinline__ void apply_items(const OptArgs& a, int bid, int nblk,
       const long base = sg.off + w.start;
       const long n4 = ((base & 3) == 0) ? (w.count / 4) * 4 : 0;  // segments are 64-aligned; chunks 8192
       long j = threadIdx.x * 4;
+      auto at16 = [&](bf16* q, long jj) { return q ? q + w.start + jj : nullptr; };
+      auto at32 = [&](float* q, long jj) { return q ? q + w.start + jj : nullptr; };
       for (; j + 3 * 1024 < n4; j += 4 * 1024)  // 4 independent vec4 updates in flight per thread
-        update_vec4x<KIND, 4, G16>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
+        update_vec4x<KIND, 4, G16>(a, lr_t, base + j, at16(sg.w16, j), at16(sg.w16b, j), at32(sg.pb, j));
       for (; j < n4; j += 256 * 4)
-        update_vec4<KIND, G16>(a, lr_t, base + j, sg.w16 ? sg.w16 + w.start + j : nullptr);
+        update_vec4<KIND, G16>(a, lr_t, base + j, at16(sg.w16, j), at16(sg.w16b, j), at32(sg.pb, j));
       for (long j = n4 + threadIdx.x; j < w.count; j += 256) {
         const long li = w.start + j, i = sg.off + li;
         const float v = update_one<KIND>(a, lr_t, i, load_grad<G16>(a, i));
         if (sg.w16) sg.w16[li] = f2bf(v);
+        if (sg.w16b) sg.w16b[li] = f2bf(v);
+        if (sg.pb) sg.pb[li] = v;
       }
+    } else if (w.kind == 2) {
+      if constexpr (!G16) part_item<KIND>(a, lr_t, w, reinterpret_cast<f32x4_t(*)[17]>(&tile[0][0]));
     } else {
       // 64x64 tile of tap t: rows r0.., cols c0.. of the [R][C] slice; transposed copy via LDS
       // the 16 elements of a thread are loaded together before any update (the update's stores may
@@ -172,17 +272,39 @@ __device__ __forceinline__ void apply_items(const OptArgs& a, int bid, int nblk,
           if (KIND == OPT_ADAM || KIND == OPT_RMSPROP) a.s2[i] = x2;
           const bf16 b = f2bf(v);
           if (sg.w16) sg.w16[li] = b;
+          if (sg.w16b) sg.w16b[li] = b;
+          if (sg.pb) sg.pb[li] = v;
           tile[rr][tx] = b;
         }
       }
       __syncthreads();
       for (int cc = ty; cc < 64; cc += 4) {
         const int c = w.c0 + cc, r = w.r0 + tx;
-        if (r < sg.R && c < sg.C) sg.wt16[((long)c * sg.T + w.t) * sg.R + r] = tile[tx][cc];
+        if (r < sg.R && c < sg.C) {
+          const long ti = ((long)c * sg.T + w.t) * sg.R + r;
+          if (sg.wt16) sg.wt16[ti] = tile[tx][cc];
+          if (sg.wt16b) sg.wt16b[ti] = tile[tx][cc];
+        }
       }
       __syncthreads();
     }
   }
+}
+
+// the ps reply words (ps_link.h PsWord: REP_GS 9, REP_VER 10, REP_STALE 11, REP_SEQ 8 last) into
+// the worker's slot of the host-mapped shared page: system-scope relaxed stores (they go to the
+// page, no cache holds them), the sequence number only after the others have completed - no
+// release fence: an L2 write-back here would wait for every dirty line the apply just wrote
+__device__ __forceinline__ void publish_reply(const OptArgs& a) {
+  uint64_t* slot = a.rep_slot;
+  const uint64_t gsv = a.rep_gs ? (uint64_t)(int64_t)__hip_atomic_load(const_cast<int32_t*>(a.rep_gs), __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                : (uint64_t)(int64_t)-1;
+  __hip_atomic_store(slot + 9, gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(slot + 10, a.rep_ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(slot + 11, (uint64_t)a.rep_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(slot + 8, a.rep_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int KIND>
@@ -192,6 +314,10 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
   // last workgroup: advance the non-slot scalars.  Every thread read them at its start and
   // used the value; after the barrier one lane takes a ticket (relaxed agent atomics - nothing
   // is handed between workgroups, so no fences) and the last arriver updates them.
+  // A folded ps reply is handed over: every wave's stores (the reply buffer copies, uncached
+  // memory) have completed before its workgroup takes the ticket, so the last arriver's reply
+  // words follow every value the worker will read.
+  if (a.rep_slot) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(a.done_counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -202,13 +328,14 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
       }
       if (a.global_step && a.gs_inc) atomicAdd(a.global_step, a.gs_inc);
     }
+    if (prev == (uint32_t)nblk - 1 && a.rep_slot) publish_reply(a);
     if (prev == (uint32_t)nblk - 1) __hip_atomic_store(a.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <int KIND>
 __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
-  __shared__ bf16 tile[64][66];
+  __shared__ __attribute__((aligned(16))) bf16 tile[64][66];
   apply_body<KIND>(a, blockIdx.x, gridDim.x, tile);
 }
 
@@ -217,19 +344,33 @@ __global__ __launch_bounds__(256) void apply_gradients_kernel(OptArgs a) {
 // beta powers and global-step increment, exactly as separate launches would.
 template <int KIND>
 __global__ __launch_bounds__(256) void apply_gradients_group_kernel(OptGroup g) {
-  __shared__ bf16 tile[64][66];
+  __shared__ __attribute__((aligned(16))) bf16 tile[64][66];
   int i = 0;
   while (i + 1 < g.n && (int)blockIdx.x >= g.first[i + 1]) ++i;
   apply_body<KIND>(g.o[i], blockIdx.x - g.first[i], g.first[i + 1] - g.first[i], tile);
 }
 
-__global__ void opt_advance_kernel(OptArgs a) {
-  if (threadIdx.x != 0) return;
+__device__ __forceinline__ void advance_one(const OptArgs& a) {
   if (a.kind == OPT_ADAM && a.beta_pow) {
     a.beta_pow[0] *= a.beta1;
     a.beta_pow[1] *= a.beta2;
   }
   if (a.global_step && a.gs_inc) atomicAdd(a.global_step, a.gs_inc);
+}
+
+__global__ void opt_advance_kernel(OptArgs a) {
+  if (threadIdx.x != 0) return;
+  advance_one(a);
+}
+
+struct OptAdvanceSet {
+  OptArgs o[OPT_GROUP_MAX];
+  int n;
+};
+__global__ void opt_advance_reply_kernel(OptAdvanceSet g) {
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < g.n; ++i) advance_one(g.o[i]);
+  if (g.o[g.n - 1].rep_slot) publish_reply(g.o[g.n - 1]);
 }
 
 static int apply_blocks(const OptArgs& a) {
@@ -258,6 +399,14 @@ void launch_apply_gradients_group(const OptArgs* o, int n, hipStream_t s) {
 
 void launch_opt_advance(const OptArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(opt_advance_kernel, dim3(1), dim3(64), 0, s, a);
+}
+
+void launch_opt_advance_reply(const OptArgs* a, int n, hipStream_t s) {
+  if (n < 1 || n > OPT_GROUP_MAX) throw std::runtime_error("opt_advance_reply: 1..4 optimizers");
+  OptAdvanceSet g{};
+  for (int i = 0; i < n; ++i) g.o[i] = a[i];
+  g.n = n;
+  hipLaunchKernelGGL(opt_advance_reply_kernel, dim3(1), dim3(64), 0, s, g);
 }
 
 void launch_apply_gradients(const OptArgs& a, hipStream_t s) {

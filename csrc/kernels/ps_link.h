@@ -6,8 +6,9 @@
 // when the worker shares the ps's GPU), a pull is its GPU reading the reply buffer.  The
 // request / reply handshake lives in a small shared-memory page mapped into both processes and
 // registered for device access: the worker's GPU publishes "request s" with a system-scope
-// release store after its push, the ps's native service thread polls the page, enqueues the
-// fused apply and the reply snapshot on its own stream and a reply store; the worker's GPU waits
+// store once its push has completed, the ps's native service thread polls the page, enqueues the
+// fused apply - which writes the worker's reply buffer and the reply words itself - on its own
+// stream; the worker's GPU waits
 // for the reply in a bounded spin kernel, then pulls.  No host round trip on the worker side,
 // so the whole worker step (compute, push, request, wait, pull) replays as one hipGraph.
 #pragma once

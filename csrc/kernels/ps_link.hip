@@ -9,8 +9,17 @@ __device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
-  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Hand-off discipline (no release / acquire fences): mailboxes and reply buffers are uncached
+// device memory, so a store is in memory once it has completed; every copy kernel drains its
+// stores before it ends (the next kernel of the stream starts after it), and the handshake
+// words are system-scope relaxed stores to the host-mapped page, the sequence number issued
+// only after the other words have completed.  A system-scope release fence would instead write
+// back every dirty line of the XCD's L2 - tens of microseconds after an apply or a backward
+// (profiles/r4_ps_1p1w_timeline.txt: ps_reply 41-47 us, ps_request 3-4 us).
 
 __device__ __forceinline__ void cvt8(const void* src, int smode_bf16, long i, float (&v)[8]) {
   if (smode_bf16) {
@@ -85,6 +94,7 @@ __global__ __launch_bounds__(256) void ps_copy_kernel(const PsSeg* __restrict__ 
     for (long j = (long)threadIdx.x * 8; j < n8; j += 256 * 8) copy8(s, w.start + j);
     for (long j = n8 + threadIdx.x; j < w.count; j += 256) copy1(s, w.start + j);
   }
+  drain_stores();  // a push / reply is complete in (uncached) memory when the kernel ends
 }
 
 __global__ void ps_request_kernel(uint64_t* slot, int64_t* ctr, const int64_t* ver, int kind, int bump) {
@@ -93,23 +103,20 @@ __global__ void ps_request_kernel(uint64_t* slot, int64_t* ctr, const int64_t* v
   // the counter (the others follow it on the same stream and reuse the value)
   const int64_t c = *ctr + bump;
   if (bump) *ctr = c;
-  // every preceding kernel of this stream (the push copies) has completed; drain this
-  // kernel's own view before publishing
-  __threadfence_system();
+  // every preceding kernel of this stream (the push copies) has completed and drained its stores
   st_sys(slot + PS_REQ_KIND, (uint64_t)kind);
   st_sys(slot + PS_REQ_TAG, ver ? (uint64_t)*ver : 0ull);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __hip_atomic_store(slot + PS_REQ_SEQ, (uint64_t)c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  drain_stores();
+  st_sys(slot + PS_REQ_SEQ, (uint64_t)c);
 }
 
 __global__ void ps_bucket_kernel(uint64_t* slot, const int64_t* ctr, int b, long lo, long hi) {
   if (threadIdx.x != 0) return;
   // the bucket's push copies (earlier on this stream) have completed: publish its range
-  __threadfence_system();
   st_sys(slot + PS_BKT_BASE + 3 * b + 1, (uint64_t)lo);
   st_sys(slot + PS_BKT_BASE + 3 * b + 2, (uint64_t)hi);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __hip_atomic_store(slot + PS_BKT_BASE + 3 * b, (uint64_t)(*ctr + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  drain_stores();
+  st_sys(slot + PS_BKT_BASE + 3 * b, (uint64_t)(*ctr + 1));
 }
 
 __global__ void ps_wait_kernel(PsWaitArgs a) {
@@ -128,17 +135,17 @@ __global__ void ps_wait_kernel(PsWaitArgs a) {
   if (a.gs_out && a.gs_slot >= 0) *a.gs_out = (int32_t)(int64_t)ld_sys(a.slot[a.gs_slot] + PS_REP_GS);
   if (a.ver_out)  // per shard: each shard's version is the staleness tag of that shard's next request
     for (int k = 0; k < a.nslots; ++k) a.ver_out[k] = (int64_t)ld_sys(a.slot[k] + PS_REP_VER);
-  __threadfence_system();
+  // (the pull that follows reads uncached reply buffers: nothing to invalidate)
 }
 
 __global__ void ps_reply_kernel(uint64_t* slot, const int32_t* gs, uint64_t seq, uint64_t ver, int stale) {
   if (threadIdx.x != 0) return;
-  __threadfence_system();
+  // the reply snapshot (earlier on this stream) has completed and drained its stores
   st_sys(slot + PS_REP_GS, gs ? (uint64_t)(int64_t)*gs : (uint64_t)(int64_t)-1);
   st_sys(slot + PS_REP_VER, ver);
   st_sys(slot + PS_REP_STALE, (uint64_t)stale);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __hip_atomic_store(slot + PS_REP_SEQ, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  drain_stores();
+  st_sys(slot + PS_REP_SEQ, seq);
 }
 
 }  // namespace

@@ -225,6 +225,10 @@ class BN:
     def bind(self, P, shape, dev, arena):
         self.P = P
         self.y = torch.empty(*shape, device=dev, dtype=ACT_DTYPE)
+        # 1-bit ReLU mask of y (a ReLU after a residual add): what the backward reads instead of y
+        self.ybits = torch.empty(math.prod(shape) // 8, device=dev, dtype=torch.uint8) \
+            if torch.device(dev).type == "cuda" else None
+        self.use_bits = False
         self.stats, self.dstats, self.mean, self.invstd = arena.take(2 * self.C), arena.take(2 * self.C), \
             arena.take(self.C), arena.take(self.C)
 
@@ -236,29 +240,36 @@ class BN:
             ops.bn_infer(x, P.view(self.gamma), P.view(self.beta), P.view(self.mm), P.view(self.mv), self.y,
                          eps=BN_EPS, act=act, res=res, rstride=rstride)
             return self.y
-        # backward recomputes the ReLU mask from x unless a shortcut was added before the ReLU
+        # backward recomputes the ReLU mask from x unless a shortcut was added before the ReLU; then
+        # it reads the 1-bit mask this apply writes beside y (1 byte per 8 channels instead of 16:
+        # the block-output BN's two backward passes read dy, x and the mask, not dy, x and y)
         self.mask_from_x = act == ops.ACT_RELU and res is None
+        self.use_bits = act == ops.ACT_RELU and res is not None and self.ybits is not None
         if not have_stats:
             ops.bn_stats(x, self.stats)
         ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
                      invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
-                     momentum=BN_MOMENTUM, act=act, res=res, rstride=rstride)
+                     momentum=BN_MOMENTUM, act=act, res=res, rstride=rstride,
+                     mask_out=self.ybits if self.use_bits else None)
         return self.y
+
+    def _mask_src(self, act):
+        """(y argument, beta) of the backward ops: the bit mask, y, or nothing (mask from x)."""
+        from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
+        if act == ops.ACT_NONE or from_x:
+            return None, (self.P.view(self.beta) if from_x else None)
+        return (self.ybits if self.use_bits and act == ops.ACT_RELU else self.y), None
 
     def bwd_stats_args(self, x, act=ops.ACT_RELU):
         """(x, y, mean, invstd, gamma, beta, stats, act) of this BN's backward statistics, for the
         launch that produces its output gradient (ops.conv_dgrad(bn_bwd=...))."""
         P = self.P
-        from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
-        y = self.y if act != ops.ACT_NONE and not from_x else None
-        beta = P.view(self.beta) if from_x else None
+        y, beta = self._mask_src(act)
         return (x, y, self.mean, self.invstd, P.view(self.gamma), beta, self.dstats, act)
 
     def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None, stats_done=False):
         P = self.P
-        from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
-        y = self.y if act != ops.ACT_NONE and not from_x else None
-        beta = P.view(self.beta) if from_x else None
+        y, beta = self._mask_src(act)
         if not stats_done:
             ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta)
         ops.bn_bwd_apply(dy, y, x, self.mean, self.invstd, P.view(self.gamma), self.dstats, dx, act=act, dres=dres,

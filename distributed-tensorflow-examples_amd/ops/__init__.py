@@ -25,7 +25,7 @@ __all__ = [
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
-    "bn_bwd_apply", "shortcut_grad_add",
+    "bn_bwd_apply", "relu_bits", "opt_pack_parts", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
@@ -409,16 +409,17 @@ def wgrad_workspace(device, numel):
 
 
 def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
-             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0):
+             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0, defer_reduce=False):
     """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY.
     On the GPU the persistent kernel stores per-workgroup partials in `workspace`
-    (default: a cached per-device buffer) and a second kernel sums them."""
+    (default: a cached per-device buffer) and a second kernel sums them.  ``defer_reduce``: no
+    second kernel - returns the partials' layout [layout, nblk, plen, MT, CTW, KC, N, nw] for the
+    optimizer to sum them itself (``Optimizer.build_fold``; [] when the launch kept none)."""
     if dw.is_cuda:
         if workspace is None and (CS % 16 == 0 or CS == 1):
             workspace = wgrad_workspace(dw.device, wgrad_ws_floats(N, KH * KW * CS))
-        require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
-                           scale, workspace, max_blocks)
-        return
+        return list(require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW,
+                                       stride, pad, scale, workspace, max_blocks, defer_reduce))
     d = dy.float().view(B, OH, OW, N) if dy is not None else _unpooled_nhwc(dy_pooled, dy_argmax, B, OH, OW, N)
     gw = torch.nn.grad.conv2d_weight(src.float().view(B, SH, SW, CS).permute(0, 3, 1, 2), (N, CS, KH, KW),
                                      d.permute(0, 3, 1, 2), stride=stride, padding=pad)
@@ -583,10 +584,17 @@ def opt_pack(segs, work, device_like):
 
 
 def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow, global_step,
-                    gs_inc, done, blob, nseg, nwork, group=0):
-    """group: 0 launch now, 1 queue, 2 queue + launch all queued optimizers as one grouped launch."""
+                    gs_inc, done, blob, nseg, nwork, group=0, parts=None):
+    """group: 0 launch now, 1 queue, 2 queue + launch all queued optimizers as one grouped launch.
+    ``parts``: opt_pack_parts table of the plan's kind-2 items (unreduced weight-gradient partials)."""
     require().apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow,
-                              global_step, gs_inc, done, blob, nseg, nwork, group)
+                              global_step, gs_inc, done, blob, nseg, nwork, group, parts)
+
+
+def opt_pack_parts(ints, scales, device_like):
+    """Device table of OptPart rows (csrc/kernels/optim.h): ints int64 [n, 11] = (ws address, nblk,
+    plen, layout, MT, CTW, KC, N, nw, weight seg, bias seg), scales float64 [n]."""
+    return require().opt_pack_parts(ints, scales, device_like)
 
 
 # ------------------------------------------------------------- elementwise
@@ -810,13 +818,15 @@ def _shortcut_view(res, OH, OW, C, rstride):
 
 
 def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=None, moving_var=None, eps=1e-3,
-             momentum=0.99, act=ACT_RELU, res=None, rstride=1):
+             momentum=0.99, act=ACT_RELU, res=None, rstride=1, mask_out=None):
     """out = act(gamma * (x - mean) * invstd + beta [+ shortcut(res)]) with batch statistics from
-    ``stats``; stores mean/invstd and updates the moving averages (TF momentum convention)."""
+    ``stats``; stores mean/invstd and updates the moving averages (TF momentum convention).
+    ``mask_out`` (ReLU): uint8 [R][C/8] bit mask of out > 0, which the backward ops take in place
+    of ``y`` (``relu_bits``)."""
     OH, OW = (x.shape[1], x.shape[2]) if x.dim() == 4 else (1, 1)
     if x.is_cuda:
         require().bn_apply(x, stats, gamma, beta, mean, invstd, moving_mean, moving_var, eps, momentum, act, res,
-                           rstride, OH, OW, out)
+                           rstride, OH, OW, out, mask_out)
         return out
     r = _rows(x)
     R, C = r.shape
@@ -833,7 +843,23 @@ def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=
     if res is not None:
         y = y + _shortcut_view(res, OH, OW, C, rstride).reshape(R, C)
     out.copy_(_act_ref(y, act).reshape(out.shape).to(out.dtype))
+    if mask_out is not None:
+        mask_out.copy_(relu_bits(out))
     return out
+
+
+def relu_bits(y):
+    """uint8 [R][C/8] bit mask of y > 0 (bit e of byte (r, j) = channel 8 j + e) - the layout
+    bn_apply(mask_out=...) writes."""
+    r = _rows(y) > 0
+    R, C = r.shape
+    w = (1 << torch.arange(8, device=r.device, dtype=torch.int32))
+    return (r.reshape(R, C // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8).reshape(-1)
+
+
+def _unbits(m, R, C):
+    e = torch.arange(8, device=m.device, dtype=torch.int32)
+    return ((m.reshape(R, C // 8, 1).to(torch.int32) >> e) & 1).reshape(R, C).bool()
 
 
 def bn_infer(x, gamma, beta, moving_mean, moving_var, out, *, eps=1e-3, act=ACT_RELU, res=None, rstride=1):
@@ -860,6 +886,8 @@ def _masked_grad(dy, y, act, x=None, mean=None, invstd=None, gamma=None, beta=No
             scale = gamma.float() * invstd
             pre = _rows(x) * scale + (beta.float() - mean * scale)
             return g * (pre > 0)
+        if y.dtype == torch.uint8:  # bn_apply's bit mask of the ReLU output
+            return g * _unbits(y, g.shape[0], g.shape[1])
         g = g * _act_grad_from_out_ref(_rows(y), act)
     return g
 

@@ -6,9 +6,10 @@ encoder/distributed_encoder.py:165).  On one MI355X node this module replaces th
 
 * ps side (``NativeShardService``): per worker a gradient mailbox and a parameter reply buffer
   in the ps GPU's HBM (one uncached hipIpc allocation), a shared request/reply page, and a C++
-  progress thread that applies every arriving mailbox with the fused TF1 optimizer kernels and
-  snapshots the shard's working copies into that worker's reply buffer - no Python, no GIL,
-  no host copies on the data path;
+  progress thread that applies every arriving mailbox with the fused TF1 optimizer kernels;
+  the apply writes the updated bf16 working copies (and fp32 variables) straight into that
+  worker's reply buffer, and its last workgroup advances the step scalars and publishes the
+  reply - no snapshot copy, no Python, no GIL, no host copies on the data path;
 * worker side (``NativePSLink``): copy plans that push the gradient buckets straight from the
   worker's flat gradient buffer into its mailbox (fp32 -> bf16 in flight for bf16-compute
   models) and pull the reply buffer straight into the worker's bf16 working copies (+ fp32
@@ -199,7 +200,9 @@ class NativePSLink:
     grad16 = None
 
     def __init__(self, server, full: FlatParams, placement: dict, shard_specs: dict, gs_ps_task: int, device,
-                 buckets=None, timeout_s: float = 60.0):
+                 buckets=None, timeout_s: float = 60.0, overlap=None):
+        """``overlap``: announce pushed buckets so the ps applies them during backward - None: only
+        to ps tasks on another GPU than this worker's (True / False: always / never)."""
         ops.require()
         lib = torch.ops.dtfe
         self.lib = lib
@@ -208,6 +211,7 @@ class NativePSLink:
         self.w = server.task_index
         self.timeout_s = timeout_s
         self.shards = []
+        overlap_arg = overlap
         st = server.store
         for k, specs in sorted(shard_specs.items()):
             if not specs:
@@ -222,7 +226,14 @@ class NativePSLink:
             shm = lib.ps_shm_open(name, n_workers * SLOT_BYTES)
             buf = lib.ps_ipc_open(torch.frombuffer(bytearray(handle), dtype=torch.uint8), self.device.index or 0)
             base = lib.ps_ipc_ptr(buf) + self.w * (mb + rb)
-            self.shards.append(dict(k=k, specs=specs, lay=lay, shm=shm, buf=buf, mailbox=base, reply=base + mb, dt=dt))
+            # a ps task on this worker's own GPU: its applies would only compete with this worker's
+            # backward for the CUs (bucket 0's apply stretched from 18 to 55-100 us beside the conv
+            # backward, profiles/r4_ps_1p1w_timeline.txt), so no bucket is announced to it - the
+            # request applies the whole push at once, while this worker waits
+            overlap = not server.colocated(server.cluster.rank_of("ps", k), server.rank) if overlap_arg is None \
+                else bool(overlap_arg)
+            self.shards.append(dict(k=k, specs=specs, lay=lay, shm=shm, buf=buf, mailbox=base, reply=base + mb, dt=dt,
+                                    overlap=overlap))
         self.gs_slot = next((i for i, sh in enumerate(self.shards) if sh["k"] == gs_ps_task), -1)
         # pull plan: reply buffers -> local working copies / masters (one launch for all shards)
         segs = []
@@ -295,9 +306,11 @@ class NativePSLink:
             self.side.wait_event(ev)
         with torch.cuda.stream(self.side):
             self._run(self._push[i])
-            if self._bkt_ranges is not None:
+            # the step's last bucket is not announced: the request that follows it makes the ps
+            # apply it in the launch that also advances the step scalars and writes the reply
+            if self._bkt_ranges is not None and len(self._launched) < len(self.buckets):
                 for sh, r in zip(self.shards, self._bkt_ranges[i]):
-                    if r is not None:
+                    if r is not None and sh["overlap"]:
                         self.lib.ps_bucket(sh["shm"], self.w, self.ctr, i, r[0], r[1])
         self._forked = True
 

@@ -56,6 +56,49 @@ def test_bn_forward_backward(shape, res_shape, rstride, from_x):
         assert _rel(g[k], c[k]) < 2e-2, k
 
 
+@pytest.mark.parametrize("shape,res_shape,rstride", [
+    ((8, 16, 16, 32), (8, 16, 16, 32), 1),   # identity shortcut
+    ((8, 8, 8, 64), (8, 16, 16, 32), 2),     # option A
+    ((4, 7, 7, 2048), (4, 7, 7, 2048), 1),   # ResNet-50 widest block output
+    ((3, 17, 19, 64), (3, 17, 19, 64), 1),   # ragged row count
+])
+def test_bn_relu_bitmask_matches_y(shape, res_shape, rstride):
+    """bn_apply(mask_out=...) writes the 1-bit ReLU mask of its output; the backward ops given that
+    mask produce the same bits as with the bf16 output y (the mask is y > 0 of the stored values),
+    and the mask equals the host-side relu_bits(y)."""
+    torch.manual_seed(3)
+    C = shape[-1]
+    x = (torch.randn(*shape, device=DEV) * 2 + 1).to(torch.bfloat16)
+    res = torch.randn(*res_shape, device=DEV).to(torch.bfloat16)
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    dy = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    st = torch.zeros(2 * C, device=DEV)
+    mean, inv = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    y = torch.empty(*shape, device=DEV, dtype=torch.bfloat16)
+    bits = torch.full((x.numel() // 8,), 0xA5, device=DEV, dtype=torch.uint8)
+    ops.bn_stats(x, st)
+    ops.bn_apply(x, st, gamma, beta, y, mean=mean, invstd=inv, act=ops.ACT_RELU, res=res, rstride=rstride,
+                 mask_out=bits)
+    torch.cuda.synchronize()
+    assert torch.equal(bits.cpu(), ops.relu_bits(y.cpu()))
+    outs = []
+    for ym in (y, bits):
+        st2 = torch.zeros(2 * C, device=DEV)
+        dx = torch.empty(*shape, device=DEV, dtype=torch.bfloat16)
+        dres = torch.empty(*shape, device=DEV, dtype=torch.bfloat16)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        ops.bn_bwd_stats(dy, ym, x, mean, inv, st2, ops.ACT_RELU, gamma=gamma)
+        ops.bn_bwd_apply(dy, ym, x, mean, inv, gamma, st2, dx, act=ops.ACT_RELU, dres=dres, dgamma=dg, dbeta=db)
+        outs.append((st2, dx, dres, dg, db))
+    torch.cuda.synchronize()
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    # the CPU reference with the mask: same gradient as with y
+    st3 = torch.zeros(2 * C)
+    ops.bn_bwd_stats(dy.cpu(), bits.cpu(), x.cpu(), mean.cpu(), inv.cpu(), st3, ops.ACT_RELU)
+    assert _rel(outs[0][0], st3) < 2e-3
+
+
 def test_shortcut_grad_add_and_gap():
     torch.manual_seed(1)
     g = torch.randn(4, 8, 8, 64).to(torch.bfloat16)
