@@ -169,7 +169,8 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
                 const optional<Tensor>& pooled, const optional<Tensor>& argmax, const optional<Tensor>& relu_mask,
                 bool accumulate, const optional<Tensor>& bnb_x, const optional<Tensor>& bnb_y,
                 const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_invstd, const optional<Tensor>& bnb_gamma,
-                const optional<Tensor>& bnb_beta, const optional<Tensor>& bnb_stats, int64_t bnb_act) {
+                const optional<Tensor>& bnb_beta, const optional<Tensor>& bnb_stats, int64_t bnb_act,
+                const optional<Tensor>& acc_src, const optional<Tensor>& acc_mask) {
   check_cuda(dy, "dy");
   if (dy.scalar_type() == at::kFloat) {  // exact-fp32 path (--dtype fp32): conv_f32.hip
     TORCH_CHECK(wt.scalar_type() == at::kFloat && dx.scalar_type() == at::kFloat && stride == 1 && !accumulate &&
@@ -209,6 +210,14 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
     a.bnb_beta = ptr_or_null<float>(bnb_beta);
     a.bnb_stats = bnb_stats->data_ptr<float>();
     a.bnb_act = (int)bnb_act;
+  }
+  if (acc_src.has_value() && acc_src->defined()) {
+    TORCH_CHECK(accumulate && acc_src->numel() == dx.numel() && acc_src->scalar_type() == at::kBFloat16 &&
+                    acc_mask.has_value() && acc_mask->defined() && acc_mask->scalar_type() == at::kByte &&
+                    acc_mask->numel() == dx.numel() / 8,
+                "conv_dgrad: acc_src (bf16, dx's shape) needs accumulate and its uint8 [R][C/8] bit mask");
+    a.acc_src = reinterpret_cast<const dtfe::bf16*>(acc_src->data_ptr());
+    a.acc_mask = acc_mask->data_ptr<uint8_t>();
   }
   a.g = geom(B, H, W, C, Cout, OH, OW, KH, KW, stride, pad, 0);
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
@@ -316,14 +325,13 @@ void conv1_gather_fwd(const Tensor& images, const Tensor& labels_src, int64_t se
   TORCH_CHECK(dtfe::launch_conv1_copies_fwd(a, cur_stream()), "conv1_gather_fwd: needs B >= 256");
 }
 
-std::vector<int64_t> imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
+void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
-              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks, bool defer_reduce) {
+              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks) {
   check_cuda(src, "src");
   dtfe::ImgWgradArgs a{};
   a.max_blocks = (int)max_blocks;
-  a.defer_reduce = defer_reduce ? 1 : 0;
   if (ws.has_value() && ws->defined()) {
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= dtfe::imgwgrad_ws_floats((int)N, (int)(KH * KW * CS)),
                 "imgwgrad: workspace too small (ops.wgrad_ws_floats)");
@@ -340,12 +348,7 @@ std::vector<int64_t> imgwgrad(const Tensor& src, const optional<Tensor>& dy, con
   a.dw = dw.data_ptr<float>();
   a.db = ptr_or_null<float>(db);
   a.scale = (float)scale;
-  dtfe::imgwgrad_last_layout() = dtfe::WgPartLayout();
   dtfe::launch_imgwgrad(a, cur_stream());
-  // defer_reduce: the partials' layout (empty when this launch kept none: no workspace / atomics)
-  const dtfe::WgPartLayout L = dtfe::imgwgrad_last_layout();
-  if (!defer_reduce || L.layout < 0) return {};
-  return {L.layout, L.nblk, L.plen, L.MT, L.CTW, L.KC, L.N, L.nw};
 }
 
 void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t H,
@@ -471,34 +474,11 @@ Tensor opt_pack(const Tensor& segs, const Tensor& work, const Tensor& device_lik
   return host.to(device_like.device());
 }
 
-// ints: int64 [n, 11] = (ws_ptr, nblk, plen, layout, MT, CTW, KC, N, nw, wseg, bseg); scales: float64 [n]
-Tensor opt_pack_parts(const Tensor& ints, const Tensor& scales, const Tensor& device_like) {
-  TORCH_CHECK(ints.device().is_cpu() && ints.scalar_type() == at::kLong && ints.dim() == 2 && ints.size(1) == 11 &&
-                  scales.device().is_cpu() && scales.numel() == ints.size(0),
-              "opt_pack_parts: CPU int64 [n, 11] + float64 [n]");
-  auto I = ints.contiguous();
-  auto S = scales.to(at::kDouble).contiguous();
-  const int64_t n = I.size(0);
-  std::vector<dtfe::OptPart> v((size_t)n);
-  const int64_t* q = I.data_ptr<int64_t>();
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t* r = q + i * 11;
-    v[i].ws = reinterpret_cast<const float*>(r[0]);
-    v[i].nblk = (int)r[1]; v[i].plen = (int)r[2]; v[i].layout = (int)r[3]; v[i].MT = (int)r[4]; v[i].CTW = (int)r[5];
-    v[i].KC = (int)r[6]; v[i].N = (int)r[7]; v[i].nw = (int)r[8]; v[i].wseg = (int)r[9]; v[i].bseg = (int)r[10];
-    v[i].scale = (float)S.data_ptr<double>()[i];
-    TORCH_CHECK(v[i].layout == 0 || v[i].layout == 1, "opt_pack_parts: layout 0 / 1");
-  }
-  Tensor host = at::empty({(int64_t)(n * sizeof(dtfe::OptPart))}, at::TensorOptions().dtype(at::kByte));
-  std::memcpy(host.data_ptr(), v.data(), n * sizeof(dtfe::OptPart));
-  return host.to(device_like.device());
-}
-
 void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, const optional<Tensor>& g16,
                      double gscale, const optional<Tensor>& s1, const optional<Tensor>& s2, double lr, double beta1,
                      double beta2, double eps, double momentum, double rho, const optional<Tensor>& beta_pow,
                      const optional<Tensor>& global_step, int64_t gs_inc, const Tensor& done, const Tensor& blob,
-                     int64_t nseg, int64_t nwork, int64_t group, const optional<Tensor>& parts) {
+                     int64_t nseg, int64_t nwork, int64_t group) {
   check_cuda(p, "p");
   // group: 0 = launch now; 1 = queue these args; 2 = queue and launch every queued optimizer in
   // ONE grouped launch (same kind, disjoint var lists: e.g. the GAN's two Adams)
@@ -522,10 +502,6 @@ void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, c
   a.segs = reinterpret_cast<const dtfe::OptSeg*>(blob.data_ptr());
   a.work = reinterpret_cast<const dtfe::OptWork*>((const char*)blob.data_ptr() + off_w);
   a.nwork = (int)nwork;
-  if (parts.has_value() && parts->defined()) {
-    TORCH_CHECK(parts->is_cuda() && a.g, "apply_gradients: partial sources need the fp32 gradient buffer");
-    a.parts = reinterpret_cast<const dtfe::OptPart*>(parts->data_ptr());
-  }
   if (kind == dtfe::OPT_ADAM) TORCH_CHECK(a.beta_pow && a.s1 && a.s2, "adam needs slots and beta powers");
   if (kind == dtfe::OPT_RMSPROP) TORCH_CHECK(a.s1 && a.s2, "rmsprop needs slots");
   if (kind == dtfe::OPT_MOMENTUM) TORCH_CHECK(a.s1, "momentum needs a slot");
@@ -974,7 +950,8 @@ TORCH_LIBRARY(dtfe, m) {
       "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
       " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask, bool accumulate=False,"
       " Tensor? bnb_x=None, Tensor? bnb_y=None, Tensor? bnb_mean=None, Tensor? bnb_invstd=None,"
-      " Tensor? bnb_gamma=None, Tensor? bnb_beta=None, Tensor(b!)? bnb_stats=None, int bnb_act=0) -> ()");
+      " Tensor? bnb_gamma=None, Tensor? bnb_beta=None, Tensor(b!)? bnb_stats=None, int bnb_act=0,"
+      " Tensor? acc_src=None, Tensor? acc_mask=None) -> ()");
   m.def("conv1_fwd_pool(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!) argmax) -> ()");
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
@@ -983,7 +960,7 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"
-      " int max_blocks=0, bool defer_reduce=False) -> int[]");
+      " int max_blocks=0) -> ()");
   m.def("conv1_wgrad_pooled(Tensor x, Tensor dp, Tensor argmax, Tensor(a!) dw, Tensor(b!)? db, float scale) -> ()");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
@@ -998,9 +975,7 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "apply_gradients(int kind, Tensor(a!) p, Tensor? g, Tensor? g16, float gscale, Tensor(b!)? s1, Tensor(c!)? s2,"
       " float lr, float beta1, float beta2, float eps, float momentum, float rho, Tensor(d!)? beta_pow,"
-      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0,"
-      " Tensor? parts=None) -> ()");
-  m.def("opt_pack_parts(Tensor ints, Tensor scales, Tensor device_like) -> Tensor");
+      " Tensor(e!)? global_step, int gs_inc, Tensor(f!) done, Tensor blob, int nseg, int nwork, int group=0) -> ()");
   m.def("wgrad_tallk(Tensor A, int lda, Tensor B, int ldb, int M, int N, int K, Tensor(a!) out, int ldc,"
         " Tensor(b!)? bias, Tensor(c!) ws, int splits, float scale) -> ()");
   m.def("seq_stage(Tensor x, Tensor(a!) xh, int T, int I, Tensor ysrc, Tensor(b!) ydst, Tensor(c!)[] zero) -> ()");
@@ -1067,7 +1042,4 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }
 
-TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) {
-  m.impl("opt_pack", &opt_pack);
-  m.impl("opt_pack_parts", &opt_pack_parts);
-}
+TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) { m.impl("opt_pack", &opt_pack); }

@@ -56,6 +56,8 @@ struct ConvDgradArgs {
   const bf16* bnb_x; const bf16* bnb_y; const float* bnb_mean; const float* bnb_invstd;
   const float* bnb_gamma; const float* bnb_beta; float* bnb_stats; int bnb_act;
   const uint8_t* bnb_ymask;   // 1-bit ReLU mask instead of bnb_y (norm.h BnArgs::ymask)
+  // accumulate onto acc_src * mask instead of onto dx's contents (igemm.h IgemmArgs::acc_src)
+  const bf16* acc_src; const uint8_t* acc_mask;
 };
 struct ConvWgradArgs {
   ConvGeom g;

@@ -34,6 +34,10 @@ struct IgemmArgs {
   int istr, OHf, OWf, ostr;
   int nphase, splits, tiles_m;
   int accum;              // out += result (bf16 read-modify-write in the epilogue)
+  // accum with a masked source: out = result + acc_src * bit (acc_mask: 1-bit [rows][N/8] mask at the
+  // output's pixel / channel), read instead of out - a residual block's shortcut gradient
+  // (dout * ReLU'(block output)) added where the input gradient is produced, never stored alone
+  const bf16* acc_src; const uint8_t* acc_mask;
   // forward only: per output tile and channel the BatchNorm partials of the stored (bf16) output,
   // [tiles_m][3][N] = (K_t = the tile's first row, sum (y - K_t), sum (y - K_t)^2)
   float* bn_part;

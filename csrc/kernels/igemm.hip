@@ -111,8 +111,23 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
   u32x4_t old[PER];
   if (a.accum) {  // e.g. a block's input gradient: the shortcut branch's share is already there;
                   // every load is issued before the first add (no per-chunk latency chain)
+    if (a.acc_src) {  // ... or computed here: the masked shortcut gradient at the same position
+      uint32_t mk[PER];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
+      for (int j = 0; j < PER; ++j) {
+        const long off = dst[j] ? (long)(dst[j] - a.out) : 0;
+        old[j] = *reinterpret_cast<const u32x4_t*>(a.acc_src + off);
+        mk[j] = a.acc_mask[off >> 3];
+      }
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          old[j][e] &= ((mk[j] >> (2 * e)) & 1u ? 0x0000ffffu : 0u) | ((mk[j] >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+    } else {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) old[j] = dst[j] ? *reinterpret_cast<const u32x4_t*>(dst[j]) : u32x4_t{0u, 0u, 0u, 0u};
+    }
   }
   // BatchNorm-backward statistics of the final values: this thread's 8 channels are the same for
   // every j (IG_THREADS % CPR == 0); x (and y for a non-recomputable mask) at the same offsets
@@ -1067,6 +1082,10 @@ bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
   a.N = g.C; a.Ktot = g.KH * g.KW * g.Cout;
   a.istr = 1; a.OHf = g.H; a.OWf = g.W; a.ostr = g.stride;
   a.accum = d.accumulate;
+  a.acc_src = d.acc_src;
+  a.acc_mask = d.acc_mask;
+  if (a.acc_src && (!a.accum || g.stride != 1 || !a.acc_mask))
+    throw std::runtime_error("conv_dgrad: a masked accumulation source needs accumulate, stride 1 and its mask");
   if (d.bnb_stats && !d.bnb_ymask) {  // (a bit-mask source: the separate statistics pass)
     a.bb_x = d.bnb_x; a.bb_y = d.bnb_y; a.bb_mean = d.bnb_mean; a.bb_invstd = d.bnb_invstd;
     a.bb_gamma = d.bnb_gamma; a.bb_beta = d.bnb_beta; a.bb_act = d.bnb_act;

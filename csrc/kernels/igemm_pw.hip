@@ -446,6 +446,7 @@ bool run_igemm_pipe(const IgemmArgs& g, long Mmax, hipStream_t s) {
   // one epilogue flavour per launch (the combinations no conv issues stay on the per-tile kernel)
   const int epi = g.bb_x ? PW_EPI_BB : g.bn_part ? PW_EPI_STATS : g.accum ? PW_EPI_ACC : PW_EPI_PLAIN;
   if ((g.bb_x || g.bn_part) && g.accum) return false;
+  if (g.acc_src) return false;  // (the masked accumulation source: per-tile kernel only)
   // too few tiles for a persistent grid: the per-tile kernel's split-K spreads them better
   const int bn = pw_cfg(a.N) == 2 ? 64 : 128;
   const long tiles = (Mmax + 127) / 128 * (a.N / bn);

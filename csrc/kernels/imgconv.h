@@ -70,20 +70,7 @@ struct ImgWgradArgs {
   // runs beside other work (MNIST conv2's weight grad on its own graph branch)
   int max_blocks;
   int diag;                 // ablation bits for kernel experiments (DTFE_DIAG iw=<bits>; 0 in production)
-  // 1: leave the per-workgroup partials in ws unsummed (no reduce launch): the fused optimizer
-  // sums them itself (OptPart work items, optim.h); the layout is in imgwgrad_last_layout()
-  int defer_reduce;
 };
-
-// Layout of the partial slabs a weight-gradient launch left in its workspace (recorded by the last
-// launch on this thread that kept them): layout 0 = the persistent kernel's register layout
-// (wp_reduce_kernel: MT x CTW 16-column tiles of f32x4 per wave, then the bias), 1 = plain
-// [nw weights][N biases] slabs (conv1 copies kernel, partials_reduce_kernel).  nblk slabs of plen
-// floats; KC = KH*KW*CS.
-struct WgPartLayout {
-  int layout = -1, nblk = 0, plen = 0, MT = 0, CTW = 0, KC = 0, N = 0, nw = 0;
-};
-WgPartLayout& imgwgrad_last_layout();
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
 void launch_imgconv(const ImgConvArgs& a, hipStream_t s);

@@ -331,12 +331,7 @@ bool launch_conv1_copies_wgrad(const ImgWgradArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(conv1c_wgrad_kernel, dim3(grid), dim3(TH), 0, s, a, diag);
   if (a.ws) {
     constexpr int LEN = NCH * 25 + NCH;
-    if (a.defer_reduce) {
-      WgPartLayout& L = imgwgrad_last_layout();
-      L.layout = 1; L.nblk = grid; L.plen = LEN; L.MT = L.CTW = 0; L.KC = 25; L.N = NCH; L.nw = NCH * 25;
-    } else {
-      launch_partials_reduce(a.ws, grid, LEN, NCH * 25, a.dw, a.db, a.scale, s);
-    }
+    launch_partials_reduce(a.ws, grid, LEN, NCH * 25, a.dw, a.db, a.scale, s);
   }
   return true;
 }

@@ -422,13 +422,8 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, ad, G);
     if (a.ws) {
       const int plen = wp_part_len(MT, CTW, a.N), KC = a.KH * a.KW * a.CS;
-      if (a.defer_reduce) {
-        WgPartLayout& L = imgwgrad_last_layout();
-        L.layout = 0; L.nblk = grid; L.plen = plen; L.MT = MT; L.CTW = CTW; L.KC = KC; L.N = a.N; L.nw = a.N * KC;
-      } else {
-        hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW, KC,
-                           a.N, a.dw, a.db, a.scale);
-      }
+      hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW, KC,
+                         a.N, a.dw, a.db, a.scale);
     }
     return true;
   };
@@ -449,11 +444,6 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
 }
 
 }  // namespace
-
-WgPartLayout& imgwgrad_last_layout() {
-  thread_local WgPartLayout L;
-  return L;
-}
 
 long imgwgrad_ws_floats(int N, int KC) {
   const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 8;  // the wp_launch instances below

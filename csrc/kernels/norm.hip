@@ -566,7 +566,7 @@ void launch_bn_apply(const BnArgs& a, hipStream_t s) {
 
 void check_bwd(const BnArgs& a) {
   check(a);
-  if (a.act != ACT_NONE && !a.y && (a.act != ACT_RELU || !a.gamma || !a.beta))
+  if (a.act != ACT_NONE && !a.y && !(a.ymask && a.act == ACT_RELU) && (a.act != ACT_RELU || !a.gamma || !a.beta))
     throw std::runtime_error("bn_bwd: the activation mask needs y, or (ReLU) gamma and beta");
 }
 

@@ -24,24 +24,10 @@ struct OptSeg {
 };
 
 // Work item: kind 0 = flat range [start, start+count) of segment seg;
-// kind 1 = 64x64 tile (r0, c0) of tap t of segment seg (transpose path);
-// kind 2 = 16 f32x4 (start = first) of partial source t (OptPart): the gradient of those
-// elements is first summed over the source's unreduced weight-gradient slabs - the fold of
-// wp_reduce_kernel / partials_reduce_kernel into the optimizer launch.
+// kind 1 = 64x64 tile (r0, c0) of tap t of segment seg (transpose path).
 struct OptWork {
   int kind, seg, t, r0, c0;
   long start, count;
-};
-
-// Unreduced per-workgroup weight-gradient partials (imgconv.h WgPartLayout): nblk slabs of plen
-// floats at ws; layout 0 = the persistent weight-gradient kernel's register layout (MT x CTW tiles,
-// bias tail), 1 = plain [nw weights][N biases].  The reduced value is added into the gradient
-// buffer g (dW += scale * sum, exactly as the reduce kernels do) and then applied; wseg / bseg:
-// the OptSeg of the weight [N][KC] and bias [N] variables (bseg -1: none).
-struct OptPart {
-  const float* ws;
-  int nblk, plen, layout, MT, CTW, KC, N, nw, wseg, bseg;
-  float scale;
 };
 
 struct OptArgs {
@@ -63,7 +49,6 @@ struct OptArgs {
   const int32_t* rep_gs;
   uint64_t rep_seq, rep_ver;
   int rep_stale;
-  const OptPart* parts;     // kind-2 work items' sources (fp32 gradient path only)
 };
 
 void launch_apply_gradients(const OptArgs& a, hipStream_t s);

@@ -130,90 +130,6 @@ __device__ __forceinline__ void update_vec4x(const OptArgs& a, float lr_t, long 
   }
 }
 
-// apply one element of a segment from its (just reduced) fp32 gradient dwv: the master / slots,
-// the gradient buffer (the reduced value stays observable, as after the reduce kernels) and the
-// bf16 working copies (natural, and transposed [C][T][R])
-template <int KIND>
-__device__ __forceinline__ void apply_elem(const OptArgs& a, float lr_t, const OptSeg& sg, long li, float dwv) {
-  const long i = sg.off + li;
-  const_cast<float*>(a.g)[i] = dwv;
-  const float v = update_one<KIND>(a, lr_t, i, dwv * a.gscale);
-  const bf16 b = f2bf(v);
-  if (sg.w16) sg.w16[li] = b;
-  if (sg.wt16) {
-    const long TC = (long)sg.T * sg.C;
-    const long r = li / TC, rem = li - r * TC, t = rem / sg.C, c = rem - t * sg.C;
-    sg.wt16[(c * sg.T + t) * sg.R + r] = b;
-  }
-}
-
-// kind-2 item: wp_reduce_kernel / partials_reduce_kernel's block (16 f32x4 columns c16, 16 strided
-// slab subsets pg, subsets summed in order through LDS - the same additions in the same order, so
-// the applied gradient is bit-identical to the reduce-then-apply pair), then the update of the
-// <= 64 elements those columns hold
-template <int KIND>
-__device__ void part_item(const OptArgs& a, float lr_t, const OptWork& w, f32x4_t (*red)[17]) {
-  const OptPart pa = a.parts[w.t];
-  const int c16 = threadIdx.x & 15, pg = threadIdx.x >> 4;
-  const int v = (int)w.start + c16;  // f32x4 index within a slab
-  const int nv = (pa.plen + 3) / 4;
-  const int ntile = pa.layout == 0 ? 8 * pa.CTW * pa.MT * 64 : 0;
-  bool live = v < nv;
-  if (pa.layout == 0) live = live && (v >= ntile || ((v >> 6) / pa.MT / pa.CTW * pa.CTW + (v >> 6) / pa.MT % pa.CTW) * 16 < pa.KC);
-  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  if (live) {
-    for (int p0 = pg; p0 < pa.nblk; p0 += 16 * 8) {
-      f32x4_t x[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int p = p0 + 16 * j;
-        x[j] = p < pa.nblk ? *reinterpret_cast<const f32x4_t*>(pa.ws + (long)p * pa.plen + 4 * v) : f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc += x[j];
-    }
-  }
-  red[pg][c16] = acc;
-  __syncthreads();
-  if (pg == 0 && live) {
-    f32x4_t t = red[0][c16];
-#pragma unroll
-    for (int q = 1; q < 16; ++q) t += red[q][c16];
-    const OptSeg& ws = a.segs[pa.wseg];
-    if (pa.layout == 1) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 4 * v + e;
-        if (k < pa.nw) {
-          apply_elem<KIND>(a, lr_t, ws, k, __builtin_fmaf(pa.scale, t[e], a.g[ws.off + k]));
-        } else if (k < pa.plen && pa.bseg >= 0) {
-          const OptSeg& bs = a.segs[pa.bseg];
-          apply_elem<KIND>(a, lr_t, bs, k - pa.nw, __builtin_fmaf(pa.scale, t[e], a.g[bs.off + k - pa.nw]));
-        }
-      }
-    } else if (v < ntile) {
-      const int lane = v & 63, r = v >> 6, mt = r % pa.MT, rc = r / pa.MT, c = rc % pa.CTW, wv = rc / pa.CTW;
-      const int col = (wv * pa.CTW + c) * 16 + (lane & 15), n0 = mt * 16 + (lane >> 4) * 4;
-      if (col < pa.KC) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (n0 + j >= pa.N) continue;
-          const long li = (long)(n0 + j) * pa.KC + col;
-          apply_elem<KIND>(a, lr_t, ws, li, __builtin_fmaf(pa.scale, t[j], a.g[ws.off + li]));
-        }
-      }
-    } else if (pa.bseg >= 0) {
-      const OptSeg& bs = a.segs[pa.bseg];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = (v - ntile) * 4 + j;
-        if (n < pa.N) apply_elem<KIND>(a, lr_t, bs, n, __builtin_fmaf(pa.scale, t[j], a.g[bs.off + n]));
-      }
-    }
-  }
-  __syncthreads();  // (red is reused by the next item)
-}
-
 // One optimizer's share of a launch: workgroups bid = 0..nblk-1 of the grid (the whole grid for a
 // plain launch, a contiguous range of it for a grouped one).
 template <int KIND, bool G16>
@@ -240,8 +156,6 @@ __device__ __forceinline__ void apply_items(const OptArgs& a, int bid, int nblk,
         if (sg.w16b) sg.w16b[li] = f2bf(v);
         if (sg.pb) sg.pb[li] = v;
       }
-    } else if (w.kind == 2) {
-      if constexpr (!G16) part_item<KIND>(a, lr_t, w, reinterpret_cast<f32x4_t(*)[17]>(&tile[0][0]));
     } else {
       // 64x64 tile of tap t: rows r0.., cols c0.. of the [R][C] slice; transposed copy via LDS
       // the 16 elements of a thread are loaded together before any update (the update's stores may

@@ -211,7 +211,6 @@ class MnistCnnTrainer:
         # all-reduce attached are the oracles the fused / split schedule is checked against)
         self.fused_gather = True
         self.late_split = True
-        self.fold_reduces = True   # (test hook: False = reduce kernels + plain apply, the fold's oracle)
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the forward
         # (one 64x64 tile per CU, 49 k-tiles) with two 4-wave k-groups per workgroup, 3 stages each
         # (tile 19: 15.6 us vs 19.9 for one group, torch.mm 21.3 - profiles/r4_fc1_kgroups.txt);
@@ -238,12 +237,9 @@ class MnistCnnTrainer:
         if self.par:
             self.s_c2 = torch.cuda.Stream(device=d)
             self.ws_c2 = torch.empty(ops.wgrad_ws_floats(C2, KS * KS * C1), device=d, dtype=torch.float32)
-            self.ws_c1 = torch.empty(ops.wgrad_ws_floats(C1, KS * KS), device=d, dtype=torch.float32)
-        # one replica: the conv weight gradients' partial sums are left unreduced and the Adam launch
-        # sums them itself (Optimizer.build_fold) - no reduce launches, and the sums run beside the
-        # fc Adam instead of ahead of it
-        self._defer = False
-        self._parts = []
+        # (the conv weight-gradient partial reduces stay their own launches: summing the partial slabs
+        # inside the Adam launch measured 0.2033-0.2042 vs 0.1989-0.1997 ms/step,
+        # profiles/r4_cnn_step_b1024.txt)
 
     def _glds_tile(self, A, Bm, M, N, K, lda, ldb, tile, b_ones_row=-1):
         if self.device.type == "cuda" and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row):
@@ -309,14 +305,10 @@ class MnistCnnTrainer:
         self.schedule.append("conv2_dgrad")
         with torch.cuda.stream(self.s_c2) if self.par else contextlib.nullcontext():
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
-            l2 = ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
-                              workspace=self.ws_c2 if self.par else None,
-                              max_blocks=self.c2_blocks if self.par else 0, defer_reduce=self._defer, **self.ic2)
-        l1 = ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1,
-                          workspace=self.ws_c1 if self._defer else None, defer_reduce=self._defer, **self.ic1)
-        if self._defer:
-            self._parts = [(ws, lay, self.names[w], self.names[b]) for ws, lay, w, b in
-                           ((self.ws_c2, l2, "wc2", "bc2"), (self.ws_c1, l1, "wc1", "bc1")) if lay]
+            ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
+                         workspace=self.ws_c2 if self.par else None,
+                         max_blocks=self.c2_blocks if self.par else 0, **self.ic2)
+        ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
         if self.par:
             main.wait_stream(self.s_c2)
         if self.allreduce is not None:
@@ -378,18 +370,8 @@ class MnistCnnTrainer:
         bf16 gradients to apply instead of P.grad; ``gscale`` defaults to 1/world."""
         gscale = 1.0 / self.world if gscale is None else gscale
         if not self.par or not (self.late_split and self.allreduce is not None):
-            # one replica: fold the conv weight-gradient reduces into the Adam launch (the fold plan
-            # is built on the first, eager, step - never inside a graph capture)
-            fold = (self.par and self.allreduce is None and grad16 is None and self.fold_reduces and
-                    (self.opt._fold is not None or not torch.cuda.is_current_stream_capturing()))
-            self._defer = fold
-            try:
-                self.forward_backward()
-            finally:
-                self._defer = False
-            if fold and self.opt._fold is None:
-                self.opt.build_fold([(ws, lay, w, b, 1.0) for ws, lay, w, b in self._parts])
-            self.opt.step(grad16=grad16, gscale=gscale, fold=fold)
+            self.forward_backward()
+            self.opt.step(grad16=grad16, gscale=gscale)
             return
         self._ensure_split()
         self._late = (grad16, gscale)

@@ -157,9 +157,10 @@ class Conv:
         profiles/r2_resnet50_bn_bwd_fuse_ab.txt.)"""
         return not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0 and self.stride == 1
 
-    def dgrad(self, dy, dx, accumulate=False, bn_bwd=None):
+    def dgrad(self, dy, dx, accumulate=False, bn_bwd=None, acc_src=None):
         """``bn_bwd``: BN.bwd_stats_args of the BatchNorm that consumes dx; returns True when its
-        backward statistics were produced with dx (the BN then skips its statistics pass)."""
+        backward statistics were produced with dx (the BN then skips its statistics pass).
+        ``acc_src``: (src, relu bits) - dx = dgrad + src * bit (ops.conv_dgrad)."""
         if self.img_dgrad:
             assert not accumulate
             ops.imgconv(self.wt, dx, src=dy, flip_taps=True, B=self.B, SH=self.OH, SW=self.OW, CS=self.cout,
@@ -167,7 +168,8 @@ class Conv:
                         pad=self.k - 1 - self.pad, dil=self.dil)
             return False
         fuse = bn_bwd is not None and self.dgrad_fuses_bn(accumulate)
-        ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate, bn_bwd=bn_bwd if fuse else None)
+        ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate, bn_bwd=bn_bwd if fuse else None,
+                       acc_src=acc_src)
         return fuse
 
 
@@ -380,7 +382,10 @@ class Bottleneck:
         # shortcut gradient straight into dx, the conv1 data gradient accumulated on top
         fuse = (dx is not None and self.conv1.can_accum and (not self.proj or self.convs.can_accum)
                 and _SHORTCUT_FUSE)
-        dres = dx if (fuse and not self.proj) else self.dres
+        # identity shortcut: its gradient dout * ReLU'(block output) is added by conv1's data-gradient
+        # epilogue from dout and bn3's bit mask - bn3's backward does not store it at all
+        masked = fuse and not self.proj and self.bn3.use_bits and self.conv1.stride == 1
+        dres = None if masked else (dx if (fuse and not self.proj) else self.dres)
         self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres, stats_done=dout_stats_done)
         self.conv3.wgrad(self.dc3, self.bn2.y)
         done = self.conv3.dgrad(self.dc3, self.dh2, bn_bwd=self.bn2.bwd_stats_args(self.conv2.y))
@@ -402,7 +407,8 @@ class Bottleneck:
                     # bn3 backward statistics into its epilogue
                     self.convs.dgrad(self.dsc, dx)
                     return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
-                return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
+                return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb,
+                                        acc_src=(dout, self.bn3.ybits) if masked else None)
             else:
                 self.conv1.dgrad(self.dc1, dx)
                 if self.proj:

@@ -25,7 +25,7 @@ __all__ = [
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
-    "bn_bwd_apply", "relu_bits", "opt_pack_parts", "shortcut_grad_add",
+    "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
@@ -409,17 +409,16 @@ def wgrad_workspace(device, numel):
 
 
 def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
-             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0, defer_reduce=False):
+             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0):
     """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY.
     On the GPU the persistent kernel stores per-workgroup partials in `workspace`
-    (default: a cached per-device buffer) and a second kernel sums them.  ``defer_reduce``: no
-    second kernel - returns the partials' layout [layout, nblk, plen, MT, CTW, KC, N, nw] for the
-    optimizer to sum them itself (``Optimizer.build_fold``; [] when the launch kept none)."""
+    (default: a cached per-device buffer) and a second kernel sums them."""
     if dw.is_cuda:
         if workspace is None and (CS % 16 == 0 or CS == 1):
             workspace = wgrad_workspace(dw.device, wgrad_ws_floats(N, KH * KW * CS))
-        return list(require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW,
-                                       stride, pad, scale, workspace, max_blocks, defer_reduce))
+        require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
+                           scale, workspace, max_blocks)
+        return
     d = dy.float().view(B, OH, OW, N) if dy is not None else _unpooled_nhwc(dy_pooled, dy_argmax, B, OH, OW, N)
     gw = torch.nn.grad.conv2d_weight(src.float().view(B, SH, SW, CS).permute(0, 3, 1, 2), (N, CS, KH, KW),
                                      d.permute(0, 3, 1, 2), stride=stride, padding=pad)
@@ -451,17 +450,25 @@ def conv1_wgrad_pooled(x, dp, argmax, dw, db, scale=1.0):
     conv_wgrad(dz, x, dw, db, g, scale)
 
 
-def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None, accumulate=False, bn_bwd=None):
+def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None, accumulate=False, bn_bwd=None,
+               acc_src=None):
     """dX of an NHWC conv (wt = W laid out [C][KH][KW][Cout]); optional un-pool epilogue, or a
     ReLU mask (dx = mask > 0 ? dx : 0) when the consumer un-pools itself.  ``accumulate``:
-    dx += dX (implicit-GEMM path: C and Cout multiples of 64).  ``bn_bwd``: the consuming
-    BatchNorm's backward statistics of the final dx, ``(x, y, mean, invstd, gamma, beta, stats,
-    act)`` with ``bn_bwd_stats`` semantics - computed in the implicit-GEMM epilogue (no separate
-    pass over dx and x), or by a statistics pass after the launch."""
+    dx += dX (implicit-GEMM path: C and Cout multiples of 64); with ``acc_src = (src, bits)``
+    dx = dX + src * bit instead (bits: relu_bits layout) - dx's old contents are not read.
+    ``bn_bwd``: the consuming BatchNorm's backward statistics of the final dx, ``(x, y, mean,
+    invstd, gamma, beta, stats, act)`` with ``bn_bwd_stats`` semantics - computed in the
+    implicit-GEMM epilogue (no separate pass over dx and x), or by a statistics pass after the launch."""
     if dx.is_cuda:
         b = bn_bwd or (None,) * 7 + (0,)
-        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask, accumulate, *b)
+        src, bits = acc_src or (None, None)
+        require().conv_dgrad(dy, wt, dx, *_conv_geom_args(g), pooled, argmax, relu_mask, accumulate, *b, src, bits)
         return dx
+    if acc_src is not None:
+        src, bits = acc_src
+        R, C = dx.numel() // dx.shape[-1], dx.shape[-1]
+        dx.copy_((src.float().reshape(R, C) * _unbits(bits, R, C)).reshape(dx.shape).to(dx.dtype))
+        return conv_dgrad(dy, wt, dx, g, pooled, argmax, relu_mask, True, bn_bwd)
     if bn_bwd is not None:
         conv_dgrad(dy, wt, dx, g, pooled, argmax, relu_mask, accumulate)
         x, y, mean, invstd, gamma, beta, stats, act = bn_bwd
@@ -584,17 +591,10 @@ def opt_pack(segs, work, device_like):
 
 
 def apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow, global_step,
-                    gs_inc, done, blob, nseg, nwork, group=0, parts=None):
-    """group: 0 launch now, 1 queue, 2 queue + launch all queued optimizers as one grouped launch.
-    ``parts``: opt_pack_parts table of the plan's kind-2 items (unreduced weight-gradient partials)."""
+                    gs_inc, done, blob, nseg, nwork, group=0):
+    """group: 0 launch now, 1 queue, 2 queue + launch all queued optimizers as one grouped launch."""
     require().apply_gradients(kind, p, g, g16, gscale, s1, s2, lr, beta1, beta2, eps, momentum, rho, beta_pow,
-                              global_step, gs_inc, done, blob, nseg, nwork, group, parts)
-
-
-def opt_pack_parts(ints, scales, device_like):
-    """Device table of OptPart rows (csrc/kernels/optim.h): ints int64 [n, 11] = (ws address, nblk,
-    plen, layout, MT, CTW, KC, N, nw, weight seg, bias seg), scales float64 [n]."""
-    return require().opt_pack_parts(ints, scales, device_like)
+                              global_step, gs_inc, done, blob, nseg, nwork, group)
 
 
 # ------------------------------------------------------------- elementwise

@@ -173,7 +173,6 @@ class Optimizer:
             if cfg.kind == "adam" else None
         self.done = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._blob = None
-        self._fold = None
         if self.device.type == "cuda":
             self._build_plan()
 
@@ -206,52 +205,16 @@ class Optimizer:
         self._blob = ops.opt_pack(torch.tensor(segs, dtype=torch.int64), torch.tensor(work, dtype=torch.int64),
                                   self.P.master)
 
-    def build_fold(self, parts):
-        """A second plan whose weight-gradient variables are summed from their unreduced partial
-        slabs inside the apply (kind-2 work items: the reduce kernels folded into this launch).
-        ``parts``: [(ws tensor, layout list from ops.imgwgrad(defer_reduce=True), weight var,
-        bias var or None, scale)]."""
-        chunk = int(os.environ.get("DTFE_OPT_CHUNK", "8192"))
-        folded = {p[2] for p in parts} | {p[3] for p in parts if p[3] is not None}
-        segs, work = [], []
-        index = {}
-        for si, name in enumerate(self.var_list):
-            index[name] = si
-            s = self.P.spec(name)
-            w16, wt16 = self.P.w16.get(name), self.P.wt16.get(name)
-            R, T, C = s.transpose if s.transpose is not None else (s.numel, 1, 1)
-            segs.append([self.P.offsets[name], R, T, C, w16.data_ptr() if w16 is not None else 0,
-                         wt16.data_ptr() if wt16 is not None else 0])
-            if name in folded:
-                continue
-            if wt16 is not None:
-                work += [[1, si, t, r0, c0, 0, 0] for t in range(T) for r0 in range(0, R, 64) for c0 in range(0, C, 64)]
-            else:
-                work += [[0, si, 0, 0, 0, st, min(chunk, s.numel - st)] for st in range(0, s.numel, chunk)]
-        ints, scales = [], []
-        for pi, (ws, lay, wname, bname, scale) in enumerate(parts):
-            layout, nblk, plen, MT, CTW, KC, N, nw = lay
-            ints.append([ws.data_ptr(), nblk, plen, layout, MT, CTW, KC, N, nw, index[wname],
-                         index[bname] if bname is not None else -1])
-            scales.append(float(scale))
-            work += [[2, 0, pi, 0, 0, v0, 16] for v0 in range(0, (plen + 3) // 4, 16)]
-        blob = ops.opt_pack(torch.tensor(segs, dtype=torch.int64), torch.tensor(work, dtype=torch.int64), self.P.master)
-        ptab = ops.opt_pack_parts(torch.tensor(ints, dtype=torch.int64), torch.tensor(scales, dtype=torch.float64),
-                                  self.P.master)
-        self._fold = (blob, len(segs), len(work), ptab)
-
-    def step(self, grad=None, grad16=None, gscale: float = 1.0, gs_inc: int = 1, group: int = 0, fold: bool = False):
+    def step(self, grad=None, grad16=None, gscale: float = 1.0, gs_inc: int = 1, group: int = 0):
         """Apply gradients (default: the FlatParams grad buffer) to var_list.  ``group`` (GPU):
-        1 queues this apply, 2 queues it and launches every queued one together (``step_all``).
-        ``fold``: the build_fold plan (the folded variables' partials are summed in the apply)."""
+        1 queues this apply, 2 queues it and launches every queued one together (``step_all``)."""
         c = self.cfg
         if grad is None and grad16 is None:
             grad = self.P.grad
         if self.device.type == "cuda":
-            blob, nseg, nwork, parts = self._fold if fold else (self._blob, self.nseg, self.nwork, None)
             ops.apply_gradients(self.kind, self.P.master, grad, grad16, gscale, self.s1, self.s2, c.lr, c.beta1,
                                 c.beta2, c.resolved_eps(), c.momentum, c.rho, self.beta_pow, self.global_step, gs_inc,
-                                self.done, blob, nseg, nwork, group, parts)
+                                self.done, self._blob, self.nseg, self.nwork, group)
             return
         self._step_cpu(grad if grad is not None else grad16.float(), gscale, gs_inc)
 

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r4combo
 mkdir -p $O
-timeout -k 10 700 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_mnist_cnn_gpu.py tests/test_norm_gpu.py tests/test_cluster_gpu.py tests/test_resnet.py -m gpu > $O/pytest.log 2>&1
+timeout -k 10 700 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_mnist_cnn_gpu.py tests/test_norm_gpu.py tests/test_igemm_gpu.py tests/test_cluster_gpu.py tests/test_resnet.py -m gpu > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
 for i in 1 2; do
   timeout -k 10 180 python3 bench.py --steps 200 --warmup 20 > $O/cnn_$i.log 2>&1 || { tail -5 $O/cnn_$i.log; exit 1; }

@@ -110,3 +110,25 @@ def test_igemm_wgrad_scale_and_splits(monkeypatch):
         outs.append(dw.cpu())
     for o in outs:
         assert _rel(o, 0.25 * ref) < 1e-3
+
+
+@pytest.mark.parametrize("B,H,C,Cout", [(4, 14, 256, 64), (2, 7, 512, 128), (3, 9, 64, 64)])
+def test_igemm_dgrad_masked_accumulation_source(B, H, C, Cout):
+    """conv_dgrad(accumulate=True, acc_src=(src, bits)): dx = dgrad + src * bit, dx's old contents
+    never read - equal (bit for bit) to accumulating onto a dx pre-filled with the masked src."""
+    g = _geom(B, H, C, Cout, 1, 1)
+    torch.manual_seed(4)
+    dy = torch.randn(B, H, H, Cout, device=DEV).to(torch.bfloat16)
+    wt = (torch.randn(C, 1, 1, Cout, device=DEV) / Cout ** 0.5).to(torch.bfloat16)
+    src = torch.randn(B, H, H, C, device=DEV).to(torch.bfloat16)
+    y = torch.relu(torch.randn(B, H, H, C, device=DEV)).to(torch.bfloat16)
+    bits = ops.relu_bits(y)
+    dx = torch.full((B, H, H, C), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy, wt, dx, g, accumulate=True, acc_src=(src, bits))
+    ref = torch.where(y > 0, src, torch.zeros_like(src))
+    ops.conv_dgrad(dy, wt, ref, g, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)
+    cpu = torch.empty(B, H, H, C, dtype=torch.bfloat16)
+    ops.conv_dgrad(dy.cpu(), wt.cpu(), cpu, g, accumulate=True, acc_src=(src.cpu(), bits.cpu()))
+    assert (cpu.float() - dx.cpu().float()).abs().max().item() <= 2e-2 * dx.float().abs().max().item()

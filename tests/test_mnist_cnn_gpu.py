@@ -236,34 +236,6 @@ def test_cnn_training_is_bitwise_reproducible(B):
     assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
 
 
-@pytest.mark.parametrize("B", [256, 1024])
-def test_cnn_folded_wgrad_reduces_match_reduce_kernels(B):
-    """One replica's step sums the conv weight-gradient partial slabs inside the Adam launch
-    (kind-2 work items) instead of launching wp_reduce / partials_reduce first: the same additions
-    in the same order, so parameters, Adam slots, bf16 / transposed copies and the gradient buffer
-    stay bit-identical to the reduce-then-apply step over several steps."""
-    from dtfe.models.mnist_cnn import MnistCnnTrainer
-
-    outs = []
-    for fold in (True, False):
-        tr = MnistCnnTrainer(B, "cuda", seed=9)
-        tr.fold_reduces = fold
-        for _ in range(4):
-            tr.step()
-        torch.cuda.synchronize()
-        assert (tr.opt._fold is not None) == fold
-        n = tr.names
-        outs.append(dict(master=tr.P.master.clone(), grad=tr.P.grad.clone(), s1=tr.opt.s1.clone(),
-                         s2=tr.opt.s2.clone(), w16=tr.P.w16[n["wc2"]].clone(), wt16=tr.P.wt16[n["wc2"]].clone(),
-                         w1=tr.P.w16[n["wc1"]].clone(), gs=int(tr.global_step.item())))
-    a, b = outs
-    for k in a:
-        if k == "gs":
-            assert a[k] == b[k] == 4
-        else:
-            assert torch.equal(a[k], b[k]), (k, float((a[k].float() - b[k].float()).abs().max()))
-
-
 def test_cnn_evaluate_matches_argmax_agreement():
     """CnnProgram.evaluate (the Test-Accuracy line) = argmax agreement of the no-dropout forward
     with fp32 autograd's logits on a fixed batch, including a padded last chunk."""
