@@ -931,6 +931,8 @@ template <int BM, int BN>
 void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
   a.tiles_m = (int)((Mmax + BM - 1) / BM);
   dim3 grid(a.tiles_m * (a.N / BN), a.splits, a.nphase);
+  // (a 32-deep-k-tile, 4-stage ring variant in the same 64 KB measured 12 % slower per conv pass:
+  // profiles/r4_igemm_kb32_ab.txt)
   int nk_max = 0;
   for (int p = 0; p < a.nphase; ++p) nk_max = std::max(nk_max, a.ph[p].ntaps * (a.SC / IG_BK));
   // (a 1-stage, 3-workgroups-per-CU instance for the one-k-tile 1x1 convs measured 15-25 % slower
