@@ -8,6 +8,7 @@
 // the [2][C] accumulators with one atomic per channel and workgroup.
 #include "norm.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace dtfe {
@@ -347,10 +348,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
 // Statistics kernels: few enough workgroups that the per-channel atomics stay cheap
 // (about 2 per CU), each looping over U_STATS-row batches.  Apply kernels: one U_APPLY-row
 // batch per thread, as many workgroups as that takes (no atomics to amortise).
+// Workgroup cap: every workgroup adds 2C atomics, and with 512 of them those serialized adds were a
+// visible part of the small layers' time.  ResNet-50 B=256 sweep (profiles/r4_bn_stats_grid.txt):
+// 256 beats 512 on every shape, 128 is better still below ~64 MB of activations and worse above.
 int stats_grid(long R, int C) {
   const long rows_per_block = (long)(NT / (C / 8)) * U_STATS;
   long g = (R + rows_per_block - 1) / rows_per_block;
-  if (g > 512) g = 512;
+  const long cap = R * C * 2 <= (64L << 20) ? 128 : 256;
+  if (g > cap) g = cap;
   return g < 1 ? 1 : (int)g;
 }
 
