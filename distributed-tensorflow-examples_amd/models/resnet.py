@@ -139,10 +139,11 @@ class Conv:
         ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats)
         return self.y, stats is not None
 
-    def wgrad(self, dy, x):
+    def wgrad(self, dy, x, after=None):
+        """``after``: the side stream's fork point (SideStream.fork_point, taken when dy was final)."""
         side = getattr(self, "side", None)
         if side is not None and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0:
-            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g))
+            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g), after)
             return
         if self.img_wgrad:
             ops.imgwgrad(x, self.gw, None, dy=dy, **self.ic)
@@ -185,13 +186,23 @@ class SideStream:
     their own workspace (igemm.hip ``g_wg``), so the two streams never share scratch memory."""
 
     def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)
+        # high-priority queue: the weight gradients are the step's tail once the data-gradient chain
+        # no longer waits on them (11,260 vs 11,234-11,251 img/s, profiles/r4_resnet50_graph_order.txt)
+        self.stream = torch.cuda.Stream(device=device, priority=-1)
         self.pending = False
 
-    def run(self, fn):
+    @staticmethod
+    def fork_point():
+        """An event on the current stream now: a later ``run(fn, after=...)`` depends on exactly the
+        work before this point, though it is launched after the main stream's next kernels."""
         ev = torch.cuda.Event()
         ev.record()
-        self.stream.wait_event(ev)
+        return ev
+
+    def run(self, fn, after=None):
+        if after is None:
+            after = self.fork_point()
+        self.stream.wait_event(after)
         with torch.cuda.stream(self.stream):
             fn()
         self.pending = True
@@ -386,18 +397,28 @@ class Bottleneck:
         # epilogue from dout and bn3's bit mask - bn3's backward does not store it at all
         masked = fuse and not self.proj and self.bn3.use_bits and self.conv1.stride == 1
         dres = None if masked else (dx if (fuse and not self.proj) else self.dres)
+        # Capture order: each data gradient BEFORE the weight gradient forked at the same point (the
+        # fork event is taken when dy is final).  The hipGraph executor keeps a node's first-captured
+        # child on its queue; with the weight gradient captured first, the data-gradient chain kept
+        # landing on the side queue behind the weight gradients - 13 stalls, ~1.5 ms per step
+        # (profiles/r4_resnet50_graph_order.txt)
+        fork = SideStream.fork_point
         self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres, stats_done=dout_stats_done)
-        self.conv3.wgrad(self.dc3, self.bn2.y)
+        ev = fork()
         done = self.conv3.dgrad(self.dc3, self.dh2, bn_bwd=self.bn2.bwd_stats_args(self.conv2.y))
+        self.conv3.wgrad(self.dc3, self.bn2.y, after=ev)
         self.bn2.bwd(self.dh2, self.conv2.y, self.dc2, stats_done=done)
-        self.conv2.wgrad(self.dc2, self.bn1.y)
+        ev = fork()
         done = self.conv2.dgrad(self.dc2, self.dh1, bn_bwd=self.bn1.bwd_stats_args(self.conv1.y))
+        self.conv2.wgrad(self.dc2, self.bn1.y, after=ev)
         self.bn1.bwd(self.dh1, self.conv1.y, self.dc1, stats_done=done)
-        self.conv1.wgrad(self.dc1, self.x)
+        ev1 = fork()
+        evs = None
         if self.proj:
             self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
-            self.convs.wgrad(self.dsc, self.x)
+            evs = fork()
         nb = next_bn[0].bwd_stats_args(next_bn[1]) if next_bn is not None else None
+        ret = None
         if dx is not None:
             if fuse:
                 if self.proj:
@@ -406,9 +427,10 @@ class Bottleneck:
                     # the LAST producer of dx covers every pixel, so it can fold the previous block's
                     # bn3 backward statistics into its epilogue
                     self.convs.dgrad(self.dsc, dx)
-                    return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
-                return self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb,
-                                        acc_src=(dout, self.bn3.ybits) if masked else None)
+                    ret = self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb)
+                else:
+                    ret = self.conv1.dgrad(self.dc1, dx, accumulate=True, bn_bwd=nb,
+                                           acc_src=(dout, self.bn3.ybits) if masked else None)
             else:
                 self.conv1.dgrad(self.dc1, dx)
                 if self.proj:
@@ -416,6 +438,10 @@ class Bottleneck:
                     ops.shortcut_grad_add(self.dxs, dx, 1)
                 else:
                     ops.shortcut_grad_add(self.dres, dx, 1)
+        self.conv1.wgrad(self.dc1, self.x, after=ev1)
+        if self.proj:
+            self.convs.wgrad(self.dsc, self.x, after=evs)
+        return ret
 
 
 class Dense:
