@@ -45,6 +45,8 @@ def main():
                                      keep=t.keep, seed=2, counter=t.data_ctr), fc1_flops),
         "head": (lambda: ops.head_xent(t.h, t.w["out"], t.b["bout"], t.labels, t.dzf, t.dl, t.loss_sum,
                                        t.correct, None, scale=1.0 / B, inv_keep=1.0 / t.keep), 0),
+        "head_noacc": (lambda: ops.head_xent(t.h, t.w["out"], t.b["bout"], t.labels, t.dzf, t.dl, None, None, None,
+                                             scale=1.0 / B, inv_keep=1.0 / t.keep), 0),
         "head_wgrad": (lambda: ops.gemm(t.dl, t.h, t.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=16,
                                         bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=t.gw["bout"],
                                         atomic=True, splits=max(1, min(16, B // 128)), tile=4), 0),

@@ -398,7 +398,8 @@ void transpose_taps_f32(const Tensor& in, const Tensor& out, int64_t O, int64_t 
 // ------------------------------------------------------------------- head
 void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, const Tensor& labels, const Tensor& dz,
                const Tensor& dl, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
-               const optional<Tensor>& logits, double scale, double inv_keep, const optional<Tensor>& step_counter) {
+               const optional<Tensor>& logits, double scale, double inv_keep, const optional<Tensor>& step_counter,
+               const optional<Tensor>& parts) {
   check_cuda(h, "h");
   TORCH_CHECK(dl.scalar_type() == at::kBFloat16 && dl.dim() == 2, "head_xent: dl must be bf16 [B][ld]");
   dtfe::HeadArgs a{};
@@ -417,11 +418,17 @@ void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, cons
     TORCH_CHECK(step_counter->scalar_type() == at::kLong && step_counter->is_cuda(), "head_xent: int64 step_counter");
     a.step_counter = step_counter->data_ptr<int64_t>();
   }
+  if (parts.has_value() && parts->defined()) {
+    TORCH_CHECK(parts->scalar_type() == at::kFloat && parts->is_cuda() && parts->numel() >= 2 * ((a.B + 3) / 4),
+                "head_xent: parts must be fp32 [>= 2 * ceil(B / 4)]");
+    a.parts = parts->data_ptr<float>();
+  }
   dtfe::launch_head_xent(a, cur_stream());
 }
 
 void head_wgrad(const Tensor& dl, const Tensor& h, const Tensor& dw, const optional<Tensor>& db, int64_t nc,
-                double scale) {
+                double scale, const optional<Tensor>& parts, const optional<Tensor>& loss_sum,
+                const optional<Tensor>& correct) {
   check_cuda(h, "h");
   TORCH_CHECK(dl.scalar_type() == at::kBFloat16 && h.scalar_type() == at::kBFloat16 && dl.dim() == 2 && h.dim() == 2,
               "head_wgrad: bf16 dl [B][ld] and h [B][K]");
@@ -440,6 +447,14 @@ void head_wgrad(const Tensor& dl, const Tensor& h, const Tensor& dw, const optio
     a.db = db->data_ptr<float>();
   }
   a.scale = (float)scale;
+  if (parts.has_value() && parts->defined()) {
+    TORCH_CHECK(parts->scalar_type() == at::kFloat && parts->is_cuda() && parts->numel() >= 2 * ((a.B + 3) / 4),
+                "head_wgrad: parts must be fp32 [>= 2 * ceil(B / 4)] (head_xent's)");
+    TORCH_CHECK(loss_sum.has_value() && loss_sum->scalar_type() == at::kFloat && correct.has_value() &&
+                correct->scalar_type() == at::kInt, "head_wgrad: parts need fp32 loss_sum and int32 correct");
+    a.parts = parts->data_ptr<float>(); a.nparts = (a.B + 3) / 4;
+    a.loss_sum = loss_sum->data_ptr<float>(); a.correct = correct->data_ptr<int32_t>();
+  }
   dtfe::launch_head_wgrad(a, cur_stream());
 }
 
@@ -968,8 +983,9 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl,"
       " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep,"
-      " Tensor(f!)? step_counter=None) -> ()");
-  m.def("head_wgrad(Tensor dl, Tensor h, Tensor(a!) dw, Tensor(b!)? db, int nc, float scale) -> ()");
+      " Tensor(f!)? step_counter=None, Tensor(g!)? parts=None) -> ()");
+  m.def("head_wgrad(Tensor dl, Tensor h, Tensor(a!) dw, Tensor(b!)? db, int nc, float scale, Tensor? parts=None,"
+        " Tensor(c!)? loss_sum=None, Tensor(d!)? correct=None) -> ()");
   m.def("gemm_group(Tensor anchor, bool begin) -> ()");
   m.def("opt_pack(Tensor segs, Tensor work, Tensor device_like) -> Tensor");
   m.def(

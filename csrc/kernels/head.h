@@ -17,6 +17,12 @@ struct HeadArgs {
   // counter of the fused MNIST step, whose readers (the conv1 gather, fc1 dropout) all run
   // before this kernel: one plain increment instead of a grid-wide last-arriver atomic
   int64_t* step_counter;
+  // optional: per-workgroup partials instead of the loss / hit atomics - workgroup g stores its
+  // loss sum at parts[g] and its hit count at parts[gridDim.x + g] ((B + 3) / 4 workgroups); the
+  // head weight gradient's bias workgroup folds them into loss_sum / correct (HeadWgradArgs.parts).
+  // 256 same-address atomics per launch cost ~2.5 us of the kernel's 7.8 (bench/cnn_kernels.py
+  // head vs head_noacc); the fold is also a fixed-order, bitwise-reproducible sum.
+  float* parts;
 };
 
 void launch_head_xent(const HeadArgs& a, hipStream_t s);
@@ -30,8 +36,32 @@ struct HeadWgradArgs {
   float* dw; int ldw;          // [NC][ldw]
   float* db;                   // [NC] (optional)
   float scale;
+  // optional: head_xent's per-workgroup loss / hit partials (2 x nparts floats), summed in a fixed
+  // order by the bias workgroup and added to loss_sum / correct (one plain read-modify-write)
+  const float* parts; int nparts; float* loss_sum; int32_t* correct;
 };
 void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s);
+
+// Bias workgroup: loss_sum += sum(parts[0:n]), correct += sum(parts[n:2n]) (wave 0, lane-strided
+// partial sums, then a butterfly: lane 0's total has a fixed summation order)
+__device__ __forceinline__ void head_fold_parts(const HeadWgradArgs& a) {
+  if (!a.parts || threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  float l = 0.f, c = 0.f;
+  for (int i = lane; i < a.nparts; i += 64) {
+    l += a.parts[i];
+    c += a.parts[a.nparts + i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    l += __shfl_xor(l, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if (lane == 0) {
+    *a.loss_sum += l;
+    *a.correct += (int)c;
+  }
+}
 
 // Workgroup `bid` (256 threads) of the head weight gradient: columns 8*bid..+7 of dW for the whole
 // batch (bid == K/8: the bias); red: 4 x 80 floats of LDS.  See head.hip.
@@ -100,6 +130,7 @@ __device__ __forceinline__ void head_wgrad_body(const HeadWgradArgs& a, int bid,
     if (!bias_blk) a.dw[(long)n * a.ldw + col0 + e] = s * a.scale;
     else if (e == 0) a.db[n] = s * a.scale;
   }
+  if (bias_blk) head_fold_parts(a);
 }
 
 // The grouped fc-backward launch's head piece (gemm_dense.hip): 4 columns of dW per workgroup
@@ -169,6 +200,7 @@ __device__ __forceinline__ void head_wgrad4_body(const HeadWgradArgs& a, int bid
     if (!bias_blk) a.dw[(long)n * a.ldw + col0 + e] = s * a.scale;
     else if (e == 0) a.db[n] = s * a.scale;
   }
+  if (bias_blk) head_fold_parts(a);
 }
 
 }  // namespace dtfe

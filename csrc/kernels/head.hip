@@ -111,8 +111,15 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (a.loss_sum) atomicAdd(a.loss_sum, red_loss[0] + red_loss[1] + red_loss[2] + red_loss[3]);
-    if (a.correct) atomicAdd(a.correct, red_correct[0] + red_correct[1] + red_correct[2] + red_correct[3]);
+    const float l = red_loss[0] + red_loss[1] + red_loss[2] + red_loss[3];
+    const int c = red_correct[0] + red_correct[1] + red_correct[2] + red_correct[3];
+    if (a.parts) {  // folded by the head weight gradient's bias workgroup (head.h)
+      a.parts[blockIdx.x] = l;
+      a.parts[gridDim.x + blockIdx.x] = (float)c;
+    } else {
+      if (a.loss_sum) atomicAdd(a.loss_sum, l);
+      if (a.correct) atomicAdd(a.correct, c);
+    }
   }
 }
 
@@ -145,6 +152,8 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(HeadWgradArgs a) {
 void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s) {
   if (a.NC != 10 || a.K % 8 || a.ld_dl < 16 || a.ld_dl % 8 || a.ldh % 8 || a.B > 1024)
     throw std::runtime_error("head_wgrad: needs NC=10, K % 8 == 0, 16-B aligned dl rows of >= 16 and h rows, B <= 1024");
+  if (a.parts && (!a.db || !a.loss_sum || !a.correct))
+    throw std::runtime_error("head_wgrad: folding the loss partials needs db (the bias workgroup), loss_sum and correct");
   if (glds_group_record_head(a)) return;  // recorded into a grouped launch (gemm_dense.hip)
   const int blocks = a.K / 8 + (a.db ? 1 : 0);
   if (a.B <= 256) hipLaunchKernelGGL((head_wgrad_kernel<10, 1>), dim3(blocks), dim3(256), 0, s, a);

@@ -222,6 +222,10 @@ class MnistCnnTrainer:
         # head weight gradient: the dedicated whole-batch kernel up to B = 1024, above that a split-K
         # GEMM with the deterministic last-arriver combine (own workspace: it runs in the group)
         self.head_gemm = batch > 1024
+        # head_xent's per-workgroup loss / hit partials, folded by the head weight gradient's bias
+        # workgroup instead of 256 same-address atomics (0.1943-0.1961 vs 0.1952-0.1985 ms/step,
+        # profiles/r4_cnn_head_parts_ab.txt)
+        self.head_parts = None if self.head_gemm else torch.zeros(2 * ((B + 3) // 4), device=d, dtype=torch.float32)
         self.head_splits = max(1, min(16, B // 128))
         bm, bn = ops.TILE_DIMS[4]
         ntiles = -(-NCLS // bm) * -(-(FC + 1) // bn)
@@ -277,7 +281,8 @@ class MnistCnnTrainer:
                  keep=keep, seed=self.seed + 2, counter=self.data_ctr, tile=self.t_fwd)
         ops.head_xent(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf, self.dl, self.loss_sum,
                       self.correct, logits, scale=1.0 / B, inv_keep=1.0 / keep,
-                      step_counter=self.data_ctr if fused else None)
+                      step_counter=self.data_ctr if fused else None,
+                      parts=self.head_parts)
 
     def forward_backward(self):
         B = self.B
@@ -329,7 +334,10 @@ class MnistCnnTrainer:
                      lda=self.dl.shape[1], bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],
                      splits=self.head_splits, tile=4, workspace=self.ws_head)
         else:
-            ops.head_wgrad(self.dl, self.h, self.gw["out"], self.gw["bout"], NCLS)  # B <= 1024
+            # B <= 1024; its bias workgroup also folds head_xent's loss / hit partials into
+            # loss_sum / correct (256 same-address atomics cost ~2.5 us of head_xent's 7.8)
+            ops.head_wgrad(self.dl, self.h, self.gw["out"], self.gw["bout"], NCLS, parts=self.head_parts,
+                           loss_sum=self.loss_sum, correct=self.correct)
 
     def _fc1_wgrad(self, B, K1):
         """fc1 wgrad: dW[1024][3136] = dZf^T . P2 ; bias grad = sum dZf via the ones column."""

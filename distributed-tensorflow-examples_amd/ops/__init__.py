@@ -528,12 +528,15 @@ def transpose_taps_f32(w, out, O, T, C):
 
 
 # -------------------------------------------------------------------- head
-def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0, step_counter=None):
+def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0, step_counter=None,
+              parts=None):
     """Per-row classifier head: logits, softmax-xent (loss/correct sums), dlogit rows (bf16 [B][ld] into
     ``dl``) and dZ = (dlogit . W) * inv_keep * (h > 0).  dW/db come from a wgrad GEMM over ``dl``.
-    ``step_counter`` (int64 [1], optional) is advanced by one."""
+    ``step_counter`` (int64 [1], optional) is advanced by one.  ``parts`` (fp32 [>= 2 * ceil(B/4)],
+    optional): the loss / hit sums of each 4-row workgroup are stored there instead of being added
+    to ``loss_sum`` / ``correct``; ``head_wgrad(..., parts=...)`` folds them in (no atomics)."""
     if h.is_cuda:
-        require().head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits, scale, inv_keep, step_counter)
+        require().head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits, scale, inv_keep, step_counter, parts)
         return
     if step_counter is not None:
         step_counter += 1
@@ -543,10 +546,18 @@ def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0
         logits.copy_(lg)
     lse = torch.logsumexp(lg, dim=1)
     lab = labels.long()
-    if loss_sum is not None:
-        loss_sum += (lse - lg.gather(1, lab[:, None])[:, 0]).sum()
-    if correct is not None:
-        correct += (lg.argmax(1) == lab).sum().to(correct.dtype)
+    rows = lse - lg.gather(1, lab[:, None])[:, 0]
+    hits = (lg.argmax(1) == lab).float()
+    if parts is not None:
+        n = (len(lab) + 3) // 4
+        pad = 4 * n - len(lab)
+        parts[:n] = torch.nn.functional.pad(rows, (0, pad)).view(n, 4).sum(1)
+        parts[n:2 * n] = torch.nn.functional.pad(hits, (0, pad)).view(n, 4).sum(1)
+    else:
+        if loss_sum is not None:
+            loss_sum += rows.sum()
+        if correct is not None:
+            correct += hits.sum().to(correct.dtype)
     p = torch.softmax(lg, dim=1)
     p[torch.arange(len(lab)), lab] -= 1
     d = p * scale
@@ -556,16 +567,22 @@ def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0
     dz.copy_(g.to(dz.dtype))
 
 
-def head_wgrad(dl, h, dw, db, nc, scale=1.0):
+def head_wgrad(dl, h, dw, db, nc, scale=1.0, parts=None, loss_sum=None, correct=None):
     """Classifier-head weight / bias gradient, stored: dw[c][:K] = scale * sum_b dl[b][c] h[b][:],
-    db[c] = scale * sum_b dl[b][c] (one workgroup per 8 columns over the whole batch, fixed order)."""
+    db[c] = scale * sum_b dl[b][c] (one workgroup per 8 columns over the whole batch, fixed order).
+    ``parts``: head_xent's per-workgroup loss / hit partials, summed by the bias workgroup into
+    ``loss_sum`` / ``correct`` (needs ``db``)."""
     if h.is_cuda:
-        require().head_wgrad(dl, h, dw, db, nc, scale)
+        require().head_wgrad(dl, h, dw, db, nc, scale, parts, loss_sum, correct)
         return
     d = dl[:, :nc].float()
     dw[:, : h.shape[1]] = (scale * (d.t() @ h.float())).to(dw.dtype)
     if db is not None:
         db.copy_((scale * d.sum(0)).to(db.dtype))
+    if parts is not None:
+        n = (h.shape[0] + 3) // 4
+        loss_sum += parts[:n].sum()
+        correct += parts[n:2 * n].sum().to(correct.dtype)
 
 
 @contextlib.contextmanager

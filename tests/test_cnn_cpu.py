@@ -5,7 +5,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from dtfe import train
+from dtfe import ops, train
 from dtfe.models.mnist_cnn import MnistCnnModel
 from dtfe.utils import flags as flagmod
 
@@ -142,3 +142,23 @@ def test_bucket_mb_boundaries():
     for bad in (0, -2):
         with pytest.raises(ValueError):
             train._buckets(_P(), bad)
+
+
+def test_head_loss_partials_cpu_semantics():
+    """CPU path of head_xent(parts=) + head_wgrad(parts=): 4-row workgroup sums, folded into the
+    accumulators by the weight-gradient call - the same totals as the direct accumulation."""
+    torch.manual_seed(3)
+    B, K, NC = 30, 64, 10
+    h = torch.relu(torch.randn(B, K))
+    w = torch.randn(NC, K) * 0.1
+    labels = torch.randint(0, NC, (B,), dtype=torch.int32)
+    args = lambda: (torch.empty(B, K), torch.empty(B, 16))  # noqa: E731
+    loss_a, corr_a = torch.zeros(1), torch.zeros(1, dtype=torch.int32)
+    ops.head_xent(h, w, None, labels, *args(), loss_a, corr_a, scale=1.0 / B)
+    parts = torch.zeros(2 * ((B + 3) // 4))
+    loss, corr = torch.ones(1), torch.ones(1, dtype=torch.int32)
+    dz, dl = args()
+    ops.head_xent(h, w, None, labels, dz, dl, loss, corr, scale=1.0 / B, parts=parts)
+    assert float(loss) == 1.0 and int(corr) == 1
+    ops.head_wgrad(dl, h, torch.empty(NC, K), torch.empty(NC), NC, parts=parts, loss_sum=loss, correct=corr)
+    assert abs(float(loss) - 1.0 - float(loss_a)) < 1e-5 and int(corr) - 1 == int(corr_a)

@@ -337,6 +337,43 @@ def test_head_wgrad_matches_fp32(B):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)   # fixed summation order
 
 
+@pytest.mark.parametrize("B,grouped", [(1024, True), (1024, False), (301, False)])
+def test_head_loss_partials_fold(B, grouped):
+    """head_xent's per-workgroup loss / hit partials folded by the head weight gradient's bias
+    workgroup == the atomic accumulation; the fold is bitwise reproducible.  (grouped: through a
+    gemm_group holding only the head piece - the one-by-one fallback; the fused grouped launch is
+    covered by the MNIST CNN step tests' loss checks.)"""
+    torch.manual_seed(12)
+    K, NC = 1024, 10
+    h = torch.relu(torch.randn(B, K)).to(DEV, torch.bfloat16)
+    w = (torch.randn(NC, K) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(NC, device=DEV)
+    labels = torch.randint(0, NC, (B,), dtype=torch.int32, device=DEV)
+    dz = torch.empty(B, K, device=DEV, dtype=torch.bfloat16)
+    dl = torch.empty(B, 16, device=DEV, dtype=torch.bfloat16)
+    dw = torch.empty(NC, K, device=DEV)
+    db = torch.empty(NC, device=DEV)
+    loss_a = torch.full((1,), 3.0, device=DEV)
+    corr_a = torch.full((1,), 5, dtype=torch.int32, device=DEV)
+    ops.head_xent(h, w, b, labels, dz, dl, loss_a, corr_a, scale=1.0 / B)
+    parts = torch.full((2 * ((B + 3) // 4),), float("nan"), device=DEV)
+    outs = []
+    for _ in range(2):
+        loss = torch.full((1,), 3.0, device=DEV)
+        corr = torch.full((1,), 5, dtype=torch.int32, device=DEV)
+        ops.head_xent(h, w, b, labels, dz, dl, loss, corr, scale=1.0 / B, parts=parts)
+        assert float(loss) == 3.0 and int(corr) == 5   # untouched until the fold
+        if grouped:
+            with ops.gemm_group(dz):
+                ops.head_wgrad(dl, h, dw, db, NC, parts=parts, loss_sum=loss, correct=corr)
+        else:
+            ops.head_wgrad(dl, h, dw, db, NC, parts=parts, loss_sum=loss, correct=corr)
+        outs.append((loss.clone(), corr.clone()))
+    assert int(outs[0][1]) == int(corr_a)
+    assert abs(float(outs[0][0]) - float(loss_a)) < 1e-4 * abs(float(loss_a))
+    assert torch.equal(outs[0][0], outs[1][0])   # fixed summation order
+
+
 def _plan(n, dev):
     segs = torch.tensor([[0, n, 1, 1, 0, 0]], dtype=torch.int64)
     work = torch.tensor([[0, 0, 0, 0, 0, 0, n]], dtype=torch.int64)
