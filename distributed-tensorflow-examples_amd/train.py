@@ -352,6 +352,10 @@ def run_worker_ps(flags, model, server, device, log):
             acc = prog.evaluate(torch.from_numpy(data.test.images[:test_len]).to(device),
                                 torch.from_numpy(data.test.labels[:test_len]).to(device))
             log("Test-Accuracy: %2.4f" % acc)
+        # the chief's checkpoint / step-counter threads talk to the ps: join them before the done
+        # message (the last done makes the ps quit, and a save started after it fails on a closed
+        # connection)
+        sv.stop()
         client.done()
     finally:
         hb.stop()
