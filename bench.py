@@ -15,7 +15,8 @@ code; rank 0's JSON line is the result.  Every rank asserts WORLD_SIZE == --gpus
 
 Weak scaling: every rank trains --batch_size images per step (global batch =
 batch_size * N).  Synthetic MNIST-shaped data resident in HBM, random-init
-weights.  The timed region is exactly K full training steps (device-side batch
+weights.  Before the W warmup steps, --prewarm_ms (150) of training steps bring the
+GPU clocks up (reported as config.prewarm; see timed()).  The timed region is exactly K full training steps (device-side batch
 sampling, forward, backward, gradient all-reduce, fused Adam), bracketed by
 barrier + device synchronize on both sides; the reported time is the MAX over
 ranks.  The K steps are also cut into up to 5 windows by hipEvents recorded
@@ -52,6 +53,9 @@ def parse_args(argv=None):
                     "or WORLD_SIZE under torchrun")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--prewarm_ms", type=float, default=150.0,
+                    help="before the W warmup steps, replay training steps for this long (GPU clock ramp; "
+                         "reported as config.prewarm); 0 disables")
     ap.add_argument("--batch_size", type=int, default=None, help="per-GPU batch (default: per model)")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--bucket_mb", type=float, default=None,
@@ -171,9 +175,26 @@ def replicas_identical(params, d: Dist):
     return bool(float(diff.item()) == 0.0)
 
 
-def timed(runner, steps: int, warmup: int, d: Dist):
-    """W untimed steps, then exactly K steps between barrier+sync brackets.  Returns
-    (elapsed_s max over ranks, per-window ms/step list measured on this rank)."""
+def timed(runner, steps: int, warmup: int, d: Dist, prewarm_ms: float = 0.0):
+    """Pre-warm, W untimed steps, then exactly K steps between barrier+sync brackets.  Returns
+    (elapsed_s max over ranks, per-window ms/step list measured on this rank, pre-warm steps).
+
+    Pre-warm: full training steps, replayed in chunks of 10 until ``prewarm_ms`` have passed
+    (the rank-max elapsed time decides, so every rank runs the same steps).  An idle MI355X
+    ramps its clocks over the first tens of ms of load: with the driver's W=5 / K=20 CNN run
+    (1 + 4 ms of GPU work) the timed windows fell from 0.212 to 0.204 ms/step, after 100
+    untimed steps they sat at 0.195-0.196 (profiles/r4_cnn_clock_ramp.txt).  The pre-warm
+    steps are real steps (they train the model) and are reported in the JSON config."""
+    pre = 0
+    if prewarm_ms > 0:
+        t = time.perf_counter()
+        while True:
+            for _ in range(10):
+                runner()
+            pre += 10
+            torch.cuda.synchronize()
+            if d.max(time.perf_counter() - t) * 1000.0 >= prewarm_ms:
+                break
     for _ in range(warmup):
         runner()
     torch.cuda.synchronize()
@@ -195,7 +216,7 @@ def timed(runner, steps: int, warmup: int, d: Dist):
     torch.cuda.synchronize()
     elapsed = d.max(time.perf_counter() - t0)
     win = [evs[i].elapsed_time(evs[i + 1]) / max(1, cuts[i + 1] - cuts[i]) for i in range(nwin)]
-    return elapsed, win
+    return elapsed, win, pre
 
 
 def _baseline(n_gpus, batch, model="mnist_cnn"):
@@ -291,14 +312,14 @@ def bench_cnn(args, d: Dist):
     # the whole step (with the overlapped all-reduce at world > 1) is one hipGraph replay
     runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
                                                 and graphs_enabled()), capture_error_mode="thread_local")
-    elapsed, win = timed(runner, args.steps, args.warmup, d)
+    elapsed, win, pre = timed(runner, args.steps, args.warmup, d, args.prewarm_ms)
     if comm is not None and hasattr(comm, "check_health"):
         comm.check_health()
     loss = float(trainer.loss_sum.item()) / B
     same = replicas_identical(trainer.P.master, d) if d.world > 1 else None
     ndev = d.distinct_devices()
     extra = {"optimizer": "adam (TF1)", "hip_graph": runner.graph is not None, "last_loss": round(loss, 4),
-             "replicas_identical": same, "distinct_gpus": ndev}
+             "replicas_identical": same, "distinct_gpus": ndev, "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
     extra.update(_comm_info(args, d, comm))
     _emit(d, args, "images/sec (whole node), MNIST CNN sync all-reduce", B * d.world * args.steps / elapsed,
           elapsed, win, "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(),
@@ -363,13 +384,13 @@ def bench_resnet(args, d: Dist):
 
     runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
                                                 and graphs_enabled()), capture_error_mode="thread_local")
-    elapsed, win = timed(runner, args.steps, args.warmup, d)
+    elapsed, win, pre = timed(runner, args.steps, args.warmup, d, args.prewarm_ms)
     # trainable variables only: BN moving statistics are per-replica (each rank's own batches)
     train_vals = torch.cat([prog.P.view(n).reshape(-1) for n in names])
     same = replicas_identical(train_vals, d) if d.world > 1 else None
     extra = {"optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None,
              "last_loss": round(float(prog.loss.item()) / B, 4), "replicas_identical": same,
-             "distinct_gpus": d.distinct_devices()}
+             "distinct_gpus": d.distinct_devices(), "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
     extra.update(_comm_info(args, d, comm))
     _emit(d, args, "images/sec (whole node), %s sync all-reduce" % args.model, B * d.world * args.steps / elapsed,
           elapsed, win, "%s (%d params)" % (args.model, model.num_params()), B, extra,
@@ -466,7 +487,7 @@ def bench_ps(args):
         def max(x):
             return wsum(x, dist.ReduceOp.MAX)
 
-    elapsed, win = timed(run1, args.steps, args.warmup, _D)
+    elapsed, win, pre = timed(run1, args.steps, args.warmup, _D, args.prewarm_ms)
     gs = link.host_reply()
     link.check()
     loss = float(tr.loss_sum.item()) / B
@@ -474,13 +495,14 @@ def bench_ps(args):
     client.done()
     stats = json.loads(server.store.get("dtfe/bench/ps_stats").decode()) if idx == 0 else None
     if idx == 0:
-        pushes = N * (args.steps + args.warmup)  # every runner() call is exactly one step (one push)
+        pushes = N * (args.steps + args.warmup + pre)  # every runner() call is exactly one step (one push)
         rec_extra = {"optimizer": "adam (TF1), applied on the ps", "hip_graph": runner.graph is not None,
                      "last_loss": round(loss, 4), "global_step": gs, "ps_applies": stats.get("applies"),
                      "ps_bucket_applies": stats.get("bucket_applies"),
                      "ps_global_step": stats.get("global_step"),
                      "pushes_issued": pushes, "transport": "hipIpc mailboxes + C++ ps service (bf16 push, bf16 pull)",
-                     "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": 0}
+                     "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": 0,
+                     "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
 
         class _R:
             rank = 0

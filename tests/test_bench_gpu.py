@@ -31,7 +31,8 @@ def test_bench_self_launches_two_ranks():
     assert r["n_gpus"] == 2 and r["steps"] == 6 and r["warmup"] == 3
     cfg = r["config"]
     assert cfg["ranks_seen_by_comm"] == 2
-    assert cfg["replicas_identical"] is True
+    assert cfg["replicas_identical"] is True   # (also: both ranks ran the same pre-warm steps)
+    assert cfg["prewarm"]["steps"] >= 10
     assert cfg["global_batch"] == 512 and cfg["parallelism"] == "dp2"
     assert "ipc" in cfg["grad_allreduce"] and cfg["hip_graph"] is True
     assert len(r["window_ms_per_step"]) >= 1 and r["value"] > 0

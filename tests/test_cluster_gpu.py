@@ -107,10 +107,12 @@ def test_bench_ps_native_plane(hogwild):
     rec = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["value"] > 0
     c = rec["config"]
-    assert c["ps_applies"] == c["pushes_issued"] == 2 * 34
+    n = 34 + c["prewarm"]["steps"]   # timed + warmup + pre-warm steps per worker
+    assert c["prewarm"]["steps"] >= 10
+    assert c["ps_applies"] == c["pushes_issued"] == 2 * n
     # the CNN pushes two buckets per step; the first is announced and applied as it lands (during
     # backward - or with the request, if the ps noticed it only then); the last is never announced:
     # the request applies it in the launch that advances the step scalars and writes the reply
-    assert c["ps_bucket_applies"] == (0 if hogwild else 2 * 1 * 34)
-    assert c["ps_global_step"] == 2 * 34 and 0 < c["global_step"] <= 2 * 34
+    assert c["ps_bucket_applies"] == (0 if hogwild else 2 * 1 * n)
+    assert c["ps_global_step"] == 2 * n and 0 < c["global_step"] <= 2 * n
     assert 0.0 < c["last_loss"] < 10.0
