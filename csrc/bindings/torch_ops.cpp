@@ -919,6 +919,26 @@ void maxpool3_fwd(const Tensor& x, const Tensor& y, const Tensor& am) {
                             (int)y.size(1), (int)y.size(2), cur_stream());
 }
 
+void bn_relu_pool3(const Tensor& x, const Tensor& stats, const Tensor& gamma, const Tensor& beta,
+                   const optional<Tensor>& mean, const optional<Tensor>& invstd, const optional<Tensor>& moving_mean,
+                   const optional<Tensor>& moving_var, double eps, double momentum, const Tensor& y,
+                   const Tensor& am) {
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && am.dim() == 4, "bn_relu_pool3: NHWC tensors");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && am.scalar_type() == at::kByte && y.sizes() == am.sizes() &&
+                  y.size(0) == x.size(0) && y.size(3) == x.size(3) && y.size(1) == (x.size(1) + 1) / 2 &&
+                  y.size(2) == (x.size(2) + 1) / 2, "bn_relu_pool3: y bf16 / am uint8 [B][ceil(H/2)][ceil(W/2)][C]");
+  dtfe::BnArgs a = bn_common(x, stats, 1);
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.mean = ptr_or_null<float>(mean);
+  a.invstd = ptr_or_null<float>(invstd);
+  a.moving_mean = ptr_or_null<float>(moving_mean);
+  a.moving_var = ptr_or_null<float>(moving_var);
+  a.eps = (float)eps; a.momentum = (float)momentum;
+  dtfe::launch_bn_relu_pool3(a, reinterpret_cast<dtfe::bf16*>(y.data_ptr()), am.data_ptr<uint8_t>(), (int)x.size(0),
+                             (int)x.size(1), (int)x.size(2), (int)y.size(1), (int)y.size(2), cur_stream());
+}
+
 void maxpool3_bwd(const Tensor& dy, const Tensor& am, const Tensor& dx) {
   dtfe::launch_maxpool3_bwd(reinterpret_cast<const dtfe::bf16*>(dy.data_ptr()), am.data_ptr<uint8_t>(),
                             reinterpret_cast<dtfe::bf16*>(dx.data_ptr()), (int)dx.size(0), (int)dx.size(1),
@@ -948,6 +968,9 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx) -> ()");
   m.def("maxpool3_fwd(Tensor x, Tensor(a!) y, Tensor(b!) am) -> ()");
   m.def("maxpool3_bwd(Tensor dy, Tensor am, Tensor(a!) dx) -> ()");
+  m.def("bn_relu_pool3(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
+        " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, Tensor(e!) y,"
+        " Tensor(f!) am) -> ()");
   m.def("lstm_cell_fwd(Tensor gates, Tensor(a!) act, Tensor? c_prev, Tensor(b!) c, Tensor(c!) h_out, int ld_h,"
         " float forget_bias) -> ()");
   m.def("lstm_cell_bwd(Tensor act, Tensor? c_prev, Tensor c, Tensor? dh, Tensor? dh2, Tensor? dc_next,"
@@ -1029,6 +1052,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("gap_bwd", &gap_bwd);
   m.impl("maxpool3_fwd", &maxpool3_fwd);
   m.impl("maxpool3_bwd", &maxpool3_bwd);
+  m.impl("bn_relu_pool3", &bn_relu_pool3);
   m.impl("gemm", &gemm);
   m.impl("conv_fwd", &conv_fwd);
   m.impl("conv_dgrad", &conv_dgrad);

@@ -58,5 +58,10 @@ void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int 
                          hipStream_t s);
 void launch_maxpool3_bwd(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH, int OW,
                          hipStream_t s);
+// bn_apply (training mode, ReLU) fused with maxpool3_fwd: x = the conv output [B][H][W][C] (a.x,
+// a.stats, gamma, beta, mean / invstd / moving averages as bn_apply) -> pooled y + argmax; the
+// normalised map is never stored (ResNet-50 stem)
+void launch_bn_relu_pool3(const BnArgs& a, bf16* y, uint8_t* am, int B, int H, int W, int OH, int OW,
+                          hipStream_t s);
 
 }  // namespace dtfe

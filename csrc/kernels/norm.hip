@@ -469,6 +469,76 @@ __global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const bf16* x, bf16* 
   }
 }
 
+// BatchNorm apply + ReLU + 3x3 / stride-2 / pad-1 max pool in ONE pass (the ResNet-50 stem): each
+// thread normalises the 9 window pixels of its pooled pixel x 8 channels straight from the conv
+// output and keeps the max and its argmax.  The bn_apply -> maxpool3_fwd pair wrote the 112x112
+// normalised map (411 MB bf16 at B=256) and read it back; the backward never needs it (the stem BN
+// recomputes its ReLU mask from x, maxpool3_bwd reads the argmax).  Every value is formed exactly as
+// bn_apply forms it (same scale / shift, bf16 rounding) and compared as maxpool3_fwd compares it
+// (first max wins), so y / am are bit-identical to the pair's.  Workgroup 0 also stores mean /
+// invstd and updates the moving averages, as bn_apply does.
+__global__ __launch_bounds__(256) void bn_relu_pool3_kernel(BnArgs a, bf16* y, uint8_t* am, int B, int H, int W,
+                                                            int OH, int OW) {
+  const int C = a.C, cpr = C / 8;
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float mean, invstd;
+      chan_params(a, c, mean, invstd);
+      if (a.mean) a.mean[c] = mean;
+      if (a.invstd) a.invstd[c] = invstd;
+      if (a.moving_mean) {
+        const float var = 1.f / (invstd * invstd) - a.eps;
+        const float unb = a.R > 1 ? var * (float)a.R / (float)(a.R - 1) : var;
+        a.moving_mean[c] = a.moving_mean[c] * a.momentum + mean * (1.f - a.momentum);
+        a.moving_var[c] = a.moving_var[c] * a.momentum + unb * (1.f - a.momentum);
+      }
+    }
+  }
+  // the grid stride is a multiple of cpr (the launcher checks 256 % cpr == 0): one chunk per thread
+  const int ch = (int)(((long)blockIdx.x * 256 + threadIdx.x) % cpr) * 8;
+  float scale[8], shift[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float mean, invstd;
+    chan_params(a, ch + e, mean, invstd);
+    scale[e] = a.gamma[ch + e] * invstd;
+    shift[e] = a.beta[ch + e] - mean * scale[e];
+  }
+  const long n = (long)B * OH * OW * cpr;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long row = i / cpr;
+    const long hw = (long)OH * OW, b = row / hw;
+    const int p = (int)(row - b * hw), oy = p / OW, ox = p - oy * OW;
+    u32x4_t v[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = oy * 2 - 1 + t / 3, ix = ox * 2 - 1 + t % 3;
+      ok[t] = iy >= 0 && iy < H && ix >= 0 && ix < W;
+      if (ok[t]) v[t] = ld16(a.x + ((b * H + iy) * W + ix) * C + ch);
+    }
+    float best[8];
+    uint32_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -3.0e38f; arg[e] = 0; }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!ok[t]) continue;
+      float f[8];
+      unpack8(v[t], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e] * scale[e] + shift[e], ACT_RELU);
+      unpack8(pack8(f), f);  // the bf16 value bn_apply would have stored
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (f[e] > best[e]) { best[e] = f[e]; arg[e] = t; }
+    }
+    *reinterpret_cast<u32x4_t*>(y + row * C + ch) = pack8(best);
+    u32x2_t packed = {arg[0] | arg[1] << 8 | arg[2] << 16 | arg[3] << 24, arg[4] | arg[5] << 8 | arg[6] << 16 | arg[7] << 24};
+    *reinterpret_cast<u32x2_t*>(am + row * C + ch) = packed;
+  }
+}
+
 // one thread per (2x2 input cell, 8-channel chunk): input rows 2k, 2k+1 are covered only by window
 // rows k (both) and k+1 (the odd row), columns likewise, so the thread issues the <= 4 window loads
 // (dy 16 B + argmax 8 B each) up front and writes 4 input pixels; each pixel sums its windows in
@@ -623,6 +693,14 @@ void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int 
   if (C % 8) throw std::runtime_error("maxpool3: C % 8");
   hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(ew_grid((long)B * OH * OW * C / 8)), dim3(256), 0, s, x, y, am, B, H,
                      W, C, OH, OW);
+}
+
+void launch_bn_relu_pool3(const BnArgs& a, bf16* y, uint8_t* am, int B, int H, int W, int OH, int OW,
+                          hipStream_t s) {
+  if (a.C % 8 || 256 % (a.C / 8) || a.R != (long)B * H * W || a.infer)
+    throw std::runtime_error("bn_relu_pool3: training mode, C % 8 == 0, 256 % (C / 8) == 0, R == B*H*W");
+  hipLaunchKernelGGL(bn_relu_pool3_kernel, dim3(ew_grid((long)B * OH * OW * a.C / 8)), dim3(256), 0, s, a, y, am, B, H,
+                     W, OH, OW);
 }
 
 void launch_maxpool3_bwd(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH, int OW,

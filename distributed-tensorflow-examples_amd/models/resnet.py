@@ -266,6 +266,26 @@ class BN:
                      mask_out=self.ybits if self.use_bits else None)
         return self.y
 
+    def fwd_pool3(self, x, pool, am):
+        """BN + ReLU + the 3x3 / stride-2 max pool of the ResNet-50 stem.  Training on the GPU: ONE
+        pass (ops.bn_relu_pool3) that never stores the normalised 112x112 map - the backward
+        recomputes this BN's ReLU mask from x and the pool's from ``am`` (bn_apply + maxpool3_fwd
+        wrote 411 MB and read it back at B=256: 22.64-22.69 vs 22.74-22.77 ms per ResNet-50 step,
+        profiles/r4_resnet50_stem_pool_ab.txt).  Returns ``pool``."""
+        xx = x[0] if isinstance(x, tuple) else x
+        if self.infer or not xx.is_cuda:
+            ops.maxpool3_fwd(self.fwd(x), pool, am)
+            return pool
+        P = self.P
+        x, have_stats = x if isinstance(x, tuple) else (x, False)
+        self.mask_from_x, self.use_bits = True, False
+        if not have_stats:
+            ops.bn_stats(x, self.stats)
+        ops.bn_relu_pool3(x, self.stats, P.view(self.gamma), P.view(self.beta), pool, am, mean=self.mean,
+                          invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
+                          momentum=BN_MOMENTUM)
+        return pool
+
     def _mask_src(self, act):
         """(y argument, beta) of the backward ops: the bit mask, y, or nothing (mask from x)."""
         from_x = act == ops.ACT_RELU and getattr(self, "mask_from_x", False)
@@ -617,10 +637,11 @@ class ResNetProgram(StepProgram):
 
     def forward(self):
         L = self.L
-        h = L["stem_bn"].fwd(L["stem"].fwd(self.x, L["stem_bn"].stats))
+        z = L["stem"].fwd(self.x, L["stem_bn"].stats)
         if "pool_hw" in L:
-            ops.maxpool3_fwd(h, self.pool, self.pool_am)
-            h = self.pool
+            h = L["stem_bn"].fwd_pool3(z, self.pool, self.pool_am)
+        else:
+            h = L["stem_bn"].fwd(z)
         for b in L["blocks"]:
             h = b.fwd(h)
         ops.gap_fwd(h, self.feat16)

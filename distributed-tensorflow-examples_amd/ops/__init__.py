@@ -26,7 +26,7 @@ __all__ = [
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
-    "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "imgconv", "imgwgrad", "hash_uniform",
+    "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -986,6 +986,20 @@ def maxpool3_fwd(x, y, am):
     y.copy_(v.view(B, C, OH, OW).permute(0, 2, 3, 1).to(y.dtype))
     am.copy_(i.view(B, C, OH, OW).permute(0, 2, 3, 1).to(am.dtype))
     return y
+
+
+def bn_relu_pool3(x, stats, gamma, beta, y, am, *, mean=None, invstd=None, moving_mean=None, moving_var=None,
+                  eps=1e-3, momentum=0.99):
+    """bn_apply(act=ReLU) + maxpool3_fwd in one pass: the pooled output ``y`` and argmax ``am`` of
+    the normalised map, which is never stored; mean / invstd / moving averages as bn_apply.  Bit-
+    identical to the two-op sequence (the ResNet-50 stem)."""
+    if x.is_cuda:
+        require().bn_relu_pool3(x, stats, gamma, beta, mean, invstd, moving_mean, moving_var, eps, momentum, y, am)
+        return y
+    h = torch.empty_like(x)
+    bn_apply(x, stats, gamma, beta, h, mean=mean, invstd=invstd, moving_mean=moving_mean, moving_var=moving_var,
+             eps=eps, momentum=momentum, act=ACT_RELU)
+    return maxpool3_fwd(h, y, am)
 
 
 def maxpool3_bwd(dy, am, dx):

@@ -22,9 +22,11 @@ for dev in ("cpu", "cuda"):
     p.P.grad.zero_(); p.arena.buf.zero_(); p.loss.zero_(); p.correct.zero_()
     p.forward()
     L = p.L
-    a = [("stem_conv", L["stem"].y), ("stem_bn", L["stem_bn"].y)]
-    if "pool_hw" in L:
+    a = [("stem_conv", L["stem"].y)]
+    if "pool_hw" in L:  # (BN + ReLU + pool are one pass on the GPU: the stem BN map is not stored)
         a.append(("pool", p.pool))
+    else:
+        a.append(("stem_bn", L["stem_bn"].y))
     for i, b in enumerate(L["blocks"]):
         a.append(("block%d.conv1" % i, b.conv1.y))
         a.append(("block%d.out" % i, b.bn3.y if hasattr(b, "bn3") else b.bn2.y))

@@ -190,3 +190,34 @@ def test_stem_fwd_fused_bn_stats_match_separate_pass(B):
     v1, v2 = s1[64:] / R - m1 * m1, s2[64:] / R - m2 * m2
     assert torch.allclose(m1, m2, rtol=1e-3, atol=1e-5)
     assert torch.allclose(v1, v2, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(4, 112, 112, 64), (3, 17, 13, 16), (2, 9, 10, 256)])
+def test_bn_relu_pool3_bitwise_vs_apply_then_pool(shape):
+    """bn_relu_pool3 (ResNet-50 stem: BN + ReLU + 3x3/s2 max pool in one pass) == bn_apply followed
+    by maxpool3_fwd, bit for bit: pooled values, argmax, saved mean / invstd and moving averages.
+    Odd spatial sizes exercise the padded last window row / column."""
+    torch.manual_seed(5)
+    B, H, W, C = shape
+    x = (torch.randn(B, H, W, C) * 1.7 + 0.4).to(DEV, torch.bfloat16)
+    g = (torch.rand(C) + 0.5).to(DEV)
+    bt = (torch.randn(C) * 0.3).to(DEV)
+    stats = torch.zeros(2 * C, device=DEV)
+    ops.bn_stats(x, stats)
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    outs = []
+    for fused in (False, True):
+        mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        mm, mv = torch.full((C,), 0.1, device=DEV), torch.full((C,), 0.9, device=DEV)
+        y = torch.full((B, OH, OW, C), float("nan"), device=DEV, dtype=torch.bfloat16)
+        am = torch.full((B, OH, OW, C), 255, device=DEV, dtype=torch.uint8)
+        kw = dict(mean=mean, invstd=inv, moving_mean=mm, moving_var=mv, eps=1e-5, momentum=0.9)
+        if fused:
+            ops.bn_relu_pool3(x, stats, g, bt, y, am, **kw)
+        else:
+            h = torch.empty_like(x)
+            ops.bn_apply(x, stats, g, bt, h, act=ops.ACT_RELU, **kw)
+            ops.maxpool3_fwd(h, y, am)
+        outs.append((y, am, mean, inv, mm, mv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
