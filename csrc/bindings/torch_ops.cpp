@@ -919,6 +919,26 @@ void maxpool3_fwd(const Tensor& x, const Tensor& y, const Tensor& am) {
                             (int)y.size(1), (int)y.size(2), cur_stream());
 }
 
+void pool3_bn_bwd(const Tensor& dp, const Tensor& am, const Tensor& x, const Tensor& mean, const Tensor& invstd,
+                  const Tensor& gamma, const Tensor& beta, const Tensor& stats, const Tensor& dx,
+                  const optional<Tensor>& dgamma, const optional<Tensor>& dbeta) {
+  TORCH_CHECK(dp.dim() == 4 && x.dim() == 4 && dx.sizes() == x.sizes() && am.sizes() == dp.sizes() &&
+                  am.scalar_type() == at::kByte && dp.scalar_type() == at::kBFloat16 &&
+                  dx.scalar_type() == at::kBFloat16 && dp.size(0) == x.size(0) && dp.size(3) == x.size(3),
+              "pool3_bn_bwd: dp / am [B][OH][OW][C], x / dx [B][H][W][C]");
+  dtfe::BnArgs a = bn_common(x, stats, 1);
+  a.dy = reinterpret_cast<const dtfe::bf16*>(dp.data_ptr());
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.out = reinterpret_cast<dtfe::bf16*>(dx.data_ptr());
+  a.dgamma = ptr_or_null<float>(dgamma);
+  a.dbeta = ptr_or_null<float>(dbeta);
+  dtfe::launch_pool3_bn_bwd(a, am.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                            (int)dp.size(1), (int)dp.size(2), cur_stream());
+}
+
 void bn_relu_pool3(const Tensor& x, const Tensor& stats, const Tensor& gamma, const Tensor& beta,
                    const optional<Tensor>& mean, const optional<Tensor>& invstd, const optional<Tensor>& moving_mean,
                    const optional<Tensor>& moving_var, double eps, double momentum, const Tensor& y,
@@ -971,6 +991,8 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("bn_relu_pool3(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, Tensor(e!) y,"
         " Tensor(f!) am) -> ()");
+  m.def("pool3_bn_bwd(Tensor dp, Tensor am, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta,"
+        " Tensor(a!) stats, Tensor(b!) dx, Tensor(c!)? dgamma, Tensor(d!)? dbeta) -> ()");
   m.def("lstm_cell_fwd(Tensor gates, Tensor(a!) act, Tensor? c_prev, Tensor(b!) c, Tensor(c!) h_out, int ld_h,"
         " float forget_bias) -> ()");
   m.def("lstm_cell_bwd(Tensor act, Tensor? c_prev, Tensor c, Tensor? dh, Tensor? dh2, Tensor? dc_next,"
@@ -1053,6 +1075,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("maxpool3_fwd", &maxpool3_fwd);
   m.impl("maxpool3_bwd", &maxpool3_bwd);
   m.impl("bn_relu_pool3", &bn_relu_pool3);
+  m.impl("pool3_bn_bwd", &pool3_bn_bwd);
   m.impl("gemm", &gemm);
   m.impl("conv_fwd", &conv_fwd);
   m.impl("conv_dgrad", &conv_dgrad);

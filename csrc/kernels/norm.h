@@ -58,6 +58,10 @@ void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int 
                          hipStream_t s);
 void launch_maxpool3_bwd(const bf16* dy, const uint8_t* am, bf16* dx, int B, int H, int W, int C, int OH, int OW,
                          hipStream_t s);
+// maxpool3_bwd fused into the following BatchNorm's backward (ReLU mask from x): a.dy = the POOLED
+// gradient [B][OH][OW][C], am its argmax, a.x the BN input [B][H][W][C]; launches the statistics
+// pass (into a.stats, zeroed by the caller) and the apply pass (a.out = dx, dgamma / dbeta +=)
+void launch_pool3_bn_bwd(const BnArgs& a, const uint8_t* am, int B, int H, int W, int OH, int OW, hipStream_t s);
 // bn_apply (training mode, ReLU) fused with maxpool3_fwd: x = the conv output [B][H][W][C] (a.x,
 // a.stats, gamma, beta, mean / invstd / moving averages as bn_apply) -> pooled y + argmax; the
 // normalised map is never stored (ResNet-50 stem)

@@ -601,6 +601,112 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const bf16* dy, const
   }
 }
 
+// maxpool3_bwd fused into the stem BatchNorm's backward (ReLU mask recomputed from x, MM_X): one
+// thread per (2x2 input cell, 8-channel chunk) as in maxpool3_bwd - the <= 4 pooled windows (dy 16 B
+// + argmax 8 B each) and the 4 pixels of x are loaded up front, each pixel's upstream gradient is
+// summed in maxpool3_bwd's (oy, ox) order and rounded to bf16 exactly as that kernel stores it, then
+// masked and either reduced into the statistics (STATS) or turned into dx (apply).  The 112x112
+// unpooled gradient (411 MB bf16 at B=256) is never stored or read back.  The apply half is bit-
+// identical to maxpool3_bwd + bn_bwd_apply on the same statistics.
+template <bool STATS>
+__global__ __launch_bounds__(NT) void pool3_bn_bwd_kernel(BnArgs a, const uint8_t* am, int B, int H, int W, int OH,
+                                                          int OW) {
+  const int C = a.C, cpr = C / 8;
+  if (!STATS && blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += NT) {
+      if (a.dbeta) a.dbeta[c] += a.stats[c];
+      if (a.dgamma) a.dgamma[c] += a.stats[C + c];
+    }
+  }
+  const int chunk = threadIdx.x % cpr;  // the grid stride is a multiple of cpr (NT % cpr == 0)
+  const int ch = chunk * 8;
+  const BwdMask M(a, chunk, true);
+  const float inv_r = 1.f / (float)a.R;
+  float mean[8], invstd[8], k[8], sg[8], sgx[8], s[8] = {}, q[8] = {};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mean[e] = a.mean[ch + e];
+    invstd[e] = a.invstd[ch + e];
+    if (!STATS) {
+      k[e] = a.gamma[ch + e] * invstd[e];
+      sg[e] = a.stats[ch + e] * inv_r;
+      sgx[e] = a.stats[C + ch + e] * inv_r;
+    }
+  }
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2;
+  const long n = (long)B * QH * QW * cpr;
+  for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    const long cell = i / cpr;
+    const long qhw = (long)QH * QW, b = cell / qhw;
+    const int p = (int)(cell - b * qhw), kq = p / QW, jq = p - kq * QW;
+    u32x4_t d[2][2], xv[2][2];
+    u32x2_t m[2][2];
+    bool ok[2][2];
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const int oy = kq + a2, ox = jq + c2;
+        ok[a2][c2] = oy < OH && ox < OW;
+        if (ok[a2][c2]) {
+          const long o = ((b * OH + oy) * OW + ox) * C + ch;
+          d[a2][c2] = ld16(a.dy + o);
+          m[a2][c2] = *reinterpret_cast<const u32x2_t*>(am + o);
+        }
+        const int iy = 2 * kq + a2, ix = 2 * jq + c2;
+        if (iy < H && ix < W) xv[a2][c2] = ld16(a.x + ((b * H + iy) * W + ix) * C + ch);
+      }
+#pragma unroll
+    for (int yi = 0; yi < 2; ++yi) {
+      const int iy = 2 * kq + yi;
+      if (iy >= H) continue;
+#pragma unroll
+      for (int xi = 0; xi < 2; ++xi) {
+        const int ix = 2 * jq + xi;
+        if (ix >= W) continue;
+        float g[8] = {};
+#pragma unroll
+        for (int a2 = 0; a2 < 2; ++a2) {
+          const int ty = yi - 2 * a2 + 1;  // tap row of (iy) in window row kq + a2
+          if (ty < 0) continue;
+#pragma unroll
+          for (int c2 = 0; c2 < 2; ++c2) {
+            const int tx = xi - 2 * c2 + 1;
+            if (tx < 0 || !ok[a2][c2]) continue;
+            const uint32_t t = (uint32_t)(ty * 3 + tx);
+            float dv[8];
+            unpack8(d[a2][c2], dv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t ae = ((e < 4 ? m[a2][c2][0] : m[a2][c2][1]) >> (8 * (e & 3))) & 0xffu;
+              if (ae == t) g[e] += dv[e];
+            }
+          }
+        }
+        float x[8];
+        unpack8(xv[yi][xi], x);
+        masked_grad<MM_X>(a, M, pack8(g), u32x4_t{0u, 0u, 0u, 0u}, x, g);  // bf16 dy as maxpool3_bwd stores it
+        if constexpr (STATS) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s[e] += g[e];
+            q[e] += g[e] * (x[e] - mean[e]) * invstd[e];
+          }
+        } else {
+          float dx[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xh = (x[e] - mean[e]) * invstd[e];
+            dx[e] = k[e] * (g[e] - sg[e] - xh * sgx[e]);
+          }
+          *reinterpret_cast<u32x4_t*>(a.out + ((b * H + iy) * W + ix) * C + ch) = pack8(dx);
+        }
+      }
+    }
+  }
+  if constexpr (STATS) reduce_stats(s, q, C, a.stats);
+}
+
 int ew_grid(long n) {
   long g = (n + 255) / 256;
   if (g > 65536) g = 65536;
@@ -693,6 +799,20 @@ void launch_maxpool3_fwd(const bf16* x, bf16* y, uint8_t* am, int B, int H, int 
   if (C % 8) throw std::runtime_error("maxpool3: C % 8");
   hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(ew_grid((long)B * OH * OW * C / 8)), dim3(256), 0, s, x, y, am, B, H,
                      W, C, OH, OW);
+}
+
+void launch_pool3_bn_bwd(const BnArgs& a, const uint8_t* am, int B, int H, int W, int OH, int OW, hipStream_t s) {
+  check(a);
+  if (NT % (a.C / 8) || a.R != (long)B * H * W || a.act != ACT_RELU || !a.gamma || !a.beta || a.y || a.ymask ||
+      a.dres || OH != (H + 1) / 2 || OW != (W + 1) / 2)
+    throw std::runtime_error("pool3_bn_bwd: ReLU mask from x (gamma, beta), NT % (C/8) == 0, 3x3/s2/p1 pool geometry");
+  const long n = (long)B * ((H + 1) / 2) * ((W + 1) / 2) * (a.C / 8);
+  const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
+  // statistics: a few workgroups per CU (2C atomics each; cf. stats_grid), apply: the whole range
+  long gs = (n + NT - 1) / NT;
+  if (gs > 1024) gs = 1024;
+  hipLaunchKernelGGL(pool3_bn_bwd_kernel<true>, dim3((unsigned)gs), dim3(NT), lds, s, a, am, B, H, W, OH, OW);
+  hipLaunchKernelGGL(pool3_bn_bwd_kernel<false>, dim3(ew_grid(n)), dim3(NT), 0, s, a, am, B, H, W, OH, OW);
 }
 
 void launch_bn_relu_pool3(const BnArgs& a, bf16* y, uint8_t* am, int B, int H, int W, int OH, int OW,

@@ -26,7 +26,7 @@ __all__ = [
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
-    "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "imgconv", "imgwgrad", "hash_uniform",
+    "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -1000,6 +1000,19 @@ def bn_relu_pool3(x, stats, gamma, beta, y, am, *, mean=None, invstd=None, movin
     bn_apply(x, stats, gamma, beta, h, mean=mean, invstd=invstd, moving_mean=moving_mean, moving_var=moving_var,
              eps=eps, momentum=momentum, act=ACT_RELU)
     return maxpool3_fwd(h, y, am)
+
+
+def pool3_bn_bwd(dp, am, x, mean, invstd, gamma, beta, stats, dx, *, dgamma=None, dbeta=None):
+    """maxpool3_bwd + bn_bwd_stats + bn_bwd_apply (ReLU mask recomputed from x) without the unpooled
+    gradient: ``dp`` / ``am`` are the pooled gradient and argmax, ``x`` the BN input, ``stats`` the
+    zeroed [2][C] backward accumulators; dx, dgamma / dbeta (+=) as bn_bwd_apply (the ResNet-50 stem)."""
+    if dx.is_cuda:
+        require().pool3_bn_bwd(dp, am, x, mean, invstd, gamma, beta, stats, dx, dgamma, dbeta)
+        return dx
+    d = maxpool3_bwd(dp, am, torch.empty_like(x))
+    bn_bwd_stats(d, None, x, mean, invstd, stats, ACT_RELU, gamma=gamma, beta=beta)
+    bn_bwd_apply(d, None, x, mean, invstd, gamma, stats, dx, act=ACT_RELU, dgamma=dgamma, dbeta=dbeta, beta=beta)
+    return dx
 
 
 def maxpool3_bwd(dy, am, dx):

@@ -221,3 +221,37 @@ def test_bn_relu_pool3_bitwise_vs_apply_then_pool(shape):
         outs.append((y, am, mean, inv, mm, mv))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape", [(4, 112, 112, 64), (3, 17, 13, 16), (2, 9, 10, 256)])
+def test_pool3_bn_bwd_matches_pool_bwd_then_bn_bwd(shape):
+    """pool3_bn_bwd (max-pool backward fused into the stem BN's backward, ReLU mask from x) vs
+    maxpool3_bwd + bn_bwd_stats + bn_bwd_apply: statistics to fp32 summation-order tolerance (both
+    reduce with atomics), dx / dgamma / dbeta bit-identical given the same statistics."""
+    torch.manual_seed(6)
+    B, H, W, C = shape
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    x = (torch.randn(B, H, W, C) * 1.3 + 0.2).to(DEV, torch.bfloat16)
+    g = (torch.rand(C) + 0.5).to(DEV)
+    bt = (torch.randn(C) * 0.3).to(DEV)
+    st = torch.zeros(2 * C, device=DEV)
+    ops.bn_stats(x, st)
+    mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    pool = torch.empty(B, OH, OW, C, device=DEV, dtype=torch.bfloat16)
+    am = torch.empty(B, OH, OW, C, device=DEV, dtype=torch.uint8)
+    ops.bn_relu_pool3(x, st, g, bt, pool, am, mean=mean, invstd=inv, eps=1e-5, momentum=0.9)
+    dp = torch.randn(B, OH, OW, C).to(DEV, torch.bfloat16)
+    # reference: unpooled gradient, then the two BN backward passes
+    d = torch.empty_like(x)
+    ops.maxpool3_bwd(dp, am, d)
+    s_ref = torch.zeros(2 * C, device=DEV)
+    ops.bn_bwd_stats(d, None, x, mean, inv, s_ref, ops.ACT_RELU, gamma=g, beta=bt)
+    s_f = torch.zeros(2 * C, device=DEV)
+    dx_f = torch.full_like(x, float("nan"))
+    dg_f, db_f = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ops.pool3_bn_bwd(dp, am, x, mean, inv, g, bt, s_f, dx_f, dgamma=dg_f, dbeta=db_f)
+    assert torch.allclose(s_f, s_ref, rtol=1e-3, atol=1e-3 * float(s_ref.abs().max()))
+    dx_r = torch.empty_like(x)
+    dg_r, db_r = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ops.bn_bwd_apply(d, None, x, mean, inv, g, s_f, dx_r, act=ops.ACT_RELU, dgamma=dg_r, dbeta=db_r, beta=bt)
+    assert torch.equal(dx_f, dx_r) and torch.equal(dg_f, dg_r) and torch.equal(db_f, db_r)
