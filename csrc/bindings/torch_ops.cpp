@@ -793,8 +793,18 @@ void bn_apply(const Tensor& x, const Tensor& stats, const Tensor& gamma, const T
               const optional<Tensor>& mean, const optional<Tensor>& invstd, const optional<Tensor>& moving_mean,
               const optional<Tensor>& moving_var, double eps, double momentum, int64_t act,
               const optional<Tensor>& res, int64_t rstride, int64_t OH, int64_t OW, const Tensor& out,
-              const optional<Tensor>& mask_out) {
+              const optional<Tensor>& mask_out, const optional<std::vector<Tensor>>& res_bn) {
   dtfe::BnArgs a = bn_common(x, stats, act);
+  if (res_bn.has_value() && !res_bn->empty()) {
+    // [stats, gamma, beta, mean, invstd, moving_mean, moving_var] of the residual's own BatchNorm
+    const auto& r = *res_bn;
+    TORCH_CHECK(r.size() == 7 && res.has_value() && res->sizes() == x.sizes(),
+                "bn_apply: res_bn = [stats, gamma, beta, mean, invstd, moving_mean, moving_var] of a same-shape raw residual");
+    for (const auto& t : r) TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat, "bn_apply: res_bn fp32 tensors");
+    a.r_stats = r[0].data_ptr<float>(); a.r_gamma = r[1].data_ptr<float>(); a.r_beta = r[2].data_ptr<float>();
+    a.r_mean = r[3].data_ptr<float>(); a.r_invstd = r[4].data_ptr<float>();
+    a.r_moving_mean = r[5].data_ptr<float>(); a.r_moving_var = r[6].data_ptr<float>();
+  }
   if (mask_out.has_value() && mask_out->defined()) {
     TORCH_CHECK(mask_out->is_cuda() && mask_out->scalar_type() == at::kByte && mask_out->numel() == x.numel() / 8 &&
                     act == 1, "bn_apply: mask_out is a uint8 [R][C/8] ReLU bit mask");
@@ -978,7 +988,7 @@ TORCH_LIBRARY(dtfe, m) {
         " Tensor? res, int rstride, int OH, int OW, Tensor(a!) out) -> ()");
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
-        " int rstride, int OH, int OW, Tensor(e!) out, Tensor(f!)? mask_out=None) -> ()");
+        " int rstride, int OH, int OW, Tensor(e!) out, Tensor(f!)? mask_out=None, Tensor(g!)[]? res_bn=None) -> ()");
   m.def("bn_bwd_stats(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) stats, int act,"
         " Tensor? gamma=None, Tensor? beta=None) -> ()");
   m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor stats,"

@@ -38,6 +38,14 @@ struct BnArgs {
   // kernels read it (ymask) instead of that bf16 output - 1 byte per 8 channels instead of 16
   uint8_t* mask_out;
   const uint8_t* ymask;
+  // bn_apply only: the residual through its own BatchNorm (a projection shortcut, no activation).
+  // res is then the shortcut conv's RAW output (same shape as x); its batch statistics r_stats
+  // (accumulated like stats), r_gamma / r_beta normalise it on the fly - rounded to bf16 exactly as
+  // bn_apply would have stored that BN's output - and workgroup 0 also saves r_mean / r_invstd and
+  // updates r_moving_mean / r_moving_var.  The shortcut BN's own apply pass (write + re-read of its
+  // output) disappears.
+  const float* r_stats; const float* r_gamma; const float* r_beta;
+  float* r_mean; float* r_invstd; float* r_moving_mean; float* r_moving_var;
 };
 
 void launch_bn_stats(const BnArgs& a, hipStream_t s);

@@ -101,12 +101,30 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   reduce_stats(s, q, a.C, a.stats);
 }
 
+__device__ __forceinline__ void chan_params_of(const bf16* x, const float* stats, long R, int C, float eps, int c,
+                                               float& mean, float& invstd) {
+  const float inv_r = 1.f / (float)R;
+  const float d = stats[c] * inv_r;
+  mean = bf2f(x[c]) + d;
+  const float var = fmaxf(stats[C + c] * inv_r - d * d, 0.f);
+  invstd = rsqrtf(var + eps);
+}
+
 __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean, float& invstd) {
-  const float inv_r = 1.f / (float)a.R;
-  const float d = a.stats[c] * inv_r;
-  mean = bf2f(a.x[c]) + d;
-  const float var = fmaxf(a.stats[a.C + c] * inv_r - d * d, 0.f);
-  invstd = rsqrtf(var + a.eps);
+  chan_params_of(a.x, a.stats, a.R, a.C, a.eps, c, mean, invstd);
+}
+
+// saved statistics + moving averages of one channel (TF: unbiased batch variance)
+__device__ __forceinline__ void save_chan(const BnArgs& a, int c, float mean, float invstd, float* smean,
+                                          float* sinv, float* mm, float* mv) {
+  if (smean) smean[c] = mean;
+  if (sinv) sinv[c] = invstd;
+  if (mm) {
+    const float var = 1.f / (invstd * invstd) - a.eps;
+    const float unb = a.R > 1 ? var * (float)a.R / (float)(a.R - 1) : var;
+    mm[c] = mm[c] * a.momentum + mean * (1.f - a.momentum);
+    mv[c] = mv[c] * a.momentum + unb * (1.f - a.momentum);
+  }
 }
 
 __device__ __forceinline__ long res_offset(const BnArgs& a, long r, int chunk, bool identity) {
@@ -122,21 +140,30 @@ __device__ __forceinline__ long res_offset(const BnArgs& a, long r, int chunk, b
 // ACTC: the activation as a compile-time constant (ACT_NONE / ACT_RELU), or -1 for the runtime a.act;
 // RES: a residual source is given.  (The runtime forms of both put a branch on every value of the
 // row loop: 2.4k static VALU instructions against ~0.8k for the ReLU / residual instance.)
-template <bool INFER, int ACTC, bool RES>
+// RBN: the residual goes through its own BatchNorm first (BnArgs.r_stats: a projection shortcut)
+template <bool INFER, int ACTC, bool RES, bool RBN = false>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
   const Slots S(a.C);
   if (!INFER && blockIdx.x == 0) {  // saved statistics + moving averages (TF: unbiased batch variance)
     for (int c = threadIdx.x; c < a.C; c += NT) {
       float mean, invstd;
       chan_params(a, c, mean, invstd);
-      if (a.mean) a.mean[c] = mean;
-      if (a.invstd) a.invstd[c] = invstd;
-      if (a.moving_mean) {
-        const float var = 1.f / (invstd * invstd) - a.eps;
-        const float unb = a.R > 1 ? var * (float)a.R / (float)(a.R - 1) : var;
-        a.moving_mean[c] = a.moving_mean[c] * a.momentum + mean * (1.f - a.momentum);
-        a.moving_var[c] = a.moving_var[c] * a.momentum + unb * (1.f - a.momentum);
+      save_chan(a, c, mean, invstd, a.mean, a.invstd, a.moving_mean, a.moving_var);
+      if (RBN) {
+        chan_params_of(a.res, a.r_stats, a.R, a.C, a.eps, c, mean, invstd);
+        save_chan(a, c, mean, invstd, a.r_mean, a.r_invstd, a.r_moving_mean, a.r_moving_var);
       }
+    }
+  }
+  float rscale[8], rshift[8];
+  if constexpr (RBN) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = S.chunk * 8 + e;
+      float mean, invstd;
+      chan_params_of(a.res, a.r_stats, a.R, a.C, a.eps, c, mean, invstd);
+      rscale[e] = a.r_gamma[c] * invstd;
+      rshift[e] = a.r_beta[c] - mean * rscale[e];
     }
   }
   float scale[8], shift[8];
@@ -175,6 +202,11 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
       if (res_chunk) {
         float g[8];
         unpack8(w[u], g);
+        if constexpr (RBN) {  // the shortcut BN's output as its own bn_apply (ACT_NONE) would store it
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = act_fwd(g[e] * rscale[e] + rshift[e], ACT_NONE);
+          unpack8(pack8(g), g);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += g[e];
       }
@@ -727,6 +759,13 @@ void launch_bn_apply(const BnArgs& a, hipStream_t s) {
   if (a.res && (a.RC % 8 || a.RC > a.C)) throw std::runtime_error("bn_apply: residual channels");
   const dim3 g(apply_grid(a.R, a.C)), b(NT);
   const bool res = a.res != nullptr;
+  if (a.r_stats) {  // projection shortcut BN folded into this residual apply (training, ReLU, same shape)
+    if (!res || a.infer || a.act != ACT_RELU || a.rstride != 1 || a.RC != a.C || a.RH != a.OH || a.RW != a.OW ||
+        !a.r_gamma || !a.r_beta)
+      throw std::runtime_error("bn_apply: a residual BN needs training mode, ReLU and a same-shape raw residual");
+    hipLaunchKernelGGL((bn_apply_kernel<false, ACT_RELU, true, true>), g, b, 0, s, a);
+    return;
+  }
   const int act = a.act == ACT_NONE || a.act == ACT_RELU ? a.act : -1;
 #define BN_APPLY(INF, ACT)                                                              \
   do {                                                                                  \

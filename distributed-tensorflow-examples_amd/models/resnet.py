@@ -245,8 +245,24 @@ class BN:
         self.stats, self.dstats, self.mean, self.invstd = arena.take(2 * self.C), arena.take(2 * self.C), \
             arena.take(self.C), arena.take(self.C)
 
-    def fwd(self, x, act=ops.ACT_RELU, res=None, rstride=1):
-        """``x``: the conv output, or (conv output, statistics already accumulated by the conv)."""
+    def stats_only(self, x):
+        """A projection shortcut's BN (no activation) whose apply is folded into the residual add of
+        the block's last BN (``fwd(..., res_bn=self)``): only the statistics here.  Returns the raw
+        conv output."""
+        x, have_stats = x if isinstance(x, tuple) else (x, False)
+        if not have_stats:
+            ops.bn_stats(x, self.stats)
+        self.mask_from_x, self.use_bits = False, False
+        return x
+
+    def res_bn_args(self):
+        P = self.P
+        return [self.stats, P.view(self.gamma), P.view(self.beta), self.mean, self.invstd, P.view(self.mm),
+                P.view(self.mv)]
+
+    def fwd(self, x, act=ops.ACT_RELU, res=None, rstride=1, res_bn=None):
+        """``x``: the conv output, or (conv output, statistics already accumulated by the conv).
+        ``res_bn``: the BN of a projection shortcut whose raw output ``res`` is (see stats_only)."""
         P = self.P
         x, have_stats = x if isinstance(x, tuple) else (x, False)
         if self.infer:  # evaluation: moving averages, nothing updated (TF training=False)
@@ -263,7 +279,8 @@ class BN:
         ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
                      invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
                      momentum=BN_MOMENTUM, act=act, res=res, rstride=rstride,
-                     mask_out=self.ybits if self.use_bits else None)
+                     mask_out=self.ybits if self.use_bits else None,
+                     res_bn=res_bn.res_bn_args() if res_bn is not None else None)
         return self.y
 
     def fwd_pool3(self, x, pool, am):
@@ -413,12 +430,19 @@ class Bottleneck:
 
     def fwd(self, x):
         self.x = x
-        res = x
+        res, res_bn = x, None
         if self.proj:
-            res = self.bns.fwd(self.convs.fwd(x, self.bns.stats), act=ops.ACT_NONE)
+            zs = self.convs.fwd(x, self.bns.stats)
+            if x.is_cuda and not self.bns.infer:
+                # the shortcut BN is applied inside bn3's residual apply (bn_apply res_bn): its output
+                # (411 MB at the first stage, B=256) is neither written nor read back: 22.47-22.49 vs
+                # 22.66-22.69 ms per step (profiles/r4_resnet50_residual_bn_fold_ab.txt)
+                res, res_bn = self.bns.stats_only(zs), self.bns
+            else:
+                res = self.bns.fwd(zs, act=ops.ACT_NONE)
         h1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats))
         h2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats))
-        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats), res=res, rstride=1)
+        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats), res=res, rstride=1, res_bn=res_bn)
 
     def bwd(self, dout, dx, dout_stats_done=False, next_bn=None):
         """``next_bn``: (BN, its x) of the layer that consumes dx (the previous block's bn3): its

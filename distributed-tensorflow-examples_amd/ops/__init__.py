@@ -835,16 +835,25 @@ def _shortcut_view(res, OH, OW, C, rstride):
 
 
 def bn_apply(x, stats, gamma, beta, out, *, mean=None, invstd=None, moving_mean=None, moving_var=None, eps=1e-3,
-             momentum=0.99, act=ACT_RELU, res=None, rstride=1, mask_out=None):
+             momentum=0.99, act=ACT_RELU, res=None, rstride=1, mask_out=None, res_bn=None):
     """out = act(gamma * (x - mean) * invstd + beta [+ shortcut(res)]) with batch statistics from
     ``stats``; stores mean/invstd and updates the moving averages (TF momentum convention).
     ``mask_out`` (ReLU): uint8 [R][C/8] bit mask of out > 0, which the backward ops take in place
-    of ``y`` (``relu_bits``)."""
+    of ``y`` (``relu_bits``).  ``res_bn`` = [stats, gamma, beta, mean, invstd, moving_mean,
+    moving_var] of the residual's own BatchNorm (a projection shortcut, no activation): ``res`` is
+    then that BN's raw input, normalised here exactly as its own bn_apply would store it, and that
+    BN's mean / invstd / moving averages are saved / updated here too."""
     OH, OW = (x.shape[1], x.shape[2]) if x.dim() == 4 else (1, 1)
     if x.is_cuda:
         require().bn_apply(x, stats, gamma, beta, mean, invstd, moving_mean, moving_var, eps, momentum, act, res,
-                           rstride, OH, OW, out, mask_out)
+                           rstride, OH, OW, out, mask_out, res_bn)
         return out
+    if res_bn is not None:
+        rs, rg, rb, rm, ri, rmm, rmv = res_bn
+        r_out = torch.empty_like(res)
+        bn_apply(res, rs, rg, rb, r_out, mean=rm, invstd=ri, moving_mean=rmm, moving_var=rmv, eps=eps,
+                 momentum=momentum, act=ACT_NONE)
+        res = r_out
     r = _rows(x)
     R, C = r.shape
     m, inv, var = _bn_params(stats, R, eps, r[0])

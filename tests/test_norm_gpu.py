@@ -255,3 +255,41 @@ def test_pool3_bn_bwd_matches_pool_bwd_then_bn_bwd(shape):
     dg_r, db_r = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     ops.bn_bwd_apply(d, None, x, mean, inv, g, s_f, dx_r, act=ops.ACT_RELU, dgamma=dg_r, dbeta=db_r, beta=bt)
     assert torch.equal(dx_f, dx_r) and torch.equal(dg_f, dg_r) and torch.equal(db_f, db_r)
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256), (3, 5, 7, 64)])
+def test_bn_apply_residual_bn_fold_bitwise(shape):
+    """bn_apply(res=raw shortcut, res_bn=...) (a projection shortcut's BN folded into the residual
+    apply) == the shortcut's own bn_apply(ACT_NONE) followed by the residual bn_apply: the output,
+    its ReLU bit mask and both BNs' saved statistics / moving averages, bit for bit."""
+    torch.manual_seed(9)
+    B, H, W, C = shape
+    x = (torch.randn(B, H, W, C) * 1.1 - 0.3).to(DEV, torch.bfloat16)
+    zs = (torch.randn(B, H, W, C) * 0.7 + 0.5).to(DEV, torch.bfloat16)
+    st, sst = torch.zeros(2 * C, device=DEV), torch.zeros(2 * C, device=DEV)
+    ops.bn_stats(x, st)
+    ops.bn_stats(zs, sst)
+    g, bt = (torch.rand(C) + 0.5).to(DEV), (torch.randn(C) * 0.2).to(DEV)
+    gs, bs = (torch.rand(C) + 0.5).to(DEV), (torch.randn(C) * 0.2).to(DEV)
+
+    def bufs():
+        return ([torch.empty(C, device=DEV) for _ in range(2)] + [torch.full((C,), 0.1, device=DEV),
+                                                                 torch.full((C,), 0.9, device=DEV)])
+    outs = []
+    for fused in (False, True):
+        m, i, mm, mv = bufs()
+        rm, ri, rmm, rmv = bufs()
+        y = torch.empty_like(x)
+        bits = torch.empty(x.numel() // 8, device=DEV, dtype=torch.uint8)
+        kw = dict(mean=m, invstd=i, moving_mean=mm, moving_var=mv, eps=1e-3, momentum=0.99, act=ops.ACT_RELU,
+                  mask_out=bits)
+        if fused:
+            ops.bn_apply(x, st, g, bt, y, res=zs, res_bn=[sst, gs, bs, rm, ri, rmm, rmv], **kw)
+        else:
+            ys = torch.empty_like(zs)
+            ops.bn_apply(zs, sst, gs, bs, ys, mean=rm, invstd=ri, moving_mean=rmm, moving_var=rmv, eps=1e-3,
+                         momentum=0.99, act=ops.ACT_NONE)
+            ops.bn_apply(x, st, g, bt, y, res=ys, **kw)
+        outs.append((y, bits, m, i, mm, mv, rm, ri, rmm, rmv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
