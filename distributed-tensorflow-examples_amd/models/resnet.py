@@ -47,6 +47,8 @@ BN_EPS, BN_MOMENTUM = 1e-3, 0.99
 # bottleneck input gradient: shortcut share written into dx, conv1's data gradient accumulated on
 # top (DTFE_R50_SHORTCUT_FUSE=0: separate buffer + add pass, for A/B)
 _SHORTCUT_FUSE = os.environ.get("DTFE_R50_SHORTCUT_FUSE", "1") != "0"
+# (test hook, not a knob: tests/test_resnet.py compares against the stored-dres path)
+_PROJ_FROM_BITS = True
 # activation / activation-gradient storage dtype: bf16 on the GPU kernels; the CPU reference
 # path also runs with fp32 storage (exactness tests of the program logic)
 ACT_DTYPE = torch.bfloat16
@@ -331,9 +333,11 @@ class BN:
         y, beta = self._mask_src(act)
         return (x, y, self.mean, self.invstd, P.view(self.gamma), beta, self.dstats, act)
 
-    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None, stats_done=False):
+    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None, stats_done=False, mask=None):
+        """``mask``: a uint8 ReLU bit mask to take act' from instead of this BN's own (a projection
+        shortcut's BN differentiated straight from the block's output gradient and bn3's mask)."""
         P = self.P
-        y, beta = self._mask_src(act)
+        y, beta = (mask, None) if mask is not None else self._mask_src(act)
         if not stats_done:
             ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta)
         ops.bn_bwd_apply(dy, y, x, self.mean, self.invstd, P.view(self.gamma), self.dstats, dx, act=act, dres=dres,
@@ -454,7 +458,11 @@ class Bottleneck:
         # identity shortcut: its gradient dout * ReLU'(block output) is added by conv1's data-gradient
         # epilogue from dout and bn3's bit mask - bn3's backward does not store it at all
         masked = fuse and not self.proj and self.bn3.use_bits and self.conv1.stride == 1
-        dres = None if masked else (dx if (fuse and not self.proj) else self.dres)
+        # projection shortcut: its BN's backward reads dout and bn3's bit mask directly - bn3's backward
+        # does not store the masked gradient (dres) for it to read back twice: 22.32-22.34 vs 22.43-22.46
+        # ms per step (profiles/r4_resnet50_residual_bn_fold_ab.txt)
+        proj_bits = self.proj and self.bn3.use_bits and _PROJ_FROM_BITS
+        dres = None if (masked or proj_bits) else (dx if (fuse and not self.proj) else self.dres)
         # Capture order: each data gradient BEFORE the weight gradient forked at the same point (the
         # fork event is taken when dy is final).  The hipGraph executor keeps a node's first-captured
         # child on its queue; with the weight gradient captured first, the data-gradient chain kept
@@ -473,7 +481,10 @@ class Bottleneck:
         ev1 = fork()
         evs = None
         if self.proj:
-            self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
+            if proj_bits:  # g = dout * ReLU'(block output) = what dres held, bit for bit
+                self.bns.bwd(dout, self.convs.y, self.dsc, act=ops.ACT_RELU, mask=self.bn3.ybits)
+            else:
+                self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
             evs = fork()
         nb = next_bn[0].bwd_stats_args(next_bn[1]) if next_bn is not None else None
         ret = None

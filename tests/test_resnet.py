@@ -397,3 +397,29 @@ def test_resnet50_bf16_grads_vs_stock_amp_gpu():
     md = sum(cd for _, cd, _ in rows) / len(rows)
     ma = sum(ca for _, _, ca in rows) / len(rows)
     assert md >= ma - 0.02, (md, ma)
+
+
+@pytest.mark.gpu
+def test_resnet50_projection_bn_from_bits_matches(monkeypatch):
+    """The projection shortcut's BN backward read straight from dout + bn3's ReLU bit mask (no stored
+    masked gradient) computes the same g as the dres path, bit for bit; the gradients then differ
+    only by the run-to-run order of the BN statistics' atomics (measured here between two runs of
+    the old path)."""
+    from dtfe.models import resnet as rn
+
+    model = ResNetModel(arch="resnet50")
+    torch.manual_seed(0)
+    B = 2
+    x = torch.rand(B, 224, 224, 3).cuda()
+    y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,)), 1000).float().cuda()
+    grads = []
+    for flag in (False, False, True):
+        monkeypatch.setattr(rn, "_PROJ_FROM_BITS", flag)
+        prog = model.program("cuda", B, seed=1)
+        prog.load_batch((x, y))
+        prog.compute_grads()
+        torch.cuda.synchronize()
+        grads.append(prog.P.grad.clone())
+    noise = float((grads[0] - grads[1]).abs().max())
+    cross = float((grads[0] - grads[2]).abs().max())
+    assert cross <= 4 * noise + 1e-6 * float(grads[0].abs().max()), (cross, noise)
