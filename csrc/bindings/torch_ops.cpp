@@ -869,8 +869,18 @@ void set_bwd_y(dtfe::BnArgs& a, const optional<Tensor>& y, const Tensor& x) {
 
 void bn_bwd_stats(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                   const Tensor& invstd, const Tensor& stats, int64_t act, const optional<Tensor>& gamma,
-                  const optional<Tensor>& beta) {
+                  const optional<Tensor>& beta, const optional<std::vector<Tensor>>& res_bn) {
   dtfe::BnArgs a = bn_common(x, stats, act);
+  if (res_bn.has_value() && !res_bn->empty()) {
+    // [x, mean, invstd, stats] of a projection shortcut's BN: its statistics from the same g
+    const auto& r = *res_bn;
+    TORCH_CHECK(r.size() == 4 && r[0].sizes() == x.sizes() && r[0].scalar_type() == at::kBFloat16 &&
+                    r[1].scalar_type() == at::kFloat && r[2].scalar_type() == at::kFloat &&
+                    r[3].scalar_type() == at::kFloat && r[3].numel() == 2 * a.C,
+                "bn_bwd_stats: res_bn = [x bf16 (same shape), mean, invstd, stats [2][C]]");
+    a.res = reinterpret_cast<const dtfe::bf16*>(r[0].data_ptr());
+    a.r_mean = r[1].data_ptr<float>(); a.r_invstd = r[2].data_ptr<float>(); a.r_stats = r[3].data_ptr<float>();
+  }
   a.dy = reinterpret_cast<const dtfe::bf16*>(dy.data_ptr());
   set_bwd_y(a, y, x);
   a.gamma = ptr_or_null<float>(gamma);
@@ -990,7 +1000,7 @@ TORCH_LIBRARY(dtfe, m) {
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
         " int rstride, int OH, int OW, Tensor(e!) out, Tensor(f!)? mask_out=None, Tensor(g!)[]? res_bn=None) -> ()");
   m.def("bn_bwd_stats(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) stats, int act,"
-        " Tensor? gamma=None, Tensor? beta=None) -> ()");
+        " Tensor? gamma=None, Tensor? beta=None, Tensor(b!)[]? res_bn=None) -> ()");
   m.def("bn_bwd_apply(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor stats,"
         " int act, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, Tensor? beta=None) -> ()");
   m.def("shortcut_grad_add(Tensor g, Tensor(a!) dx, int stride) -> ()");

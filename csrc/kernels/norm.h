@@ -44,7 +44,10 @@ struct BnArgs {
   // bn_apply would have stored that BN's output - and workgroup 0 also saves r_mean / r_invstd and
   // updates r_moving_mean / r_moving_var.  The shortcut BN's own apply pass (write + re-read of its
   // output) disappears.
-  const float* r_stats; const float* r_gamma; const float* r_beta;
+  // bn_bwd_stats only (MM_BITS): res = that projection BN's input; r_mean / r_invstd its saved batch
+  // statistics, and its backward statistics (sum g, sum g * xhat_res) are accumulated into r_stats
+  // from the same g in the same pass (g = dy * the block output's ReLU bit)
+  float* r_stats; const float* r_gamma; const float* r_beta;
   float* r_mean; float* r_invstd; float* r_moving_mean; float* r_moving_var;
 };
 

@@ -283,45 +283,60 @@ __device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, c
   }
 }
 
-template <int MM>
+// DUAL (MM_BITS only): also the backward statistics of a projection shortcut's BN (BnArgs.res /
+// r_mean / r_invstd -> r_stats) from the same g - that BN's own statistics pass re-read dy and the mask
+template <int MM, bool DUAL = false>
 __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   const Slots S(a.C);
   const BwdMask M(a, S.chunk, MM == MM_X);
   constexpr bool need_y = MM == MM_YRELU || MM == MM_YACT;
-  float mean[8], invstd[8];
+  float mean[8], invstd[8], rmean[8], rinv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     mean[e] = a.mean[S.chunk * 8 + e];
     invstd[e] = a.invstd[S.chunk * 8 + e];
+    if (DUAL) {
+      rmean[e] = a.r_mean[S.chunk * 8 + e];
+      rinv[e] = a.r_invstd[S.chunk * 8 + e];
+    }
   }
-  float s[8] = {}, q[8] = {};
-  const long step = (long)gridDim.x * S.rpp * U_STATS;
-  for (long r0 = (long)blockIdx.x * S.rpp * U_STATS + S.slot; r0 < a.R; r0 += step) {
-    u32x4_t dv[U_STATS], xv[U_STATS], yv[U_STATS];
+  constexpr int U = DUAL ? U_STATS / 2 : U_STATS;  // (registers: the shortcut input's loads ride along)
+  float s[8] = {}, q[8] = {}, q2[8] = {};
+  const long step = (long)gridDim.x * S.rpp * U;
+  for (long r0 = (long)blockIdx.x * S.rpp * U + S.slot; r0 < a.R; r0 += step) {
+    u32x4_t dv[U], xv[U], yv[U], zv[U];
 #pragma unroll
-    for (int u = 0; u < U_STATS; ++u) {
+    for (int u = 0; u < U; ++u) {
       const long r = r0 + (long)u * S.rpp;
       const long off = (r < a.R ? r : 0) * a.C + S.chunk * 8;
       dv[u] = ld16(a.dy + off);
       xv[u] = ld16(a.x + off);
       if (need_y) yv[u] = ld16(a.y + off);
       if (MM == MM_BITS) yv[u][0] = a.ymask[off >> 3];
+      if (DUAL) zv[u] = ld16(a.res + off);
     }
 #pragma unroll
-    for (int u = 0; u < U_STATS; ++u) {
+    for (int u = 0; u < U; ++u) {
       const float live = (r0 + (long)u * S.rpp) < a.R ? 1.f : 0.f;
       float g[8], x[8];
       unpack8(xv[u], x);
       masked_grad<MM>(a, M, dv[u], yv[u], x, g);
+      float z[8];
+      if (DUAL) unpack8(zv[u], z);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float gl = g[e] * live;
         s[e] += gl;
         q[e] += gl * (x[e] - mean[e]) * invstd[e];
+        if (DUAL) q2[e] += gl * (z[e] - rmean[e]) * rinv[e];
       }
     }
   }
   reduce_stats(s, q, a.C, a.stats);
+  if constexpr (DUAL) {
+    __syncthreads();  // the LDS scratch is reused
+    reduce_stats(s, q2, a.C, a.r_stats);
+  }
 }
 
 template <int MM>
@@ -792,13 +807,18 @@ void check_bwd(const BnArgs& a) {
 
 void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s) {
   check_bwd(a);
+  if (a.r_stats && (mask_mode(a) != MM_BITS || !a.res || !a.r_mean || !a.r_invstd))
+    throw std::runtime_error("bn_bwd_stats: the shortcut BN's statistics ride along only with a bit mask (res, r_mean, r_invstd)");
   const size_t lds = (size_t)(NT / (a.C / 8)) * 2 * a.C * sizeof(float);
   const dim3 g(stats_grid(a.R, a.C)), b(NT);
   switch (mask_mode(a)) {
     case MM_NONE: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_NONE>, g, b, lds, s, a); break;
     case MM_X: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_X>, g, b, lds, s, a); break;
     case MM_YRELU: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_YRELU>, g, b, lds, s, a); break;
-    case MM_BITS: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_BITS>, g, b, lds, s, a); break;
+    case MM_BITS:
+      if (a.r_stats) hipLaunchKernelGGL((bn_bwd_stats_kernel<MM_BITS, true>), g, b, lds, s, a);
+      else hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_BITS>, g, b, lds, s, a);
+      break;
     default: hipLaunchKernelGGL(bn_bwd_stats_kernel<MM_YACT>, g, b, lds, s, a); break;
   }
 }

@@ -333,13 +333,17 @@ class BN:
         y, beta = self._mask_src(act)
         return (x, y, self.mean, self.invstd, P.view(self.gamma), beta, self.dstats, act)
 
-    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None, stats_done=False, mask=None):
+    def bwd(self, dy, x, dx, act=ops.ACT_RELU, dres=None, stats_done=False, mask=None, res_bn=None):
         """``mask``: a uint8 ReLU bit mask to take act' from instead of this BN's own (a projection
-        shortcut's BN differentiated straight from the block's output gradient and bn3's mask)."""
+        shortcut's BN differentiated straight from the block's output gradient and bn3's mask).
+        ``res_bn`` = (that shortcut BN, its x): its backward statistics ride along in this BN's
+        statistics pass (same g)."""
         P = self.P
         y, beta = (mask, None) if mask is not None else self._mask_src(act)
         if not stats_done:
-            ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta)
+            ops.bn_bwd_stats(dy, y, x, self.mean, self.invstd, self.dstats, act, gamma=P.view(self.gamma), beta=beta,
+                             res_bn=None if res_bn is None else [res_bn[1], res_bn[0].mean, res_bn[0].invstd,
+                                                                 res_bn[0].dstats])
         ops.bn_bwd_apply(dy, y, x, self.mean, self.invstd, P.view(self.gamma), self.dstats, dx, act=act, dres=dres,
                          dgamma=P.gview(self.gamma), dbeta=P.gview(self.beta), beta=beta)
 
@@ -469,7 +473,10 @@ class Bottleneck:
         # landing on the side queue behind the weight gradients - 13 stalls, ~1.5 ms per step
         # (profiles/r4_resnet50_graph_order.txt)
         fork = SideStream.fork_point
-        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres, stats_done=dout_stats_done)
+        # (projection block: the shortcut BN's backward statistics come out of bn3's statistics pass)
+        dual = proj_bits and not dout_stats_done  # 22.19-22.30 vs 22.30-22.41 ms (r4_resnet50_residual_bn_fold_ab)
+        self.bn3.bwd(dout, self.conv3.y, self.dc3, dres=dres, stats_done=dout_stats_done,
+                     res_bn=(self.bns, self.convs.y) if dual else None)
         ev = fork()
         done = self.conv3.dgrad(self.dc3, self.dh2, bn_bwd=self.bn2.bwd_stats_args(self.conv2.y))
         self.conv3.wgrad(self.dc3, self.bn2.y, after=ev)
@@ -482,7 +489,7 @@ class Bottleneck:
         evs = None
         if self.proj:
             if proj_bits:  # g = dout * ReLU'(block output) = what dres held, bit for bit
-                self.bns.bwd(dout, self.convs.y, self.dsc, act=ops.ACT_RELU, mask=self.bn3.ybits)
+                self.bns.bwd(dout, self.convs.y, self.dsc, act=ops.ACT_RELU, mask=self.bn3.ybits, stats_done=dual)
             else:
                 self.bns.bwd(self.dres, self.convs.y, self.dsc, act=ops.ACT_NONE)
             evs = fork()
@@ -715,7 +722,10 @@ class ResNetProgram(StepProgram):
         done = False
         for i in range(len(blocks) - 1, -1, -1):
             if isinstance(blocks[i], Bottleneck):
-                nb = (blocks[i - 1].bn3, blocks[i - 1].conv3.y) if i > 0 else None
+                # (a projection block's bn3 statistics stay with that block: its statistics pass also
+                # produces the shortcut BN's, Bottleneck.bwd)
+                nb = (blocks[i - 1].bn3, blocks[i - 1].conv3.y) if i > 0 and not (
+                    _PROJ_FROM_BITS and blocks[i - 1].proj and blocks[i - 1].bn3.use_bits) else None
                 done = bool(blocks[i].bwd(dout, self.d_in[i], dout_stats_done=done, next_bn=nb))
             else:
                 blocks[i].bwd(dout, self.d_in[i])

@@ -918,17 +918,23 @@ def _masked_grad(dy, y, act, x=None, mean=None, invstd=None, gamma=None, beta=No
     return g
 
 
-def bn_bwd_stats(dy, y, x, mean, invstd, stats, act=ACT_RELU, gamma=None, beta=None):
+def bn_bwd_stats(dy, y, x, mean, invstd, stats, act=ACT_RELU, gamma=None, beta=None, res_bn=None):
     """stats += (sum g, sum g*xhat), g = dy*act'(y).  With y=None and act=ReLU the mask is
-    recomputed from x (the forward had no residual add): pass gamma and beta."""
+    recomputed from x (the forward had no residual add): pass gamma and beta.  ``res_bn`` = [x2,
+    mean2, invstd2, stats2] (y a uint8 ReLU bit mask): the same pass also adds (sum g, sum g*xhat2)
+    into stats2 - a projection shortcut's BN, whose gradient is this g."""
     if x.is_cuda:
-        require().bn_bwd_stats(dy, y, x, mean, invstd, stats, act, gamma, beta)
+        require().bn_bwd_stats(dy, y, x, mean, invstd, stats, act, gamma, beta, res_bn)
         return
     g = _masked_grad(dy, y, act, x, mean, invstd, gamma, beta)
     xh = (_rows(x) - mean) * invstd
     C = g.shape[1]
     stats[:C] += g.sum(0)
     stats[C:] += (g * xh).sum(0)
+    if res_bn is not None:
+        x2, m2, i2, s2 = res_bn
+        s2[:C] += g.sum(0)
+        s2[C:] += (g * ((_rows(x2) - m2) * i2)).sum(0)
 
 
 def bn_bwd_apply(dy, y, x, mean, invstd, gamma, stats, dx, *, act=ACT_RELU, dres=None, dgamma=None, dbeta=None,

@@ -293,3 +293,24 @@ def test_bn_apply_residual_bn_fold_bitwise(shape):
         outs.append((y, bits, m, i, mm, mv, rm, ri, rmm, rmv))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_bn_bwd_stats_dual_matches_two_passes():
+    """bn_bwd_stats(res_bn=[x2, mean2, invstd2, stats2]) == two bn_bwd_stats passes sharing the
+    bit-masked g (the second over x2), to fp32 summation-order tolerance."""
+    torch.manual_seed(10)
+    R, C = 3000, 256
+    x = torch.randn(R, C).to(DEV, torch.bfloat16)
+    x2 = (torch.randn(R, C) * 0.5 + 1).to(DEV, torch.bfloat16)
+    dy = torch.randn(R, C).to(DEV, torch.bfloat16)
+    y = torch.relu(torch.randn(R, C)).to(DEV, torch.bfloat16)
+    bits = ops.relu_bits(y)
+    mean, inv = (torch.randn(C) * 0.1).to(DEV), (torch.rand(C) + 0.5).to(DEV)
+    m2, i2 = (torch.randn(C) * 0.1 + 1).to(DEV), (torch.rand(C) + 1.5).to(DEV)
+    a, b = torch.zeros(2 * C, device=DEV), torch.zeros(2 * C, device=DEV)
+    ops.bn_bwd_stats(dy, bits, x, mean, inv, a, ops.ACT_RELU)
+    ops.bn_bwd_stats(dy, bits, x2, m2, i2, b, ops.ACT_RELU)
+    a2, b2 = torch.zeros(2 * C, device=DEV), torch.zeros(2 * C, device=DEV)
+    ops.bn_bwd_stats(dy, bits, x, mean, inv, a2, ops.ACT_RELU, res_bn=[x2, m2, i2, b2])
+    for u, v in ((a, a2), (b, b2)):
+        assert torch.allclose(u, v, rtol=1e-4, atol=1e-4 * float(u.abs().max()))
