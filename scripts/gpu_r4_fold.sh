@@ -1,0 +1,13 @@
+# ResNet-50 forward BN statistics folded inside the conv launch vs two reduce launches,
+# alternating on one box
+set -o pipefail
+O=gpurun_out/r4fold
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_norm_gpu.py tests/test_resnet.py tests/test_igemm_tiles_gpu.py tests/test_igemm_gpu.py -m gpu > $O/pytest.log 2>&1
+rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
+for r in 1 2 3; do
+  for v in 1 0; do
+    DTFE_BN_FOLD=$v timeout -k 10 300 python3 bench.py --model resnet50 --steps 20 --warmup 5 > $O/r50_${v}_$r.log 2>&1 || { tail -5 $O/r50_${v}_$r.log; exit 1; }
+    echo "fold=$v $(grep -o '"value": [0-9.]*' $O/r50_${v}_$r.log) $(grep -o '"ms_per_step": [0-9.]*' $O/r50_${v}_$r.log)"
+  done
+done

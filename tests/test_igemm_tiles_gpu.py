@@ -169,3 +169,4 @@ def test_igemm_wgrad_all_taps_kernel(case, split):
                     os.environ[k] = v
     assert _rel(out["1"], ref) < 1e-2
     assert _rel(out["1"], out["0"]) < 1e-3
+
