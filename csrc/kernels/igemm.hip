@@ -1178,9 +1178,12 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   int sp = env_int("DTFE_IG_WSPLIT", 0);
   // splits: enough workgroups to fill the chip (target), each split at least 256 rows, and the
   // fp32 partial slabs (splits x weight size, written once and re-read by the reduce) bounded by
-  // part_mb.  ResNet-50 B=256 sweep (profiles/r2_resnet50_wgrad_splits_ab.txt):
-  // 768 WGs / unbounded 27.8 ms -> 512 WGs / 32 MB 27.0 ms per step
-  constexpr long target = 512, part_mb = 32;
+  // part_mb.  ResNet-50 B=256 sweeps: round 2 (profiles/r2_resnet50_wgrad_splits_ab.txt) 768 WGs /
+  // unbounded 27.8 ms -> 512 WGs / 32 MB 27.0 ms per step; round 4, with the weight gradients on
+  // their side stream beside the data-gradient chain (profiles/r4_resnet50_wgrad_target_sweep.txt):
+  // 192 WGs 21.86-21.96 vs 512 22.31-22.35 ms (fewer partial slabs to write and reduce, and CUs
+  // left to the main chain)
+  constexpr long target = 192, part_mb = 32;
   if (sp <= 0) {
     sp = (int)std::max(1L, std::min((target + tiles - 1) / tiles, (M + 255) / 256));
     const long len0 = (long)g.Cout * g.KH * g.KW * g.C;
