@@ -1157,7 +1157,8 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
     const long len = (long)g.Cout * 9 * g.C;
     // one workgroup per CU (the 36 accumulator tiles take the whole register file): aim for one
     // wave of 256 workgroups, at least 4 k-tiles each, fp32 partial slabs up to 40 MB
-    constexpr long target = 256;
+    constexpr long target = 192;  // (256 before round 4's side-stream sweep: 21.66-21.75 vs 21.76-21.81 ms,
+                                  // profiles/r4_resnet50_wgrad_target_sweep.txt)
     long sp = env_int("DTFE_IG_WSPLIT", 0);
     if (sp <= 0) {
       sp = std::max(1L, std::min((target + tiles - 1) / tiles, T / 4));
