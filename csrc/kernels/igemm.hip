@@ -1155,8 +1155,9 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
     const long tiles = (long)(g.Cout / 64) * (g.C / 64);
     const long T = (long)g.B * kpi;
     const long len = (long)g.Cout * 9 * g.C;
-    // one workgroup per CU (the 36 accumulator tiles take the whole register file): aim for one
-    // wave of 256 workgroups, at least 4 k-tiles each, fp32 partial slabs up to 40 MB
+    // one workgroup per CU (the 36 accumulator tiles take the whole register file): aim for 192
+    // workgroups (fewer than the CUs - the data-gradient chain keeps some), at least 4 k-tiles
+    // each, fp32 partial slabs up to 40 MB
     constexpr long target = 192;  // (256 before round 4's side-stream sweep: 21.66-21.75 vs 21.76-21.81 ms,
                                   // profiles/r4_resnet50_wgrad_target_sweep.txt)
     long sp = env_int("DTFE_IG_WSPLIT", 0);
