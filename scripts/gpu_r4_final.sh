@@ -1,7 +1,7 @@
 # Round-4 final check: every GPU test, smoke(), driver-shaped benches (CNN, ps 1+1, ResNet-50), CNN + ResNet-50
 # kernel tables and step timelines (profiled runs without the pre-warm so step counts stay readable)
 set -o pipefail
-O=gpurun_out/r4final
+O=gpurun_out/r4final2
 mkdir -p $O
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
