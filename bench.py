@@ -74,6 +74,13 @@ def parse_args(argv=None):
     ap.add_argument("--ps_overlap", choices=["auto", "on", "off"], default="auto",
                     help="--mode ps: apply pushed buckets during backward (auto: only on a ps GPU other "
                          "than the worker's)")
+    ap.add_argument("--ps_fused_reply", choices=["on", "off"], default="on",
+                    help="--mode ps: async applies write the worker's reply buffer themselves (on) or the ps "
+                         "copies a snapshot into it (off; tests compare the two bit for bit)")
+    ap.add_argument("--ps_stream", default="normal",
+                    help="--mode ps: the ps apply stream - normal, high (highest queue priority) or cu<N> (CU mask "
+                         "of N CUs); the ps shares GPU 0 with worker 0")
+    ap.add_argument("--ps_verify", type=int, default=0, help=argparse.SUPPRESS)  # test hook, see bench_ps
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
     return ap.parse_args(argv)
@@ -439,7 +446,8 @@ def bench_ps(args):
     if job == "ps":
         shard = Shard(shard_specs[0], model.opt_groups, dev, True, model.gs_increments)
         ps = PSServer(server, shard, num_workers=N, comm_device="cpu", log=lambda *_: None)
-        ps.native = ps_native.NativeShardService(server, shard, N, hogwild=args.hogwild)
+        ps.native = ps_native.NativeShardService(server, shard, N, hogwild=args.hogwild,
+                                                 fused_replies=args.ps_fused_reply == "on", stream=args.ps_stream)
         ps.serve_forever()
         st = ps.native.stats()
         ps.native.stop()
@@ -487,6 +495,9 @@ def bench_ps(args):
         def max(x):
             return wsum(x, dist.ReduceOp.MAX)
 
+    if args.ps_verify:
+        _ps_verify(args, run1, link, client, tr, shard_specs, dev, server)
+
     elapsed, win, pre = timed(run1, args.steps, args.warmup, _D, args.prewarm_ms)
     gs = link.host_reply()
     link.check()
@@ -499,8 +510,9 @@ def bench_ps(args):
         rec_extra = {"optimizer": "adam (TF1), applied on the ps", "hip_graph": runner.graph is not None,
                      "last_loss": round(loss, 4), "global_step": gs, "ps_applies": stats.get("applies"),
                      "ps_bucket_applies": stats.get("bucket_applies"),
+                     "ps_refreshed_ranges": stats.get("refreshed_ranges"),
                      "ps_global_step": stats.get("global_step"),
-                     "pushes_issued": pushes, "transport": "hipIpc mailboxes + C++ ps service (bf16 push, bf16 pull)",
+                     "pushes_issued": pushes, "ps_stream": args.ps_stream, "transport": "hipIpc mailboxes + C++ ps service (bf16 push, bf16 pull)",
                      "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": 0,
                      "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
 
@@ -514,6 +526,52 @@ def bench_ps(args):
               "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(), B,
               dict(rec_extra, parallelism="ps1+w%d" % N),
               "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)")
+    _rank_exit()
+
+
+def _ps_verify(args, run1, link, client, tr, shard_specs, dev, server):
+    """--ps_verify K (1 ps + 1 worker, a test hook): K replayed worker steps; after each, the pulled
+    bf16 working copies (natural + transposed) and fp32 variables must equal, bit for bit, what the
+    ps shard's fp32 variables give (fetched over the control channel while the ps is idle - one
+    worker, its push applied).  Prints one JSON line with the per-step digests of the pulled copies
+    (other data-plane variants must reproduce them) and exits."""
+    import hashlib
+
+    from dtfe.optim import FlatParams
+
+    assert args.gpus in (None, 1) and len(shard_specs) == 1, "--ps_verify: 1 ps + 1 worker"
+    specs = shard_specs[0]
+    ref = FlatParams(specs, dev, init=False)
+    digests, mismatches = [], []
+    for i in range(args.ps_verify):
+        run1()
+        link.host_reply()
+        torch.cuda.synchronize()
+        link.check()
+        st, _gs = client.fetch_state()
+        ref.master.copy_(st[0][:ref.total].to(dev))
+        ref.refresh_copies()
+        h = hashlib.sha1()
+        for sp in specs:
+            parts = []
+            if sp.name in ref.w16:
+                parts.append(("w16", tr.P.w16[sp.name], ref.w16[sp.name]))
+            if sp.name in ref.wt16:
+                parts.append(("wt16", tr.P.wt16[sp.name], ref.wt16[sp.name]))
+            if not parts:
+                parts.append(("master", tr.P.view(sp.name), ref.view(sp.name)))
+            for part, got, want in parts:
+                g = got.contiguous().view(-1).view(torch.int16 if got.dtype == torch.bfloat16 else torch.int32)
+                w = want.contiguous().view(-1).view(g.dtype)
+                if not torch.equal(g, w):
+                    mismatches.append({"step": i, "var": sp.name, "part": part,
+                                       "n_diff": int((g != w).sum().item())})
+                h.update(g.cpu().numpy().tobytes())
+        digests.append(h.hexdigest()[:16])
+    print(json.dumps({"ps_verify": digests, "mismatches": mismatches[:20], "n_mismatch": len(mismatches),
+                      "fused_reply": args.ps_fused_reply, "overlap": args.ps_overlap}), flush=True)
+    link.close()
+    client.done()
     _rank_exit()
 
 

@@ -38,7 +38,6 @@ def main():
                                            counter=t.data_ctr, done=t.data_done), 0),
         "conv1_fwd": (lambda: ops.imgconv(t.w["wc1"], t.p1, src=t.x, bias=t.b["bc1"], argmax=t.a1,
                                           act=ops.ACT_RELU, pool=True, **t.ic1), 2.0 * B * 784 * 32 * 25),
-        "conv1_fwd_old": (lambda: ops.conv1_fwd_pool(t.x, t.w["wc1"], t.b["bc1"], t.p1, t.a1), 2.0 * B * 784 * 32 * 25),
         "conv2_fwd": (lambda: ops.imgconv(t.w["wc2"], t.p2, src=t.p1, bias=t.b["bc2"], argmax=t.a2,
                                           act=ops.ACT_RELU, pool=True, **t.ic2), conv2_flops),
         "fc1_fwd": (lambda: ops.gemm(t.p2, t.w["wd1"], t.h, M=B, N=FC, K=K1, bias=t.b["bd1"], act=ops.ACT_RELU,
@@ -64,8 +63,6 @@ def main():
                                                 workspace=t.ws_c2, max_blocks=t.c2_blocks, **t.ic2), conv2_flops),
         "conv1_wgrad": (lambda: ops.imgwgrad(t.x, t.gw["wc1"], t.gw["bc1"], dy_pooled=t.dp1, dy_argmax=t.a1,
                                              **t.ic1), 2.0 * B * 784 * 32 * 25),
-        "conv1_wgrad_old": (lambda: ops.conv1_wgrad_pooled(t.x, t.dp1, t.a1, t.gw["wc1"], t.gw["bc1"]),
-                            2.0 * B * 784 * 32 * 25),
         "adam": (lambda: t.opt.step(), 0),
         "grad_zero": (lambda: t.P.grad.zero_(), 0),
     }

@@ -32,6 +32,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -324,6 +325,7 @@ struct WorkerCh {
   uint64_t bkt_done[dtfe::PS_MAX_BUCKETS] = {};
   uint64_t range_seq = 0;
   std::vector<std::pair<long, long>> ranges;
+  std::vector<uint64_t> range_stamp;  // apply stamp of each entry of `ranges` (Service::stamp)
   // fused replies: per optimizer group, this worker's copy of the group's plan segments with the
   // second destinations (w16b / wt16b / pb) aimed at its reply buffer - the apply writes the
   // reply itself, no snapshot copy; sub-plans by shard range.  Empty: snapshot copies instead.
@@ -344,10 +346,25 @@ struct Service {
   long acc_n = 0;
   int acc_count = 0;
   uint64_t version = 0;
+  // async pulls stay current: every range apply gets a stamp and goes into `log` (bounded); a
+  // worker's bucket range whose reply values were captured at its own apply is re-copied at its
+  // request if another worker applied an overlapping range since (refresh_stale_ranges)
+  struct ApplyRec {
+    long lo, hi;
+    uint64_t stamp;
+    int w;
+  };
+  uint64_t stamp = 0;
+  std::deque<ApplyRec> log;
+  bool fused_replies = true;     // ps_service_set_fused (tests: the snapshot-copy path)
+  // the apply stream on a GPU it shares with a worker (ps_service_set_stream): 1 = the device's
+  // highest queue priority (its workgroups are dispatched ahead of the worker's as CUs free up);
+  // cu_slice > 0 = a CU mask of that many CUs (hipExtStreamCreateWithCUMask)
+  int stream_prio = 0, cu_slice = 0;
   hipStream_t stream = nullptr;
   std::thread th;
   std::atomic<bool> stop{false}, pause{false}, paused{false};
-  std::atomic<int64_t> n_req{0}, n_apply{0}, n_stale{0}, n_bucket{0};
+  std::atomic<int64_t> n_req{0}, n_apply{0}, n_stale{0}, n_bucket{0}, n_refresh{0};
   std::string error;
 };
 std::vector<Service*> g_svc;
@@ -646,11 +663,44 @@ void finish_fused(Service* s, WorkerCh& c, int w, hipStream_t st, uint64_t seq, 
   dtfe::launch_opt_advance_reply(adv.data(), (int)adv.size(), st);
 }
 
+// a range apply of worker w (any path): its stamp, logged for refresh_stale_ranges
+uint64_t note_apply(Service* s, int w, long lo, long hi) {
+  const uint64_t t = ++s->stamp;
+  if (s->nworkers > 1) {
+    s->log.push_back({lo, hi, t, w});
+    if (s->log.size() > 4096) s->log.pop_front();
+  }
+  return t;
+}
+
+// Worker w's bucket ranges were written into its reply buffer when ITS apply ran (fused: by the
+// apply itself; snapshot path: the per-range copy right after it).  A range another worker applied
+// since then would reach w's pull one update late - the reference's pull reads the variable's
+// value at pull time (gan/distributed_gan.py:193) - so it is copied again now.  Every non-hogwild
+// apply and copy runs on the service stream in issue order, so the copy reads the current values.
+// (hogwild: the applies race by design; nothing to refresh against.)
+void refresh_stale_ranges(Service* s, WorkerCh& c, int w, hipStream_t st) {
+  if (s->nworkers < 2 || s->hogwild || c.snap_off.empty()) return;
+  const uint64_t oldest = s->log.empty() ? 0 : s->log.front().stamp;
+  for (size_t i = 0; i < c.ranges.size(); ++i) {
+    const long lo = c.ranges[i].first, hi = c.ranges[i].second;
+    const uint64_t t = i < c.range_stamp.size() ? c.range_stamp[i] : 0;
+    bool stale = t < oldest;  // fell out of the log: copy conservatively
+    for (auto it = s->log.rbegin(); !stale && it != s->log.rend() && it->stamp > t; ++it)
+      stale = it->w != w && it->lo < hi && lo < it->hi;
+    if (stale) {
+      snap_range(s, c, st, lo, hi);
+      s->n_refresh++;
+    }
+  }
+}
+
 // async push with buckets: apply every bucket range of request `seq` not applied yet (the gaps
 // between the ranges already applied - all of the shard when the worker sent no bucket), then
 // advance each group's step scalars once.  Returns true when the reply buffer is already current.
 bool finish_bucketed(Service* s, WorkerCh& c, int w, hipStream_t st, uint64_t seq) {
   std::vector<std::pair<long, long>> done = c.range_seq == seq ? c.ranges : std::vector<std::pair<long, long>>{};
+  if (!done.empty()) refresh_stale_ranges(s, c, w, st);
   std::sort(done.begin(), done.end());
   if (c.fused) {
     std::vector<std::pair<long, long>> todo;
@@ -660,18 +710,27 @@ bool finish_bucketed(Service* s, WorkerCh& c, int w, hipStream_t st, uint64_t se
       at = std::max(at, r.second);
     }
     if (at < s->total) todo.emplace_back(at, s->total);
+    for (const auto& r : todo) note_apply(s, w, r.first, r.second);
     finish_fused(s, c, w, st, seq, s->version + 1, todo);
     c.ranges.clear();
+    c.range_stamp.clear();
     return true;
   }
   long at = 0;
   for (const auto& r : done) {
-    if (r.first > at) apply_bucket(s, c, st, at, r.first);
+    if (r.first > at) {
+      apply_bucket(s, c, st, at, r.first);
+      note_apply(s, w, at, r.first);
+    }
     at = std::max(at, r.second);
   }
-  if (at < s->total) apply_bucket(s, c, st, at, s->total);
+  if (at < s->total) {
+    apply_bucket(s, c, st, at, s->total);
+    note_apply(s, w, at, s->total);
+  }
   for (const auto& g : s->groups) dtfe::launch_opt_advance(g.args, st);
   c.ranges.clear();
+  c.range_stamp.clear();
   return !c.snap_off.empty();
 }
 
@@ -687,6 +746,27 @@ struct AccPlan {
   Tensor blob;
   int64_t nwork = 0;
 };
+
+hipStream_t make_service_stream(int prio, int cu_slice) {
+  hipStream_t st = nullptr;
+  if (cu_slice > 0) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int words = (ncu + 31) / 32;
+    std::vector<uint32_t> mask((size_t)words, 0u);
+    for (int i = 0; i < std::min(cu_slice, ncu); ++i) mask[(size_t)(i / 32)] |= 1u << (i % 32);
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask.data()) == hipSuccess) return st;
+    st = nullptr;
+  }
+  if (prio > 0) {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi) == hipSuccess) return st;
+  }
+  (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  return st;
+}
 
 void run(Service* s) {
   if (hipSetDevice(s->device) != hipSuccess) {
@@ -705,7 +785,7 @@ void run(Service* s) {
     }
     if (s->hogwild) (void)hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
   }
-  (void)hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  s->stream = make_service_stream(s->stream_prio, s->cu_slice);
   (void)hipDeviceSynchronize();
   // accumulate plans for sync mode: mailbox(w) -> acc, mode first/add
   std::vector<AccPlan> acc_first, acc_add;
@@ -757,10 +837,12 @@ void run(Service* s) {
           if (c.range_seq != bseq) {
             c.range_seq = bseq;
             c.ranges.clear();
+            c.range_stamp.clear();
           }
           if (lo < hi) {
             apply_bucket(s, c, bst, lo, hi);
             c.ranges.emplace_back(lo, hi);
+            c.range_stamp.push_back(note_apply(s, w, lo, hi));
             s->n_bucket++;
           }
           any = true;
@@ -846,13 +928,23 @@ void run(Service* s) {
   (void)hipStreamDestroy(s->stream);
 }
 
+// the apply stream's priority / CU slice (see Service::stream_prio); before start
+void ps_service_set_stream(int64_t h, int64_t prio, int64_t cu_slice) {
+  Service* s = svc_of(h);
+  s->stream_prio = (int)prio;
+  s->cu_slice = (int)cu_slice;
+}
+
+// fused replies (default) or the snapshot-copy path for every async channel; before start
+void ps_service_set_fused(int64_t h, bool on) { svc_of(h)->fused_replies = on; }
+
 void ps_service_start(int64_t h) {
   Service* s = svc_of(h);
   TORCH_CHECK(!s->groups.empty(), "dtfe ps: service has no optimizer group");
   for (auto& c : s->ch) TORCH_CHECK(c.mailbox != nullptr, "dtfe ps: every worker channel needs a mailbox");
   TORCH_CHECK(!s->sync || s->acc, "dtfe ps: sync mode needs an accumulator");
   // async channels with per-variable reply segments: replies written by the applies themselves
-  if (!s->sync && (int)s->groups.size() <= dtfe::OPT_GROUP_MAX)
+  if (!s->sync && s->fused_replies && (int)s->groups.size() <= dtfe::OPT_GROUP_MAX)
     for (auto& c : s->ch) build_fused(s, c);
   s->th = std::thread(run, s);
 }
@@ -868,8 +960,9 @@ void ps_service_resume(int64_t h) { svc_of(h)->pause.store(false, std::memory_or
 
 Tensor ps_service_stats(int64_t h) {
   Service* s = svc_of(h);
-  Tensor t = at::empty({5}, at::TensorOptions().dtype(at::kLong));
+  Tensor t = at::empty({6}, at::TensorOptions().dtype(at::kLong));
   t.data_ptr<int64_t>()[4] = s->n_bucket.load();
+  t.data_ptr<int64_t>()[5] = s->n_refresh.load();
   t.data_ptr<int64_t>()[0] = s->n_req.load();
   t.data_ptr<int64_t>()[1] = s->n_apply.load();
   t.data_ptr<int64_t>()[2] = s->n_stale.load();
@@ -927,6 +1020,8 @@ TORCH_LIBRARY_FRAGMENT(dtfe, m) {
   m.def("ps_bucket(int shm, int w, Tensor ctr, int b, int lo, int hi) -> ()", &ps_bucket);
   m.def("ps_service_set_gs(int h, Tensor gs) -> ()", &ps_service_set_gs);
   m.def("ps_service_set_acc(int h, Tensor(a!) acc) -> ()", &ps_service_set_acc);
+  m.def("ps_service_set_fused(int h, bool on) -> ()", &ps_service_set_fused);
+  m.def("ps_service_set_stream(int h, int prio, int cu_slice) -> ()", &ps_service_set_stream);
   m.def("ps_service_start(int h) -> ()", &ps_service_start);
   m.def("ps_service_pause(int h) -> ()", &ps_service_pause);
   m.def("ps_service_resume(int h) -> ()", &ps_service_resume);

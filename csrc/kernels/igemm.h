@@ -47,30 +47,15 @@ struct IgemmArgs {
   // bb_y == nullptr with ReLU: the mask is recomputed from x (norm.hip BwdMask).
   const bf16* bb_x; const bf16* bb_y; const float* bb_mean; const float* bb_invstd;
   const float* bb_gamma; const float* bb_beta; int bb_act;
+  // forward only (optional): fp32 [2][SC] = (sc, sh) - the source is a BatchNorm's input x and the conv
+  // reads h = relu(x * sc + sh) (the BN's apply folded into this operand load; ConvFwdArgs::xf)
+  const float* xf;
   IgPhase ph[4];
-};
-
-// Implicit-GEMM conv as a persistent pipelined GEMM (igemm_pw.hip): GEMM row m is pixel (b, i, j)
-// of an RH x RW grid; tap t reads source pixel (i*istr + dy[t], j*istr + dx[t]) of an SH x SW image
-// (out of image: zeros) and weight tap kt[t]; the result goes to pixel (i*ostr + oy, j*ostr + ox)
-// of an OHf x OWf image.  1x1: one tap (0, 0, 0).
-struct PwArgs {
-  const bf16* A; const bf16* W; bf16* out; const bf16* zeros;
-  bf16* sink;             // 16 KB scratch the epilogue's out-of-range rows store into
-  int M, N, SC, Ktot;     // rows, output channels, source channels, weight row length (taps * SC)
-  int RH, RW, SH, SW, istr, OHf, OWf, ostr, oy, ox;
-  int ntaps;
-  int dy[IG_MAX_TAPS], dx[IG_MAX_TAPS], kt[IG_MAX_TAPS];
-  int accum, tiles_m;
-  float* bn_part;         // [tiles_m][3][N]: forward - shifted BatchNorm partials of the stored output;
-                          // data gradient with bb_x - the consuming BN's backward partials (0, sum g,
-                          // sum g*xhat), g = out * act'(.) (the IgemmArgs bb_* semantics)
-  const bf16* bb_x; const bf16* bb_y; const float* bb_mean; const float* bb_invstd;
-  const float* bb_gamma; const float* bb_beta; int bb_act;
 };
 
 struct IgWgradArgs {
   const bf16* dy; const bf16* x; const bf16* zeros; float* ws;
+  const float* xf;        // optional [2][C] (sc, sh): the operand is relu(x * sc + sh) (ConvWgradArgs::xf)
   int B, H, W, C, OH, OW, Cout, KH, KW, stride, pad;
   int splits, mchunk;
 };
@@ -81,8 +66,6 @@ struct IgWgradArgs {
 // value into stats[2][N], as bn_stats would.  bn_part_buffer: the device scratch for `tiles`
 // tiles plus the fold's chunk table (valid until the next call on this device).
 float* bn_part_buffer(long tiles, int N, hipStream_t s);
-// a 16 KB device page that kernels may write garbage into (per device, created on first use)
-bf16* ig_sink_page(hipStream_t s);
 void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s);
 
 // true when the igemm path handles the conv (and launches it)
@@ -90,8 +73,5 @@ void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, floa
 bool launch_igemm_fwd(const ConvFwdArgs& a, hipStream_t s, bool* stats_done = nullptr);
 bool launch_igemm_dgrad(const ConvDgradArgs& a, hipStream_t s);
 bool launch_igemm_wgrad(const ConvWgradArgs& a, hipStream_t s);
-// the persistent pipelined path (igemm_pw.hip) for one-phase launches without split-K or BN-backward
-// statistics: true when it took the launch (DTFE_PW=off: never; =bb: only data gradients with BN-backward statistics)
-bool run_igemm_pipe(const IgemmArgs& a, long Mmax, hipStream_t s);
 
 }  // namespace dtfe

@@ -13,7 +13,7 @@ __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Hand-off discipline (no release / acquire fences): mailboxes and reply buffers are uncached
+// Hand-off discipline (no release fences; one acquire in ps_wait_kernel): mailboxes and reply buffers are uncached
 // device memory, so a store is in memory once it has completed; every copy kernel drains its
 // stores before it ends (the next kernel of the stream starts after it), and the handshake
 // words are system-scope relaxed stores to the host-mapped page, the sequence number issued
@@ -132,10 +132,15 @@ __global__ void ps_wait_kernel(PsWaitArgs a) {
       __builtin_amdgcn_s_sleep(4);
     }
   }
+  // system-scope acquire: one cache invalidate on the waiting side.  The reply buffers are allocated
+  // uncached by their exporter, but the pull that follows may read them through a hipIpc import on
+  // ANOTHER GPU, whose mapping attributes this code does not control - stale lines of an earlier
+  // reply in that GPU's L2 must not be served to the pull (the release side stays fence-free: its
+  // stores are drained to uncached memory, see the note above)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   if (a.gs_out && a.gs_slot >= 0) *a.gs_out = (int32_t)(int64_t)ld_sys(a.slot[a.gs_slot] + PS_REP_GS);
   if (a.ver_out)  // per shard: each shard's version is the staleness tag of that shard's next request
     for (int k = 0; k < a.nslots; ++k) a.ver_out[k] = (int64_t)ld_sys(a.slot[k] + PS_REP_VER);
-  // (the pull that follows reads uncached reply buffers: nothing to invalidate)
 }
 
 __global__ void ps_reply_kernel(uint64_t* slot, const int32_t* gs, uint64_t seq, uint64_t ver, int stale) {

@@ -132,32 +132,40 @@ class Conv:
         # shortcut share first, then the conv's on top: no separate add pass)
         self.can_accum = not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0
 
-    def fwd(self, x, stats=None):
+    def reads_bn_on_load(self):
+        """Whether forward and weight gradient run on the implicit-GEMM kernels, which can form a
+        preceding BatchNorm + ReLU on their operand loads (ops.conv_fwd / conv_wgrad ``xf``)."""
+        return not self.img_fwd and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0
+
+    def fwd(self, x, stats=None, xf=None):
         """Forward; ``stats``: the following BatchNorm's [2][C] accumulators, filled by the conv
-        launch itself where it can (returns True then; the BN skips its statistics pass)."""
+        launch itself where it can (returns True then; the BN skips its statistics pass).  ``xf``:
+        x is the input of the preceding BatchNorm + ReLU, applied on the operand load (BN.fwd_fold)."""
         if self.img_fwd:
+            assert xf is None
             ops.imgconv(self.w, self.y, src=x, **self.ic)
             return self.y, False
-        ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats)
+        ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats, xf=xf)
         return self.y, stats is not None
 
-    def wgrad(self, dy, x, after=None):
-        """``after``: the side stream's fork point (SideStream.fork_point, taken when dy was final)."""
+    def wgrad(self, dy, x, xf=None, after=None):
+        """``after``: the side stream's fork point (SideStream.fork_point, taken when dy was final).
+        ``xf``: as in fwd."""
         side = getattr(self, "side", None)
         if side is not None and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0:
-            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g), after)
+            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g, xf=xf), after)
             return
         if self.img_wgrad:
+            assert xf is None
             ops.imgwgrad(x, self.gw, None, dy=dy, **self.ic)
         else:
-            ops.conv_wgrad(dy, x, self.gw, None, self.g)
+            ops.conv_wgrad(dy, x, self.gw, None, self.g, xf=xf)
 
     def dgrad_fuses_bn(self, accumulate=False):
-        """Whether this data gradient runs on the one-phase persistent kernel (igemm_pw.hip), whose
-        register epilogue folds the consuming BatchNorm's backward statistics in: every stride-1
-        conv.  (A strided data gradient with statistics needs all its parity phases - the per-tile
-        kernel's LDS epilogue, measured slower than the separate statistics pass,
-        profiles/r2_resnet50_bn_bwd_fuse_ab.txt.)"""
+        """Whether conv_dgrad produces the consuming BatchNorm's backward statistics with dx (every
+        stride-1 implicit-GEMM data gradient: the statistics pass is launched inside conv_dgrad right
+        after the GEMM; the per-tile kernel's LDS epilogue for them measured slower,
+        profiles/r2_resnet50_bn_bwd_fuse_ab.txt)."""
         return not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0 and self.stride == 1
 
     def dgrad(self, dy, dx, accumulate=False, bn_bwd=None, acc_src=None):
@@ -224,6 +232,9 @@ class SideStream:
 
 
 _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
+# (test hook, not a knob: tests compare the folded bn1 / bn2 applies against the materialised ones;
+# DTFE_R5_FOLD=0 only for this round's A/B run, scripts/gpu_r5_fold.sh)
+_FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "1") != "0"
 
 
 class BN:
@@ -246,6 +257,25 @@ class BN:
         self.use_bits = False
         self.stats, self.dstats, self.mean, self.invstd = arena.take(2 * self.C), arena.take(2 * self.C), \
             arena.take(self.C), arena.take(self.C)
+        # (scale, shift) of a folded apply (fwd_fold); outside the zero-per-step arena
+        self.xf = torch.empty(2 * self.C, device=dev)
+        self.folded = False
+
+    def fwd_fold(self, x):
+        """BN + ReLU whose output is read only by implicit-GEMM convs (forward and weight gradient):
+        no apply pass - ops.bn_finalize saves mean / invstd, updates the moving averages and writes
+        (scale, shift) into ``self.xf``, which the consumers apply on their operand loads (h is never
+        stored; bit-identical to bn_apply's output).  The backward recomputes the ReLU mask from x, as
+        after bn_apply.  Returns the raw input x (consumers take ``x, xf=self.xf``)."""
+        P = self.P
+        x, have_stats = x if isinstance(x, tuple) else (x, False)
+        if not have_stats:
+            ops.bn_stats(x, self.stats)
+        ops.bn_finalize(x, self.stats, P.view(self.gamma), P.view(self.beta), self.xf, mean=self.mean,
+                        invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
+                        momentum=BN_MOMENTUM)
+        self.mask_from_x, self.use_bits, self.folded = True, False, True
+        return x
 
     def stats_only(self, x):
         """A projection shortcut's BN (no activation) whose apply is folded into the residual add of
@@ -276,6 +306,7 @@ class BN:
         # the block-output BN's two backward passes read dy, x and the mask, not dy, x and y)
         self.mask_from_x = act == ops.ACT_RELU and res is None
         self.use_bits = act == ops.ACT_RELU and res is not None and self.ybits is not None
+        self.folded = False
         if not have_stats:
             ops.bn_stats(x, self.stats)
         ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
@@ -325,6 +356,11 @@ class BN:
         if act == ops.ACT_NONE or from_x:
             return None, (self.P.view(self.beta) if from_x else None)
         return (self.ybits if self.use_bits and act == ops.ACT_RELU else self.y), None
+
+    def consumer_operand(self, x):
+        """(tensor, xf) a consumer conv's weight gradient reads for this BN's output: (x, xf) when the
+        apply was folded (fwd_fold; ``x`` = this BN's input), else (y, None)."""
+        return (x, self.xf) if self.folded else (self.y, None)
 
     def bwd_stats_args(self, x, act=ops.ACT_RELU):
         """(x, y, mean, invstd, gamma, beta, stats, act) of this BN's backward statistics, for the
@@ -448,9 +484,18 @@ class Bottleneck:
                 res, res_bn = self.bns.stats_only(zs), self.bns
             else:
                 res = self.bns.fwd(zs, act=ops.ACT_NONE)
-        h1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats))
-        h2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats))
-        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats), res=res, rstride=1, res_bn=res_bn)
+        # bn1 / bn2 (+ ReLU) feed only conv2 / conv3 (forward and weight gradient): on the GPU their
+        # applies are folded into those convs' operand loads (BN.fwd_fold, _FOLD_BN_APPLY)
+        fold = x.is_cuda and not self.bn1.infer and _FOLD_BN_APPLY
+        if fold and self.conv2.reads_bn_on_load():
+            h1, xf1 = self.bn1.fwd_fold(self.conv1.fwd(x, self.bn1.stats)), self.bn1.xf
+        else:
+            h1, xf1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats)), None
+        if fold and self.conv3.reads_bn_on_load():
+            h2, xf2 = self.bn2.fwd_fold(self.conv2.fwd(h1, self.bn2.stats, xf=xf1)), self.bn2.xf
+        else:
+            h2, xf2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats, xf=xf1)), None
+        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats, xf=xf2), res=res, rstride=1, res_bn=res_bn)
 
     def bwd(self, dout, dx, dout_stats_done=False, next_bn=None):
         """``next_bn``: (BN, its x) of the layer that consumes dx (the previous block's bn3): its
@@ -479,11 +524,11 @@ class Bottleneck:
                      res_bn=(self.bns, self.convs.y) if dual else None)
         ev = fork()
         done = self.conv3.dgrad(self.dc3, self.dh2, bn_bwd=self.bn2.bwd_stats_args(self.conv2.y))
-        self.conv3.wgrad(self.dc3, self.bn2.y, after=ev)
+        self.conv3.wgrad(self.dc3, *self.bn2.consumer_operand(self.conv2.y), after=ev)
         self.bn2.bwd(self.dh2, self.conv2.y, self.dc2, stats_done=done)
         ev = fork()
         done = self.conv2.dgrad(self.dc2, self.dh1, bn_bwd=self.bn1.bwd_stats_args(self.conv1.y))
-        self.conv2.wgrad(self.dc2, self.bn1.y, after=ev)
+        self.conv2.wgrad(self.dc2, *self.bn1.consumer_operand(self.conv1.y), after=ev)
         self.bn1.bwd(self.dh1, self.conv1.y, self.dc1, stats_done=done)
         ev1 = fork()
         evs = None

@@ -18,6 +18,24 @@ encoder/distributed_encoder.py:165).  On one MI355X node this module replaces th
   request, wait, pull - is one hipGraph replay.  ``launch(i)`` / ``wait()`` are the
   ``BucketAllReduce`` hooks the step programs already call during backward.
 
+Consistency of an async exchange (what a pull returns), against the reference's async PS where
+every ``ApplyAdam`` / ``ApplyRMSProp`` reads the shared ``beta*_power`` / slots at its own time
+and a pull reads each variable's value at pull time (gan/distributed_gan.py:158-159,193):
+
+* a worker's gradient buckets may be applied at different moments (bucket 0 during its backward,
+  the rest at its request).  Every range apply of one push uses the step scalars as they are at
+  that apply (``skip_advance``), and the push's last launch advances them once - so with several
+  workers, another worker's advance can fall between the two buckets of one push and the two
+  ranges see different Adam beta powers.  TF1 behaves the same way (each variable's ApplyAdam
+  reads the shared beta powers independently, ``use_locking=False``); with one worker, or with
+  the whole push applied at the request (the default for a ps on the worker's own GPU), every
+  range of a push sees the same scalars;
+* a range's reply values are written when that worker's own apply of it runs (fused replies) or
+  copied right after it; if ANOTHER worker applied an overlapping range after that, the range
+  is copied again at this worker's request (``refreshed_ranges`` in ``stats()``), so a pull
+  returns the values current at reply time, as the reference's does.  --hogwild applies race by
+  design and are not refreshed.
+
 Everything is keyed by the cluster spec in the TCPStore (shm name, IPC handle, buffer
 sizes), and each shard's layout is the same ``FlatParams`` offsets on both sides, so a worker
 needs no gather / scatter index tensors.  Control messages (INIT, SAVE, SET_STATE, STATUS,
@@ -104,7 +122,12 @@ class NativeShardService:
     """ps task side: the shard's mailboxes / reply buffers, shared page and progress thread."""
 
     def __init__(self, server, shard, num_workers: int, sync: bool = False, replicas_to_aggregate=None,
-                 hogwild: bool = False, timeout_s: float = 60.0):
+                 hogwild: bool = False, timeout_s: float = 60.0, fused_replies: bool = True,
+                 stream: str = "normal"):
+        """``fused_replies``: async applies write each worker's reply buffer themselves (default);
+        False keeps the snapshot copies (bitwise the same pulls - tests/test_cluster_gpu.py).
+        ``stream``: the apply stream - "normal", "high" (highest queue priority) or "cu<N>" (a
+        mask of N CUs), for a ps sharing its GPU with a worker (bench.py --ps_stream)."""
         ops.require()
         lib = torch.ops.dtfe
         self.lib = lib
@@ -123,6 +146,9 @@ class NativeShardService:
         base = lib.ps_ipc_ptr(self.buf)
         R = replicas_to_aggregate or num_workers
         self.svc = lib.ps_service_create(self.shm, num_workers, dev.index or 0, sync, R, hogwild)
+        lib.ps_service_set_fused(self.svc, bool(fused_replies))
+        prio, cus = (1, 0) if stream == "high" else ((0, int(stream[2:])) if stream.startswith("cu") else (0, 0))
+        lib.ps_service_set_stream(self.svc, prio, cus)
         g16 = self.dtype == "bf16"
         last = len(shard.opts) - 1
         for i, o in enumerate(shard.opts):
@@ -176,8 +202,8 @@ class NativeShardService:
             self.lib.ps_service_resume(self.svc)
 
     def stats(self):
-        r, a, s, v, b = [int(x) for x in self.lib.ps_service_stats(self.svc)]
-        return {"requests": r, "applies": a, "stale": s, "version": v, "bucket_applies": b}
+        r, a, s, v, b, f = [int(x) for x in self.lib.ps_service_stats(self.svc)]
+        return {"requests": r, "applies": a, "stale": s, "version": v, "bucket_applies": b, "refreshed_ranges": f}
 
     def stop(self):
         if getattr(self, "started", False):

@@ -424,9 +424,10 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None, store=
         if (flags.phase_timers or flags.trace_json) else None
     phase = timer.phase if timer else (lambda _n: contextlib.nullcontext())
     faults = FaultInjector("worker", rank, log=log)
-    # failure detection: with --heartbeat_secs every rank beats into the TCPStore and a
-    # watchdog thread aborts the collectives and ends this rank when a peer goes silent / the store
-    # vanishes / RCCL reports an error - the step graph itself would wait on a dead peer forever
+    # failure detection, on by default in this mode (utils/flags.py resolve_mode): every
+    # rank beats into the TCPStore and a watchdog thread aborts the collectives and ends this rank when
+    # a peer goes silent (or never beats) / the store vanishes / RCCL reports an error - the step graph
+    # itself would wait on a dead peer forever
     hb = wd = None
     if world > 1 and store is not None and flags.heartbeat_secs > 0:
         hb = Heartbeat(store, "worker", rank, flags.heartbeat_secs)
@@ -483,6 +484,7 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None, store=
             local_step += 1
         if wd is not None:  # training is over: peers may now leave at their own pace
             wd.stop()
+            _leave_watchdog(store, rank, world, flags.heartbeat_timeout)
         if ar is not None and ar.comm is not None:
             ar.comm.check_health()
         prog.check_health()
@@ -503,6 +505,19 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None, store=
             timer.close()
         sv.stop()
     return prog, opts, gstep
+
+
+def _leave_watchdog(store, rank, world, timeout_s):
+    """End of training with the comm watchdog on: the TCPStore lives in rank 0's process, so rank 0
+    waits (bounded) until every rank has stopped its watchdog before it can exit - a peer still
+    polling would otherwise read the vanished store as a failure."""
+    key = "dtfe/hb/watchdogs_stopped"
+    store.add(key, 1)
+    if rank != 0:
+        return
+    t_end = time.time() + timeout_s
+    while store.add(key, 0) < world and time.time() < t_end:
+        time.sleep(0.01)
 
 
 def _ps_buckets(prog, bucket_mb=None):
@@ -546,7 +561,7 @@ def run(model_name: str, argv=None, log=_print):
         raise SystemExit(str(e))
     torch.manual_seed(flags.seed)
     np.random.seed(flags.seed)
-    mode = flags.mode or ("ps" if flags.ps_hosts else ("allreduce" if flags.worker_hosts else "local"))
+    mode = flagmod.resolve_mode(flags)  # (+ mode-dependent defaults: --heartbeat_secs)
     local_rank = int(os.environ.get("LOCAL_RANK", flags.task_index if flags.job_name == "worker" else 0))
     device = resolve_device(flags.device, local_rank)
     if device.type == "cuda":

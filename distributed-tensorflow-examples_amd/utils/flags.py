@@ -26,6 +26,21 @@ def add_bool(ap, name, default, help_):
     ap.add_argument("--no" + name, dest=name, action="store_false", help=argparse.SUPPRESS)
 
 
+# --heartbeat_secs default of --mode=allreduce: a survivor's watchdog aborts the collectives and exits
+# non-zero --heartbeat_timeout seconds after a peer's last beat (parallel/health.py CommWatchdog)
+AR_HEARTBEAT_SECS = 1.0
+
+
+def resolve_mode(flags) -> str:
+    """The run mode (explicit --mode, else ps when --ps_hosts is set, else allreduce when
+    --worker_hosts is, else local) with the mode-dependent defaults filled in: --heartbeat_secs
+    (None -> AR_HEARTBEAT_SECS for allreduce, 0 otherwise)."""
+    mode = flags.mode or ("ps" if flags.ps_hosts else ("allreduce" if flags.worker_hosts else "local"))
+    if flags.heartbeat_secs is None:
+        flags.heartbeat_secs = AR_HEARTBEAT_SECS if mode == "allreduce" else 0.0
+    return mode
+
+
 def build_parser(model_defaults: dict | None = None, prog=None):
     d = dict(batch_size=None, num_steps=None, learning_rate=None)
     if model_defaults:
@@ -78,8 +93,10 @@ def build_parser(model_defaults: dict | None = None, prog=None):
                     help="--mode=ps data plane: native = hipIpc mailboxes + C++ service thread (one node, GPUs; "
                          "parallel/ps_native.py), pg = torch.distributed send/recv; auto = native when eligible")
     ap.add_argument("--metrics_jsonl", default="", help="append {step, gs, ms, images/sec, loss} lines here")
-    ap.add_argument("--heartbeat_secs", type=float, default=0.0,
-                    help="publish a TCPStore heartbeat every N s (0: off, the reference has none)")
+    ap.add_argument("--heartbeat_secs", type=float, default=None,
+                    help="publish a TCPStore heartbeat every N s; 0: off.  Default: %s s in --mode=allreduce "
+                         "(failure detection on: a dead peer ends every rank), 0 in --mode=ps / local (the "
+                         "reference has no heartbeat)" % AR_HEARTBEAT_SECS)
     ap.add_argument("--heartbeat_timeout", type=float, default=30.0,
                     help="ps: count a worker silent for this long as lost; all-reduce: a rank whose peer "
                          "is silent this long aborts the collectives and exits non-zero (with --heartbeat_secs)")

@@ -15,7 +15,7 @@ rows = []
 for f in files:
     rs = list(csv.DictReader(open(f)))
     names = {r["Kernel_Name"] for r in rs}
-    role = "ps" if any("ps_reply" in n or "ps_apply" in n for n in names) else "worker"
+    role = "worker" if any("conv1c_fwd" in n for n in names) else "ps"
     for r in rs:
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), role, r.get("Queue_Id", "?"), r["Kernel_Name"]))
 rows.sort()

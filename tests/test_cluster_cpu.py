@@ -120,6 +120,20 @@ def test_allreduce_mode_two_workers(tmp_path):
     assert _gs_lines(out[("worker", 1)]) == [1, 2, 3, 4, 5]
 
 
+def test_allreduce_rank_crash_ends_every_rank_cpu(tmp_path):
+    """--mode=allreduce with default flags (no --heartbeat_secs): worker 1 crashes at step 5, worker
+    0 must not hang - its comm watchdog (on by default in this mode) or the gloo collective ends it
+    with a non-zero code."""
+    env = dict(os.environ, DTFE_FAULT="crash@worker:1:step=5")
+    t0 = time.time()
+    codes, out, _ = local_cluster.launch("encoder", 0, 2, COMMON + [
+        "--num_steps=100000", "--mode=allreduce", "--batch_size=32", "--save_model_secs=0",
+        "--heartbeat_timeout=3", "--model_dir=" + str(tmp_path)], env=env, timeout=200, stream=False)
+    assert time.time() - t0 < 150
+    assert codes[("worker", 1)] == 17, out[("worker", 1)][-10:]
+    assert codes[("worker", 0)] not in (0, None), (codes, out[("worker", 0)][-20:])
+
+
 def test_killed_non_chief_worker_does_not_stall_others(tmp_path):
     """device_filters semantics: worker 1 dies, worker 0 finishes; the ps keeps waiting
     for the missing done signal exactly like the reference (C07) until we stop it."""

@@ -71,12 +71,13 @@ def test_cnn_allreduce_two_workers_ipc_in_graph(tmp_path):
 def test_allreduce_rank_crash_ends_every_rank(tmp_path):
     """--mode=allreduce, 2 workers sharing cuda:0 (gloo + in-graph IPC all-reduce), worker 1 crashes
     at step 5 (DTFE_FAULT): worker 0's step graph would wait on the dead peer; its comm watchdog
-    sees the silent heartbeat, aborts the collectives and exits non-zero - no rank hangs."""
+    sees the silent heartbeat, aborts the collectives and exits non-zero - no rank hangs.  No
+    --heartbeat_secs: failure detection is on by default in --mode=allreduce."""
     import time
 
     extra = ["--mode=allreduce", "--device=cuda", "--backend=gloo", "--comm=ipc", "--comm_dtype=bf16",
              "--synthetic", "--num_steps=400", "--batch_size=128", "--model_dir=" + str(tmp_path / "ck"),
-             "--save_model_secs=0", "--heartbeat_secs=0.5", "--heartbeat_timeout=6"]
+             "--save_model_secs=0", "--heartbeat_timeout=6"]
     env = dict(os.environ, DTFE_FAULT="crash@worker:1:step=5")
     t0 = time.time()
     codes, out, _ = local_cluster.launch("cnn", 0, 2, extra, env=env, timeout=240, stream=False, gpus=1)
@@ -116,3 +117,35 @@ def test_bench_ps_native_plane(hogwild):
     assert c["ps_bucket_applies"] == (0 if hogwild else 2 * 1 * n)
     assert c["ps_global_step"] == 2 * n and 0 < c["global_step"] <= 2 * n
     assert 0.0 < c["last_loss"] < 10.0
+    # with announced buckets, the other worker's bucket applies land between a worker's own bucket
+    # apply and its request: those ranges are re-copied into its reply (the pull is current)
+    if not hogwild:
+        assert c["ps_refreshed_ranges"] > 0
+
+
+def _ps_verify(extra):
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--mode", "ps", "--gpus", "1", "--ps_verify", "6",
+           "--batch_size", "256", "--prewarm_ms", "0"] + extra
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    return json.loads([l for l in p.stdout.splitlines() if l.startswith('{"ps_verify"')][-1])
+
+
+def test_ps_replies_bitwise_across_data_plane_variants():
+    """1 ps + 1 worker (async, one GPU): after every exchange the worker's pulled bf16 copies
+    (natural + transposed) and fp32 variables equal, bit for bit, the ps shard's variables (fetched
+    over the control channel); and the fused-reply path (the apply writes the reply buffer, default),
+    the snapshot-copy path, and the bucket announcements on / off all give the same pulled
+    parameters, step by step."""
+    variants = [[], ["--ps_overlap", "on"], ["--ps_fused_reply", "off"],
+                ["--ps_fused_reply", "off", "--ps_overlap", "on"]]
+    recs = [_ps_verify(v) for v in variants]
+    for v, r in zip(variants, recs):
+        assert r["n_mismatch"] == 0, (v, r["mismatches"])
+    for v, r in zip(variants[1:], recs[1:]):
+        assert r["ps_verify"] == recs[0]["ps_verify"], (v, r["ps_verify"], recs[0]["ps_verify"])
+    assert len(set(recs[0]["ps_verify"])) == len(recs[0]["ps_verify"])  # the parameters do move

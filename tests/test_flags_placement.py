@@ -23,6 +23,22 @@ def test_reference_flag_defaults_and_absl_syntax():
         flags.parse(["--not_a_flag=1"])
 
 
+def test_heartbeat_default_per_mode():
+    """Failure detection is on by default in --mode=allreduce and off in --mode=ps / local (the
+    reference has no heartbeat); an explicit value always wins."""
+    a = flags.parse(["--worker_hosts=w0:1,w1:2"])
+    assert a.heartbeat_secs is None
+    assert flags.resolve_mode(a) == "allreduce" and a.heartbeat_secs == flags.AR_HEARTBEAT_SECS > 0
+    a = flags.parse(["--ps_hosts=p:1", "--worker_hosts=w0:1"])
+    assert flags.resolve_mode(a) == "ps" and a.heartbeat_secs == 0.0
+    a = flags.parse([])
+    assert flags.resolve_mode(a) == "local" and a.heartbeat_secs == 0.0
+    a = flags.parse(["--worker_hosts=w0:1", "--heartbeat_secs=0"])
+    assert flags.resolve_mode(a) == "allreduce" and a.heartbeat_secs == 0.0
+    a = flags.parse(["--ps_hosts=p:1", "--mode=allreduce", "--heartbeat_secs=2.5"])
+    assert flags.resolve_mode(a) == "allreduce" and a.heartbeat_secs == 2.5
+
+
 def test_model_hyperparameter_defaults():
     a = flags.parse([], model_defaults=dict(batch_size=128, num_steps=100000, learning_rate=0.0002))
     assert (a.batch_size, a.num_steps, a.learning_rate) == (128, 100000, 0.0002)

@@ -8,7 +8,7 @@ import pytest
 import torch.distributed as dist
 
 from dtfe.parallel import comm as commmod
-from dtfe.parallel.health import CommWatchdog, Heartbeat
+from dtfe.parallel.health import BeatTracker, CommWatchdog, Heartbeat, Watchdog, hb_key
 
 
 class FakeEngine:
@@ -76,3 +76,38 @@ def test_watchdog_aborts_on_rccl_async_error():
     eng._status = 6
     assert done.wait(5.0) and eng.aborted
     wd.stop()
+
+
+def test_watchdog_aborts_when_a_peer_never_beats():
+    """A peer that died before its heartbeat thread started (comm setup, first capture) counts as
+    silent once the timeout has passed since the watchdog started."""
+    store = _store()
+    hb0 = Heartbeat(store, "worker", 0, 0.1)
+    codes = []
+    done = threading.Event()
+    wd = CommWatchdog(store, "worker", 0, 2, comm=None, interval=0.1, timeout=0.6, log=lambda m: None,
+                      exit_fn=lambda c: (codes.append(c), done.set()))
+    assert done.wait(5.0) and codes == [3]
+    wd.stop()
+    hb0.stop()
+
+
+def test_beat_ages_use_the_local_clock():
+    """A peer whose wall clock is far behind (or ahead) of ours is not silent while its beat
+    counter advances: ages come from this process's monotonic clock."""
+    store = _store()
+    tr = BeatTracker(store)
+    age, beaten = tr.age("worker", 1)
+    assert not beaten and age < 1.0
+    for n in range(1, 4):
+        store.set(hb_key("worker", 1), "%d %.3f" % (n, time.time() - 3600.0))   # an hour of clock skew
+        age, beaten = tr.age("worker", 1)
+        assert beaten and age < 0.5
+        time.sleep(0.05)
+    time.sleep(0.3)
+    age, _ = tr.age("worker", 1)     # no new beat: silence grows on our clock
+    assert 0.25 < age < 5.0
+    # the ps-side tracker ignores workers that never started (they may still join)
+    wd = Watchdog(store, [("worker", 2)], timeout=0.1)
+    time.sleep(0.2)
+    assert wd.poll() == []

@@ -76,11 +76,9 @@ def test_igemm_fwd_dgrad_wgrad(case, tile):
     assert _rel(dw - 0.5, ref_dw) < 1e-3
 
 
-@pytest.mark.parametrize("wpipe", ["0", "1", "2"])
 @pytest.mark.parametrize("case", CASES)
-def test_igemm_wgrad_pipelines(case, wpipe, monkeypatch):
-    """Every k-tile depth / LDS ring of the weight-gradient kernel (DTFE_IG_WPIPE) against fp32."""
-    monkeypatch.setenv("DTFE_IG_WPIPE", wpipe)
+def test_igemm_wgrad_per_tap(case, monkeypatch):
+    """The per-tap weight-gradient kernel (4-stage ring of 32-pixel k-tiles) against fp32."""
     monkeypatch.setenv("DTFE_IG_W3", "0")   # the per-tap kernel for the 3x3 shapes too
     B, H, C, Cout, k, s = case
     g = _geom(B, H, C, Cout, k, s)

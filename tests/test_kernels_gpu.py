@@ -247,32 +247,6 @@ def test_conv_wgrad(g):
     assert _rel(db.cpu(), dbr) < 1e-2
 
 
-def test_conv1_dedicated_kernels():
-    torch.manual_seed(11)
-    B = 6
-    x = torch.rand(B, 28, 28, 1).to(DEV, torch.bfloat16)
-    w = (torch.randn(32, 5, 5, 1) * 0.3).to(DEV, torch.bfloat16)
-    b = torch.randn(32, device=DEV) * 0.1
-    y = torch.empty(B, 14, 14, 32, device=DEV, dtype=torch.bfloat16)
-    am = torch.empty(B, 14, 14, 32, device=DEV, dtype=torch.uint8)
-    ops.conv1_fwd_pool(x, w, b, y, am)
-    yr = torch.empty(y.shape)
-    amr = torch.empty(y.shape, dtype=torch.uint8)
-    ops.conv1_fwd_pool(x.cpu(), w.cpu(), b.cpu(), yr, amr)
-    assert _rel(y.cpu(), yr) < 2e-2
-    pos = yr > 0.05
-    assert (am.cpu()[pos] == amr[pos]).float().mean().item() > 0.97
-    # weight gradient from the pooled gradient: use the kernel's own argmax for both paths
-    dp = (torch.randn(B, 14, 14, 32) * (yr > 0)).to(DEV, torch.bfloat16)
-    dw = torch.zeros(32, 5, 5, 1, device=DEV)
-    db = torch.zeros(32, device=DEV)
-    ops.conv1_wgrad_pooled(x, dp, am, dw, db, scale=0.5)
-    dwr, dbr = torch.zeros(32, 5, 5, 1), torch.zeros(32)
-    ops.conv1_wgrad_pooled(x.cpu(), dp.cpu(), am.cpu(), dwr, dbr, scale=0.5)
-    assert _rel(dw.cpu(), dwr) < 1e-3
-    assert _rel(db.cpu(), dbr) < 1e-3
-
-
 def test_conv_dgrad_relu_mask():
     g = CONV_CASES[1]
     torch.manual_seed(12)

@@ -300,16 +300,12 @@ BN_BWD_CASES = [  # (B, H, Cin, Cout, K, stride, accumulate, mask)  - dgrad shap
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipe", ["1", "0"])
 @pytest.mark.parametrize("case", BN_BWD_CASES)
-def test_conv_dgrad_bn_bwd_stats_gpu(case, pipe, monkeypatch):
-    """conv_dgrad(bn_bwd=...) fills the consuming BN's backward statistics from the implicit-GEMM
-    epilogue; they must equal a separate bn_bwd_stats pass over the same finished dx.  pipe=1: the
-    persistent pipelined kernel's register epilogue (igemm_pw.hip) wherever the launch has one
-    phase; pipe=0: the per-tile kernel's LDS epilogue (strided) or the separate statistics pass
-    (one phase)."""
+def test_conv_dgrad_bn_bwd_stats_gpu(case):
+    """conv_dgrad(bn_bwd=...) fills the consuming BN's backward statistics (the per-tile kernel's LDS
+    epilogue for a strided data gradient, the separate statistics pass after a one-phase one); they
+    must equal a separate bn_bwd_stats pass over the same finished dx."""
     from dtfe import ops
-    monkeypatch.setenv("DTFE_PW", "all,mintiles=1" if pipe == "1" else "off")
     B, H, C, CO, K, s, acc, mask = case
     dev = torch.device("cuda", 0)
     pad = (K - 1) // 2
@@ -423,3 +419,114 @@ def test_resnet50_projection_bn_from_bits_matches(monkeypatch):
     noise = float((grads[0] - grads[1]).abs().max())
     cross = float((grads[0] - grads[2]).abs().max())
     assert cross <= 4 * noise + 1e-6 * float(grads[0].abs().max()), (cross, noise)
+
+
+XF_CASES = [
+    (2, 56, 64, 64, 3, 1),      # the all-taps 3x3 weight-gradient kernel (igemm_wgrad3)
+    (2, 14, 256, 256, 3, 1),
+    (2, 28, 128, 128, 3, 2),    # strided: out-of-image taps on the bottom / right edge
+    (3, 7, 512, 2048, 1, 1),    # M = 147: rows past the end of the last tile
+    (2, 14, 256, 1024, 1, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", XF_CASES)
+def test_conv_bn_on_load_matches_materialised_gpu(case):
+    """bn_finalize + conv_fwd / conv_wgrad(xf=...) - the BatchNorm + ReLU formed on the implicit-GEMM
+    operand loads - against bn_apply's stored output fed to the same convs: the saved statistics and
+    moving averages, the conv output, its fused BN statistics and the weight gradient are bit-identical
+    (zero padding of h, not of x, at the image border)."""
+    from dtfe import ops
+    B, H, C, CO, K, s = case
+    pad = (K - 1) // 2
+    OH = (H + 2 * pad - K) // s + 1
+    g = dict(B=B, H=H, W=H, C=C, Cout=CO, OH=OH, OW=OH, KH=K, KW=K, stride=s, pad=pad)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1)
+    x = (torch.randn(B, H, H, C, device=dev) * 1.5 + 0.3).to(torch.bfloat16)
+    w = (torch.randn(CO, K, K, C, device=dev) / (K * K * C) ** 0.5).to(torch.bfloat16)
+    dy = torch.randn(B, OH, OH, CO, device=dev).to(torch.bfloat16)
+    gamma, beta = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.5
+    stats = torch.zeros(2 * C, device=dev)
+    ops.bn_stats(x, stats)
+    outs = []
+    for fold in (False, True):
+        mean, inv = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        mm, mv = torch.full((C,), 0.1, device=dev), torch.full((C,), 2.0, device=dev)
+        xf = torch.empty(2 * C, device=dev)
+        if fold:
+            ops.bn_finalize(x, stats, gamma, beta, xf, mean=mean, invstd=inv, moving_mean=mm, moving_var=mv)
+            src, kw = x, dict(xf=xf)
+        else:
+            h = torch.empty_like(x)
+            ops.bn_apply(x, stats, gamma, beta, h, mean=mean, invstd=inv, moving_mean=mm, moving_var=mv)
+            src, kw = h, {}
+        y = torch.empty(B, OH, OH, CO, dtype=torch.bfloat16, device=dev)
+        yst = torch.zeros(2 * CO, device=dev)
+        ops.conv_fwd(src, w, None, y, None, g, act=ops.ACT_NONE, stats=yst, **kw)
+        dw = torch.zeros(CO, K, K, C, device=dev)
+        ops.conv_wgrad(dy, src, dw, None, g, **kw)
+        torch.cuda.synchronize()
+        outs.append((mean, inv, mm, mv, y, yst, dw))
+    names = ("mean", "invstd", "moving_mean", "moving_var", "y", "y_stats", "dw")
+    for n, a, b in zip(names, outs[0], outs[1]):
+        assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
+
+
+@pytest.mark.gpu
+def test_resnet50_folded_bn_applies_match(monkeypatch):
+    """ResNet-50 step with bn1 / bn2 folded into conv2 / conv3's operand loads (default) against the
+    materialised applies: the same gradients up to the run-to-run order of the BN statistics'
+    atomics (measured between two runs of the materialised path)."""
+    from dtfe.models import resnet as rn
+
+    model = ResNetModel(arch="resnet50")
+    torch.manual_seed(0)
+    B = 2
+    x = torch.rand(B, 224, 224, 3).cuda()
+    y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,)), 1000).float().cuda()
+    grads, losses = [], []
+    for flag in (False, False, True):
+        monkeypatch.setattr(rn, "_FOLD_BN_APPLY", flag)
+        prog = model.program("cuda", B, seed=1)
+        prog.load_batch((x, y))
+        m = prog.compute_grads()
+        torch.cuda.synchronize()
+        grads.append(prog.P.grad.clone())
+        losses.append(float(prog.loss.item()))
+        folded = sum(1 for b in prog.L["blocks"] for bn in (b.bn1, b.bn2) if bn.folded)
+        assert folded == (32 if flag else 0)
+    noise = float((grads[0] - grads[1]).abs().max())
+    cross = float((grads[0] - grads[2]).abs().max())
+    assert cross <= 4 * noise + 1e-6 * float(grads[0].abs().max()), (cross, noise)
+    assert abs(losses[2] - losses[0]) <= 1e-4 * abs(losses[0]) + 1e-6
+
+
+def test_bn_finalize_and_xf_reference_cpu():
+    """CPU reference of the folded apply: bn_finalize's (scale, shift) fed to conv_fwd / conv_wgrad(xf)
+    equals bn_apply(ReLU) fed to the plain convs (fp32 tensors: the same math up to rounding)."""
+    from dtfe import ops
+    B, H, C, CO, K = 2, 6, 8, 4, 3
+    g = dict(B=B, H=H, W=H, C=C, Cout=CO, OH=H, OW=H, KH=K, KW=K, stride=1, pad=1)
+    torch.manual_seed(3)
+    x = torch.randn(B, H, H, C) + 0.2
+    w = torch.randn(CO, K, K, C) * 0.3
+    dy = torch.randn(B, H, H, CO)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.5
+    st = torch.zeros(2 * C)
+    ops.bn_stats(x, st)
+    m1, i1, m2, i2 = torch.zeros(C), torch.zeros(C), torch.zeros(C), torch.zeros(C)
+    h = torch.empty_like(x)
+    ops.bn_apply(x, st, gamma, beta, h, mean=m1, invstd=i1)
+    xf = torch.empty(2 * C)
+    ops.bn_finalize(x, st, gamma, beta, xf, mean=m2, invstd=i2)
+    assert torch.allclose(m1, m2) and torch.allclose(i1, i2)
+    y1, y2 = torch.empty(B, H, H, CO), torch.empty(B, H, H, CO)
+    ops.conv_fwd(h, w, None, y1, None, g, act=ops.ACT_NONE)
+    ops.conv_fwd(x, w, None, y2, None, g, act=ops.ACT_NONE, xf=xf)
+    assert torch.allclose(y1, y2, atol=1e-5)
+    d1, d2 = torch.zeros(CO, K, K, C), torch.zeros(CO, K, K, C)
+    ops.conv_wgrad(dy, h, d1, None, g)
+    ops.conv_wgrad(dy, x, d2, None, g, xf=xf)
+    assert torch.allclose(d1, d2, atol=1e-4)
