@@ -8,7 +8,12 @@ with the 6.5 MB bf16 fc-bucket all-reduce launched concurrently on a third strea
 takes part in the all-reduce.  The IPC kernel's workgroups spin on their barriers while the
 peer's half has not arrived, so they hold CUs the conv kernels could use.
 
-    python bench/ipc_interference.py [--batch 1024] [--reps 50]
+    python bench/ipc_interference.py [--batch 1024] [--reps 50] [--caps 128,64,32,16]
+
+Sweeps the all-reduce kernel's grid cap (IpcComm.set_max_blocks).  Caveat: both ranks run on the
+same GPU here, so the all-reduce's kernels of BOTH ranks share the conv kernels' CUs and every
+peer read is a local HBM read; on a node each GPU hosts one rank and the peer reads cross xGMI -
+the interference and the all-reduce time both differ there.
 
 (self-launches its two ranks; one GPU)
 """
@@ -68,23 +73,23 @@ def child(rank, port, args):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1000 / reps
 
-    rows = []
-    for rnd in range(3):
-        if rank == 0:
-            t_conv = timed(convs, args.reps)
-        else:
-            dist.barrier()
-        t_ar = timed(allreduce, args.reps)
-        if rank == 0:
-            t_both = timed(lambda: (allreduce(), convs()), args.reps)
-        else:
-            t_both = timed(allreduce, args.reps)
-        rows.append((t_conv if rank == 0 else 0.0, t_ar, t_both))
-    if rank == 0:
-        for t_conv, t_ar, t_both in rows:
-            print("conv2 dgrad+wgrad alone %.1f us | fc-bucket IPC all-reduce alone %.1f us | both concurrent %.1f us"
-                  " | interference on the convs %+.1f %%" % (t_conv, t_ar, t_both, 100.0 * (t_both - t_conv) / t_conv),
-                  flush=True)
+    caps = [int(c) for c in args.caps.split(",")]
+    for rnd in range(2):
+        for cap in caps:
+            comm.set_max_blocks(cap)
+            if rank == 0:
+                t_conv = timed(convs, args.reps)
+            else:
+                dist.barrier()
+            t_ar = timed(allreduce, args.reps)
+            if rank == 0:
+                t_both = timed(lambda: (allreduce(), convs()), args.reps)
+            else:
+                t_both = timed(allreduce, args.reps)
+            if rank == 0:
+                print("grid cap %3d | conv2 dgrad+wgrad alone %.1f us | fc-bucket IPC all-reduce alone %.1f us | "
+                      "both concurrent (span) %.1f us | serial sum %.1f us | interference on the convs %+.1f %%"
+                      % (cap, t_conv, t_ar, t_both, t_conv + t_ar, 100.0 * (t_both - t_conv) / t_conv), flush=True)
     comm.close()
     dist.destroy_process_group()
 
@@ -93,6 +98,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--caps", default="128,64,32,16", help="all-reduce grid caps to sweep")
     ap.add_argument("--child", type=int, default=-1)
     ap.add_argument("--port", type=int, default=0)
     a = ap.parse_args()
@@ -105,7 +111,7 @@ def main():
     port = s.getsockname()[1]
     s.close()
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", str(r), "--port", str(port),
-                               "--batch", str(a.batch), "--reps", str(a.reps)]) for r in range(2)]
+                               "--batch", str(a.batch), "--reps", str(a.reps), "--caps", a.caps]) for r in range(2)]
     codes = [p.wait() for p in procs]
     sys.exit(max(codes))
 

@@ -50,6 +50,13 @@ __device__ __forceinline__ float apply_act(float x, int act) {
   }
 }
 
+// BatchNorm affine with ONE rounding, written out: y = x * scale + shift with scale = gamma * invstd,
+// shift = beta - mean * scale.  Every kernel that forms a BN output or recomputes its ReLU mask from x
+// (bn_apply, bn_finalize + the implicit-GEMM operand transform, the backward's mask from x, the stem's
+// BN + pool) uses these, so the values agree bit for bit whatever the compiler would contract
+__device__ __forceinline__ float bn_shift(float beta, float mean, float scale) { return __builtin_fmaf(-mean, scale, beta); }
+__device__ __forceinline__ float bn_affine(float x, float scale, float shift) { return __builtin_fmaf(x, scale, shift); }
+
 // derivative of the activation expressed through its OUTPUT y = act(z)
 __device__ __forceinline__ float act_grad_from_out(float y, int act) {
   switch (act) {

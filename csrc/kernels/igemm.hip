@@ -151,7 +151,7 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
       binv[e] = a.bb_invstd[c];
       if (bb_from_x) {  // = norm.hip BwdMask (bit-identical to the forward's pre-activation)
         bsc[e] = a.bb_gamma[c] * a.bb_invstd[c];
-        bsh[e] = a.bb_beta[c] - a.bb_mean[c] * bsc[e];
+        bsh[e] = bn_shift(a.bb_beta[c], a.bb_mean[c], bsc[e]);
       }
     }
   }
@@ -231,7 +231,7 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
         const float x = bf2f((bf16)((xv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu));
         float g = g0;
         if (bb_from_x) {
-          g = (x * bsc[e] + bsh[e]) > 0.f ? g0 : 0.f;
+          g = bn_affine(x, bsc[e], bsh[e]) > 0.f ? g0 : 0.f;
         } else if (a.bb_act != ACT_NONE) {
           g = g0 * act_grad_from_out(bf2f((bf16)((yv[j][e >> 1] >> (16 * (e & 1))) & 0xffffu)), a.bb_act);
         }
@@ -284,9 +284,9 @@ __device__ __forceinline__ u32x4_t bn_relu8(const u32x4_t v, const f32x4_t (&sc)
   u32x4_t o;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    // the same expression bn_apply evaluates (norm.hip): bit-identical h
-    float lo = __uint_as_float(v[i] << 16) * sc[i >> 1][(2 * i) & 3] + sh[i >> 1][(2 * i) & 3];
-    float hi = __uint_as_float(v[i] & 0xffff0000u) * sc[i >> 1][(2 * i + 1) & 3] + sh[i >> 1][(2 * i + 1) & 3];
+    // bn_apply's rounding (one fma, common.h bn_affine): bit-identical h
+    float lo = bn_affine(__uint_as_float(v[i] << 16), sc[i >> 1][(2 * i) & 3], sh[i >> 1][(2 * i) & 3]);
+    float hi = bn_affine(__uint_as_float(v[i] & 0xffff0000u), sc[i >> 1][(2 * i + 1) & 3], sh[i >> 1][(2 * i + 1) & 3]);
     lo = lo > 0.f ? lo : 0.f;
     hi = hi > 0.f ? hi : 0.f;
     o[i] = pack_bf16x2(lo, hi);
@@ -861,68 +861,87 @@ __device__ __forceinline__ void shift_fold(float Kt, float st, float qt, float n
   Q += qt + 2.f * d * st + nt * d * d;
 }
 
-// part [tiles][3][N] -> chunk [P][3][N] (+ rows per chunk implied); grid (ceil(N/64), P)
-__global__ __launch_bounds__(256) void bn_part_stage1(const float* __restrict__ part, int tiles, int N, long Mp,
-                                                      int BMr, float* __restrict__ chunk) {
+// Both stages in ONE launch (grid (ceil(N/64), P)): block (g, p) folds tiles [64p, 64p+64) of channel
+// group g onto the chunk's first K and leaves the chunk partial [P][3][N] in write-through (sc1)
+// stores; per channel group the last block to arrive (relaxed agent-scope ticket, no release fence -
+// the split-K hand-off of gemm_dense.h) acquires once and folds the P chunks in chunk order (the
+// result does not depend on arrival order) into stats.  ctr: one zeroed uint32 per channel group,
+// reset by its last arriver.  (Round 3 had stage 1 and stage 2 as two launches: one launch and one
+// dependent boundary more per convolution with BN statistics.)
+__global__ __launch_bounds__(256) void bn_part_fold(const float* __restrict__ part, int tiles, int N, long Mp, int BMr,
+                                                    float* chunk, uint32_t* ctr, float* __restrict__ stats) {
   __shared__ float red[4][2][64];
   const int cl = threadIdx.x & 63, ln = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, p = blockIdx.y;
   const int t0 = p * BN_TCH, t1 = min(tiles, t0 + BN_TCH);
-  float S = 0.f, Q = 0.f, K = 0.f;
-  if (c < N) {
-    K = part[(long)t0 * 3 * N + c];
-    // all of this lane's tiles (<= BN_TCH / 4) loaded before the first fold: one latency, not 16
-    constexpr int PT = BN_TCH / 4;
-    float kt[PT], st[PT], qt[PT];
+  {
+    float S = 0.f, Q = 0.f, K = 0.f;
+    if (c < N) {
+      K = part[(long)t0 * 3 * N + c];
+      constexpr int PT = BN_TCH / 4;
+      float kt[PT], st[PT], qt[PT];
 #pragma unroll
-    for (int i = 0; i < PT; ++i) {
-      const int t = t0 + ln + 4 * i;
-      const float* pt = part + (long)(t < t1 ? t : t0) * 3 * N + c;
-      kt[i] = pt[0];
-      st[i] = pt[N];
-      qt[i] = pt[2 * N];
+      for (int i = 0; i < PT; ++i) {
+        const int t = t0 + ln + 4 * i;
+        const float* pt = part + (long)(t < t1 ? t : t0) * 3 * N + c;
+        kt[i] = pt[0];
+        st[i] = pt[N];
+        qt[i] = pt[2 * N];
+      }
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        const int t = t0 + ln + 4 * i;
+        if (t < t1) shift_fold(kt[i], st[i], qt[i], (float)min((long)BMr, Mp - (long)t * BMr), K, S, Q);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-      const int t = t0 + ln + 4 * i;
-      if (t < t1) shift_fold(kt[i], st[i], qt[i], (float)min((long)BMr, Mp - (long)t * BMr), K, S, Q);
+    red[ln][0][cl] = S;
+    red[ln][1][cl] = Q;
+    __syncthreads();
+    if (ln == 0 && c < N) {
+      S = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
+      Q = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(chunk + (long)p * 3 * N, (short)0, 3 * N * 4,
+                                                                          0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(K), rs, c * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(S), rs, (N + c) * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(Q), rs, (2 * N + c) * 4, 0, 16);
     }
   }
-  red[ln][0][cl] = S;
-  red[ln][1][cl] = Q;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (ln == 0 && c < N) {
-    S = ((red[0][0][cl] + red[1][0][cl]) + red[2][0][cl]) + red[3][0][cl];
-    Q = ((red[0][1][cl] + red[1][1][cl]) + red[2][1][cl]) + red[3][1][cl];
-    float* o = chunk + (long)p * 3 * N + c;
-    o[0] = K;
-    o[N] = S;
-    o[2 * N] = Q;
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(ctr + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == gridDim.y - 1;
+    if (last) {
+      __hip_atomic_store(ctr + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    red[0][0][0] = last ? 1.f : 0.f;
   }
-}
-
-// chunk [P][3][N] -> stats[c] += S, stats[N + c] += Q around chunk 0's K; grid ceil(N/64)
-__global__ __launch_bounds__(256) void bn_part_stage2(const float* __restrict__ chunk, int P, int N, long Mp, int BMr,
-                                                      float* __restrict__ stats) {
-  __shared__ float red[4][2][64];
-  const int cl = threadIdx.x & 63, ln = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  __syncthreads();
+  const bool last = red[0][0][0] != 0.f;
+  __syncthreads();
+  if (!last) return;
+  // stage 2 for this channel group (bn_part_stage2's fold)
+  const int P = gridDim.y;
   float S = 0.f, Q = 0.f;
   if (c < N) {
     const float K = chunk[c];
     const long rows_chunk = (long)BN_TCH * BMr;
-    for (int p0 = ln; p0 < P; p0 += 4 * 8) {  // 8 chunks per lane in flight
+    for (int p0 = ln; p0 < P; p0 += 4 * 8) {
       float kp[8], sp[8], qp[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int p = p0 + 4 * i;
-        const float* pc = chunk + (long)(p < P ? p : 0) * 3 * N + c;
+        const int pp = p0 + 4 * i;
+        const float* pc = chunk + (long)(pp < P ? pp : 0) * 3 * N + c;
         kp[i] = pc[0];
         sp[i] = pc[N];
         qp[i] = pc[2 * N];
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int p = p0 + 4 * i;
-        if (p < P) shift_fold(kp[i], sp[i], qp[i], (float)min(rows_chunk, Mp - (long)p * rows_chunk), K, S, Q);
+        const int pp = p0 + 4 * i;
+        if (pp < P) shift_fold(kp[i], sp[i], qp[i], (float)min(rows_chunk, Mp - (long)pp * rows_chunk), K, S, Q);
       }
     }
   }
@@ -985,12 +1004,16 @@ float* workspace(size_t bytes, hipStream_t s, DevScratch* pool = g_dev) {
 }
 
 DevScratch g_bn[64];
+// the BN partial workspace starts with BN_CTR_BYTES of hand-off counters (bn_part_fold), zeroed at
+// allocation and left zero by every launch; the partials follow
+constexpr size_t BN_CTR_BYTES = 256;
 
 float* bn_workspace(size_t bytes, hipStream_t s) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_mu);
   DevScratch& d = g_bn[dev];
+  bytes += BN_CTR_BYTES;
   if (d.ws_bytes < bytes) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &st);
@@ -1002,9 +1025,24 @@ float* bn_workspace(size_t bytes, hipStream_t s) {
     }
     const size_t nb = std::max(bytes, d.ws_bytes * 3 / 2);
     if (hipMalloc(&d.ws, nb) != hipSuccess) throw std::runtime_error("igemm: BN partial workspace alloc");
+    if (hipMemset(d.ws, 0, BN_CTR_BYTES) != hipSuccess) throw std::runtime_error("igemm: BN counter memset");
     d.ws_bytes = nb;
   }
-  return reinterpret_cast<float*>(d.ws);
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(d.ws) + BN_CTR_BYTES);
+}
+
+// the hand-off counters of the partials returned by bn_workspace (same device)
+uint32_t* bn_counters(const float* part) {
+  return reinterpret_cast<uint32_t*>(const_cast<char*>(reinterpret_cast<const char*>(part) - BN_CTR_BYTES));
+}
+
+void launch_bn_fold(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s) {
+  const int nchunk = (tiles + BN_TCH - 1) / BN_TCH;
+  float* chunk = part + (size_t)tiles * 3 * N;
+  const unsigned cg = (unsigned)((N + 63) / 64);
+  if (cg * sizeof(uint32_t) > BN_CTR_BYTES) throw std::runtime_error("bn_part_fold: too many channel groups");
+  hipLaunchKernelGGL(bn_part_fold, dim3(cg, nchunk), dim3(256), 0, s, part, tiles, N, Mp, BMr, chunk, bn_counters(part),
+                     stats);
 }
 
 int env_int(const char* name, int dflt) {
@@ -1103,13 +1141,9 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
                        a.splits, len, a.out, a.accum);
   }
   if (!fuse_bn) return false;
-  float* chunk = a.bn_part + (size_t)tiles_all * 3 * a.N;
-  const unsigned cg = (unsigned)((a.N + 63) / 64);
   // (backward partials carry a zero shift: the row counts passed here then do not enter the fold)
-  // (a one-launch variant - last-arriving workgroup per channel group folds the chunks - saved a
-  // graph node per conv but shared one hand-off counter array per device; removed in round 3)
-  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, a.bn_part, tiles_all, a.N, Mmax, t.bm, chunk);
-  hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, a.N, Mmax, t.bm, bn_stats);
+  (void)nchunk;
+  launch_bn_fold(a.bn_part, tiles_all, a.N, Mmax, t.bm, bn_stats, s);
   return true;
 }
 
@@ -1121,11 +1155,7 @@ float* bn_part_buffer(long tiles, int N, hipStream_t s) {
 }
 
 void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s) {
-  const int nchunk = (tiles + BN_TCH - 1) / BN_TCH;
-  float* chunk = part + (size_t)tiles * 3 * N;
-  const unsigned cg = (unsigned)((N + 63) / 64);
-  hipLaunchKernelGGL(bn_part_stage1, dim3(cg, nchunk), dim3(256), 0, s, part, tiles, N, Mp, BMr, chunk);
-  hipLaunchKernelGGL(bn_part_stage2, dim3(cg), dim3(256), 0, s, chunk, nchunk, N, Mp, BMr, stats);
+  launch_bn_fold(part, tiles, N, Mp, BMr, stats, s);
 }
 
 bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {

@@ -101,8 +101,13 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   reduce_stats(s, q, a.C, a.stats);
 }
 
+// (no fp contraction here: every kernel that recomputes a channel's mean / invstd - bn_apply's
+// workgroup 0 and its threads, bn_finalize, bn_relu_pool3 - must get the same bits whatever inlining
+// context the compiler sees; contracted `x[c] + stats[c] * inv_r` in one of them made the folded and
+// the materialised BN outputs differ in the last place)
 __device__ __forceinline__ void chan_params_of(const bf16* x, const float* stats, long R, int C, float eps, int c,
                                                float& mean, float& invstd) {
+#pragma clang fp contract(off)
   const float inv_r = 1.f / (float)R;
   const float d = stats[c] * inv_r;
   mean = bf2f(x[c]) + d;
@@ -117,6 +122,7 @@ __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean,
 // saved statistics + moving averages of one channel (TF: unbiased batch variance)
 __device__ __forceinline__ void save_chan(const BnArgs& a, int c, float mean, float invstd, float* smean,
                                           float* sinv, float* mm, float* mv) {
+#pragma clang fp contract(off)
   if (smean) smean[c] = mean;
   if (sinv) sinv[c] = invstd;
   if (mm) {
@@ -163,7 +169,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
       float mean, invstd;
       chan_params_of(a.res, a.r_stats, a.R, a.C, a.eps, c, mean, invstd);
       rscale[e] = a.r_gamma[c] * invstd;
-      rshift[e] = a.r_beta[c] - mean * rscale[e];
+      rshift[e] = bn_shift(a.r_beta[c], mean, rscale[e]);
     }
   }
   float scale[8], shift[8];
@@ -178,7 +184,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
       chan_params(a, c, mean, invstd);
     }
     scale[e] = a.gamma[c] * invstd;
-    shift[e] = a.beta[c] - mean * scale[e];
+    shift[e] = bn_shift(a.beta[c], mean, scale[e]);
   }
   const bool res_identity = RES && a.rstride == 1 && a.RC == a.C && a.RH == a.OH && a.RW == a.OW;
   const bool res_chunk = RES && S.chunk * 8 < a.RC;
@@ -198,13 +204,13 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
       float f[8];
       unpack8(v[u], f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = f[e] * scale[e] + shift[e];
+      for (int e = 0; e < 8; ++e) f[e] = bn_affine(f[e], scale[e], shift[e]);
       if (res_chunk) {
         float g[8];
         unpack8(w[u], g);
         if constexpr (RBN) {  // the shortcut BN's output as its own bn_apply (ACT_NONE) would store it
 #pragma unroll
-          for (int e = 0; e < 8; ++e) g[e] = act_fwd(g[e] * rscale[e] + rshift[e], ACT_NONE);
+          for (int e = 0; e < 8; ++e) g[e] = act_fwd(bn_affine(g[e], rscale[e], rshift[e]), ACT_NONE);
           unpack8(pack8(g), g);
         }
 #pragma unroll
@@ -253,7 +259,7 @@ struct BwdMask {
       for (int e = 0; e < 8; ++e) {
         const int c = chunk * 8 + e;
         scale[e] = a.gamma[c] * a.invstd[c];
-        shift[e] = a.beta[c] - a.mean[c] * scale[e];
+        shift[e] = bn_shift(a.beta[c], a.mean[c], scale[e]);
       }
     }
   }
@@ -269,7 +275,7 @@ __device__ __forceinline__ void masked_grad(const BnArgs& a, const BwdMask& M, c
     for (int e = 0; e < 8; ++e) g[e] = (yv[0] >> e) & 1u ? g[e] : 0.f;
   } else if constexpr (MM == MM_X) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = (x[e] * M.scale[e] + M.shift[e]) > 0.f ? g[e] : 0.f;
+    for (int e = 0; e < 8; ++e) g[e] = bn_affine(x[e], M.scale[e], M.shift[e]) > 0.f ? g[e] : 0.f;
   } else if constexpr (MM == MM_YRELU) {
     float y[8];
     unpack8(yv, y);
@@ -549,7 +555,7 @@ __global__ __launch_bounds__(256) void bn_relu_pool3_kernel(BnArgs a, bf16* y, u
     float mean, invstd;
     chan_params(a, ch + e, mean, invstd);
     scale[e] = a.gamma[ch + e] * invstd;
-    shift[e] = a.beta[ch + e] - mean * scale[e];
+    shift[e] = bn_shift(a.beta[ch + e], mean, scale[e]);
   }
   const long n = (long)B * OH * OW * cpr;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
@@ -574,7 +580,7 @@ __global__ __launch_bounds__(256) void bn_relu_pool3_kernel(BnArgs a, bf16* y, u
       float f[8];
       unpack8(v[t], f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = act_fwd(f[e] * scale[e] + shift[e], ACT_RELU);
+      for (int e = 0; e < 8; ++e) f[e] = act_fwd(bn_affine(f[e], scale[e], shift[e]), ACT_RELU);
       unpack8(pack8(f), f);  // the bf16 value bn_apply would have stored
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -765,7 +771,7 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a, float* xf) {
     save_chan(a, c, mean, invstd, a.mean, a.invstd, a.moving_mean, a.moving_var);
     const float scale = a.gamma[c] * invstd;
     xf[c] = scale;
-    xf[a.C + c] = a.beta[c] - mean * scale;
+    xf[a.C + c] = bn_shift(a.beta[c], mean, scale);
   }
 }
 

@@ -18,13 +18,14 @@ import torch.distributed as dist
 from .ipc import IpcComm
 from .rccl import RcclComm
 
-# Gradient bucket size (MB of fp32 gradient; half that on a bf16 wire).  Measured, ResNet-50 B=256
-# data-parallel over the IPC engine at W=2 (two ranks sharing one MI355X, the rehearsal this pool
-# allows; profiles/r4_comm_rehearsal.txt): 2 / 4 / 8 / 16 / 32 MB -> 55.5 / 54.9 / 53.9 / 54.1 /
-# 53.6 ms per step - flat within 3.5 %, small buckets slightly worse (one barrier latency and graph
-# node each).  16 MB keeps ResNet-50's 51 MB bf16 gradient in 7 buckets so the first all-reduces
-# start while the backward still has most of its layers to run (the overlap an 8-GPU node needs),
-# at the IPC staging cap of one 8 MB bucket.  Override with --bucket_mb.
+# Gradient bucket size (MB of fp32 gradient; half that on a bf16 wire).  What was measured: ResNet-50
+# B=256 data-parallel over the IPC engine at W=2 with BOTH ranks sharing one MI355X (the only multi-rank
+# setup this pool allows; profiles/r4_comm_rehearsal.txt): 2 / 4 / 8 / 16 / 32 MB -> 55.5 / 54.9 / 53.9 /
+# 54.1 / 53.6 ms per step, flat within 3.5 %.  What that can NOT show: the xGMI side - per-link
+# bandwidth, the 7-peer fan-in of one IPC launch and RCCL's ring latency on a real node - so the choice
+# below is reasoned, not measured on xGMI: 16 MB keeps ResNet-50's 51 MB bf16 gradient in 7 buckets so
+# the first all-reduces start while the backward still has most of its layers to run (the overlap an
+# 8-GPU node needs), at the IPC staging cap of one 8 MB bucket.  Override with --bucket_mb.
 DEFAULT_BUCKET_MB = 16.0
 
 

@@ -21,9 +21,15 @@ import torch.distributed as dist
 from .. import ops
 
 
+# workgroups per all-reduce launch (the kernel's own cap is 128): its workgroups spin at the
+# exchange barriers while the peers' halves arrive, holding CUs the overlapped backward kernels
+# could use.  Set from bench/ipc_interference.py (profiles/r5_ipc_grid_cap.txt).
+DEFAULT_MAX_BLOCKS = 128
+
+
 class IpcComm:
     def __init__(self, device, group=None, cap_bytes: int = 64 << 20, timeout_s: float = 30.0, fallback=None,
-                 self_check: bool = True):
+                 self_check: bool = True, max_blocks: int | None = None):
         ops.require()
         self.device = torch.device(device)
         self.group = group
@@ -39,6 +45,7 @@ class IpcComm:
             self.handle = lib.ipc_create(int(cap_bytes), self.rank, self.world, self.device.index or 0,
                                          float(timeout_s))
             self.cap = lib.ipc_capacity(self.handle)
+            lib.ipc_set_max_blocks(self.handle, int(max_blocks or DEFAULT_MAX_BLOCKS))
             mine = lib.ipc_handle(self.handle).numpy().tobytes()
         except Exception as e:  # noqa: BLE001
             err = e
@@ -69,6 +76,10 @@ class IpcComm:
         if not ok:
             self.close()
             raise RuntimeError("IpcComm %s failed on %s: %s" % (what, "this rank" if err else "a peer rank", err))
+
+    def set_max_blocks(self, n: int):
+        """Grid cap of the following launches (the same value on every rank)."""
+        torch.ops.dtfe.ipc_set_max_blocks(self.handle, int(n))
 
     def fits(self, t: torch.Tensor) -> bool:
         return t.numel() * t.element_size() + 64 <= self.cap and t.dtype in (torch.bfloat16, torch.float32)

@@ -22,3 +22,7 @@ for st in normal high; do
   timeout -k 10 240 python3 bench.py --mode ps --gpus 2 --steps 200 --warmup 20 --ps_stream $st > $O/ps12_$st.log 2>&1 || { tail -5 $O/ps12_$st.log; exit 1; }
   echo "ps12 $st $(grep -o '"value": [0-9.]*' $O/ps12_$st.log) $(grep -o '"ms_per_step": [0-9.]*' $O/ps12_$st.log) $(grep -o '"ps_refreshed_ranges": [0-9]*' $O/ps12_$st.log)"
 done
+timeout -k 10 200 python3 bench/cnn_kernels.py --iters 30 > $O/cnn_kernels.txt 2>&1 || { tail -5 $O/cnn_kernels.txt; exit 1; }
+cat $O/cnn_kernels.txt
+timeout -k 10 300 python3 bench/ipc_interference.py --reps 40 > $O/ipc_caps.txt 2>&1 || { tail -5 $O/ipc_caps.txt; exit 1; }
+grep "grid cap" $O/ipc_caps.txt

@@ -435,8 +435,8 @@ XF_CASES = [
 def test_conv_bn_on_load_matches_materialised_gpu(case):
     """bn_finalize + conv_fwd / conv_wgrad(xf=...) - the BatchNorm + ReLU formed on the implicit-GEMM
     operand loads - against bn_apply's stored output fed to the same convs: the saved statistics and
-    moving averages, the conv output, its fused BN statistics and the weight gradient are bit-identical
-    (zero padding of h, not of x, at the image border)."""
+    moving averages, the conv output and the weight gradient are bit-identical, the output's BN
+    statistics equal up to the statistics pass's atomics (zero padding of h, not of x, at the border)."""
     from dtfe import ops
     B, H, C, CO, K, s = case
     pad = (K - 1) // 2
@@ -471,7 +471,10 @@ def test_conv_bn_on_load_matches_materialised_gpu(case):
         outs.append((mean, inv, mm, mv, y, yst, dw))
     names = ("mean", "invstd", "moving_mean", "moving_var", "y", "y_stats", "dw")
     for n, a, b in zip(names, outs[0], outs[1]):
-        assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
+        if n == "y_stats":  # (a split-K launch takes the separate statistics pass: per-channel atomics)
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-3), (n, float((a - b).abs().max()))
+        else:
+            assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
 
 
 @pytest.mark.gpu
