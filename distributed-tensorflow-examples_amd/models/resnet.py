@@ -232,9 +232,12 @@ class SideStream:
 
 
 _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
-# (test hook, not a knob: tests compare the folded bn1 / bn2 applies against the materialised ones;
-# DTFE_R5_FOLD=0 only for this round's A/B run, scripts/gpu_r5_fold.sh)
-_FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "1") != "0"
+# bn1 / bn2 applies folded into conv2 / conv3's operand loads (BN.fwd_fold, igemm xf paths): OFF - measured
+# slower end to end, 23.42 vs 21.35 ms per ResNet-50 B=256 step (profiles/r5_resnet50_bn_fold_ab.txt: the
+# forward transform sits between a k-tile's loads and its barrier, and the weight gradients' in-place LDS
+# rewrite costs a barrier per k-tile of their 4-stage ring - 319 vs 157 us per 128x128 launch).  Kept as
+# a tested path (tests/test_resnet.py) for the next kernel iteration.  (Test hook, not a knob.)
+_FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "0") == "1"
 
 
 class BN:

@@ -23,8 +23,12 @@ from .. import ops
 
 # workgroups per all-reduce launch (the kernel's own cap is 128): its workgroups spin at the
 # exchange barriers while the peers' halves arrive, holding CUs the overlapped backward kernels
-# could use.  Set from bench/ipc_interference.py (profiles/r5_ipc_grid_cap.txt).
-DEFAULT_MAX_BLOCKS = 128
+# could use.  bench/ipc_interference.py, MNIST CNN fc bucket (6.5 MB bf16) beside conv2's backward,
+# two ranks on ONE GPU (profiles/r5_ipc_grid_cap.txt): conv+all-reduce span 128 -> 217 / 205 us,
+# 64 -> 214 / 181, 32 -> 229 / 237, 16 -> 175 / 175 (all-reduce alone 125 -> 150 us).  16 is the span
+# minimum there.  On a node each GPU hosts one rank and reads its 7 peers over xGMI, whose per-link
+# rate - not the workgroup count - bounds a 16-workgroup launch; that part is unmeasured here.
+DEFAULT_MAX_BLOCKS = 16
 
 
 class IpcComm:

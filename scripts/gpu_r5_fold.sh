@@ -26,3 +26,5 @@ timeout -k 10 200 python3 bench/cnn_kernels.py --iters 30 > $O/cnn_kernels.txt 2
 cat $O/cnn_kernels.txt
 timeout -k 10 300 python3 bench/ipc_interference.py --reps 40 > $O/ipc_caps.txt 2>&1 || { tail -5 $O/ipc_caps.txt; exit 1; }
 grep "grid cap" $O/ipc_caps.txt
+timeout -k 10 200 python3 bench/write_roofline.py > $O/write_roofline.txt 2>&1 || { tail -5 $O/write_roofline.txt; exit 1; }
+cat $O/write_roofline.txt

@@ -503,7 +503,8 @@ def test_resnet50_folded_bn_applies_match(monkeypatch):
     noise = float((grads[0] - grads[1]).abs().max())
     cross = float((grads[0] - grads[2]).abs().max())
     assert cross <= 4 * noise + 1e-6 * float(grads[0].abs().max()), (cross, noise)
-    assert abs(losses[2] - losses[0]) <= 1e-4 * abs(losses[0]) + 1e-6
+    lnoise = abs(losses[1] - losses[0])
+    assert abs(losses[2] - losses[0]) <= 4 * lnoise + 1e-3 * abs(losses[0]), losses
 
 
 def test_bn_finalize_and_xf_reference_cpu():
