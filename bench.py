@@ -58,6 +58,9 @@ def parse_args(argv=None):
                          "reported as config.prewarm); 0 disables")
     ap.add_argument("--batch_size", type=int, default=None, help="per-GPU batch (default: per model)")
     ap.add_argument("--comm_dtype", choices=["fp32", "bf16"], default="bf16")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="compute dtype of the MNIST CNN: bf16 (the headline) or fp32 (the reference's precision: "
+                         "exact-fp32 MFMA kernels, fp32 activations; one GPU)")
     ap.add_argument("--bucket_mb", type=float, default=None,
                     help="ResNet gradient bucket size, MB of fp32 gradient (default parallel.comm.DEFAULT_BUCKET_MB; "
                          "the CNN keeps its two buckets [head + fc1] / [convs])")
@@ -272,7 +275,8 @@ def _comm_info(args, d: Dist, comm):
 
 
 def _emit(d: Dist, args, metric, value, elapsed, win, model_desc, B, extra, data_desc):
-    base = _baseline(d.world, B, args.model)
+    # (the stock baseline rows are bf16; an fp32 run is compared in BASELINE.md against the stock fp32 row)
+    base = _baseline(d.world, B, args.model) if getattr(args, "dtype", "bf16") == "bf16" else None
     rec = {
         "metric": metric,
         "value": round(value, 1),
@@ -284,7 +288,7 @@ def _emit(d: Dist, args, metric, value, elapsed, win, model_desc, B, extra, data
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / base, 3) if base else None,
-        "dtype": "bf16",
+        "dtype": getattr(args, "dtype", "bf16"),
         "data": data_desc,
         "config": dict({"model": model_desc, "global_batch": B * d.world, "seq_len": None,
                         "parallelism": "dp%d" % d.world, "per_gpu_batch": B}, **extra),
@@ -302,7 +306,13 @@ def bench_cnn(args, d: Dist):
     from dtfe.utils.graphs import StepGraph, graphs_enabled
 
     B = args.batch_size or MODEL_BATCH["mnist_cnn"]
-    trainer = MnistCnnTrainer(B, d.device, seed=0, world_size=d.world, rank=d.rank)
+    if args.dtype == "fp32":
+        from dtfe.models.mnist_cnn import MnistCnnF32Trainer
+        if d.world != 1:
+            raise SystemExit("bench.py --dtype fp32: one GPU (the reference-precision row)")
+        trainer = MnistCnnF32Trainer(B, d.device, seed=0)
+    else:
+        trainer = MnistCnnTrainer(B, d.device, seed=0, world_size=d.world, rank=d.rank)
     comm = allreduce = None
     cdt = torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32
     if d.world > 1:

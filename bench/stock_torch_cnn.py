@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch_size", type=int, default=1024)
     ap.add_argument("--write", action="store_true")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="bf16 autocast (the headline row) or plain fp32 (the reference's precision)")
     ap.add_argument("--graph", action="store_true", help="capture the whole step (fwd, bwd, fused optimizer) in one "
                     "CUDA/HIP graph (1 GPU); implies --fused")
     ap.add_argument("--fused", action="store_true", help="torch.optim fused=True optimizer kernels")
@@ -72,7 +74,7 @@ def main():
     def step():
         idx = torch.randint(0, 60000, (a.batch_size,), device=dev, generator=g)
         x = (data[idx].float() / 255).contiguous(memory_format=torch.channels_last)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16"):
             loss = F.cross_entropy(model(x), labels[idx])
         opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -86,7 +88,7 @@ def main():
         def gstep():  # the captured step: backward ASSIGNS fresh grads (set to None before capture)
             idx = torch.randint(0, n_pool_, (B_,), device=dev)
             x = xform(idx)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16"):
                 loss = F.cross_entropy(model(x), labels[idx])
             loss.backward()
             opt.step()
@@ -122,7 +124,7 @@ def main():
         el = t.item()
     v = a.batch_size * world * a.steps / el
     if rank == 0:
-        print(json.dumps({"stock_torch_images_per_sec": round(v, 1), "n_gpus": world, "batch_size": a.batch_size,
+        print(json.dumps({"stock_torch_images_per_sec": round(v, 1), "dtype": a.dtype, "n_gpus": world, "batch_size": a.batch_size,
                           "ms_per_step": round(el / a.steps * 1000, 3), "graph": a.graph, "fused_optimizer": a.fused}),
               flush=True)
         if a.write:

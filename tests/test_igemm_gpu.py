@@ -130,3 +130,4 @@ def test_igemm_dgrad_masked_accumulation_source(B, H, C, Cout):
     cpu = torch.empty(B, H, H, C, dtype=torch.bfloat16)
     ops.conv_dgrad(dy.cpu(), wt.cpu(), cpu, g, accumulate=True, acc_src=(src.cpu(), bits.cpu()))
     assert (cpu.float() - dx.cpu().float()).abs().max().item() <= 2e-2 * dx.float().abs().max().item()
+
