@@ -169,44 +169,38 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
         Cs[(wm * WM + i * 16 + (lane >> 4) * 4 + q) * CLD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][q]);
   __syncthreads();
   if (a.bn_part && !a.bb_x) {
-    // BatchNorm statistics of this tile's stored (bf16) values, replacing a separate pass over y: each
-    // lane sums its accumulator column's rows (as rounded for the store) around the tile's first row
-    // K (read back from the staged C tile), the 4 lane groups of a wave combine by xor-shuffles, the
-    // waves' row halves in wave order through the LDS past the C tile - deterministic.  (Round 4 summed
-    // 16-B chunks of the staged tile per row group: 8 + 32 serial LDS reads per thread, ~26 us of the
-    // 64 -> 256 1x1 forward's 190 us at 56x56, profiles/r5_write_roofline.txt.)
-    constexpr int NWM = IG_THREADS / 128;
-    static_assert(BM * CLD * 2 + NWM * 2 * BN * 4 <= SMEM_EL * 2, "stats scratch fits");
+    // BatchNorm statistics of this tile's stored values (replaces a separate pass over y):
+    // thread = (8-channel chunk, row group); sums around the tile's first row, then the row
+    // groups in order through the LDS past the C tile (deterministic)
+    constexpr int CH = BN / 8, RG = IG_THREADS / CH;
+    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= SMEM_EL * 2, "stats scratch fits");
     float* red = reinterpret_cast<float*>(smem + BM * CLD);
-    const int rows = min(BM, Mp - m_base);
+    const int ch = tid % CH, rg = tid / CH, rows = min(BM, Mp - m_base);
+    float k[8], sm[8] = {}, sq[8] = {};
+    const u32x4_t kv = *reinterpret_cast<const u32x4_t*>(Cs + ch * 8);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WN + j * 16 + (lane & 15);
-      const float K = bf2f(Cs[col]);
-      float sm = 0.f, sq = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      k[2 * e] = bf2f((bf16)(kv[e] & 0xffffu));
+      k[2 * e + 1] = bf2f((bf16)(kv[e] >> 16));
+    }
+    for (int r = rg; r < rows; r += RG) {
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Cs + r * CLD + ch * 8);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = wm * WM + i * 16 + (lane >> 4) * 4 + q;
-          const float d = r < rows ? bf2f(f2bf(acc[i][j][q])) - K : 0.f;
-          sm += d;
-          sq += d * d;
-        }
-      sm += __shfl_xor(sm, 16, 64);
-      sq += __shfl_xor(sq, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
-      sq += __shfl_xor(sq, 32, 64);
-      if (lane < 16) {
-        red[(wm * 2) * BN + col] = sm;
-        red[(wm * 2 + 1) * BN + col] = sq;
+      for (int e = 0; e < 4; ++e) {
+        const float d0 = bf2f((bf16)(v[e] & 0xffffu)) - k[2 * e], d1 = bf2f((bf16)(v[e] >> 16)) - k[2 * e + 1];
+        sm[2 * e] += d0; sq[2 * e] += d0 * d0;
+        sm[2 * e + 1] += d1; sq[2 * e + 1] += d1 * d1;
       }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 2) * BN + ch * 8 + e] = sm[e];
+      red[(rg * 2 + 1) * BN + ch * 8 + e] = sq[e];
     }
     __syncthreads();
     for (int c = tid; c < BN; c += IG_THREADS) {
       float S = 0.f, Q = 0.f;
-#pragma unroll
-      for (int g2 = 0; g2 < NWM; ++g2) {
+      for (int g2 = 0; g2 < RG; ++g2) {
         S += red[(g2 * 2) * BN + c];
         Q += red[(g2 * 2 + 1) * BN + c];
       }
@@ -248,7 +242,7 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
   }
   if (bb) {  // row groups -> per-tile partial, fixed order, through the LDS past the C tile
     constexpr int RG = IG_THREADS / CPR;
-    static_assert(!BB || BM * CLD * 2 + RG * 2 * BN * 4 <= SMEM_EL * 2, "bwd stats scratch fits");
+    static_assert(BM * CLD * 2 + RG * 2 * BN * 4 <= SMEM_EL * 2, "bwd stats scratch fits");
     float* red = reinterpret_cast<float*>(smem + BM * CLD);
     const int rg = tid / CPR;
 #pragma unroll
@@ -277,8 +271,7 @@ __device__ __forceinline__ void igemm_store(const IgemmArgs& a, const f32x4_t (&
 // per CU the register allocation must allow
 template <int BM, int BN, int NST, bool BB>
 constexpr int ig_smem_el() {
-  // statistics scratch: BN-backward row groups (BB) or the forward statistics' per-wave row halves
-  constexpr int stage = NST * (BM + BN) * IG_BK, cld = BN + 8, rg = BB ? IG_THREADS / (BN / 8) : IG_THREADS / 128;
+  constexpr int stage = NST * (BM + BN) * IG_BK, cld = BN + 8, rg = IG_THREADS / (BN / 8);
   constexpr int epi = (BM * cld * 2 + rg * 2 * BN * 4 + 3) / 4 * 2;  // C tile + statistics scratch, in bf16 units
   return stage > epi ? stage : epi;
 }
@@ -1090,9 +1083,10 @@ void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
   // (a 1-stage, 3-workgroups-per-CU instance for the one-k-tile 1x1 convs measured 15-25 % slower
   // than this one: profiles/r3_resnet50_b256_kernels.txt)
   (void)nk_max;
-  // (64 x 256 whole-row tiles for the one-k-tile 1x1 convs - each output row one contiguous 512 B -
-  // measured slower: 64 -> 256 forward 175-180 vs 164-166 us, its data gradient 170 vs 155 us at
-  // B=256, profiles/r5_igemm_epilogue_ab.txt)
+  // (round 5, measured and removed: 64 x 256 whole-row tiles for the one-k-tile 1x1 convs - 64 -> 256
+  // forward 175-180 vs 164-166 us, its data gradient 170 vs 155 us at B=256 - and the forward BN
+  // statistics summed from the accumulator registers instead of the staged tile - no faster with the
+  // statistics, 9-13 us slower per launch without them: profiles/r5_igemm_epilogue_ab.txt)
   if (a.xf)
     hipLaunchKernelGGL((igemm_kernel<BM, BN, 2, false, 2, true>), grid, dim3(IG_THREADS), 0, s, a);
   else if (a.bb_x)
