@@ -1,0 +1,11 @@
+# Round 5 full check: every GPU test, smoke(), the driver-shaped CNN bench (with and without the pre-warm)
+set -o pipefail
+O=gpurun_out/${1:-r5full}
+mkdir -p $O
+timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log || { tail -5 $O/smoke.log; exit 1; }
+for pw in 150 0; do
+  timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --prewarm_ms $pw > $O/cnn_pw$pw.log 2>&1 || { tail -5 $O/cnn_pw$pw.log; exit 1; }
+  echo "cnn prewarm=$pw $(grep -o '"value": [0-9.]*' $O/cnn_pw$pw.log) $(grep -o '"ms_per_step": [0-9.]*' $O/cnn_pw$pw.log)"
+done
