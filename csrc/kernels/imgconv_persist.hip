@@ -61,6 +61,7 @@ struct PGeom {
   int nchunks;    // 16-byte source chunks per image (pooled chunks for a pooled source)
   int npf;        // chunks per thread
   int blocked;    // output rows in 2x2-window order (OH, OW even)
+  int stage_out;  // un-pooled output staged in LDS [OH*OW][N] after the image, stored as 16-B rows
 };
 
 // output row m of an image -> (oy, ox); false for padding rows of the last tile.
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
         const int n = i / kc_row, k = (i - n * kc_row) * 8;
         off[u] = i < total ? n * G.KP + k : -1;
         v[u] = u32x4_t{0u, 0u, 0u, 0u};
-        if (i < total && n < a.N && k < G.K) {
+        if (i < total && n < a.N && k < G.K && !(a.diag & 8)) {
           int sk = k;
           if (a.flip_taps) {
             const int tap = k / CS;
@@ -189,12 +190,12 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   const bf16* wlane = wl + (wn * NT * 16 + (lane & 15)) * G.KP + 8 * g;
 
   long b = blockIdx.x;
-  if (b < a.B) load_src(b);
+  if (b < a.B && !(a.diag & 2)) load_src(b);
   __syncthreads();  // zero border before the first interior write
   for (; b < a.B; b += gridDim.x) {
-    write_src();
+    if (!(a.diag & 2)) write_src();
     __syncthreads();
-    if (b + gridDim.x < a.B) load_src(b + gridDim.x);
+    if (b + gridDim.x < a.B && !(a.diag & 2)) load_src(b + gridDim.x);
     for (int t0 = wm; t0 < tiles; t0 += WM * RT) {
       int pix[RT];
 #pragma unroll
@@ -217,7 +218,8 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
       for (int n = 0; n < NT; ++n) bfr[n] = *reinterpret_cast<const u32x4_t*>(wlane + n * 16 * G.KP);
 #pragma unroll
       for (int r = 0; r < RT; ++r) af[r] = *reinterpret_cast<const u32x4_t*>(img + pix[r] + toff);
-      for (int s = 0; s < nk; ++s) {
+      const int nkk = (a.diag & 4) ? 0 : nk;
+      for (int s = 0; s < nkk; ++s) {
         cs += 32;
         toff += 32;
         while (cs >= CS) {
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
         const int tile = t0 + WM * r;
-        if (tile >= tiles) break;
+        if (tile >= tiles || (a.diag & 1)) break;
         const int m0 = tile * 16 + (lane >> 4) * 4;
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
@@ -266,6 +268,14 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
             const long o = ((b * (a.OH >> 1) + (oy >> 1)) * (a.OW >> 1) + (ox >> 1)) * a.N + col;
             a.y[o] = f2bf(apply_act(mx + bias, a.act));
             if (a.argmax) a.argmax[o] = (uint8_t)am;
+          } else if (G.stage_out) {
+            bf16* sy = img + G.LH * LWP * PS + G.slack;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              int oy, ox;
+              if (!row_pixel(m0 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
+              sy[(oy * a.OW + ox) * a.N + col] = f2bf(apply_act(v[j] + bias, a.act));
+            }
           } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -278,6 +288,28 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
             }
           }
         }
+      }
+    }
+    if (G.stage_out && !(a.diag & 1)) {
+      // the image's [OH*OW][N] output leaves as contiguous 16-B chunks (ReLU'-mask of the data
+      // gradient applied here from 16-B mask loads): the per-lane 2-byte scatter cost ~8 of the
+      // 19 us of ResNet-20's stage-1 conv (DTFE_DIAG icr=1 ablation, profiles/r5_resnet20_kernels.txt)
+      __syncthreads();
+      const bf16* sy = img + G.LH * LWP * PS + G.slack;
+      const int nch = M * a.N / 8;
+      const long ob = b * (long)M * a.N;
+      for (int i = tid; i < nch; i += THREADS) {
+        u32x4_t v = *reinterpret_cast<const u32x4_t*>(sy + i * 8);
+        if (a.relu_mask) {
+          const u32x4_t m = *reinterpret_cast<const u32x4_t*>(a.relu_mask + ob + i * 8);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // keep element where mask > 0 (bf16 bits: positive, non-zero, not NaN)
+            const uint32_t ml = m[e] & 0xffffu, mh = m[e] >> 16;
+            v[e] = (((ml - 1u) < 0x7f80u) ? (v[e] & 0xffffu) : 0u) | (((mh - 1u) < 0x7f80u) ? (v[e] & 0xffff0000u) : 0u);
+          }
+        }
+        *reinterpret_cast<u32x4_t*>(a.y + ob + i * 8) = v;
       }
     }
     __syncthreads();  // image b fully consumed before the next write
@@ -578,6 +610,7 @@ double a_read_conflicts(int PSs, int LWP, int OH, int OW, int stride, int blocke
 
 PGeom persist_geom(const ImgConvArgs& a, int WN, int NT, int threads) {
   PGeom G;
+  G.stage_out = 0;
   G.LH = (a.OH - 1) * a.stride + a.KH;
   G.LW = (a.OW - 1) * a.stride + a.KW;
   G.K = a.KH * a.KW * a.CS;
@@ -620,14 +653,20 @@ size_t persist_lds(const PGeom& G) {
 template <int NT, int RT, int WM, int WN, bool POOLED>
 bool launch_cfg(const ImgConvArgs& a, hipStream_t s) {
   constexpr int THREADS = 64 * WM * WN;
-  const PGeom G = persist_geom(a, WN, NT, THREADS);
-  const size_t lds = persist_lds(G);
+  PGeom G = persist_geom(a, WN, NT, THREADS);
+  size_t lds = persist_lds(G);
   if (lds > 160 * 1024) return false;
+  const size_t stage = (size_t)a.OH * a.OW * a.N * sizeof(bf16);
+  G.stage_out = !a.pool && a.N % 8 == 0 && lds + stage <= 160 * 1024 && !(diag_bits("icr") & 16);
+  if (G.stage_out) lds += stage;
   if (a.pool && !G.blocked) return false;
   const int grid = a.B < 256 ? a.B : 256;  // one workgroup per CU, persistent over the batch
+  static const int diag = diag_bits("icr");
+  ImgConvArgs ad = a;
+  ad.diag = diag;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(THREADS), lds, s, a, G);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(THREADS), lds, s, ad, G);
   };
   switch (G.npf) {
     case 1: go(imgconv_persist_kernel<NT, RT, WM, WN, 1, POOLED>); return true;
@@ -689,6 +728,8 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
   // wave grid (measured on MNIST conv2, B=1024): 8 x 2 waves, 4 per SIMD (fwd 48 us, dgrad 68) beat
   // 4 x 2 (48 / 74) and 4 x 1 waves holding every n-tile (fewer LDS reads, but one wave per SIMD
   // exposes the read latency: fwd 48 vs 63 us); the alternatives were removed in round 3
+  if (a.N <= 16 && !(diag_bits("icr") & 32))  // one n-tile: a second wave column would only compute padding
+    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s) : launch_cfg<1, 2, 16, 1, false>(a, s);
   if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s) : launch_cfg<1, 2, 8, 2, false>(a, s);
   return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s) : launch_cfg<2, 2, 8, 2, false>(a, s);
 }

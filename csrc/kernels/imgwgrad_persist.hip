@@ -412,7 +412,12 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   if (lds > 150 * 1024) return false;
   if ((G.ctiles + CTW - 1) / CTW > 8) return false;
   const int npfs = (G.schunks + 511) / 512, npfd = (G.dchunks + 511) / 512;
-  const int gcap = a.max_blocks > 0 && a.max_blocks < 256 ? a.max_blocks : 256;
+  // at least ~256 output pixels per workgroup: on small maps the per-workgroup partial slab (up to
+  // 229 KB, written and re-read by wp_reduce) outweighs one image's work - ResNet-20 stage 3
+  // (8x8, B=256): 64 workgroups 18.8 us vs 256: 26.3 (profiles/r5_resnet20_kernels.txt)
+  const int ipw = (256 + a.OH * a.OW - 1) / (a.OH * a.OW);
+  int gcap = a.max_blocks > 0 && a.max_blocks < 256 ? a.max_blocks : 256;
+  if ((a.B + ipw - 1) / ipw < gcap) gcap = (a.B + ipw - 1) / ipw;
   const int grid = a.B < gcap ? a.B : gcap;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -404,6 +404,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
 // Workgroup cap: every workgroup adds 2C atomics, and with 512 of them those serialized adds were a
 // visible part of the small layers' time.  ResNet-50 B=256 sweep (profiles/r4_bn_stats_grid.txt):
 // 256 beats 512 on every shape, 128 is better still below ~64 MB of activations and worse above.
+// ResNet-20 shapes (2-8 MB) re-swept in round 5: 128 / 256 / 512 / 1024 all within 0.1 us except
+// stage 1 (128: 6.4 us, more: 7.5) - the same-address atomics, not the grid, set the floor
+// (profiles/r5_resnet20_kernels.txt).
 int stats_grid(long R, int C) {
   const long rows_per_block = (long)(NT / (C / 8)) * U_STATS;
   long g = (R + rows_per_block - 1) / rows_per_block;

@@ -82,6 +82,7 @@ PERSIST_CASES = [  # B > 256 so persistent workgroups loop over several images
     (300, 14, 32, 64, 5, 1, 2, True),   # MNIST conv2 fwd
     (300, 32, 16, 16, 3, 1, 1, False),  # ResNet-20 stage 1
     (270, 16, 32, 32, 3, 2, 1, False),  # strided
+    (300, 8, 64, 64, 3, 1, 1, False),   # ResNet-20 stage 3
     (300, 28, 1, 32, 5, 1, 2, True),    # MNIST conv1 (shifted-copy kernel, B >= 256)
 ]
 
@@ -107,6 +108,29 @@ def test_imgconv_persistent_dgrad_unpool_source_and_mask():
     ops.imgconv(wt.cpu(), yr, src_pooled=dp.cpu(), src_argmax=am.cpu(), relu_mask=mask.cpu(), **kw)
     assert _rel(y.cpu(), yr) < 2e-2
     assert float(y.cpu()[mask.cpu() <= 0].abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,C", [(32, 16), (16, 32), (8, 64)])
+def test_imgconv_persistent_dgrad_relu_mask_resnet20(H, C):
+    """ResNet-20 data gradient (plain source, ReLU'-mask from a bf16 tensor): the LDS-staged
+    epilogue applies the mask from 16-B loads at store time."""
+    torch.manual_seed(6)
+    B, K = 300, 3
+    dy = torch.randn(B, H, H, C).to(DEV, torch.bfloat16)
+    wt = (torch.randn(C, K, K, C) * 0.1).to(DEV, torch.bfloat16)
+    mask = torch.randn(B, H, H, C).to(DEV, torch.bfloat16)
+    mask[0, 0, 0, :4] = float("nan")
+    mask[0, 0, 1, :4] = float("inf")
+    kw = dict(B=B, SH=H, SW=H, CS=C, OH=H, OW=H, N=C, KH=K, KW=K, pad=1, flip_taps=True)
+    y = torch.empty(B, H, H, C, device=DEV, dtype=torch.bfloat16)
+    ops.imgconv(wt, y, src=dy, relu_mask=mask, **kw)
+    yr = torch.empty(B, H, H, C)
+    ops.imgconv(wt.cpu(), yr, src=dy.cpu(), relu_mask=mask.cpu(), **kw)
+    assert _rel(y.cpu(), yr) < 2e-2
+    keep = mask.cpu().float() > 0
+    assert float(y.cpu()[~keep].abs().max()) == 0.0
+    assert torch.equal(y.cpu()[0, 0, 1, :4], yr[0, 0, 1, :4].bfloat16())
 
 
 WG_CASES = [  # (B, SH, CS, N, K, stride, pad, pooled_dy)
