@@ -241,11 +241,11 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
   dtfe::launch_conv_dgrad(a, cur_stream());
 }
 
-void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, const optional<Tensor>& src_argmax,
+bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, const optional<Tensor>& src_argmax,
              const Tensor& w, const optional<Tensor>& bias, const Tensor& y, const optional<Tensor>& argmax,
              const optional<Tensor>& relu_mask, int64_t B, int64_t SH, int64_t SW, int64_t CS, int64_t OH, int64_t OW,
              int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool,
-             int64_t dil) {
+             int64_t dil, const optional<Tensor>& sc_src, int64_t sc_stride) {
   check_cuda(w, "w");
   TORCH_CHECK((src.has_value() && src->defined()) != (src_pooled.has_value() && src_pooled->defined()),
               "imgconv: exactly one of src / src_pooled");
@@ -265,7 +265,16 @@ void imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
   a.relu_mask = ptr_or_null<dtfe::bf16>(relu_mask);
   TORCH_CHECK(w.numel() == N * KH * KW * CS, "imgconv: weight size");
   TORCH_CHECK(y.numel() == B * OH * OW * N / (pool ? 4 : 1), "imgconv: output size");
-  dtfe::launch_imgconv(a, cur_stream());
+  a.sc_src = ptr_or_null<dtfe::bf16>(sc_src);
+  if (a.sc_src) {
+    TORCH_CHECK(sc_stride >= 1 && OH % sc_stride == 0 && OW % sc_stride == 0 && sc_src->dim() == 4 &&
+                    sc_src->size(0) == B && sc_src->size(1) == OH / sc_stride && sc_src->size(2) == OW / sc_stride &&
+                    sc_src->size(3) >= N,
+                "imgconv: shortcut gradient [B][OH/s][OW/s][>= N]");
+    a.sc_stride = (int)sc_stride;
+    a.sc_C = (int)sc_src->size(3);
+  }
+  return dtfe::launch_imgconv(a, cur_stream());
 }
 
 // MNIST conv1 forward with the step's batch sampling fused in (imgconv1_copies.hip): samples B rows
@@ -1034,7 +1043,8 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
-      " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1) -> ()");
+      " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1, Tensor? sc_src=None,"
+      " int sc_stride=1) -> bool");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"

@@ -49,6 +49,11 @@ struct ImgConvArgs {
   long zlen[4];
   int nz;
   int diag;                 // ablation bits for kernel experiments (DTFE_DIAG ic=<bits>; 0 in production)
+  // option-A shortcut gradient added in the (LDS-staged) epilogue of a data gradient:
+  // y[b][oy][ox][c] += sc_src[b][oy/s][ox/s][c] where oy, ox are multiples of s = sc_stride
+  // (sc_src: [B][OH/s][OW/s][sc_C], c < N <= sc_C) - ops.shortcut_grad_add without its pass
+  const bf16* sc_src;
+  int sc_stride, sc_C;
 };
 
 // Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]
@@ -73,10 +78,12 @@ struct ImgWgradArgs {
 };
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
-void launch_imgconv(const ImgConvArgs& a, hipStream_t s);
+// returns whether a.sc_src was added by the launch (false: the caller adds the shortcut gradient)
+bool launch_imgconv(const ImgConvArgs& a, hipStream_t s);
 // persistent variant (weights resident in LDS, one workgroup per CU streaming images);
-// returns false when the shape does not fit it (launch_imgconv then uses the per-image kernel)
-bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s);
+// returns false when the shape does not fit it (launch_imgconv then uses the per-image kernel);
+// *sc_done: whether the shortcut gradient (a.sc_src) was added
+bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done = nullptr);
 bool imgwgrad_supported(const ImgWgradArgs& a);
 // floats of the partial-sum workspace the weight-gradient kernels need (256 workgroup slabs);
 // mirrored by ops.wgrad_ws_floats

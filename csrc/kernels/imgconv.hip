@@ -310,20 +310,22 @@ static void launch_nt(const ImgConvArgs& a, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(k, dim3(a.B), dim3(IC_THREADS), lds, s, a);
 }
 
-void launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
+bool launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
   if (!imgconv_supported(a.SH, a.SW, a.CS, a.N, a.KH, a.KW, a.stride, a.pad))
     throw std::runtime_error("imgconv: shape not supported");
   if (a.CS <= 4 && (!a.src || a.flip_taps || a.dil > 1))
     throw std::runtime_error("imgconv: the few-channel path is forward-only");
   if (a.pool && ((a.OH | a.OW) & 1)) throw std::runtime_error("imgconv: pool needs even output dims");
-  if (a.CS <= 4 && launch_conv1_copies_fwd(a, s)) return;
-  if (a.CS > 4 && launch_imgconv_persistent(a, s)) return;
+  if (a.CS <= 4 && launch_conv1_copies_fwd(a, s)) return false;
+  bool sc_done = false;
+  if (a.CS > 4 && launch_imgconv_persistent(a, s, &sc_done)) return sc_done;
   if (a.dil > 1) throw std::runtime_error("imgconv: dilated sources need the persistent kernel (B >= 64)");
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
   const size_t lds = (size_t)LH * LW * a.CS * sizeof(bf16);
   if (a.N <= 16) launch_nt<1>(a, lds, s);
   else if (a.N <= 32) launch_nt<2>(a, lds, s);
   else launch_nt<4>(a, lds, s);
+  return false;
 }
 
 // ------------------------------------------------------------------- wgrad

@@ -309,6 +309,20 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
             v[e] = (((ml - 1u) < 0x7f80u) ? (v[e] & 0xffffu) : 0u) | (((mh - 1u) < 0x7f80u) ? (v[e] & 0xffff0000u) : 0u);
           }
         }
+        if (a.sc_src) {  // + the shortcut's gradient at its (strided) pixels, in fp32 then one rounding
+          const int CPN = a.N >> 3, p = i / CPN, cc = i - p * CPN, oy = p / a.OW, ox = p - oy * a.OW;
+          const int st = a.sc_stride;
+          if ((oy % st) == 0 && (ox % st) == 0) {
+            const long gi = ((b * (a.OH / st) + oy / st) * (long)(a.OW / st) + ox / st) * a.sc_C + cc * 8;
+            const u32x4_t gv = *reinterpret_cast<const u32x4_t*>(a.sc_src + gi);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = __uint_as_float(v[e] << 16) + __uint_as_float(gv[e] << 16);
+              const float hi = __uint_as_float(v[e] & 0xffff0000u) + __uint_as_float(gv[e] & 0xffff0000u);
+              v[e] = pack_bf16x2(lo, hi);
+            }
+          }
+        }
         *reinterpret_cast<u32x4_t*>(a.y + ob + i * 8) = v;
       }
     }
@@ -651,7 +665,7 @@ size_t persist_lds(const PGeom& G) {
 }
 
 template <int NT, int RT, int WM, int WN, bool POOLED>
-bool launch_cfg(const ImgConvArgs& a, hipStream_t s) {
+bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   constexpr int THREADS = 64 * WM * WN;
   PGeom G = persist_geom(a, WN, NT, THREADS);
   size_t lds = persist_lds(G);
@@ -659,22 +673,27 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s) {
   const size_t stage = (size_t)a.OH * a.OW * a.N * sizeof(bf16);
   G.stage_out = !a.pool && a.N % 8 == 0 && lds + stage <= 160 * 1024 && !(diag_bits("icr") & 16);
   if (G.stage_out) lds += stage;
+  const bool sc = a.sc_src && G.stage_out && a.sc_stride >= 1 && a.OH % a.sc_stride == 0 &&
+                  a.OW % a.sc_stride == 0 && a.sc_C % 8 == 0 && a.N <= a.sc_C;
   if (a.pool && !G.blocked) return false;
   const int grid = a.B < 256 ? a.B : 256;  // one workgroup per CU, persistent over the batch
   static const int diag = diag_bits("icr");
   ImgConvArgs ad = a;
   ad.diag = diag;
+  if (!sc) ad.sc_src = nullptr;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(THREADS), lds, s, ad, G);
   };
+  if (G.npf < 1 || G.npf > 4) return false;
   switch (G.npf) {
-    case 1: go(imgconv_persist_kernel<NT, RT, WM, WN, 1, POOLED>); return true;
-    case 2: go(imgconv_persist_kernel<NT, RT, WM, WN, 2, POOLED>); return true;
-    case 3: go(imgconv_persist_kernel<NT, RT, WM, WN, 3, POOLED>); return true;
-    case 4: go(imgconv_persist_kernel<NT, RT, WM, WN, 4, POOLED>); return true;
-    default: return false;
+    case 1: go(imgconv_persist_kernel<NT, RT, WM, WN, 1, POOLED>); break;
+    case 2: go(imgconv_persist_kernel<NT, RT, WM, WN, 2, POOLED>); break;
+    case 3: go(imgconv_persist_kernel<NT, RT, WM, WN, 3, POOLED>); break;
+    default: go(imgconv_persist_kernel<NT, RT, WM, WN, 4, POOLED>); break;
   }
+  if (sc_done) *sc_done = sc;
+  return true;
 }
 
 }  // namespace
@@ -710,7 +729,8 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
   }
 }
 
-bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
+bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
+  if (sc_done) *sc_done = false;
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
   if (a.OH == 14 && a.OW == 14 && a.B >= 256) {
     // compile-time geometry, one 16-row tile per wave (13 waves); 2 / 4 tiles per wave (7 / 4
@@ -729,9 +749,9 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s) {
   // 4 x 2 (48 / 74) and 4 x 1 waves holding every n-tile (fewer LDS reads, but one wave per SIMD
   // exposes the read latency: fwd 48 vs 63 us); the alternatives were removed in round 3
   if (a.N <= 16 && !(diag_bits("icr") & 32))  // one n-tile: a second wave column would only compute padding
-    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s) : launch_cfg<1, 2, 16, 1, false>(a, s);
-  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s) : launch_cfg<1, 2, 8, 2, false>(a, s);
-  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s) : launch_cfg<2, 2, 8, 2, false>(a, s);
+    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s, sc_done) : launch_cfg<1, 2, 16, 1, false>(a, s, sc_done);
+  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<1, 2, 8, 2, false>(a, s, sc_done);
+  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<2, 2, 8, 2, false>(a, s, sc_done);
 }
 
 }  // namespace dtfe

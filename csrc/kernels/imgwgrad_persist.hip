@@ -62,9 +62,15 @@ __host__ __device__ inline int odd16(int e) {  // round up to 16 * odd elements
 // floats per workgroup slab of the register-layout partials (tiles + db, rounded to 16 B)
 __host__ __device__ inline int wp_part_len(int MT, int CTW, int N) { return 8 * CTW * MT * 256 + (N + 3) / 4 * 4; }
 
-template <int MT, int CTW, int NPFS, int NPFD, bool POOLED>
+// KG > 1: the 8 waves form KG k-groups x (8/KG) column groups - wave (kg, cg) runs column tiles
+// [cg*CTW, +CTW) over the k-steps s = kg (mod KG), and the k-groups' accumulators are summed through
+// LDS before the flush.  Small-KC layers (ResNet-20: 9 or 18 column tiles) otherwise leave most
+// waves with dead tiles while one or two carry every MFMA (profiles/r5_resnet20_kernels.txt).
+template <int MT, int CTW, int NPFS, int NPFD, bool POOLED, int KG = 1>
 __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, WPGeom G) {
   constexpr int THREADS = 512;
+  constexpr int CG = 8 / KG;
+  static_assert(KG == 1 || KG == 2 || KG == 4 || KG == 8, "k-groups divide the 8 waves");
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   bf16* simg = lds;
   bf16* dimg = lds + G.img_off;
@@ -160,7 +166,8 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     doff[h] = kl * NPS + 4 * p4;
   }
   const int sstep = rows_per_step * a.stride * LW * PS, dstep = 32 * NPS;
-  const int ct0 = wid * CTW;
+  const int kg = wid / CG, cgi = wid - kg * CG;  // (KG == 1: kg = 0, cgi = wid)
+  const int ct0 = cgi * CTW;
   int coff[CTW];  // column tile -> tap offset + channel chunk of this lane
 #pragma unroll
   for (int c = 0; c < CTW; ++c) {
@@ -209,11 +216,11 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     // transposing reads right before its 4 MFMAs: rocprof ablation, 37.7 of the 57.7 us launch in
     // the MFMA loop at ~56 % MFMA utilisation.)
     const int nk = (a.diag & 4) ? 0 : G.nk;
-    if (nk > 0) {
-      bf16x8_t a_cur[MT], a_nxt[MT], b_cur = load_b(0, 0);
-      load_a(0, a_cur);
-      for (int s = 0; s < nk; ++s) {
-        const int sn = s + 1 < nk ? s + 1 : s;  // the last step re-reads its own fragments (unused)
+    if (kg < nk) {
+      bf16x8_t a_cur[MT], a_nxt[MT], b_cur = load_b(kg, 0);
+      load_a(kg, a_cur);
+      for (int s = kg; s < nk; s += KG) {
+        const int sn = s + KG < nk ? s + KG : s;  // the last step re-reads its own fragments (unused)
         static_for_c<0, CTW>([&](auto cc) {
           constexpr int c = decltype(cc)::value;
           bf16x8_t b_nxt;
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
           __builtin_amdgcn_sched_group_barrier(0x8, MT, 0);
           b_cur = b_nxt;
         });
-        if (wid == 0) {  // bias gradient from this step's dY fragments (wave-uniform branch)
+        if (KG == 1 && wid == 0) {  // bias gradient from this step's dY fragments (wave-uniform branch)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const s16x8_t v = __builtin_bit_cast(s16x8_t, a_cur[mt]);
@@ -249,16 +256,36 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
   // scatter happens once, in the reduce kernel) - then db[N] after the 8 * CTW * MT tiles.
   // Without: scaled atomics into dw / db.
   if (a.diag & 1) return;
+  if constexpr (KG > 1) {
+    // k-group partials -> k-group 0 through LDS (the images are consumed: the loop ended on a
+    // barrier), summed in k-group order
+    f32x4_t* red = reinterpret_cast<f32x4_t*>(lds);
+    if (kg > 0) {
+      f32x4_t* mine = red + ((kg - 1) * CG + cgi) * CTW * MT * 64 + lane;
+      static_for_c<0, CTW * MT>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        mine[i * 64] = acc[i % MT][i / MT];
+      });
+    }
+    __syncthreads();
+    if (kg > 0) return;
+    for (int q = 1; q < KG; ++q) {
+      const f32x4_t* theirs = red + ((q - 1) * CG + cgi) * CTW * MT * 64 + lane;
+      static_for_c<0, CTW * MT>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        acc[i % MT][i / MT] += theirs[i * 64];
+      });
+    }
+  }
   if (a.ws) {
     float* part = a.ws + (long)blockIdx.x * wp_part_len(MT, CTW, a.N);
-    f32x4_t* pv = reinterpret_cast<f32x4_t*>(part) + (long)wid * CTW * MT * 64 + lane;
-#pragma unroll
-    for (int c = 0; c < CTW; ++c) {
-      if (c >= nct) break;  // dead tiles (past the weight's columns) are neither stored nor reduced
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) pv[(c * MT + mt) * 64] = acc[mt][c];
-    }
-    if (wid == 0) {
+    f32x4_t* pv = reinterpret_cast<f32x4_t*>(part) + (long)cgi * CTW * MT * 64 + lane;
+    // dead tiles (past the weight's columns) are neither stored nor reduced
+    static_for_c<0, CTW * MT>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if (i / MT < nct) pv[i * 64] = acc[i % MT][i / MT];
+    });
+    if (KG == 1 && wid == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         float v = dbacc[mt];
@@ -270,19 +297,18 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
     }
     return;
   }
-#pragma unroll
-  for (int c = 0; c < CTW; ++c) {
-    if (c >= nct) break;
+  static_for_c<0, CTW * MT>([&](auto ic) {
+    constexpr int i = decltype(ic)::value, c = i / MT, mt = i % MT;
     const int col = (ct0 + c) * 16 + i16;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    if (c < nct) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = mt * 16 + g * 4 + j;
         if (n < a.N) atomicAdd(a.dw + (long)n * KC + col, acc[mt][c][j] * a.scale);
       }
-  }
-  if (wid == 0 && a.db) {
+    }
+  });
+  if (KG == 1 && wid == 0 && a.db) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       float v = dbacc[mt];
@@ -406,11 +432,15 @@ WPGeom wp_geom(const ImgWgradArgs& a) {
 
 size_t wp_lds(const WPGeom& G) { return ((size_t)G.img_off + (size_t)G.nk * 32 * G.NPS) * sizeof(bf16); }
 
-template <int MT, int CTW, bool POOLED>
+template <int MT, int CTW, bool POOLED, int KG = 1>
 bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
-  const size_t lds = wp_lds(G);
+  size_t lds = wp_lds(G);
   if (lds > 150 * 1024) return false;
-  if ((G.ctiles + CTW - 1) / CTW > 8) return false;
+  if ((G.ctiles + CTW - 1) / CTW > 8 / KG) return false;
+  if (KG > 1 && a.db) return false;  // (the bias gradient is summed by the k-group-0 waves only)
+  const size_t red = (size_t)(KG - 1) * (8 / KG) * CTW * MT * 64 * sizeof(f32x4_t);
+  if (red > lds) lds = red;
+  if (lds > 160 * 1024) return false;
   const int npfs = (G.schunks + 511) / 512, npfd = (G.dchunks + 511) / 512;
   // at least ~256 output pixels per workgroup: on small maps the per-workgroup partial slab (up to
   // 229 KB, written and re-read by wp_reduce) outweighs one image's work - ResNet-20 stage 3
@@ -435,15 +465,15 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   // prefetch chunks per thread (source, dY): 1, 2 or 4 each
   auto q = [](int n) { return n <= 1 ? 1 : (n <= 2 ? 2 : (n <= 4 ? 4 : 0)); };
   switch (q(npfs) * 8 + q(npfd)) {
-    case 9: return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED>);
-    case 10: return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED>);
-    case 12: return go(imgwgrad_persist_kernel<MT, CTW, 1, 4, POOLED>);
-    case 17: return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED>);
-    case 18: return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED>);
-    case 20: return go(imgwgrad_persist_kernel<MT, CTW, 2, 4, POOLED>);
-    case 33: return go(imgwgrad_persist_kernel<MT, CTW, 4, 1, POOLED>);
-    case 34: return go(imgwgrad_persist_kernel<MT, CTW, 4, 2, POOLED>);
-    case 36: return go(imgwgrad_persist_kernel<MT, CTW, 4, 4, POOLED>);
+    case 9: return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED, KG>);
+    case 10: return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED, KG>);
+    case 12: return go(imgwgrad_persist_kernel<MT, CTW, 1, 4, POOLED, KG>);
+    case 17: return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED, KG>);
+    case 18: return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED, KG>);
+    case 20: return go(imgwgrad_persist_kernel<MT, CTW, 2, 4, POOLED, KG>);
+    case 33: return go(imgwgrad_persist_kernel<MT, CTW, 4, 1, POOLED, KG>);
+    case 34: return go(imgwgrad_persist_kernel<MT, CTW, 4, 2, POOLED, KG>);
+    case 36: return go(imgwgrad_persist_kernel<MT, CTW, 4, 4, POOLED, KG>);
     default: return false;
   }
 }
@@ -451,7 +481,7 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
 }  // namespace
 
 long imgwgrad_ws_floats(int N, int KC) {
-  const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 8;  // the wp_launch instances below
+  const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 9;  // the largest wp_launch slabs below
   const long plain = (long)N * KC + N;                   // imgconv1_copies / per-image kernels
   const long reg = wp_part_len(MT, CTW, N);
   return 256L * (plain > reg ? plain : reg);
@@ -462,9 +492,15 @@ bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s) {
   const bool pooled = a.dy == nullptr;
   if (pooled && ((a.OH | a.OW) & 1)) return false;
   const WPGeom G = wp_geom(a);
-  // 8 waves share the column tiles; MNIST conv2: 50 tiles -> 7 per wave
+  // 8 waves share the column tiles; MNIST conv2: 50 tiles -> 7 per wave.  Few column tiles (<= 9
+  // per column group, no bias gradient): k-groups of waves instead (KG, see the kernel)
   const int ctw = (G.ctiles + 7) / 8;
+  const bool ks = !a.db && !(diag_bits("iwk") & 1);
+  if (ks && G.ctiles <= 9 && a.N <= 16 && !pooled) return wp_launch<1, 9, false, 8>(a, G, s);
+  if (ks && G.ctiles <= 9 && a.N <= 32 && !pooled) return wp_launch<2, 9, false, 8>(a, G, s);
+  if (ks && G.ctiles <= 18 && a.N <= 32 && !pooled) return wp_launch<2, 9, false, 4>(a, G, s);
   if (a.N > 32) {
+    if (ks && G.ctiles <= 40 && !pooled) return wp_launch<4, 5, false>(a, G, s);
     if (ctw <= 7) return pooled ? wp_launch<4, 7, true>(a, G, s) : wp_launch<4, 7, false>(a, G, s);
     return false;
   }

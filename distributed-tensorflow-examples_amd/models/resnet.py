@@ -168,15 +168,19 @@ class Conv:
         profiles/r2_resnet50_bn_bwd_fuse_ab.txt)."""
         return not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0 and self.stride == 1
 
-    def dgrad(self, dy, dx, accumulate=False, bn_bwd=None, acc_src=None):
+    def dgrad(self, dy, dx, accumulate=False, bn_bwd=None, acc_src=None, shortcut=None):
         """``bn_bwd``: BN.bwd_stats_args of the BatchNorm that consumes dx; returns True when its
         backward statistics were produced with dx (the BN then skips its statistics pass).
-        ``acc_src``: (src, relu bits) - dx = dgrad + src * bit (ops.conv_dgrad)."""
+        ``acc_src``: (src, relu bits) - dx = dgrad + src * bit (ops.conv_dgrad).  ``shortcut``:
+        (g, stride) of an option-A shortcut whose gradient the whole-image kernel adds to dx in its
+        epilogue (ops.imgconv_shortcut; returns True when it did)."""
         if self.img_dgrad:
             assert not accumulate
-            ops.imgconv(self.wt, dx, src=dy, flip_taps=True, B=self.B, SH=self.OH, SW=self.OW, CS=self.cout,
-                        OH=self.H, OW=self.W, N=self.cin, KH=self.k, KW=self.k, stride=1,
-                        pad=self.k - 1 - self.pad, dil=self.dil)
+            geom = dict(B=self.B, SH=self.OH, SW=self.OW, CS=self.cout, OH=self.H, OW=self.W, N=self.cin, KH=self.k,
+                        KW=self.k, stride=1, pad=self.k - 1 - self.pad, dil=self.dil)
+            if shortcut is not None:
+                return ops.imgconv_shortcut(self.wt, dx, shortcut[0], shortcut[1], src=dy, **geom)
+            ops.imgconv(self.wt, dx, src=dy, flip_taps=True, **geom)
             return False
         fuse = bn_bwd is not None and self.dgrad_fuses_bn(accumulate)
         ops.conv_dgrad(dy, self.wt, dx, self.g, accumulate=accumulate, bn_bwd=bn_bwd if fuse else None,
@@ -433,8 +437,10 @@ class BasicBlock:
         self.bn1.bwd(self.dh1, self.conv1.y, self.dc1)
         self.conv1.wgrad(self.dc1, self.x)
         if dx is not None:
-            self.conv1.dgrad(self.dc1, dx)
-            ops.shortcut_grad_add(self.dres, dx, self.stride)
+            # the shortcut's gradient rides in the data gradient's epilogue where the kernel allows
+            # (profiles/r5_resnet20_kernels.txt); else its own pass
+            if not self.conv1.dgrad(self.dc1, dx, shortcut=(self.dres, self.stride)):
+                ops.shortcut_grad_add(self.dres, dx, self.stride)
 
 
 class Bottleneck:

@@ -27,6 +27,7 @@ __all__ = [
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
+    "imgconv_shortcut",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -394,6 +395,22 @@ def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None
     return y
 
 
+def imgconv_shortcut(w, dx, g, sc_stride, *, src, **geom) -> bool:
+    """Data gradient of a whole-image conv (flipped taps over ``src`` = dY, ``geom`` as for
+    imgconv(flip_taps=True)) with the option-A shortcut's gradient added in the same launch:
+    dx[:, ::s, ::s, :] += g[..., :N] (ops.shortcut_grad_add).  Returns True when the launch added it
+    (the persistent kernel's LDS-staged epilogue); False: only dx was written and the caller adds
+    the shortcut gradient.  The CPU path does both (the oracle)."""
+    if dx.is_cuda:
+        k = geom
+        return bool(require().imgconv(src, None, None, w, None, dx, None, None, k["B"], k["SH"], k["SW"], k["CS"],
+                                      k["OH"], k["OW"], k["N"], k["KH"], k["KW"], k.get("stride", 1), k.get("pad", 0),
+                                      True, ACT_NONE, False, k.get("dil", 1), g, sc_stride))
+    imgconv(w, dx, src=src, flip_taps=True, **geom)
+    shortcut_grad_add(g, dx, sc_stride)
+    return True
+
+
 _WG_WS = {}
 
 
@@ -401,7 +418,7 @@ def wgrad_ws_floats(N: int, KC: int) -> int:
     """Floats of the weight-gradient partial-sum workspace (256 workgroup slabs) - mirrors
     imgwgrad_ws_floats in csrc/kernels/imgwgrad_persist.hip (the register-layout slabs of the
     persistent kernel: 8 waves x CTW column tiles x MT row tiles x 64 lanes x 4, + db)."""
-    MT, CTW = (4, 7) if N > 32 else (2, 8)
+    MT, CTW = (4, 7) if N > 32 else (2, 9)
     return 256 * max(N * KC + N, 8 * CTW * MT * 256 + (N + 3) // 4 * 4)
 
 

@@ -225,3 +225,61 @@ def test_few_channel_conv_fwd_wgrad(cs):
     ops.imgwgrad(x.cpu(), dwr, None, dy=dy.cpu(), **kw)
     assert _rel(dw.cpu(), dwr) < 1e-2
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,CIN,COUT,s", [(256, 32, 16, 16, 1), (300, 16, 32, 32, 1), (256, 8, 64, 64, 1),
+                                            (256, 32, 16, 32, 2), (130, 16, 32, 64, 2)])
+def test_imgconv_shortcut_grad_fused(B, H, CIN, COUT, s):
+    """Data gradient with the option-A shortcut gradient added in the epilogue == imgconv followed
+    by shortcut_grad_add, bit for bit (stride 1 and the stride-2 dilated form)."""
+    torch.manual_seed(9)
+    OH = H // s
+    dy = torch.randn(B, OH, OH, COUT).to(DEV, torch.bfloat16)
+    wt = (torch.randn(CIN, 3, 3, COUT) * 0.1).to(DEV, torch.bfloat16)
+    g = torch.randn(B, OH, OH, COUT).to(DEV, torch.bfloat16)
+    geom = dict(B=B, SH=OH, SW=OH, CS=COUT, OH=H, OW=H, N=CIN, KH=3, KW=3, stride=1, pad=1, dil=s)
+    ref = torch.empty(B, H, H, CIN, device=DEV, dtype=torch.bfloat16)
+    ops.imgconv(wt, ref, src=dy, flip_taps=True, **geom)
+    ops.shortcut_grad_add(g, ref, s)
+    dx = torch.empty_like(ref)
+    assert ops.imgconv_shortcut(wt, dx, g, s, src=dy, **geom)
+    assert torch.equal(dx, ref)
+
+
+def test_imgconv_shortcut_cpu_oracle():
+    torch.manual_seed(10)
+    B, H, C = 2, 8, 16
+    dy = torch.randn(B, H // 2, H // 2, 2 * C).bfloat16()
+    wt = (torch.randn(C, 3, 3, 2 * C) * 0.1).bfloat16()
+    g = torch.randn(B, H // 2, H // 2, 2 * C).bfloat16()
+    geom = dict(B=B, SH=H // 2, SW=H // 2, CS=2 * C, OH=H, OW=H, N=C, KH=3, KW=3, stride=1, pad=1, dil=2)
+    dx = torch.empty(B, H, H, C, dtype=torch.bfloat16)
+    assert ops.imgconv_shortcut(wt, dx, g, 2, src=dy, **geom)
+    ref = torch.empty_like(dx)
+    ops.imgconv(wt, ref, src=dy, flip_taps=True, **geom)
+    ops.shortcut_grad_add(g, ref, 2)
+    assert torch.equal(dx, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(256, 32, 16, 16, 3, 1, 1), (256, 32, 16, 32, 3, 2, 1), (300, 16, 32, 32, 3, 1, 1),
+                                  (256, 8, 64, 64, 3, 1, 1), (130, 16, 16, 32, 3, 2, 1)])
+def test_imgwgrad_persistent_kgroups(case):
+    """Weight gradient without a bias gradient (ResNet convs): the k-group wave split (KG = 8 / 4 for
+    9 / 18 column tiles) and the 5-tile column groups of the 64-channel layers vs the fp32 reference,
+    and equal to the wave-per-column-tiles kernel (DTFE_DIAG iwk=1 path) to fp32 rounding."""
+    B, SH, CS, N, K, s, pad = case
+    OH = (SH + 2 * pad - K) // s + 1
+    torch.manual_seed(11)
+    x = torch.randn(B, SH, SH, CS).to(DEV, torch.bfloat16)
+    dy = torch.randn(B, OH, OH, N).to(DEV, torch.bfloat16)
+    kw = dict(B=B, SH=SH, SW=SH, CS=CS, OH=OH, OW=OH, N=N, KH=K, KW=K, stride=s, pad=pad, scale=0.5)
+    dw = torch.zeros(N, K, K, CS, device=DEV)
+    ops.imgwgrad(x, dw, None, dy=dy, **kw)
+    dwr = torch.zeros(N, K, K, CS)
+    ops.imgwgrad(x.cpu(), dwr, None, dy=dy.cpu(), **kw)
+    assert _rel(dw.cpu(), dwr) < 1e-2
+    dw2 = torch.zeros_like(dw)
+    ops.imgwgrad(x, dw2, None, dy=dy, **kw)  # a second launch (workspace / LDS reuse)
+    assert torch.equal(dw, dw2)
