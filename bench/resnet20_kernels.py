@@ -47,11 +47,45 @@ def bwd_stats(bn, dy, x):
     ops.bn_bwd_stats(dy, y, xx, mean, inv, st, act, gamma=gam, beta=beta)
 
 
+def phases(prog, blocks):
+    """Phase boundaries of the persistent conv (imgconv_persist_kernel stamps): 0 start, 1 weights
+    staged + LDS zeroed, 2 first image in LDS, 3 first tile pass's MFMAs done, 4 epilogue into LDS
+    done, 5 copy-out issued, 6 workgroup end - microseconds after the earliest workgroup start."""
+    lib = ops.require()
+    names = ["start", "w+zero", "img", "mfma1", "epi", "store", "end"]
+    print("conv              " + " ".join(f"{n:>14s}" for n in names))
+    for tag, i in (("s1", 1), ("s2", 4), ("s3", 7)):
+        b = blocks[i]
+        for kind in ("fwd", "dgrad"):
+            c = b.conv2
+            ts = torch.zeros(256 * 8, dtype=torch.int64, device="cuda")
+            if kind == "fwd":
+                g = c.ic
+                call = lambda: lib.imgconv(b.bn1.y, None, None, c.w, None, c.y, None, None, g["B"], g["SH"], g["SW"],
+                                           g["CS"], g["OH"], g["OW"], g["N"], g["KH"], g["KW"], g["stride"], g["pad"],
+                                           False, ops.ACT_NONE, False, 1, None, 1, ts)
+            else:
+                call = lambda: lib.imgconv(b.dc2, None, None, c.wt, None, b.dh1, None, None, c.B, c.OH, c.OW, c.cout,
+                                           c.H, c.W, c.cin, c.k, c.k, 1, c.k - 1 - c.pad, True, ops.ACT_NONE, False,
+                                           c.dil, None, 1, ts)
+            for _ in range(5):
+                call()
+            torch.cuda.synchronize()
+            t = ts.view(256, 8)[:, :7].double().cpu()
+            t0 = t[:, 0].min()
+            rel = (t - t0) / 100.0  # 100 MHz -> us
+            med = rel.median(0).values
+            mx = rel.max(0).values
+            print(f"{tag} conv2 {kind:6s}  " + " ".join(f"{m:6.2f}/{x:6.2f} " for m, x in zip(med, mx)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch_size", type=int, default=256)
     ap.add_argument("--wgrad_grids", default="")
     ap.add_argument("--only", default="", help="comma-separated substrings of the rows to time")
+    ap.add_argument("--phases", action="store_true",
+                    help="per-workgroup phase stamps of the whole-image conv (s_memrealtime, 10 ns ticks)")
     a = ap.parse_args()
     prog = ResNetModel(arch="resnet20").program(torch.device("cuda"), a.batch_size)
     prog.compute_grads()
@@ -84,6 +118,9 @@ def main():
                          lambda c=c, b=b, gcap=gcap: ops.imgwgrad(b.bn1.y, c.gw, None, dy=b.dc2, max_blocks=gcap,
                                                                   **c.ic)))
     print(f"{'launch':30s} {'us':>8s}")
+    if a.phases:
+        phases(prog, blocks)
+        return
     only = [x for x in a.only.split(",") if x]
     for name, fn in rows:
         if only and not any(o in name for o in only):

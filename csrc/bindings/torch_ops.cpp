@@ -245,7 +245,7 @@ bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
              const Tensor& w, const optional<Tensor>& bias, const Tensor& y, const optional<Tensor>& argmax,
              const optional<Tensor>& relu_mask, int64_t B, int64_t SH, int64_t SW, int64_t CS, int64_t OH, int64_t OW,
              int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool,
-             int64_t dil, const optional<Tensor>& sc_src, int64_t sc_stride) {
+             int64_t dil, const optional<Tensor>& sc_src, int64_t sc_stride, const optional<Tensor>& tstamp) {
   check_cuda(w, "w");
   TORCH_CHECK((src.has_value() && src->defined()) != (src_pooled.has_value() && src_pooled->defined()),
               "imgconv: exactly one of src / src_pooled");
@@ -265,6 +265,7 @@ bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
   a.relu_mask = ptr_or_null<dtfe::bf16>(relu_mask);
   TORCH_CHECK(w.numel() == N * KH * KW * CS, "imgconv: weight size");
   TORCH_CHECK(y.numel() == B * OH * OW * N / (pool ? 4 : 1), "imgconv: output size");
+  a.tstamp = tstamp.has_value() && tstamp->defined() ? reinterpret_cast<uint64_t*>(tstamp->data_ptr()) : nullptr;
   a.sc_src = ptr_or_null<dtfe::bf16>(sc_src);
   if (a.sc_src) {
     TORCH_CHECK(sc_stride >= 1 && OH % sc_stride == 0 && OW % sc_stride == 0 && sc_src->dim() == 4 &&
@@ -1044,7 +1045,7 @@ TORCH_LIBRARY(dtfe, m) {
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
       " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1, Tensor? sc_src=None,"
-      " int sc_stride=1) -> bool");
+      " int sc_stride=1, Tensor(e!)? tstamp=None) -> bool");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"

@@ -49,6 +49,9 @@ struct ImgConvArgs {
   long zlen[4];
   int nz;
   int diag;                 // ablation bits for kernel experiments (DTFE_DIAG ic=<bits>; 0 in production)
+  // diagnostics (bench/resnet20_kernels.py --phases): per-workgroup s_memrealtime stamps [grid][8] at the
+  // persistent kernel's phase boundaries, written by thread 0 (nullptr in production)
+  uint64_t* tstamp;
   // option-A shortcut gradient added in the (LDS-staged) epilogue of a data gradient:
   // y[b][oy][ox][c] += sc_src[b][oy/s][ox/s][c] where oy, ox are multiples of s = sc_stride
   // (sc_src: [B][OH/s][OW/s][sc_C], c < N <= sc_C) - ops.shortcut_grad_add without its pass

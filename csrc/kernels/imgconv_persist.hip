@@ -92,6 +92,10 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   const int wm = wid % WM, wn = wid / WM;
   const int T = a.KH * a.KW, CS = a.CS, PS = G.PS, LWP = G.LWP;
   const int CPP = CS / 8;
+  auto stamp = [&](int k) {  // phase stamps (diagnostics: a.tstamp, bench/resnet20_kernels.py --phases)
+    if (a.tstamp && tid == 0) a.tstamp[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   // ---- one-time: zero image region (+ slack), stage (possibly tap-flipped) weights
   for (int i = tid; i < (G.LH * LWP * PS + G.slack) / 8; i += THREADS)
@@ -192,9 +196,11 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   long b = blockIdx.x;
   if (b < a.B && !(a.diag & 2)) load_src(b);
   __syncthreads();  // zero border before the first interior write
+  stamp(1);
   for (; b < a.B; b += gridDim.x) {
     if (!(a.diag & 2)) write_src();
     __syncthreads();
+    if (b == blockIdx.x) stamp(2);
     if (b + gridDim.x < a.B && !(a.diag & 2)) load_src(b + gridDim.x);
     for (int t0 = wm; t0 < tiles; t0 += WM * RT) {
       int pix[RT];
@@ -245,6 +251,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
 #pragma unroll
         for (int n = 0; n < NT; ++n) bfr[n] = bn[n];
       }
+      if (b == blockIdx.x && t0 == wm) stamp(3);
       // epilogue: lane holds rows (lane>>4)*4 + j of each tile (one 2x2 window when blocked),
       // column lane&15 of each n-tile
 #pragma unroll
@@ -290,6 +297,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
         }
       }
     }
+    if (b == blockIdx.x) stamp(4);
     if (G.stage_out && !(a.diag & 1)) {
       // the image's [OH*OW][N] output leaves as contiguous 16-B chunks (ReLU'-mask of the data
       // gradient applied here from 16-B mask loads): the per-lane 2-byte scatter cost ~8 of the
@@ -326,8 +334,10 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
         *reinterpret_cast<u32x4_t*>(a.y + ob + i * 8) = v;
       }
     }
+    if (b == blockIdx.x) stamp(5);
     __syncthreads();  // image b fully consumed before the next write
   }
+  stamp(6);
 }
 
 // ----------------------------------------------------- compile-time geometry

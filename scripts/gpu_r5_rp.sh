@@ -1,0 +1,14 @@
+# Round 5: shift-based row_pixel in the persistent conv: numerics + phases + kernels + step
+set -o pipefail
+O=gpurun_out/r5rp
+mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_imgconv.py tests/test_resnet.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
+timeout -k 10 120 python3 bench/resnet20_kernels.py --phases > $O/ph.txt 2>&1 || { tail -5 $O/ph.txt; exit 1; }
+grep -v amdgpu.ids $O/ph.txt
+timeout -k 10 120 python3 bench/resnet20_kernels.py --only "fwd,dgrad" > $O/k.txt 2>&1 || { tail -5 $O/k.txt; exit 1; }
+grep -v amdgpu.ids $O/k.txt
+for rep in 1 2; do
+  timeout -k 10 200 python3 bench.py --model resnet20 --steps 20 --warmup 5 > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+  echo "r20 $(grep -o '"ms_per_step": [0-9.]*' $O/bench.log)"
+done
