@@ -20,7 +20,15 @@ from dtfe import ops  # noqa: E402
 from dtfe.models.resnet import ResNetModel  # noqa: E402
 
 
+NO_GRAPH = False
+
+
 def per_launch_us(fn, n=40, reps=10):
+    if NO_GRAPH:  # (PMC collection: plain launches)
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return 0.0
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         for _ in range(2):
@@ -86,7 +94,10 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated substrings of the rows to time")
     ap.add_argument("--phases", action="store_true",
                     help="per-workgroup phase stamps of the whole-image conv (s_memrealtime, 10 ns ticks)")
+    ap.add_argument("--no_graph", action="store_true", help="plain launches (for rocprofv3 --pmc passes)")
     a = ap.parse_args()
+    global NO_GRAPH
+    NO_GRAPH = a.no_graph
     prog = ResNetModel(arch="resnet20").program(torch.device("cuda"), a.batch_size)
     prog.compute_grads()
     torch.cuda.synchronize()

@@ -241,11 +241,33 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, const Tensor& dx, int64_t B,
   dtfe::launch_conv_dgrad(a, cur_stream());
 }
 
+// [stats, gamma, beta, mean, invstd, moving_mean, moving_var] of a BatchNorm + ReLU formed on a
+// whole-image conv's source (the last four may be undefined: nothing saved / updated)
+dtfe::BnSrc bn_src_of(const optional<at::TensorList>& t, long R, int64_t C, double eps, double momentum, bool save) {
+  dtfe::BnSrc b{};
+  if (!t.has_value() || t->empty()) return b;
+  TORCH_CHECK(t->size() == 7, "bn_src: [stats, gamma, beta, mean, invstd, moving_mean, moving_var]");
+  const auto& v = *t;
+  for (int i = 0; i < 3; ++i) {
+    check_cuda(v[i], "bn_src");
+    TORCH_CHECK(v[i].scalar_type() == at::kFloat && v[i].numel() >= (i == 0 ? 2 : 1) * C, "bn_src: fp32 [C] / [2][C]");
+  }
+  b.stats = v[0].data_ptr<float>();
+  b.gamma = v[1].data_ptr<float>();
+  b.beta = v[2].data_ptr<float>();
+  auto opt = [&](int i) { return save && v[i].defined() ? v[i].data_ptr<float>() : nullptr; };
+  b.mean = opt(3); b.invstd = opt(4); b.moving_mean = opt(5); b.moving_var = opt(6);
+  TORCH_CHECK((b.moving_mean == nullptr) == (b.moving_var == nullptr), "bn_src: both moving averages or neither");
+  b.R = R; b.eps = (float)eps; b.momentum = (float)momentum;
+  return b;
+}
+
 bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, const optional<Tensor>& src_argmax,
              const Tensor& w, const optional<Tensor>& bias, const Tensor& y, const optional<Tensor>& argmax,
              const optional<Tensor>& relu_mask, int64_t B, int64_t SH, int64_t SW, int64_t CS, int64_t OH, int64_t OW,
              int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool,
-             int64_t dil, const optional<Tensor>& sc_src, int64_t sc_stride, const optional<Tensor>& tstamp) {
+             int64_t dil, const optional<Tensor>& sc_src, int64_t sc_stride, const optional<Tensor>& tstamp,
+             const optional<at::TensorList>& bn_src, double bn_eps, double bn_momentum, bool bn_save) {
   check_cuda(w, "w");
   TORCH_CHECK((src.has_value() && src->defined()) != (src_pooled.has_value() && src_pooled->defined()),
               "imgconv: exactly one of src / src_pooled");
@@ -266,6 +288,8 @@ bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
   TORCH_CHECK(w.numel() == N * KH * KW * CS, "imgconv: weight size");
   TORCH_CHECK(y.numel() == B * OH * OW * N / (pool ? 4 : 1), "imgconv: output size");
   a.tstamp = tstamp.has_value() && tstamp->defined() ? reinterpret_cast<uint64_t*>(tstamp->data_ptr()) : nullptr;
+  a.bns = bn_src_of(bn_src, (long)B * SH * SW, CS, bn_eps, bn_momentum, bn_save);
+  TORCH_CHECK(!a.bns.stats || a.src, "imgconv: BN-on-load needs a plain source");
   a.sc_src = ptr_or_null<dtfe::bf16>(sc_src);
   if (a.sc_src) {
     TORCH_CHECK(sc_stride >= 1 && OH % sc_stride == 0 && OW % sc_stride == 0 && sc_src->dim() == 4 &&
@@ -316,9 +340,11 @@ void conv1_gather_fwd(const Tensor& images, const Tensor& labels_src, int64_t se
 void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tensor>& dy_pooled,
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
-              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks) {
+              int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks,
+              const optional<at::TensorList>& bn_src, double bn_eps) {
   check_cuda(src, "src");
   dtfe::ImgWgradArgs a{};
+  a.bns = bn_src_of(bn_src, (long)B * SH * SW, CS, bn_eps, 0.0, false);
   a.max_blocks = (int)max_blocks;
   if (ws.has_value() && ws->defined()) {
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= dtfe::imgwgrad_ws_floats((int)N, (int)(KH * KW * CS)),
@@ -1045,11 +1071,12 @@ TORCH_LIBRARY(dtfe, m) {
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
       " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1, Tensor? sc_src=None,"
-      " int sc_stride=1, Tensor(e!)? tstamp=None) -> bool");
+      " int sc_stride=1, Tensor(e!)? tstamp=None, Tensor(f!)[]? bn_src=None, float bn_eps=0.001,"
+      " float bn_momentum=0.99, bool bn_save=False) -> bool");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"
-      " int max_blocks=0) -> ()");
+      " int max_blocks=0, Tensor[]? bn_src=None, float bn_eps=0.001) -> ()");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
       " int OW, int KH, int KW, int stride, int pad, float scale, Tensor? xf=None) -> ()");

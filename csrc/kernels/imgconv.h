@@ -1,4 +1,5 @@
 #pragma once
+#include "bn_chan.h"
 #include "common.h"
 
 namespace dtfe {
@@ -57,6 +58,9 @@ struct ImgConvArgs {
   // (sc_src: [B][OH/s][OW/s][sc_C], c < N <= sc_C) - ops.shortcut_grad_add without its pass
   const bf16* sc_src;
   int sc_stride, sc_C;
+  // BatchNorm + ReLU of the source formed while staging it (persistent kernel, plain source; the
+  // source is the BN's raw input).  bns.stats == nullptr: none
+  BnSrc bns;
 };
 
 // Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]
@@ -78,6 +82,7 @@ struct ImgWgradArgs {
   // runs beside other work (MNIST conv2's weight grad on its own graph branch)
   int max_blocks;
   int diag;                 // ablation bits for kernel experiments (DTFE_DIAG iw=<bits>; 0 in production)
+  BnSrc bns;                // BatchNorm + ReLU of src formed while staging it (persistent kernel; see ImgConvArgs)
 };
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);

@@ -316,9 +316,11 @@ bool launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
   if (a.CS <= 4 && (!a.src || a.flip_taps || a.dil > 1))
     throw std::runtime_error("imgconv: the few-channel path is forward-only");
   if (a.pool && ((a.OH | a.OW) & 1)) throw std::runtime_error("imgconv: pool needs even output dims");
+  if (a.bns.stats && (a.CS <= 4 || !a.src)) throw std::runtime_error("imgconv: BN-on-load needs a plain source");
   if (a.CS <= 4 && launch_conv1_copies_fwd(a, s)) return false;
   bool sc_done = false;
   if (a.CS > 4 && launch_imgconv_persistent(a, s, &sc_done)) return sc_done;
+  if (a.bns.stats) throw std::runtime_error("imgconv: BN-on-load needs the persistent kernel (B >= 64)");
   if (a.dil > 1) throw std::runtime_error("imgconv: dilated sources need the persistent kernel (B >= 64)");
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
   const size_t lds = (size_t)LH * LW * a.CS * sizeof(bf16);
@@ -652,6 +654,7 @@ static void launch_wg1(const ImgWgradArgs& a0, hipStream_t s) {
 
 void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s) {
   if (!imgwgrad_supported(a)) throw std::runtime_error("imgwgrad: shape not supported");
+  if (a.bns.stats && a.CS <= 4) throw std::runtime_error("imgwgrad: BN-on-load needs the persistent kernel");
   if (a.CS <= 4) {
     if (!a.src) throw std::runtime_error("imgwgrad: few-channel path needs src");
     if (launch_conv1_copies_wgrad(a, s)) return;
@@ -663,6 +666,7 @@ void launch_imgwgrad(const ImgWgradArgs& a, hipStream_t s) {
     return;
   }
   if (launch_imgwgrad_persistent(a, s)) return;
+  if (a.bns.stats) throw std::runtime_error("imgwgrad: BN-on-load needs the persistent kernel (B >= 128)");
   if (a.N <= 16) launch_wg<1, 8>(a, s);
   else if (a.N <= 32) launch_wg<2, 6>(a, s);
   else launch_wg<4, 4>(a, s);

@@ -82,7 +82,7 @@ __host__ __device__ inline bool row_pixel(int m, int OH, int OW, int blocked, in
   return true;
 }
 
-template <int NT, int RT, int WM, int WN, int NPF, bool POOLED>
+template <int NT, int RT, int WM, int WN, int NPF, bool POOLED, bool BNX = false>
 __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArgs a, PGeom G) {
   constexpr int THREADS = 64 * WM * WN;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
@@ -92,6 +92,15 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   const int wm = wid % WM, wn = wid / WM;
   const int T = a.KH * a.KW, CS = a.CS, PS = G.PS, LWP = G.LWP;
   const int CPP = CS / 8;
+  // BatchNorm + ReLU of the source on staging (a.bns): this thread's chunks are channels
+  // [(tid % CPP) * 8, +8) of every pixel (THREADS % CPP == 0); workgroup 0 saves the statistics
+  // (a compile-time instance: the plain kernel keeps its registers and schedule)
+  constexpr bool bnx = BNX && !POOLED;
+  float bsc[8], bsh[8];
+  if constexpr (bnx) {
+    bn_src_coeffs(a.bns, a.src, CS, (tid % CPP) * 8, bsc, bsh);
+    if (blockIdx.x == 0) bn_src_save(a.bns, a.src, CS, THREADS);
+  }
   auto stamp = [&](int k) {  // phase stamps (diagnostics: a.tstamp, bench/resnet20_kernels.py --phases)
     if (a.tstamp && tid == 0) a.tstamp[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
@@ -172,7 +181,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
     for (int j = 0; j < NPF; ++j) {
       if (dst[j] < 0) continue;
       if (!POOLED) {
-        *reinterpret_cast<u32x4_t*>(img + dst[j]) = pf[j];
+        *reinterpret_cast<u32x4_t*>(img + dst[j]) = bnx ? bn_relu_chunk(pf[j], bsc, bsh) : pf[j];
       } else {
         u32x4_t v[4];
         unpool4(pf[j], pam[j], v);
@@ -696,6 +705,20 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(THREADS), lds, s, ad, G);
   };
   if (G.npf < 1 || G.npf > 4) return false;
+  if constexpr (!POOLED) {
+    if (a.bns.stats) {
+      switch (G.npf) {
+        case 1: go(imgconv_persist_kernel<NT, RT, WM, WN, 1, false, true>); break;
+        case 2: go(imgconv_persist_kernel<NT, RT, WM, WN, 2, false, true>); break;
+        case 3: go(imgconv_persist_kernel<NT, RT, WM, WN, 3, false, true>); break;
+        default: go(imgconv_persist_kernel<NT, RT, WM, WN, 4, false, true>); break;
+      }
+      if (sc_done) *sc_done = sc;
+      return true;
+    }
+  } else {
+    if (a.bns.stats) return false;
+  }
   switch (G.npf) {
     case 1: go(imgconv_persist_kernel<NT, RT, WM, WN, 1, POOLED>); break;
     case 2: go(imgconv_persist_kernel<NT, RT, WM, WN, 2, POOLED>); break;
@@ -742,7 +765,7 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
 bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   if (sc_done) *sc_done = false;
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
-  if (a.OH == 14 && a.OW == 14 && a.B >= 256) {
+  if (a.OH == 14 && a.OW == 14 && a.B >= 256 && !a.bns.stats) {
     // compile-time geometry, one 16-row tile per wave (13 waves); 2 / 4 tiles per wave (7 / 4
     // waves) measured slower and were removed in round 3
     if (launch_fixed<32, 5, 5, 20, 48, 4, 1, 13, false, ACT_RELU>(a, s)) return true;  // conv2 forward

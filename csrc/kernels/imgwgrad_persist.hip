@@ -66,7 +66,7 @@ __host__ __device__ inline int wp_part_len(int MT, int CTW, int N) { return 8 * 
 // [cg*CTW, +CTW) over the k-steps s = kg (mod KG), and the k-groups' accumulators are summed through
 // LDS before the flush.  Small-KC layers (ResNet-20: 9 or 18 column tiles) otherwise leave most
 // waves with dead tiles while one or two carry every MFMA (profiles/r5_resnet20_kernels.txt).
-template <int MT, int CTW, int NPFS, int NPFD, bool POOLED, int KG = 1>
+template <int MT, int CTW, int NPFS, int NPFD, bool POOLED, int KG = 1, bool BNX = false>
 __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, WPGeom G) {
   constexpr int THREADS = 512;
   constexpr int CG = 8 / KG;
@@ -114,6 +114,11 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
       ddst[j] = (oy * G.OWP + ox) * NPS + cc * 8;
     }
   }
+  // BatchNorm + ReLU of the source on staging (a.bns; the conv forward saved the statistics): this
+  // thread's source chunks are channels [(tid % (CS/8)) * 8, +8) (512 % (CS/8) == 0)
+  constexpr bool bnx = BNX;  // (compile-time instance: the plain kernel is unchanged)
+  float bsc[8], bsh[8];
+  if constexpr (bnx) bn_src_coeffs(a.bns, a.src, CS, (tid % (CS / 8)) * 8, bsc, bsh);
   u32x4_t sreg[NPFS], dreg[NPFD];
   u32x2_t dam[NPFD];
   auto load_img = [&](long b) {
@@ -139,7 +144,10 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
   auto write_img = [&]() {
 #pragma unroll
     for (int j = 0; j < NPFS; ++j)
-      if (sdst[j] >= 0) *reinterpret_cast<u32x4_t*>(simg + sdst[j]) = sreg[j];
+      if (sdst[j] >= 0) {
+        if constexpr (bnx) *reinterpret_cast<u32x4_t*>(simg + sdst[j]) = bn_relu_chunk(sreg[j], bsc, bsh);
+        else *reinterpret_cast<u32x4_t*>(simg + sdst[j]) = sreg[j];
+      }
 #pragma unroll
     for (int j = 0; j < NPFD; ++j) {
       if (ddst[j] < 0) continue;
@@ -432,7 +440,7 @@ WPGeom wp_geom(const ImgWgradArgs& a) {
 
 size_t wp_lds(const WPGeom& G) { return ((size_t)G.img_off + (size_t)G.nk * 32 * G.NPS) * sizeof(bf16); }
 
-template <int MT, int CTW, bool POOLED, int KG = 1>
+template <int MT, int CTW, bool POOLED, int KG = 1, bool BNX = false>
 bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   size_t lds = wp_lds(G);
   if (lds > 150 * 1024) return false;
@@ -465,15 +473,15 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   // prefetch chunks per thread (source, dY): 1, 2 or 4 each
   auto q = [](int n) { return n <= 1 ? 1 : (n <= 2 ? 2 : (n <= 4 ? 4 : 0)); };
   switch (q(npfs) * 8 + q(npfd)) {
-    case 9: return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED, KG>);
-    case 10: return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED, KG>);
-    case 12: return go(imgwgrad_persist_kernel<MT, CTW, 1, 4, POOLED, KG>);
-    case 17: return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED, KG>);
-    case 18: return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED, KG>);
-    case 20: return go(imgwgrad_persist_kernel<MT, CTW, 2, 4, POOLED, KG>);
-    case 33: return go(imgwgrad_persist_kernel<MT, CTW, 4, 1, POOLED, KG>);
-    case 34: return go(imgwgrad_persist_kernel<MT, CTW, 4, 2, POOLED, KG>);
-    case 36: return go(imgwgrad_persist_kernel<MT, CTW, 4, 4, POOLED, KG>);
+    case 9: return go(imgwgrad_persist_kernel<MT, CTW, 1, 1, POOLED, KG, BNX>);
+    case 10: return go(imgwgrad_persist_kernel<MT, CTW, 1, 2, POOLED, KG, BNX>);
+    case 12: return go(imgwgrad_persist_kernel<MT, CTW, 1, 4, POOLED, KG, BNX>);
+    case 17: return go(imgwgrad_persist_kernel<MT, CTW, 2, 1, POOLED, KG, BNX>);
+    case 18: return go(imgwgrad_persist_kernel<MT, CTW, 2, 2, POOLED, KG, BNX>);
+    case 20: return go(imgwgrad_persist_kernel<MT, CTW, 2, 4, POOLED, KG, BNX>);
+    case 33: return go(imgwgrad_persist_kernel<MT, CTW, 4, 1, POOLED, KG, BNX>);
+    case 34: return go(imgwgrad_persist_kernel<MT, CTW, 4, 2, POOLED, KG, BNX>);
+    case 36: return go(imgwgrad_persist_kernel<MT, CTW, 4, 4, POOLED, KG, BNX>);
     default: return false;
   }
 }
@@ -496,11 +504,18 @@ bool launch_imgwgrad_persistent(const ImgWgradArgs& a, hipStream_t s) {
   // per column group, no bias gradient): k-groups of waves instead (KG, see the kernel)
   const int ctw = (G.ctiles + 7) / 8;
   const bool ks = !a.db && !(diag_bits("iwk") & 1);
-  if (ks && G.ctiles <= 9 && a.N <= 16 && !pooled) return wp_launch<1, 9, false, 8>(a, G, s);
-  if (ks && G.ctiles <= 9 && a.N <= 32 && !pooled) return wp_launch<2, 9, false, 8>(a, G, s);
-  if (ks && G.ctiles <= 18 && a.N <= 32 && !pooled) return wp_launch<2, 9, false, 4>(a, G, s);
+  // (BN + ReLU of the source on staging: compile-time instances of the ResNet configurations only)
+  const bool bn = a.bns.stats != nullptr;
+  if (ks && G.ctiles <= 9 && a.N <= 16 && !pooled)
+    return bn ? wp_launch<1, 9, false, 8, true>(a, G, s) : wp_launch<1, 9, false, 8>(a, G, s);
+  if (ks && G.ctiles <= 9 && a.N <= 32 && !pooled)
+    return bn ? wp_launch<2, 9, false, 8, true>(a, G, s) : wp_launch<2, 9, false, 8>(a, G, s);
+  if (ks && G.ctiles <= 18 && a.N <= 32 && !pooled)
+    return bn ? wp_launch<2, 9, false, 4, true>(a, G, s) : wp_launch<2, 9, false, 4>(a, G, s);
+  if (a.N > 32 && ks && G.ctiles <= 40 && !pooled)
+    return bn ? wp_launch<4, 5, false, 1, true>(a, G, s) : wp_launch<4, 5, false>(a, G, s);
+  if (bn) return false;
   if (a.N > 32) {
-    if (ks && G.ctiles <= 40 && !pooled) return wp_launch<4, 5, false>(a, G, s);
     if (ctw <= 7) return pooled ? wp_launch<4, 7, true>(a, G, s) : wp_launch<4, 7, false>(a, G, s);
     return false;
   }

@@ -7,6 +7,7 @@
 // Channel statistics are reduced per workgroup through LDS and then added to
 // the [2][C] accumulators with one atomic per channel and workgroup.
 #include "norm.h"
+#include "bn_chan.h"
 
 #include <cstdlib>
 #include <stdexcept>
@@ -107,12 +108,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 // the materialised BN outputs differ in the last place)
 __device__ __forceinline__ void chan_params_of(const bf16* x, const float* stats, long R, int C, float eps, int c,
                                                float& mean, float& invstd) {
-#pragma clang fp contract(off)
-  const float inv_r = 1.f / (float)R;
-  const float d = stats[c] * inv_r;
-  mean = bf2f(x[c]) + d;
-  const float var = fmaxf(stats[C + c] * inv_r - d * d, 0.f);
-  invstd = rsqrtf(var + eps);
+  bn_chan_params(x, stats, R, C, eps, c, mean, invstd);  // (bn_chan.h: shared with the whole-image convs)
 }
 
 __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean, float& invstd) {
@@ -122,15 +118,7 @@ __device__ __forceinline__ void chan_params(const BnArgs& a, int c, float& mean,
 // saved statistics + moving averages of one channel (TF: unbiased batch variance)
 __device__ __forceinline__ void save_chan(const BnArgs& a, int c, float mean, float invstd, float* smean,
                                           float* sinv, float* mm, float* mv) {
-#pragma clang fp contract(off)
-  if (smean) smean[c] = mean;
-  if (sinv) sinv[c] = invstd;
-  if (mm) {
-    const float var = 1.f / (invstd * invstd) - a.eps;
-    const float unb = a.R > 1 ? var * (float)a.R / (float)(a.R - 1) : var;
-    mm[c] = mm[c] * a.momentum + mean * (1.f - a.momentum);
-    mv[c] = mv[c] * a.momentum + unb * (1.f - a.momentum);
-  }
+  bn_save_chan(a.R, a.eps, a.momentum, c, mean, invstd, smean, sinv, mm, mv);
 }
 
 __device__ __forceinline__ long res_offset(const BnArgs& a, long r, int chunk, bool identity) {

@@ -137,20 +137,31 @@ class Conv:
         preceding BatchNorm + ReLU on their operand loads (ops.conv_fwd / conv_wgrad ``xf``)."""
         return not self.img_fwd and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0
 
-    def fwd(self, x, stats=None, xf=None):
+    def fwd(self, x, stats=None, xf=None, bn_src=None):
         """Forward; ``stats``: the following BatchNorm's [2][C] accumulators, filled by the conv
         launch itself where it can (returns True then; the BN skips its statistics pass).  ``xf``:
-        x is the input of the preceding BatchNorm + ReLU, applied on the operand load (BN.fwd_fold)."""
+        x is the input of the preceding BatchNorm + ReLU, applied on the operand load (BN.fwd_fold).
+        ``bn_src``: that BN (BN.src_fold) for the whole-image kernel, which forms BN + ReLU while
+        staging x and saves the BN's statistics / moving averages."""
         if self.img_fwd:
             assert xf is None
+            if bn_src is not None:
+                ops.imgconv(self.w, self.y, src=x, bn_src=bn_src.src_args(), bn_eps=BN_EPS, bn_momentum=BN_MOMENTUM,
+                            bn_save=True, **self.ic)
+                return self.y, False
             ops.imgconv(self.w, self.y, src=x, **self.ic)
             return self.y, False
+        assert bn_src is None
         ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats, xf=xf)
         return self.y, stats is not None
 
-    def wgrad(self, dy, x, xf=None, after=None):
+    def wgrad(self, dy, x, xf=None, after=None, bn_src=None):
         """``after``: the side stream's fork point (SideStream.fork_point, taken when dy was final).
-        ``xf``: as in fwd."""
+        ``xf`` / ``bn_src``: as in fwd (x is then the BN's raw input)."""
+        if bn_src is not None:
+            assert self.img_wgrad
+            ops.imgwgrad(x, self.gw, None, dy=dy, bn_src=bn_src.src_args(), bn_eps=BN_EPS, **self.ic)
+            return
         side = getattr(self, "side", None)
         if side is not None and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0:
             side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g, xf=xf), after)
@@ -242,6 +253,8 @@ _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
 # rewrite costs a barrier per k-tile of their 4-stage ring - 319 vs 157 us per 128x128 launch).  Kept as
 # a tested path (tests/test_resnet.py) for the next kernel iteration.  (Test hook, not a knob.)
 _FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "0") == "1"
+# ResNet-20: bn1's apply formed by conv2's whole-image kernels (BN.src_fold).  (A/B hook, not a knob.)
+_R20_SRC_FOLD = os.environ.get("DTFE_R20_SRC_FOLD", "1") == "1"
 
 
 class BN:
@@ -283,6 +296,22 @@ class BN:
                         momentum=BN_MOMENTUM)
         self.mask_from_x, self.use_bits, self.folded = True, False, True
         return x
+
+    def src_fold(self, x):
+        """BN + ReLU whose output only whole-image convs read (ResNet-20's bn1 -> conv2 forward and
+        weight gradient): no apply pass - the consumers form it from the raw input x while staging
+        it (Conv.fwd / wgrad ``bn_src=self``; the forward's kernel saves mean / invstd and updates the
+        moving averages).  The backward recomputes the ReLU mask from x.  Returns x."""
+        x, have_stats = x if isinstance(x, tuple) else (x, False)
+        if not have_stats:
+            ops.bn_stats(x, self.stats)
+        self.mask_from_x, self.use_bits, self.folded = True, False, False
+        return x
+
+    def src_args(self):
+        P = self.P
+        return [self.stats, P.view(self.gamma), P.view(self.beta), self.mean, self.invstd, P.view(self.mm),
+                P.view(self.mv)]
 
     def stats_only(self, x):
         """A projection shortcut's BN (no activation) whose apply is folded into the residual add of
@@ -415,6 +444,7 @@ class BasicBlock:
         self.bn2 = BN(reg, cout)
         self.OH, self.OW = self.conv2.OH, self.conv2.OW
         self.stats_len = 6 * cout * 2 + 64
+        self.src_fold = False
 
     def bind(self, P, B, dev, arena):
         for c in (self.conv1, self.conv2):
@@ -427,12 +457,22 @@ class BasicBlock:
 
     def fwd(self, x):
         self.x = x
+        # bn1's apply formed by conv2's whole-image kernels while they stage its input (forward and
+        # weight gradient): no bn_apply pass (profiles/r5_resnet20_kernels.txt)
+        self.src_fold = (_R20_SRC_FOLD and not BN.infer and x.is_cuda and self.conv2.img_fwd
+                         and self.conv2.img_wgrad and self.conv2.B >= 128)
+        if self.src_fold:
+            r1 = self.bn1.src_fold(self.conv1.fwd(x, self.bn1.stats))
+            return self.bn2.fwd(self.conv2.fwd(r1, self.bn2.stats, bn_src=self.bn1), res=x, rstride=self.stride)
         h1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats))
         return self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats), res=x, rstride=self.stride)
 
     def bwd(self, dout, dx):
         self.bn2.bwd(dout, self.conv2.y, self.dc2, dres=self.dres)
-        self.conv2.wgrad(self.dc2, self.bn1.y)
+        if self.src_fold:
+            self.conv2.wgrad(self.dc2, self.conv1.y, bn_src=self.bn1)
+        else:
+            self.conv2.wgrad(self.dc2, self.bn1.y)
         self.conv2.dgrad(self.dc2, self.dh1)
         self.bn1.bwd(self.dh1, self.conv1.y, self.dc1)
         self.conv1.wgrad(self.dc1, self.x)

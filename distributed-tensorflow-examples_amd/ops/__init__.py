@@ -359,17 +359,30 @@ def _unpooled_nhwc(pooled, argmax, B, H, W, C):
     return out.view(B, H, W, C)
 
 
+def _bn_src_ref(src, bn_src, eps, momentum, save):
+    """CPU oracle of a BN + ReLU formed on a conv's source (bn_src = [stats, gamma, beta, mean,
+    invstd, moving_mean, moving_var]): bn_apply's output."""
+    st, g, b, m, i, mm, mv = bn_src
+    h = torch.empty_like(src)
+    kw = dict(mean=m, invstd=i, moving_mean=mm, moving_var=mv) if save else {}
+    bn_apply(src, st, g, b, h, eps=eps, momentum=momentum, act=ACT_RELU, **kw)
+    return h
+
+
 def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None, src_pooled=None,
             src_argmax=None, bias=None, argmax=None, relu_mask=None, flip_taps=False, act=ACT_NONE, pool=False,
-            dil=1):
+            dil=1, bn_src=None, bn_eps=1e-3, bn_momentum=0.99, bn_save=False):
     """Whole-image LDS convolution (small feature maps): forward (+bias/act/pool) or, with
     flip_taps and pad = K-1-pad, the data gradient of a stride-1 conv (w = Wt [cin][tap][cout]).
     The source may be un-pooled on load from (src_pooled, src_argmax), or dilated (``dil``: source
     pixel (y, x) at (y*dil, x*dil), zeros between - the data gradient of a stride-``dil`` conv)."""
     if y.is_cuda:
         require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW, N, KH,
-                          KW, stride, pad, flip_taps, act, pool, dil)
+                          KW, stride, pad, flip_taps, act, pool, dil, bn_src=bn_src, bn_eps=bn_eps,
+                          bn_momentum=bn_momentum, bn_save=bn_save)
         return y
+    if bn_src is not None:  # BN + ReLU formed on the source (the kernel does it while staging)
+        src = _bn_src_ref(src, bn_src, bn_eps, bn_momentum, bn_save)
     s = src.float().view(B, SH, SW, CS) if src is not None else _unpooled_nhwc(src_pooled, src_argmax, B, SH, SW, CS)
     if dil > 1:
         sd = torch.zeros(B, SH * dil, SW * dil, CS)
@@ -436,7 +449,7 @@ def wgrad_workspace(device, numel):
 
 
 def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
-             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0):
+             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0, bn_src=None, bn_eps=1e-3):
     """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY.
     On the GPU the persistent kernel stores per-workgroup partials in `workspace`
     (default: a cached per-device buffer) and a second kernel sums them."""
@@ -444,8 +457,10 @@ def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, 
         if workspace is None and (CS % 16 == 0 or CS == 1):
             workspace = wgrad_workspace(dw.device, wgrad_ws_floats(N, KH * KW * CS))
         require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
-                           scale, workspace, max_blocks)
+                           scale, workspace, max_blocks, bn_src=bn_src, bn_eps=bn_eps)
         return
+    if bn_src is not None:  # the source's BN + ReLU (nothing saved: the forward did)
+        src = _bn_src_ref(src, bn_src, bn_eps, 0.99, False)
     d = dy.float().view(B, OH, OW, N) if dy is not None else _unpooled_nhwc(dy_pooled, dy_argmax, B, OH, OW, N)
     gw = torch.nn.grad.conv2d_weight(src.float().view(B, SH, SW, CS).permute(0, 3, 1, 2), (N, CS, KH, KW),
                                      d.permute(0, 3, 1, 2), stride=stride, padding=pad)

@@ -283,3 +283,56 @@ def test_imgwgrad_persistent_kgroups(case):
     dw2 = torch.zeros_like(dw)
     ops.imgwgrad(x, dw2, None, dy=dy, **kw)  # a second launch (workspace / LDS reuse)
     assert torch.equal(dw, dw2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,C", [(256, 32, 16), (200, 16, 32), (160, 8, 64)])
+def test_imgconv_bn_src_on_load_matches_materialised(B, H, C):
+    """A BN + ReLU formed on the whole-image conv's source while staging it (bn_src) == bn_apply's
+    materialised output fed to the conv: forward output, saved mean / invstd, moving averages and
+    the weight gradient bit for bit."""
+    torch.manual_seed(12)
+    x = (torch.randn(B, H, H, C) * 2 + 0.5).to(DEV, torch.bfloat16)
+    stats = torch.zeros(2 * C, device=DEV)
+    ops.bn_stats(x, stats)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    mm0, mv0 = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5
+    h = torch.empty_like(x)
+    ref = [torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), mm0.clone(), mv0.clone()]
+    ops.bn_apply(x, stats, gamma, beta, h, mean=ref[0], invstd=ref[1], moving_mean=ref[2], moving_var=ref[3],
+                 eps=1e-3, momentum=0.99)
+    w = (torch.randn(C, 3, 3, C) * 0.1).to(DEV, torch.bfloat16)
+    kw = dict(B=B, SH=H, SW=H, CS=C, OH=H, OW=H, N=C, KH=3, KW=3, stride=1, pad=1)
+    y_ref = torch.empty_like(x)
+    ops.imgconv(w, y_ref, src=h, **kw)
+    got = [torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), mm0.clone(), mv0.clone()]
+    y = torch.empty_like(x)
+    ops.imgconv(w, y, src=x, bn_src=[stats, gamma, beta] + got, bn_eps=1e-3, bn_momentum=0.99, bn_save=True, **kw)
+    assert torch.equal(y, y_ref)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    dy = torch.randn(B, H, H, C).to(DEV, torch.bfloat16)
+    wk = {k: v for k, v in kw.items()}
+    dw_ref, dw = torch.zeros(C, 3, 3, C, device=DEV), torch.zeros(C, 3, 3, C, device=DEV)
+    ops.imgwgrad(h, dw_ref, None, dy=dy, **wk)
+    ops.imgwgrad(x, dw, None, dy=dy, bn_src=[stats, gamma, beta] + got, bn_eps=1e-3, **wk)
+    assert torch.equal(dw, dw_ref)
+
+
+def test_imgconv_bn_src_cpu_oracle():
+    torch.manual_seed(13)
+    B, H, C = 2, 8, 16
+    x = torch.randn(B, H, H, C).bfloat16()
+    stats = torch.zeros(2 * C)
+    ops.bn_stats(x, stats)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    h = torch.empty_like(x)
+    ops.bn_apply(x, stats, gamma, beta, h, eps=1e-3, momentum=0.99)
+    w = (torch.randn(C, 3, 3, C) * 0.1).bfloat16()
+    kw = dict(B=B, SH=H, SW=H, CS=C, OH=H, OW=H, N=C, KH=3, KW=3, stride=1, pad=1)
+    y_ref, y = torch.empty_like(x), torch.empty_like(x)
+    ops.imgconv(w, y_ref, src=h, **kw)
+    z = torch.zeros(C)
+    ops.imgconv(w, y, src=x, bn_src=[stats, gamma, beta, z, z.clone(), z.clone(), z.clone() + 1], **kw)
+    assert torch.equal(y, y_ref)

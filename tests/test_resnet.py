@@ -534,3 +534,34 @@ def test_bn_finalize_and_xf_reference_cpu():
     ops.conv_wgrad(dy, h, d1, None, g)
     ops.conv_wgrad(dy, x, d2, None, g, xf=xf)
     assert torch.allclose(d1, d2, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_resnet20_bn_src_fold_matches_materialised_gpu(monkeypatch):
+    """ResNet-20 at the bench batch with bn1's apply formed by conv2's whole-image kernels (BN.src_fold)
+    vs the materialised bn_apply schedule (the kernels themselves are pinned bit for bit by
+    test_imgconv_bn_src_on_load_matches_materialised): loss, gradients and moving averages within
+    the run-to-run noise of the BN statistics' atomics (measured here by repeating the unfolded run)."""
+    import dtfe.models.resnet as R
+    torch.manual_seed(0)
+    B = 256
+    x = torch.rand(B, 32, 32, 3)
+    y = torch.nn.functional.one_hot(torch.randint(0, 10, (B,)), 10).float()
+    runs = []
+    for fold in (False, False, True):
+        monkeypatch.setattr(R, "_R20_SRC_FOLD", fold)
+        prog = ResNetModel(arch="resnet20").program("cuda", B, seed=3)
+        prog.load_batch((x.cuda(), y.cuda()))
+        m = prog.compute_grads()
+        torch.cuda.synchronize()
+        assert all(b.src_fold == fold for b in prog.L["blocks"])
+        bns = prog.batchnorms()
+        mov = torch.cat([prog.P.view(bn.mm) for bn in bns] + [prog.P.view(bn.mv) for bn in bns])
+        runs.append((float(m["loss"]), prog.P.grad.clone(), mov.clone()))
+    (l0, g0, m0), (l1, g1, m1), (l2, g2, m2) = runs
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-12))
+    assert abs(l2 - l0) <= 4 * abs(l1 - l0) + 1e-3 * abs(l0)
+    assert rel(g2, g0) <= 4 * rel(g1, g0) + 2e-2
+    assert rel(m2, m0) <= 4 * rel(m1, m0) + 1e-4
