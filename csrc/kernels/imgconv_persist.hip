@@ -62,7 +62,26 @@ struct PGeom {
   int npf;        // chunks per thread
   int blocked;    // output rows in 2x2-window order (OH, OW even)
   int stage_out;  // un-pooled output staged in LDS [OH*OW][N] after the image, stored as 16-B rows
+  int lg_ow;      // log2(OW) when OW is a power of two (row_pixel by shifts), else -1
 };
+
+// row_pixel for OW = 2^lg: shifts and masks instead of two integer divisions by a runtime OW (each
+// ~30 VALU; the staged epilogue evaluates it per output value - rocprof: ~70 VALU per MFMA in the
+// stage-1 ResNet-20 conv, profiles/r5_resnet20_kernels.txt)
+__device__ __forceinline__ bool row_pixel_p2(int m, int OH, int lg, int blocked, int& oy, int& ox) {
+  if (blocked) {
+    const int t = m >> 4, quad = (m >> 2) & 3, q = m & 3;
+    const int w = t * 4 + (quad == 0 ? 0 : quad == 1 ? 2 : quad == 2 ? 3 : 1);
+    if (w >= (OH >> 1) << (lg - 1)) return false;
+    oy = 2 * (w >> (lg - 1)) + (q >> 1);
+    ox = 2 * (w & ((1 << (lg - 1)) - 1)) + (q & 1);
+    return true;
+  }
+  if (m >= OH << lg) return false;
+  oy = m >> lg;
+  ox = m & ((1 << lg) - 1);
+  return true;
+}
 
 // output row m of an image -> (oy, ox); false for padding rows of the last tile.
 // Blocked order: row quad `quad` of 16-row tile t is window t*4 + {0,2,3,1}[quad].
@@ -92,6 +111,9 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   const int wm = wid % WM, wn = wid / WM;
   const int T = a.KH * a.KW, CS = a.CS, PS = G.PS, LWP = G.LWP;
   const int CPP = CS / 8;
+  auto rp = [&](int m, int blocked, int& oy, int& ox) {
+    return G.lg_ow > 0 ? row_pixel_p2(m, a.OH, G.lg_ow, blocked, oy, ox) : row_pixel(m, a.OH, a.OW, blocked, oy, ox);
+  };
   // BatchNorm + ReLU of the source on staging (a.bns): this thread's chunks are channels
   // [(tid % CPP) * 8, +8) of every pixel (THREADS % CPP == 0); workgroup 0 saves the statistics
   // (a compile-time instance: the plain kernel keeps its registers and schedule)
@@ -112,13 +134,23 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   {
     // 8 loads in flight per thread: the ~100 KB prologue costs a few latencies, not one per chunk
     const int kc_row = G.KP / 8, total = G.NTOT * kc_row;
+    // (n, chunk) of i = i0 + u * THREADS stepped incrementally: one runtime division per thread, not
+    // one per chunk (~30 VALU each)
+    const int dn = THREADS / kc_row, dr = THREADS - dn * kc_row;
+    int n_i = tid / kc_row, r_i = tid - n_i * kc_row;
     for (int i0 = tid; i0 < total; i0 += 8 * THREADS) {
       u32x4_t v[8];
       int off[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int i = i0 + u * THREADS;
-        const int n = i / kc_row, k = (i - n * kc_row) * 8;
+        const int n = n_i, k = r_i * 8;
+        n_i += dn;
+        r_i += dr;
+        if (r_i >= kc_row) {
+          r_i -= kc_row;
+          ++n_i;
+        }
         off[u] = i < total ? n * G.KP + k : -1;
         v[u] = u32x4_t{0u, 0u, 0u, 0u};
         if (i < total && n < a.N && k < G.K && !(a.diag & 8)) {
@@ -217,7 +249,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
       for (int r = 0; r < RT; ++r) {
         int oy = 0, ox = 0;
         // padding rows read pixel 0 and are dropped by the epilogue
-        row_pixel((t0 + WM * r) * 16 + (lane & 15), a.OH, a.OW, G.blocked, oy, ox);
+        rp((t0 + WM * r) * 16 + (lane & 15), G.blocked, oy, ox);
         pix[r] = (oy * a.stride * LWP + ox * a.stride) * PS;
       }
       f32x4_t acc[RT][NT];
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
           const f32x4_t v = acc[r][n];
           if (a.pool) {  // pool implies blocked rows: the quad is one window
             int oy, ox;
-            if (!row_pixel(m0, a.OH, a.OW, 1, oy, ox)) continue;
+            if (!rp(m0, 1, oy, ox)) continue;
             int am = 0;
             float mx = v[0];
 #pragma unroll
@@ -289,14 +321,14 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               int oy, ox;
-              if (!row_pixel(m0 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
-              sy[(oy * a.OW + ox) * a.N + col] = f2bf(apply_act(v[j] + bias, a.act));
+              if (!rp(m0 + j, G.blocked, oy, ox)) continue;
+              sy[((oy << G.lg_ow) + ox) * a.N + col] = f2bf(apply_act(v[j] + bias, a.act));
             }
           } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               int oy, ox;
-              if (!row_pixel(m0 + j, a.OH, a.OW, G.blocked, oy, ox)) continue;
+              if (!rp(m0 + j, G.blocked, oy, ox)) continue;
               const long o = ((b * a.OH + oy) * a.OW + ox) * a.N + col;
               float x = apply_act(v[j] + bias, a.act);
               if (a.relu_mask && !(bf2f(a.relu_mask[o]) > 0.f)) x = 0.f;
@@ -644,6 +676,9 @@ double a_read_conflicts(int PSs, int LWP, int OH, int OW, int stride, int blocke
 PGeom persist_geom(const ImgConvArgs& a, int WN, int NT, int threads) {
   PGeom G;
   G.stage_out = 0;
+  G.lg_ow = -1;
+  for (int l = 1; l <= 10; ++l)
+    if (a.OW == (1 << l)) G.lg_ow = l;
   G.LH = (a.OH - 1) * a.stride + a.KH;
   G.LW = (a.OW - 1) * a.stride + a.KW;
   G.K = a.KH * a.KW * a.CS;
@@ -690,7 +725,7 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   size_t lds = persist_lds(G);
   if (lds > 160 * 1024) return false;
   const size_t stage = (size_t)a.OH * a.OW * a.N * sizeof(bf16);
-  G.stage_out = !a.pool && a.N % 8 == 0 && lds + stage <= 160 * 1024 && !(diag_bits("icr") & 16);
+  G.stage_out = !a.pool && a.N % 8 == 0 && lds + stage <= 160 * 1024 && !(diag_bits("icr") & 16) && G.lg_ow > 0;
   if (G.stage_out) lds += stage;
   const bool sc = a.sc_src && G.stage_out && a.sc_stride >= 1 && a.OH % a.sc_stride == 0 &&
                   a.OW % a.sc_stride == 0 && a.sc_C % 8 == 0 && a.N <= a.sc_C;
