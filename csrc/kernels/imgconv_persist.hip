@@ -101,7 +101,12 @@ __host__ __device__ inline bool row_pixel(int m, int OH, int OW, int blocked, in
   return true;
 }
 
-template <int NT, int RT, int WM, int WN, int NPF, bool POOLED, bool BNX = false>
+// CSC != 0: a 3x3 conv over CSC source channels (ResNet-20) with the k walk in closed form - step s's
+// A offset from k = 32 s + 8 g by divisions by compile-time constants - and the step loop unrolled
+// with its fragment reads pinned one step ahead of the MFMAs.  The runtime walk (a per-step while
+// loop under exec masking, ~35 instructions and the LDS read latency exposed per 2 MFMAs in the
+// stage-1 instance) stays for every other shape.
+template <int NT, int RT, int WM, int WN, int NPF, bool POOLED, bool BNX = false, int CSC = 0>
 __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArgs a, PGeom G) {
   constexpr int THREADS = 64 * WM * WN;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
@@ -257,6 +262,43 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
       for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[r][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr (CSC != 0) {
+        constexpr int NK = (9 * CSC + 31) / 32, KP = NK * 32 + 16;
+        auto toff_of = [&](int st) {
+          const int k = 32 * st + 8 * g, tap = k / CSC, kh = tap / 3;
+          return (kh * LWP + (tap - 3 * kh)) * PS + (k - tap * CSC);
+        };
+        u32x4_t fa[2][RT], fb[2][NT];
+        {
+          const int t = toff_of(0);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) fb[0][n] = *reinterpret_cast<const u32x4_t*>(wlane + n * 16 * KP);
+#pragma unroll
+          for (int r = 0; r < RT; ++r) fa[0][r] = *reinterpret_cast<const u32x4_t*>(img + pix[r] + t);
+        }
+        if (!(a.diag & 4)) static_for<0, NK>([&](auto sc) {
+          constexpr int st = decltype(sc)::value, cur = st & 1, nxt = cur ^ 1;
+          if constexpr (st + 1 < NK) {
+            const int t = toff_of(st + 1);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+              fb[nxt][n] = *reinterpret_cast<const u32x4_t*>(wlane + n * 16 * KP + (st + 1) * 32);
+#pragma unroll
+            for (int r = 0; r < RT; ++r) fa[nxt][r] = *reinterpret_cast<const u32x4_t*>(img + pix[r] + t);
+          }
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+              acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[cur][r]),
+                                                                  __builtin_bit_cast(bf16x8_t, fb[cur][n]), acc[r][n],
+                                                                  0, 0, 0);
+          // next step's reads ahead of this step's MFMAs (the scheduler would sink them to their use)
+          constexpr int nr = st + 1 < NK ? RT + NT : 0;
+          if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
+          __builtin_amdgcn_sched_group_barrier(0x8, RT * NT, 0);
+        });
+      } else {
       // software pipeline: fragments of step s+1 are read while step s's MFMAs run.
       // Past K the weight rows are zero (and the image slack is zero), so no masking.
       int cs = cs0, kw = kw0, toff = toff0;
@@ -292,6 +334,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
 #pragma unroll
         for (int n = 0; n < NT; ++n) bfr[n] = bn[n];
       }
+      }  // (runtime k walk)
       if (b == blockIdx.x && t0 == wm) stamp(3);
       // epilogue: lane holds rows (lane>>4)*4 + j of each tile (one 2x2 window when blocked),
       // column lane&15 of each n-tile
@@ -741,6 +784,28 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   };
   if (G.npf < 1 || G.npf > 4) return false;
   if constexpr (!POOLED) {
+    // ResNet-20's 3x3 convs: the closed-form k walk (CSC instances; DTFE_DIAG icr=64 -> runtime walk)
+    const int csc = a.KH == 3 && a.KW == 3 && G.npf <= 2 && !(diag & 64) &&
+                            (a.CS == 16 || a.CS == 32 || a.CS == 64) && G.K == 9 * a.CS &&
+                            G.KP == (9 * a.CS + 31) / 32 * 32 + 16
+                        ? a.CS : 0;
+    if (csc) {
+      auto pick = [&](auto cst) {
+        constexpr int C = decltype(cst)::value;
+        if (a.bns.stats) {
+          if (G.npf == 1) go(imgconv_persist_kernel<NT, RT, WM, WN, 1, false, true, C>);
+          else go(imgconv_persist_kernel<NT, RT, WM, WN, 2, false, true, C>);
+        } else {
+          if (G.npf == 1) go(imgconv_persist_kernel<NT, RT, WM, WN, 1, false, false, C>);
+          else go(imgconv_persist_kernel<NT, RT, WM, WN, 2, false, false, C>);
+        }
+      };
+      if (csc == 16) pick(std::integral_constant<int, 16>{});
+      else if (csc == 32) pick(std::integral_constant<int, 32>{});
+      else pick(std::integral_constant<int, 64>{});
+      if (sc_done) *sc_done = sc;
+      return true;
+    }
     if (a.bns.stats) {
       switch (G.npf) {
         case 1: go(imgconv_persist_kernel<NT, RT, WM, WN, 1, false, true>); break;
