@@ -453,7 +453,10 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
   // at least ~256 output pixels per workgroup: on small maps the per-workgroup partial slab (up to
   // 229 KB, written and re-read by wp_reduce) outweighs one image's work - ResNet-20 stage 3
   // (8x8, B=256): 64 workgroups 18.8 us vs 256: 26.3 (profiles/r5_resnet20_kernels.txt)
-  const int ipw = (256 + a.OH * a.OW - 1) / (a.OH * a.OW);
+  // (k-group configs: ~512 pixels - their per-image MFMA time is shorter; stage 2: 128 workgroups
+  // 14.2 us vs 256: 16.0)
+  const int px = KG > 1 ? 512 : 256;
+  const int ipw = (px + a.OH * a.OW - 1) / (a.OH * a.OW);
   int gcap = a.max_blocks > 0 && a.max_blocks < 256 ? a.max_blocks : 256;
   if ((a.B + ipw - 1) / ipw < gcap) gcap = (a.B + ipw - 1) / ipw;
   const int grid = a.B < gcap ? a.B : gcap;
