@@ -884,6 +884,11 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_don
   if (a.N <= 16 && !(diag_bits("icr") & 32))  // one n-tile: a second wave column would only compute padding
     return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s, sc_done) : launch_cfg<1, 2, 16, 1, false>(a, s, sc_done);
   if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<1, 2, 8, 2, false>(a, s, sc_done);
+  // small maps (<= 4 row tiles: ResNet-20 stage 3, 8x8): 4 x 2 waves of one tile x 2 n-tiles each -
+  // the 8 x 2 grid left half its waves idle and computed a padding tile in the rest (s3 conv 8.98 ->
+  // 8.27 us, step -6 us; DTFE_DIAG icr=128 -> the 8 x 2 grid, profiles/r5_resnet20_kernels.txt)
+  if (a.OH * a.OW <= 64 && !pooled && a.N <= 64 && !(diag_bits("icr") & 128))
+    return launch_cfg<2, 1, 4, 2, false>(a, s, sc_done);
   return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<2, 2, 8, 2, false>(a, s, sc_done);
 }
 
