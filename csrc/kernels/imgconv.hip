@@ -90,16 +90,43 @@ __device__ __forceinline__ void stage_image(bf16* img, int LH, int LW, int lo, i
 }
 
 // Few-channel LDS image [LH][LW][CS] (CS <= 4; source [SH][SW][CS] at offset lo), then `extra` zeros.
+// The source image is contiguous: its 16-B chunks are loaded up front (all in flight at once), the
+// LDS image is zeroed meanwhile, and the chunks' elements are scattered into the padded layout.  (The
+// per-element 2-byte global loads before - one dependent round trip per element and channel - held
+// ResNet-20's stem at ~25 us per launch, profiles/r5_resnet20_b256_kernels.txt.)  Contains a barrier.
 __device__ __forceinline__ void stage_image_small(bf16* img, int LH, int LW, int CS, int lo, int SH, int SW,
                                                   const bf16* src, int extra) {
-  const int npix = LH * LW;
-  const float inv_lw = 1.f / (float)LW;
-  for (int pix = threadIdx.x; pix < npix; pix += IC_THREADS) {
-    const int ly = fdiv(pix, LW, inv_lw), sy = ly - lo, sx = pix - ly * LW - lo;
-    const bool in = sy >= 0 && sy < SH && sx >= 0 && sx < SW;
-    for (int c = 0; c < CS; ++c) img[pix * CS + c] = in ? src[(sy * SW + sx) * CS + c] : (bf16)0;
+  const int npix = LH * LW, n = SH * SW * CS;
+  const bool vec = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+  const int nch = vec ? n >> 3 : 0;
+  constexpr int PF = 4;
+  const float inv_cs = 1.f / (float)CS, inv_sw = 1.f / (float)SW;
+  auto put = [&](int q, bf16 v) {
+    const int p = fdiv(q, CS, inv_cs), c = q - p * CS, sy = fdiv(p, SW, inv_sw), sx = p - sy * SW;
+    img[((sy + lo) * LW + sx + lo) * CS + c] = v;
+  };
+  for (int base = 0; base < nch || base == 0; base += PF * IC_THREADS) {
+    u32x4_t v[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int i = base + threadIdx.x + u * IC_THREADS;
+      if (i < nch) v[u] = *reinterpret_cast<const u32x4_t*>(src + (long)i * 8);
+    }
+    if (base == 0) {
+      for (int i = threadIdx.x; i < npix * CS + extra; i += IC_THREADS) img[i] = (bf16)0;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int i = base + threadIdx.x + u * IC_THREADS;
+      if (i < nch) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) put(i * 8 + e, (bf16)((v[u][e >> 1] >> (16 * (e & 1))) & 0xffffu));
+      }
+    }
+    if (nch == 0) break;
   }
-  for (int i = threadIdx.x; i < extra; i += IC_THREADS) img[npix * CS + i] = (bf16)0;
+  for (int q = nch * 8 + threadIdx.x; q < n; q += IC_THREADS) put(q, src[q]);  // tail / unaligned source
 }
 
 // epilogue: lane holds rows (lane>>4)*4 + j of each 16-row tile, column lane&15 of each n-tile
