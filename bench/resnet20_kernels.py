@@ -102,7 +102,8 @@ def main():
     prog.compute_grads()
     torch.cuda.synchronize()
     blocks = prog.L["blocks"]
-    rows = []
+    st = prog.L["stem"]
+    rows = [("stem fwd", lambda: st.fwd(prog.x)), ("stem wgrad", lambda: st.wgrad(prog.dc_stem, prog.x))]
     for tag, i in (("s1", 1), ("s2d", 3), ("s2", 4), ("s3", 7)):
         b = blocks[i]
         dout = prog.d_in[i + 1]

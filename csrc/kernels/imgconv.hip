@@ -264,12 +264,14 @@ __global__ __launch_bounds__(IC_THREADS) void imgconv_kernel(ImgConvArgs a) {
 // k = tap*CS + c (KH*KW*CS <= 32, one k-step), A fragment = 8 (tap, c) values
 // of one output pixel gathered from the LDS image with per-lane constant
 // offsets, weights [N][T*CS] held in registers.
-template <int NT, int RT>
+// STAGE: the (un-pooled, unmasked) output staged in LDS after the image and stored as 16-B rows
+template <int NT, int RT, bool STAGE = false>
 __global__ __launch_bounds__(IC_THREADS) void imgconv1_kernel(ImgConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 img[];
   const long b = blockIdx.x;
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;
   const int CS = a.CS;
+  bf16* sy = img + (LH * LW * CS + 7) / 8 * 8;
   stage_image_small(img, LH, LW, CS, a.pad, a.SH, a.SW, a.src + b * a.SH * a.SW * CS, 0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4;
@@ -318,7 +320,31 @@ __global__ __launch_bounds__(IC_THREADS) void imgconv1_kernel(ImgConvArgs a) {
       for (int n = 0; n < NT; ++n)
         acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[n], f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
-    imgconv_epilogue<NT, RT>(a, acc, t0, tiles, M, b, lane);
+    if constexpr (STAGE) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int tile = t0 + 4 * r;
+        if (tile >= tiles) break;
+        const int m0 = tile * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int col = n * 16 + (lane & 15);
+          if (col >= a.N) continue;
+          const float bias = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (m0 + j < M) sy[(m0 + j) * a.N + col] = f2bf(apply_act(acc[r][n][j] + bias, a.act));
+        }
+      }
+    } else {
+      imgconv_epilogue<NT, RT>(a, acc, t0, tiles, M, b, lane);
+    }
+  }
+  if constexpr (STAGE) {  // the image's output leaves as contiguous 16-B chunks
+    __syncthreads();
+    const long ob = b * (long)M * a.N;
+    for (int i = threadIdx.x; i < M * a.N / 8; i += IC_THREADS)
+      *reinterpret_cast<u32x4_t*>(a.y + ob + i * 8) = *reinterpret_cast<const u32x4_t*>(sy + i * 8);
   }
 }
 
@@ -332,6 +358,16 @@ bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride
 template <int NT>
 static void launch_nt(const ImgConvArgs& a, size_t lds, hipStream_t s) {
   constexpr int RT = 4;
+  if (a.CS <= 4 && !a.pool && !a.relu_mask && a.N % 8 == 0 && !(diag_bits("ic1") & 1)) {
+    // few-channel forward (ResNet-20 stem): output staged in LDS, 16-B stores
+    const size_t st = (lds + 15) / 16 * 16 + (size_t)a.OH * a.OW * a.N * sizeof(bf16);
+    if (st <= 150 * 1024) {
+      auto k = imgconv1_kernel<NT, RT, true>;
+      if (st > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)st);
+      hipLaunchKernelGGL(k, dim3(a.B), dim3(IC_THREADS), st, s, a);
+      return;
+    }
+  }
   auto k = a.CS <= 4 ? imgconv1_kernel<NT, RT> : imgconv_kernel<NT, RT>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, dim3(a.B), dim3(IC_THREADS), lds, s, a);
@@ -672,7 +708,10 @@ template <int NC>
 static void launch_wg1(const ImgWgradArgs& a0, hipStream_t s) {
   ImgWgradArgs a = a0;
   const size_t lds = wg_lds(a);
-  a.imgs_per_block = wg_ipb(a.B, 512, 2);
+  // one image per workgroup up to 512 images (ResNet-20 stem, B = 256: 16.4 us vs 18.5 at two,
+  // 27.0 at four - profiles/r5_resnet20_kernels.txt; DTFE_DIAG iw1=<n> forces n)
+  static const int ipb_diag = diag_bits("iw1");
+  a.imgs_per_block = ipb_diag > 0 ? ipb_diag : wg_ipb(a.B, 512, 1);
   const int groups = (a.B + a.imgs_per_block - 1) / a.imgs_per_block;
   auto k = imgwgrad1_kernel<NC>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
