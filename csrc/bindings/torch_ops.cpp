@@ -688,6 +688,28 @@ void softmax_xent(const Tensor& logits, const optional<Tensor>& labels_i, const 
   dtfe::launch_softmax_xent(a, cur_stream());
 }
 
+bool dense_head(const Tensor& feat, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
+                const optional<Tensor>& logits, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
+                const Tensor& dw, const optional<Tensor>& db, const Tensor& dfeat, double scale) {
+  check_cuda(feat, "feat");
+  TORCH_CHECK(feat.scalar_type() == at::kBFloat16 && feat.dim() == 2, "dense_head: bf16 feat [B][F]");
+  const int64_t B = feat.size(0), F = feat.size(1), NC = w.size(0);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == NC * F, "dense_head: fp32 w [NC][F]");
+  TORCH_CHECK(y.scalar_type() == at::kFloat && y.numel() == B * NC, "dense_head: fp32 one-hot y [B][NC]");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.numel() == NC * F, "dense_head: fp32 dw");
+  TORCH_CHECK(dfeat.scalar_type() == at::kBFloat16 && dfeat.numel() == B * F, "dense_head: bf16 dfeat");
+  TORCH_CHECK(!logits.has_value() || !logits->defined() || logits->numel() == B * NC, "dense_head: logits");
+  dtfe::DenseHeadArgs a{};
+  a.feat = reinterpret_cast<const dtfe::bf16*>(feat.data_ptr());
+  a.w = w.data_ptr<float>(); a.bias = ptr_or_null<float>(bias); a.y = y.data_ptr<float>();
+  a.logits = ptr_or_null<float>(logits); a.loss_sum = ptr_or_null<float>(loss_sum);
+  a.correct = ptr_or_null<int32_t>(correct);
+  a.dw = dw.data_ptr<float>(); a.db = ptr_or_null<float>(db);
+  a.dfeat = reinterpret_cast<dtfe::bf16*>(dfeat.data_ptr());
+  a.B = (int)B; a.F = (int)F; a.NC = (int)NC; a.scale = (float)scale;
+  return dtfe::launch_dense_head(a, cur_stream());
+}
+
 void gan_loss(const Tensor& d_real, const Tensor& d_fake, const Tensor& gen_loss, const Tensor& disc_loss,
               const Tensor& dz_real_disc, const Tensor& dz_fake_disc, const Tensor& dz_fake_gen, double clamp_eps) {
   check_cuda(d_real, "d_real");
@@ -1068,6 +1090,9 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor? bnb_gamma=None, Tensor? bnb_beta=None, Tensor(b!)? bnb_stats=None, int bnb_act=0,"
       " Tensor? acc_src=None, Tensor? acc_mask=None) -> ()");
   m.def(
+      "dense_head(Tensor feat, Tensor w, Tensor? bias, Tensor y, Tensor(a!)? logits, Tensor(b!)? loss_sum,"
+      " Tensor(c!)? correct, Tensor(d!) dw, Tensor(e!)? db, Tensor(f!) dfeat, float scale) -> bool");
+  m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
       " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1, Tensor? sc_src=None,"
@@ -1154,6 +1179,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("act_grad", &act_grad);
   m.impl("bias_act", &bias_act);
   m.impl("imgconv", &imgconv);
+  m.impl("dense_head", &dense_head);
   m.impl("imgwgrad", &imgwgrad);
   m.impl("lstm_cell_fwd", &lstm_cell_fwd);
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);

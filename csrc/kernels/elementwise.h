@@ -53,6 +53,19 @@ struct XentArgs {
 };
 void launch_softmax_xent(const XentArgs& a, hipStream_t s);
 
+// A small dense classifier head, forward AND backward, in ONE workgroup (ResNet-20: 64 features ->
+// 10 classes, B = 256): logits = feat W^T + b (fp32, also stored), softmax cross-entropy against
+// one-hot labels (loss sum += , hit count +=), dlogits = (p - y) scale, dW += dlogits^T feat,
+// db += column sums of dlogits, dfeat = bf16(dlogits W).  Replaces the cast / GEMM / softmax /
+// GEMM / column-sum / GEMM / cast chain (7 launches).  False when it does not fit one workgroup's LDS.
+struct DenseHeadArgs {
+  const bf16* feat; const float* w; const float* bias; const float* y;  // [B][F], [NC][F], [NC], [B][NC]
+  float* logits; float* loss_sum; int32_t* correct;
+  float* dw; float* db; bf16* dfeat;                                    // [NC][F] +=, [NC] +=, [B][F]
+  int B, F, NC; float scale;
+};
+bool launch_dense_head(const DenseHeadArgs& a, hipStream_t s);
+
 // GAN losses on the sigmoid outputs of D, with grads w.r.t. the
 // pre-sigmoid logits.  No epsilon inside log, as in the reference (GAN:142-143),
 // unless clamp_eps > 0.

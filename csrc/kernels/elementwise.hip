@@ -234,6 +234,94 @@ void launch_softmax_xent(const XentArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(softmax_xent_kernel, dim3((a.B + 3) / 4), dim3(256), 0, s, a);
 }
 
+__global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
+  extern __shared__ float hsm[];
+  const int B = a.B, F = a.F, NC = a.NC, FP = F + 1, tid = threadIdx.x;
+  float* sf = hsm;             // [B][F+1] features (fp32; padded rows: conflict-free column walks)
+  float* sw = sf + B * FP;     // [NC][F+1] weights
+  float* sd = sw + NC * FP;    // [B][NC] logits, then dlogits
+  float* red = sd + B * NC;    // [2][32] block-reduce scratch
+  for (int i = tid; i < B * F; i += 1024) {
+    const int b = i / F, f = i - b * F;
+    sf[b * FP + f] = bf2f(a.feat[i]);
+  }
+  for (int i = tid; i < NC * F; i += 1024) {
+    const int c = i / F, f = i - c * F;
+    sw[c * FP + f] = a.w[i];
+  }
+  __syncthreads();
+  for (int o = tid; o < B * NC; o += 1024) {
+    const int b = o / NC, c = o - b * NC;
+    float acc = a.bias ? a.bias[c] : 0.f;
+    for (int f = 0; f < F; ++f) acc = __builtin_fmaf(sf[b * FP + f], sw[c * FP + f], acc);
+    sd[o] = acc;
+    if (a.logits) a.logits[o] = acc;
+  }
+  __syncthreads();
+  // rows: softmax_xent_kernel's expressions (first-max argmax, lse, loss, (p - y) * scale)
+  float loss = 0.f, hits = 0.f;
+  for (int b = tid; b < B; b += 1024) {
+    float* l = sd + b * NC;
+    const float* y = a.y + (long)b * NC;
+    float mx = -INFINITY, ymax = -1.f;
+    int am = 0, yarg = 0;
+    for (int c = 0; c < NC; ++c) {
+      if (l[c] > mx) { mx = l[c]; am = c; }
+      if (y[c] > ymax) { ymax = y[c]; yarg = c; }
+    }
+    float se = 0.f;
+    for (int c = 0; c < NC; ++c) se += __expf(l[c] - mx);
+    const float lse = mx + __logf(se);
+    for (int c = 0; c < NC; ++c) {
+      const float p = __expf(l[c] - lse);
+      loss += y[c] * (lse - l[c]);
+      l[c] = (p - y[c]) * a.scale;
+    }
+    hits += am == yarg ? 1.f : 0.f;
+  }
+  loss = wave_sum(loss);
+  hits = wave_sum(hits);
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = loss;
+    red[32 + (tid >> 6)] = hits;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float tl = 0.f, th = 0.f;
+    for (int w = 0; w < 16; ++w) {
+      tl += red[w];
+      th += red[32 + w];
+    }
+    if (a.loss_sum) atomicAdd(a.loss_sum, tl);
+    if (a.correct) atomicAdd(a.correct, (int)th);
+  }
+  for (int o = tid; o < NC * F; o += 1024) {  // dW[c][f] += sum_b dlogits[b][c] feat[b][f]
+    const int c = o / F, f = o - c * F;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc = __builtin_fmaf(sd[b * NC + c], sf[b * FP + f], acc);
+    a.dw[o] += acc;
+  }
+  if (tid < NC && a.db) {
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += sd[b * NC + tid];
+    a.db[tid] += acc;
+  }
+  for (int i = tid; i < B * F; i += 1024) {  // dfeat = dlogits W
+    const int b = i / F, f = i - b * F;
+    float acc = 0.f;
+    for (int c = 0; c < NC; ++c) acc = __builtin_fmaf(sd[b * NC + c], sw[c * FP + f], acc);
+    a.dfeat[i] = f2bf(acc);
+  }
+}
+
+bool launch_dense_head(const DenseHeadArgs& a, hipStream_t s) {
+  const size_t lds = ((size_t)(a.B + a.NC) * (a.F + 1) + (size_t)a.B * a.NC + 64) * sizeof(float);
+  if (lds > 150 * 1024 || a.NC > 64 || !a.dw || !a.dfeat) return false;
+  (void)hipFuncSetAttribute((const void*)dense_head_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(dense_head_kernel, dim3(1), dim3(1024), lds, s, a);
+  return true;
+}
+
 __global__ __launch_bounds__(256) void gan_loss_kernel(GanLossArgs a) {
   __shared__ float sg[4], sd[4];
   float gl = 0.f, dl = 0.f;

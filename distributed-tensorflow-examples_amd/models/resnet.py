@@ -255,6 +255,8 @@ _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
 _FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "0") == "1"
 # ResNet-20: bn1's apply formed by conv2's whole-image kernels (BN.src_fold).  (A/B hook, not a knob.)
 _R20_SRC_FOLD = os.environ.get("DTFE_R20_SRC_FOLD", "1") == "1"
+# classifier head forward + backward in one launch (ops.dense_head).  (A/B hook, not a knob.)
+_HEAD_FUSE = os.environ.get("DTFE_HEAD_FUSE", "1") == "1"
 
 
 class BN:
@@ -795,8 +797,18 @@ class ResNetProgram(StepProgram):
         for b in L["blocks"]:
             h = b.fwd(h)
         ops.gap_fwd(h, self.feat16)
-        ops.cast_(self.feat16, self.feat)
         d, P, B = L["dense"], self.P, self.batch_size
+        # the classifier head's forward and backward as one launch where it fits one workgroup
+        # (ResNet-20: 7 launches fewer, profiles/r5_resnet20_kernels.txt); not in evaluation (it
+        # writes the dense gradients)
+        self.head_fused = False
+        if self.device.type == "cuda" and not BN.infer and _HEAD_FUSE:
+            self.head_fused = ops.dense_head(self.feat16, P.view(d.kernel), P.view(d.bias), self.y, self.logits,
+                                             self.loss, self.correct, P.gview(d.kernel), P.gview(d.bias),
+                                             self.dfeat16, 1.0 / B)
+            if self.head_fused:
+                return
+        ops.cast_(self.feat16, self.feat)
         ops.gemm(self.feat, P.view(d.kernel), self.logits, M=B, N=d.cout, K=d.cin, bias=P.view(d.bias))
         ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
                          correct=self.correct)
@@ -804,12 +816,15 @@ class ResNetProgram(StepProgram):
     def backward(self):
         L, P, B = self.L, self.P, self.batch_size
         d = L["dense"]
-        ops.gemm(self.dlogits, self.feat, P.gview(d.kernel), M=d.cout, N=d.cin, K=B, amode=ops.RMAJ, lda=d.cout,
-                 bmode=ops.RMAJ, ldb=d.cin)
-        ops.colsum(self.dlogits, B, d.cout, d.cout, P.gview(d.bias))
+        fused = getattr(self, "head_fused", False)
+        if not fused:
+            ops.gemm(self.dlogits, self.feat, P.gview(d.kernel), M=d.cout, N=d.cin, K=B, amode=ops.RMAJ,
+                     lda=d.cout, bmode=ops.RMAJ, ldb=d.cin)
+            ops.colsum(self.dlogits, B, d.cout, d.cout, P.gview(d.bias))
         self._ready(self.dense_lo)
-        ops.gemm(self.dlogits, P.view(d.kernel), self.dfeat, M=B, N=d.cin, K=d.cout, bmode=ops.RMAJ, ldb=d.cin)
-        ops.cast_(self.dfeat, self.dfeat16)
+        if not fused:
+            ops.gemm(self.dlogits, P.view(d.kernel), self.dfeat, M=B, N=d.cin, K=d.cout, bmode=ops.RMAJ, ldb=d.cin)
+            ops.cast_(self.dfeat, self.dfeat16)
         ops.gap_bwd(self.dfeat16, self.d_last)
         dout = self.d_last
         blocks = L["blocks"]

@@ -27,7 +27,7 @@ __all__ = [
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
-    "imgconv_shortcut",
+    "imgconv_shortcut", "dense_head",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -767,6 +767,26 @@ def mse_sigmoid(y, t, loss, dz):
     d = y - t
     loss.fill_((d * d).mean().item())
     dz.copy_(2 * d / n * y * (1 - y))
+
+
+def dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale) -> bool:
+    """A small dense classifier head, forward and backward in one launch (GPU: one workgroup; False when
+    it does not fit): logits = feat W^T + b, softmax cross-entropy against one-hot y (loss_sum +=,
+    correct +=), dlogits = (p - y) * scale, dw += dlogits^T feat, db += column sums, dfeat16 =
+    bf16(dlogits W).  The CPU path is the fp32 oracle."""
+    if feat16.is_cuda:
+        return bool(require().dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale))
+    f = feat16.float()
+    lg = f @ w.float().t() + (bias.float() if bias is not None else 0.0)
+    if logits is not None:
+        logits.copy_(lg)
+    dl = torch.empty_like(lg)
+    softmax_xent(lg, labels_oh=y, scale=scale, dlogits=dl, loss_sum=loss_sum, correct=correct)
+    dw += dl.t() @ f
+    if db is not None:
+        db += dl.sum(0)
+    dfeat16.copy_((dl @ w.float()).to(dfeat16.dtype))
+    return True
 
 
 def colsum(x, M, N, ld, db, scale=1.0):

@@ -1,0 +1,59 @@
+"""The one-launch dense classifier head (ops.dense_head) vs the unfused chain it replaces."""
+import pytest
+import torch
+
+import dtfe.ops as ops
+
+
+def _unfused(feat16, w, b, y, B, scale):
+    f = feat16.float()
+    lg = f @ w.t() + b
+    dl = torch.empty_like(lg)
+    loss = torch.zeros(1, device=f.device)
+    hits = torch.zeros(1, dtype=torch.int32, device=f.device)
+    ops.softmax_xent(lg, labels_oh=y, scale=scale, dlogits=dl, loss_sum=loss, correct=hits)
+    return lg, loss, hits, dl.t() @ f, dl.sum(0), (dl @ w).bfloat16()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,F,NC", [(256, 64, 10), (64, 64, 10), (300, 96, 16)])
+def test_dense_head_matches_unfused_gpu(B, F, NC):
+    torch.manual_seed(0)
+    d = "cuda"
+    feat16 = torch.randn(B, F, device=d).bfloat16()
+    w, b = torch.randn(NC, F, device=d) * 0.2, torch.randn(NC, device=d) * 0.1
+    y = torch.nn.functional.one_hot(torch.randint(0, NC, (B,), device=d), NC).float()
+    logits, loss, hits = torch.empty(B, NC, device=d), torch.zeros(1, device=d), torch.zeros(1, dtype=torch.int32, device=d)
+    dw, db, dfeat = torch.full((NC, F), 0.5, device=d), torch.full((NC,), 0.25, device=d), torch.empty(B, F, device=d).bfloat16()
+    assert ops.dense_head(feat16, w, b, y, logits, loss, hits, dw, db, dfeat, 1.0 / B)
+    lg_r, loss_r, hits_r, dw_r, db_r, df_r = _unfused(feat16, w, b, y, B, 1.0 / B)
+    assert torch.allclose(logits, lg_r, atol=1e-4, rtol=1e-5)
+    assert torch.allclose(loss, loss_r, rtol=1e-5)
+    assert int(hits) == int(hits_r)
+    assert torch.allclose(dw - 0.5, dw_r, atol=1e-5, rtol=1e-4)   # (+=)
+    assert torch.allclose(db - 0.25, db_r, atol=1e-6, rtol=1e-4)
+    assert (dfeat.float() - df_r.float()).abs().max() <= 2 * df_r.float().abs().max() * 2 ** -8 + 1e-6
+
+
+@pytest.mark.gpu
+def test_dense_head_declines_what_does_not_fit_gpu():
+    """Beyond one workgroup's LDS the launch is declined (False) and the caller runs the unfused chain."""
+    d = "cuda"
+    B, F, NC = 1024, 64, 10
+    z = torch.zeros(NC, F, device=d)
+    assert not ops.dense_head(torch.zeros(B, F, device=d).bfloat16(), z, None, torch.zeros(B, NC, device=d), None, None,
+                              None, z.clone(), None, torch.empty(B, F, device=d).bfloat16(), 1.0)
+
+
+def test_dense_head_cpu_oracle():
+    torch.manual_seed(1)
+    B, F, NC = 8, 16, 4
+    feat16 = torch.randn(B, F).bfloat16()
+    w, b = torch.randn(NC, F), torch.randn(NC)
+    y = torch.nn.functional.one_hot(torch.randint(0, NC, (B,)), NC).float()
+    logits, loss, hits = torch.empty(B, NC), torch.zeros(1), torch.zeros(1, dtype=torch.int32)
+    dw, db, dfeat = torch.zeros(NC, F), torch.zeros(NC), torch.empty(B, F).bfloat16()
+    assert ops.dense_head(feat16, w, b, y, logits, loss, hits, dw, db, dfeat, 1.0 / B)
+    lg_r, loss_r, hits_r, dw_r, db_r, df_r = _unfused(feat16, w, b, y, B, 1.0 / B)
+    assert torch.allclose(logits, lg_r) and torch.allclose(loss, loss_r) and int(hits) == int(hits_r)
+    assert torch.allclose(dw, dw_r) and torch.allclose(db, db_r) and torch.equal(dfeat, df_r)
