@@ -103,7 +103,11 @@ def main():
     torch.cuda.synchronize()
     blocks = prog.L["blocks"]
     st = prog.L["stem"]
-    rows = [("stem fwd", lambda: st.fwd(prog.x)), ("stem wgrad", lambda: st.wgrad(prog.dc_stem, prog.x))]
+    dn, P = prog.L["dense"], prog.P
+    rows = [("stem fwd", lambda: st.fwd(prog.x)), ("stem wgrad", lambda: st.wgrad(prog.dc_stem, prog.x)),
+            ("dense head", lambda: ops.dense_head(prog.feat16, P.view(dn.kernel), P.view(dn.bias), prog.y, prog.logits,
+                                                  prog.loss, prog.correct, P.gview(dn.kernel), P.gview(dn.bias),
+                                                  prog.dfeat16, 1.0 / a.batch_size))]
     for tag, i in (("s1", 1), ("s2d", 3), ("s2", 4), ("s3", 7)):
         b = blocks[i]
         dout = prog.d_in[i + 1]
