@@ -341,9 +341,10 @@ void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tens
               const optional<Tensor>& dy_argmax, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t SH,
               int64_t SW, int64_t CS, int64_t OH, int64_t OW, int64_t N, int64_t KH, int64_t KW, int64_t stride,
               int64_t pad, double scale, const optional<Tensor>& ws, int64_t max_blocks,
-              const optional<at::TensorList>& bn_src, double bn_eps) {
+              const optional<at::TensorList>& bn_src, double bn_eps, bool defer) {
   check_cuda(src, "src");
   dtfe::ImgWgradArgs a{};
+  a.defer_reduce = defer ? 1 : 0;
   a.bns = bn_src_of(bn_src, (long)B * SH * SW, CS, bn_eps, 0.0, false);
   a.max_blocks = (int)max_blocks;
   if (ws.has_value() && ws->defined()) {
@@ -1101,7 +1102,8 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"
-      " int max_blocks=0, Tensor[]? bn_src=None, float bn_eps=0.001) -> ()");
+      " int max_blocks=0, Tensor[]? bn_src=None, float bn_eps=0.001, bool defer=False) -> ()");
+  m.def("wgrad_flush() -> int");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
       " int OW, int KH, int KW, int stride, int pad, float scale, Tensor? xf=None) -> ()");
@@ -1185,4 +1187,10 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }
 
-TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) { m.impl("opt_pack", &opt_pack); }
+// every weight-gradient reduce queued with imgwgrad(defer=True), as one grouped launch on the current stream
+int64_t wgrad_flush() { return dtfe::flush_wgrad_reduces(cur_stream()); }
+
+TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) {
+  m.impl("opt_pack", &opt_pack);
+  m.impl("wgrad_flush", &wgrad_flush);
+}

@@ -83,7 +83,14 @@ struct ImgWgradArgs {
   int max_blocks;
   int diag;                 // ablation bits for kernel experiments (DTFE_DIAG iw=<bits>; 0 in production)
   BnSrc bns;                // BatchNorm + ReLU of src formed while staging it (persistent kernel; see ImgConvArgs)
+  // persistent kernel with a workspace: queue the partial-slab reduce instead of launching it;
+  // flush_wgrad_reduces launches every queued one together (the caller's workspaces must differ)
+  int defer_reduce;
 };
+
+// launch every deferred weight-gradient reduce (ImgWgradArgs::defer_reduce) as ONE grouped launch on s;
+// returns how many there were
+int flush_wgrad_reduces(hipStream_t s);
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
 // returns whether a.sc_src was added by the launch (false: the caller adds the shortcut gradient)

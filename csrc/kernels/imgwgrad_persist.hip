@@ -27,6 +27,7 @@
 
 #include <stdexcept>
 #include <type_traits>
+#include <vector>
 
 namespace dtfe {
 
@@ -331,11 +332,11 @@ __global__ __launch_bounds__(512) void imgwgrad_persist_kernel(ImgWgradArgs a, W
 // sum of the register-layout partial slabs over the nblk workgroups in a fixed order (16
 // strided subsets, then the subsets in order through LDS: bitwise reproducible, no atomics),
 // scattered once into dw[n][col] / db[n]
-__global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict__ ws, int nblk, int plen, int MT,
-                                                        int CTW, int KC, int N, float* dw, float* db, float scale) {
-  __shared__ f32x4_t red[16][17];
+__device__ __forceinline__ void wp_reduce_body(const float* __restrict__ ws, int nblk, int plen, int MT, int CTW,
+                                               int KC, int N, float* dw, float* db, float scale, int blk,
+                                               f32x4_t (&red)[16][17]) {
   const int c16 = threadIdx.x & 15, pg = threadIdx.x >> 4;
-  const int v = blockIdx.x * 16 + c16;  // f32x4 index within a slab
+  const int v = blk * 16 + c16;  // f32x4 index within a slab
   const int nv = (plen + 3) / 4;
   const int ntile = 8 * CTW * MT * 64;  // f32x4 of the tile region
   // live entries only: a tile past the weight's KC columns was never stored (small convs such as
@@ -376,6 +377,33 @@ __global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict_
     }
   }
 }
+
+__global__ __launch_bounds__(256) void wp_reduce_kernel(const float* __restrict__ ws, int nblk, int plen, int MT,
+                                                        int CTW, int KC, int N, float* dw, float* db, float scale) {
+  __shared__ f32x4_t red[16][17];
+  wp_reduce_body(ws, nblk, plen, MT, CTW, KC, N, dw, db, scale, blockIdx.x, red);
+}
+
+// Several deferred weight-gradient reduces (each its own workspace) in ONE launch: workgroup
+// ranges [first[i], first[i + 1]) reduce item i, exactly as its own wp_reduce_kernel launch would
+struct WpReduceItem {
+  const float* ws; float* dw; float* db; float scale; int nblk, plen, MT, CTW, KC, N;
+};
+constexpr int WP_GROUP_MAX = 32;
+struct WpReduceGroup {
+  WpReduceItem it[WP_GROUP_MAX];
+  int first[WP_GROUP_MAX + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void wp_reduce_group_kernel(WpReduceGroup g) {
+  __shared__ f32x4_t red[16][17];
+  int i = 0;
+  while (i + 1 < g.n && (int)blockIdx.x >= g.first[i + 1]) ++i;
+  const WpReduceItem& t = g.it[i];
+  wp_reduce_body(t.ws, t.nblk, t.plen, t.MT, t.CTW, t.KC, t.N, t.dw, t.db, t.scale, blockIdx.x - g.first[i], red);
+}
+
+thread_local std::vector<WpReduceItem> g_wp_deferred;  // queued by deferred launches, flushed together
 
 }  // namespace
 
@@ -468,8 +496,13 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, ad, G);
     if (a.ws) {
       const int plen = wp_part_len(MT, CTW, a.N), KC = a.KH * a.KW * a.CS;
-      hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW, KC,
-                         a.N, a.dw, a.db, a.scale);
+      if (a.defer_reduce) {
+        if (g_wp_deferred.size() >= (size_t)WP_GROUP_MAX) throw std::runtime_error("imgwgrad: too many deferred reduces");
+        g_wp_deferred.push_back(WpReduceItem{a.ws, a.dw, a.db, a.scale, grid, plen, MT, CTW, KC, a.N});
+      } else {
+        hipLaunchKernelGGL(wp_reduce_kernel, dim3((plen / 4 + 15) / 16), dim3(256), 0, s, a.ws, grid, plen, MT, CTW,
+                           KC, a.N, a.dw, a.db, a.scale);
+      }
     }
     return true;
   };
@@ -490,6 +523,21 @@ bool wp_launch(const ImgWgradArgs& a, const WPGeom& G, hipStream_t s) {
 }
 
 }  // namespace
+
+int flush_wgrad_reduces(hipStream_t s) {
+  const int n = (int)g_wp_deferred.size();
+  if (n == 0) return 0;
+  WpReduceGroup g{};
+  g.n = n;
+  g.first[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    g.it[i] = g_wp_deferred[i];
+    g.first[i + 1] = g.first[i] + (g.it[i].plen / 4 + 15) / 16;
+  }
+  g_wp_deferred.clear();
+  hipLaunchKernelGGL(wp_reduce_group_kernel, dim3(g.first[n]), dim3(256), 0, s, g);
+  return n;
+}
 
 long imgwgrad_ws_floats(int N, int KC) {
   const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 9;  // the largest wp_launch slabs below

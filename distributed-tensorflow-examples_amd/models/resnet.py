@@ -158,9 +158,14 @@ class Conv:
     def wgrad(self, dy, x, xf=None, after=None, bn_src=None):
         """``after``: the side stream's fork point (SideStream.fork_point, taken when dy was final).
         ``xf`` / ``bn_src``: as in fwd (x is then the BN's raw input)."""
+        dws = getattr(self, "defer_ws", None)
         if bn_src is not None:
             assert self.img_wgrad
-            ops.imgwgrad(x, self.gw, None, dy=dy, bn_src=bn_src.src_args(), bn_eps=BN_EPS, **self.ic)
+            ops.imgwgrad(x, self.gw, None, dy=dy, bn_src=bn_src.src_args(), bn_eps=BN_EPS, workspace=dws,
+                         defer=dws is not None, **self.ic)
+            return
+        if dws is not None and self.img_wgrad and xf is None:
+            ops.imgwgrad(x, self.gw, None, dy=dy, workspace=dws, defer=True, **self.ic)
             return
         side = getattr(self, "side", None)
         if side is not None and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0:
@@ -257,6 +262,8 @@ _FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "0") == "1"
 _R20_SRC_FOLD = os.environ.get("DTFE_R20_SRC_FOLD", "1") == "1"
 # classifier head forward + backward in one launch (ops.dense_head).  (A/B hook, not a knob.)
 _HEAD_FUSE = os.environ.get("DTFE_HEAD_FUSE", "1") == "1"
+# ResNet-20 weight-gradient reduces deferred to one grouped launch (ops.wgrad_flush).  (A/B hook.)
+_WGRAD_DEFER = os.environ.get("DTFE_WGRAD_DEFER", "1") == "1"
 
 
 class BN:
@@ -757,6 +764,12 @@ class ResNetProgram(StepProgram):
         self.block_lo = [min(P.offsets[n] for n in b.var_names) for b in L["blocks"]]
         self.dense_lo = min(P.offsets[d.kernel], P.offsets[d.bias])
         self.grad_ready = None  # optional backward-progress hook (BucketAllReduce.ready)
+        self._defer_convs = [c for b in L["blocks"] for c in (b.conv1, b.conv2, getattr(b, "conv3", None))
+                             if c is not None and c.img_wgrad and c.cin % 16 == 0 and B >= 128]
+        self._defer_ok = self.device.type == "cuda" and _WGRAD_DEFER and 0 < len(self._defer_convs) <= 32
+        self._defer_ws = {c: torch.empty(ops.wgrad_ws_floats(c.cout, c.k * c.k * c.cin), device=dev)
+                          for c in self._defer_convs} if self._defer_ok else {}
+        self.defer_wgrad = False
         # ResNet-50 (bottleneck) weight gradients on a side stream (SideStream; DTFE_WGRAD_STREAM=0 off)
         self.side = None
         if self.device.type == "cuda" and _WGRAD_STREAM and model.arch == "resnet50":
@@ -815,6 +828,12 @@ class ResNetProgram(StepProgram):
 
     def backward(self):
         L, P, B = self.L, self.P, self.batch_size
+        # one replica (no bucket hook waiting on per-block gradients): the whole-image weight gradients
+        # queue their partial-slab reduces (own workspaces) and ONE grouped launch sums them all at the
+        # end (profiles/r5_resnet20_kernels.txt)
+        self.defer_wgrad = self._defer_ok and self.grad_ready is None
+        for c in self._defer_convs:
+            c.defer_ws = self._defer_ws[c] if self.defer_wgrad else None
         d = L["dense"]
         fused = getattr(self, "head_fused", False)
         if not fused:
@@ -846,6 +865,8 @@ class ResNetProgram(StepProgram):
         else:
             L["stem_bn"].bwd(dout, st.y, self.dc_stem)
         st.wgrad(self.dc_stem, self.x)
+        if self.defer_wgrad:
+            ops.wgrad_flush()  # every block's deferred weight-gradient reduce in one launch
         if self.side is not None:
             self.side.join()
         self._ready(0)

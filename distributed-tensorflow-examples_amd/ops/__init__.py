@@ -27,7 +27,7 @@ __all__ = [
     "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
-    "imgconv_shortcut", "dense_head",
+    "imgconv_shortcut", "dense_head", "wgrad_flush",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -427,6 +427,14 @@ def imgconv_shortcut(w, dx, g, sc_stride, *, src, **geom) -> bool:
 _WG_WS = {}
 
 
+def wgrad_flush() -> int:
+    """Launch every weight-gradient reduce queued by imgwgrad(defer=True) as ONE grouped launch on the
+    current stream (each deferred call needs its own workspace).  CPU: nothing is ever deferred."""
+    if available():
+        return int(require().wgrad_flush())
+    return 0
+
+
 def wgrad_ws_floats(N: int, KC: int) -> int:
     """Floats of the weight-gradient partial-sum workspace (256 workgroup slabs) - mirrors
     imgwgrad_ws_floats in csrc/kernels/imgwgrad_persist.hip (the register-layout slabs of the
@@ -449,7 +457,7 @@ def wgrad_workspace(device, numel):
 
 
 def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, dy=None, dy_pooled=None,
-             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0, bn_src=None, bn_eps=1e-3):
+             dy_argmax=None, scale=1.0, workspace=None, max_blocks=0, bn_src=None, bn_eps=1e-3, defer=False):
     """dW[n][tap][c] += scale * sum_p dY[p][n] src[p*stride-pad+tap][c]; db += scale * sum dY.
     On the GPU the persistent kernel stores per-workgroup partials in `workspace`
     (default: a cached per-device buffer) and a second kernel sums them."""
@@ -457,7 +465,7 @@ def imgwgrad(src, dw, db, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, 
         if workspace is None and (CS % 16 == 0 or CS == 1):
             workspace = wgrad_workspace(dw.device, wgrad_ws_floats(N, KH * KW * CS))
         require().imgwgrad(src, dy, dy_pooled, dy_argmax, dw, db, B, SH, SW, CS, OH, OW, N, KH, KW, stride, pad,
-                           scale, workspace, max_blocks, bn_src=bn_src, bn_eps=bn_eps)
+                           scale, workspace, max_blocks, bn_src=bn_src, bn_eps=bn_eps, defer=defer)
         return
     if bn_src is not None:  # the source's BN + ReLU (nothing saved: the forward did)
         src = _bn_src_ref(src, bn_src, bn_eps, 0.99, False)

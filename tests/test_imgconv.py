@@ -336,3 +336,33 @@ def test_imgconv_bn_src_cpu_oracle():
     z = torch.zeros(C)
     ops.imgconv(w, y, src=x, bn_src=[stats, gamma, beta, z, z.clone(), z.clone(), z.clone() + 1], **kw)
     assert torch.equal(y, y_ref)
+
+
+@pytest.mark.gpu
+def test_imgwgrad_deferred_reduces_grouped_flush():
+    """Weight gradients whose partial-slab reduces are queued (defer=True, own workspaces) and summed
+    by ONE grouped launch (ops.wgrad_flush) == the per-call reduce, bit for bit."""
+    torch.manual_seed(16)
+    shapes = [(256, 32, 16, 16, 1), (256, 16, 32, 32, 1), (256, 8, 64, 64, 1), (256, 32, 16, 32, 2)]
+    ref, got, ws = [], [], []
+    args = []
+    for B, SH, CS, N, s in shapes:
+        OH = (SH + 2 - 3) // s + 1
+        x = torch.randn(B, SH, SH, CS).to(DEV, torch.bfloat16)
+        dy = torch.randn(B, OH, OH, N).to(DEV, torch.bfloat16)
+        kw = dict(B=B, SH=SH, SW=SH, CS=CS, OH=OH, OW=OH, N=N, KH=3, KW=3, stride=s, pad=1)
+        args.append((x, dy, kw))
+        r = torch.zeros(N, 3, 3, CS, device=DEV)
+        ops.imgwgrad(x, r, None, dy=dy, **kw)
+        ref.append(r)
+    for x, dy, kw in args:
+        g = torch.zeros(kw["N"], 3, 3, kw["CS"], device=DEV)
+        w = torch.empty(ops.wgrad_ws_floats(kw["N"], 9 * kw["CS"]), device=DEV)
+        ops.imgwgrad(x, g, None, dy=dy, workspace=w, defer=True, **kw)
+        got.append(g)
+        ws.append(w)
+    assert ops.wgrad_flush() == len(shapes)
+    torch.cuda.synchronize()
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    assert ops.wgrad_flush() == 0
