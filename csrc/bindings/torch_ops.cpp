@@ -107,6 +107,12 @@ void gemm(const Tensor& A, int64_t amode, int64_t lda, const Tensor& B, int64_t 
   } else if (tile >= 5) {
     TORCH_CHECK(dtfe::gemm_glds_eligible(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, a),
                 "gemm: shape / layout not eligible for the global_load_lds tile ", tile);
+    // the glds kernels load whole k-tiles of whole operand rows with no bounds checks: every element
+    // they may touch must lie inside the tensors
+    const int64_t b_rows = b_ones_row >= 0 ? b_ones_row : N;
+    const int64_t a_need = amode == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
+    const int64_t b_need = bmode == 0 ? (b_rows - 1) * ldb + K : (K - 1) * ldb + b_rows;
+    TORCH_CHECK(A.numel() >= a_need && B.numel() >= b_need, "gemm: operands smaller than M/N/K/ld imply");
   }
   dtfe::launch_gemm_dense(dt == 0 ? 0 : 1, (int)amode, (int)bmode, (int)tile, real_splits, a, cur_stream());
 }
@@ -1104,6 +1110,8 @@ TORCH_LIBRARY(dtfe, m) {
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"
       " int max_blocks=0, Tensor[]? bn_src=None, float bn_eps=0.001, bool defer=False) -> ()");
   m.def("wgrad_flush() -> int");
+  m.def("wgrad_pending() -> int");
+  m.def("wgrad_discard() -> int");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
       " int OW, int KH, int KW, int stride, int pad, float scale, Tensor? xf=None) -> ()");
@@ -1189,8 +1197,12 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
 
 // every weight-gradient reduce queued with imgwgrad(defer=True), as one grouped launch on the current stream
 int64_t wgrad_flush() { return dtfe::flush_wgrad_reduces(cur_stream()); }
+int64_t wgrad_pending() { return dtfe::pending_wgrad_reduces(); }
+int64_t wgrad_discard() { return dtfe::discard_wgrad_reduces(); }
 
 TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) {
   m.impl("opt_pack", &opt_pack);
   m.impl("wgrad_flush", &wgrad_flush);
+  m.impl("wgrad_pending", &wgrad_pending);
+  m.impl("wgrad_discard", &wgrad_discard);
 }

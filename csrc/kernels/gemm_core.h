@@ -208,6 +208,7 @@ struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, WARPS_M = WARPS_M_, WARPS_N = WARPS_N_, BK = BK_;
   static constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
   static constexpr int TM = WM / 16, TN = WN / 16;
+  static constexpr int WAVES = 4;  // waves holding the accumulators (dense_epilogue)
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 16x16");
 };
 

@@ -96,7 +96,8 @@ __device__ __forceinline__ void dense_epilogue(const DenseGemmArgs& a, char* sme
   constexpr int CLD = Cfg::BN + 4;  // f32 C tile row stride: 16*(odd) bytes, conflict-free quad writes
   float* Cs = reinterpret_cast<float*>(smem_raw);
   const int m_base = tm * Cfg::BM, n_base = tn * Cfg::BN;
-  if (NT == GEMM_THREADS || threadIdx.x < GEMM_THREADS) {  // (NT > 256: the first 4 waves hold the folded tile)
+  // (k-group kernels: NT > 256 threads, the first 4 waves hold the folded tile; the 8-wave fc tile: all 8)
+  if (NT == Cfg::WAVES * 64 || threadIdx.x < Cfg::WAVES * 64) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid / Cfg::WARPS_N, wn = wid % Cfg::WARPS_N;
 #pragma unroll
@@ -267,12 +268,12 @@ constexpr int GEMM_TILE_SMALL = 13;
 bool gemm_small_eligible(int dtype, const DenseGemmArgs& a);
 void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s);
 // Grouped launch (gemm_dense.hip): between begin and end, launch_gemm_dense calls with glds tile 12
-// and one split, and launch_head_wgrad calls, are recorded instead of launched (record functions
+// or 22 (both pieces the same tile) and one split, and launch_head_wgrad calls, are recorded instead of launched (record functions
 // return false when a call does not fit the group); end launches the recorded pieces as one grid
 // (head weight gradient, then a (KMAJ, RMAJ) and a (RMAJ, RMAJ) GEMM), or one by one otherwise.
 struct HeadWgradArgs;
 void glds_group_begin();
-bool glds_group_record(int amode, int bmode, const DenseGemmArgs& a);
+bool glds_group_record(int amode, int bmode, int tile, const DenseGemmArgs& a);
 bool glds_group_record_head(const HeadWgradArgs& a);
 void glds_group_end(hipStream_t s);
 // block tile of a tile id; returns the k-tile depth (split-K chunks are multiples of it)

@@ -1,6 +1,7 @@
 // Instantiation + dispatch of the dense GEMM kernel family.
 #include "gemm_dense.h"
 #include "gemm_glds.h"
+#include "gemm_fc.h"
 #include "head.h"
 
 #include <cstring>
@@ -19,12 +20,12 @@ static void launch_one(int splits, const DenseGemmArgs& args, hipStream_t s) {
 }
 
 int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
-  static const int dims[22][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
+  static const int dims[23][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64}, {16, 16},
                                   {64, 64}, {64, 64}, {64, 64}, {128, 64}, {128, 64},
-                                  {64, 64}, {64, 64}, {64, 64}};
-  if (tile < 0 || tile > 21) return -1;
+                                  {64, 64}, {64, 64}, {64, 64}, {FC_BM, FC_BN}};
+  if (tile < 0 || tile > FC_TILE) return -1;
   bm = dims[tile][0];
   bn = dims[tile][1];
   if (tile == GEMM_TILE_SMALL) return 16;
@@ -32,6 +33,7 @@ int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
 }
 
 bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGemmArgs& a) {
+  if (tile == FC_TILE) return gemm_fc_eligible(dtype, amode, bmode, a);
   int bm = 0, bn = 0;
   if (tile < 5 || gemm_dense_tile_dims(tile, bm, bn) < 0) return false;
   if (dtype != 0 || a.a_ones_row >= 0 || a.K % GL_BK || a.k_chunk % GL_BK || a.M % bm) return false;
@@ -112,7 +114,14 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
     launch_gemm_small(amode, bmode, args, stream);
     return;
   }
-  if (tile == 12 && splits == 1 && dtype == 0 && glds_group_record(amode, bmode, args)) return;  // inside a group
+  if ((tile == 12 || tile == FC_TILE) && splits == 1 && dtype == 0 && glds_group_record(amode, bmode, tile, args))
+    return;  // inside a group
+  if (tile == FC_TILE) {
+    if (!gemm_fc_eligible(dtype, amode, bmode, args))
+      throw std::runtime_error("gemm_dense: this GEMM is not eligible for tile 22 (gemm_fc_eligible)");
+    launch_gemm_fc(amode, bmode, splits, args, stream);
+    return;
+  }
   if (tile >= 5) {
     if (!gemm_glds_eligible(dtype, amode, bmode, tile, args))
       throw std::runtime_error("gemm_dense: this GEMM is not eligible for the global_load_lds tiles");
@@ -169,6 +178,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 1) void gemm_glds_group_kernel(GlGrou
 namespace {
 struct GlGroupRec {
   bool active = false;
+  int tile = 12;  // the pieces' tile: 12 (64x64 glds) or 22 (the 8-wave fc tile, gemm_fc.hip)
   int ng = 0, am[2] = {0, 0}, bm[2] = {0, 0};
   DenseGemmArgs g[2];
   bool has_h = false;
@@ -184,9 +194,11 @@ void glds_group_begin() {
   g_group.active = true;
 }
 
-bool glds_group_record(int amode, int bmode, const DenseGemmArgs& a) {
+bool glds_group_record(int amode, int bmode, int tile, const DenseGemmArgs& a) {
   if (!g_group.active || g_group.ng == 2) return false;
-  if (!gemm_glds_eligible(0, amode, bmode, 12, a)) return false;
+  if (g_group.ng == 1 && g_group.tile != tile) return false;
+  if (!gemm_glds_eligible(0, amode, bmode, tile, a)) return false;
+  g_group.tile = tile;
   g_group.am[g_group.ng] = amode;
   g_group.bm[g_group.ng] = bmode;
   g_group.g[g_group.ng++] = a;
@@ -207,7 +219,11 @@ void glds_group_end(hipStream_t s) {
   const bool fused = r.ng == 2 && r.am[0] == KMAJ && r.bm[0] == RMAJ && r.am[1] == RMAJ && r.bm[1] == RMAJ;
   if (!fused) {  // any other combination: the pieces as separate launches, in recording order
     if (r.has_h) launch_head_wgrad(r.h, s);
-    for (int i = 0; i < r.ng; ++i) launch_gemm_dense(0, r.am[i], r.bm[i], 12, 1, r.g[i], s);
+    for (int i = 0; i < r.ng; ++i) launch_gemm_dense(0, r.am[i], r.bm[i], r.tile, 1, r.g[i], s);
+    return;
+  }
+  if (r.tile == FC_TILE) {
+    launch_gemm_fc_group(r.g[0], r.g[1], r.has_h ? &r.h : nullptr, s);
     return;
   }
   GlGroupArgs ga;

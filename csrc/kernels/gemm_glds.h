@@ -27,8 +27,14 @@ namespace dtfe {
 constexpr int GL_BK = 64;
 typedef __attribute__((address_space(3))) void gl_lds_t;
 
+// The DMA is issued from inline asm (M0 = the wave-uniform LDS destination), as igemm.hip's
+// glds16_async: with the builtin, the compiler's LDS-DMA alias tracking puts an `s_waitcnt vmcnt(0)`
+// in front of every ds_read_b64_tr_b16 of an RMAJ operand (that builtin carries no memory operand),
+// draining the whole prefetch ring each k-tile.  gemm_glds_body orders every stage with its own
+// counted vmcnt wait + barrier; the compiler's own vmcnt waits stay conservative (these are older).
 __device__ __forceinline__ void gl_dma16(const void* g, bf16* lds_piece) {
-  __builtin_amdgcn_global_load_lds(g, (gl_lds_t*)lds_piece, 16, 0, 0);
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_piece);
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(l) : "memory");
 }
 
 // chunk XOR of k-row k in a [64 k][COLS] RMAJ image

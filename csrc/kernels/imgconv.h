@@ -91,6 +91,10 @@ struct ImgWgradArgs {
 // launch every deferred weight-gradient reduce (ImgWgradArgs::defer_reduce) as ONE grouped launch on s;
 // returns how many there were
 int flush_wgrad_reduces(hipStream_t s);
+// queued-but-unflushed deferred reduces of this thread, and dropping them (a backward that was
+// interrupted between an imgwgrad(defer=True) and its flush leaves them behind)
+int pending_wgrad_reduces();
+int discard_wgrad_reduces();
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
 // returns whether a.sc_src was added by the launch (false: the caller adds the shortcut gradient)

@@ -539,6 +539,14 @@ int flush_wgrad_reduces(hipStream_t s) {
   return n;
 }
 
+int pending_wgrad_reduces() { return (int)g_wp_deferred.size(); }
+
+int discard_wgrad_reduces() {
+  const int n = (int)g_wp_deferred.size();
+  g_wp_deferred.clear();
+  return n;
+}
+
 long imgwgrad_ws_floats(int N, int KC) {
   const int MT = N > 32 ? 4 : 2, CTW = N > 32 ? 7 : 9;  // the largest wp_launch slabs below
   const long plain = (long)N * KC + N;                   // imgconv1_copies / per-image kernels

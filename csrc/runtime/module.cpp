@@ -22,17 +22,36 @@ PYBIND11_MODULE(_dtfe_rt, m) {
       .def(py::init<>())
       .def("add", [](BundleWriter& w, const std::string& name, int dtype, const std::vector<int64_t>& shape,
                      const py::bytes& data) { w.add(name, dtype, shape, as_str(data)); })
+      .def("add_slice", [](BundleWriter& w, const std::string& name, int dtype, const std::vector<int64_t>& full_shape,
+                           const SliceSpec& slice, const py::bytes& data) {
+        w.add_slice(name, dtype, full_shape, slice, as_str(data));
+      })
       .def("finish", &BundleWriter::finish, py::call_guard<py::gil_scoped_release>());
+  m.def("encode_tensor_name_slice", [](const std::string& name, const SliceSpec& slice) {
+    return py::bytes(encode_tensor_name_slice(name, slice));
+  });
 
   m.def("read_bundle_index", [](const std::string& prefix) {
     std::map<std::string, BundleEntry> idx;
     std::string err;
     if (!bundle_read_index(prefix, idx, &err)) throw std::runtime_error("bundle index: " + err);
     py::dict out;
-    for (const auto& e : idx)
+    for (const auto& e : idx) {
+      if (!e.first.empty() && e.first[0] == '\0') continue;  // slice data entries (read_bundle_slice)
       out[py::str(e.first)] = py::make_tuple(e.second.dtype, e.second.shape, e.second.offset, e.second.size,
-                                             e.second.crc);
+                                             e.second.crc, e.second.slices);
+    }
     return out;
+  });
+  m.def("read_bundle_slice", [](const std::string& prefix, const std::string& name, const SliceSpec& slice) {
+    std::map<std::string, BundleEntry> idx;
+    std::string err;
+    if (!bundle_read_index(prefix, idx, &err)) throw std::runtime_error("bundle index: " + err);
+    auto it = idx.find(encode_tensor_name_slice(name, slice));
+    if (it == idx.end()) throw py::key_error(name + " (slice)");
+    std::string bytes;
+    if (!bundle_read_tensor(prefix, it->second, bytes, &err)) throw std::runtime_error("bundle slice: " + err);
+    return py::bytes(bytes);
   });
   m.def("read_bundle_tensor", [](const std::string& prefix, const std::string& name) {
     std::map<std::string, BundleEntry> idx;

@@ -291,14 +291,88 @@ static std::string encode_shape(const std::vector<int64_t>& shape) {
   return s.buf;
 }
 
+// TensorSliceProto { repeated Extent extent = 1; }  Extent { int64 start = 1; int64 length = 2 (oneof) }
+// A full extent is an empty Extent (TensorSlice::AsProto).
+static std::string encode_slice(const SliceSpec& sl) {
+  PbWriter w;
+  for (const auto& d : sl) {
+    PbWriter ext;
+    if (d.second != -1) {
+      if (d.first) ext.i64(1, d.first);
+      ext.i64(2, d.second);
+    }
+    w.bytes(1, ext.buf);
+  }
+  return w.buf;
+}
+
 std::string encode_bundle_entry(const BundleEntry& e) {
   PbWriter w;
   if (e.dtype) w.u64(1, (uint64_t)e.dtype);
   w.bytes(2, encode_shape(e.shape));
   if (e.offset) w.i64(4, e.offset);
   if (e.size) w.i64(5, e.size);
-  w.fixed32(6, crc_mask(e.crc));
+  if (e.size || e.slices.empty()) w.fixed32(6, crc_mask(e.crc));  // (a sliced tensor's entry holds no data)
+  for (const auto& sl : e.slices) w.bytes(7, encode_slice(sl));
   return w.buf;
+}
+
+// ---- OrderedCode (tensorflow/core/lib/strings/ordered_code.cc), the three writers the slice key uses
+static void oc_write_num_increasing(std::string& dest, uint64_t val) {
+  unsigned char buf[9];
+  int len = 0;
+  while (val > 0) {
+    ++len;
+    buf[9 - len] = (unsigned char)(val & 0xff);
+    val >>= 8;
+  }
+  buf[9 - len - 1] = (unsigned char)len;
+  ++len;
+  dest.append(reinterpret_cast<const char*>(buf + 9 - len), len);
+}
+
+static void oc_write_string(std::string& dest, const std::string& s) {
+  for (unsigned char c : s) {  // 0x00 -> 0x00 0xff, 0xff -> 0xff 0x00
+    if (c == 0x00) { dest.push_back('\x00'); dest.push_back('\xff'); }
+    else if (c == 0xff) { dest.push_back('\xff'); dest.push_back('\x00'); }
+    else dest.push_back((char)c);
+  }
+  dest.push_back('\x00');  // separator
+  dest.push_back('\x01');
+}
+
+static void oc_write_signed_num_increasing(std::string& dest, int64_t val) {
+  static const unsigned char kHeader[11][2] = {{0, 0},    {0x80, 0}, {0xc0, 0}, {0xe0, 0},    {0xf0, 0},   {0xf8, 0},
+                                               {0xfc, 0}, {0xfe, 0}, {0xff, 0}, {0xff, 0x80}, {0xff, 0xc0}};
+  const uint64_t x = val < 0 ? ~(uint64_t)val : (uint64_t)val;
+  if (x < 64) {
+    dest.push_back((char)(kHeader[1][0] ^ (unsigned char)val));
+    return;
+  }
+  // bits needed (incl. sign) -> encoded length: 7 payload bits per byte minus the header's
+  int bits = 64;
+  while (bits > 0 && !((x >> (bits - 1)) & 1)) --bits;
+  const int len = bits / 7 + 1;  // x >= 64: bits >= 7 -> len >= 2 (each byte carries 7 header/value bits)
+  unsigned char buf[10];
+  const unsigned char sign = val < 0 ? 0xff : 0x00;
+  buf[0] = buf[1] = sign;
+  for (int i = 0; i < 8; ++i) buf[2 + i] = (unsigned char)(((uint64_t)val) >> (8 * (7 - i)));
+  unsigned char* begin = buf + 10 - len;
+  begin[0] ^= kHeader[len][0];
+  begin[1] ^= kHeader[len][1];
+  dest.append(reinterpret_cast<const char*>(begin), len);
+}
+
+std::string encode_tensor_name_slice(const std::string& name, const SliceSpec& slice) {
+  std::string key;
+  oc_write_num_increasing(key, 0);
+  oc_write_string(key, name);
+  oc_write_num_increasing(key, (uint64_t)slice.size());
+  for (const auto& d : slice) {
+    oc_write_signed_num_increasing(key, d.second == -1 ? 0 : d.first);
+    oc_write_signed_num_increasing(key, d.second);
+  }
+  return key;
 }
 
 bool decode_bundle_entry(const std::string& s, BundleEntry& e) {
@@ -310,6 +384,23 @@ bool decode_bundle_entry(const std::string& s, BundleEntry& e) {
     else if (f.field == 4) e.offset = (int64_t)f.v;
     else if (f.field == 5) e.size = (int64_t)f.v;
     else if (f.field == 6) e.crc = crc_unmask((uint32_t)f.v);
+    else if (f.field == 7) {
+      std::vector<PbField> exts;
+      if (!pb_parse(f.s, exts)) return false;
+      SliceSpec sl;
+      for (const auto& x : exts) {
+        if (x.field != 1) continue;
+        std::vector<PbField> ee;
+        if (!pb_parse(x.s, ee)) return false;
+        int64_t start = 0, length = -1;
+        for (const auto& y : ee) {
+          if (y.field == 1) start = (int64_t)y.v;
+          else if (y.field == 2) length = (int64_t)y.v;
+        }
+        sl.emplace_back(start, length);
+      }
+      e.slices.push_back(sl);
+    }
     else if (f.field == 2) {
       std::vector<PbField> dims;
       if (!pb_parse(f.s, dims)) return false;
@@ -337,6 +428,29 @@ void BundleWriter::add(const std::string& name, int dtype, const std::vector<int
   items_[name] = {e, bytes};
 }
 
+void BundleWriter::add_slice(const std::string& name, int dtype, const std::vector<int64_t>& full_shape,
+                             const SliceSpec& slice, const std::string& bytes) {
+  if (name.empty()) throw std::runtime_error("bundle: empty tensor name is reserved for the header");
+  if (slice.size() != full_shape.size()) throw std::runtime_error("bundle: slice rank != tensor rank");
+  auto it = items_.find(name);
+  if (it == items_.end()) {
+    BundleEntry full;
+    full.dtype = dtype;
+    full.shape = full_shape;
+    it = items_.emplace(name, std::make_pair(full, std::string())).first;
+  } else if (it->second.first.dtype != dtype || it->second.first.shape != full_shape || !it->second.second.empty()) {
+    throw std::runtime_error("bundle: slice of " + name + " disagrees with its other slices");
+  }
+  it->second.first.slices.push_back(slice);
+  std::vector<int64_t> shape;
+  for (size_t d = 0; d < slice.size(); ++d) {
+    if (slice[d].second != -1 && (slice[d].first < 0 || slice[d].first + slice[d].second > full_shape[d]))
+      throw std::runtime_error("bundle: slice of " + name + " out of range");
+    shape.push_back(slice[d].second == -1 ? full_shape[d] : slice[d].second);
+  }
+  add(encode_tensor_name_slice(name, slice), dtype, shape, bytes);
+}
+
 static void write_file_atomic(const std::string& path, const std::string& contents) {
   const std::string tmp = path + ".tempstate";
   {
@@ -360,8 +474,10 @@ void BundleWriter::finish(const std::string& prefix) {
   kv.emplace_back("", hdr.buf);
   for (auto& it : items_) {  // std::map: sorted bytewise
     BundleEntry e = it.second.first;
-    e.offset = (int64_t)data.size();
-    data += it.second.second;
+    if (!it.second.second.empty() || e.slices.empty()) {
+      e.offset = (int64_t)data.size();
+      data += it.second.second;
+    }
     kv.emplace_back(it.first, encode_bundle_entry(e));
   }
   write_file_atomic(prefix + ".data-00000-of-00001", data);

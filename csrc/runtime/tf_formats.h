@@ -69,16 +69,31 @@ bool sstable_parse(const std::string& file, std::vector<std::pair<std::string, s
 // TF DataType enum values for the dtypes we save
 enum TfDtype : int { DT_FLOAT = 1, DT_DOUBLE = 2, DT_INT32 = 3, DT_UINT8 = 4, DT_INT64 = 9, DT_BFLOAT16 = 14 };
 
+// one TensorSliceProto: per dimension (start, length); length -1 = the full extent
+typedef std::vector<std::pair<int64_t, int64_t>> SliceSpec;
+
 struct BundleEntry {
   int dtype = 0;
   std::vector<int64_t> shape;
   int64_t offset = 0, size = 0;
   uint32_t crc = 0;  // unmasked crc32c of the bytes
+  // a partitioned variable's full-tensor entry (BundleEntryProto.slices): metadata only, the data of
+  // each slice lives under the key encode_tensor_name_slice(name, slice)
+  std::vector<SliceSpec> slices;
 };
+
+// TF's checkpoint::EncodeTensorNameSlice (tensorflow/core/util/saved_tensor_slice_util.cc): the
+// OrderedCode key of one slice of a partitioned tensor - 0, the name, the rank, then (start, length)
+// per dimension as signed increasing numbers (a full extent: start 0, length -1)
+std::string encode_tensor_name_slice(const std::string& name, const SliceSpec& slice);
 
 class BundleWriter {
  public:
   void add(const std::string& name, int dtype, const std::vector<int64_t>& shape, const std::string& bytes);
+  // one slice of a partitioned tensor (BundleWriter::AddSlice): records the slice in the full
+  // tensor's entry and stores the slice's data under its encoded key
+  void add_slice(const std::string& name, int dtype, const std::vector<int64_t>& full_shape, const SliceSpec& slice,
+                 const std::string& bytes);
   // writes <prefix>.index and <prefix>.data-00000-of-00001 (atomically via .tempstate files)
   void finish(const std::string& prefix);
 

@@ -40,12 +40,33 @@ def _tensor_bytes(t: torch.Tensor) -> bytes:
     return t.numpy().tobytes()
 
 
+class Sliced:
+    """A partitioned variable's full value (TF layout) and its partitions along ``axis``:
+    ``bounds`` = [(start, length), ...].  ``save_bundle`` writes it the way tf.train.Saver writes a
+    PartitionedVariable: one full-tensor entry listing the slices (BundleEntryProto.slices), each
+    slice's data under its ``EncodeTensorNameSlice`` key; ``load_bundle`` reassembles the full tensor."""
+
+    def __init__(self, full: torch.Tensor, axis: int, bounds):
+        self.full, self.axis, self.bounds = full, axis, [(int(a), int(b)) for a, b in bounds]
+
+    def slice_specs(self):
+        for start, length in self.bounds:
+            yield [(start, length) if d == self.axis else (0, -1) for d in range(self.full.dim())], \
+                self.full.narrow(self.axis, start, length)
+
+
 def save_bundle(prefix: str, tensors: dict, write_meta: bool = True):
     """Write ``prefix.index`` + ``prefix.data-00000-of-00001`` (+ ``prefix.meta``)."""
     rt = native.rt()
     w = rt.BundleWriter()
     meta_vars = []
     for name, t in tensors.items():
+        if isinstance(t, Sliced):
+            dt = _TORCH_TO_TF[t.full.dtype]
+            for spec, part in t.slice_specs():
+                w.add_slice(name, dt, list(t.full.shape), spec, _tensor_bytes(part))
+            meta_vars.append((name, dt, list(t.full.shape)))
+            continue
         if not isinstance(t, torch.Tensor):
             t = torch.as_tensor(t)
         dt = _TORCH_TO_TF[t.dtype]
@@ -63,14 +84,26 @@ def load_bundle(prefix: str) -> dict:
     """Read every tensor of a bundle into CPU tensors (crc32c verified)."""
     rt = native.rt()
     out = {}
-    for name, (dt, shape, _off, _size, _crc) in rt.read_bundle_index(prefix).items():
-        raw = rt.read_bundle_tensor(prefix, name)
+
+    def decode(raw, dt, shape):
         if dt == DT_BFLOAT16:
-            arr = np.frombuffer(raw, dtype=np.int16).copy()
-            out[name] = torch.from_numpy(arr).view(torch.bfloat16).reshape(shape)
-        else:
-            arr = np.frombuffer(raw, dtype=_TF_TO_NP[dt]).copy()
-            out[name] = torch.from_numpy(arr).reshape(shape)
+            return torch.from_numpy(np.frombuffer(raw, dtype=np.int16).copy()).view(torch.bfloat16).reshape(shape)
+        return torch.from_numpy(np.frombuffer(raw, dtype=_TF_TO_NP[dt]).copy()).reshape(shape)
+
+    for name, (dt, shape, _off, _size, _crc, slices) in rt.read_bundle_index(prefix).items():
+        if not slices:
+            out[name] = decode(rt.read_bundle_tensor(prefix, name), dt, shape)
+            continue
+        # a partitioned variable: every slice read from its own key and placed into the full tensor
+        full = None
+        for spec in slices:
+            sshape = [shape[d] if ln == -1 else ln for d, (_st, ln) in enumerate(spec)]
+            part = decode(rt.read_bundle_slice(prefix, name, spec), dt, sshape)
+            if full is None:
+                full = torch.zeros(shape, dtype=part.dtype)
+            idx = tuple(slice(None) if ln == -1 else slice(st, st + ln) for st, ln in spec)
+            full[idx] = part
+        out[name] = full
     return out
 
 

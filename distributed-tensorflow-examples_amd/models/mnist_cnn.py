@@ -214,11 +214,19 @@ class MnistCnnTrainer:
         # fc1 GEMMs on the global_load_lds tiles (gemm_glds.h) where the shapes allow: the forward
         # (one 64x64 tile per CU, 49 k-tiles) with two 4-wave k-groups per workgroup, 3 stages each
         # (tile 19: 15.6 us vs 19.9 for one group, torch.mm 21.3 - profiles/r4_fc1_kgroups.txt);
-        # data / weight gradient take the 2-stage variant (784 / 800 tiles, several per CU)
+        # data / weight gradient: the 8-wave 256x128 tile (gemm_fc.hip: 100 tiles each, 154 MB of
+        # L2 -> LDS traffic for the pair instead of 410 MB on 64x64 tiles, profiles/r6_fc1_tile22.txt),
+        # else the 64x64 2-stage tile
         K1 = 7 * 7 * C2
         self.t_fwd = self._glds_tile(self.p2, P.w16[n["wd1"]], B, FC, K1, K1, K1, 19)
-        self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
-        self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
+        self.t_dgrad = (self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, ops.FC_TILE, bmode=ops.RMAJ)
+                        or self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12))
+        self.t_wgrad = (self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, ops.FC_TILE, b_ones_row=K1,
+                                        bmode=ops.RMAJ)
+                        or self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1))
+        if (self.t_dgrad == ops.FC_TILE) != (self.t_wgrad == ops.FC_TILE):  # one grouped launch: same tile
+            self.t_dgrad = self._glds_tile(self.dzf, P.w16[n["wd1"]], B, K1, FC, FC, K1, 12)
+            self.t_wgrad = self._glds_tile(self.dzf, self.p2, FC, K1 + 1, B, FC, K1, 12, b_ones_row=K1)
         # head weight gradient: the dedicated whole-batch kernel up to B = 1024, above that a split-K
         # GEMM with the deterministic last-arriver combine (own workspace: it runs in the group)
         self.head_gemm = batch > 1024
@@ -245,8 +253,9 @@ class MnistCnnTrainer:
         # inside the Adam launch measured 0.2033-0.2042 vs 0.1989-0.1997 ms/step,
         # profiles/r4_cnn_step_b1024.txt)
 
-    def _glds_tile(self, A, Bm, M, N, K, lda, ldb, tile, b_ones_row=-1):
-        if self.device.type == "cuda" and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row):
+    def _glds_tile(self, A, Bm, M, N, K, lda, ldb, tile, b_ones_row=-1, bmode=ops.KMAJ):
+        if self.device.type == "cuda" and ops.glds_ok(A, Bm, M, N, K, tile, lda, ldb, b_ones_row=b_ones_row,
+                                                      bmode=bmode):
             return tile
         return None
 

@@ -468,7 +468,8 @@ class BasicBlock:
         self.x = x
         # bn1's apply formed by conv2's whole-image kernels while they stage its input (forward and
         # weight gradient): no bn_apply pass (profiles/r5_resnet20_kernels.txt)
-        self.src_fold = (_R20_SRC_FOLD and not BN.infer and x.is_cuda and self.conv2.img_fwd
+        # (instance flag: ResNetProgram.evaluate sets it on every BN; evaluation takes the plain path)
+        self.src_fold = (_R20_SRC_FOLD and not self.bn1.infer and x.is_cuda and self.conv2.img_fwd
                          and self.conv2.img_wgrad and self.conv2.B >= 128)
         if self.src_fold:
             r1 = self.bn1.src_fold(self.conv1.fwd(x, self.bn1.stats))
@@ -764,6 +765,7 @@ class ResNetProgram(StepProgram):
         self.block_lo = [min(P.offsets[n] for n in b.var_names) for b in L["blocks"]]
         self.dense_lo = min(P.offsets[d.kernel], P.offsets[d.bias])
         self.grad_ready = None  # optional backward-progress hook (BucketAllReduce.ready)
+        self.training = True    # False inside evaluate(): no fused head (it writes gradients), no BN folds
         self._defer_convs = [c for b in L["blocks"] for c in (b.conv1, b.conv2, getattr(b, "conv3", None))
                              if c is not None and c.img_wgrad and c.cin % 16 == 0 and B >= 128]
         self._defer_ok = self.device.type == "cuda" and _WGRAD_DEFER and 0 < len(self._defer_convs) <= 32
@@ -783,12 +785,28 @@ class ResNetProgram(StepProgram):
         """Backward progress: every gradient at flat offset >= lo has been launched.  The bucket's
         weight gradients may still run on the wgrad side stream: the all-reduce fork waits on an
         event recorded there, the compute stream does not (no per-block join serialising the
-        data-gradient chain behind the weight gradients)."""
+        data-gradient chain behind the weight gradients).
+
+        Deferred weight-gradient reduces: the ones queued so far are flushed as ONE grouped launch
+        just before the hook launches a bucket (only when a bucket boundary is crossed, so the
+        multi-rank schedules keep most of the 18 -> 1 saving; profiles/r6_resnet20_bucket_flush.txt)."""
         if self.grad_ready is not None:
+            if self.defer_wgrad and self._bucket_completes(lo):
+                ops.wgrad_flush()
             after = None
             if self.side is not None and self.side.pending:
                 after = [self.side.mark()]
             self.grad_ready(lo, after)
+
+    def _bucket_completes(self, lo):
+        """Whether the progress hook launches a bucket at ``lo`` (some bucket starts at or above lo
+        and was not reached before).  Hooks without a bucket list: every call counts."""
+        bks = getattr(getattr(self.grad_ready, "__self__", None), "buckets", None)
+        if bks is None:
+            return True
+        fire = any(self._ready_lo > b[0] >= lo for b in bks)
+        self._ready_lo = min(self._ready_lo, lo)
+        return fire
 
     def load_batch(self, batch):
         x, y = batch
@@ -813,9 +831,9 @@ class ResNetProgram(StepProgram):
         d, P, B = L["dense"], self.P, self.batch_size
         # the classifier head's forward and backward as one launch where it fits one workgroup
         # (ResNet-20: 7 launches fewer, profiles/r5_resnet20_kernels.txt); not in evaluation (it
-        # writes the dense gradients)
+        # writes the dense gradients: only while training, never from evaluate())
         self.head_fused = False
-        if self.device.type == "cuda" and not BN.infer and _HEAD_FUSE:
+        if self.device.type == "cuda" and self.training and _HEAD_FUSE:
             self.head_fused = ops.dense_head(self.feat16, P.view(d.kernel), P.view(d.bias), self.y, self.logits,
                                              self.loss, self.correct, P.gview(d.kernel), P.gview(d.bias),
                                              self.dfeat16, 1.0 / B)
@@ -827,11 +845,30 @@ class ResNetProgram(StepProgram):
                          correct=self.correct)
 
     def backward(self):
+        # the deferred weight-gradient queue (a thread-local list of device pointers in the kernel
+        # library) must be empty here: a stale entry would reduce into freed or foreign buffers
+        if self._defer_ok:
+            stale = ops.wgrad_pending()
+            if stale:
+                ops.wgrad_discard()
+                raise RuntimeError(f"ResNetProgram.backward: {stale} deferred weight-gradient reduce(s) left "
+                                   "queued by an earlier interrupted backward or a stray imgwgrad(defer=True); "
+                                   "discarded - rerun the step")
+        try:
+            self._backward()
+        except BaseException:
+            if self._defer_ok:
+                ops.wgrad_discard()  # nothing queued by this backward may leak into the next one
+            raise
+
+    def _backward(self):
         L, P, B = self.L, self.P, self.batch_size
-        # one replica (no bucket hook waiting on per-block gradients): the whole-image weight gradients
-        # queue their partial-slab reduces (own workspaces) and ONE grouped launch sums them all at the
-        # end (profiles/r5_resnet20_kernels.txt)
-        self.defer_wgrad = self._defer_ok and self.grad_ready is None
+        # the whole-image weight gradients queue their partial-slab reduces (own workspaces); ONE
+        # grouped launch sums them: at the end of the backward with one replica
+        # (profiles/r5_resnet20_kernels.txt), before each bucket's launch when a progress hook (all-reduce
+        # / ps push) waits on per-block gradients (_ready)
+        self.defer_wgrad = self._defer_ok
+        self._ready_lo = 1 << 62
         for c in self._defer_convs:
             c.defer_ws = self._defer_ws[c] if self.defer_wgrad else None
         d = L["dense"]
@@ -866,7 +903,7 @@ class ResNetProgram(StepProgram):
             L["stem_bn"].bwd(dout, st.y, self.dc_stem)
         st.wgrad(self.dc_stem, self.x)
         if self.defer_wgrad:
-            ops.wgrad_flush()  # every block's deferred weight-gradient reduce in one launch
+            ops.wgrad_flush()  # every (remaining) deferred weight-gradient reduce in one launch
         if self.side is not None:
             self.side.join()
         self._ready(0)
@@ -902,6 +939,7 @@ class ResNetProgram(StepProgram):
         bns = self.batchnorms()
         for bn in bns:
             bn.infer = True
+        self.training = False
         hits = 0
         try:
             for lo in range(0, n, B):
@@ -911,6 +949,7 @@ class ResNetProgram(StepProgram):
                 self.forward()
                 hits += int((self.logits[:m].argmax(1) == self.y[:m].argmax(1)).sum().item())
         finally:
+            self.training = True
             for bn in bns:
                 bn.infer = False
             for t in self.step_accumulators()[1:]:

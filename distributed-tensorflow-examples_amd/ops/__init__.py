@@ -24,10 +24,10 @@ __all__ = [
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
-    "TILE_DIMS", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
+    "TILE_DIMS", "FC_TILE", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
-    "imgconv_shortcut", "dense_head", "wgrad_flush",
+    "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -38,8 +38,10 @@ TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)
              13: (16, 16),   # exact-fp32 small-layer kernel (gemm_small.hip): no split-K, in-WG K split
              14: (64, 64), 15: (64, 64), 16: (64, 64),  # 4 / 6 / 8 stages (long-K grids, ~1 WG per CU)
              17: (128, 64), 18: (128, 64),              # 4 / 6 stages
-             19: (64, 64), 20: (64, 64), 21: (64, 64)}  # 2 / 4 / 2 in-workgroup k-groups (3 / 2 / 4 stages)
-GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21)
+             19: (64, 64), 20: (64, 64), 21: (64, 64),  # 2 / 4 / 2 in-workgroup k-groups (3 / 2 / 4 stages)
+             22: (256, 128)}  # 8-wave fc tile (gemm_fc.hip): M % 256, N any (clamped last tile), 3 stages
+FC_TILE = 22
+GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22)
 TILE_SMALL = 13
 _ONES = {}
 
@@ -53,13 +55,18 @@ def ones_page(device):
     return t
 
 
-def glds_ok(A, B, M, N, K, tile, lda, ldb, b_ones_row=-1, a_ones_row=-1):
+def glds_ok(A, B, M, N, K, tile, lda, ldb, b_ones_row=-1, a_ones_row=-1, bmode=KMAJ):
     """Host mirror of gemm_glds_eligible: can the global_load_lds tile `tile` run this GEMM?"""
     bm, bn = TILE_DIMS[tile]
     if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16 or a_ones_row >= 0 or K % 64 or M % bm:
         return False
     if lda % 8 or ldb % 8 or A.data_ptr() % 16 or B.data_ptr() % 16:
         return False
+    if tile == FC_TILE:  # mirror of gemm_fc_eligible (csrc/kernels/gemm_fc.hip)
+        valid = b_ones_row if b_ones_row >= 0 else N
+        if b_ones_row >= 0 and (b_ones_row != N - 1 or b_ones_row % 8):
+            return False
+        return valid >= 8 and valid % 8 == 0 and (bmode == RMAJ or (N % bn == 0 and b_ones_row < 0))
     if b_ones_row >= 0:
         return b_ones_row == N - 1 and b_ones_row % bn == 0
     return N % bn == 0
@@ -432,6 +439,20 @@ def wgrad_flush() -> int:
     current stream (each deferred call needs its own workspace).  CPU: nothing is ever deferred."""
     if available():
         return int(require().wgrad_flush())
+    return 0
+
+
+def wgrad_pending() -> int:
+    """Deferred weight-gradient reduces queued on this thread and not yet flushed."""
+    if available():
+        return int(require().wgrad_pending())
+    return 0
+
+
+def wgrad_discard() -> int:
+    """Drop this thread's queued deferred reduces (after an interrupted backward); returns how many."""
+    if available():
+        return int(require().wgrad_discard())
     return 0
 
 

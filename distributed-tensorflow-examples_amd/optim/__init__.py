@@ -85,7 +85,23 @@ class FlatParams:
         for s in self.specs:
             if s.name == name:
                 return s
+        a = getattr(self, "aliases", {}).get(name)
+        if a is not None:
+            return a
         raise KeyError(name)
+
+    def add_alias(self, spec: VarSpec, parent: str, elem_off: int):
+        """Register ``spec`` as a view of elements [elem_off, elem_off + numel) of variable ``parent``
+        (a partition of it, parallel/partition.py): ``offsets`` / ``view`` / ``gview`` / ``w16`` then
+        address it like a variable; layout, initialisation and copies stay the parent's."""
+        ps = self.spec(parent)
+        assert spec.transpose is None and elem_off + spec.numel <= ps.numel, spec.name
+        if not hasattr(self, "aliases"):
+            self.aliases = {}
+        self.aliases[spec.name] = spec
+        self.offsets[spec.name] = self.offsets[parent] + elem_off
+        if parent in self.w16:
+            self.w16[spec.name] = self.w16[parent].view(-1)[elem_off:elem_off + spec.numel].view(spec.shape)
 
     def range_of(self, names):
         """[lo, hi) element range covering the given variables (must be contiguous)."""

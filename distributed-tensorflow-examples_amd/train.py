@@ -43,6 +43,7 @@ from .parallel.cluster import ClusterSpec, Server
 from .parallel.health import CommWatchdog, Heartbeat, Watchdog
 from .utils.faults import FaultInjector
 from .utils.timers import PhaseTimer
+from .parallel.partition import PartitionedModel
 from .parallel.placement import round_robin
 from .parallel import ps_native
 from .parallel.ps import PSClient, PSServer, Shard, wait_for_init
@@ -193,7 +194,15 @@ def _shard_layout(model, num_ps):
     return placement, shard_specs
 
 
+def ps_view(flags, model):
+    """The model as the ps tasks see it: with --ps_partition_mb, large variables split into
+    partitions that are placed (and checkpointed) like TF's PartitionedVariable parts."""
+    mb = getattr(flags, "ps_partition_mb", 0.0) or 0.0
+    return PartitionedModel(model, int(mb * (1 << 20))) if mb > 0 else model
+
+
 def run_ps(flags, model, server, device, log):
+    model = ps_view(flags, model)
     placement, shard_specs = _shard_layout(model, len(server.cluster.ps))
     k = server.task_index
     gs_here = placement[model.gs_name] == k
@@ -241,7 +250,8 @@ def _native_ps(flags, server, device) -> bool:
 
 
 def ps_state(client, model, shard_specs, placement):
-    """Gather every shard's params + slots from the ps tasks into one TF-named dict."""
+    """Gather every shard's params + slots from the ps tasks into one TF-named dict (partitioned
+    variables: one ``ckpt.Sliced`` per variable / slot)."""
     states, gs = client.fetch_state()
     out = {}
     for k, flat in states.items():
@@ -249,12 +259,16 @@ def ps_state(client, model, shard_specs, placement):
         mirror.load_state_payload(flat)
         out.update(tensors_from_flat(model, mirror.P, mirror.opts, gs))
     out[model.gs_name] = torch.tensor(int(gs), dtype=torch.int32)
+    if isinstance(model, PartitionedModel):
+        out = model.merge_tf(out)
     return out, gs
 
 
 def ps_restore(client, model, shard_specs, tensors):
     states = {}
     gs = int(tensors.get(model.gs_name, torch.tensor(0)).item())
+    if isinstance(model, PartitionedModel):
+        tensors = model.split_tf(tensors)
     for k, specs in shard_specs.items():
         if not specs:
             continue
@@ -266,9 +280,12 @@ def ps_restore(client, model, shard_specs, tensors):
 
 def run_worker_ps(flags, model, server, device, log):
     cl = server.cluster
+    full_model, model = model, ps_view(flags, model)
     placement, shard_specs = _shard_layout(model, len(cl.ps))
     gs_rank = cl.rank_of("ps", placement[model.gs_name])
-    prog = model.program(device, flags.batch_size, seed=flags.seed)
+    prog = full_model.program(device, flags.batch_size, seed=flags.seed)
+    if isinstance(model, PartitionedModel):
+        model.add_aliases(prog.P)  # the parts as views of the worker's full variables
     comm = "cpu" if server.backend == "gloo" else device
     client = PSClient(server, prog.P, placement, shard_specs, gs_rank, model.opt_groups, comm_device=comm)
     is_chief = server.task_index == 0

@@ -92,6 +92,10 @@ def build_parser(model_defaults: dict | None = None, prog=None):
     ap.add_argument("--ps_transport", choices=["auto", "native", "pg"], default="auto",
                     help="--mode=ps data plane: native = hipIpc mailboxes + C++ service thread (one node, GPUs; "
                          "parallel/ps_native.py), pg = torch.distributed send/recv; auto = native when eligible")
+    ap.add_argument("--ps_partition_mb", type=float, default=0.0,
+                    help="--mode=ps: split every variable larger than this many MB (fp32) into partitions "
+                         "'<var>/part_<i>' dealt round-robin over the ps tasks (tf.variable_axis_size_partitioner "
+                         "semantics; checkpoints keep the TF slice layout).  0: whole variables, as the reference")
     ap.add_argument("--metrics_jsonl", default="", help="append {step, gs, ms, images/sec, loss} lines here")
     ap.add_argument("--heartbeat_secs", type=float, default=None,
                     help="publish a TCPStore heartbeat every N s; 0: off.  Default: %s s in --mode=allreduce "

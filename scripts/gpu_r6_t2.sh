@@ -1,0 +1,21 @@
+# Round 6: tile-22 GEMM tests + CNN step tests, new ResNet-20 tests, CNN bench + in-graph trace
+set -o pipefail
+O=gpurun_out/${1:-r6t2}
+mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_gemm_glds_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "tile22 or dgrad_and_wgrad or group" > $O/pytest_gemm.log 2>&1
+rc=$?; tail -5 $O/pytest_gemm.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_gemm.log | head -30; exit $rc; }
+timeout -k 10 300 python3 -u -m pytest tests/test_mnist_cnn_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_cnn.log 2>&1
+rc=$?; tail -3 $O/pytest_cnn.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_cnn.log | head -30; exit $rc; }
+for pw in 150 0; do
+  timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --prewarm_ms $pw > $O/cnn_pw$pw.log 2>&1 || { tail -5 $O/cnn_pw$pw.log; exit 1; }
+  echo "cnn prewarm=$pw $(grep -o '"ms_per_step": [0-9.]*' $O/cnn_pw$pw.log)"
+done
+timeout -k 10 200 python3 bench/gemm_sweep.py --iters 20 --tiles 12,22 --splits 1 > $O/gemm.log 2>&1 || { tail -5 $O/gemm.log; exit 1; }
+cat $O/gemm.log
+timeout -k 10 600 python3 -u -m pytest tests/test_resnet.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "fold_batch or queue_guard or grouped_flush or bucket_flush or bench_shaped or evaluate" > $O/pytest_r20.log 2>&1
+rc2=$?; grep -E "PASS|FAIL|Error" $O/pytest_r20.log | head -20
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 > $GRAFT_REPO_ROOT/$O/prof.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/$O/prof.log; exit 1; }
+cd $GRAFT_REPO_ROOT
+python3 scripts/timeline.py $(ls $O/prof/*/run_kernel_trace.csv | head -1) conv1c_fwd 15 > $O/timeline.txt && cat $O/timeline.txt
+exit $rc2

@@ -61,8 +61,8 @@ def test_bundle_roundtrip_and_layout(tmp_path):
     assert rt().pb_parse(ver)[0][:3] == (1, 0, 1)
     # entry: dtype DT_FLOAT=1, shape dims, offset/size, masked crc32c of the bytes
     idx = rt().read_bundle_index(prefix)
-    dt, shape, off, size, crc = idx["Variable"]
-    assert dt == 1 and list(shape) == [3, 4] and size == 48
+    dt, shape, off, size, crc, slices = idx["Variable"]
+    assert dt == 1 and list(shape) == [3, 4] and size == 48 and slices == []
     assert crc == rt().crc32c(ckpt._tensor_bytes(tensors["Variable"]))
     # corrupting the data file is detected by the crc
     with open(prefix + ".data-00000-of-00001", "r+b") as f:

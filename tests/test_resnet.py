@@ -567,3 +567,209 @@ def test_resnet20_bn_src_fold_matches_materialised_gpu(monkeypatch):
     assert abs(l2 - l0) <= 4 * abs(l1 - l0) + 1e-3 * abs(l0)
     assert rel(g2, g0) <= 4 * rel(g1, g0) + 2e-2
     assert rel(m2, m0) <= 4 * rel(m1, m0) + 1e-4
+
+
+# ---------------------------------------------------------------------------------------------
+# Round 6: evaluation at the fold / fused-head batch sizes, the deferred weight-gradient queue,
+# the per-bucket grouped flush of the multi-rank schedules, and the bench-shaped step vs fp32.
+
+class _Hook:
+    """Stand-in for BucketAllReduce / the ps link: a bucket list and a ready(lo, after) hook."""
+
+    def __init__(self, buckets):
+        self.buckets = buckets
+        self.fired = []
+
+    def ready(self, lo, after=None):
+        for i, (blo, _hi) in enumerate(self.buckets):
+            if blo >= lo and i not in self.fired:
+                self.fired.append(i)
+
+
+def _r20_buckets(prog, n):
+    """n contiguous buckets over the flat gradient, back to front (the all-reduce's order)."""
+    N = prog.P.grad.numel()
+    cuts = [N * k // n for k in range(n + 1)]
+    return [(cuts[k], cuts[k + 1]) for k in range(n - 1, -1, -1)]
+
+
+def test_bucket_completes_fires_once_per_bucket_cpu():
+    prog = ResNetModel(arch="resnet20").program("cpu", 2, seed=0)
+    hook = _Hook(_r20_buckets(prog, 3))
+    prog.grad_ready = hook.ready
+    prog._ready_lo = 1 << 62
+    lo0, lo1, lo2 = (b[0] for b in hook.buckets)
+    fires = [prog._bucket_completes(x) for x in (lo0 + 5, lo0, lo0 - 1, lo1 + 1, lo1, 0, 0)]
+    assert fires == [False, True, False, False, True, True, False]
+
+
+@pytest.mark.gpu
+def test_resnet20_evaluate_at_fold_batch_gpu():
+    """evaluate() at B=128 (the bn1 source-fold and fused-head gates are open at this batch) with
+    moving averages far from the batch statistics: logits equal the CPU inference-BN path on the
+    same weights, and parameters, moving averages and gradients are untouched."""
+    B = 128
+    torch.manual_seed(7)
+    model = ResNetModel(arch="resnet20")
+    progs = {dev: model.program(dev, B, seed=4) for dev in ("cpu", "cuda")}
+    gp, cp = progs["cuda"], progs["cpu"]
+    g = torch.Generator().manual_seed(9)
+    for bn in cp.batchnorms():  # moving averages unrelated to any batch's statistics
+        cp.P.view(bn.mm).copy_(torch.randn(bn.C, generator=g) * 0.3)
+        cp.P.view(bn.mv).copy_(torch.rand(bn.C, generator=g) * 2 + 0.5)
+    gp.P.master.copy_(cp.P.master.to("cuda"))
+    gp.P.refresh_copies()
+    cp.P.refresh_copies()
+    x = torch.rand(B, 32, 32, 3, generator=g)
+    y = torch.randint(0, 10, (B,), generator=g)
+    gp.P.grad.fill_(0.25)
+    before_m, before_g = gp.P.master.clone(), gp.P.grad.clone()
+    acc = gp.evaluate(x.cuda(), y.view(-1, 1).cuda())
+    torch.cuda.synchronize()
+    gl = gp.logits.float().cpu()
+    cp.evaluate(x, y.view(-1, 1))
+    assert all(not b.src_fold for b in gp.L["blocks"]) and not gp.head_fused
+    assert torch.equal(before_m, gp.P.master), "evaluate() changed parameters / moving averages"
+    assert torch.equal(before_g, gp.P.grad), "evaluate() wrote gradients"
+    assert _rel(gl, cp.logits.float()) < 3e-2
+    assert abs(acc - (gl.argmax(1) == y).float().mean().item()) < 1e-6
+    # training afterwards still takes the fused schedule
+    gp.load_batch((x.cuda(), F.one_hot(y, 10).float().cuda()))
+    gp.compute_grads()
+    assert gp.head_fused and all(b.src_fold for b in gp.L["blocks"])
+
+
+@pytest.mark.gpu
+def test_resnet20_deferred_queue_guard_gpu(monkeypatch):
+    """A deferred weight-gradient reduce left in the queue (a stray imgwgrad(defer=True), or a
+    backward interrupted between its deferred launches and the flush) makes the next backward fail
+    loudly and is discarded; an exception inside backward leaves the queue empty."""
+    from dtfe import ops
+    B = 128
+    prog = ResNetModel(arch="resnet20").program("cuda", B, seed=1)
+    x = torch.rand(B, 32, 32, 3, device="cuda")
+    y = F.one_hot(torch.randint(0, 10, (B,), device="cuda"), 10).float()
+    prog.load_batch((x, y))
+    prog.compute_grads()
+    assert prog.defer_wgrad and ops.wgrad_pending() == 0
+    c = prog._defer_convs[0]
+    dy = torch.randn(B, c.OH, c.OW, c.cout, device="cuda").to(torch.bfloat16)
+    src = torch.randn(B, c.H, c.W, c.cin, device="cuda").to(torch.bfloat16)
+    ops.imgwgrad(src, torch.zeros_like(c.gw), None, dy=dy, workspace=prog._defer_ws[c], defer=True, **c.ic)
+    assert ops.wgrad_pending() == 1
+    with pytest.raises(RuntimeError, match="deferred weight-gradient"):
+        prog.compute_grads()
+    assert ops.wgrad_pending() == 0
+    # an exception after some deferred launches: nothing survives into the next backward
+    blk = prog.L["blocks"][0]
+    real = blk.bwd
+
+    def boom(*a, **k):
+        raise ValueError("injected")
+    monkeypatch.setattr(blk, "bwd", boom)
+    with pytest.raises(ValueError):
+        prog.compute_grads()
+    assert ops.wgrad_pending() == 0
+    monkeypatch.setattr(blk, "bwd", real)
+    prog.compute_grads()
+    torch.cuda.synchronize()
+    assert ops.wgrad_pending() == 0 and torch.isfinite(prog.P.grad).all()
+
+
+@pytest.mark.gpu
+def test_wgrad_grouped_flush_bitwise_gpu():
+    """The grouped flush of several deferred reduces equals each conv's own reduce launch bit for bit
+    (ResNet-20's whole-image weight-gradient shapes at B=256)."""
+    from dtfe import ops
+    B = 256
+    prog = ResNetModel(arch="resnet20").program("cuda", B, seed=1)
+    convs = prog._defer_convs[::3]
+    torch.manual_seed(2)
+    ins = [(torch.randn(B, c.H, c.W, c.cin, device="cuda").to(torch.bfloat16),
+            torch.randn(B, c.OH, c.OW, c.cout, device="cuda").to(torch.bfloat16)) for c in convs]
+    outs = []
+    for defer in (False, True):
+        dws = [torch.full_like(c.gw, 0.5) for c in convs]
+        for c, (src, dy), dw in zip(convs, ins, dws):
+            ops.imgwgrad(src, dw, None, dy=dy, workspace=prog._defer_ws[c], defer=defer, **c.ic)
+        if defer:
+            assert ops.wgrad_flush() == len(convs)
+        torch.cuda.synchronize()
+        outs.append(dws)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb", [1, 3])
+def test_resnet20_bucket_flush_matches_per_call_reduce_gpu(monkeypatch, nb):
+    """Multi-rank schedule (a bucket hook set) at B=256: the deferred reduces flushed once per bucket
+    (nb + at most 1 grouped launches instead of one reduce per conv) give the per-call reduce's
+    gradients, within the run-to-run noise of the BN statistics' atomics."""
+    import dtfe.models.resnet as R
+    from dtfe import ops
+    B = 256
+    torch.manual_seed(0)
+    x = torch.rand(B, 32, 32, 3).cuda()
+    y = F.one_hot(torch.randint(0, 10, (B,)), 10).float().cuda()
+    flushes = []
+    real_flush = ops.wgrad_flush
+
+    def counting_flush():
+        n = real_flush()
+        if n:
+            flushes.append(n)
+        return n
+    monkeypatch.setattr(ops, "wgrad_flush", counting_flush)
+    runs = []
+    for defer in (False, False, True):
+        monkeypatch.setattr(R, "_WGRAD_DEFER", defer)
+        prog = ResNetModel(arch="resnet20").program("cuda", B, seed=3)
+        hook = _Hook(_r20_buckets(prog, nb))
+        prog.grad_ready = hook.ready
+        prog.load_batch((x, y))
+        m = prog.compute_grads()
+        torch.cuda.synchronize()
+        assert prog.defer_wgrad == defer and sorted(hook.fired) == list(range(nb))
+        runs.append((float(m["loss"]), prog.P.grad.clone()))
+    n_conv = len(prog._defer_convs)
+    assert sum(flushes) == n_conv and len(flushes) <= nb + 1, flushes
+    (l0, g0), (l1, g1), (l2, g2) = runs
+    assert abs(l2 - l0) <= 4 * abs(l1 - l0) + 1e-3 * abs(l0)
+    assert _rel(g2, g0) <= 4 * _rel(g1, g0) + 1e-3, (_rel(g2, g0), _rel(g1, g0))
+
+
+@pytest.mark.gpu
+def test_resnet20_bench_shaped_step_matches_autograd():
+    """ResNet-20 at the bench batch (B=256) on its default schedule - deferred grouped weight-gradient
+    reduce, fused classifier head, bn1's apply folded into conv2's staging, the stem's LDS epilogue -
+    against fp32 autograd of the same network with the forward rounded to bf16 at the program's
+    storage points (the CNN's test_cnn_bench_shaped_step_matches_autograd counterpart).  Per-variable
+    relative error for the head and the last block, cosine elsewhere."""
+    B = 256
+    model = ResNetModel(arch="resnet20")
+    torch.manual_seed(0)
+    prog = model.program("cuda", B, seed=1)
+    x = torch.rand(B, 32, 32, 3, device="cuda")
+    y = F.one_hot(torch.randint(0, 10, (B,), device="cuda"), 10).float()
+    prog.load_batch((x, y))
+    m = prog.compute_grads()
+    torch.cuda.synchronize()
+    assert prog.defer_wgrad and prog.head_fused and all(b.src_fold for b in prog.L["blocks"])
+    loss, ref = _ref_forward(model, prog.P, prog.x, y, device="cuda", round_act=True)
+    assert abs(float(m["loss"].item()) - loss.item()) < 5e-3 * max(1.0, abs(loss.item()))
+    names = [s.name for s in model.specs if not s.name.endswith(("moving_mean", "moving_variance"))]
+    last = set(prog.L["blocks"][-1].var_names)
+    rows = []
+    for n in names:
+        g, r = prog.P.gview(n).detach().float(), ref[n].grad.float()
+        rows.append((n, _rel(g, r), _cos(g, r)))
+    head = [r for r in rows if r[0].startswith("dense")]
+    tail = [r for r in rows if r[0] in last]
+    rest = [r for r in rows if r not in head and r not in tail]
+    # (measured on MI355X: head rel <= 0.3 %, last block rel 0.1-9.7 % at cos >= 0.995 - its gradients
+    # pass through bf16-stored backward activations the oracle keeps in fp32; elsewhere cos >= 0.98)
+    assert all(e < 2e-2 for _, e, _ in head), head
+    assert all(e < 0.15 and c > 0.99 for _, e, c in tail), tail
+    bad = [r for r in rest if r[2] < 0.98]
+    assert not bad, bad
