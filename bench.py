@@ -83,6 +83,11 @@ def parse_args(argv=None):
     ap.add_argument("--ps_stream", default="normal",
                     help="--mode ps: the ps apply stream - normal, high (highest queue priority) or cu<N> (CU mask "
                          "of N CUs); the ps shares GPU 0 with worker 0")
+    ap.add_argument("--num_ps", type=int, default=1,
+                    help="--mode ps: ps tasks (P); ps k runs on GPU k * ndev / P (distinct GPUs when ndev >= P)")
+    ap.add_argument("--ps_partition_mb", type=float, default=0.0,
+                    help="--mode ps: partition variables larger than this many MB over the ps tasks "
+                         "(parallel/partition.py; the CNN's fc1 weight is 12.8 MB)")
     ap.add_argument("--ps_verify", type=int, default=0, help=argparse.SUPPRESS)  # test hook, see bench_ps
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (one rank per GPU); gloo only to rehearse several ranks on one GPU")
@@ -418,11 +423,12 @@ def bench_resnet(args, d: Dist):
 
 
 def bench_ps(args):
-    """BASELINE.json config 4: MNIST CNN async parameter-server SGD, 1 ps + N workers on one node.
+    """BASELINE.json config 4: MNIST CNN async parameter-server SGD, P ps + N workers on one node.
 
-    Rank 0 is the ps task (its shard of every variable + the TF1 Adam slots on GPU 0, served by
-    the native C++ progress thread of ``parallel/ps_native.py``); ranks 1..N are workers on GPUs
-    0..N-1.  A worker step = HBM batch sampling fused into conv1, forward, backward with the
+    Ranks 0..P-1 are the ps tasks (each its round-robin shard of the variables + their TF1 Adam slots,
+    ps k on GPU k * ndev / P, served by the native C++ progress thread of ``parallel/ps_native.py``;
+    with --ps_partition_mb the fc1 weight is split into partitions dealt over the ps tasks,
+    parallel/partition.py); ranks P..P+N-1 are workers on GPUs 0..N-1.  A worker step = HBM batch sampling fused into conv1, forward, backward with the
     gradient buckets pushed into the ps's hipIpc mailboxes on a side stream while backward
     continues (bf16 over xGMI), a device-side request / wait for the ps's apply, and the pull of
     the fresh bf16 working copies - one hipGraph replay, no host round trip.  Every push is
@@ -435,34 +441,41 @@ def bench_ps(args):
     from dtfe.parallel import ps_native
     from dtfe.parallel.cluster import ClusterSpec, Server
     from dtfe.parallel.ps import PSClient, PSServer, Shard, wait_for_init
+    from dtfe.parallel.partition import PartitionedModel
     from dtfe.train import _shard_layout
     from dtfe.utils.graphs import StepGraph, graphs_enabled
 
-    N = args.gpus or 1
+    N, NP = args.gpus or 1, max(1, args.num_ps)
     world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
-    if world != N + 1:
-        raise SystemExit("bench.py --mode ps: expected %d processes (1 ps + %d workers), got %d" % (N + 1, N, world))
+    if world != N + NP:
+        raise SystemExit("bench.py --mode ps: expected %d processes (%d ps + %d workers), got %d"
+                         % (N + NP, NP, N, world))
     ndev = max(1, torch.cuda.device_count())
     port = int(os.environ["MASTER_PORT"])
-    cluster = ClusterSpec(["127.0.0.1:%d" % port], ["127.0.0.1:%d" % (port + 1 + i) for i in range(N)])
+    cluster = ClusterSpec(["127.0.0.1:%d" % (port + i) for i in range(NP)],
+                          ["127.0.0.1:%d" % (port + NP + i) for i in range(N)])
     job, idx = cluster.task_of(rank)
-    gpu = 0 if job == "ps" else idx % ndev
+    gpu = (idx * ndev // NP) % ndev if job == "ps" else idx % ndev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     server = Server(cluster, job, idx, backend="nccl", device=dev)
-    model = MnistCnnModel()
-    placement, shard_specs = _shard_layout(model, 1)
+    full_model = MnistCnnModel()
+    model = PartitionedModel(full_model, int(args.ps_partition_mb * (1 << 20))) if args.ps_partition_mb > 0 \
+        else full_model
+    placement, shard_specs = _shard_layout(model, NP)
+    gs_ps = placement[model.gs_name]
     B = args.batch_size or MODEL_BATCH["mnist_cnn"]
     if job == "ps":
-        shard = Shard(shard_specs[0], model.opt_groups, dev, True, model.gs_increments)
+        shard = Shard(shard_specs[idx], model.opt_groups, dev, gs_ps == idx, model.gs_increments)
         ps = PSServer(server, shard, num_workers=N, comm_device="cpu", log=lambda *_: None)
         ps.native = ps_native.NativeShardService(server, shard, N, hogwild=args.hogwild,
                                                  fused_replies=args.ps_fused_reply == "on", stream=args.ps_stream)
         ps.serve_forever()
         st = ps.native.stats()
         ps.native.stop()
-        server.store.set("dtfe/bench/ps_stats", json.dumps(dict(st, global_step=shard.global_step())))
-        print("ps: %s" % json.dumps(st), file=sys.stderr, flush=True)
+        server.store.set("dtfe/bench/ps_stats/%d" % idx, json.dumps(dict(st, global_step=shard.global_step(),
+                                                                         numel=shard.numel, gpu=gpu)))
+        print("ps %d: %s" % (idx, json.dumps(st)), file=sys.stderr, flush=True)
         server.shutdown()
         _rank_exit()
 
@@ -472,13 +485,15 @@ def bench_ps(args):
         return float(t.item())
 
     tr = MnistCnnTrainer(B, dev, seed=0, rank=idx)
-    client = PSClient(server, tr.P, placement, shard_specs, cluster.rank_of("ps", 0), model.opt_groups,
+    if isinstance(model, PartitionedModel):
+        model.add_aliases(tr.P)   # partitions as views of the worker's full variables
+    client = PSClient(server, tr.P, placement, shard_specs, cluster.rank_of("ps", gs_ps), model.opt_groups,
                       comm_device="cpu")
     if idx == 0:
         client.init_variables()   # the chief's global_variables_initializer
     else:
         wait_for_init(client, poll_s=0.05)
-    link = ps_native.NativePSLink(server, tr.P, placement, shard_specs, placement[model.gs_name], dev,
+    link = ps_native.NativePSLink(server, tr.P, placement, shard_specs, gs_ps, dev,
                                   buckets=tr.buckets, overlap={"auto": None, "on": True, "off": False}[args.ps_overlap])
     tr.allreduce = link           # bucket pushes fork off backward (MnistCnnTrainer.forward_backward)
     link.pull()
@@ -514,8 +529,10 @@ def bench_ps(args):
     loss = float(tr.loss_sum.item()) / B
     link.close()
     client.done()
-    stats = json.loads(server.store.get("dtfe/bench/ps_stats").decode()) if idx == 0 else None
+    allst = [json.loads(server.store.get("dtfe/bench/ps_stats/%d" % k).decode()) for k in range(NP)] \
+        if idx == 0 else None
     if idx == 0:
+        stats = allst[gs_ps]
         pushes = N * (args.steps + args.warmup + pre)  # every runner() call is exactly one step (one push)
         rec_extra = {"optimizer": "adam (TF1), applied on the ps", "hip_graph": runner.graph is not None,
                      "last_loss": round(loss, 4), "global_step": gs, "ps_applies": stats.get("applies"),
@@ -523,7 +540,9 @@ def bench_ps(args):
                      "ps_refreshed_ranges": stats.get("refreshed_ranges"),
                      "ps_global_step": stats.get("global_step"),
                      "pushes_issued": pushes, "ps_stream": args.ps_stream, "transport": "hipIpc mailboxes + C++ ps service (bf16 push, bf16 pull)",
-                     "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": 0,
+                     "hogwild": bool(args.hogwild), "distinct_gpus": min(N, ndev), "ps_gpu": allst[0]["gpu"],
+                     "num_ps": NP, "ps_partition_mb": args.ps_partition_mb,
+                     "ps_shards": [{"gpu": a["gpu"], "params": a["numel"], "applies": a["applies"]} for a in allst],
                      "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
 
         class _R:
@@ -531,27 +550,26 @@ def bench_ps(args):
             world = N
         args_ps = argparse.Namespace(**vars(args))
         args_ps.model = "mnist_cnn_ps"
-        _emit(_R, args_ps, "images/sec (whole node), MNIST CNN async parameter server (1 ps + %d workers)" % N,
+        _emit(_R, args_ps, "images/sec (whole node), MNIST CNN async parameter server (%d ps + %d workers)" % (NP, N),
               B * N * args.steps / elapsed, elapsed, win,
               "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout-fc10, %d params)" % num_params(), B,
-              dict(rec_extra, parallelism="ps1+w%d" % N),
+              dict(rec_extra, parallelism="ps%d+w%d" % (NP, N)),
               "synthetic (HBM-resident MNIST-shaped uint8 images, random labels; random-init weights)")
     _rank_exit()
 
 
 def _ps_verify(args, run1, link, client, tr, shard_specs, dev, server):
-    """--ps_verify K (1 ps + 1 worker, a test hook): K replayed worker steps; after each, the pulled
+    """--ps_verify K (P ps + 1 worker, a test hook): K replayed worker steps; after each, the pulled
     bf16 working copies (natural + transposed) and fp32 variables must equal, bit for bit, what the
-    ps shard's fp32 variables give (fetched over the control channel while the ps is idle - one
+    ps shards' fp32 variables give (partitions compared as the worker's alias views) (fetched over the control channel while the ps is idle - one
     worker, its push applied).  Prints one JSON line with the per-step digests of the pulled copies
     (other data-plane variants must reproduce them) and exits."""
     import hashlib
 
     from dtfe.optim import FlatParams
 
-    assert args.gpus in (None, 1) and len(shard_specs) == 1, "--ps_verify: 1 ps + 1 worker"
-    specs = shard_specs[0]
-    ref = FlatParams(specs, dev, init=False)
+    assert args.gpus in (None, 1), "--ps_verify: P ps + 1 worker"
+    refs = {k: FlatParams(specs, dev, init=False) for k, specs in shard_specs.items() if specs}
     digests, mismatches = [], []
     for i in range(args.ps_verify):
         run1()
@@ -559,24 +577,25 @@ def _ps_verify(args, run1, link, client, tr, shard_specs, dev, server):
         torch.cuda.synchronize()
         link.check()
         st, _gs = client.fetch_state()
-        ref.master.copy_(st[0][:ref.total].to(dev))
-        ref.refresh_copies()
         h = hashlib.sha1()
-        for sp in specs:
-            parts = []
-            if sp.name in ref.w16:
-                parts.append(("w16", tr.P.w16[sp.name], ref.w16[sp.name]))
-            if sp.name in ref.wt16:
-                parts.append(("wt16", tr.P.wt16[sp.name], ref.wt16[sp.name]))
-            if not parts:
-                parts.append(("master", tr.P.view(sp.name), ref.view(sp.name)))
-            for part, got, want in parts:
-                g = got.contiguous().view(-1).view(torch.int16 if got.dtype == torch.bfloat16 else torch.int32)
-                w = want.contiguous().view(-1).view(g.dtype)
-                if not torch.equal(g, w):
-                    mismatches.append({"step": i, "var": sp.name, "part": part,
-                                       "n_diff": int((g != w).sum().item())})
-                h.update(g.cpu().numpy().tobytes())
+        for k, ref in sorted(refs.items()):
+            ref.master.copy_(st[k][:ref.total].to(dev))
+            ref.refresh_copies()
+            for sp in shard_specs[k]:
+                parts = []
+                if sp.name in ref.w16:
+                    parts.append(("w16", tr.P.w16[sp.name], ref.w16[sp.name]))
+                if sp.name in ref.wt16:
+                    parts.append(("wt16", tr.P.wt16[sp.name], ref.wt16[sp.name]))
+                if not parts:
+                    parts.append(("master", tr.P.view(sp.name), ref.view(sp.name)))
+                for part, got, want in parts:
+                    g = got.contiguous().view(-1).view(torch.int16 if got.dtype == torch.bfloat16 else torch.int32)
+                    w = want.contiguous().view(-1).view(g.dtype)
+                    if not torch.equal(g, w):
+                        mismatches.append({"step": i, "var": sp.name, "part": part,
+                                           "n_diff": int((g != w).sum().item())})
+                    h.update(g.cpu().numpy().tobytes())
         digests.append(h.hexdigest()[:16])
     print(json.dumps({"ps_verify": digests, "mismatches": mismatches[:20], "n_mismatch": len(mismatches),
                       "fused_reply": args.ps_fused_reply, "overlap": args.ps_overlap}), flush=True)
@@ -602,8 +621,8 @@ def main(argv=None):
     args = parse_args(argv)
     if args.mode == "ps":
         if os.environ.get("DTFE_BENCH_CHILD") != "1":
-            # 1 ps + N workers = N + 1 processes on N GPUs (the ps shares GPU 0 with worker 0)
-            return launch_ranks((args.gpus or 1) + 1, argv)
+            # P ps + N workers = N + P processes on N GPUs (ps k shares GPU k * N / P with a worker)
+            return launch_ranks((args.gpus or 1) + max(1, args.num_ps), argv)
         return bench_ps(args)
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         return launch_ranks(args.gpus, argv)

@@ -134,18 +134,10 @@ dtfe::ConvGeom geom(int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, in
   return g;
 }
 
-// optional fp32 [2][C] (scale, shift) of the BatchNorm whose input x is (ConvFwdArgs::xf)
-const float* xf_ptr(const optional<Tensor>& xf, int64_t C, const char* who) {
-  if (!xf.has_value() || !xf->defined()) return nullptr;
-  TORCH_CHECK(xf->is_cuda() && xf->scalar_type() == at::kFloat && xf->is_contiguous() && xf->numel() == 2 * C,
-              who, ": xf must be a contiguous fp32 [2][C] (scale, shift) tensor");
-  return xf->data_ptr<float>();
-}
-
 void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
               const optional<Tensor>& argmax, int64_t B, int64_t H, int64_t W, int64_t C, int64_t Cout, int64_t OH,
               int64_t OW, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool pool, int64_t act,
-              const optional<Tensor>& bn_stats, const optional<Tensor>& xf) {
+              const optional<Tensor>& bn_stats) {
   check_cuda(x, "x");
   if (x.scalar_type() == at::kFloat) {  // exact-fp32 path (--dtype fp32): conv_f32.hip
     TORCH_CHECK(w.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat && !(bn_stats.has_value() && bn_stats->defined()),
@@ -174,7 +166,6 @@ void conv_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, co
   a.y = reinterpret_cast<dtfe::bf16*>(y.data_ptr());
   a.argmax = ptr_or_null<uint8_t>(argmax);
   a.act = (int)act;
-  a.xf = xf_ptr(xf, C, "conv_fwd");
   dtfe::launch_conv_fwd(a, cur_stream());
 }
 
@@ -374,7 +365,7 @@ void imgwgrad(const Tensor& src, const optional<Tensor>& dy, const optional<Tens
 
 void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optional<Tensor>& db, int64_t B, int64_t H,
                 int64_t W, int64_t C, int64_t Cout, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t stride,
-                int64_t pad, double scale, const optional<Tensor>& xf) {
+                int64_t pad, double scale) {
   check_cuda(dz, "dz");
   TORCH_CHECK(dw.scalar_type() == at::kFloat, "conv_wgrad: fp32 grad buffer");
   if (dz.scalar_type() == at::kFloat) {  // exact-fp32 path (--dtype fp32): conv_f32.hip
@@ -394,7 +385,6 @@ void conv_wgrad(const Tensor& dz, const Tensor& x, const Tensor& dw, const optio
   a.dw = dw.data_ptr<float>();
   a.db = ptr_or_null<float>(db);
   a.scale = (float)scale;
-  a.xf = xf_ptr(xf, C, "conv_wgrad");
   dtfe::launch_conv_wgrad(a, cur_stream());
 }
 
@@ -872,23 +862,6 @@ void bn_apply(const Tensor& x, const Tensor& stats, const Tensor& gamma, const T
   dtfe::launch_bn_apply(a, cur_stream());
 }
 
-// bn_apply's channel setup without the pass: mean / invstd / moving averages and xf = (scale, shift)
-void bn_finalize(const Tensor& x, const Tensor& stats, const Tensor& gamma, const Tensor& beta,
-                 const optional<Tensor>& mean, const optional<Tensor>& invstd, const optional<Tensor>& moving_mean,
-                 const optional<Tensor>& moving_var, double eps, double momentum, const Tensor& xf) {
-  dtfe::BnArgs a = bn_common(x, stats, 1);
-  TORCH_CHECK(xf.is_cuda() && xf.scalar_type() == at::kFloat && xf.is_contiguous() && xf.numel() >= 2 * a.C,
-              "bn_finalize: xf must be fp32 [2][C]");
-  a.gamma = gamma.data_ptr<float>();
-  a.beta = beta.data_ptr<float>();
-  a.mean = ptr_or_null<float>(mean);
-  a.invstd = ptr_or_null<float>(invstd);
-  a.moving_mean = ptr_or_null<float>(moving_mean);
-  a.moving_var = ptr_or_null<float>(moving_var);
-  a.eps = (float)eps; a.momentum = (float)momentum;
-  dtfe::launch_bn_finalize(a, xf.data_ptr<float>(), cur_stream());
-}
-
 // inference-mode BatchNorm: out = act(gamma * (x - moving_mean) * rsqrt(moving_var + eps) + beta [+ res])
 void bn_infer(const Tensor& x, const Tensor& gamma, const Tensor& beta, const Tensor& moving_mean,
               const Tensor& moving_var, double eps, int64_t act, const optional<Tensor>& res, int64_t rstride,
@@ -1057,8 +1030,6 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("bn_stats(Tensor x, Tensor(a!) stats) -> ()");
   m.def("bn_infer(Tensor x, Tensor gamma, Tensor beta, Tensor moving_mean, Tensor moving_var, float eps, int act,"
         " Tensor? res, int rstride, int OH, int OW, Tensor(a!) out) -> ()");
-  m.def("bn_finalize(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
-        " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, Tensor(e!) xf) -> ()");
   m.def("bn_apply(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor(a!)? mean, Tensor(b!)? invstd,"
         " Tensor(c!)? moving_mean, Tensor(d!)? moving_var, float eps, float momentum, int act, Tensor? res,"
         " int rstride, int OH, int OW, Tensor(e!) out, Tensor(f!)? mask_out=None, Tensor(g!)[]? res_bn=None) -> ()");
@@ -1088,8 +1059,8 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(c!)? bias_out, Tensor(d!)? ws, Tensor(e!)? tile_ctr, int a_ones_row=-1, Tensor? ones=None) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, Tensor(b!)? argmax, int B, int H, int W, int C,"
-      " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act, Tensor(c!)? bn_stats=None,"
-      " Tensor? xf=None) -> ()");
+      " int Cout, int OH, int OW, int KH, int KW, int stride, int pad, bool pool, int act, Tensor(c!)? bn_stats=None)"
+      " -> ()");
   m.def(
       "conv_dgrad(Tensor dy, Tensor wt, Tensor(a!) dx, int B, int H, int W, int C, int Cout, int OH, int OW, int KH,"
       " int KW, int stride, int pad, Tensor? pooled, Tensor? argmax, Tensor? relu_mask, bool accumulate=False,"
@@ -1114,7 +1085,7 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("wgrad_discard() -> int");
   m.def(
       "conv_wgrad(Tensor dz, Tensor x, Tensor(a!) dw, Tensor(b!)? db, int B, int H, int W, int C, int Cout, int OH,"
-      " int OW, int KH, int KW, int stride, int pad, float scale, Tensor? xf=None) -> ()");
+      " int OW, int KH, int KW, int stride, int pad, float scale) -> ()");
   m.def(
       "head_xent(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl,"
       " Tensor(c!)? loss_sum, Tensor(d!)? correct, Tensor(e!)? logits, float scale, float inv_keep,"
@@ -1156,7 +1127,6 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("lstm_seq_bwd", &lstm_seq_bwd);
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
-  m.impl("bn_finalize", &bn_finalize);
   m.impl("bn_infer", &bn_infer);
   m.impl("bn_bwd_stats", &bn_bwd_stats);
   m.impl("bn_bwd_apply", &bn_bwd_apply);

@@ -43,9 +43,6 @@ struct ConvFwdArgs {
   const bf16* x; const bf16* w; const float* bias;
   bf16* y; uint8_t* argmax; int act;
   float* bn_stats;   // optional [2][Cout] (zeroed): BatchNorm statistics of y, as bn_stats computes them
-  // optional fp32 [2][C] = (sc, sh): x is the INPUT of a BatchNorm (+ ReLU) whose output the conv reads,
-  // h = relu(x * sc + sh) formed on the operand load (bn_finalize computes sc / sh; implicit-GEMM path)
-  const float* xf;
 };
 struct ConvDgradArgs {
   ConvGeom g;
@@ -66,7 +63,6 @@ struct ConvWgradArgs {
   ConvGeom g;
   const bf16* dz; const bf16* x;    // dz: [B*OH*OW][Cout] (full resolution)
   float* dw; float* db; float scale; int k_chunk;
-  const float* xf;   // optional [2][C] (sc, sh): the operand is relu(x * sc + sh) (ConvFwdArgs::xf)
 };
 
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);

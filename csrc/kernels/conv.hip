@@ -392,13 +392,6 @@ static void bn_stats_of(const ConvFwdArgs& a, hipStream_t s) {
 }
 
 void launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
-  if (a.xf) {  // the BN-on-load operand exists only on the implicit-GEMM path: never silently ignored
-    bool fused = false;
-    if (!launch_igemm_fwd(a, s, &fused))
-      throw std::runtime_error("conv_fwd: a BatchNorm-transformed source (xf) needs the implicit-GEMM path (C % 64 == 0, Cout % 64 == 0, no bias / act / pool)");
-    if (!fused) bn_stats_of(a, s);
-    return;
-  }
   bool stem_stats = false;
   if (launch_stem_fwd(a, s, &stem_stats)) {  // ImageNet 7x7/2 stem (+ BN partials in its epilogue)
     if (!stem_stats) bn_stats_of(a, s);
@@ -451,11 +444,6 @@ static void wgrad_launch(const ConvWgradArgs& a0, int target_blocks, hipStream_t
 }
 
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
-  if (a.xf) {
-    if (!launch_igemm_wgrad(a, s))
-      throw std::runtime_error("conv_wgrad: a BatchNorm-transformed operand (xf) needs the implicit-GEMM path (C % 64 == 0, Cout % 64 == 0, no bias)");
-    return;
-  }
   if (launch_stem_wgrad(a, s, true)) return;
   if (launch_igemm_wgrad(a, s)) return;
   const ConvGeom& g = a.g;

@@ -47,15 +47,11 @@ struct IgemmArgs {
   // bb_y == nullptr with ReLU: the mask is recomputed from x (norm.hip BwdMask).
   const bf16* bb_x; const bf16* bb_y; const float* bb_mean; const float* bb_invstd;
   const float* bb_gamma; const float* bb_beta; int bb_act;
-  // forward only (optional): fp32 [2][SC] = (sc, sh) - the source is a BatchNorm's input x and the conv
-  // reads h = relu(x * sc + sh) (the BN's apply folded into this operand load; ConvFwdArgs::xf)
-  const float* xf;
   IgPhase ph[4];
 };
 
 struct IgWgradArgs {
   const bf16* dy; const bf16* x; const bf16* zeros; float* ws;
-  const float* xf;        // optional [2][C] (sc, sh): the operand is relu(x * sc + sh) (ConvWgradArgs::xf)
   int B, H, W, C, OH, OW, Cout, KH, KW, stride, pad;
   int splits, mchunk;
 };

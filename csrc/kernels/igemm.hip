@@ -276,25 +276,7 @@ constexpr int ig_smem_el() {
   return stage > epi ? stage : epi;
 }
 
-// XF: the source operand is a BatchNorm's input x, used as h = relu(x * sc[c] + sh[c]) (IgemmArgs::xf):
-// the A tile goes HBM -> registers -> (transform) -> LDS instead of by DMA, loaded for k-tile t+1 while
-// the MFMAs of k-tile t run and written to the other LDS stage after them; out-of-image taps and rows
-// past the end are zeros AFTER the transform (the padding of h, not of x)
-__device__ __forceinline__ u32x4_t bn_relu8(const u32x4_t v, const f32x4_t (&sc)[2], const f32x4_t (&sh)[2]) {
-  u32x4_t o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    // bn_apply's rounding (one fma, common.h bn_affine): bit-identical h
-    float lo = bn_affine(__uint_as_float(v[i] << 16), sc[i >> 1][(2 * i) & 3], sh[i >> 1][(2 * i) & 3]);
-    float hi = bn_affine(__uint_as_float(v[i] & 0xffff0000u), sc[i >> 1][(2 * i + 1) & 3], sh[i >> 1][(2 * i + 1) & 3]);
-    lo = lo > 0.f ? lo : 0.f;
-    hi = hi > 0.f ? hi : 0.f;
-    o[i] = pack_bf16x2(lo, hi);
-  }
-  return o;
-}
-
-template <int BM, int BN, int NST, bool BB, int MINB, bool XF = false>
+template <int BM, int BN, int NST, bool BB, int MINB>
 __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_kernel(const IgemmArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_EL = BM * IG_BK, B_EL = BN * IG_BK;
@@ -344,10 +326,6 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_kernel(const IgemmArgs
 #pragma unroll
   for (int j = 0; j < NB; ++j) b_src[j] = a.w + (long)(n_base + (j * 4 + w) * 8 + lrow) * a.Ktot + lchunk * 8;
 
-  // XF: this k-tile's A pieces in registers (ok: tap in the image) and the lane's 8 channels' sc / sh
-  u32x4_t areg[XF ? NA : 1];
-  bool aok[XF ? NA : 1];
-  f32x4_t xsc[2], xsh[2];
   auto issue = [&](int kt, int buf) {
     const int tap = kt / cpt, cb = kt - tap * cpt;
     const int dy = P.dy[tap], dx = P.dx[tap];
@@ -359,34 +337,11 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_kernel(const IgemmArgs
       const int sy = a_iy[j] + dy, sx = a_ix[j] + dx;
       const bool ok = (unsigned)sy < (unsigned)a.SH && (unsigned)sx < (unsigned)a.SW;
       const bf16* p = ok ? a.src + (long)(a_pix[j] + sy * a.SW + sx) * a.SC + cb * IG_BK + lchunk * 8 : a.zeros;
-      if constexpr (XF) {
-        areg[j] = *reinterpret_cast<const u32x4_t*>(p);
-        aok[j] = ok;
-      } else {
-        glds16(p, As + (j * 4 + w) * 512);
-      }
-    }
-    if constexpr (XF) {
-      const f32x4_t* q = reinterpret_cast<const f32x4_t*>(a.xf + cb * IG_BK + lchunk * 8);
-      const f32x4_t* r = reinterpret_cast<const f32x4_t*>(a.xf + a.SC + cb * IG_BK + lchunk * 8);
-      xsc[0] = q[0]; xsc[1] = q[1];
-      xsh[0] = r[0]; xsh[1] = r[1];
+      glds16(p, As + (j * 4 + w) * 512);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) glds16(b_src[j] + woff, Bs + (j * 4 + w) * 512);
   };
-  // XF: the registers of the k-tile issued last -> h -> its LDS stage (lane-linear, as the DMA writes)
-  auto commit_a = [&](int buf) {
-    if constexpr (XF) {
-      bf16* As = smem + buf * (A_EL + B_EL);
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const u32x4_t o = bn_relu8(areg[j], xsc, xsh);
-        *reinterpret_cast<u32x4_t*>(As + (j * 4 + w) * 512 + lane * 8) = aok[j] ? o : u32x4_t{0u, 0u, 0u, 0u};
-      }
-    }
-  };
-
   const int wm = w >> 1, wn = w & 1;
   f32x4_t acc[TM][TN];
 #pragma unroll
@@ -394,10 +349,7 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_kernel(const IgemmArgs
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    issue(kt0, 0);
-    commit_a(0);
-  }
+  if (nk > 0) issue(kt0, 0);
   for (int t = 0; t < nk; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -420,7 +372,6 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_kernel(const IgemmArgs
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (XF && NST > 1 && t + 1 < nk) commit_a((t + 1) & 1);  // (its stage was last read in iteration t-1)
   }
 
   igemm_store<BM, BN, IG_THREADS, SMEM_EL, BB>(a, acc, smem, tid, lane, w, m_base, n_base, tm, Mp, P);
@@ -471,10 +422,7 @@ __device__ __forceinline__ void wg_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// XF (IgWgradArgs::xf): x is a BatchNorm's input and the operand is h = relu(x * sc[c] + sh[c]); each
-// thread rewrites the B chunks it DMA'd once k-tile t has landed (zeros for out-of-image taps - the
-// padding of h), and a second barrier publishes them to the fragment reads
-template <int BM, int BN, int BKW, int NS, int MINB, bool XF = false>
+template <int BM, int BN, int BKW, int NS, int MINB>
 __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgWgradArgs a, float* dw, float scale) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_EL = BKW * BM, B_EL = BKW * BN, ST_EL = A_EL + B_EL;
@@ -511,28 +459,6 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgW
   }
   const bf16* dy_col = a.dy + tm * BM;
   const bf16* x_col = a.x + cb * BN;
-  f32x4_t bsc[XF ? NB : 1][2], bsh[XF ? NB : 1][2];
-  if constexpr (XF) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const f32x4_t* q = reinterpret_cast<const f32x4_t*>(a.xf + cb * BN + b_chk[j] * 8);
-      const f32x4_t* r = reinterpret_cast<const f32x4_t*>(a.xf + a.C + cb * BN + b_chk[j] * 8);
-      bsc[j][0] = q[0]; bsc[j][1] = q[1];
-      bsh[j][0] = r[0]; bsh[j][1] = r[1];
-    }
-  }
-  // is B chunk j of k-tile t a pixel of the image (the same test issue() makes)
-  auto b_in_image = [&](int t, int j) -> bool {
-    const int m = m0 + t * BKW + b_row[j];
-    if (m >= m1) return false;
-    const int q1 = qdiv(m, a.OW, inv_ow);
-    const int ox = m - q1 * a.OW;
-    const int b = qdiv(q1, a.OH, inv_oh);
-    const int oy = q1 - b * a.OH;
-    const int sy = oy * a.stride - a.pad + kh, sx = ox * a.stride - a.pad + kw;
-    return (unsigned)sy < (unsigned)a.H && (unsigned)sx < (unsigned)a.W;
-  };
-
   auto issue = [&](int t) {
     bf16* As = smem + (t % NS) * ST_EL;
     bf16* Bs = As + A_EL;
@@ -577,18 +503,6 @@ __global__ __launch_bounds__(IG_THREADS, MINB) void igemm_wgrad_kernel(const IgW
     __builtin_amdgcn_s_barrier();  // k-tile t landed for every wave; stage (t-1) % NS read by every wave
     __builtin_amdgcn_sched_barrier(0);
     if (t + NS - 1 < nk) issue(t + NS - 1);
-    if constexpr (XF) {
-      bf16* Bw = smem + (t % NS) * ST_EL + A_EL;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        u32x4_t* p = reinterpret_cast<u32x4_t*>(Bw + (j * 4 + w) * 512 + lane * 8);
-        const u32x4_t o = bn_relu8(*p, bsc[j], bsh[j]);
-        *p = b_in_image(t, j) ? o : u32x4_t{0u, 0u, 0u, 0u};
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
     const bf16* As = smem + (t % NS) * ST_EL;
     const bf16* Bs = As + A_EL;
 #pragma unroll
@@ -646,13 +560,10 @@ constexpr int W3_PATCH = 192;  // patch pixels staged per k-tile (>= (R+2)(W+2) 
 // (bank-row half, 32-B segment) pairs - the 64-column form of wg_swz
 __device__ __forceinline__ int w3_swz(int pix) { return wg_swz<64>(pix); }
 
-// XF: as igemm_wgrad_kernel's (the patch chunks rewritten in place; the tile's 64 channels' sc / sh in LDS)
-template <bool XF>
 __global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgradArgs a, float* dw, float scale,
                                                                     int R, int ktiles_per_img) {
   constexpr int A_EL = 64 * 64, P_EL = W3_PATCH * 64, ST_EL = A_EL + P_EL;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * ST_EL];
-  __shared__ __attribute__((aligned(16))) float sxf[XF ? 128 : 4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, W = a.W, PW = W + 2;
@@ -685,9 +596,6 @@ __global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgr
   }
   const bf16* dy_col = a.dy + tco * 64;
   const bf16* x_col = a.x + tc * 64;
-  if constexpr (XF) {
-    if (tid < 128) sxf[tid] = a.xf[(tid >> 6) * a.C + tc * 64 + (tid & 63)];  // [sc 64][sh 64]
-  }
   auto issue = [&](int t, int buf) {
     const int kt = t0 + t, b = kt / ktiles_per_img, oy0 = (kt - b * ktiles_per_img) * R;
     bf16* As = smem + buf * ST_EL;
@@ -696,7 +604,7 @@ __global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgr
     for (int j = 0; j < 2; ++j) {
       const int oy = oy0 + a_r[j];
       const bf16* p = (a_ok[j] && oy < H) ? dy_col + ((long)(b * H + oy) * W + a_x[j]) * a.Cout + a_chk[j] * 8 : a.zeros;
-      glds16(p, As + (j * 4 + w) * 512);
+      glds16_async(p, As + (j * 4 + w) * 512);
     }
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -704,7 +612,7 @@ __global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgr
       const bf16* p = ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W)
                           ? x_col + ((long)(b * H + sy) * W + sx) * a.C + p_chk[j] * 8
                           : a.zeros;
-      glds16(p, Ps + (j * 4 + w) * 512);
+      glds16_async(p, Ps + (j * 4 + w) * 512);
     }
   };
 
@@ -738,23 +646,6 @@ __global__ __launch_bounds__(IG_THREADS, 1) void igemm_wgrad3_kernel(const IgWgr
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
-    if constexpr (XF) {
-      const int kt = t0 + t, b = kt / ktiles_per_img, oy0 = (kt - b * ktiles_per_img) * R;
-      (void)b;
-      bf16* Pw = smem + (t & 1) * ST_EL + A_EL;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int sy = oy0 - 1 + p_r[j], sx = p_c[j] - 1;
-        const int c0 = p_chk[j] * 8;
-        const f32x4_t sc[2] = {*reinterpret_cast<const f32x4_t*>(sxf + c0), *reinterpret_cast<const f32x4_t*>(sxf + c0 + 4)};
-        const f32x4_t sh[2] = {*reinterpret_cast<const f32x4_t*>(sxf + 64 + c0),
-                               *reinterpret_cast<const f32x4_t*>(sxf + 64 + c0 + 4)};
-        u32x4_t* p = reinterpret_cast<u32x4_t*>(Pw + (j * 4 + w) * 512 + lane * 8);
-        const u32x4_t o = bn_relu8(*p, sc, sh);
-        *p = ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W) ? o : u32x4_t{0u, 0u, 0u, 0u};
-      }
-      __syncthreads();
-    }
     const bf16* As = smem + (t & 1) * ST_EL;
     const bf16* Ps = As + A_EL;
 #pragma unroll
@@ -1087,9 +978,7 @@ void launch_ig(IgemmArgs& a, long Mmax, hipStream_t s) {
   // forward 175-180 vs 164-166 us, its data gradient 170 vs 155 us at B=256 - and the forward BN
   // statistics summed from the accumulator registers instead of the staged tile - no faster with the
   // statistics, 9-13 us slower per launch without them: profiles/r5_igemm_epilogue_ab.txt)
-  if (a.xf)
-    hipLaunchKernelGGL((igemm_kernel<BM, BN, 2, false, 2, true>), grid, dim3(IG_THREADS), 0, s, a);
-  else if (a.bb_x)
+  if (a.bb_x)
     hipLaunchKernelGGL((igemm_kernel<BM, BN, 2, true, 2>), grid, dim3(IG_THREADS), 0, s, a);
   else
     hipLaunchKernelGGL((igemm_kernel<BM, BN, 2, false, 2>), grid, dim3(IG_THREADS), 0, s, a);
@@ -1165,10 +1054,9 @@ void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, floa
 bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
   const ConvGeom& g = f.g;
   if (g.C % IG_BK || g.Cout % 64 || g.KH * g.KW > IG_MAX_TAPS || g.pool_order || f.bias || f.act != 0) return false;
-  if (env_int("DTFE_IG_OFF", 0)) return false;
   IgemmArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.src = f.x; a.w = f.w; a.out = f.y; a.xf = f.xf;
+  a.src = f.x; a.w = f.w; a.out = f.y;
   a.B = g.B; a.SH = g.H; a.SW = g.W; a.SC = g.C;
   a.N = g.Cout; a.Ktot = g.KH * g.KW * g.C;
   a.istr = g.stride; a.OHf = g.OH; a.OWf = g.OW; a.ostr = 1;
@@ -1189,7 +1077,6 @@ bool launch_igemm_fwd(const ConvFwdArgs& f, hipStream_t s, bool* stats_done) {
 bool launch_igemm_dgrad(const ConvDgradArgs& d, hipStream_t s) {
   const ConvGeom& g = d.g;
   if (g.Cout % IG_BK || g.C % 64 || g.KH * g.KW > IG_MAX_TAPS || g.stride > 2 || d.unpool || d.relu_mask) return false;
-  if (env_int("DTFE_IG_OFF", 0)) return false;
   IgemmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.src = d.dy; a.w = d.wt; a.out = d.dx;
@@ -1253,10 +1140,9 @@ static bool use_wgrad3(const ConvGeom& g) {
 bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   const ConvGeom& g = f.g;
   if (g.C % 64 || g.Cout % 64 || f.db || g.pool_order) return false;
-  if (env_int("DTFE_IG_OFF", 0)) return false;
   IgWgradArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.dy = f.dz; a.x = f.x; a.xf = f.xf;
+  a.dy = f.dz; a.x = f.x;
   a.B = g.B; a.H = g.H; a.W = g.W; a.C = g.C; a.OH = g.OH; a.OW = g.OW; a.Cout = g.Cout;
   a.KH = g.KH; a.KW = g.KW; a.stride = g.stride; a.pad = g.pad;
   a.zeros = zero_page(s);
@@ -1281,12 +1167,8 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
     sp = std::min(sp, T);
     a.splits = (int)sp;
     if (sp > 1) a.ws = workspace((size_t)sp * len * sizeof(float), s, g_wg);
-    if (a.xf)
-      hipLaunchKernelGGL(igemm_wgrad3_kernel<true>, dim3((unsigned)tiles, (unsigned)sp), dim3(IG_THREADS), 0, s, a,
-                         f.dw, f.scale, R, kpi);
-    else
-      hipLaunchKernelGGL(igemm_wgrad3_kernel<false>, dim3((unsigned)tiles, (unsigned)sp), dim3(IG_THREADS), 0, s, a,
-                         f.dw, f.scale, R, kpi);
+    hipLaunchKernelGGL(igemm_wgrad3_kernel, dim3((unsigned)tiles, (unsigned)sp), dim3(IG_THREADS), 0, s, a, f.dw,
+                       f.scale, R, kpi);
     if (sp > 1)
       launch_wgrad_splits_reduce(a.ws, (int)sp, len, f.dw, f.scale, s);
     return true;
@@ -1318,19 +1200,14 @@ bool launch_igemm_wgrad(const ConvWgradArgs& f, hipStream_t s) {
   dim3 grid((unsigned)tiles, sp);
   // 32-pixel k-tiles in a 4-stage ring (3 in flight, 2 WGs per CU); the 64-pixel 2- and 3-stage
   // rings measured slower (profiles/r4_igemm_kb32_ab.txt, scripts/archive/gpu_r4_wpipe.sh)
-#define DTFE_WG_LAUNCH(BM_, BN_)                                                                                 \
-  do {                                                                                                           \
-    if (a.xf)                                                                                                    \
-      hipLaunchKernelGGL((igemm_wgrad_kernel<BM_, BN_, 32, 4, 2, true>), grid, dim3(IG_THREADS), 0, s, a, f.dw,    \
-                         f.scale);                                                                               \
-    else                                                                                                         \
-      hipLaunchKernelGGL((igemm_wgrad_kernel<BM_, BN_, 32, 4, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale); \
-  } while (0)
-  if (bm == 128 && bn == 128) DTFE_WG_LAUNCH(128, 128);
-  else if (bm == 128) DTFE_WG_LAUNCH(128, 64);
-  else if (bn == 128) DTFE_WG_LAUNCH(64, 128);
-  else DTFE_WG_LAUNCH(64, 64);
-#undef DTFE_WG_LAUNCH
+  if (bm == 128 && bn == 128)
+    hipLaunchKernelGGL((igemm_wgrad_kernel<128, 128, 32, 4, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else if (bm == 128)
+    hipLaunchKernelGGL((igemm_wgrad_kernel<128, 64, 32, 4, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else if (bn == 128)
+    hipLaunchKernelGGL((igemm_wgrad_kernel<64, 128, 32, 4, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
+  else
+    hipLaunchKernelGGL((igemm_wgrad_kernel<64, 64, 32, 4, 2>), grid, dim3(IG_THREADS), 0, s, a, f.dw, f.scale);
   if (sp > 1)
     launch_wgrad_splits_reduce(a.ws, sp, len, f.dw, f.scale, s);
   return true;

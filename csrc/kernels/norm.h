@@ -51,9 +51,6 @@ struct BnArgs {
   float* r_mean; float* r_invstd; float* r_moving_mean; float* r_moving_var;
 };
 
-// mean / invstd / moving averages + xf[2][C] = (gamma * invstd, beta - mean * gamma * invstd) from
-// the statistics, without touching the tensor (the apply is folded into consumer convs, ConvFwdArgs::xf)
-void launch_bn_finalize(const BnArgs& a, float* xf, hipStream_t s);
 void launch_bn_stats(const BnArgs& a, hipStream_t s);
 void launch_bn_apply(const BnArgs& a, hipStream_t s);
 void launch_bn_bwd_stats(const BnArgs& a, hipStream_t s);

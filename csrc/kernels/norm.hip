@@ -751,21 +751,6 @@ __global__ __launch_bounds__(NT) void pool3_bn_bwd_kernel(BnArgs a, const uint8_
   if constexpr (STATS) reduce_stats(s, q, C, a.stats);
 }
 
-// The apply of a BatchNorm (+ ReLU) whose output is only ever read by implicit-GEMM convs, which form
-// it on their operand loads (ConvFwdArgs::xf): what bn_apply's channel setup computes - saved mean /
-// invstd, moving averages, and the per-channel (scale, shift) into xf[2][C] - with no pass over the
-// tensor.  Same expressions as bn_apply's, so the convs' h is bit-identical to bn_apply's output.
-__global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a, float* xf) {
-  for (int c = threadIdx.x; c < a.C; c += NT) {
-    float mean, invstd;
-    chan_params(a, c, mean, invstd);
-    save_chan(a, c, mean, invstd, a.mean, a.invstd, a.moving_mean, a.moving_var);
-    const float scale = a.gamma[c] * invstd;
-    xf[c] = scale;
-    xf[a.C + c] = bn_shift(a.beta[c], mean, scale);
-  }
-}
-
 int ew_grid(long n) {
   long g = (n + 255) / 256;
   if (g > 65536) g = 65536;
@@ -773,11 +758,6 @@ int ew_grid(long n) {
 }
 
 }  // namespace
-
-void launch_bn_finalize(const BnArgs& a, float* xf, hipStream_t s) {
-  check(a);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(NT), 0, s, a, xf);
-}
 
 void launch_bn_stats(const BnArgs& a, hipStream_t s) {
   check(a);

@@ -76,7 +76,7 @@ class LstmProgram(StepProgram):
         self.gWo, self.gbo = self.P.gview("Variable"), self.P.gview("Variable_1")
         self.gK, self.gb = self.P.gview(m.kname), self.P.gview(m.bname)
         # the kernel gradient's own split-K workspace (DTFE_LSTM_TALLK=0: the generic GEMM instead)
-        self.k_splits = int(os.environ.get("DTFE_LSTM_KSPLITS", "32"))
+        self.k_splits = 32  # tall-K kernel-gradient splits (profiles/r2_lstm_wgrad_sweep.txt)
         self.ws_k = None
         if self.device.type == "cuda" and os.environ.get("DTFE_LSTM_TALLK", "1") != "0":
             self.ws_k = torch.empty(ops.tallk_ws_floats(I + H, 4 * H, self.k_splits), **f)

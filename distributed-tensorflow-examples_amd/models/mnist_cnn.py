@@ -337,7 +337,7 @@ class MnistCnnTrainer:
 
     def _head_wgrad(self):
         """head wgrad: dW[10][1024] = dlogit^T . H, db = sum dlogit (dedicated whole-batch kernel; the
-        split-K GEMM path is kept behind DTFE_CNN_HEAD_GEMM=1)"""
+        split-K GEMM path takes B > 1024)"""
         if self.head_gemm:
             ops.gemm(self.dl, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=self.B, amode=ops.RMAJ,
                      lda=self.dl.shape[1], bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"],

@@ -44,9 +44,11 @@ from ..optim import OptimizerConfig, VarSpec
 from .base import ModelDef, ScaledScalar, StepProgram
 
 BN_EPS, BN_MOMENTUM = 1e-3, 0.99
+# Schedule switches below are module constants - test hooks that tests/test_resnet.py monkeypatches
+# to compare a fused path against its unfused oracle, not environment knobs.
 # bottleneck input gradient: shortcut share written into dx, conv1's data gradient accumulated on
-# top (DTFE_R50_SHORTCUT_FUSE=0: separate buffer + add pass, for A/B)
-_SHORTCUT_FUSE = os.environ.get("DTFE_R50_SHORTCUT_FUSE", "1") != "0"
+# top (False: separate buffer + add pass; profiles/r2_resnet50_shortcut_fuse_ab.txt)
+_SHORTCUT_FUSE = True
 # (test hook, not a knob: tests/test_resnet.py compares against the stored-dres path)
 _PROJ_FROM_BITS = True
 # activation / activation-gradient storage dtype: bf16 on the GPU kernels; the CPU reference
@@ -132,19 +134,12 @@ class Conv:
         # shortcut share first, then the conv's on top: no separate add pass)
         self.can_accum = not self.img_dgrad and self.cin % 64 == 0 and self.cout % 64 == 0
 
-    def reads_bn_on_load(self):
-        """Whether forward and weight gradient run on the implicit-GEMM kernels, which can form a
-        preceding BatchNorm + ReLU on their operand loads (ops.conv_fwd / conv_wgrad ``xf``)."""
-        return not self.img_fwd and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0
-
-    def fwd(self, x, stats=None, xf=None, bn_src=None):
+    def fwd(self, x, stats=None, bn_src=None):
         """Forward; ``stats``: the following BatchNorm's [2][C] accumulators, filled by the conv
-        launch itself where it can (returns True then; the BN skips its statistics pass).  ``xf``:
-        x is the input of the preceding BatchNorm + ReLU, applied on the operand load (BN.fwd_fold).
-        ``bn_src``: that BN (BN.src_fold) for the whole-image kernel, which forms BN + ReLU while
-        staging x and saves the BN's statistics / moving averages."""
+        launch itself where it can (returns True then; the BN skips its statistics pass).
+        ``bn_src``: the preceding BatchNorm + ReLU (BN.src_fold) for the whole-image kernel, which
+        forms it while staging the raw input x and saves the BN's statistics / moving averages."""
         if self.img_fwd:
-            assert xf is None
             if bn_src is not None:
                 ops.imgconv(self.w, self.y, src=x, bn_src=bn_src.src_args(), bn_eps=BN_EPS, bn_momentum=BN_MOMENTUM,
                             bn_save=True, **self.ic)
@@ -152,30 +147,29 @@ class Conv:
             ops.imgconv(self.w, self.y, src=x, **self.ic)
             return self.y, False
         assert bn_src is None
-        ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats, xf=xf)
+        ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats)
         return self.y, stats is not None
 
-    def wgrad(self, dy, x, xf=None, after=None, bn_src=None):
+    def wgrad(self, dy, x, after=None, bn_src=None):
         """``after``: the side stream's fork point (SideStream.fork_point, taken when dy was final).
-        ``xf`` / ``bn_src``: as in fwd (x is then the BN's raw input)."""
+        ``bn_src``: as in fwd (x is then the BN's raw input)."""
         dws = getattr(self, "defer_ws", None)
         if bn_src is not None:
             assert self.img_wgrad
             ops.imgwgrad(x, self.gw, None, dy=dy, bn_src=bn_src.src_args(), bn_eps=BN_EPS, workspace=dws,
                          defer=dws is not None, **self.ic)
             return
-        if dws is not None and self.img_wgrad and xf is None:
+        if dws is not None and self.img_wgrad:
             ops.imgwgrad(x, self.gw, None, dy=dy, workspace=dws, defer=True, **self.ic)
             return
         side = getattr(self, "side", None)
         if side is not None and not self.img_wgrad and self.cin % 64 == 0 and self.cout % 64 == 0:
-            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g, xf=xf), after)
+            side.run(lambda: ops.conv_wgrad(dy, x, self.gw, None, self.g), after)
             return
         if self.img_wgrad:
-            assert xf is None
             ops.imgwgrad(x, self.gw, None, dy=dy, **self.ic)
         else:
-            ops.conv_wgrad(dy, x, self.gw, None, self.g, xf=xf)
+            ops.conv_wgrad(dy, x, self.gw, None, self.g)
 
     def dgrad_fuses_bn(self, accumulate=False):
         """Whether conv_dgrad produces the consuming BatchNorm's backward statistics with dx (every
@@ -252,18 +246,12 @@ class SideStream:
 
 
 _WGRAD_STREAM = os.environ.get("DTFE_WGRAD_STREAM", "1") != "0"
-# bn1 / bn2 applies folded into conv2 / conv3's operand loads (BN.fwd_fold, igemm xf paths): OFF - measured
-# slower end to end, 23.42 vs 21.35 ms per ResNet-50 B=256 step (profiles/r5_resnet50_bn_fold_ab.txt: the
-# forward transform sits between a k-tile's loads and its barrier, and the weight gradients' in-place LDS
-# rewrite costs a barrier per k-tile of their 4-stage ring - 319 vs 157 us per 128x128 launch).  Kept as
-# a tested path (tests/test_resnet.py) for the next kernel iteration.  (Test hook, not a knob.)
-_FOLD_BN_APPLY = os.environ.get("DTFE_R5_FOLD", "0") == "1"
-# ResNet-20: bn1's apply formed by conv2's whole-image kernels (BN.src_fold).  (A/B hook, not a knob.)
-_R20_SRC_FOLD = os.environ.get("DTFE_R20_SRC_FOLD", "1") == "1"
-# classifier head forward + backward in one launch (ops.dense_head).  (A/B hook, not a knob.)
-_HEAD_FUSE = os.environ.get("DTFE_HEAD_FUSE", "1") == "1"
-# ResNet-20 weight-gradient reduces deferred to one grouped launch (ops.wgrad_flush).  (A/B hook.)
-_WGRAD_DEFER = os.environ.get("DTFE_WGRAD_DEFER", "1") == "1"
+# ResNet-20: bn1's apply formed by conv2's whole-image kernels (BN.src_fold; profiles/r5_resnet20_kernels.txt)
+_R20_SRC_FOLD = True
+# classifier head forward + backward in one launch (ops.dense_head)
+_HEAD_FUSE = True
+# ResNet-20 weight-gradient reduces deferred to grouped launches (ops.wgrad_flush)
+_WGRAD_DEFER = True
 
 
 class BN:
@@ -286,25 +274,6 @@ class BN:
         self.use_bits = False
         self.stats, self.dstats, self.mean, self.invstd = arena.take(2 * self.C), arena.take(2 * self.C), \
             arena.take(self.C), arena.take(self.C)
-        # (scale, shift) of a folded apply (fwd_fold); outside the zero-per-step arena
-        self.xf = torch.empty(2 * self.C, device=dev)
-        self.folded = False
-
-    def fwd_fold(self, x):
-        """BN + ReLU whose output is read only by implicit-GEMM convs (forward and weight gradient):
-        no apply pass - ops.bn_finalize saves mean / invstd, updates the moving averages and writes
-        (scale, shift) into ``self.xf``, which the consumers apply on their operand loads (h is never
-        stored; bit-identical to bn_apply's output).  The backward recomputes the ReLU mask from x, as
-        after bn_apply.  Returns the raw input x (consumers take ``x, xf=self.xf``)."""
-        P = self.P
-        x, have_stats = x if isinstance(x, tuple) else (x, False)
-        if not have_stats:
-            ops.bn_stats(x, self.stats)
-        ops.bn_finalize(x, self.stats, P.view(self.gamma), P.view(self.beta), self.xf, mean=self.mean,
-                        invstd=self.invstd, moving_mean=P.view(self.mm), moving_var=P.view(self.mv), eps=BN_EPS,
-                        momentum=BN_MOMENTUM)
-        self.mask_from_x, self.use_bits, self.folded = True, False, True
-        return x
 
     def src_fold(self, x):
         """BN + ReLU whose output only whole-image convs read (ResNet-20's bn1 -> conv2 forward and
@@ -314,7 +283,7 @@ class BN:
         x, have_stats = x if isinstance(x, tuple) else (x, False)
         if not have_stats:
             ops.bn_stats(x, self.stats)
-        self.mask_from_x, self.use_bits, self.folded = True, False, False
+        self.mask_from_x, self.use_bits = True, False
         return x
 
     def src_args(self):
@@ -351,7 +320,6 @@ class BN:
         # the block-output BN's two backward passes read dy, x and the mask, not dy, x and y)
         self.mask_from_x = act == ops.ACT_RELU and res is None
         self.use_bits = act == ops.ACT_RELU and res is not None and self.ybits is not None
-        self.folded = False
         if not have_stats:
             ops.bn_stats(x, self.stats)
         ops.bn_apply(x, self.stats, P.view(self.gamma), P.view(self.beta), self.y, mean=self.mean,
@@ -401,11 +369,6 @@ class BN:
         if act == ops.ACT_NONE or from_x:
             return None, (self.P.view(self.beta) if from_x else None)
         return (self.ybits if self.use_bits and act == ops.ACT_RELU else self.y), None
-
-    def consumer_operand(self, x):
-        """(tensor, xf) a consumer conv's weight gradient reads for this BN's output: (x, xf) when the
-        apply was folded (fwd_fold; ``x`` = this BN's input), else (y, None)."""
-        return (x, self.xf) if self.folded else (self.y, None)
 
     def bwd_stats_args(self, x, act=ops.ACT_RELU):
         """(x, y, mean, invstd, gamma, beta, stats, act) of this BN's backward statistics, for the
@@ -543,18 +506,11 @@ class Bottleneck:
                 res, res_bn = self.bns.stats_only(zs), self.bns
             else:
                 res = self.bns.fwd(zs, act=ops.ACT_NONE)
-        # bn1 / bn2 (+ ReLU) feed only conv2 / conv3 (forward and weight gradient): on the GPU their
-        # applies are folded into those convs' operand loads (BN.fwd_fold, _FOLD_BN_APPLY)
-        fold = x.is_cuda and not self.bn1.infer and _FOLD_BN_APPLY
-        if fold and self.conv2.reads_bn_on_load():
-            h1, xf1 = self.bn1.fwd_fold(self.conv1.fwd(x, self.bn1.stats)), self.bn1.xf
-        else:
-            h1, xf1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats)), None
-        if fold and self.conv3.reads_bn_on_load():
-            h2, xf2 = self.bn2.fwd_fold(self.conv2.fwd(h1, self.bn2.stats, xf=xf1)), self.bn2.xf
-        else:
-            h2, xf2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats, xf=xf1)), None
-        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats, xf=xf2), res=res, rstride=1, res_bn=res_bn)
+        # (bn1 / bn2 formed on conv2 / conv3's operand loads instead of stored - bit-identical, 10 %
+        # slower end to end: measured in round 5 and removed, profiles/r5_resnet50_bn_fold_ab.txt)
+        h1 = self.bn1.fwd(self.conv1.fwd(x, self.bn1.stats))
+        h2 = self.bn2.fwd(self.conv2.fwd(h1, self.bn2.stats))
+        return self.bn3.fwd(self.conv3.fwd(h2, self.bn3.stats), res=res, rstride=1, res_bn=res_bn)
 
     def bwd(self, dout, dx, dout_stats_done=False, next_bn=None):
         """``next_bn``: (BN, its x) of the layer that consumes dx (the previous block's bn3): its
@@ -583,11 +539,11 @@ class Bottleneck:
                      res_bn=(self.bns, self.convs.y) if dual else None)
         ev = fork()
         done = self.conv3.dgrad(self.dc3, self.dh2, bn_bwd=self.bn2.bwd_stats_args(self.conv2.y))
-        self.conv3.wgrad(self.dc3, *self.bn2.consumer_operand(self.conv2.y), after=ev)
+        self.conv3.wgrad(self.dc3, self.bn2.y, after=ev)
         self.bn2.bwd(self.dh2, self.conv2.y, self.dc2, stats_done=done)
         ev = fork()
         done = self.conv2.dgrad(self.dc2, self.dh1, bn_bwd=self.bn1.bwd_stats_args(self.conv1.y))
-        self.conv2.wgrad(self.dc2, *self.bn1.consumer_operand(self.conv1.y), after=ev)
+        self.conv2.wgrad(self.dc2, self.bn1.y, after=ev)
         self.bn1.bwd(self.dh1, self.conv1.y, self.dc1, stats_done=done)
         ev1 = fork()
         evs = None

@@ -314,23 +314,13 @@ def _conv_geom_args(g):
     return (g["B"], g["H"], g["W"], g["C"], g["Cout"], g["OH"], g["OW"], g["KH"], g["KW"], g["stride"], g["pad"])
 
 
-def _xf_ref(x, xf):
-    """relu(x * scale + shift) per channel, rounded to x's dtype (what bn_apply would have stored)."""
-    C = x.shape[-1]
-    return torch.relu(x.float() * xf[:C].float() + xf[C:].float()).to(x.dtype)
-
-
-def conv_fwd(x, w, bias, y, argmax, g, pool=False, act=ACT_RELU, stats=None, xf=None):
+def conv_fwd(x, w, bias, y, argmax, g, pool=False, act=ACT_RELU, stats=None):
     """NHWC conv (+bias, act, optional fused 2x2 max-pool writing argmax).  ``stats`` (f32 [2][Cout],
     zeroed): also accumulate the BatchNorm statistics of y exactly as ``bn_stats`` does (the
-    implicit-GEMM path computes them from its epilogue tiles: no separate pass over y).  ``xf`` (f32
-    [2][C], from ``bn_finalize``): x is the input of a BatchNorm + ReLU and the conv reads its output
-    relu(x * scale + shift), formed on the operand load (implicit-GEMM path; padding is zero in h)."""
+    implicit-GEMM path computes them from its epilogue tiles: no separate pass over y)."""
     if y.is_cuda:
-        require().conv_fwd(x, w, bias, y, argmax, *_conv_geom_args(g), pool, act, stats, xf)
+        require().conv_fwd(x, w, bias, y, argmax, *_conv_geom_args(g), pool, act, stats)
         return y
-    if xf is not None:
-        x = _xf_ref(x, xf)
     if stats is not None:
         conv_fwd(x, w, bias, y, argmax, g, pool, act)
         bn_stats(y, stats)
@@ -540,14 +530,11 @@ def conv_dgrad(dy, wt, dx, g, pooled=None, argmax=None, relu_mask=None, accumula
     return dx
 
 
-def conv_wgrad(dz, x, dw, db, g, scale=1.0, xf=None):
-    """dW[Cout][KH][KW][C] += scale * sum dz (x) im2col(x);  db += scale * sum dz.  ``xf``: the
-    operand is relu(x * scale + shift) (see conv_fwd)."""
+def conv_wgrad(dz, x, dw, db, g, scale=1.0):
+    """dW[Cout][KH][KW][C] += scale * sum dz (x) im2col(x);  db += scale * sum dz."""
     if dw.is_cuda:
-        require().conv_wgrad(dz, x, dw, db, *_conv_geom_args(g), scale, xf)
+        require().conv_wgrad(dz, x, dw, db, *_conv_geom_args(g), scale)
         return dw
-    if xf is not None:
-        x = _xf_ref(x, xf)
     xt = x.float().view(g["B"], g["H"], g["W"], g["C"]).permute(0, 3, 1, 2)
     dzt = dz.float().view(g["B"], g["OH"], g["OW"], g["Cout"]).permute(0, 3, 1, 2)
     gw = torch.nn.grad.conv2d_weight(xt, (g["Cout"], g["C"], g["KH"], g["KW"]), dzt, stride=g["stride"],
@@ -957,31 +944,6 @@ def relu_bits(y):
 def _unbits(m, R, C):
     e = torch.arange(8, device=m.device, dtype=torch.int32)
     return ((m.reshape(R, C // 8, 1).to(torch.int32) >> e) & 1).reshape(R, C).bool()
-
-
-def bn_finalize(x, stats, gamma, beta, xf, *, mean=None, invstd=None, moving_mean=None, moving_var=None, eps=1e-3,
-                momentum=0.99):
-    """bn_apply's bookkeeping without its pass over the tensor: mean / invstd, the moving averages, and
-    xf[2][C] = (gamma * invstd, beta - mean * gamma * invstd), the per-channel transform the consumer
-    convs apply on their operand loads (conv_fwd / conv_wgrad ``xf``) - bit-identical to bn_apply(ReLU)."""
-    if x.is_cuda:
-        require().bn_finalize(x, stats, gamma, beta, mean, invstd, moving_mean, moving_var, eps, momentum, xf)
-        return xf
-    r = _rows(x)
-    R, C = r.shape
-    m, inv, var = _bn_params(stats, R, eps, r[0])
-    if mean is not None:
-        mean.copy_(m)
-    if invstd is not None:
-        invstd.copy_(inv)
-    if moving_mean is not None:
-        unb = var * R / max(R - 1, 1)
-        moving_mean.mul_(momentum).add_(m * (1 - momentum))
-        moving_var.mul_(momentum).add_(unb * (1 - momentum))
-    sc = gamma.float() * inv
-    xf[:C].copy_(sc)
-    xf[C:].copy_(beta.float() - m * sc)
-    return xf
 
 
 def bn_infer(x, gamma, beta, moving_mean, moving_var, out, *, eps=1e-3, act=ACT_RELU, res=None, rstride=1):

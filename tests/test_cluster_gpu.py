@@ -149,3 +149,42 @@ def test_ps_replies_bitwise_across_data_plane_variants():
     for v, r in zip(variants[1:], recs[1:]):
         assert r["ps_verify"] == recs[0]["ps_verify"], (v, r["ps_verify"], recs[0]["ps_verify"])
     assert len(set(recs[0]["ps_verify"])) == len(recs[0]["ps_verify"])  # the parameters do move
+
+
+def test_ps_replies_bitwise_two_partitioned_ps():
+    """2 ps tasks with the fc1 weight in 4 partitions dealt over both (--ps_partition_mb 4): after every
+    exchange the worker's pulled copies equal both shards' variables bit for bit (partitions compared
+    through the worker's alias views), and the fused-reply / snapshot / announced-bucket data-plane
+    variants give the same pulled parameters step by step.  (The partitioned model trains the same
+    function as the unpartitioned one but its applies split into different launches, so only
+    variants of the partitioned layout are compared with each other.)"""
+    part = ["--num_ps", "2", "--ps_partition_mb", "4"]
+    variants = [part, part + ["--ps_overlap", "on"], part + ["--ps_fused_reply", "off"]]
+    recs = [_ps_verify(v) for v in variants]
+    for v, r in zip(variants, recs):
+        assert r["n_mismatch"] == 0, (v, r["mismatches"])
+    for v, r in zip(variants[1:], recs[1:]):
+        assert r["ps_verify"] == recs[0]["ps_verify"], (v, r["ps_verify"], recs[0]["ps_verify"])
+    assert len(set(recs[0]["ps_verify"])) == len(recs[0]["ps_verify"])
+
+
+def test_bench_ps_two_partitioned_ps():
+    """bench.py --mode ps --num_ps 2 --ps_partition_mb 4: 2 ps + 2 workers (all sharing cuda:0 here;
+    ps k sits on GPU k * ndev / 2 on a node), each ps holding half the fc1 partitions - every push
+    applied once on each shard, the params split near evenly."""
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--mode", "ps", "--gpus", "2", "--steps", "20",
+           "--warmup", "3", "--batch_size", "256", "--num_ps", "2", "--ps_partition_mb", "4"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    rec = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    c = rec["config"]
+    assert c["num_ps"] == 2 and c["parallelism"] == "ps2+w2" and rec["value"] > 0
+    n = 23 + c["prewarm"]["steps"]
+    shards = c["ps_shards"]
+    assert [s_["applies"] for s_ in shards] == [2 * n, 2 * n]
+    big = max(s_["params"] for s_ in shards)
+    assert big < 0.6 * sum(s_["params"] for s_ in shards)  # fc1 split, not on one ps

@@ -421,123 +421,6 @@ def test_resnet50_projection_bn_from_bits_matches(monkeypatch):
     assert cross <= 4 * noise + 1e-6 * float(grads[0].abs().max()), (cross, noise)
 
 
-XF_CASES = [
-    (2, 56, 64, 64, 3, 1),      # the all-taps 3x3 weight-gradient kernel (igemm_wgrad3)
-    (2, 14, 256, 256, 3, 1),
-    (2, 28, 128, 128, 3, 2),    # strided: out-of-image taps on the bottom / right edge
-    (3, 7, 512, 2048, 1, 1),    # M = 147: rows past the end of the last tile
-    (2, 14, 256, 1024, 1, 1),
-]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", XF_CASES)
-def test_conv_bn_on_load_matches_materialised_gpu(case):
-    """bn_finalize + conv_fwd / conv_wgrad(xf=...) - the BatchNorm + ReLU formed on the implicit-GEMM
-    operand loads - against bn_apply's stored output fed to the same convs: the saved statistics and
-    moving averages, the conv output and the weight gradient are bit-identical, the output's BN
-    statistics equal up to the statistics pass's atomics (zero padding of h, not of x, at the border)."""
-    from dtfe import ops
-    B, H, C, CO, K, s = case
-    pad = (K - 1) // 2
-    OH = (H + 2 * pad - K) // s + 1
-    g = dict(B=B, H=H, W=H, C=C, Cout=CO, OH=OH, OW=OH, KH=K, KW=K, stride=s, pad=pad)
-    dev = torch.device("cuda", 0)
-    torch.manual_seed(1)
-    x = (torch.randn(B, H, H, C, device=dev) * 1.5 + 0.3).to(torch.bfloat16)
-    w = (torch.randn(CO, K, K, C, device=dev) / (K * K * C) ** 0.5).to(torch.bfloat16)
-    dy = torch.randn(B, OH, OH, CO, device=dev).to(torch.bfloat16)
-    gamma, beta = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.5
-    stats = torch.zeros(2 * C, device=dev)
-    ops.bn_stats(x, stats)
-    outs = []
-    for fold in (False, True):
-        mean, inv = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
-        mm, mv = torch.full((C,), 0.1, device=dev), torch.full((C,), 2.0, device=dev)
-        xf = torch.empty(2 * C, device=dev)
-        if fold:
-            ops.bn_finalize(x, stats, gamma, beta, xf, mean=mean, invstd=inv, moving_mean=mm, moving_var=mv)
-            src, kw = x, dict(xf=xf)
-        else:
-            h = torch.empty_like(x)
-            ops.bn_apply(x, stats, gamma, beta, h, mean=mean, invstd=inv, moving_mean=mm, moving_var=mv)
-            src, kw = h, {}
-        y = torch.empty(B, OH, OH, CO, dtype=torch.bfloat16, device=dev)
-        yst = torch.zeros(2 * CO, device=dev)
-        ops.conv_fwd(src, w, None, y, None, g, act=ops.ACT_NONE, stats=yst, **kw)
-        dw = torch.zeros(CO, K, K, C, device=dev)
-        ops.conv_wgrad(dy, src, dw, None, g, **kw)
-        torch.cuda.synchronize()
-        outs.append((mean, inv, mm, mv, y, yst, dw))
-    names = ("mean", "invstd", "moving_mean", "moving_var", "y", "y_stats", "dw")
-    for n, a, b in zip(names, outs[0], outs[1]):
-        if n == "y_stats":  # (a split-K launch takes the separate statistics pass: per-channel atomics)
-            assert torch.allclose(a, b, rtol=1e-5, atol=1e-3), (n, float((a - b).abs().max()))
-        else:
-            assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
-
-
-@pytest.mark.gpu
-def test_resnet50_folded_bn_applies_match(monkeypatch):
-    """ResNet-50 step with bn1 / bn2 folded into conv2 / conv3's operand loads (default) against the
-    materialised applies: the same gradients up to the run-to-run order of the BN statistics'
-    atomics (measured between two runs of the materialised path)."""
-    from dtfe.models import resnet as rn
-
-    model = ResNetModel(arch="resnet50")
-    torch.manual_seed(0)
-    B = 2
-    x = torch.rand(B, 224, 224, 3).cuda()
-    y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,)), 1000).float().cuda()
-    grads, losses = [], []
-    for flag in (False, False, True):
-        monkeypatch.setattr(rn, "_FOLD_BN_APPLY", flag)
-        prog = model.program("cuda", B, seed=1)
-        prog.load_batch((x, y))
-        m = prog.compute_grads()
-        torch.cuda.synchronize()
-        grads.append(prog.P.grad.clone())
-        losses.append(float(prog.loss.item()))
-        folded = sum(1 for b in prog.L["blocks"] for bn in (b.bn1, b.bn2) if bn.folded)
-        assert folded == (32 if flag else 0)
-    noise = float((grads[0] - grads[1]).abs().max())
-    cross = float((grads[0] - grads[2]).abs().max())
-    assert cross <= 4 * noise + 1e-6 * float(grads[0].abs().max()), (cross, noise)
-    # (the batch-2 loss swings ~1 % between identical runs - BN statistics' atomics through 50
-    # layers: a single noise sample under-estimates it, hence the 1 % floor)
-    lnoise = abs(losses[1] - losses[0])
-    assert abs(losses[2] - losses[0]) <= 4 * lnoise + 1e-2 * abs(losses[0]), losses
-
-
-def test_bn_finalize_and_xf_reference_cpu():
-    """CPU reference of the folded apply: bn_finalize's (scale, shift) fed to conv_fwd / conv_wgrad(xf)
-    equals bn_apply(ReLU) fed to the plain convs (fp32 tensors: the same math up to rounding)."""
-    from dtfe import ops
-    B, H, C, CO, K = 2, 6, 8, 4, 3
-    g = dict(B=B, H=H, W=H, C=C, Cout=CO, OH=H, OW=H, KH=K, KW=K, stride=1, pad=1)
-    torch.manual_seed(3)
-    x = torch.randn(B, H, H, C) + 0.2
-    w = torch.randn(CO, K, K, C) * 0.3
-    dy = torch.randn(B, H, H, CO)
-    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.5
-    st = torch.zeros(2 * C)
-    ops.bn_stats(x, st)
-    m1, i1, m2, i2 = torch.zeros(C), torch.zeros(C), torch.zeros(C), torch.zeros(C)
-    h = torch.empty_like(x)
-    ops.bn_apply(x, st, gamma, beta, h, mean=m1, invstd=i1)
-    xf = torch.empty(2 * C)
-    ops.bn_finalize(x, st, gamma, beta, xf, mean=m2, invstd=i2)
-    assert torch.allclose(m1, m2) and torch.allclose(i1, i2)
-    y1, y2 = torch.empty(B, H, H, CO), torch.empty(B, H, H, CO)
-    ops.conv_fwd(h, w, None, y1, None, g, act=ops.ACT_NONE)
-    ops.conv_fwd(x, w, None, y2, None, g, act=ops.ACT_NONE, xf=xf)
-    assert torch.allclose(y1, y2, atol=1e-5)
-    d1, d2 = torch.zeros(CO, K, K, C), torch.zeros(CO, K, K, C)
-    ops.conv_wgrad(dy, h, d1, None, g)
-    ops.conv_wgrad(dy, x, d2, None, g, xf=xf)
-    assert torch.allclose(d1, d2, atol=1e-4)
-
-
 @pytest.mark.gpu
 def test_resnet20_bn_src_fold_matches_materialised_gpu(monkeypatch):
     """ResNet-20 at the bench batch with bn1's apply formed by conv2's whole-image kernels (BN.src_fold)
