@@ -419,5 +419,18 @@ __device__ __forceinline__ void tile_coords(int bid, int tiles_m, int tiles_n, i
 __device__ __forceinline__ void tile_coords(int tiles_m, int tiles_n, int& tm, int& tn) {
   tile_coords(blockIdx.x, tiles_m, tiles_n, tm, tn);
 }
+// The same with the tiles grouped GM m-tiles high, m fastest inside a group: the consecutive ids one
+// XCD gets (xcd_remap) form a GM x (its share / GM) block, so its L2 serves every A panel and every
+// B panel of the block to several workgroups (the row-major order above gives each XCD ~2 A panels
+// and up to all of the B panels)
+template <int GM>
+__device__ __forceinline__ void tile_coords_grouped(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int id = xcd_remap(bid, tiles_m * tiles_n);
+  const int gsz = GM * tiles_n, grp = id / gsz, first = grp * GM;
+  const int gm = tiles_m - first < GM ? tiles_m - first : GM;
+  const int r = id - grp * gsz;
+  tm = first + r % gm;
+  tn = r / gm;
+}
 
 }  // namespace dtfe

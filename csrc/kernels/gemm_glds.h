@@ -123,7 +123,7 @@ __device__ __forceinline__ void gemm_glds_body(const DenseGemmArgs& a, int bid, 
 
   const int tiles_m = a.M / BM, tiles_n = (a.N + BN - 1) / BN;
   int tm, tn;
-  tile_coords(bid, tiles_m, tiles_n, tm, tn);
+  tile_coords_grouped<4>(bid, tiles_m, tiles_n, tm, tn);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
   const int m_base = tm * BM, n_base = tn * BN;
