@@ -19,6 +19,7 @@
 #include "imgconv.h"
 
 #include <stdexcept>
+#include <type_traits>
 
 namespace dtfe {
 
@@ -34,6 +35,15 @@ constexpr int XCH = HI * HI / 4;         // 8-byte chunks of an image (196)
 
 __device__ __forceinline__ u32x4_t ld16l(const bf16* p) { return *reinterpret_cast<const u32x4_t*>(p); }
 
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for_c1(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for_c1<B + 1, E>(f);
+  }
+}
+
 // image b -> P interior (8-byte chunks: 4 pixels of one row; rows are 56 B)
 __device__ __forceinline__ void load_img(const bf16* x, long b, u32x2_t& v) {
   if (threadIdx.x < XCH) v = *reinterpret_cast<const u32x2_t*>(x + b * (HI * HI) + threadIdx.x * 4);
@@ -45,16 +55,37 @@ __device__ __forceinline__ void write_img(bf16* P, const u32x2_t& v) {
   }
 }
 
-// copies s < S (rows 0..31, 32 columns each = 4 chunks of 8)
+// copies s < S (rows 0..31, 32 columns each = 4 chunks of 8).  Thread (r, c8, half) reads the three
+// aligned 16-B chunks P[r][c8 .. c8+23] once and forms its copies' 8-element windows (first element
+// s + 2) with dword funnel shifts (v_alignbyte) - an earlier form gathered every element with its own
+// ds_read_u16 (8 LDS reads + 8 VALU per chunk, bank conflicts: rocprof PMC r6pmc2)
+__device__ __forceinline__ uint32_t shr16(uint32_t lo, uint32_t hi) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> 16);
+}
 template <int S>
 __device__ __forceinline__ void build_copies(const bf16* P, bf16* C) {
-  for (int q = threadIdx.x; q < S * PRW * 4; q += TH) {
-    const int s = q / (PRW * 4), rem = q - s * PRW * 4, r = rem >> 2, c8 = (rem & 3) * 8;
-    const unsigned short* src = reinterpret_cast<const unsigned short*>(P + r * PWD + c8 + s + 2);
-    u32x4_t v;
+  constexpr int HALF = (S + 1) / 2;  // copies per thread: threads 0..127 take s < HALF, 128..255 the rest
+  const int t = threadIdx.x & 127, r = t >> 2, c8 = (t & 3) * 8;
+  const u32x4_t* src = reinterpret_cast<const u32x4_t*>(P + r * PWD + c8);
+  uint32_t d[12];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) v[w] = (uint32_t)src[2 * w] | ((uint32_t)src[2 * w + 1] << 16);
-    *reinterpret_cast<u32x4_t*>(C + s * CSZ + r * CWD + c8) = v;
+  for (int j = 0; j < 3; ++j) {
+    const u32x4_t v = src[j];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[4 * j + e] = v[e];
+  }
+  auto emit = [&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    constexpr int e0 = s + 2;
+    u32x4_t o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (e0 & 1) ? shr16(d[(e0 >> 1) + j], d[(e0 >> 1) + j + 1]) : d[(e0 >> 1) + j];
+    *reinterpret_cast<u32x4_t*>(C + s * CSZ + r * CWD + c8) = o;
+  };
+  if (threadIdx.x < 128) {
+    static_for_c1<0, HALF>(emit);
+  } else {
+    static_for_c1<HALF, S>(emit);
   }
 }
 
@@ -190,7 +221,12 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float dbacc[2] = {0.f, 0.f};
+  // bias gradient: the same A fragments against a B of ones (every column = sum over the row's pixels)
+  // - one MFMA per n-tile and row instead of 16 VALU per fragment
+  f32x4_t dbacc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
 
   // pooled dY chunks: 14*14 windows x 4 chunks of 8 channels = 784 per image
   constexpr int PCH = 14 * 14 * (NCH / 8);
@@ -221,7 +257,10 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const int oy = 2 * py + (qq >> 1), ox = 2 * px + (qq & 1);
-        *reinterpret_cast<u32x4_t*>(D + (oy * 32 + ox) * DP + c8) = v[qq];
+        // the 32-B channel half of pixel ox is swapped when bit 3 of ox is set: a transposed read's
+        // 8 pixels (ox, ox+1, .., ox+3, ox+8, .., ox+11) then cover all 64 banks (64-B pixel pitch
+        // put ox and ox+8 on the same banks: 2-way conflicts, r6pmc2)
+        *reinterpret_cast<u32x4_t*>(D + (oy * 32 + ox) * DP + (c8 ^ (((ox >> 3) & 1) << 4))) = v[qq];
       }
     }
   };
@@ -240,15 +279,12 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
       bf16x8_t af[2];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const bf16* base = D + oy * 32 * DP + nt * 16;
+        const bf16* base = D + oy * 32 * DP + ((nt ^ (g & 1)) * 16);  // (pixel bit 3 = g: write_dy's swap)
         const s16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + aoff[0]));
         const s16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + aoff[1]));
         const s16x8_t v = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
         af[nt] = __builtin_bit_cast(bf16x8_t, v);
-        float sum = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sum += bf2f((bf16)v[e]);
-        dbacc[nt] += sum;
+        dbacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nt], ones, dbacc[nt], 0, 0, 0);
       }
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -260,7 +296,7 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
     __syncthreads();
   }
   if (diag & 8) {  // ablation: keep the loads live without the flush
-    if (a.ws && acc[0][0][0] == 12345.f) a.ws[blockIdx.x] = dbacc[0];
+    if (a.ws && acc[0][0][0] == 12345.f) a.ws[blockIdx.x] = dbacc[0][0];
     return;
   }
   // cross-wave reduction in LDS: every wave stores its own partial (no LDS float atomics), the
@@ -273,12 +309,10 @@ __global__ __launch_bounds__(TH) void conv1c_wgrad_kernel(ImgWgradArgs a, int di
 #pragma unroll
       for (int j = 0; j < 4; ++j) mine[(nt * 16 + g * 4 + j) * 32 + tt * 16 + i16] = acc[nt][tt][j];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    float v = dbacc[nt];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lane < 16) mine[32 * 32 + nt * 16 + lane] = v;
-  }
+  for (int nt = 0; nt < 2; ++nt)  // column 0 of the ones product: rows 4g..4g+3 of n-tile nt
+    if (i16 == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mine[32 * 32 + nt * 16 + g * 4 + j] = dbacc[nt][j];
   __syncthreads();
   // flush: dW[n][tap] (tap < 25) and db[n]; one partial per workgroup (summed by the reduce
   // kernel) or, without a workspace, scaled atomics

@@ -24,7 +24,7 @@ __all__ = [
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
-    "TILE_DIMS", "FC_TILE", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
+    "TILE_DIMS", "FC_TILE", "FC_TILE_RING", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
     "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard",
@@ -39,9 +39,10 @@ TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)
              14: (64, 64), 15: (64, 64), 16: (64, 64),  # 4 / 6 / 8 stages (long-K grids, ~1 WG per CU)
              17: (128, 64), 18: (128, 64),              # 4 / 6 stages
              19: (64, 64), 20: (64, 64), 21: (64, 64),  # 2 / 4 / 2 in-workgroup k-groups (3 / 2 / 4 stages)
-             22: (256, 128)}  # 8-wave fc tile (gemm_fc.hip): M % 256, N any (clamped last tile), 3 stages
-FC_TILE = 22
-GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22)
+             22: (256, 128),  # 8-wave fc tile (gemm_fc.hip): M % 256, N any (clamped last tile), 3 stages
+             23: (256, 128)}  # the same tile as a warp-specialized ring (4 loader + 4 MFMA waves, 6 slots)
+FC_TILE, FC_TILE_RING = 22, 23
+GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23)
 TILE_SMALL = 13
 _ONES = {}
 
@@ -62,7 +63,7 @@ def glds_ok(A, B, M, N, K, tile, lda, ldb, b_ones_row=-1, a_ones_row=-1, bmode=K
         return False
     if lda % 8 or ldb % 8 or A.data_ptr() % 16 or B.data_ptr() % 16:
         return False
-    if tile == FC_TILE:  # mirror of gemm_fc_eligible (csrc/kernels/gemm_fc.hip)
+    if tile in (FC_TILE, FC_TILE_RING):  # mirror of gemm_fc_eligible (csrc/kernels/gemm_fc.hip)
         valid = b_ones_row if b_ones_row >= 0 else N
         if b_ones_row >= 0 and (b_ones_row != N - 1 or b_ones_row % 8):
             return False
