@@ -160,6 +160,7 @@ struct IpcComm {
   int* err = nullptr;
   double timeout_s = 30.0;
   int max_blocks = dtfe::IPC_MAXB;  // grid cap (ipc_set_max_blocks; identical on every rank)
+  long cap_upto = -1;               // ... applied to launches of at most this many bytes (-1: all)
 };
 std::vector<IpcComm*> g_ipc;
 
@@ -230,11 +231,13 @@ void ipc_open(int64_t h, const Tensor& handles) {
 
 int64_t ipc_capacity(int64_t h) { return ipc_of(h)->cap; }
 
-// workgroup cap of every launch of this comm (1..IPC_MAXB): fewer workgroups hold fewer CUs while
-// they wait for the peers (bench/ipc_interference.py); must be the same on every rank
-void ipc_set_max_blocks(int64_t h, int64_t n) {
+// workgroup cap of the launches of this comm of at most `upto_bytes` (-1: every launch; 1..IPC_MAXB):
+// fewer workgroups hold fewer CUs while they wait for the peers (bench/ipc_interference.py); larger
+// buffers keep the full grid.  Must be the same on every rank.
+void ipc_set_max_blocks(int64_t h, int64_t n, int64_t upto_bytes) {
   TORCH_CHECK(n >= 1 && n <= dtfe::IPC_MAXB, "dtfe: ipc max_blocks must be 1..", dtfe::IPC_MAXB);
   ipc_of(h)->max_blocks = (int)n;
+  ipc_of(h)->cap_upto = (long)upto_bytes;
 }
 
 void ipc_all_reduce(Tensor buf, int64_t h) {
@@ -261,7 +264,8 @@ void ipc_all_reduce(Tensor buf, int64_t h) {
   // the block count must be identical on every rank: a function of (n, world) only
   const long seg_vec = (bytes / 16 + c->world - 1) / c->world;
   long blocks = (seg_vec + 2 * dtfe::IPC_THREADS - 1) / (2 * dtfe::IPC_THREADS);
-  a.blocks = (int)std::max(1L, std::min((long)c->max_blocks, blocks));
+  const long cap = c->cap_upto < 0 || bytes <= c->cap_upto ? c->max_blocks : dtfe::IPC_MAXB;
+  a.blocks = (int)std::max(1L, std::min(cap, blocks));
   dtfe::launch_ipc_allreduce(a, buf.scalar_type() == at::kBFloat16 ? 0 : 1,
                              at::hip::getCurrentHIPStream().stream());
 }
@@ -301,7 +305,7 @@ TORCH_LIBRARY_FRAGMENT(dtfe, m) {
   m.def("ipc_handle(int comm) -> Tensor", &ipc_handle);
   m.def("ipc_open(int comm, Tensor handles) -> ()", &ipc_open);
   m.def("ipc_capacity(int comm) -> int", &ipc_capacity);
-  m.def("ipc_set_max_blocks(int comm, int n) -> ()", &ipc_set_max_blocks);
+  m.def("ipc_set_max_blocks(int comm, int n, int upto_bytes=-1) -> ()", &ipc_set_max_blocks);
   m.def("ipc_all_reduce(Tensor(a!) buf, int comm) -> ()", &ipc_all_reduce);
   m.def("ipc_status(int comm) -> int", &ipc_status);
   m.def("ipc_destroy(int comm) -> ()", &ipc_destroy);

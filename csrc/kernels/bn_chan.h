@@ -19,6 +19,14 @@ __device__ __forceinline__ void bn_chan_params(const bf16* x, const float* stats
   invstd = rsqrtf(var + eps);
 }
 
+// Partial statistics (K_t, s_t = sum (y - K_t), q_t = sum (y - K_t)^2) over n_t rows moved to the
+// shift K and added to (S, Q):  s = s_t + n_t d,  q = q_t + 2 d s_t + n_t d^2  with d = K_t - K
+__device__ __forceinline__ void bn_shift_fold(float Kt, float st, float qt, float nt, float K, float& S, float& Q) {
+  const float d = Kt - K;
+  S += st + nt * d;
+  Q += qt + 2.f * d * st + nt * d * d;
+}
+
 // saved statistics + moving averages of one channel (TF: unbiased batch variance)
 __device__ __forceinline__ void bn_save_chan(long R, float eps, float momentum, int c, float mean, float invstd,
                                              float* smean, float* sinv, float* mm, float* mv) {

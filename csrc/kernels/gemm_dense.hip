@@ -20,12 +20,12 @@ static void launch_one(int splits, const DenseGemmArgs& args, hipStream_t s) {
 }
 
 int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
-  static const int dims[24][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
+  static const int dims[23][2] = {{64, 64}, {128, 128}, {128, 64}, {64, 128}, {32, 32},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64},
                                   {128, 128}, {128, 64}, {64, 128}, {64, 64}, {16, 16},
                                   {64, 64}, {64, 64}, {64, 64}, {128, 64}, {128, 64},
-                                  {64, 64}, {64, 64}, {64, 64}, {FC_BM, FC_BN}, {FC_BM, FC_BN}};
-  if (tile < 0 || tile > FC_TILE_RING) return -1;
+                                  {64, 64}, {64, 64}, {64, 64}, {FC_BM, FC_BN}};
+  if (tile < 0 || tile > FC_TILE) return -1;
   bm = dims[tile][0];
   bn = dims[tile][1];
   if (tile == GEMM_TILE_SMALL) return 16;
@@ -33,7 +33,7 @@ int gemm_dense_tile_dims(int tile, int& bm, int& bn) {
 }
 
 bool gemm_glds_eligible(int dtype, int amode, int bmode, int tile, const DenseGemmArgs& a) {
-  if (tile == FC_TILE || tile == FC_TILE_RING) return gemm_fc_eligible(dtype, amode, bmode, a);
+  if (tile == FC_TILE) return gemm_fc_eligible(dtype, amode, bmode, a);
   int bm = 0, bn = 0;
   if (tile < 5 || gemm_dense_tile_dims(tile, bm, bn) < 0) return false;
   if (dtype != 0 || a.a_ones_row >= 0 || a.K % GL_BK || a.k_chunk % GL_BK || a.M % bm) return false;
@@ -114,13 +114,12 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
     launch_gemm_small(amode, bmode, args, stream);
     return;
   }
-  if ((tile == 12 || tile == FC_TILE || tile == FC_TILE_RING) && splits == 1 && dtype == 0 &&
-      glds_group_record(amode, bmode, tile, args))
+  if ((tile == 12 || tile == FC_TILE) && splits == 1 && dtype == 0 && glds_group_record(amode, bmode, tile, args))
     return;  // inside a group
-  if (tile == FC_TILE || tile == FC_TILE_RING) {
+  if (tile == FC_TILE) {
     if (!gemm_fc_eligible(dtype, amode, bmode, args))
-      throw std::runtime_error("gemm_dense: this GEMM is not eligible for tiles 22 / 23 (gemm_fc_eligible)");
-    launch_gemm_fc(amode, bmode, splits, args, stream, tile == FC_TILE_RING);
+      throw std::runtime_error("gemm_dense: this GEMM is not eligible for tile 22 (gemm_fc_eligible)");
+    launch_gemm_fc(amode, bmode, splits, args, stream);
     return;
   }
   if (tile >= 5) {
@@ -223,8 +222,8 @@ void glds_group_end(hipStream_t s) {
     for (int i = 0; i < r.ng; ++i) launch_gemm_dense(0, r.am[i], r.bm[i], r.tile, 1, r.g[i], s);
     return;
   }
-  if (r.tile == FC_TILE || r.tile == FC_TILE_RING) {
-    launch_gemm_fc_group(r.g[0], r.g[1], r.has_h ? &r.h : nullptr, s, r.tile == FC_TILE_RING);
+  if (r.tile == FC_TILE) {
+    launch_gemm_fc_group(r.g[0], r.g[1], r.has_h ? &r.h : nullptr, s);
     return;
   }
   GlGroupArgs ga;

@@ -15,15 +15,13 @@
 namespace dtfe {
 
 constexpr int FC_TILE = 22;
-constexpr int FC_TILE_RING = 23;  // the same tile as a warp-specialized ring (4 loader + 4 MFMA waves)
 constexpr int FC_BM = 256, FC_BN = 128, FC_THREADS = 512;
 
 // whether tile 22 can run this GEMM (bf16, M % 256 == 0, K % 64 == 0, 16 B aligned operands; a
 // KMAJ B operand needs whole n-tiles)
 bool gemm_fc_eligible(int dtype, int amode, int bmode, const DenseGemmArgs& a);
-void launch_gemm_fc(int amode, int bmode, int splits, const DenseGemmArgs& a, hipStream_t s, bool ring = false);
+void launch_gemm_fc(int amode, int bmode, int splits, const DenseGemmArgs& a, hipStream_t s);
 // the grouped fc backward: head weight gradient (optional) + a (KMAJ, RMAJ) and a (RMAJ, RMAJ) GEMM
-void launch_gemm_fc_group(const DenseGemmArgs& g0, const DenseGemmArgs& g1, const HeadWgradArgs* h, hipStream_t s,
-                          bool ring = false);
+void launch_gemm_fc_group(const DenseGemmArgs& g0, const DenseGemmArgs& g1, const HeadWgradArgs* h, hipStream_t s);
 
 }  // namespace dtfe

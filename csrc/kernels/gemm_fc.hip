@@ -189,200 +189,6 @@ __global__ __launch_bounds__(FC_THREADS, 1) void gemm_fc_kernel(DenseGemmArgs a)
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Tile 23: the same 256 x 128 tile as a warp-specialized ring (MI355X_MICROARCH.md "ring-gemm"):
-// waves 4-7 only load (global_load_lds into a 6-slot ring of 32-deep k-steps, 3 k-steps in flight per
-// loader wave, FULL counter per slot after the wave's own counted vmcnt), waves 0-3 only read
-// fragments and multiply (64 x 128 per wave, 4 x 8 accumulators; FREE counter per slot once its
-// fragments are in registers).  No workgroup barrier inside the k-loop: the loaders stream as fast as
-// free slots allow instead of re-synchronising with the MFMA waves every k-tile (tile 22 moves
-// ~27 GB/s per CU, profiles/r6_fc1_tile22.txt).
-constexpr int RK = 32, RNS = 6, RD = 3;              // k-step depth, ring slots, k-steps in flight
-constexpr int RA_EL = FC_BM * RK, RB_EL = FC_BN * RK, RSLOT_EL = RA_EL + RB_EL;
-constexpr int RSTAGING_BYTES = RNS * RSLOT_EL * 2;   // 144 KB
-constexpr int RSMEM_BYTES = (RSTAGING_BYTES > CTILE_BYTES ? RSTAGING_BYTES : CTILE_BYTES) + 2 * RNS * 4;
-
-struct RingCfg {
-  static constexpr int BM = FC_BM, BN = FC_BN, WARPS_M = 4, WARPS_N = 1;
-  static constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N, TM = WM / 16, TN = WN / 16;
-  static constexpr int WAVES = 4;  // the consumer waves 0-3 hold the accumulators
-};
-
-// One operand of a ring slot (32-deep k-step): R rows, R / 16 pieces of 1 KB, R / 64 per loader wave.
-//   KMAJ: piece = 16 rows x 64 B; logical 16-B chunk c of row r in slot c ^ ((r >> 1) & 3)
-//         (conflict-free ds_read_b128 fragment reads of 64-B rows)
-//   RMAJ: [32 k][R] image, chunk c of k-row k at c ^ rswz(k) (as the 64-deep images)
-template <int R, int MODE>
-struct RingOperand {
-  static constexpr int NP = R / 64;
-  const bf16* src[NP];
-  long kstep[NP];
-
-  __device__ __forceinline__ void init(const bf16* p, long ld, int r0, int valid, int ones_col, const bf16* ones,
-                                       int lw, int lane) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int piece = j * 4 + lw;
-      if constexpr (MODE == KMAJ) {
-        const int row = piece * 16 + (lane >> 2);
-        const int lchunk = (lane & 3) ^ ((row >> 1) & 3);
-        src[j] = p + (long)(r0 + row) * ld + lchunk * 8;
-        kstep[j] = RK;
-      } else {
-        constexpr int CPR = R / 8, RPP = 64 / CPR;
-        const int krow = piece * RPP + lane / CPR;
-        const int chunk = (lane % CPR) ^ rswz(krow);
-        int col = r0 + chunk * 8;
-        if (col == ones_col) {
-          src[j] = ones;
-          kstep[j] = 0;
-          continue;
-        }
-        if (col + 8 > valid) col = valid - 8;
-        src[j] = p + (long)krow * ld + col;
-        kstep[j] = (long)RK * ld;
-      }
-    }
-  }
-  __device__ __forceinline__ void issue(int kt, bf16* img, int lw) const {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(img + (j * 4 + lw) * 512));
-      asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src[j] + kt * kstep[j]), "{m0}"(l) : "memory");
-    }
-  }
-  __device__ __forceinline__ bf16x8_t frag(const bf16* img, int rbase, int lane) const {
-    if constexpr (MODE == KMAJ) {
-      const int row = rbase + (lane & 15);
-      const int pc = (lane >> 4) ^ ((row >> 1) & 3);
-      return *reinterpret_cast<const bf16x8_t*>(img + row * RK + pc * 8);
-    } else {
-      const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-      const int c = rbase + 4 * p;
-      const int k0 = 8 * g + q, k1 = k0 + 4;
-      const bf16* p0 = img + k0 * R + (c ^ (rswz(k0) * 8));
-      const bf16* p1 = img + k1 * R + (c ^ (rswz(k1) * 8));
-      s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p0));
-      s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p1));
-      s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      return __builtin_bit_cast(bf16x8_t, v);
-    }
-  }
-};
-
-// spin on an LDS counter (bounded: a broken hand-off ends the kernel with wrong numbers instead of
-// hanging the GPU; `err` records it)
-__device__ __forceinline__ void ring_wait(const int* f, int target, int* err) {
-  int spins = 0;
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1 << 22)) {
-      *err = 1;
-      break;
-    }
-  }
-}
-
-template <int AMODE, int BMODE>
-__device__ __forceinline__ void fcr_body(const DenseGemmArgs& a, int bid, char* smem_raw) {
-  using OA = RingOperand<FC_BM, AMODE>;
-  using OB = RingOperand<FC_BN, BMODE>;
-  constexpr int NPL = OA::NP + OB::NP;  // DMA instructions per loader wave and k-step (6)
-  bf16* smem = reinterpret_cast<bf16*>(smem_raw);
-  int* fullc = reinterpret_cast<int*>(smem_raw + (RSMEM_BYTES - 2 * RNS * 4));
-  int* freec = fullc + RNS;
-  __shared__ int ring_err;
-  const int tiles_m = a.M / FC_BM, tiles_n = (a.N + FC_BN - 1) / FC_BN;
-  const int id = xcd_remap(bid, tiles_m * tiles_n);
-  const int tm = id % tiles_m, tn = id / tiles_m;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int m_base = tm * FC_BM, n_base = tn * FC_BN;
-  const int kt0 = blockIdx.z * (a.k_chunk / RK);
-  const int nk = min(a.K, (int)(blockIdx.z + 1) * a.k_chunk) / RK - kt0;
-  if (threadIdx.x < 2 * RNS) fullc[threadIdx.x] = 0;
-  if (threadIdx.x == 0) ring_err = 0;
-  __syncthreads();
-
-  f32x4_t acc[RingCfg::TM][RingCfg::TN];
-#pragma unroll
-  for (int i = 0; i < RingCfg::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < RingCfg::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  if (w >= 4) {
-    // ---- loaders
-    const int lw = w - 4;
-    const int b_valid = a.b_ones_row >= 0 ? a.b_ones_row : a.N;
-    OA oa;
-    OB ob;
-    oa.init((const bf16*)a.A + (AMODE == KMAJ ? (long)kt0 * RK : (long)kt0 * RK * a.lda), a.lda, m_base, a.M, -1,
-            a.ones, lw, lane);
-    ob.init((const bf16*)a.B + (BMODE == KMAJ ? (long)kt0 * RK : (long)kt0 * RK * a.ldb), a.ldb, n_base, b_valid,
-            a.b_ones_row, a.ones, lw, lane);
-    for (int t = 0; t < nk; ++t) {
-      const int sl = t % RNS;
-      if (t >= RNS) ring_wait(freec + sl, 4 * (t / RNS), &ring_err);  // every consumer read round t/RNS-1
-      bf16* img = smem + sl * RSLOT_EL;
-      oa.issue(t, img, lw);
-      ob.issue(t, img + RA_EL, lw);
-      if (t >= RD) {  // k-step t - RD landed (this wave's pieces): publish it
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RD * NPL) : "memory");
-        if (lane == 0) __hip_atomic_fetch_add(fullc + (t - RD) % RNS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    // drain: publish the last min(nk, RD) k-steps, oldest first
-#pragma unroll
-    for (int i = 0; i < RD; ++i) {
-      const int t = nk - RD + i;
-      if (t < 0) continue;
-      if (i == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * NPL) : "memory");
-      else if (i == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 2) * NPL) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(fullc + t % RNS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    // ---- consumers: wave w owns rows w*64 .. +64, all 128 columns
-    OA oa;
-    OB ob;
-    for (int t = 0; t < nk; ++t) {
-      const int sl = t % RNS;
-      ring_wait(fullc + sl, 4 * (t / RNS + 1), &ring_err);
-      const bf16* As = smem + sl * RSLOT_EL;
-      const bf16* Bs = As + RA_EL;
-      bf16x8_t af[RingCfg::TM], bfr[RingCfg::TN];
-#pragma unroll
-      for (int i = 0; i < RingCfg::TM; ++i) af[i] = oa.frag(As, w * RingCfg::WM + i * 16, lane);
-#pragma unroll
-      for (int j = 0; j < RingCfg::TN; ++j) bfr[j] = ob.frag(Bs, j * 16, lane);
-      // the fragments are in registers: release the slot (LDS ops of a wave complete in order)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(freec + sl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int i = 0; i < RingCfg::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < RingCfg::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  __syncthreads();  // ring drained, every fragment read: the epilogue reuses the staging LDS
-  if (ring_err && threadIdx.x == 0 && a.tile_ctr == nullptr) {
-    // (a hand-off timed out: poison the tile so no test can pass on it)
-#pragma unroll
-    for (int i = 0; i < RingCfg::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < RingCfg::TN; ++j) acc[i][j] = f32x4_t{__builtin_nanf(""), 0.f, 0.f, 0.f};
-  }
-  dense_epilogue<RingCfg, FC_THREADS>(a, smem_raw, acc, tm, tn, tiles_m, tiles_n);
-}
-
-template <int AMODE, int BMODE>
-__global__ __launch_bounds__(FC_THREADS, 1) void gemm_fcr_kernel(DenseGemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem_raw[RSMEM_BYTES];
-  fcr_body<AMODE, BMODE>(a, blockIdx.x, smem_raw);
-}
-
 // Head weight gradient, one WAVE per 4 columns of dW (piece p: columns 4p..4p+3; p == K / 4: the
 // bias), the whole batch streamed by the wave's 64 lanes - 40 accumulators, no cross-wave reduce.
 // The bias piece also folds head_xent's loss / hit partials (it must run on wave 0: head_fold_parts).
@@ -458,9 +264,9 @@ struct FcGroupArgs {
   int ph, t0, t1;     // head pieces (waves), real GEMM tiles
 };
 
-template <bool HEAD, bool RING>
+template <bool HEAD>
 __global__ __launch_bounds__(FC_THREADS, 1) void gemm_fc_group_kernel(FcGroupArgs ga) {
-  __shared__ __attribute__((aligned(16))) char smem_raw[RING ? RSMEM_BYTES : SMEM_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM_BYTES];
   int bid = blockIdx.x;
   if constexpr (HEAD) {
     if (bid < ga.nh) {
@@ -471,17 +277,11 @@ __global__ __launch_bounds__(FC_THREADS, 1) void gemm_fc_group_kernel(FcGroupArg
     bid -= ga.nh;
   }
   if (bid < ga.n0) {
-    if (bid < ga.t0) {
-      if constexpr (RING) fcr_body<KMAJ, RMAJ>(ga.g0, bid, smem_raw);
-      else fc_body<KMAJ, RMAJ>(ga.g0, bid, smem_raw);
-    }
+    if (bid < ga.t0) fc_body<KMAJ, RMAJ>(ga.g0, bid, smem_raw);
     return;
   }
   bid -= ga.n0;
-  if (bid < ga.t1) {
-    if constexpr (RING) fcr_body<RMAJ, RMAJ>(ga.g1, bid, smem_raw);
-    else fc_body<RMAJ, RMAJ>(ga.g1, bid, smem_raw);
-  }
+  if (bid < ga.t1) fc_body<RMAJ, RMAJ>(ga.g1, bid, smem_raw);
 }
 
 int tiles_of(const DenseGemmArgs& a) { return (a.M / FC_BM) * ((a.N + FC_BN - 1) / FC_BN); }
@@ -503,26 +303,18 @@ bool gemm_fc_eligible(int dtype, int amode, int bmode, const DenseGemmArgs& a) {
   return true;
 }
 
-void launch_gemm_fc(int amode, int bmode, int splits, const DenseGemmArgs& a, hipStream_t s, bool ring) {
+void launch_gemm_fc(int amode, int bmode, int splits, const DenseGemmArgs& a, hipStream_t s) {
   if (splits < 1) splits = 1;
   if (splits > 1 && !a.atomic && (!a.ws || !a.tile_ctr))
     throw std::runtime_error("gemm_fc: split-K with a fused epilogue needs a workspace");
   dim3 grid(tiles_of(a), 1, splits);
-  if (ring) {
-    if (amode == KMAJ && bmode == KMAJ) hipLaunchKernelGGL((gemm_fcr_kernel<KMAJ, KMAJ>), grid, dim3(FC_THREADS), 0, s, a);
-    else if (amode == KMAJ && bmode == RMAJ) hipLaunchKernelGGL((gemm_fcr_kernel<KMAJ, RMAJ>), grid, dim3(FC_THREADS), 0, s, a);
-    else if (amode == RMAJ && bmode == KMAJ) hipLaunchKernelGGL((gemm_fcr_kernel<RMAJ, KMAJ>), grid, dim3(FC_THREADS), 0, s, a);
-    else hipLaunchKernelGGL((gemm_fcr_kernel<RMAJ, RMAJ>), grid, dim3(FC_THREADS), 0, s, a);
-    return;
-  }
   if (amode == KMAJ && bmode == KMAJ) hipLaunchKernelGGL((gemm_fc_kernel<KMAJ, KMAJ>), grid, dim3(FC_THREADS), 0, s, a);
   else if (amode == KMAJ && bmode == RMAJ) hipLaunchKernelGGL((gemm_fc_kernel<KMAJ, RMAJ>), grid, dim3(FC_THREADS), 0, s, a);
   else if (amode == RMAJ && bmode == KMAJ) hipLaunchKernelGGL((gemm_fc_kernel<RMAJ, KMAJ>), grid, dim3(FC_THREADS), 0, s, a);
   else hipLaunchKernelGGL((gemm_fc_kernel<RMAJ, RMAJ>), grid, dim3(FC_THREADS), 0, s, a);
 }
 
-void launch_gemm_fc_group(const DenseGemmArgs& g0, const DenseGemmArgs& g1, const HeadWgradArgs* h, hipStream_t s,
-                          bool ring) {
+void launch_gemm_fc_group(const DenseGemmArgs& g0, const DenseGemmArgs& g1, const HeadWgradArgs* h, hipStream_t s) {
   FcGroupArgs ga;
   std::memset(&ga, 0, sizeof(ga));
   ga.g0 = g0;
@@ -535,11 +327,9 @@ void launch_gemm_fc_group(const DenseGemmArgs& g0, const DenseGemmArgs& g1, cons
     ga.h = *h;
     ga.ph = h->K / 4 + (h->db ? 1 : 0);
     ga.nh = pad8((ga.ph + NWAVE - 1) / NWAVE);
-    if (ring) hipLaunchKernelGGL((gemm_fc_group_kernel<true, true>), dim3(ga.nh + ga.n0 + ga.n1), dim3(FC_THREADS), 0, s, ga);
-    else hipLaunchKernelGGL((gemm_fc_group_kernel<true, false>), dim3(ga.nh + ga.n0 + ga.n1), dim3(FC_THREADS), 0, s, ga);
+    hipLaunchKernelGGL((gemm_fc_group_kernel<true>), dim3(ga.nh + ga.n0 + ga.n1), dim3(FC_THREADS), 0, s, ga);
   } else {
-    if (ring) hipLaunchKernelGGL((gemm_fc_group_kernel<false, true>), dim3(ga.n0 + ga.n1), dim3(FC_THREADS), 0, s, ga);
-    else hipLaunchKernelGGL((gemm_fc_group_kernel<false, false>), dim3(ga.n0 + ga.n1), dim3(FC_THREADS), 0, s, ga);
+    hipLaunchKernelGGL((gemm_fc_group_kernel<false>), dim3(ga.n0 + ga.n1), dim3(FC_THREADS), 0, s, ga);
   }
 }
 

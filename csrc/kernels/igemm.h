@@ -62,6 +62,9 @@ struct IgWgradArgs {
 // value into stats[2][N], as bn_stats would.  bn_part_buffer: the device scratch for `tiles`
 // tiles plus the fold's chunk table (valid until the next call on this device).
 float* bn_part_buffer(long tiles, int N, hipStream_t s);
+// a zeroed hand-off counter beside a bn_part_buffer (not one the fold launches use); whoever takes
+// it leaves it zero again (last-arriver reset)
+uint32_t* bn_part_counter(const float* part);
 void launch_bn_part_reduce(float* part, int tiles, int N, long Mp, int BMr, float* stats, hipStream_t s);
 
 // true when the igemm path handles the conv (and launches it)

@@ -19,6 +19,7 @@
 // Replaces Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter of the ResNet-50
 // configuration (BASELINE.json config 5).
 #include "igemm.h"
+#include "bn_chan.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -747,9 +748,7 @@ void launch_wgrad_splits_reduce(const float* ws, int splits, long len, float* dw
 constexpr int BN_TCH = 64;
 
 __device__ __forceinline__ void shift_fold(float Kt, float st, float qt, float nt, float K, float& S, float& Q) {
-  const float d = Kt - K;
-  S += st + nt * d;
-  Q += qt + 2.f * d * st + nt * d * d;
+  bn_shift_fold(Kt, st, qt, nt, K, S, Q);
 }
 
 // Both stages in ONE launch (grid (ceil(N/64), P)): block (g, p) folds tiles [64p, 64p+64) of channel
@@ -1041,6 +1040,8 @@ bool run_igemm(IgemmArgs& a, hipStream_t s, float* bn_stats = nullptr) {
 }
 
 }  // namespace
+
+uint32_t* bn_part_counter(const float* part) { return bn_counters(part) + (BN_CTR_BYTES / 4 - 1); }
 
 float* bn_part_buffer(long tiles, int N, hipStream_t s) {
   const long nchunk = (tiles + BN_TCH - 1) / BN_TCH;

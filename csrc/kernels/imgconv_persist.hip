@@ -28,6 +28,7 @@
 // once.  With flip_taps (data gradient) the taps are flipped while staging the
 // weights, so the inner loop is the same for fwd and dgrad.
 #include "imgconv.h"
+#include "igemm.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -99,6 +100,81 @@ __host__ __device__ inline bool row_pixel(int m, int OH, int OW, int blocked, in
   oy = m / OW;
   ox = m % OW;
   return true;
+}
+
+// Output BatchNorm statistics of the persistent forward (ImgConvArgs.ostats).  Thread t owns the
+// 8 channels of chunk t % (N/8) of every pixel it stored and summed (sk: its workgroup's shift =
+// the first image's pixel 0).  Block reduce through LDS (`red`, the weight region: the k-loops are
+// over), one (K, s, q) row per workgroup in opart (write-through stores), then the last workgroup
+// to take a ticket folds the rows in workgroup order (the result does not depend on the arrival
+// order) onto row 0's value and adds them to ostats[2][N].  Same hand-off as igemm's bn_part_fold.
+template <int THREADS>
+__device__ __attribute__((noinline)) void out_stats_fold(const ImgConvArgs& a, int M, float* red, const float (&sk)[8],
+                                                         const float (&ss)[8], const float (&sq)[8]) {
+  __shared__ int last_flag;
+  const int N = a.N, CPN = N >> 3, tid = threadIdx.x, cc = tid % CPN, slot = tid / CPN;
+  const int SL = THREADS / CPN;
+  // LDS floats: [SL][2][N] partials (16 THREADS), red2 [<= 2 THREADS], kred [N] (persist_ostat_lds)
+  float* red2 = red + 16 * THREADS;
+  float* kred = red2 + 2 * THREADS;  // [N] shifts (slot 0)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[slot * 2 * N + cc * 8 + e] = ss[e];
+    red[slot * 2 * N + N + cc * 8 + e] = sq[e];
+  }
+  if (slot == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) kred[cc * 8 + e] = sk[e];
+  }
+  __syncthreads();
+  // L = THREADS / 2N threads per output column fold SL / L slots each
+  const int O = 2 * N, L = THREADS / O;
+  {
+    const int o = tid % O, j = tid / O;
+    float v = 0.f;
+    for (int r = j; r < SL; r += L) v += red[r * O + o];
+    red2[j * O + o] = v;
+  }
+  __syncthreads();
+  float* part = a.opart + (long)blockIdx.x * 3 * N;
+  if (tid < O) {
+    float v = 0.f;
+    for (int j = 0; j < L; ++j) v += red2[j * O + tid];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 3 * N * 4, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (N + tid) * 4, 0, 16);
+    if (tid < N) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(kred[tid]), rs, tid * 4, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.octr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == gridDim.x - 1;
+    if (last) {
+      __hip_atomic_store(a.octr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    last_flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  // fold the G workgroup rows: L3 threads per channel, rows j, j + L3, ... (fixed order)
+  const int G = gridDim.x, L3 = THREADS / N;
+  const int c = tid % N, j = tid / N;
+  float S = 0.f, Q = 0.f;
+  const float K = a.opart[c];
+  for (int p = j; p < G; p += L3) {
+    const float* pp = a.opart + (long)p * 3 * N;
+    const float nt = (float)((a.B - p + G - 1) / G) * (float)M;
+    bn_shift_fold(pp[c], pp[N + c], pp[2 * N + c], nt, K, S, Q);
+  }
+  red2[j * O + c] = S;
+  red2[j * O + N + c] = Q;
+  __syncthreads();
+  if (tid < O) {
+    float v = 0.f;
+    for (int jj = 0; jj < L3; ++jj) v += red2[jj * O + tid];
+    a.ostats[tid] += v;
+  }
 }
 
 // CSC != 0: a 3x3 conv over CSC source channels (ResNet-20) with the k walk in closed form - step s's
@@ -238,6 +314,10 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   const int toff0 = (kh0 * LWP + kw0) * PS + cs0;
   const int wrap_jump = PS - CS, row_jump = (LWP - a.KW) * PS;
   const bf16* wlane = wl + (wn * NT * 16 + (lane & 15)) * G.KP + 8 * g;
+
+  // output statistics (a.ostats, forward only - the host never combines it with relu_mask / sc_src)
+  const bool ostat = a.ostats != nullptr && G.stage_out && !(a.diag & 1);
+  float sk[8] = {}, ss[8] = {}, sq[8] = {};
 
   long b = blockIdx.x;
   if (b < a.B && !(a.diag & 2)) load_src(b);
@@ -390,8 +470,27 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
       const bf16* sy = img + G.LH * LWP * PS + G.slack;
       const int nch = M * a.N / 8;
       const long ob = b * (long)M * a.N;
+      if (ostat && b == blockIdx.x) {  // the workgroup's shift: its first image's pixel 0
+        const u32x4_t k8 = *reinterpret_cast<const u32x4_t*>(sy + (tid % (a.N >> 3)) * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sk[2 * e] = __uint_as_float(k8[e] << 16);
+          sk[2 * e + 1] = __uint_as_float(k8[e] & 0xffff0000u);
+        }
+      }
       for (int i = tid; i < nch; i += THREADS) {
         u32x4_t v = *reinterpret_cast<const u32x4_t*>(sy + i * 8);
+        if (ostat) {  // the stored (bf16) values, as bn_stats reads them back
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = __uint_as_float(v[e] << 16) - sk[2 * e];
+            const float hi = __uint_as_float(v[e] & 0xffff0000u) - sk[2 * e + 1];
+            ss[2 * e] += lo;
+            sq[2 * e] += lo * lo;
+            ss[2 * e + 1] += hi;
+            sq[2 * e + 1] += hi * hi;
+          }
+        }
         if (a.relu_mask) {
           const u32x4_t m = *reinterpret_cast<const u32x4_t*>(a.relu_mask + ob + i * 8);
 #pragma unroll
@@ -422,6 +521,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
     __syncthreads();  // image b fully consumed before the next write
   }
   stamp(6);
+  if (ostat) out_stats_fold<THREADS>(a, M, reinterpret_cast<float*>(lds), sk, ss, sq);
 }
 
 // ----------------------------------------------------- compile-time geometry
@@ -762,7 +862,7 @@ size_t persist_lds(const PGeom& G) {
 }
 
 template <int NT, int RT, int WM, int WN, bool POOLED>
-bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
+bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done, bool* st_done) {
   constexpr int THREADS = 64 * WM * WN;
   PGeom G = persist_geom(a, WN, NT, THREADS);
   size_t lds = persist_lds(G);
@@ -778,6 +878,20 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   ImgConvArgs ad = a;
   ad.diag = diag;
   if (!sc) ad.sc_src = nullptr;
+  // output statistics in the staged epilogue (out_stats_fold's LDS: 18 THREADS + N floats)
+  const size_t st_lds = (18 * (size_t)THREADS + 64) * sizeof(float);
+  const bool st = a.ostats && G.stage_out && !a.relu_mask && !ad.sc_src && !a.bias && a.N >= 16 && a.N <= 64 &&
+                  THREADS % (a.N / 8) == 0 && std::max(lds, st_lds) <= 160 * 1024;
+  ad.ostats = nullptr;
+  ad.opart = nullptr;
+  ad.octr = nullptr;
+  if (st) {
+    lds = std::max(lds, st_lds);
+    ad.ostats = a.ostats;
+    ad.opart = bn_part_buffer(grid, a.N, s);
+    ad.octr = bn_part_counter(ad.opart);
+  }
+  if (st_done) *st_done = st;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(THREADS), lds, s, ad, G);
@@ -862,8 +976,9 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
   }
 }
 
-bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
+bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done, bool* st_done) {
   if (sc_done) *sc_done = false;
+  if (st_done) *st_done = false;
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
   if (a.OH == 14 && a.OW == 14 && a.B >= 256 && !a.bns.stats) {
     // compile-time geometry, one 16-row tile per wave (13 waves); 2 / 4 tiles per wave (7 / 4
@@ -882,14 +997,14 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_don
   // 4 x 2 (48 / 74) and 4 x 1 waves holding every n-tile (fewer LDS reads, but one wave per SIMD
   // exposes the read latency: fwd 48 vs 63 us); the alternatives were removed in round 3
   if (a.N <= 16 && !(diag_bits("icr") & 32))  // one n-tile: a second wave column would only compute padding
-    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s, sc_done) : launch_cfg<1, 2, 16, 1, false>(a, s, sc_done);
-  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<1, 2, 8, 2, false>(a, s, sc_done);
+    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s, sc_done, st_done) : launch_cfg<1, 2, 16, 1, false>(a, s, sc_done, st_done);
+  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s, sc_done, st_done) : launch_cfg<1, 2, 8, 2, false>(a, s, sc_done, st_done);
   // small maps (<= 4 row tiles: ResNet-20 stage 3, 8x8): 4 x 2 waves of one tile x 2 n-tiles each -
   // the 8 x 2 grid left half its waves idle and computed a padding tile in the rest (s3 conv 8.98 ->
   // 8.27 us, step -6 us; DTFE_DIAG icr=128 -> the 8 x 2 grid, profiles/r5_resnet20_kernels.txt)
   if (a.OH * a.OW <= 64 && !pooled && a.N <= 64 && !(diag_bits("icr") & 128))
-    return launch_cfg<2, 1, 4, 2, false>(a, s, sc_done);
-  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<2, 2, 8, 2, false>(a, s, sc_done);
+    return launch_cfg<2, 1, 4, 2, false>(a, s, sc_done, st_done);
+  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s, sc_done, st_done) : launch_cfg<2, 2, 8, 2, false>(a, s, sc_done, st_done);
 }
 
 }  // namespace dtfe

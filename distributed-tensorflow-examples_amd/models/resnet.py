@@ -140,12 +140,13 @@ class Conv:
         ``bn_src``: the preceding BatchNorm + ReLU (BN.src_fold) for the whole-image kernel, which
         forms it while staging the raw input x and saves the BN's statistics / moving averages."""
         if self.img_fwd:
+            st = stats if _OUT_STATS and self.y.is_cuda else None
             if bn_src is not None:
-                ops.imgconv(self.w, self.y, src=x, bn_src=bn_src.src_args(), bn_eps=BN_EPS, bn_momentum=BN_MOMENTUM,
-                            bn_save=True, **self.ic)
-                return self.y, False
-            ops.imgconv(self.w, self.y, src=x, **self.ic)
-            return self.y, False
+                done = ops.imgconv(self.w, self.y, src=x, bn_src=bn_src.src_args(), bn_eps=BN_EPS,
+                                   bn_momentum=BN_MOMENTUM, bn_save=True, stats=st, **self.ic)
+                return self.y, st is not None and done
+            done = ops.imgconv(self.w, self.y, src=x, stats=st, **self.ic)
+            return self.y, st is not None and done
         assert bn_src is None
         ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats)
         return self.y, stats is not None
@@ -252,6 +253,9 @@ _R20_SRC_FOLD = True
 _HEAD_FUSE = True
 # ResNet-20 weight-gradient reduces deferred to grouped launches (ops.wgrad_flush)
 _WGRAD_DEFER = True
+# the whole-image forward convs accumulate their BatchNorm's statistics in the staged epilogue
+# (ops.imgconv(stats=...)): no bn_stats pass over y
+_OUT_STATS = True
 
 
 class BN:

@@ -24,7 +24,7 @@ __all__ = [
     "gather_rows", "uniform_fill", "cast_", "softmax_xent", "gan_loss", "mse_sigmoid", "colsum", "act_grad",
     "bias_act", "ACT_NONE", "ACT_RELU", "ACT_SIGMOID", "ACT_TANH", "ACT_CODES", "KMAJ", "RMAJ", "OPT_SGD",
     "OPT_MOMENTUM", "OPT_ADAM", "OPT_RMSPROP", "available", "load", "require", "pick_tile", "split_workspace",
-    "TILE_DIMS", "FC_TILE", "FC_TILE_RING", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
+    "TILE_DIMS", "FC_TILE", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
     "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard",
@@ -39,10 +39,9 @@ TILE_DIMS = {0: (64, 64), 1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (32, 32)
              14: (64, 64), 15: (64, 64), 16: (64, 64),  # 4 / 6 / 8 stages (long-K grids, ~1 WG per CU)
              17: (128, 64), 18: (128, 64),              # 4 / 6 stages
              19: (64, 64), 20: (64, 64), 21: (64, 64),  # 2 / 4 / 2 in-workgroup k-groups (3 / 2 / 4 stages)
-             22: (256, 128),  # 8-wave fc tile (gemm_fc.hip): M % 256, N any (clamped last tile), 3 stages
-             23: (256, 128)}  # the same tile as a warp-specialized ring (4 loader + 4 MFMA waves, 6 slots)
-FC_TILE, FC_TILE_RING = 22, 23
-GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23)
+             22: (256, 128)}  # 8-wave fc tile (gemm_fc.hip): M % 256, N any (clamped last tile), 3 stages
+FC_TILE = 22
+GLDS_TILES = (5, 6, 7, 8, 9, 10, 11, 12, 14, 15, 16, 17, 18, 19, 20, 21, 22)
 TILE_SMALL = 13
 _ONES = {}
 
@@ -63,7 +62,7 @@ def glds_ok(A, B, M, N, K, tile, lda, ldb, b_ones_row=-1, a_ones_row=-1, bmode=K
         return False
     if lda % 8 or ldb % 8 or A.data_ptr() % 16 or B.data_ptr() % 16:
         return False
-    if tile in (FC_TILE, FC_TILE_RING):  # mirror of gemm_fc_eligible (csrc/kernels/gemm_fc.hip)
+    if tile == FC_TILE:  # mirror of gemm_fc_eligible (csrc/kernels/gemm_fc.hip)
         valid = b_ones_row if b_ones_row >= 0 else N
         if b_ones_row >= 0 and (b_ones_row != N - 1 or b_ones_row % 8):
             return False
@@ -369,16 +368,26 @@ def _bn_src_ref(src, bn_src, eps, momentum, save):
 
 def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None, src_pooled=None,
             src_argmax=None, bias=None, argmax=None, relu_mask=None, flip_taps=False, act=ACT_NONE, pool=False,
-            dil=1, bn_src=None, bn_eps=1e-3, bn_momentum=0.99, bn_save=False):
+            dil=1, bn_src=None, bn_eps=1e-3, bn_momentum=0.99, bn_save=False, stats=None):
     """Whole-image LDS convolution (small feature maps): forward (+bias/act/pool) or, with
     flip_taps and pad = K-1-pad, the data gradient of a stride-1 conv (w = Wt [cin][tap][cout]).
     The source may be un-pooled on load from (src_pooled, src_argmax), or dilated (``dil``: source
-    pixel (y, x) at (y*dil, x*dil), zeros between - the data gradient of a stride-``dil`` conv)."""
+    pixel (y, x) at (y*dil, x*dil), zeros between - the data gradient of a stride-``dil`` conv).
+    ``stats`` (f32 [2][N], zeroed; plain forward): also accumulate the BatchNorm statistics of y as
+    ``bn_stats`` does where the launch can (the persistent kernel's staged epilogue, one fixed-order
+    fold - no pass over y); then returns True, else False (the caller runs bn_stats).  Without
+    ``stats`` it returns y."""
     if y.is_cuda:
-        require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW, N, KH,
-                          KW, stride, pad, flip_taps, act, pool, dil, bn_src=bn_src, bn_eps=bn_eps,
-                          bn_momentum=bn_momentum, bn_save=bn_save)
-        return y
+        done = require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW,
+                                 N, KH, KW, stride, pad, flip_taps, act, pool, dil, bn_src=bn_src, bn_eps=bn_eps,
+                                 bn_momentum=bn_momentum, bn_save=bn_save, out_stats=stats)
+        return bool(done) if stats is not None else y
+    if stats is not None:
+        imgconv(w, y, B=B, SH=SH, SW=SW, CS=CS, OH=OH, OW=OW, N=N, KH=KH, KW=KW, stride=stride, pad=pad, src=src,
+                src_pooled=src_pooled, src_argmax=src_argmax, bias=bias, act=act, dil=dil, bn_src=bn_src,
+                bn_eps=bn_eps, bn_momentum=bn_momentum, bn_save=bn_save)
+        bn_stats(y, stats)
+        return True
     if bn_src is not None:  # BN + ReLU formed on the source (the kernel does it while staging)
         src = _bn_src_ref(src, bn_src, bn_eps, bn_momentum, bn_save)
     s = src.float().view(B, SH, SW, CS) if src is not None else _unpooled_nhwc(src_pooled, src_argmax, B, SH, SW, CS)

@@ -27,8 +27,12 @@ from .. import ops
 # two ranks on ONE GPU (profiles/r5_ipc_grid_cap.txt): conv+all-reduce span 128 -> 217 / 205 us,
 # 64 -> 214 / 181, 32 -> 229 / 237, 16 -> 175 / 175 (all-reduce alone 125 -> 150 us).  16 is the span
 # minimum there.  On a node each GPU hosts one rank and reads its 7 peers over xGMI, whose per-link
-# rate - not the workgroup count - bounds a 16-workgroup launch; that part is unmeasured here.
+# rate - not the workgroup count - bounds a 16-workgroup launch; that part is unmeasured here, so
+# the cap applies only to buffers up to DEFAULT_CAP_UPTO (the CNN's 6.5 MB fc bucket and smaller,
+# the ones that overlap a short backward); larger ones (ResNet-50's 16 MB buckets) keep the
+# kernel's full 128-workgroup grid.
 DEFAULT_MAX_BLOCKS = 16
+DEFAULT_CAP_UPTO = 8 << 20
 
 
 class IpcComm:
@@ -49,7 +53,7 @@ class IpcComm:
             self.handle = lib.ipc_create(int(cap_bytes), self.rank, self.world, self.device.index or 0,
                                          float(timeout_s))
             self.cap = lib.ipc_capacity(self.handle)
-            lib.ipc_set_max_blocks(self.handle, int(max_blocks or DEFAULT_MAX_BLOCKS))
+            lib.ipc_set_max_blocks(self.handle, int(max_blocks or DEFAULT_MAX_BLOCKS), DEFAULT_CAP_UPTO)
             mine = lib.ipc_handle(self.handle).numpy().tobytes()
         except Exception as e:  # noqa: BLE001
             err = e
@@ -81,9 +85,10 @@ class IpcComm:
             self.close()
             raise RuntimeError("IpcComm %s failed on %s: %s" % (what, "this rank" if err else "a peer rank", err))
 
-    def set_max_blocks(self, n: int):
-        """Grid cap of the following launches (the same value on every rank)."""
-        torch.ops.dtfe.ipc_set_max_blocks(self.handle, int(n))
+    def set_max_blocks(self, n: int, upto_bytes: int = -1):
+        """Grid cap of the following launches of at most `upto_bytes` (-1: all; the same values on
+        every rank)."""
+        torch.ops.dtfe.ipc_set_max_blocks(self.handle, int(n), int(upto_bytes))
 
     def fits(self, t: torch.Tensor) -> bool:
         return t.numel() * t.element_size() + 64 <= self.cap and t.dtype in (torch.bfloat16, torch.float32)

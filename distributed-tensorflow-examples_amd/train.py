@@ -527,13 +527,18 @@ def run_allreduce(flags, model, device, log, world=1, rank=0, group=None, store=
 def _leave_watchdog(store, rank, world, timeout_s):
     """End of training with the comm watchdog on: the TCPStore lives in rank 0's process, so rank 0
     waits (bounded) until every rank has stopped its watchdog before it can exit - a peer still
-    polling would otherwise read the vanished store as a failure."""
+    polling would otherwise read the vanished store as a failure.
+    The counter is never reset: a store reused by a later run (tests, an in-process rerun) keeps
+    counting, and each rank's own ticket tells which run it belongs to - every rank adds exactly
+    once per run and a run cannot start before all ranks left the previous one - so rank 0 waits
+    for the end of ITS run's group of `world` tickets."""
     key = "dtfe/hb/watchdogs_stopped"
-    store.add(key, 1)
+    ticket = store.add(key, 1)
     if rank != 0:
         return
+    target = ((ticket - 1) // world + 1) * world
     t_end = time.time() + timeout_s
-    while store.add(key, 0) < world and time.time() < t_end:
+    while store.add(key, 0) < target and time.time() < t_end:
         time.sleep(0.01)
 
 

@@ -94,6 +94,7 @@ def test_glds_fc1_dgrad_and_wgrad():
 def test_fc_tile22_layouts(modes, N, splits):
     """tile 22 (8-wave 256x128, gemm_fc.hip): every layout, a partial last n-tile (RMAJ B: sources
     clamped inside the row, outputs past N never stored), split-K with the last-arriver epilogue."""
+    tile = ops.FC_TILE
     am, bm = modes
     M, K = 512, 640
     g = torch.Generator(device="cuda").manual_seed(N + am * 2 + bm)
@@ -101,12 +102,12 @@ def test_fc_tile22_layouts(modes, N, splits):
          torch.randn(K, M, device="cuda", generator=g)).to(bf)
     B = (torch.randn(N, K, device="cuda", generator=g) if bm == ops.KMAJ else
          torch.randn(K, N, device="cuda", generator=g)).to(bf)
-    eligible = ops.glds_ok(A, B, M, N, K, ops.FC_TILE, K if am == 0 else M, K if bm == 0 else N, bmode=bm)
+    eligible = ops.glds_ok(A, B, M, N, K, tile, K if am == 0 else M, K if bm == 0 else N, bmode=bm)
     assert eligible == (bm == ops.RMAJ or N % 128 == 0)
     if not eligible:
         return
     out = torch.full((M, N + 8), 123.0, device="cuda")
-    ops.gemm(A, B, out, M=M, N=N, K=K, amode=am, bmode=bm, ldc=N + 8, tile=ops.FC_TILE, splits=splits)
+    ops.gemm(A, B, out, M=M, N=N, K=K, amode=am, bmode=bm, ldc=N + 8, tile=tile, splits=splits)
     ref = _mat(A, am, M, K) @ _mat(B, bm, N, K).t()
     err = (out[:, :N] - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-5, err

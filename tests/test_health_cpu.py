@@ -111,3 +111,27 @@ def test_beat_ages_use_the_local_clock():
     wd = Watchdog(store, [("worker", 2)], timeout=0.1)
     time.sleep(0.2)
     assert wd.poll() == []
+
+
+def test_leave_watchdog_counter_survives_store_reuse():
+    """train._leave_watchdog on a store reused by a second run: rank 0 waits for ITS run's peers
+    (the never-reset counter already holds the first run's tickets)."""
+    import threading
+    import time
+
+    import torch.distributed as dist
+
+    from dtfe.train import _leave_watchdog
+
+    store = dist.HashStore()
+    for r in (1, 0):  # run 1
+        _leave_watchdog(store, r, 2, 5.0)
+    # run 2: rank 0 arrives first and must wait for rank 1
+    t = threading.Thread(target=lambda: (time.sleep(0.5), _leave_watchdog(store, 1, 2, 5.0)))
+    t0 = time.time()
+    t.start()
+    _leave_watchdog(store, 0, 2, 5.0)
+    waited = time.time() - t0
+    t.join()
+    assert 0.4 < waited < 4.0, waited
+    assert store.add("dtfe/hb/watchdogs_stopped", 0) == 4
