@@ -50,6 +50,7 @@ struct Im2colF32 {
   using Lay = LdsLayout<float, R, KMAJ>;
   using C = Chunks<float, R, KMAJ>;
   const float* src; ConvGeom g; int rows, K, SC, SH, SW;
+  float inv_sc, inv_kw;  // (reciprocal divisions: two runtime integer divisions per chunk and k-step otherwise)
   int rb[C::NC], ry[C::NC], rx[C::NC];  // per chunk: batch (-1: out of range), tap-0 source coords
   u32x4_t regs[C::NC];
 
@@ -60,6 +61,8 @@ struct Im2colF32 {
     SW = TRANS ? g.OW : g.W;
     rows = g.B * RH * RW;
     K = g.KH * g.KW * SC;
+    inv_sc = 1.f / (float)SC;
+    inv_kw = 1.f / (float)g.KW;
 #pragma unroll
     for (int c = 0; c < C::NC; ++c) {
       int r, k;
@@ -92,7 +95,7 @@ struct Im2colF32 {
       f32x4_t v = {0.f, 0.f, 0.f, 0.f};
       if (rb[c] >= 0 && gk < K) {
         if ((SC & 3) == 0) {  // 4 channels of one tap: one 16-B load
-          const int tap = gk / SC, ch = gk - tap * SC, kh = tap / g.KW, kw = tap - kh * g.KW;
+          const int tap = fdiv(gk, SC, inv_sc), ch = gk - tap * SC, kh = fdiv(tap, g.KW, inv_kw), kw = tap - kh * g.KW;
           const int sy = TRANS ? ry[c] - kh : ry[c] + kh, sx = TRANS ? rx[c] - kw : rx[c] + kw;
           if (sy >= 0 && sy < SH && sx >= 0 && sx < SW)
             v = *reinterpret_cast<const f32x4_t*>(src + (((long)rb[c] * SH + sy) * SW + sx) * SC + ch);
@@ -108,20 +111,42 @@ struct Im2colF32 {
 };
 
 // B operand of the weight gradient (RMAJ, transposed while staging): rows = k = (kh, kw, c) of the
-// forward conv + one ones row (the bias column), reduction = output pixel m.
+// forward conv + one ones row (the bias column), reduction = output pixel m.  A thread's chunk rows
+// (4 consecutive k) are the same at every k-step (Chunks<RMAJ>: only the pixel moves), so their
+// (kh, kw, c) decomposition is done once here; a load is then two reciprocal divisions of the pixel
+// index and, when C % 4 == 0, ONE 16-B load of 4 channels of one tap (per-element loads with four
+// runtime integer divisions each had the conv2 weight gradient at ~26 TFLOP/s, 800 us per step).
 template <int R>
 struct Im2colWgradF32 {
   using Lay = LdsLayout<float, R, RMAJ>;
   using C = Chunks<float, R, RMAJ>;
-  const float* x; ConvGeom g; int Kw, Mred, r0;
+  const float* x; ConvGeom g; int Mred;
   float inv_ow, inv_oh;
+  static_assert(GEMM_THREADS % (R / 4) == 0, "a thread's chunks must share their rows");
+  int kh[4], kw[4], off[4];  // per chunk row: tap coordinates and channel offset; kh = -1: zero, -2: ones
+  bool vec;                  // the 4 rows are 4 channels of one tap (C % 4 == 0)
   u32x4_t regs[C::NC];
 
-  __device__ __forceinline__ Im2colWgradF32(const float* x_, const ConvGeom& g_, int r0_) : x(x_), g(g_), r0(r0_) {
-    Kw = g.KH * g.KW * g.C;
+  __device__ __forceinline__ Im2colWgradF32(const float* x_, const ConvGeom& g_, int r0) : x(x_), g(g_) {
+    const int Kw = g.KH * g.KW * g.C;
     Mred = g.B * g.OH * g.OW;
     inv_ow = 1.f / (float)g.OW;
     inv_oh = 1.f / (float)g.OH;
+    int r, k;
+    C::rk(threadIdx.x, r, k);  // (the same rows for every chunk of this thread)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = r0 + r + i;
+      kh[i] = kk == Kw ? -2 : -1;
+      kw[i] = off[i] = 0;
+      if (kk < Kw) {
+        const int tap = kk / g.C;
+        kh[i] = tap / g.KW;
+        kw[i] = tap - kh[i] * g.KW;
+        off[i] = kk - tap * g.C;
+      }
+    }
+    vec = (g.C & 3) == 0 && kh[0] >= 0 && kh[3] >= 0;
   }
   template <bool FAST = false>
   __device__ __forceinline__ void load(int k0) {
@@ -132,21 +157,25 @@ struct Im2colWgradF32 {
       if (C::N % GEMM_THREADS == 0 || idx < C::N) {
         int r, k;
         C::rk(idx, r, k);
-        const int m = k0 + k, gr = r0 + r;
+        const int m = k0 + k;
         if (m < Mred) {
           const int q1 = fdiv(m, g.OW, inv_ow);
           const int ox = m - q1 * g.OW;
           const int b = fdiv(q1, g.OH, inv_oh);
           const int oy = q1 - b * g.OH;
+          const int y0 = oy * g.stride - g.pad, x0 = ox * g.stride - g.pad;
+          const float* xb = x + (long)b * g.H * g.W * g.C;
+          if (vec) {
+            const int sy = y0 + kh[0], sx = x0 + kw[0];
+            if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W)
+              v = *reinterpret_cast<const f32x4_t*>(xb + ((long)sy * g.W + sx) * g.C + off[0]);
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int kk = gr + i;
-            if (kk < Kw) {
-              const int tap = kk / g.C, ch = kk - tap * g.C, kh = tap / g.KW, kw = tap - kh * g.KW;
-              const int sy = oy * g.stride - g.pad + kh, sx = ox * g.stride - g.pad + kw;
-              if (sy >= 0 && sy < g.H && sx >= 0 && sx < g.W) v[i] = x[(((long)b * g.H + sy) * g.W + sx) * g.C + ch];
-            } else if (kk == Kw) {
-              v[i] = 1.f;  // bias column
+            for (int i = 0; i < 4; ++i) {
+              const int sy = y0 + kh[i], sx = x0 + kw[i];
+              if (kh[i] == -2) v[i] = 1.f;  // bias column
+              else if (kh[i] >= 0 && sy >= 0 && sy < g.H && sx >= 0 && sx < g.W)
+                v[i] = xb[((long)sy * g.W + sx) * g.C + off[i]];
             }
           }
         }
@@ -305,11 +334,13 @@ void launch_conv_wgrad_f32(const ConvF32Args& a0, hipStream_t s) {
   using Cfg = TileCfg<float, 32, 64, 2, 2>;
   const int M = g.Cout, N = g.KH * g.KW * g.C + (a.db ? 1 : 0), Kred = g.B * g.OH * g.OW;
   const int tiles = ntiles<Cfg>(M, N);
-  // split the pixel reduction so ~512 workgroups fill the chip, at least 8 k-tiles each
-  int splits = (512 + tiles - 1) / tiles;
+  // split the pixel reduction so ~2048 workgroups (8 per CU, 2 waves per SIMD each) hide the
+  // gather latency, at least 16 k-tiles each (512 workgroups left conv2's weight gradient at 2 per
+  // CU and ~30 TFLOP/s, latency-bound)
+  int splits = (2048 + tiles - 1) / tiles;
   int chunk = (Kred + splits - 1) / splits;
   chunk = (chunk + BK - 1) / BK * BK;
-  if (chunk < 8 * BK) chunk = 8 * BK;
+  if (chunk < 16 * BK) chunk = 16 * BK;
   splits = (Kred + chunk - 1) / chunk;
   a.k_chunk = chunk;
   hipLaunchKernelGGL(conv_wgrad_f32_kernel<Cfg>, dim3(tiles, 1, splits), dim3(GEMM_THREADS), 0, s, a);

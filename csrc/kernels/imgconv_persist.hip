@@ -104,46 +104,60 @@ __host__ __device__ inline bool row_pixel(int m, int OH, int OW, int blocked, in
 
 // Output BatchNorm statistics of the persistent forward (ImgConvArgs.ostats).  Thread t owns the
 // 8 channels of chunk t % (N/8) of every pixel it stored and summed (sk: its workgroup's shift =
-// the first image's pixel 0).  Block reduce through LDS (`red`, the weight region: the k-loops are
-// over), one (K, s, q) row per workgroup in opart (write-through stores), then the last workgroup
-// to take a ticket folds the rows in workgroup order (the result does not depend on the arrival
-// order) onto row 0's value and adds them to ostats[2][N].  Same hand-off as igemm's bn_part_fold.
+// the first image's pixel 0).  Workgroup sums: butterfly over the lanes of a wave that hold the
+// same chunk, then the waves' rows through LDS; one (K, s, q) row per workgroup in opart
+// (write-through stores); the last workgroup to take a ticket folds the G rows onto row 0's value
+// (every row moved to that one shift, so the sum is a plain fixed-order tree) and adds them to
+// ostats[2][N].  Same hand-off as igemm's bn_part_fold.  Every reduction is a fixed tree: the
+// result does not depend on arrival order.  (A first version summed the thread slots with serial LDS
+// loops - 16 + 32 + 64 dependent reads - and cost the convs 10-15 us each.)
 template <int THREADS>
-__device__ __attribute__((noinline)) void out_stats_fold(const ImgConvArgs& a, int M, float* red, const float (&sk)[8],
-                                                         const float (&ss)[8], const float (&sq)[8]) {
+__device__ __forceinline__ void out_stats_fold(const ImgConvArgs& a, int M, float* red, const float (&sk)[8],
+                                               float (&ss)[8], float (&sq)[8]) {
+  constexpr int WAVES = THREADS / 64;
   __shared__ int last_flag;
-  const int N = a.N, CPN = N >> 3, tid = threadIdx.x, cc = tid % CPN, slot = tid / CPN;
-  const int SL = THREADS / CPN;
-  // LDS floats: [SL][2][N] partials (16 THREADS), red2 [<= 2 THREADS], kred [N] (persist_ostat_lds)
-  float* red2 = red + 16 * THREADS;
-  float* kred = red2 + 2 * THREADS;  // [N] shifts (slot 0)
+  const int N = a.N, CPN = N >> 3, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = lane >> 4;
+  // lanes of one 16-lane row holding the same chunk (lane % CPN) summed by DPP row rotations (ror
+  // CPN, 2 CPN, .., 8: no LDS traffic - the ds_bpermute butterfly cost the conv ~4 us), then each
+  // row's sums go to LDS and the 4 x WAVES rows are added in a fixed order
+  auto ror_add = [&](float (&v)[8], int n) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    red[slot * 2 * N + cc * 8 + e] = ss[e];
-    red[slot * 2 * N + N + cc * 8 + e] = sq[e];
+    for (int e = 0; e < 8; ++e) {
+      int r;
+      switch (n) {
+        case 2: r = __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x122, 0xF, 0xF, false); break;
+        case 4: r = __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x124, 0xF, 0xF, false); break;
+        default: r = __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x128, 0xF, 0xF, false); break;
+      }
+      v[e] += __int_as_float(r);
+    }
+  };
+  for (int n = CPN; n < 16; n <<= 1) {
+    ror_add(ss, n);
+    ror_add(sq, n);
   }
-  if (slot == 0) {
+  float* wred = red;                     // [WAVES * 4 rows][2N]
+  float* kred = red + WAVES * 4 * 128;   // [N]
+  if ((lane & 15) < CPN) {
+    const int l = lane & 15;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) kred[cc * 8 + e] = sk[e];
-  }
-  __syncthreads();
-  // L = THREADS / 2N threads per output column fold SL / L slots each
-  const int O = 2 * N, L = THREADS / O;
-  {
-    const int o = tid % O, j = tid / O;
-    float v = 0.f;
-    for (int r = j; r < SL; r += L) v += red[r * O + o];
-    red2[j * O + o] = v;
+    for (int e = 0; e < 8; ++e) {
+      wred[(w * 4 + row) * 2 * N + l * 8 + e] = ss[e];
+      wred[(w * 4 + row) * 2 * N + N + l * 8 + e] = sq[e];
+      if (w == 0 && row == 0) kred[l * 8 + e] = sk[e];
+    }
   }
   __syncthreads();
   float* part = a.opart + (long)blockIdx.x * 3 * N;
-  if (tid < O) {
+  if (tid < 2 * N) {
     float v = 0.f;
-    for (int j = 0; j < L; ++j) v += red2[j * O + tid];
+#pragma unroll
+    for (int i = 0; i < WAVES * 4; ++i) v += wred[i * 2 * N + tid];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 3 * N * 4, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (N + tid) * 4, 0, 16);
     if (tid < N) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(kred[tid]), rs, tid * 4, 0, 16);
   }
+  if (a.diag & 256) return;  // (DTFE_DIAG icr=256: no hand-off - timing ablation, wrong statistics)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -156,23 +170,42 @@ __device__ __attribute__((noinline)) void out_stats_fold(const ImgConvArgs& a, i
     last_flag = last ? 1 : 0;
   }
   __syncthreads();
-  if (!last_flag) return;
-  // fold the G workgroup rows: L3 threads per channel, rows j, j + L3, ... (fixed order)
-  const int G = gridDim.x, L3 = THREADS / N;
-  const int c = tid % N, j = tid / N;
-  float S = 0.f, Q = 0.f;
+  if (!last_flag || (a.diag & 512)) return;
+  // the last workgroup: thread (j, c) folds rows j, j + L3, ... of channel c (loads issued 8 rows at
+  // a time), lanes of one channel are combined by a butterfly, the waves through LDS
+  const int G = gridDim.x, L3 = THREADS / N, c = tid % N, j = tid / N;
   const float K = a.opart[c];
-  for (int p = j; p < G; p += L3) {
-    const float* pp = a.opart + (long)p * 3 * N;
-    const float nt = (float)((a.B - p + G - 1) / G) * (float)M;
-    bn_shift_fold(pp[c], pp[N + c], pp[2 * N + c], nt, K, S, Q);
+  float S = 0.f, Q = 0.f;
+  for (int p0 = j; p0 < G; p0 += 8 * L3) {
+    float kt[8], st[8], qt[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int p = p0 + i * L3;
+      const float* pp = a.opart + (long)(p < G ? p : 0) * 3 * N;
+      kt[i] = pp[c];
+      st[i] = pp[N + c];
+      qt[i] = pp[2 * N + c];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int p = p0 + i * L3;
+      if (p < G) bn_shift_fold(kt[i], st[i], qt[i], (float)((a.B - p + G - 1) / G) * (float)M, K, S, Q);
+    }
   }
-  red2[j * O + c] = S;
-  red2[j * O + N + c] = Q;
+  for (int off = N; off < 64; off <<= 1) {
+    S += __shfl_xor(S, off);
+    Q += __shfl_xor(Q, off);
+  }
+  __syncthreads();  // (wred reads of the workgroup row are done)
+  if (lane < N) {
+    wred[w * 2 * N + lane] = S;
+    wred[w * 2 * N + N + lane] = Q;
+  }
   __syncthreads();
-  if (tid < O) {
+  if (tid < 2 * N) {
     float v = 0.f;
-    for (int jj = 0; jj < L3; ++jj) v += red2[jj * O + tid];
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) v += wred[i * 2 * N + tid];
     a.ostats[tid] += v;
   }
 }
@@ -521,7 +554,7 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
     __syncthreads();  // image b fully consumed before the next write
   }
   stamp(6);
-  if (ostat) out_stats_fold<THREADS>(a, M, reinterpret_cast<float*>(lds), sk, ss, sq);
+  if (ostat && !(a.diag & 1024)) out_stats_fold<THREADS>(a, M, reinterpret_cast<float*>(lds), sk, ss, sq);
 }
 
 // ----------------------------------------------------- compile-time geometry
@@ -878,8 +911,8 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done, bool* st_don
   ImgConvArgs ad = a;
   ad.diag = diag;
   if (!sc) ad.sc_src = nullptr;
-  // output statistics in the staged epilogue (out_stats_fold's LDS: 18 THREADS + N floats)
-  const size_t st_lds = (18 * (size_t)THREADS + 64) * sizeof(float);
+  // output statistics in the staged epilogue (out_stats_fold's LDS: [waves][2N] + [N] floats)
+  const size_t st_lds = ((size_t)THREADS / 64 * 4 * 128 + 64) * sizeof(float);
   const bool st = a.ostats && G.stage_out && !a.relu_mask && !ad.sc_src && !a.bias && a.N >= 16 && a.N <= 64 &&
                   THREADS % (a.N / 8) == 0 && std::max(lds, st_lds) <= 160 * 1024;
   ad.ostats = nullptr;

@@ -289,6 +289,19 @@ __device__ __forceinline__ void finish_launch(const SplitSync& y) {
   }
 }
 
+// (row group, split) of this workgroup.  Workgroups are dealt to the 8 XCDs round-robin by id, so
+// with a multiple of 8 row groups the NS workgroups of one group - the ones that exchange h / dh
+// every step - get ids rg, rg + G, ... and sit on ONE XCD (its L2); otherwise consecutive ids.
+__device__ __forceinline__ void split_coords(int groups, int& rg, int& sp) {
+  if (groups % 8 == 0) {
+    rg = blockIdx.x % groups;
+    sp = blockIdx.x / groups;
+  } else {
+    rg = blockIdx.x / NS;
+    sp = blockIdx.x % NS;
+  }
+}
+
 __device__ __forceinline__ unsigned launch_base(const SplitSync& y) {
   return (unsigned)__hip_atomic_load(y.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * 256u;
 }
@@ -306,7 +319,9 @@ __global__ __launch_bounds__(SPT) void lstm_split_fwd_kernel(LstmSeqArgs a, Spli
   float* As = lds;            // [16][AP]
   float* Gs = lds + 16 * AP;  // [16][GP] activated gates of my columns (gate-major: gi * UPW + u)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rg = blockIdx.x / NS, sp = blockIdx.x % NS, r0 = rg * LR, B = a.B;
+  int rg, sp;
+  split_coords(a.B / LR, rg, sp);
+  const int r0 = rg * LR, B = a.B;
   const unsigned base = launch_base(y);
   const long rowKT = KT;
   unsigned long long* llg = y.llf + (long)rg * 2 * LR * H;
@@ -387,7 +402,9 @@ __global__ __launch_bounds__(SPT) void lstm_split_bwd_kernel(LstmSeqArgs a, Spli
   extern __shared__ float lds[];
   float* DG = lds;  // [2][16][DP] my dgates of step t (parity-double-buffered: one barrier per step)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rg = blockIdx.x / NS, sp = blockIdx.x % NS, r0 = rg * LR, B = a.B;
+  int rg, sp;
+  split_coords(a.B / LR, rg, sp);
+  const int r0 = rg * LR, B = a.B;
   const unsigned base = launch_base(y);
   unsigned long long* llg = y.llb + (long)rg * 2 * NS * LR * H;  // [2][NS src][16][H]
   const int mrow = lane & 15, g = lane >> 4;

@@ -594,3 +594,23 @@ def test_splitk_combine_many_splits_deterministic(dtype, tile):
         assert torch.equal(o, outs[0])
     err = (outs[0] - ref).abs().max().item()
     assert err < 1e-3 * ref.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("g", CONV_CASES + [_geom(2, 14, 14, 6, 16, 3, 3, 2, 1)])
+def test_conv_wgrad_fp32(g):
+    """conv_f32.hip weight + bias gradient (fp32 tensors route there) vs fp64 autograd: 16-B tap loads
+    (C % 4 == 0), per-element loads (C = 1, 6), strides, the bias column."""
+    torch.manual_seed(7)
+    x = torch.randn(g["B"], g["H"], g["W"], g["C"], device=DEV)
+    dz = torch.randn(g["B"], g["OH"], g["OW"], g["Cout"], device=DEV)
+    dw = torch.zeros(g["Cout"], g["KH"], g["KW"], g["C"], device=DEV)
+    db = torch.zeros(g["Cout"], device=DEV)
+    ops.conv_wgrad(dz, x, dw, db, g, scale=0.5)
+    xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    wd = torch.zeros(g["Cout"], g["C"], g["KH"], g["KW"], dtype=torch.float64, device=DEV, requires_grad=True)
+    y = torch.nn.functional.conv2d(xd, wd, stride=g["stride"], padding=g["pad"])
+    y.backward(dz.double().permute(0, 3, 1, 2) * 0.5)
+    ref_w = wd.grad.permute(0, 2, 3, 1)
+    ref_b = 0.5 * dz.double().sum((0, 1, 2))
+    assert ((dw.double() - ref_w).abs().max() / ref_w.abs().max()).item() < 1e-5
+    assert ((db.double() - ref_b).abs().max() / ref_b.abs().max()).item() < 1e-5
