@@ -264,8 +264,7 @@ bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
              const optional<Tensor>& relu_mask, int64_t B, int64_t SH, int64_t SW, int64_t CS, int64_t OH, int64_t OW,
              int64_t N, int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool flip_taps, int64_t act, bool pool,
              int64_t dil, const optional<Tensor>& sc_src, int64_t sc_stride, const optional<Tensor>& tstamp,
-             const optional<at::TensorList>& bn_src, double bn_eps, double bn_momentum, bool bn_save,
-             const optional<Tensor>& out_stats) {
+             const optional<at::TensorList>& bn_src, double bn_eps, double bn_momentum, bool bn_save) {
   check_cuda(w, "w");
   TORCH_CHECK((src.has_value() && src->defined()) != (src_pooled.has_value() && src_pooled->defined()),
               "imgconv: exactly one of src / src_pooled");
@@ -297,17 +296,7 @@ bool imgconv(const optional<Tensor>& src, const optional<Tensor>& src_pooled, co
     a.sc_stride = (int)sc_stride;
     a.sc_C = (int)sc_src->size(3);
   }
-  if (out_stats.has_value() && out_stats->defined()) {
-    check_cuda(*out_stats, "out_stats");
-    TORCH_CHECK(out_stats->scalar_type() == at::kFloat && out_stats->is_contiguous() && out_stats->numel() >= 2 * N,
-                "imgconv: out_stats fp32 [2][N]");
-    TORCH_CHECK(!a.sc_src && !a.relu_mask && !pool && !flip_taps, "imgconv: out_stats is for a plain forward");
-    a.ostats = out_stats->data_ptr<float>();
-  }
-  bool stats_done = false;
-  const bool sc_done = dtfe::launch_imgconv(a, cur_stream(), &stats_done);
-  // with out_stats: whether the launch produced them (else the caller runs bn_stats)
-  return a.ostats ? stats_done : sc_done;
+  return dtfe::launch_imgconv(a, cur_stream());
 }
 
 // MNIST conv1 forward with the step's batch sampling fused in (imgconv1_copies.hip): samples B rows
@@ -1086,7 +1075,7 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"
       " int stride, int pad, bool flip_taps, int act, bool pool, int dil=1, Tensor? sc_src=None,"
       " int sc_stride=1, Tensor(e!)? tstamp=None, Tensor(f!)[]? bn_src=None, float bn_eps=0.001,"
-      " float bn_momentum=0.99, bool bn_save=False, Tensor(g!)? out_stats=None) -> bool");
+      " float bn_momentum=0.99, bool bn_save=False) -> bool");
   m.def(
       "imgwgrad(Tensor src, Tensor? dy, Tensor? dy_pooled, Tensor? dy_argmax, Tensor(a!) dw, Tensor(b!)? db, int B,"
       " int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW, int stride, int pad, float scale, Tensor(c!)? ws=None,"

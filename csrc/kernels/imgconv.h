@@ -61,14 +61,6 @@ struct ImgConvArgs {
   // BatchNorm + ReLU of the source formed while staging it (persistent kernel, plain source; the
   // source is the BN's raw input).  bns.stats == nullptr: none
   BnSrc bns;
-  // BatchNorm statistics of the OUTPUT (forward, persistent kernel with the LDS-staged epilogue):
-  // each workgroup folds the values it stores into per-channel shifted sums, leaves
-  // (K, sum, sumsq) in opart[blockIdx][3][N], and the last workgroup to arrive (ticket octr) folds
-  // them in workgroup order into ostats[2][N] around y[0][0] (bn_stats' layout; no bn_stats pass).
-  // ostats == nullptr: none; the launcher reports whether it did it.
-  float* ostats;
-  float* opart;
-  uint32_t* octr;
 };
 
 // Whole-image weight gradient:  dW[n][tap][c] += sum_p dY[p][n] * src[p*stride - pad + tap][c]
@@ -106,12 +98,11 @@ int discard_wgrad_reduces();
 
 bool imgconv_supported(int SH, int SW, int CS, int N, int KH, int KW, int stride, int pad);
 // returns whether a.sc_src was added by the launch (false: the caller adds the shortcut gradient)
-bool launch_imgconv(const ImgConvArgs& a, hipStream_t s, bool* stats_done = nullptr);
+bool launch_imgconv(const ImgConvArgs& a, hipStream_t s);
 // persistent variant (weights resident in LDS, one workgroup per CU streaming images);
 // returns false when the shape does not fit it (launch_imgconv then uses the per-image kernel);
 // *sc_done: whether the shortcut gradient (a.sc_src) was added
-bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done = nullptr,
-                               bool* stats_done = nullptr);
+bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done = nullptr);
 bool imgwgrad_supported(const ImgWgradArgs& a);
 // floats of the partial-sum workspace the weight-gradient kernels need (256 workgroup slabs);
 // mirrored by ops.wgrad_ws_floats

@@ -373,8 +373,7 @@ static void launch_nt(const ImgConvArgs& a, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(k, dim3(a.B), dim3(IC_THREADS), lds, s, a);
 }
 
-bool launch_imgconv(const ImgConvArgs& a, hipStream_t s, bool* stats_done) {
-  if (stats_done) *stats_done = false;
+bool launch_imgconv(const ImgConvArgs& a, hipStream_t s) {
   if (!imgconv_supported(a.SH, a.SW, a.CS, a.N, a.KH, a.KW, a.stride, a.pad))
     throw std::runtime_error("imgconv: shape not supported");
   if (a.CS <= 4 && (!a.src || a.flip_taps || a.dil > 1))
@@ -383,7 +382,7 @@ bool launch_imgconv(const ImgConvArgs& a, hipStream_t s, bool* stats_done) {
   if (a.bns.stats && (a.CS <= 4 || !a.src)) throw std::runtime_error("imgconv: BN-on-load needs a plain source");
   if (a.CS <= 4 && launch_conv1_copies_fwd(a, s)) return false;
   bool sc_done = false;
-  if (a.CS > 4 && launch_imgconv_persistent(a, s, &sc_done, stats_done)) return sc_done;
+  if (a.CS > 4 && launch_imgconv_persistent(a, s, &sc_done)) return sc_done;
   if (a.bns.stats) throw std::runtime_error("imgconv: BN-on-load needs the persistent kernel (B >= 64)");
   if (a.dil > 1) throw std::runtime_error("imgconv: dilated sources need the persistent kernel (B >= 64)");
   const int LH = (a.OH - 1) * a.stride + a.KH, LW = (a.OW - 1) * a.stride + a.KW;

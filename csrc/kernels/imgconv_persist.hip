@@ -102,114 +102,6 @@ __host__ __device__ inline bool row_pixel(int m, int OH, int OW, int blocked, in
   return true;
 }
 
-// Output BatchNorm statistics of the persistent forward (ImgConvArgs.ostats).  Thread t owns the
-// 8 channels of chunk t % (N/8) of every pixel it stored and summed (sk: its workgroup's shift =
-// the first image's pixel 0).  Workgroup sums: butterfly over the lanes of a wave that hold the
-// same chunk, then the waves' rows through LDS; one (K, s, q) row per workgroup in opart
-// (write-through stores); the last workgroup to take a ticket folds the G rows onto row 0's value
-// (every row moved to that one shift, so the sum is a plain fixed-order tree) and adds them to
-// ostats[2][N].  Same hand-off as igemm's bn_part_fold.  Every reduction is a fixed tree: the
-// result does not depend on arrival order.  (A first version summed the thread slots with serial LDS
-// loops - 16 + 32 + 64 dependent reads - and cost the convs 10-15 us each.)
-template <int THREADS>
-__device__ __forceinline__ void out_stats_fold(const ImgConvArgs& a, int M, float* red, const float (&sk)[8],
-                                               float (&ss)[8], float (&sq)[8]) {
-  constexpr int WAVES = THREADS / 64;
-  __shared__ int last_flag;
-  const int N = a.N, CPN = N >> 3, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = lane >> 4;
-  // lanes of one 16-lane row holding the same chunk (lane % CPN) summed by DPP row rotations (ror
-  // CPN, 2 CPN, .., 8: no LDS traffic - the ds_bpermute butterfly cost the conv ~4 us), then each
-  // row's sums go to LDS and the 4 x WAVES rows are added in a fixed order
-  auto ror_add = [&](float (&v)[8], int n) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      int r;
-      switch (n) {
-        case 2: r = __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x122, 0xF, 0xF, false); break;
-        case 4: r = __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x124, 0xF, 0xF, false); break;
-        default: r = __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x128, 0xF, 0xF, false); break;
-      }
-      v[e] += __int_as_float(r);
-    }
-  };
-  for (int n = CPN; n < 16; n <<= 1) {
-    ror_add(ss, n);
-    ror_add(sq, n);
-  }
-  float* wred = red;                     // [WAVES * 4 rows][2N]
-  float* kred = red + WAVES * 4 * 128;   // [N]
-  if ((lane & 15) < CPN) {
-    const int l = lane & 15;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      wred[(w * 4 + row) * 2 * N + l * 8 + e] = ss[e];
-      wred[(w * 4 + row) * 2 * N + N + l * 8 + e] = sq[e];
-      if (w == 0 && row == 0) kred[l * 8 + e] = sk[e];
-    }
-  }
-  __syncthreads();
-  float* part = a.opart + (long)blockIdx.x * 3 * N;
-  if (tid < 2 * N) {
-    float v = 0.f;
-#pragma unroll
-    for (int i = 0; i < WAVES * 4; ++i) v += wred[i * 2 * N + tid];
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 3 * N * 4, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (N + tid) * 4, 0, 16);
-    if (tid < N) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(kred[tid]), rs, tid * 4, 0, 16);
-  }
-  if (a.diag & 256) return;  // (DTFE_DIAG icr=256: no hand-off - timing ablation, wrong statistics)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(a.octr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = prev == gridDim.x - 1;
-    if (last) {
-      __hip_atomic_store(a.octr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    last_flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  if (!last_flag || (a.diag & 512)) return;
-  // the last workgroup: thread (j, c) folds rows j, j + L3, ... of channel c (loads issued 8 rows at
-  // a time), lanes of one channel are combined by a butterfly, the waves through LDS
-  const int G = gridDim.x, L3 = THREADS / N, c = tid % N, j = tid / N;
-  const float K = a.opart[c];
-  float S = 0.f, Q = 0.f;
-  for (int p0 = j; p0 < G; p0 += 8 * L3) {
-    float kt[8], st[8], qt[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int p = p0 + i * L3;
-      const float* pp = a.opart + (long)(p < G ? p : 0) * 3 * N;
-      kt[i] = pp[c];
-      st[i] = pp[N + c];
-      qt[i] = pp[2 * N + c];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int p = p0 + i * L3;
-      if (p < G) bn_shift_fold(kt[i], st[i], qt[i], (float)((a.B - p + G - 1) / G) * (float)M, K, S, Q);
-    }
-  }
-  for (int off = N; off < 64; off <<= 1) {
-    S += __shfl_xor(S, off);
-    Q += __shfl_xor(Q, off);
-  }
-  __syncthreads();  // (wred reads of the workgroup row are done)
-  if (lane < N) {
-    wred[w * 2 * N + lane] = S;
-    wred[w * 2 * N + N + lane] = Q;
-  }
-  __syncthreads();
-  if (tid < 2 * N) {
-    float v = 0.f;
-#pragma unroll
-    for (int i = 0; i < WAVES; ++i) v += wred[i * 2 * N + tid];
-    a.ostats[tid] += v;
-  }
-}
-
 // CSC != 0: a 3x3 conv over CSC source channels (ResNet-20) with the k walk in closed form - step s's
 // A offset from k = 32 s + 8 g by divisions by compile-time constants - and the step loop unrolled
 // with its fragment reads pinned one step ahead of the MFMAs.  The runtime walk (a per-step while
@@ -347,10 +239,6 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
   const int toff0 = (kh0 * LWP + kw0) * PS + cs0;
   const int wrap_jump = PS - CS, row_jump = (LWP - a.KW) * PS;
   const bf16* wlane = wl + (wn * NT * 16 + (lane & 15)) * G.KP + 8 * g;
-
-  // output statistics (a.ostats, forward only - the host never combines it with relu_mask / sc_src)
-  const bool ostat = a.ostats != nullptr && G.stage_out && !(a.diag & 1);
-  float sk[8] = {}, ss[8] = {}, sq[8] = {};
 
   long b = blockIdx.x;
   if (b < a.B && !(a.diag & 2)) load_src(b);
@@ -503,27 +391,8 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
       const bf16* sy = img + G.LH * LWP * PS + G.slack;
       const int nch = M * a.N / 8;
       const long ob = b * (long)M * a.N;
-      if (ostat && b == blockIdx.x) {  // the workgroup's shift: its first image's pixel 0
-        const u32x4_t k8 = *reinterpret_cast<const u32x4_t*>(sy + (tid % (a.N >> 3)) * 8);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          sk[2 * e] = __uint_as_float(k8[e] << 16);
-          sk[2 * e + 1] = __uint_as_float(k8[e] & 0xffff0000u);
-        }
-      }
       for (int i = tid; i < nch; i += THREADS) {
         u32x4_t v = *reinterpret_cast<const u32x4_t*>(sy + i * 8);
-        if (ostat) {  // the stored (bf16) values, as bn_stats reads them back
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float lo = __uint_as_float(v[e] << 16) - sk[2 * e];
-            const float hi = __uint_as_float(v[e] & 0xffff0000u) - sk[2 * e + 1];
-            ss[2 * e] += lo;
-            sq[2 * e] += lo * lo;
-            ss[2 * e + 1] += hi;
-            sq[2 * e + 1] += hi * hi;
-          }
-        }
         if (a.relu_mask) {
           const u32x4_t m = *reinterpret_cast<const u32x4_t*>(a.relu_mask + ob + i * 8);
 #pragma unroll
@@ -554,7 +423,6 @@ __global__ __launch_bounds__(64 * WM* WN) void imgconv_persist_kernel(ImgConvArg
     __syncthreads();  // image b fully consumed before the next write
   }
   stamp(6);
-  if (ostat && !(a.diag & 1024)) out_stats_fold<THREADS>(a, M, reinterpret_cast<float*>(lds), sk, ss, sq);
 }
 
 // ----------------------------------------------------- compile-time geometry
@@ -895,7 +763,7 @@ size_t persist_lds(const PGeom& G) {
 }
 
 template <int NT, int RT, int WM, int WN, bool POOLED>
-bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done, bool* st_done) {
+bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   constexpr int THREADS = 64 * WM * WN;
   PGeom G = persist_geom(a, WN, NT, THREADS);
   size_t lds = persist_lds(G);
@@ -911,20 +779,6 @@ bool launch_cfg(const ImgConvArgs& a, hipStream_t s, bool* sc_done, bool* st_don
   ImgConvArgs ad = a;
   ad.diag = diag;
   if (!sc) ad.sc_src = nullptr;
-  // output statistics in the staged epilogue (out_stats_fold's LDS: [waves][2N] + [N] floats)
-  const size_t st_lds = ((size_t)THREADS / 64 * 4 * 128 + 64) * sizeof(float);
-  const bool st = a.ostats && G.stage_out && !a.relu_mask && !ad.sc_src && !a.bias && a.N >= 16 && a.N <= 64 &&
-                  THREADS % (a.N / 8) == 0 && std::max(lds, st_lds) <= 160 * 1024;
-  ad.ostats = nullptr;
-  ad.opart = nullptr;
-  ad.octr = nullptr;
-  if (st) {
-    lds = std::max(lds, st_lds);
-    ad.ostats = a.ostats;
-    ad.opart = bn_part_buffer(grid, a.N, s);
-    ad.octr = bn_part_counter(ad.opart);
-  }
-  if (st_done) *st_done = st;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(THREADS), lds, s, ad, G);
@@ -1009,9 +863,8 @@ bool launch_fixed(const ImgConvArgs& a, hipStream_t s) {
   }
 }
 
-bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done, bool* st_done) {
+bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_done) {
   if (sc_done) *sc_done = false;
-  if (st_done) *st_done = false;
   if (a.CS % 8 || a.N > 64 || a.B < 64) return false;
   if (a.OH == 14 && a.OW == 14 && a.B >= 256 && !a.bns.stats) {
     // compile-time geometry, one 16-row tile per wave (13 waves); 2 / 4 tiles per wave (7 / 4
@@ -1030,14 +883,14 @@ bool launch_imgconv_persistent(const ImgConvArgs& a, hipStream_t s, bool* sc_don
   // 4 x 2 (48 / 74) and 4 x 1 waves holding every n-tile (fewer LDS reads, but one wave per SIMD
   // exposes the read latency: fwd 48 vs 63 us); the alternatives were removed in round 3
   if (a.N <= 16 && !(diag_bits("icr") & 32))  // one n-tile: a second wave column would only compute padding
-    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s, sc_done, st_done) : launch_cfg<1, 2, 16, 1, false>(a, s, sc_done, st_done);
-  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s, sc_done, st_done) : launch_cfg<1, 2, 8, 2, false>(a, s, sc_done, st_done);
+    return pooled ? launch_cfg<1, 2, 16, 1, true>(a, s, sc_done) : launch_cfg<1, 2, 16, 1, false>(a, s, sc_done);
+  if (a.N <= 32) return pooled ? launch_cfg<1, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<1, 2, 8, 2, false>(a, s, sc_done);
   // small maps (<= 4 row tiles: ResNet-20 stage 3, 8x8): 4 x 2 waves of one tile x 2 n-tiles each -
   // the 8 x 2 grid left half its waves idle and computed a padding tile in the rest (s3 conv 8.98 ->
   // 8.27 us, step -6 us; DTFE_DIAG icr=128 -> the 8 x 2 grid, profiles/r5_resnet20_kernels.txt)
   if (a.OH * a.OW <= 64 && !pooled && a.N <= 64 && !(diag_bits("icr") & 128))
-    return launch_cfg<2, 1, 4, 2, false>(a, s, sc_done, st_done);
-  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s, sc_done, st_done) : launch_cfg<2, 2, 8, 2, false>(a, s, sc_done, st_done);
+    return launch_cfg<2, 1, 4, 2, false>(a, s, sc_done);
+  return pooled ? launch_cfg<2, 2, 8, 2, true>(a, s, sc_done) : launch_cfg<2, 2, 8, 2, false>(a, s, sc_done);
 }
 
 }  // namespace dtfe

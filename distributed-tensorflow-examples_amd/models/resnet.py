@@ -140,13 +140,15 @@ class Conv:
         ``bn_src``: the preceding BatchNorm + ReLU (BN.src_fold) for the whole-image kernel, which
         forms it while staging the raw input x and saves the BN's statistics / moving averages."""
         if self.img_fwd:
-            st = stats if _OUT_STATS and self.y.is_cuda else None
+            # (no output statistics: the BN runs its bn_stats pass - in the staged epilogue with a
+            # last-arriver fold they cost 11-12 us per conv against a 4.5-6.7 us pass,
+            # profiles/r6_resnet20_ostats_ab.txt)
             if bn_src is not None:
-                done = ops.imgconv(self.w, self.y, src=x, bn_src=bn_src.src_args(), bn_eps=BN_EPS,
-                                   bn_momentum=BN_MOMENTUM, bn_save=True, stats=st, **self.ic)
-                return self.y, st is not None and done
-            done = ops.imgconv(self.w, self.y, src=x, stats=st, **self.ic)
-            return self.y, st is not None and done
+                ops.imgconv(self.w, self.y, src=x, bn_src=bn_src.src_args(), bn_eps=BN_EPS,
+                            bn_momentum=BN_MOMENTUM, bn_save=True, **self.ic)
+            else:
+                ops.imgconv(self.w, self.y, src=x, **self.ic)
+            return self.y, False
         assert bn_src is None
         ops.conv_fwd(x, self.w, None, self.y, None, self.g, act=ops.ACT_NONE, stats=stats)
         return self.y, stats is not None
@@ -253,9 +255,6 @@ _R20_SRC_FOLD = True
 _HEAD_FUSE = True
 # ResNet-20 weight-gradient reduces deferred to grouped launches (ops.wgrad_flush)
 _WGRAD_DEFER = True
-# the whole-image forward convs accumulate their BatchNorm's statistics in the staged epilogue
-# (ops.imgconv(stats=...)): no bn_stats pass over y
-_OUT_STATS = True
 
 
 class BN:

@@ -368,26 +368,19 @@ def _bn_src_ref(src, bn_src, eps, momentum, save):
 
 def imgconv(w, y, *, B, SH, SW, CS, OH, OW, N, KH, KW, stride=1, pad=0, src=None, src_pooled=None,
             src_argmax=None, bias=None, argmax=None, relu_mask=None, flip_taps=False, act=ACT_NONE, pool=False,
-            dil=1, bn_src=None, bn_eps=1e-3, bn_momentum=0.99, bn_save=False, stats=None):
+            dil=1, bn_src=None, bn_eps=1e-3, bn_momentum=0.99, bn_save=False):
     """Whole-image LDS convolution (small feature maps): forward (+bias/act/pool) or, with
     flip_taps and pad = K-1-pad, the data gradient of a stride-1 conv (w = Wt [cin][tap][cout]).
     The source may be un-pooled on load from (src_pooled, src_argmax), or dilated (``dil``: source
     pixel (y, x) at (y*dil, x*dil), zeros between - the data gradient of a stride-``dil`` conv).
-    ``stats`` (f32 [2][N], zeroed; plain forward): also accumulate the BatchNorm statistics of y as
-    ``bn_stats`` does where the launch can (the persistent kernel's staged epilogue, one fixed-order
-    fold - no pass over y); then returns True, else False (the caller runs bn_stats).  Without
-    ``stats`` it returns y."""
+    Returns y.  (The output BatchNorm statistics accumulated in the staged epilogue with a
+    last-arriver fold measured 11-12 us slower per conv than the 4.5-6.7 us bn_stats pass it replaced -
+    ResNet-20 1.312 vs 1.192 ms/step - and was removed in round 6: profiles/r6_resnet20_ostats_ab.txt.)"""
     if y.is_cuda:
-        done = require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW,
-                                 N, KH, KW, stride, pad, flip_taps, act, pool, dil, bn_src=bn_src, bn_eps=bn_eps,
-                                 bn_momentum=bn_momentum, bn_save=bn_save, out_stats=stats)
-        return bool(done) if stats is not None else y
-    if stats is not None:
-        imgconv(w, y, B=B, SH=SH, SW=SW, CS=CS, OH=OH, OW=OW, N=N, KH=KH, KW=KW, stride=stride, pad=pad, src=src,
-                src_pooled=src_pooled, src_argmax=src_argmax, bias=bias, act=act, dil=dil, bn_src=bn_src,
-                bn_eps=bn_eps, bn_momentum=bn_momentum, bn_save=bn_save)
-        bn_stats(y, stats)
-        return True
+        require().imgconv(src, src_pooled, src_argmax, w, bias, y, argmax, relu_mask, B, SH, SW, CS, OH, OW,
+                          N, KH, KW, stride, pad, flip_taps, act, pool, dil, bn_src=bn_src, bn_eps=bn_eps,
+                          bn_momentum=bn_momentum, bn_save=bn_save)
+        return y
     if bn_src is not None:  # BN + ReLU formed on the source (the kernel does it while staging)
         src = _bn_src_ref(src, bn_src, bn_eps, bn_momentum, bn_save)
     s = src.float().view(B, SH, SW, CS) if src is not None else _unpooled_nhwc(src_pooled, src_argmax, B, SH, SW, CS)

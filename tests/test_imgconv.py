@@ -366,38 +366,3 @@ def test_imgwgrad_deferred_reduces_grouped_flush():
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
     assert ops.wgrad_flush() == 0
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("B,H,CI,N,s", [(128, 32, 16, 16, 1), (300, 32, 16, 16, 1), (128, 32, 16, 32, 2),
-                                         (200, 16, 32, 32, 1), (128, 16, 32, 64, 2), (128, 8, 64, 64, 1)])
-def test_imgconv_output_bn_stats_fused(B, H, CI, N, s):
-    """ops.imgconv(stats=...): the persistent forward's staged epilogue accumulates the output's
-    BatchNorm statistics (per-workgroup shifted sums, last-arriver fold) - the same y as without,
-    statistics equal to bn_stats' (shift = y[0][0]) to fp32 rounding, and the derived mean /
-    variance equal to the fp64 ones; a replayed launch (counter reset) gives identical bits."""
-    torch.manual_seed(21)
-    x = (torch.randn(B, H, H, CI) * 1.5 + 0.7).to(DEV, torch.bfloat16)
-    w = (torch.randn(N, 3, 3, CI) * 0.2).to(DEV, torch.bfloat16)
-    OH = H // s
-    kw = dict(B=B, SH=H, SW=H, CS=CI, OH=OH, OW=OH, N=N, KH=3, KW=3, stride=s, pad=1)
-    y_ref = torch.empty(B, OH, OH, N, device=DEV, dtype=torch.bfloat16)
-    ops.imgconv(w, y_ref, src=x, **kw)
-    st_ref = torch.zeros(2 * N, device=DEV)
-    ops.bn_stats(y_ref, st_ref)
-    y = torch.empty_like(y_ref)
-    st = torch.zeros(2 * N, device=DEV)
-    assert ops.imgconv(w, y, src=x, stats=st, **kw) is True
-    assert torch.equal(y, y_ref)
-    R = B * OH * OH
-    scale = st_ref.abs().max().item()
-    assert (st - st_ref).abs().max().item() <= 2e-5 * scale + 1e-3, ((st - st_ref).abs().max().item(), scale)
-    yd = y_ref.double().view(-1, N)
-    k = yd[0]
-    mean = k + st[:N].double() / R
-    var = st[N:].double() / R - (st[:N].double() / R) ** 2
-    assert torch.allclose(mean, yd.mean(0), atol=1e-5, rtol=1e-5)
-    assert torch.allclose(var, yd.var(0, unbiased=False), atol=1e-5, rtol=1e-4)
-    st2 = torch.zeros(2 * N, device=DEV)
-    assert ops.imgconv(w, y, src=x, stats=st2, **kw) is True
-    assert torch.equal(st, st2)
