@@ -19,6 +19,10 @@ import torch
 from .. import ops
 
 
+# fused apply: the transposed-tile work items ahead of the flat ranges (test hook / A/B switch)
+TILES_FIRST = True
+
+
 @dataclass
 class VarSpec:
     """One trainable variable.
@@ -217,6 +221,10 @@ class Optimizer:
                 n = s.numel
                 for st in range(0, n, chunk):
                     work.append([0, si, 0, 0, 0, st, min(chunk, n - st)])
+        if TILES_FIRST:
+            # transposed-copy tiles first: they are short latency chains (16 dependent-free loads, an
+            # LDS transpose, scattered stores); dispatched last they were the launch's tail
+            work.sort(key=lambda w: -w[0])
         self.nseg, self.nwork = len(segs), len(work)
         self._blob = ops.opt_pack(torch.tensor(segs, dtype=torch.int64), torch.tensor(work, dtype=torch.int64),
                                   self.P.master)
