@@ -400,6 +400,24 @@ void unpool_f32(const Tensor& g, const Tensor& argmax, const Tensor& out, int64_
                           (int)PW, (int)C, cur_stream());
 }
 
+// MNIST conv1 weight gradient at fp32 from the pooled gradient (conv_f32.hip); false: shape not covered
+bool conv1_wgrad_pooled_f32(const Tensor& dp, const Tensor& argmax, const Tensor& x, const Tensor& dw,
+                            const optional<Tensor>& db, const Tensor& ws, int64_t B, int64_t H, int64_t W, int64_t K,
+                            double scale) {
+  check_cuda(dp, "dp");
+  TORCH_CHECK(dp.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat && dw.scalar_type() == at::kFloat &&
+                  argmax.scalar_type() == at::kByte && ws.scalar_type() == at::kFloat,
+              "conv1_wgrad_pooled_f32: fp32 dp / x / dw / ws, uint8 argmax");
+  TORCH_CHECK(dp.is_contiguous() && argmax.is_contiguous() && x.is_contiguous() && dp.numel() == B * (H / 2) * (W / 2) * 32 &&
+                  argmax.numel() == dp.numel() && x.numel() == B * H * W && dw.numel() == 32 * K * K &&
+                  (!db.has_value() || !db->defined() || db->numel() == 32),
+              "conv1_wgrad_pooled_f32: dp [B][H/2][W/2][32], x [B][H][W][1], dw [32][K][K][1], db [32]");
+  const dtfe::ConvGeom g = geom(B, H, W, 1, 32, H, W, K, K, 1, K / 2, 0);
+  return dtfe::launch_conv1_wgrad_pooled_f32(dp.data_ptr<float>(), argmax.data_ptr<uint8_t>(), x.data_ptr<float>(),
+                                             dw.data_ptr<float>(), ptr_or_null<float>(db), ws.data_ptr<float>(),
+                                             ws.numel(), g, (float)scale, cur_stream());
+}
+
 void transpose_taps_f32(const Tensor& in, const Tensor& out, int64_t O, int64_t T, int64_t C) {
   check_cuda(in, "in");
   TORCH_CHECK(in.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && in.numel() == O * T * C &&
@@ -408,6 +426,34 @@ void transpose_taps_f32(const Tensor& in, const Tensor& out, int64_t O, int64_t 
 }
 
 // ------------------------------------------------------------------- head
+// fp32 fused head (head.hip head_xent_f32_kernel); false: shape not instantiated (caller: GEMMs + softmax_xent)
+bool head_xent_f32(const Tensor& h, const Tensor& w, const optional<Tensor>& b, const Tensor& labels, const Tensor& dz,
+                   const Tensor& dl, const Tensor& loss_sum, const Tensor& correct, const optional<Tensor>& logits,
+                   double scale, double inv_keep, const optional<Tensor>& step_counter) {
+  check_cuda(h, "h");
+  TORCH_CHECK(h.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && dz.scalar_type() == at::kFloat &&
+                  dl.scalar_type() == at::kFloat && labels.scalar_type() == at::kInt && h.dim() == 2 && w.dim() == 2 &&
+                  h.is_contiguous() && w.is_contiguous() && dz.is_contiguous() && dl.is_contiguous(),
+              "head_xent_f32: fp32 h [B][K], W [NC][K], dz, dl; int32 labels");
+  dtfe::HeadF32Args a{};
+  a.B = (int)h.size(0); a.K = (int)h.size(1); a.NC = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == a.K && dz.numel() == h.numel() && dl.numel() == (int64_t)a.B * a.NC && labels.numel() >= a.B,
+              "head_xent_f32: shapes");
+  a.h = h.data_ptr<float>(); a.w = w.data_ptr<float>(); a.b = ptr_or_null<float>(b);
+  a.labels = labels.data_ptr<int32_t>();
+  a.scale = (float)scale; a.inv_keep = (float)inv_keep;
+  a.dz = dz.data_ptr<float>(); a.dl = dl.data_ptr<float>();
+  a.logits_out = ptr_or_null<float>(logits);
+  TORCH_CHECK(!a.logits_out || logits->numel() == dl.numel(), "head_xent_f32: logits [B][NC]");
+  a.loss_sum = loss_sum.data_ptr<float>(); a.correct = correct.data_ptr<int32_t>();
+  a.step_counter = nullptr;
+  if (step_counter.has_value() && step_counter->defined()) {
+    TORCH_CHECK(step_counter->scalar_type() == at::kLong && step_counter->is_cuda(), "head_xent_f32: int64 step_counter");
+    a.step_counter = step_counter->data_ptr<int64_t>();
+  }
+  return dtfe::launch_head_xent_f32(a, cur_stream());
+}
+
 void head_xent(const Tensor& h, const Tensor& w, const optional<Tensor>& b, const Tensor& labels, const Tensor& dz,
                const Tensor& dl, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
                const optional<Tensor>& logits, double scale, double inv_keep, const optional<Tensor>& step_counter,
@@ -1116,6 +1162,10 @@ TORCH_LIBRARY(dtfe, m) {
   m.def("mse_sigmoid(Tensor y, Tensor t, Tensor(a!) loss, Tensor(b!) dz) -> ()");
   m.def("colsum(Tensor x, int M, int N, int ld, Tensor(a!) db, float scale) -> ()");
   m.def("unpool_f32(Tensor g, Tensor argmax, Tensor(a!) out, int B, int PH, int PW, int C) -> ()");
+  m.def("head_xent_f32(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl, Tensor(c!) loss_sum,"
+        " Tensor(d!) correct, Tensor(e!)? logits, float scale, float inv_keep, Tensor(f!)? step_counter) -> bool");
+  m.def("conv1_wgrad_pooled_f32(Tensor dp, Tensor argmax, Tensor x, Tensor(a!) dw, Tensor(b!)? db, Tensor(c!) ws,"
+        " int B, int H, int W, int K, float scale) -> bool");
   m.def("transpose_taps_f32(Tensor input, Tensor(a!) out, int O, int T, int C) -> ()");
   m.def("act_grad(Tensor dy, Tensor y, Tensor(a!) dz, int act) -> ()");
   m.def("bias_act(Tensor x, Tensor? bias, Tensor(a!) out, int act, float keep, int seed, Tensor? counter) -> ()");
@@ -1155,6 +1205,8 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("mse_sigmoid", &mse_sigmoid);
   m.impl("colsum", &colsum);
   m.impl("unpool_f32", &unpool_f32);
+  m.impl("head_xent_f32", &head_xent_f32);
+  m.impl("conv1_wgrad_pooled_f32", &conv1_wgrad_pooled_f32);
   m.impl("transpose_taps_f32", &transpose_taps_f32);
   m.impl("act_grad", &act_grad);
   m.impl("bias_act", &bias_act);

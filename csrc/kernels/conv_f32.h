@@ -24,5 +24,12 @@ void launch_conv_dgrad_f32(const ConvF32Args& a, hipStream_t s);   // stride 1
 void launch_conv_wgrad_f32(const ConvF32Args& a, hipStream_t s);
 void launch_unpool_f32(const float* g, const uint8_t* am, float* out, int B, int PH, int PW, int C, hipStream_t s);
 void launch_transpose_taps_f32(const float* in, float* out, int O, int T, int C, hipStream_t s);
+// MNIST conv1's weight gradient (C = 1, 32 channels, 3x3 / 5x5 SAME, stride 1) straight from the pooled
+// gradient dP [B][H/2][W/2][32] and its argmax bytes: dW += scale * sum, db += scale * sum over the
+// non-zero (argmax) pixels only, through ws (>= conv1_wgrad_pooled_f32_ws_floats(B) floats) and a
+// fixed-order partial reduce.  false: shape not covered (un-pool + launch_conv_wgrad_f32 instead).
+long conv1_wgrad_pooled_f32_ws_floats(int B);
+bool launch_conv1_wgrad_pooled_f32(const float* dp, const uint8_t* am, const float* x, float* dw, float* db, float* ws,
+                                   long ws_floats, const ConvGeom& g, float scale, hipStream_t s);
 
 }  // namespace dtfe

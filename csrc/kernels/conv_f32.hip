@@ -15,6 +15,9 @@
 #include "gemm_core.h"
 #include "conv.h"
 #include "conv_f32.h"
+#include "imgconv.h"  // launch_partials_reduce
+
+#include <algorithm>
 
 namespace dtfe {
 
@@ -302,10 +305,222 @@ __global__ __launch_bounds__(256) void transpose_taps_f32_kernel(const float* __
   out[((long)c * T + t) * O + o] = in[i];
 }
 
+// ------------------------------------------------------------------ the 1-channel input layer
+// MNIST conv1 (C = 1, 32 output channels, KSxKS SAME, stride 1, 2x2 max-pool) at fp32.  With one input
+// channel the GEMM view has K = KS*KS = 25 (one and a half 16-deep MFMA steps of padding, every A
+// element gathered on its own), so the generic im2col kernels spent 74 us (forward) and 174 us
+// (weight gradient over the materialised 103 MB un-pooled gradient) on 1.3 GFLOP.  These kernels
+// work on VALU fmaf chains over an LDS-staged image instead:
+//   forward   thread = (channel n, pooled pixel q): the 6x6 input window of its 2x2 pool window
+//             (broadcast LDS reads: the 32 lanes of a q read one window) x 25 register weights,
+//             the four outputs as packed fp32 FMAs, first-max argmax, bias + act - in the same k
+//             order as the generic kernel's fmaf chain;
+//   wgrad     thread = (channel n, tap row kh, q parity): for every pooled gradient only the argmax
+//             pixel of its window is non-zero, so dW[n][kh][kw] += dP[q][n] * x[pixel(q, n) + tap]
+//             over the pooled positions (a quarter of the dense products, no un-pooled tensor),
+//             per-workgroup partial slabs summed by partials_reduce in a fixed order (no float
+//             atomics: the fp32 step is run-to-run deterministic).
+constexpr int C1F_N = 32, C1F_LP = 36;  // channels; LDS plane pitch (W + KS - 1 <= 36)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+template <int KS>
+__global__ __launch_bounds__(256) void conv1_fwd_pool_f32_kernel(ConvF32Args a) {
+  constexpr int T = KS * KS, WIN = KS + 1;
+  __shared__ float xs[C1F_LP * C1F_LP];
+  const ConvGeom& g = a.g;
+  const int H = g.H, W = g.W, PH = H >> 1, PW = W >> 1, NQ = PH * PW, HW = H * W;
+  const int tid = threadIdx.x, n = tid & 31, qi = tid >> 5;
+  float wr[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) wr[t] = a.w[n * T + t];
+  const float bias = a.bias ? a.bias[n] : 0.f;
+  for (int i = tid; i < C1F_LP * C1F_LP; i += 256) xs[i] = 0.f;
+  // the image's pixels, 4 per thread (H*W <= 1024): prefetched one image ahead
+  float xv[4];
+  auto load = [&](long b) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * 256;
+      xv[j] = i < HW ? a.src[b * HW + i] : 0.f;
+    }
+  };
+  long b = blockIdx.x;
+  if (b < g.B) load(b);
+  __syncthreads();
+  for (; b < g.B; b += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * 256;
+      if (i < HW) {
+        const int y = i / W, x = i - y * W;
+        xs[(y + KS / 2) * C1F_LP + x + KS / 2] = xv[j];
+      }
+    }
+    __syncthreads();
+    if (b + gridDim.x < g.B) load(b + gridDim.x);
+    for (int q = qi; q < NQ; q += 8) {
+      const int py = q / PW, px = q - py * PW;
+      const float* base = xs + (2 * py) * C1F_LP + 2 * px;
+      float win[WIN][WIN];
+#pragma unroll
+      for (int r = 0; r < WIN; ++r)
+#pragma unroll
+        for (int c = 0; c < WIN; ++c) win[r][c] = base[r * C1F_LP + c];
+      f32x2v z0 = {0.f, 0.f}, z1 = {0.f, 0.f};  // (dy = 0: dx 0, 1), (dy = 1: dx 0, 1)
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const float w = wr[kh * KS + kw];
+          z0 = __builtin_elementwise_fma(f32x2v{w, w}, f32x2v{win[kh][kw], win[kh][kw + 1]}, z0);
+          z1 = __builtin_elementwise_fma(f32x2v{w, w}, f32x2v{win[kh + 1][kw], win[kh + 1][kw + 1]}, z1);
+        }
+      const float z[4] = {z0[0], z0[1], z1[0], z1[1]};
+      int am = 0;
+      float mx = z[0];
+#pragma unroll
+      for (int j = 1; j < 4; ++j)
+        if (z[j] > mx) { mx = z[j]; am = j; }
+      const long o = ((b * PH + py) * PW + px) * C1F_N + n;
+      a.out[o] = apply_act(mx + bias, a.act);  // act is monotone: pool(act(z)) == act(pool(z))
+      if (a.argmax) a.argmax[o] = (uint8_t)am;
+    }
+    __syncthreads();
+  }
+}
+
+// dP [B][PH][PW][32] fp32 (the ReLU mask already applied), argmax bytes of the same layout, x [B][H][W]
+// -> ws[blockIdx][32*T + 32] = (dW[n][t], db[n]) partial sums over the workgroup's images
+template <int KS>
+__global__ __launch_bounds__(320) void conv1_wgrad_pooled_f32_kernel(const float* __restrict__ dp,
+                                                                     const uint8_t* __restrict__ am,
+                                                                     const float* __restrict__ x, float* ws, int B,
+                                                                     int H, int W) {
+  constexpr int T = KS * KS, TH = 320, LEN = C1F_N * T + C1F_N;
+  static_assert(KS <= 5, "the 320-thread mapping covers 5 tap rows x 32 channels x 2 q parities");
+  __shared__ float xs[C1F_LP * C1F_LP];
+  __shared__ __attribute__((aligned(16))) float gs[32 * 32 * C1F_N / 4];  // pooled gradient image (<= 16x16)
+  __shared__ __attribute__((aligned(16))) uint8_t as[32 * 32 * C1F_N / 4];
+  __shared__ float red[KS * C1F_N * KS + C1F_N];
+  const int PH = H >> 1, PW = W >> 1, NQ = PH * PW, HW = H * W, NG = NQ * C1F_N;
+  const int tid = threadIdx.x, n = tid & 31, kh = (tid >> 5) % 5, qh = tid / 160;
+  const bool act_t = kh < KS;
+  float acc[KS], dbacc = 0.f;
+#pragma unroll
+  for (int j = 0; j < KS; ++j) acc[j] = 0.f;
+  for (int i = tid; i < C1F_LP * C1F_LP; i += TH) xs[i] = 0.f;
+  // per image: NG / 4 16-B gradient chunks, NG / 16 16-B argmax chunks, HW pixels; prefetched one
+  // image ahead in registers (NG <= 8192: 7 gradient chunks, 2 argmax chunks, 4 pixels per thread)
+  constexpr int GC = (32 * 32 * C1F_N / 4 / 4 + TH - 1) / TH, AC = (32 * 32 * C1F_N / 4 / 16 + TH - 1) / TH;
+  f32x4_t gv[GC];
+  u32x4_t av[AC];
+  float xv[4];
+  auto load = [&](long b) {
+#pragma unroll
+    for (int j = 0; j < GC; ++j) {
+      const int i = tid + j * TH;
+      if (i < NG / 4) gv[j] = *reinterpret_cast<const f32x4_t*>(dp + b * NG + i * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < AC; ++j) {
+      const int i = tid + j * TH;
+      if (i < NG / 16) av[j] = *reinterpret_cast<const u32x4_t*>(am + b * NG + i * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * TH;
+      xv[j] = i < HW ? x[b * HW + i] : 0.f;
+    }
+  };
+  long b = blockIdx.x;
+  if (b < B) load(b);
+  __syncthreads();
+  for (; b < B; b += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < GC; ++j) {
+      const int i = tid + j * TH;
+      if (i < NG / 4) reinterpret_cast<f32x4_t*>(gs)[i] = gv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < AC; ++j) {
+      const int i = tid + j * TH;
+      if (i < NG / 16) reinterpret_cast<u32x4_t*>(as)[i] = av[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * TH;
+      if (i < HW) {
+        const int y = i / W, xx = i - y * W;
+        xs[(y + KS / 2) * C1F_LP + xx + KS / 2] = xv[j];
+      }
+    }
+    __syncthreads();
+    if (b + gridDim.x < B) load(b + gridDim.x);
+    if (act_t) {
+      for (int q = qh; q < NQ; q += 2) {
+        const int py = q / PW, px = q - py * PW;
+        const float v = gs[q * C1F_N + n];
+        const int m = as[q * C1F_N + n];
+        // output pixel (2py + m/2, 2px + m%2); tap (kh, kw) reads x at output + (kh, kw) - pad, i.e.
+        // xs[(oy + kh) * LP + ox + kw] in the padded plane
+        const float* row = xs + (2 * py + (m >> 1) + kh) * C1F_LP + 2 * px + (m & 1);
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) acc[kw] = __builtin_fmaf(v, row[kw], acc[kw]);
+        dbacc += v;
+      }
+    }
+    __syncthreads();
+  }
+  // the two q parities -> one partial (parity 0 + parity 1, fixed order), db from the kh == 0 threads
+  if (qh == 1 && act_t) {
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw) red[(kh * C1F_N + n) * KS + kw] = acc[kw];
+    if (kh == 0) red[KS * C1F_N * KS + n] = dbacc;
+  }
+  __syncthreads();
+  if (qh == 0 && act_t) {
+    float* o = ws + (long)blockIdx.x * LEN;
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw) o[n * T + kh * KS + kw] = acc[kw] + red[(kh * C1F_N + n) * KS + kw];
+    if (kh == 0) o[C1F_N * T + n] = dbacc + red[KS * C1F_N * KS + n];
+  }
+}
+
+bool conv1_f32_shape_ok(const ConvGeom& g) {
+  return g.C == 1 && g.Cout == C1F_N && (g.KH == 5 || g.KH == 3) && g.KW == g.KH && g.stride == 1 &&
+         g.pad == g.KH / 2 && g.OH == g.H && g.OW == g.W && ((g.H | g.W) & 1) == 0 && g.W + g.KW - 1 <= C1F_LP &&
+         g.H + g.KH - 1 <= C1F_LP && g.H * g.W <= 1024;
+}
+
 }  // namespace
+
+long conv1_wgrad_pooled_f32_ws_floats(int B) {
+  return (long)(B < 512 ? B : 512) * (C1F_N * 25 + C1F_N);
+}
+
+bool launch_conv1_wgrad_pooled_f32(const float* dp, const uint8_t* am, const float* x, float* dw, float* db, float* ws,
+                                   long ws_floats, const ConvGeom& g, float scale, hipStream_t s) {
+  if (!conv1_f32_shape_ok(g) || g.B < 1) return false;
+  // >= 2 images per workgroup (the next image's loads overlap the current one), at most 2 per CU
+  const int grid = std::min(512, (g.B + 1) / 2);
+  const int T = g.KH * g.KW, LEN = C1F_N * T + C1F_N;
+  if ((long)grid * LEN > ws_floats) return false;
+  if (g.KH == 5)
+    hipLaunchKernelGGL(conv1_wgrad_pooled_f32_kernel<5>, dim3(grid), dim3(320), 0, s, dp, am, x, ws, g.B, g.H, g.W);
+  else
+    hipLaunchKernelGGL(conv1_wgrad_pooled_f32_kernel<3>, dim3(grid), dim3(320), 0, s, dp, am, x, ws, g.B, g.H, g.W);
+  launch_partials_reduce(ws, grid, LEN, C1F_N * T, dw, db, scale, s);
+  return true;
+}
 
 void launch_conv_fwd_f32(const ConvF32Args& a, hipStream_t s) {
   const ConvGeom& g = a.g;
+  if (g.pool_order && conv1_f32_shape_ok(g)) {  // the 1-channel input layer: conv1_fwd_pool_f32_kernel
+    const int grid = std::min(g.B, 1024);
+    if (g.KH == 5) hipLaunchKernelGGL(conv1_fwd_pool_f32_kernel<5>, dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv1_fwd_pool_f32_kernel<3>, dim3(grid), dim3(256), 0, s, a);
+    return;
+  }
   const int M = g.B * g.OH * g.OW;
   if (g.Cout <= 32) {
     using Cfg = TileCfg<float, 64, 32, 4, 1>;

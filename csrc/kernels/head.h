@@ -27,6 +27,21 @@ struct HeadArgs {
 
 void launch_head_xent(const HeadArgs& a, hipStream_t s);
 
+// The same per-row head at fp32 (the `--dtype fp32` CNN step): fp32 h / W / b in, fp32 logits
+// (optional), dlogit rows [B][NC] (the head weight-gradient GEMM's operand) and dZ [B][K] out;
+// loss / hits by one atomic per workgroup; step_counter as above.  Every product and sum is an
+// fp32 FMA / add (the dot products as lane-strided fmaf chains + a butterfly).
+struct HeadF32Args {
+  int B, NC, K;
+  const float* h; const float* w; const float* b; const int32_t* labels;
+  float scale, inv_keep;
+  float* dz; float* dl; float* logits_out;
+  float* loss_sum; int32_t* correct;
+  int64_t* step_counter;
+};
+// false: shape not instantiated (NC = 10, K = 1024 only)
+bool launch_head_xent_f32(const HeadF32Args& a, hipStream_t s);
+
 // dW[c][k] = scale * sum_b dl[b][c] h[b][k] (row stride ldw), db[c] = scale * sum_b dl[b][c];
 // stored, not accumulated (one workgroup per 16 columns, fixed summation order)
 struct HeadWgradArgs {

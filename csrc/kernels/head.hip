@@ -123,6 +123,92 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   }
 }
 
+// fp32 head: one wave per row as above; the wave's W slice (NC x K/64 fp32, 160 VGPRs for 10 x 16)
+// and h row go straight to registers (16-B loads); replaces the fp32 step's head GEMM + softmax-xent
+// + dlogit . W GEMM + step-counter increment (four launches, ~54 us, profiles/r6_fp32_rows.txt)
+template <int NC, int K>
+__global__ __launch_bounds__(256) void head_xent_f32_kernel(HeadF32Args a) {
+  constexpr int E = K / 64;
+  static_assert(E % 4 == 0, "K must be a multiple of 256");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __shared__ float red_loss[4];
+  __shared__ int red_correct[4];
+  if (a.step_counter && blockIdx.x == 0 && threadIdx.x == 0) *a.step_counter += 1;
+  const int row = min(blockIdx.x * 4 + wid, a.B - 1);
+  const bool live = blockIdx.x * 4 + wid < a.B;
+  f32x4_t wv[NC][E / 4], hv[E / 4];
+#pragma unroll
+  for (int c = 0; c < E / 4; ++c) hv[c] = *reinterpret_cast<const f32x4_t*>(a.h + (long)row * K + lane * E + c * 4);
+#pragma unroll
+  for (int n = 0; n < NC; ++n)
+#pragma unroll
+    for (int c = 0; c < E / 4; ++c) wv[n][c] = *reinterpret_cast<const f32x4_t*>(a.w + (long)n * K + lane * E + c * 4);
+  const int label = a.labels[row];
+  float logit[NC];
+#pragma unroll
+  for (int n = 0; n < NC; ++n) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) s = fmaf(hv[i / 4][i % 4], wv[n][i / 4][i % 4], s);
+    logit[n] = s;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int n = 0; n < NC; ++n) logit[n] += __shfl_xor(logit[n], o, 64);
+#pragma unroll
+  for (int n = 0; n < NC; ++n) logit[n] += a.b ? a.b[n] : 0.f;
+  float mx = logit[0];
+  int am = 0;
+#pragma unroll
+  for (int n = 1; n < NC; ++n) if (logit[n] > mx) { mx = logit[n]; am = n; }
+  float se = 0.f;
+#pragma unroll
+  for (int n = 0; n < NC; ++n) se += expf(logit[n] - mx);
+  const float lse = mx + logf(se);
+  float dl[NC], lg_label = 0.f;
+#pragma unroll
+  for (int n = 0; n < NC; ++n) {
+    const float p = expf(logit[n] - lse);
+    dl[n] = (p - (n == label ? 1.f : 0.f)) * a.scale;
+    if (n == label) lg_label = logit[n];
+  }
+  if (live && lane < NC) {
+    float v = 0.f, lv = 0.f;
+#pragma unroll
+    for (int n = 0; n < NC; ++n) if (n == lane) { v = dl[n]; lv = logit[n]; }
+    a.dl[(long)row * NC + lane] = v;
+    if (a.logits_out) a.logits_out[(long)row * NC + lane] = lv;
+  }
+#pragma unroll
+  for (int c = 0; c < E / 4; ++c) {
+    f32x4_t o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float g = 0.f;
+#pragma unroll
+      for (int n = 0; n < NC; ++n) g = fmaf(dl[n], wv[n][c][j], g);
+      o[j] = hv[c][j] > 0.f ? g * a.inv_keep : 0.f;
+    }
+    if (live) *reinterpret_cast<f32x4_t*>(a.dz + (long)row * K + lane * E + c * 4) = o;
+  }
+  if (lane == 0) {
+    red_loss[wid] = live ? lse - lg_label : 0.f;
+    red_correct[wid] = live && am == label;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.loss_sum) atomicAdd(a.loss_sum, red_loss[0] + red_loss[1] + red_loss[2] + red_loss[3]);
+    if (a.correct) atomicAdd(a.correct, red_correct[0] + red_correct[1] + red_correct[2] + red_correct[3]);
+  }
+}
+
+bool launch_head_xent_f32(const HeadF32Args& a, hipStream_t s) {
+  if (a.NC != 10 || a.K != 1024 || a.B < 1) return false;
+  hipLaunchKernelGGL((head_xent_f32_kernel<10, 1024>), dim3((a.B + 3) / 4), dim3(256), 0, s, a);
+  return true;
+}
+
 void launch_head_xent(const HeadArgs& a, hipStream_t s) {
   if (a.NC != 10 || a.K != 1024) throw std::runtime_error("head_xent: only NC=10, K=1024 instantiated");
   const int blocks = (a.B + 3) / 4;  // one row per wave

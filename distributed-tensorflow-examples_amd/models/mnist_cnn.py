@@ -408,17 +408,20 @@ class MnistCnnTrainer:
 
 class MnistCnnF32Trainer(MnistCnnTrainer):
     """The same CNN step at the reference's precision (``--dtype fp32``): fp32 activations and
-    gradients, every product on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain per
+    gradients, every product in exact fp32 (v_mfma_f32_16x16x4_f32 or VALU fmaf: an fmaf chain per
     dot product), fp32 weights read straight from the masters, the same fused TF1 Adam.
 
-      conv1 / conv2   conv_f32.hip implicit GEMM, bias + ReLU + 2x2 max-pool + argmax epilogue
+      conv1           conv_f32.hip 1-channel VALU kernel (LDS image, packed fp32 FMA), bias + ReLU +
+                      2x2 max-pool + argmax
+      conv2           conv_f32.hip implicit GEMM, bias + ReLU + 2x2 max-pool + argmax epilogue
       fc1             dense fp32 GEMM, bias + ReLU + dropout epilogue
-      head            fp32 GEMM -> softmax-xent kernel (loss, hits, dlogits)
+      head            one fused fp32 kernel: logits, softmax-xent (loss, hits), dlogits, dH (below)
       head / fc1 dW   fp32 GEMMs, bias gradient through a ones column
-      dH, dP2         fp32 GEMMs with the 1/keep * ReLU'(h) and ReLU'(p2) epilogues
-      un-pool         argmax routing kernel (dP2 -> dY2, dP1 -> dY1)
+      dH, dP2         1/keep * ReLU'(h) in the head kernel; fp32 GEMM with the ReLU'(p2) epilogue
+      un-pool         argmax routing kernel (dP2 -> dY2)
       conv2 dX / dW   conv_f32.hip (ReLU'(p1) epilogue; weight grad + bias grad atomics)
-      conv1 dW        conv_f32.hip
+      conv1 dW        conv_f32.hip from the pooled dP1 + argmax (only the argmax pixels: a quarter of
+                      the dense products), fixed-order partial reduce
     A parity path, not the benchmarked one: no fused sampling, no hipGraph-specific scheduling,
     one stream."""
 
@@ -477,7 +480,9 @@ class MnistCnnF32Trainer(MnistCnnTrainer):
         self._late = None
         self.schedule = []
 
-    def forward(self, keep=None, logits=None):
+    def forward(self, keep=None, logits=None, advance=False):
+        """``advance``: the training step's forward - the fused head also advances the dropout /
+        sampling counter (forward_backward's call)."""
         B, K1 = self.B, 7 * 7 * C2
         keep = self.keep if keep is None else keep
         if self.data is not None:
@@ -490,25 +495,33 @@ class MnistCnnF32Trainer(MnistCnnTrainer):
         ops.conv_fwd(self.p1, self.w["wc2"], self.b["bc2"], self.p2, self.a2, self.g2, pool=True, act=ops.ACT_RELU)
         ops.gemm(self.p2, self.w["wd1"], self.h, M=B, N=FC, K=K1, bias=self.b["bd1"], act=ops.ACT_RELU, keep=keep,
                  seed=self.seed + 2, counter=self.data_ctr)
-        ops.gemm(self.h, self.w["out"], self.logits, M=B, N=NCLS, K=FC, bias=self.b["bout"])
+        # head: logits, softmax-xent, dlogits, dZ = dlogits . W * 1/keep * ReLU'(h) (+ the counter) in
+        # one launch on the GPU; the GEMM + softmax_xent (+ GEMM in forward_backward) chain otherwise
+        ctr = self.data_ctr if (advance and self.data is not None) else None
+        self._fused_head = ops.head_xent_f32(self.h, self.w["out"], self.b["bout"], self.labels, self.dzf,
+                                             self.dlogits, self.loss_sum, self.correct, logits=self.logits,
+                                             scale=1.0 / B, inv_keep=1.0 / keep, step_counter=ctr)
+        if not self._fused_head:
+            ops.gemm(self.h, self.w["out"], self.logits, M=B, N=NCLS, K=FC, bias=self.b["bout"])
+            ops.softmax_xent(self.logits, labels_i=self.labels, scale=1.0 / B, dlogits=self.dlogits,
+                             loss_sum=self.loss_sum, correct=self.correct)
         if logits is not None and logits is not self.logits:
             logits.copy_(self.logits)
-        ops.softmax_xent(self.logits, labels_i=self.labels, scale=1.0 / B, dlogits=self.dlogits,
-                         loss_sum=self.loss_sum, correct=self.correct)
         self._keep_used = keep
 
     def forward_backward(self):
         B, K1 = self.B, 7 * 7 * C2
         self.schedule = []
-        self.forward()
-        if self.data is not None:
-            self.data_ctr += 1  # next step's batch / dropout stream (the bf16 path's head advances it)
+        self.forward(advance=True)
+        if self.data is not None and not self._fused_head:
+            self.data_ctr += 1  # next step's batch / dropout stream (the fused head advances it)
         inv_keep = 1.0 / self._keep_used
         # head: dW = dlogits^T . h (+ bias column), dh = dlogits . W * 1/keep * ReLU'(h)
         ops.gemm(self.dlogits, self.h, self.gw["out"], M=NCLS, N=FC + 1, K=B, amode=ops.RMAJ, lda=NCLS,
                  bmode=ops.RMAJ, ldb=FC, ldc=FC, b_ones_row=FC, bias_out=self.gw["bout"])
-        ops.gemm(self.dlogits, self.w["out"], self.dzf, M=B, N=FC, K=NCLS, bmode=ops.RMAJ, ldb=FC, alpha=inv_keep,
-                 aux=self.h, aux_act=ops.ACT_RELU)
+        if not self._fused_head:
+            ops.gemm(self.dlogits, self.w["out"], self.dzf, M=B, N=FC, K=NCLS, bmode=ops.RMAJ, ldb=FC,
+                     alpha=inv_keep, aux=self.h, aux_act=ops.ACT_RELU)
         # fc1: dW = dz^T . p2 (+ bias column), dP2 = dz . W1 * ReLU'(p2)
         ops.gemm(self.dzf, self.p2, self.gw["wd1"], M=FC, N=K1 + 1, K=B, amode=ops.RMAJ, lda=FC, bmode=ops.RMAJ,
                  ldb=K1, ldc=K1, b_ones_row=K1, bias_out=self.gw["bd1"])
@@ -523,9 +536,9 @@ class MnistCnnF32Trainer(MnistCnnTrainer):
         ops.conv_dgrad(self.dy2, self.wt2, self.dp1, self.g2, relu_mask=self.p1)
         self.schedule.append("conv2_dgrad")
         ops.conv_wgrad(self.dy2, self.p1, self.gw["wc2"], self.gw["bc2"], self.g2)
-        # conv1: un-pool, weight + bias gradient
-        ops.unpool_f32(self.dp1, self.a1, self.dy1)
-        ops.conv_wgrad(self.dy1, self.x, self.gw["wc1"], self.gw["bc1"], self.g1)
+        # conv1: weight + bias gradient straight from the pooled gradient (argmax pixels only; the
+        # un-pooled tensor is formed only by the oracle / fallback path)
+        ops.conv1_wgrad_pooled_f32(self.dp1, self.a1, self.x, self.gw["wc1"], self.gw["bc1"], self.g1, dy=self.dy1)
         if self.allreduce is not None:
             self.allreduce.launch(1)
             self.schedule.append("allreduce:1")

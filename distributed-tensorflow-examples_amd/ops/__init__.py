@@ -27,7 +27,8 @@ __all__ = [
     "TILE_DIMS", "FC_TILE", "TILE_SMALL", "GEMM_KTILE", "GLDS_TILES", "glds_ok", "ones_page", "bn_stats", "bn_apply", "bn_bwd_stats",
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
-    "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard",
+    "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard", "conv1_wgrad_pooled_f32",
+    "head_xent_f32",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -548,6 +549,23 @@ def conv_wgrad(dz, x, dw, db, g, scale=1.0):
     return dw
 
 
+def conv1_wgrad_pooled_f32(dp, argmax, x, dw, db, g, scale=1.0, dy=None):
+    """MNIST conv1 weight gradient at fp32 (C = 1, 32 channels, 3x3 / 5x5 SAME, stride 1) from the
+    POOLED gradient dp [B][H/2][W/2][32] (ReLU mask applied) and the pool's argmax bytes:
+    dW += scale * sum_q dp[q][n] * x[argmax pixel of q + tap], db += scale * sum dp - the gradient of
+    un-pool + conv_wgrad without the un-pooled tensor (GPU: conv1_wgrad_pooled_f32_kernel).  Other
+    shapes, and the CPU oracle: un-pool into ``dy`` [B][H][W][32] (allocated if None) + conv_wgrad."""
+    B, H, W, K = g["B"], g["H"], g["W"], g["KH"]
+    if dw.is_cuda:
+        ws = wgrad_workspace(dw.device, B * (32 * 25 + 32))
+        if require().conv1_wgrad_pooled_f32(dp, argmax, x, dw, db, ws, B, H, W, K, scale):
+            return dw
+    if dy is None:
+        dy = torch.empty(B, H, W, dp.shape[-1], device=dp.device, dtype=torch.float32)
+    unpool_f32(dp, argmax, dy)
+    return conv_wgrad(dy, x, dw, db, g, scale)
+
+
 def unpool_f32(g, argmax, out):
     """out[B][2PH][2PW][C] (fp32) = g routed to the argmax position of each 2x2 window, zeros
     elsewhere (the max-pool gradient; the ReLU mask is already in g)."""
@@ -569,6 +587,18 @@ def transpose_taps_f32(w, out, O, T, C):
 
 
 # -------------------------------------------------------------------- head
+def head_xent_f32(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0,
+                  step_counter=None) -> bool:
+    """fp32 fused classifier head (GPU, NC = 10, K = 1024): logits (optional), softmax-xent sums into
+    loss_sum / correct, dlogit rows fp32 [B][NC] into ``dl``, dZ = (dlogit . W) * inv_keep * (h > 0),
+    step_counter += 1 - one launch.  False (nothing done): CPU tensors or another shape - the caller
+    runs the GEMM + softmax_xent + GEMM chain, which is also this kernel's oracle."""
+    if not h.is_cuda:
+        return False
+    return bool(require().head_xent_f32(h, w, b, labels, dz, dl, loss_sum, correct, logits, scale, inv_keep,
+                                        step_counter))
+
+
 def head_xent(h, w, b, labels, dz, dl, loss_sum, correct, logits=None, scale=1.0, inv_keep=1.0, step_counter=None,
               parts=None):
     """Per-row classifier head: logits, softmax-xent (loss/correct sums), dlogit rows (bf16 [B][ld] into

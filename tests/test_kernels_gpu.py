@@ -614,3 +614,90 @@ def test_conv_wgrad_fp32(g):
     ref_b = 0.5 * dz.double().sum((0, 1, 2))
     assert ((dw.double() - ref_w).abs().max() / ref_w.abs().max()).item() < 1e-5
     assert ((db.double() - ref_b).abs().max() / ref_b.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("B,H,K", [(5, 28, 5), (300, 28, 5), (3, 16, 3), (1030, 28, 5)])
+def test_conv1_fwd_pool_f32_matches_fp64(B, H, K):
+    """The 1-channel fp32 forward (conv1_fwd_pool_f32_kernel: LDS image, packed fp32 FMA, fused bias +
+    ReLU + 2x2 max-pool + argmax) vs an fp64 conv2d reference; several images per workgroup
+    (B > 1024: the persistent grid), odd batch sizes, 3x3 and 5x5."""
+    torch.manual_seed(17)
+    g = _geom(B, H, H, 1, 32, K, K, 1, K // 2)
+    x = torch.rand(B, H, H, 1, device=DEV)
+    w = torch.randn(32, K, K, 1, device=DEV) * 0.2
+    b = torch.randn(32, device=DEV) * 0.1
+    y = torch.empty(B, H // 2, H // 2, 32, device=DEV)
+    am = torch.empty(B, H // 2, H // 2, 32, device=DEV, dtype=torch.uint8)
+    ops.conv_fwd(x, w, b, y, am, g, pool=True, act=ops.ACT_RELU)
+    z = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(),
+                                   padding=K // 2)
+    zz = z.view(B, 32, H // 2, 2, H // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(B, H // 2, H // 2, 32, 4)
+    mx, idx = zz.max(-1)
+    assert (y.double() - mx.clamp_min(0)).abs().max().item() < 1e-5
+    # argmax: wherever the window's maximum is unambiguous (fp32 ties / near-ties aside)
+    top2 = zz.topk(2, -1).values
+    clear = (top2[..., 0] - top2[..., 1]) > 1e-5
+    assert torch.equal(am.long()[clear], idx[clear])
+
+
+@pytest.mark.parametrize("B,H,K", [(6, 28, 5), (1024, 28, 5), (7, 16, 3)])
+def test_conv1_wgrad_pooled_f32_matches_unpooled_fp64(B, H, K):
+    """conv1_wgrad_pooled_f32 (weight + bias gradient from the pooled gradient and its argmax, only the
+    argmax pixels, per-workgroup slabs + fixed-order reduce) vs fp64 autograd over the un-pooled
+    gradient; accumulates into dw / db (scale), and two launches give identical bits."""
+    torch.manual_seed(19)
+    g = _geom(B, H, H, 1, 32, K, K, 1, K // 2)
+    x = torch.rand(B, H, H, 1, device=DEV)
+    dp = torch.randn(B, H // 2, H // 2, 32, device=DEV) * (torch.rand(B, H // 2, H // 2, 32, device=DEV) > 0.3)
+    am = torch.randint(0, 4, (B, H // 2, H // 2, 32), device=DEV, dtype=torch.uint8)
+    outs = []
+    for _ in range(2):
+        dw = torch.full((32, K, K, 1), 0.25, device=DEV)
+        db = torch.full((32,), -0.5, device=DEV)
+        ops.conv1_wgrad_pooled_f32(dp, am, x, dw, db, g, scale=0.5)
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    dy = torch.zeros(B, H, H, 32, dtype=torch.float64, device=DEV)
+    q = am.long()
+    for d in range(4):
+        dy[:, d >> 1::2, d & 1::2, :] = torch.where(q == d, dp.double(), torch.zeros_like(dp.double()))
+    xd = x.double().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(xd, (32, 1, K, K), dy.permute(0, 3, 1, 2), padding=K // 2)
+    ref_w = 0.25 + 0.5 * ref_w.permute(0, 2, 3, 1)
+    ref_b = -0.5 + 0.5 * dy.sum((0, 1, 2))
+    dw, db = outs[0]
+    assert ((dw.double() - ref_w).abs().max() / ref_w.abs().max()).item() < 1e-5
+    assert ((db.double() - ref_b).abs().max() / ref_b.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("B", [7, 1024])
+def test_head_xent_f32_matches_gemm_softmax_chain(B):
+    """The fp32 fused head (one launch: logits, softmax-xent sums, dlogits, dZ = dlogits . W * 1/keep *
+    ReLU'(h), counter + 1) vs fp64 torch of the same math."""
+    torch.manual_seed(23)
+    K, NC = 1024, 10
+    h = torch.relu(torch.randn(B, K, device=DEV))
+    w = torch.randn(NC, K, device=DEV) * 0.05
+    b = torch.randn(NC, device=DEV) * 0.1
+    lab = torch.randint(0, NC, (B,), device=DEV, dtype=torch.int32)
+    dz = torch.empty(B, K, device=DEV)
+    dl = torch.empty(B, NC, device=DEV)
+    lg = torch.empty(B, NC, device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    hits = torch.zeros(1, device=DEV, dtype=torch.int32)
+    ctr = torch.zeros(1, device=DEV, dtype=torch.int64)
+    assert ops.head_xent_f32(h, w, b, lab, dz, dl, loss, hits, logits=lg, scale=1.0 / B, inv_keep=1 / 0.75,
+                             step_counter=ctr)
+    ref = h.double() @ w.double().t() + b.double()
+    p = torch.softmax(ref, 1)
+    oh = torch.nn.functional.one_hot(lab.long(), NC).double()
+    ref_dl = (p - oh) / B
+    ref_dz = (ref_dl @ w.double()) / 0.75 * (h > 0)
+    ref_loss = (torch.logsumexp(ref, 1) - ref.gather(1, lab.long()[:, None])[:, 0]).sum()
+    assert (lg.double() - ref).abs().max().item() < 1e-4
+    assert (dl.double() - ref_dl).abs().max().item() < 1e-6
+    assert (dz.double() - ref_dz).abs().max().item() < 1e-6
+    assert abs(loss.item() - ref_loss.item()) < 1e-4 * max(1.0, abs(ref_loss.item()))
+    assert int(hits.item()) == int((ref.argmax(1) == lab.long()).sum().item())
+    assert int(ctr.item()) == 1
