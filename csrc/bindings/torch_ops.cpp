@@ -733,22 +733,29 @@ void softmax_xent(const Tensor& logits, const optional<Tensor>& labels_i, const 
 
 bool dense_head(const Tensor& feat, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
                 const optional<Tensor>& logits, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
-                const Tensor& dw, const optional<Tensor>& db, const Tensor& dfeat, double scale) {
+                const Tensor& dw, const optional<Tensor>& db, const Tensor& dfeat, double scale, bool w_fmajor,
+                bool store) {
   check_cuda(feat, "feat");
-  TORCH_CHECK(feat.scalar_type() == at::kBFloat16 && feat.dim() == 2, "dense_head: bf16 feat [B][F]");
-  const int64_t B = feat.size(0), F = feat.size(1), NC = w.size(0);
-  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == NC * F, "dense_head: fp32 w [NC][F]");
+  const bool f32 = feat.scalar_type() == at::kFloat;
+  TORCH_CHECK((f32 || feat.scalar_type() == at::kBFloat16) && feat.dim() == 2 && feat.is_contiguous(),
+              "dense_head: bf16 / fp32 feat [B][F]");
+  const int64_t B = feat.size(0), F = feat.size(1), NC = w_fmajor ? w.size(1) : w.size(0);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.dim() == 2 && w.numel() == NC * F, "dense_head: fp32 w [NC][F] / [F][NC]");
   TORCH_CHECK(y.scalar_type() == at::kFloat && y.numel() == B * NC, "dense_head: fp32 one-hot y [B][NC]");
   TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.numel() == NC * F, "dense_head: fp32 dw");
-  TORCH_CHECK(dfeat.scalar_type() == at::kBFloat16 && dfeat.numel() == B * F, "dense_head: bf16 dfeat");
+  TORCH_CHECK(dfeat.scalar_type() == feat.scalar_type() && dfeat.numel() == B * F && dfeat.is_contiguous(),
+              "dense_head: dfeat of feat's dtype [B][F]");
   TORCH_CHECK(!logits.has_value() || !logits->defined() || logits->numel() == B * NC, "dense_head: logits");
   dtfe::DenseHeadArgs a{};
-  a.feat = reinterpret_cast<const dtfe::bf16*>(feat.data_ptr());
+  a.feat = feat.data_ptr();
+  a.f32 = f32 ? 1 : 0;
+  a.w_fmajor = w_fmajor ? 1 : 0;
+  a.store = store ? 1 : 0;
   a.w = w.data_ptr<float>(); a.bias = ptr_or_null<float>(bias); a.y = y.data_ptr<float>();
   a.logits = ptr_or_null<float>(logits); a.loss_sum = ptr_or_null<float>(loss_sum);
   a.correct = ptr_or_null<int32_t>(correct);
   a.dw = dw.data_ptr<float>(); a.db = ptr_or_null<float>(db);
-  a.dfeat = reinterpret_cast<dtfe::bf16*>(dfeat.data_ptr());
+  a.dfeat = dfeat.data_ptr();
   a.B = (int)B; a.F = (int)F; a.NC = (int)NC; a.scale = (float)scale;
   return dtfe::launch_dense_head(a, cur_stream());
 }
@@ -1115,7 +1122,8 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor? acc_src=None, Tensor? acc_mask=None) -> ()");
   m.def(
       "dense_head(Tensor feat, Tensor w, Tensor? bias, Tensor y, Tensor(a!)? logits, Tensor(b!)? loss_sum,"
-      " Tensor(c!)? correct, Tensor(d!) dw, Tensor(e!)? db, Tensor(f!) dfeat, float scale) -> bool");
+      " Tensor(c!)? correct, Tensor(d!) dw, Tensor(e!)? db, Tensor(f!) dfeat, float scale, bool w_fmajor=False,"
+      " bool store=False) -> bool");
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"

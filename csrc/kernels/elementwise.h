@@ -59,10 +59,14 @@ void launch_softmax_xent(const XentArgs& a, hipStream_t s);
 // db += column sums of dlogits, dfeat = bf16(dlogits W).  Replaces the cast / GEMM / softmax /
 // GEMM / column-sum / GEMM / cast chain (7 launches).  False when it does not fit one workgroup's LDS.
 struct DenseHeadArgs {
-  const bf16* feat; const float* w; const float* bias; const float* y;  // [B][F], [NC][F], [NC], [B][NC]
+  const void* feat; const float* w; const float* bias; const float* y;  // [B][F], [NC][F], [NC], [B][NC]
   float* logits; float* loss_sum; int32_t* correct;
-  float* dw; float* db; bf16* dfeat;                                    // [NC][F] +=, [NC] +=, [B][F]
+  float* dw; float* db; void* dfeat;                                    // [NC][F] +=, [NC] +=, [B][F]
   int B, F, NC; float scale;
+  int f32;       // feat / dfeat are fp32 (else bf16)
+  int w_fmajor;  // W (and dW) stored [F][NC] (a TF Variable of shape (in, out)) instead of [NC][F]
+  int store;     // dW / db are stored, not accumulated
+  int slices;    // (set by the launcher) batch slices of the dW phase
 };
 bool launch_dense_head(const DenseHeadArgs& a, hipStream_t s);
 

@@ -3,6 +3,8 @@
 // All vectorised where the data layout allows (CDNA guide G13).
 #include "elementwise.h"
 
+#include <algorithm>
+
 namespace dtfe {
 
 // last-workgroup counter advance (see optim.hip): every workgroup has read
@@ -234,35 +236,67 @@ void launch_softmax_xent(const XentArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(softmax_xent_kernel, dim3((a.B + 3) / 4), dim3(256), 0, s, a);
 }
 
+// F32: fp32 features / feature gradient (the LSTM's fp32 head), else bf16 (ResNet's pooled features);
+// WFM: W and dW are [F][NC] (the LSTM's Variable (128, 10)), else [NC][F].
+// One 1024-thread workgroup, every phase spread so that no thread runs a long dependent chain (the
+// first form - one output per thread, 128-long fmaf chains over LDS - took 20-24 us, latency-bound):
+//   logits   thread = (row, class): 16-B reads of the feature and weight rows, four independent
+//            fmaf chains (features f = 4i + e), summed pairwise
+//   softmax  one thread per row (softmax_xent_kernel's expressions)
+//   dW, db   thread = (class c, 4 features, batch slice): 16-B feature reads, 4 independent chains,
+//            the slices summed in a fixed order through LDS
+//   dfeat    thread = (row, 4 or 8 features): NC fmaf each, one 16-B store
+constexpr int DH_NCMAX = 16;
+template <bool F32, bool WFM>
 __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
   extern __shared__ float hsm[];
-  const int B = a.B, F = a.F, NC = a.NC, FP = F + 1, tid = threadIdx.x;
-  float* sf = hsm;             // [B][F+1] features (fp32; padded rows: conflict-free column walks)
-  float* sw = sf + B * FP;     // [NC][F+1] weights
+  const int B = a.B, F = a.F, NC = a.NC, FP = F + 4, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float* sf = hsm;             // [B][F+4] features (fp32; 16-B aligned rows)
+  float* sw = sf + B * FP;     // [NC][F+4] weights
   float* sd = sw + NC * FP;    // [B][NC] logits, then dlogits
-  float* red = sd + B * NC;    // [2][32] block-reduce scratch
-  // features as 16-B chunks (F % 8 == 0, host-checked): 8 values per load instead of one 2-byte load each
-  const int CPR = F >> 3;
+  float* red = sd + B * NC;    // [2][32] block-reduce scratch, then the dW slice partials
+  constexpr int EPC = F32 ? 4 : 8;
+  const int CPR = F / EPC;
   for (int i = tid; i < B * CPR; i += 1024) {
-    const int b = i / CPR, f0 = (i - b * CPR) * 8;
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.feat + (long)i * 8);
+    const int b = i / CPR, f0 = (i - b * CPR) * EPC;
+    if constexpr (F32) {
+      *reinterpret_cast<f32x4_t*>(sf + b * FP + f0) = reinterpret_cast<const f32x4_t*>(a.feat)[i];
+    } else {
+      const u32x4_t v = reinterpret_cast<const u32x4_t*>(a.feat)[i];
+      f32x4_t lo, hi;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      sf[b * FP + f0 + 2 * e] = __uint_as_float(v[e] << 16);
-      sf[b * FP + f0 + 2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+      for (int e = 0; e < 2; ++e) {
+        lo[2 * e] = __uint_as_float(v[e] << 16);
+        lo[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+        hi[2 * e] = __uint_as_float(v[2 + e] << 16);
+        hi[2 * e + 1] = __uint_as_float(v[2 + e] & 0xffff0000u);
+      }
+      *reinterpret_cast<f32x4_t*>(sf + b * FP + f0) = lo;
+      *reinterpret_cast<f32x4_t*>(sf + b * FP + f0 + 4) = hi;
     }
   }
   for (int i = tid; i < NC * F; i += 1024) {
-    const int c = i / F, f = i - c * F;
-    sw[c * FP + f] = a.w[i];
+    if constexpr (WFM) {
+      const int f = i / NC, c = i - f * NC;
+      sw[c * FP + f] = a.w[i];
+    } else {
+      const int c = i / F, f = i - c * F;
+      sw[c * FP + f] = a.w[i];
+    }
   }
   __syncthreads();
-  for (int o = tid; o < B * NC; o += 1024) {
+  for (int o = tid; o < B * NC; o += 1024) {  // logits: 16-B row reads, four independent fmaf chains
     const int b = o / NC, c = o - b * NC;
-    float acc = a.bias ? a.bias[c] : 0.f;
-    for (int f = 0; f < F; ++f) acc = __builtin_fmaf(sf[b * FP + f], sw[c * FP + f], acc);
-    sd[o] = acc;
-    if (a.logits) a.logits[o] = acc;
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < F; f += 4) {
+      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(sf + b * FP + f);
+      const f32x4_t w = *reinterpret_cast<const f32x4_t*>(sw + c * FP + f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(x[e], w[e], acc[e]);
+    }
+    const float v = (acc[0] + acc[1]) + (acc[2] + acc[3]) + (a.bias ? a.bias[c] : 0.f);
+    sd[o] = v;
+    if (a.logits) a.logits[o] = v;
   }
   __syncthreads();
   // rows: softmax_xent_kernel's expressions (first-max argmax, lse, loss, (p - y) * scale)
@@ -288,9 +322,9 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
   }
   loss = wave_sum(loss);
   hits = wave_sum(hits);
-  if ((tid & 63) == 0) {
-    red[tid >> 6] = loss;
-    red[32 + (tid >> 6)] = hits;
+  if (lane == 0) {
+    red[wid] = loss;
+    red[32 + wid] = hits;
   }
   __syncthreads();
   if (tid == 0) {
@@ -302,37 +336,85 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
     if (a.loss_sum) atomicAdd(a.loss_sum, tl);
     if (a.correct) atomicAdd(a.correct, (int)th);
   }
-  for (int o = tid; o < NC * F; o += 1024) {  // dW[c][f] += sum_b dlogits[b][c] feat[b][f]
-    const int c = o / F, f = o - c * F;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc = __builtin_fmaf(sd[b * NC + c], sf[b * FP + f], acc);
-    a.dw[o] += acc;
+  __syncthreads();  // (red is reused below)
+  // dW[c][f..f+3] over a batch slice: items (c, f4) x S slices, S = 1024 / (NC * F / 4) (<= 8)
+  const int F4 = F / 4, NI = NC * F4, S = a.slices;
+  float* part = red + 64;  // [S][NI][4] (S > 1)
+  for (int t = tid; t < NI * S; t += 1024) {
+    const int s = t / NI, it = t - s * NI, c = it / F4, f = (it - c * F4) * 4;
+    const int b0 = s * B / S, b1 = (s + 1) * B / S;
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    for (int b = b0; b < b1; ++b) {
+      const float d = sd[b * NC + c];
+      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(sf + b * FP + f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(d, x[e], acc[e]);
+    }
+    if (S > 1) {
+      *reinterpret_cast<f32x4_t*>(part + ((long)s * NI + it) * 4) = acc;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long o = WFM ? (long)(f + e) * NC + c : (long)c * F + f + e;
+        a.dw[o] = a.store ? acc[e] : a.dw[o] + acc[e];
+      }
+    }
   }
   if (tid < NC && a.db) {
     float acc = 0.f;
     for (int b = 0; b < B; ++b) acc += sd[b * NC + tid];
-    a.db[tid] += acc;
+    a.db[tid] = a.store ? acc : a.db[tid] + acc;
   }
-  for (int i = tid; i < B * CPR; i += 1024) {  // dfeat = dlogits W, 8 values per 16-B store
-    const int b = i / CPR, f0 = (i - b * CPR) * 8;
-    float acc[8] = {};
+  __syncthreads();
+  for (int it = tid; it < (S > 1 ? NI : 0); it += 1024) {
+    f32x4_t g = *reinterpret_cast<const f32x4_t*>(part + (long)it * 4);
+    for (int s = 1; s < S; ++s) g += *reinterpret_cast<const f32x4_t*>(part + ((long)s * NI + it) * 4);
+    const int c = it / F4, f = (it - c * F4) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long o = WFM ? (long)(f + e) * NC + c : (long)c * F + f + e;
+      a.dw[o] = a.store ? g[e] : a.dw[o] + g[e];
+    }
+  }
+  for (int i = tid; i < B * CPR; i += 1024) {  // dfeat = dlogits W, one 16-B store per chunk
+    const int b = i / CPR, f0 = (i - b * CPR) * EPC;
+    float acc[EPC] = {};
     for (int c = 0; c < NC; ++c) {
       const float dl = sd[b * NC + c];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] = __builtin_fmaf(dl, sw[c * FP + f0 + e], acc[e]);
+      for (int e = 0; e < EPC; ++e) acc[e] = __builtin_fmaf(dl, sw[c * FP + f0 + e], acc[e]);
     }
-    u32x4_t o;
+    if constexpr (F32) {
+      reinterpret_cast<f32x4_t*>(a.dfeat)[i] = f32x4_t{acc[0], acc[1], acc[2], acc[3]};
+    } else {
+      u32x4_t o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[2 * e], acc[2 * e + 1]);
-    *reinterpret_cast<u32x4_t*>(a.dfeat + (long)i * 8) = o;
+      for (int e = 0; e < 4; ++e) o[e] = pack_bf16x2(acc[2 * e], acc[2 * e + 1]);
+      reinterpret_cast<u32x4_t*>(a.dfeat)[i] = o;
+    }
   }
 }
 
 bool launch_dense_head(const DenseHeadArgs& a, hipStream_t s) {
-  const size_t lds = ((size_t)(a.B + a.NC) * (a.F + 1) + (size_t)a.B * a.NC + 64) * sizeof(float);
-  if (lds > 150 * 1024 || a.NC > 64 || a.F % 8 || !a.dw || !a.dfeat) return false;
-  (void)hipFuncSetAttribute((const void*)dense_head_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(dense_head_kernel, dim3(1), dim3(1024), lds, s, a);
+  // LDS: features + weights [.][F+4], logits [B][NC], 64 reduce floats, dW slice partials (S x NI x 4)
+  const long ni = (long)a.NC * (a.F / 4), base = ((long)(a.B + a.NC) * (a.F + 4) + (long)a.B * a.NC + 64) * 4;
+  long sl = ni >= 1024 ? 1 : std::min<long>(8, 1024 / ni);
+  while (sl > 1 && base + sl * ni * 16 > 150 * 1024) --sl;
+  const size_t lds = (size_t)(base + (sl > 1 ? sl * ni * 16 : 0));
+  if (lds > 150 * 1024 || a.NC > DH_NCMAX || a.F % 8 || !a.dw || !a.dfeat) return false;
+  DenseHeadArgs ad = a;
+  ad.slices = (int)sl;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(1), dim3(1024), lds, s, ad);
+  };
+  if (a.f32) {
+    if (a.w_fmajor) go(dense_head_kernel<true, true>);
+    else go(dense_head_kernel<true, false>);
+  } else {
+    if (a.w_fmajor) go(dense_head_kernel<false, true>);
+    else go(dense_head_kernel<false, false>);
+  }
   return true;
 }
 

@@ -98,12 +98,18 @@ class LstmProgram(StepProgram):
     def _persistent(self):
         return self.device.type == "cuda" and os.environ.get("DTFE_LSTM_PERSIST", "1") != "0"
 
-    def forward(self):
+    def forward(self, head=False):
+        """``head`` (compute_grads, GPU): the classifier head forward + backward as ONE single-workgroup
+        launch (ops.dense_head: logits, softmax-xent, dW_out / db_out stored, dh) instead of the head
+        GEMM, softmax_xent and two gradient GEMMs; returns whether it ran."""
         B = self.batch_size
         if self._persistent() and ops.require().lstm_seq_fwd(self.xh, self.K, self.b, 1.0, self.act, self.c,
                                                                self.hT):
+            if head and ops.dense_head(self.hT, self.Wo, self.bo, self.y, self.logits, self.loss, self.correct,
+                                       self.gWo, self.gbo, self.dh, 1.0 / B, w_fmajor=True, store=True):
+                return True
             ops.gemm(self.hT, self.Wo, self.logits, M=B, N=NC, K=H, bmode=ops.RMAJ, ldb=NC, bias=self.bo)
-            return
+            return False
         for t in range(T):
             ops.gemm(self.xh[t], self.K, self.gates[t], M=B, N=4 * H, K=I + H, bmode=ops.RMAJ, ldb=4 * H,
                      bias=self.b)
@@ -122,12 +128,13 @@ class LstmProgram(StepProgram):
             self.loss.zero_()
             self.correct.zero_()
         self._acc_cleared = False
-        self.forward()
-        ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
-                         correct=self.correct)
-        ops.gemm(self.hT, self.dlogits, self.gWo, M=H + 1, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ,
-                 ldb=NC, a_ones_row=H, bias_out=self.gbo)
-        ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
+        fused = self.forward(head=True)
+        if not fused:
+            ops.softmax_xent(self.logits, labels_oh=self.y, scale=1.0 / B, dlogits=self.dlogits, loss_sum=self.loss,
+                             correct=self.correct)
+            ops.gemm(self.hT, self.dlogits, self.gWo, M=H + 1, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ,
+                     ldb=NC, a_ones_row=H, bias_out=self.gbo)
+            ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
         if self._persistent() and ops.require().lstm_seq_bwd(self.K, self.act, self.c, self.dh, self.dg, I):
             pass  # whole BPTT recurrence in one launch (dc / dh stay on chip)
         else:

@@ -818,23 +818,36 @@ def mse_sigmoid(y, t, loss, dz):
     dz.copy_(2 * d / n * y * (1 - y))
 
 
-def dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale) -> bool:
+def dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale, w_fmajor=False,
+               store=False) -> bool:
     """A small dense classifier head, forward and backward in one launch (GPU: one workgroup; False when
     it does not fit): logits = feat W^T + b, softmax cross-entropy against one-hot y (loss_sum +=,
     correct +=), dlogits = (p - y) * scale, dw += dlogits^T feat, db += column sums, dfeat16 =
-    bf16(dlogits W).  The CPU path is the fp32 oracle."""
+    dlogits W (in feat's dtype: bf16 or fp32).  ``w_fmajor``: W and dw are [F][NC] (a TF Variable of
+    shape (in, out)) instead of [NC][F]; ``store``: dw / db are stored, not accumulated.  The CPU path
+    is the fp32 oracle."""
     if feat16.is_cuda:
-        return bool(require().dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale))
+        return bool(require().dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale,
+                                         w_fmajor, store))
     f = feat16.float()
-    lg = f @ w.float().t() + (bias.float() if bias is not None else 0.0)
+    wf = w.float().t() if w_fmajor else w.float()   # [NC][F]
+    lg = f @ wf.t() + (bias.float() if bias is not None else 0.0)
     if logits is not None:
         logits.copy_(lg)
     dl = torch.empty_like(lg)
     softmax_xent(lg, labels_oh=y, scale=scale, dlogits=dl, loss_sum=loss_sum, correct=correct)
-    dw += dl.t() @ f
+    g = dl.t() @ f
+    g = g.t() if w_fmajor else g
+    if store:
+        dw.copy_(g)
+    else:
+        dw += g
     if db is not None:
-        db += dl.sum(0)
-    dfeat16.copy_((dl @ w.float()).to(dfeat16.dtype))
+        if store:
+            db.copy_(dl.sum(0))
+        else:
+            db += dl.sum(0)
+    dfeat16.copy_((dl @ wf).to(dfeat16.dtype))
     return True
 
 

@@ -57,3 +57,28 @@ def test_dense_head_cpu_oracle():
     lg_r, loss_r, hits_r, dw_r, db_r, df_r = _unfused(feat16, w, b, y, B, 1.0 / B)
     assert torch.allclose(logits, lg_r) and torch.allclose(loss, loss_r) and int(hits) == int(hits_r)
     assert torch.allclose(dw, dw_r) and torch.allclose(db, db_r) and torch.equal(dfeat, df_r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,F,NC", [(128, 128, 10), (40, 64, 10)])
+def test_dense_head_fp32_fmajor_store_matches_unfused_gpu(B, F, NC):
+    """The LSTM's head form: fp32 features and feature gradient, W / dW laid out [F][NC] (TF Variable
+    (in, out)), dW / db stored (not accumulated) - against the unfused fp32 chain."""
+    torch.manual_seed(2)
+    d = "cuda"
+    feat = torch.randn(B, F, device=d)
+    w_fnc, b = torch.randn(F, NC, device=d) * 0.2, torch.randn(NC, device=d) * 0.1
+    y = torch.nn.functional.one_hot(torch.randint(0, NC, (B,), device=d), NC).float()
+    logits, loss, hits = torch.empty(B, NC, device=d), torch.zeros(1, device=d), torch.zeros(1, dtype=torch.int32, device=d)
+    dw, db, dfeat = torch.full((F, NC), 9.0, device=d), torch.full((NC,), 9.0, device=d), torch.empty(B, F, device=d)
+    assert ops.dense_head(feat, w_fnc, b, y, logits, loss, hits, dw, db, dfeat, 1.0 / B, w_fmajor=True, store=True)
+    w = w_fnc.t().contiguous()
+    lg_r = feat @ w.t() + b
+    dl = torch.empty_like(lg_r)
+    loss_r, hits_r = torch.zeros(1, device=d), torch.zeros(1, dtype=torch.int32, device=d)
+    ops.softmax_xent(lg_r, labels_oh=y, scale=1.0 / B, dlogits=dl, loss_sum=loss_r, correct=hits_r)
+    assert torch.allclose(logits, lg_r, atol=1e-4, rtol=1e-5)
+    assert torch.allclose(loss, loss_r, rtol=1e-5) and int(hits) == int(hits_r)
+    assert torch.allclose(dw, (dl.t() @ feat).t(), atol=1e-5, rtol=1e-4)
+    assert torch.allclose(db, dl.sum(0), atol=1e-6, rtol=1e-4)
+    assert torch.allclose(dfeat, dl @ w, atol=1e-6, rtol=1e-4)
