@@ -23,6 +23,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dtfe {
 
@@ -236,9 +237,13 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
 // graph replays - never match, so nothing is reset between launches.  Polls are bounded by a
 // wall-clock timeout that sets an error word instead of hanging.  All 4 * B/16 workgroups must
 // be co-resident (one 512-thread workgroup per CU, <= 256): checked at launch.
-constexpr int NS = 4;
-constexpr int SPT = 512;  // 8 waves
+// NS = 8 (round 6): 8 workgroups of 256 threads per row group, each owning 16 units - half the MFMA
+// work per step and per CU (4 waves, one per SIMD) for the same exchange; used where the grid of
+// B/16 x 8 workgroups fits (B <= 512), NS = 4 above that.
+constexpr int NS_MAX = 8;
 constexpr int MAX_GROUPS = 64;
+template <int NS>
+constexpr int split_threads() { return LR * 128 / NS; }  // one thread per (row, unit) of the slice (H = 128)
 
 struct SplitSync {
   unsigned long long* llf;  // [MAX_GROUPS][2][16][H]   forward h exchange
@@ -292,6 +297,7 @@ __device__ __forceinline__ void finish_launch(const SplitSync& y) {
 // (row group, split) of this workgroup.  Workgroups are dealt to the 8 XCDs round-robin by id, so
 // with a multiple of 8 row groups the NS workgroups of one group - the ones that exchange h / dh
 // every step - get ids rg, rg + G, ... and sit on ONE XCD (its L2); otherwise consecutive ids.
+template <int NS>
 __device__ __forceinline__ void split_coords(int groups, int& rg, int& sp) {
   if (groups % 8 == 0) {
     rg = blockIdx.x % groups;
@@ -308,26 +314,29 @@ __device__ __forceinline__ unsigned launch_base(const SplitSync& y) {
 
 // forward: A = [x_t | h_{t-1}] (16 x 156, LDS) . K[:, my 128 gate columns] (each wave one 16-column
 // tile, its 39 k-steps of B fragments in VGPRs for all T steps) on v_mfma_f32_16x16x4_f32.
-template <int H, int KT4>
-__global__ __launch_bounds__(SPT) void lstm_split_fwd_kernel(LstmSeqArgs a, SplitSync y) {
-  constexpr int G4 = 4 * H, UPW = H / NS;  // units per workgroup (32)
-  constexpr int GC = 4 * UPW;              // gate columns per workgroup (128)
+template <int H, int KT4, int NS>
+__global__ __launch_bounds__(LR * H / NS) void lstm_split_fwd_kernel(LstmSeqArgs a, SplitSync y) {
+  constexpr int SPT = LR * H / NS;         // one thread per (row, unit) of the slice: 512 / 256
+  constexpr int G4 = 4 * H, UPW = H / NS;  // units per workgroup (32 / 16)
+  constexpr int GC = 4 * UPW;              // gate columns per workgroup (128 / 64) = one 16-wide tile per wave
   constexpr int GP = GC + 4;
-  constexpr int HW = LR * H / SPT;         // exchanged h words per thread (4)
+  constexpr int HW = LR * H / SPT;         // exchanged h words per thread (NS)
+  constexpr int TPG = UPW / 16;            // unit tiles per gate (2 / 1)
+  static_assert(GC / 16 == SPT / 64, "one gate-column tile per wave");
   extern __shared__ float lds[];
   const int I = a.I, KT = I + H, AP = KT + 1;
   float* As = lds;            // [16][AP]
   float* Gs = lds + 16 * AP;  // [16][GP] activated gates of my columns (gate-major: gi * UPW + u)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int rg, sp;
-  split_coords(a.B / LR, rg, sp);
+  split_coords<NS>(a.B / LR, rg, sp);
   const int r0 = rg * LR, B = a.B;
   const unsigned base = launch_base(y);
   const long rowKT = KT;
   unsigned long long* llg = y.llf + (long)rg * 2 * LR * H;
   const int mrow = lane & 15, g = lane >> 4;
-  // wave w: gate gi = w / 2, units 16 * (w & 1) .. +16 of my slice
-  const int gi = w >> 1, ul = 16 * (w & 1) + mrow, col = gi * H + sp * UPW + ul;  // global gate column
+  // wave w: gate gi = w / TPG, units 16 * (w % TPG) .. +16 of my slice
+  const int gi = w / TPG, ul = 16 * (w % TPG) + mrow, col = gi * H + sp * UPW + ul;  // global gate column
   float kreg[KT4];
 #pragma unroll
   for (int kk = 0; kk < KT4; ++kk) kreg[kk] = a.K[(long)(4 * kk + g) * G4 + col];
@@ -335,14 +344,26 @@ __global__ __launch_bounds__(SPT) void lstm_split_fwd_kernel(LstmSeqArgs a, Spli
   // cell update ownership: thread -> (row, unit) of my 16 x 32 slice
   const int cr = tid / UPW, cu = tid - cr * UPW;
   float creg = 0.f;
-  // x_t: one element per thread (LR * I = 448 <= 512), prefetched a step ahead so its load latency
-  // is off the recurrence's critical path
-  const int xr = tid / I, xk = tid - xr * I;
-  const bool xo = tid < LR * I;
-  float xv = xo ? a.xh[((long)r0 + xr) * rowKT + xk] : 0.f;
+  // x_t: XPT elements per thread (LR * I = 448), prefetched a step ahead so their load latency is
+  // off the recurrence's critical path
+  constexpr int XPT = (LR * 28 + SPT - 1) / SPT;
+  int xr[XPT], xk[XPT];
+  bool xo[XPT];
+  float xv[XPT];
+#pragma unroll
+  for (int j = 0; j < XPT; ++j) {
+    const int e = tid + j * SPT;
+    xo[j] = e < LR * I;
+    xr[j] = xo[j] ? e / I : 0;
+    xk[j] = xo[j] ? e - xr[j] * I : 0;
+    xv[j] = xo[j] ? a.xh[((long)r0 + xr[j]) * rowKT + xk[j]] : 0.f;
+  }
   for (int t = 0; t < a.T; ++t) {
-    if (xo) As[xr * AP + xk] = xv;
-    if (xo && t + 1 < a.T) xv = a.xh[((long)(t + 1) * B + r0 + xr) * rowKT + xk];
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) {
+      if (xo[j]) As[xr[j] * AP + xk[j]] = xv[j];
+      if (xo[j] && t + 1 < a.T) xv[j] = a.xh[((long)(t + 1) * B + r0 + xr[j]) * rowKT + xk[j]];
+    }
     if (t == 0) {
       for (int e = tid; e < LR * H; e += SPT) As[(e / H) * AP + I + e % H] = a.xh[((long)r0 + e / H) * rowKT + I + e % H];
     } else {
@@ -395,28 +416,31 @@ __global__ __launch_bounds__(SPT) void lstm_split_fwd_kernel(LstmSeqArgs a, Spli
 // . K_h[:, my columns]^T (8 waves = 8 unit tiles, 32 k4-steps) goes to the exchange, and each
 // thread sums the 4 partials of its (row, unit) in a fixed order - 4 words per thread per step
 // instead of gathering all 512 dgate columns.
-template <int H>
-__global__ __launch_bounds__(SPT) void lstm_split_bwd_kernel(LstmSeqArgs a, SplitSync y) {
-  constexpr int G4 = 4 * H, UPW = H / NS, GC = 4 * UPW;  // my gate columns (128) = 32 k4-steps
+template <int H, int NS>
+__global__ __launch_bounds__(LR * H / NS) void lstm_split_bwd_kernel(LstmSeqArgs a, SplitSync y) {
+  constexpr int SPT = LR * H / NS;
+  constexpr int G4 = 4 * H, UPW = H / NS, GC = 4 * UPW;  // my gate columns (128 / 64) = 32 / 16 k4-steps
   constexpr int DP = GC + 4;
+  constexpr int TPW = (H / 16) / (SPT / 64);              // dh unit tiles per wave (1 / 2)
   extern __shared__ float lds[];
   float* DG = lds;  // [2][16][DP] my dgates of step t (parity-double-buffered: one barrier per step)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int rg, sp;
-  split_coords(a.B / LR, rg, sp);
+  split_coords<NS>(a.B / LR, rg, sp);
   const int r0 = rg * LR, B = a.B;
   const unsigned base = launch_base(y);
-  unsigned long long* llg = y.llb + (long)rg * 2 * NS * LR * H;  // [2][NS src][16][H]
+  unsigned long long* llg = y.llb + (long)rg * 2 * NS * LR * H;  // [2][NS src][16][H] (groups at NS_MAX pitch below)
   const int mrow = lane & 15, g = lane >> 4;
   // B fragments: B[k = j][n = u] = K[I + u][col(j)], j = my gate column q * UPW + v -> q * H + sp * UPW + v,
-  // u = 16 w + mrow (wave w = unit tile w)
-  float kb[GC / 4];
-  {
-    const float* krow = a.K + (long)(a.I + 16 * w + mrow) * G4 + sp * UPW;
+  // u = 16 (w TPW + tt) + mrow (wave w = unit tiles w TPW .. + TPW)
+  float kb[TPW][GC / 4];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    const float* krow = a.K + (long)(a.I + 16 * (w * TPW + tt) + mrow) * G4 + sp * UPW;
 #pragma unroll
     for (int kk = 0; kk < GC / 4; ++kk) {
       const int j = 4 * kk + g;
-      kb[kk] = krow[(j / UPW) * H + j % UPW];
+      kb[tt][kk] = krow[(j / UPW) * H + j % UPW];
     }
   }
   const int cr = tid / UPW, cu = tid - cr * UPW, u = sp * UPW + cu;
@@ -453,16 +477,28 @@ __global__ __launch_bounds__(SPT) void lstm_split_bwd_kernel(LstmSeqArgs a, Spli
     }
     if (t == 0) break;
     __syncthreads();
-    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc[TPW];
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) acc[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     const float* drow = D + mrow * DP;
 #pragma unroll
-    for (int kk = 0; kk < GC / 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(drow[4 * kk + g], kb[kk], acc, 0, 0, 0);
+    for (int kk = 0; kk < GC / 4; ++kk) {
+      const float av = drow[4 * kk + g];
+#pragma unroll
+      for (int tt = 0; tt < TPW; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, kb[tt][kk], acc[tt], 0, 0, 0);
+    }
     unsigned long long* slot = llg + (long)(t & 1) * NS * LR * H;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) ll_put(slot + ((long)sp * LR + 4 * g + e) * H + 16 * w + mrow, acc[e], base + t + 1);
+    for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        ll_put(slot + ((long)sp * LR + 4 * g + e) * H + 16 * (w * TPW + tt) + mrow, acc[tt][e], base + t + 1);
     float pv[NS];
     ll_get<NS>(slot + (long)cr * H + u, (long)LR * H, base + t + 1, pv, y.err);
-    dh = ((pv[0] + pv[1]) + pv[2]) + pv[3];
+    float s = pv[0];  // the NS partials in a fixed order
+#pragma unroll
+    for (int q = 1; q < NS; ++q) s += pv[q];
+    dh = s;
   }
   finish_launch(y);
 }
@@ -472,7 +508,7 @@ char* g_split_buf[64] = {};
 SplitSync split_sync(hipStream_t s, int H) {
   char** buf = g_split_buf;
   constexpr size_t CTL = 4096;
-  const size_t fw = (size_t)MAX_GROUPS * 2 * LR * 128, bw = fw * NS;  // words, H = 128
+  const size_t fw = (size_t)MAX_GROUPS * 2 * LR * 128, bw = fw * NS_MAX;  // words, H = 128
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (H != 128 || dev < 0 || dev >= 64) return SplitSync{};
@@ -496,20 +532,24 @@ SplitSync split_sync(hipStream_t s, int H) {
 
 // every workgroup of a split launch must be resident at once (they exchange h every step): the
 // grid must fit the occupancy the runtime reports for this kernel and LDS size, times the CUs
-bool co_resident(const void* kern, size_t lds, int blocks) {
+bool co_resident(const void* kern, int threads, size_t lds, int blocks) {
   int dev = 0, per_cu = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SPT, lds) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) return false;
   return per_cu >= 1 && (long)per_cu * cus >= blocks;
 }
 
-bool split_ok(const LstmSeqArgs& a) {
-  const char* e = getenv("DTFE_LSTM_SPLIT");  // read per launch (tests A/B both paths in one process)
-  const bool on = !(e && atoi(e) == 0);
+// workgroups per row group of the split kernels: 0 = no split.  DTFE_LSTM_SPLIT (read per launch: tests A/B
+// the paths in one process): 0 off, 4 / 8 force that split, unset / 1 = 8 where B/16 x 8 <= 256, else 4.
+int split_ns(const LstmSeqArgs& a) {
+  const char* e = getenv("DTFE_LSTM_SPLIT");
+  const int v = e ? atoi(e) : 1;
   // one workgroup per CU, all co-resident: <= 256 workgroups; exchange buffers sized for MAX_GROUPS
-  return on && a.H == 128 && a.I == 28 && a.B % LR == 0 && a.B / LR <= MAX_GROUPS && (a.B / LR) * NS <= 256 &&
-         a.T < 255;
+  if (v == 0 || a.H != 128 || a.I != 28 || a.B % LR != 0 || a.B / LR > MAX_GROUPS || a.T >= 255) return 0;
+  const int groups = a.B / LR;
+  if (v != 4 && groups * 8 <= 256) return 8;
+  return groups * 4 <= 256 ? 4 : 0;
 }
 
 }  // namespace
@@ -531,16 +571,19 @@ int lstm_split_status(bool reset) {
 bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
   // register-resident K slice: instantiated for the MNIST row-LSTM (I = 28, H = 128)
   if (a.H != 128 || a.I != 28 || a.B % LR || LR * a.I > 1024) return false;
-  if (split_ok(a)) {
+  if (const int ns = split_ns(a)) {
     const SplitSync y = split_sync(s, a.H);
     if (y.llf) {
-      const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (a.H + 4)) * sizeof(float);
-      auto k = lstm_split_fwd_kernel<128, (28 + 128) / 4>;
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (co_resident((const void*)k, lds, a.B / LR * NS)) {
+      auto go = [&](auto nsc) {
+        constexpr int NS = decltype(nsc)::value, SPT = split_threads<NS>();
+        const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * (a.H / NS) + 4)) * sizeof(float);
+        auto k = lstm_split_fwd_kernel<128, (28 + 128) / 4, NS>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (!co_resident((const void*)k, SPT, lds, a.B / LR * NS)) return false;
         hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
         return true;
-      }
+      };
+      if (ns == 8 ? go(std::integral_constant<int, 8>{}) : go(std::integral_constant<int, 4>{})) return true;
     }
   }
   const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * a.H + 4)) * sizeof(float);
@@ -552,16 +595,19 @@ bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
 
 bool launch_lstm_seq_bwd(const LstmSeqArgs& a, hipStream_t s) {
   if (a.H != 128 || a.B % LR || (a.I + a.H) % 4) return false;
-  if (split_ok(a)) {
+  if (const int ns = split_ns(a)) {
     const SplitSync y = split_sync(s, a.H);
     if (y.llf) {
-      const size_t lds = (size_t)2 * 16 * (4 * (a.H / NS) + 4) * sizeof(float);
-      auto k = lstm_split_bwd_kernel<128>;
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (co_resident((const void*)k, lds, a.B / LR * NS)) {
+      auto go = [&](auto nsc) {
+        constexpr int NS = decltype(nsc)::value, SPT = split_threads<NS>();
+        const size_t lds = (size_t)2 * 16 * (4 * (a.H / NS) + 4) * sizeof(float);
+        auto k = lstm_split_bwd_kernel<128, NS>;
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (!co_resident((const void*)k, SPT, lds, a.B / LR * NS)) return false;
         hipLaunchKernelGGL(k, dim3(a.B / LR * NS), dim3(SPT), lds, s, a, y);
         return true;
-      }
+      };
+      if (ns == 8 ? go(std::integral_constant<int, 8>{}) : go(std::integral_constant<int, 4>{})) return true;
     }
   }
   const size_t lds = ((size_t)LR * (4 * a.H + 4) + 2 * (size_t)LR * a.H) * sizeof(float);

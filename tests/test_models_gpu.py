@@ -99,11 +99,12 @@ def test_lstm_trains_on_gpu_with_graph():
     assert last < 0.5 * first, (first, last)
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("split", ["1", "4", "0"])
 @pytest.mark.parametrize("batch", [128, 48, 1024])
 def test_lstm_persistent_matches_per_step(batch, split, monkeypatch):
-    """Persistent whole-sequence kernels (lstm_seq.hip; split=1: each row group over 4 CUs with a
-    per-step flag exchange, split=0: one CU per row group) vs the per-step cell kernels + GEMMs:
+    """Persistent whole-sequence kernels (lstm_seq.hip; split=1: each row group over 8 CUs (B <= 512) or
+    4 CUs with a per-step flag exchange, split=4: forced 4, split=0: one CU per row group) vs the
+    per-step cell kernels + GEMMs:
     forward activations, cell states, logits, and every gradient."""
     model = LstmModel()
     g = torch.Generator().manual_seed(3)
