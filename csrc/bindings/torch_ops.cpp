@@ -733,8 +733,8 @@ void softmax_xent(const Tensor& logits, const optional<Tensor>& labels_i, const 
 
 bool dense_head(const Tensor& feat, const Tensor& w, const optional<Tensor>& bias, const Tensor& y,
                 const optional<Tensor>& logits, const optional<Tensor>& loss_sum, const optional<Tensor>& correct,
-                const Tensor& dw, const optional<Tensor>& db, const Tensor& dfeat, double scale, bool w_fmajor,
-                bool store) {
+                const Tensor& dw, const optional<Tensor>& db, const optional<Tensor>& dfeat, double scale,
+                bool w_fmajor, bool store, const optional<Tensor>& dl_out) {
   check_cuda(feat, "feat");
   const bool f32 = feat.scalar_type() == at::kFloat;
   TORCH_CHECK((f32 || feat.scalar_type() == at::kBFloat16) && feat.dim() == 2 && feat.is_contiguous(),
@@ -743,8 +743,12 @@ bool dense_head(const Tensor& feat, const Tensor& w, const optional<Tensor>& bia
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.dim() == 2 && w.numel() == NC * F, "dense_head: fp32 w [NC][F] / [F][NC]");
   TORCH_CHECK(y.scalar_type() == at::kFloat && y.numel() == B * NC, "dense_head: fp32 one-hot y [B][NC]");
   TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.numel() == NC * F, "dense_head: fp32 dw");
-  TORCH_CHECK(dfeat.scalar_type() == feat.scalar_type() && dfeat.numel() == B * F && dfeat.is_contiguous(),
+  const bool has_df = dfeat.has_value() && dfeat->defined();
+  TORCH_CHECK(!has_df || (dfeat->scalar_type() == feat.scalar_type() && dfeat->numel() == B * F && dfeat->is_contiguous()),
               "dense_head: dfeat of feat's dtype [B][F]");
+  TORCH_CHECK(!dl_out.has_value() || !dl_out->defined() ||
+                  (dl_out->scalar_type() == at::kFloat && dl_out->numel() == B * NC && dl_out->is_contiguous()),
+              "dense_head: dl_out fp32 [B][NC]");
   TORCH_CHECK(!logits.has_value() || !logits->defined() || logits->numel() == B * NC, "dense_head: logits");
   dtfe::DenseHeadArgs a{};
   a.feat = feat.data_ptr();
@@ -755,7 +759,8 @@ bool dense_head(const Tensor& feat, const Tensor& w, const optional<Tensor>& bia
   a.logits = ptr_or_null<float>(logits); a.loss_sum = ptr_or_null<float>(loss_sum);
   a.correct = ptr_or_null<int32_t>(correct);
   a.dw = dw.data_ptr<float>(); a.db = ptr_or_null<float>(db);
-  a.dfeat = dfeat.data_ptr();
+  a.dfeat = has_df ? dfeat->data_ptr() : nullptr;
+  a.dl_out = ptr_or_null<float>(dl_out);
   a.B = (int)B; a.F = (int)F; a.NC = (int)NC; a.scale = (float)scale;
   return dtfe::launch_dense_head(a, cur_stream());
 }
@@ -844,7 +849,7 @@ bool lstm_seq_fwd(const Tensor& xh, const Tensor& K, const Tensor& bias, double 
 int64_t lstm_status(bool reset) { return dtfe::lstm_split_status(reset); }
 
 bool lstm_seq_bwd(const Tensor& K, const Tensor& act, const Tensor& c, const Tensor& dhT, const Tensor& dg,
-                  int64_t I) {
+                  int64_t I, const optional<Tensor>& dl, const optional<Tensor>& wo) {
   check_cuda(act, "act");
   dtfe::LstmSeqArgs a{};
   a.T = (int)c.size(0); a.B = (int)c.size(1); a.H = (int)c.size(2); a.I = (int)I;
@@ -853,6 +858,12 @@ bool lstm_seq_bwd(const Tensor& K, const Tensor& act, const Tensor& c, const Ten
               dhT.numel() == (int64_t)a.B * a.H, "lstm_seq_bwd: shapes");
   a.K = K.data_ptr<float>(); a.act = act.data_ptr<float>(); a.c = c.data_ptr<float>();
   a.dhT = dhT.data_ptr<float>(); a.dg = dg.data_ptr<float>();
+  if (dl.has_value() && dl->defined()) {  // dh_T = dl . W_out^T formed by the kernel (the fused head's dlogits)
+    TORCH_CHECK(wo.has_value() && wo->defined() && wo->dim() == 2 && wo->size(0) == a.H && dl->dim() == 2 &&
+                    dl->size(0) == a.B && dl->size(1) == wo->size(1) && dl->is_contiguous() && wo->is_contiguous(),
+                "lstm_seq_bwd: dl [B][NC] with W_out [H][NC]");
+    a.dl = dl->data_ptr<float>(); a.wo = wo->data_ptr<float>(); a.nc = (int)wo->size(1);
+  }
   return dtfe::launch_lstm_seq_bwd(a, cur_stream());
 }
 
@@ -1078,7 +1089,8 @@ TORCH_LIBRARY(dtfe, m) {
         " Tensor(g!)[] zero) -> ()");
   m.def("lstm_seq_fwd(Tensor(a!) xh, Tensor K, Tensor bias, float forget_bias, Tensor(b!) act, Tensor(c!) c,"
         " Tensor(d!) hT) -> bool");
-  m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I) -> bool");
+  m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I, Tensor? dl=None,"
+        " Tensor? wo=None) -> bool");
   m.def("lstm_status(bool reset=False) -> int", &lstm_status);
   m.def("bn_stats(Tensor x, Tensor(a!) stats) -> ()");
   m.def("bn_infer(Tensor x, Tensor gamma, Tensor beta, Tensor moving_mean, Tensor moving_var, float eps, int act,"
@@ -1122,8 +1134,8 @@ TORCH_LIBRARY(dtfe, m) {
       " Tensor? acc_src=None, Tensor? acc_mask=None) -> ()");
   m.def(
       "dense_head(Tensor feat, Tensor w, Tensor? bias, Tensor y, Tensor(a!)? logits, Tensor(b!)? loss_sum,"
-      " Tensor(c!)? correct, Tensor(d!) dw, Tensor(e!)? db, Tensor(f!) dfeat, float scale, bool w_fmajor=False,"
-      " bool store=False) -> bool");
+      " Tensor(c!)? correct, Tensor(d!) dw, Tensor(e!)? db, Tensor(f!)? dfeat, float scale, bool w_fmajor=False,"
+      " bool store=False, Tensor(g!)? dl_out=None) -> bool");
   m.def(
       "imgconv(Tensor? src, Tensor? src_pooled, Tensor? src_argmax, Tensor w, Tensor? bias, Tensor(a!) y,"
       " Tensor(b!)? argmax, Tensor? relu_mask, int B, int SH, int SW, int CS, int OH, int OW, int N, int KH, int KW,"

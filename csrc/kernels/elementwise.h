@@ -67,6 +67,10 @@ struct DenseHeadArgs {
   int w_fmajor;  // W (and dW) stored [F][NC] (a TF Variable of shape (in, out)) instead of [NC][F]
   int store;     // dW / db are stored, not accumulated
   int slices;    // (set by the launcher) batch slices of the dW phase
+  int ylds;      // (set by the launcher) the labels are staged in LDS (when they fit)
+  float* dl_out; // optional: the dlogits rows [B][NC] (fp32) - the consumer forms dfeat itself (dfeat may then be null)
+  int diag;      // (set by the launcher) DTFE_DIAG dh=<bits> phase-skipping ablation: 1 logits, 2 softmax,
+                 // 4 dW, 8 dfeat, 16 db, 32 feature staging - timing only, never for training
 };
 bool launch_dense_head(const DenseHeadArgs& a, hipStream_t s);
 

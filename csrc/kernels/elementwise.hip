@@ -254,10 +254,11 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
   float* sf = hsm;             // [B][F+4] features (fp32; 16-B aligned rows)
   float* sw = sf + B * FP;     // [NC][F+4] weights
   float* sd = sw + NC * FP;    // [B][NC] logits, then dlogits
-  float* red = sd + B * NC;    // [2][32] block-reduce scratch, then the dW slice partials
+  float* sy = sd + B * NC;     // [B][NC] labels (a.ylds: staged with the features, the softmax rows read LDS)
+  float* red = sy + (a.ylds ? B * NC : 0);  // [2][32] block-reduce scratch, then the dW slice partials
   constexpr int EPC = F32 ? 4 : 8;
   const int CPR = F / EPC;
-  for (int i = tid; i < B * CPR; i += 1024) {
+  for (int i = tid; i < ((a.diag & 32) ? 0 : B * CPR); i += 1024) {
     const int b = i / CPR, f0 = (i - b * CPR) * EPC;
     if constexpr (F32) {
       *reinterpret_cast<f32x4_t*>(sf + b * FP + f0) = reinterpret_cast<const f32x4_t*>(a.feat)[i];
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
       *reinterpret_cast<f32x4_t*>(sf + b * FP + f0 + 4) = hi;
     }
   }
+  for (int i = tid; i < (a.ylds ? B * NC : 0); i += 1024) sy[i] = a.y[i];
   for (int i = tid; i < NC * F; i += 1024) {
     if constexpr (WFM) {
       const int f = i / NC, c = i - f * NC;
@@ -285,7 +287,7 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
     }
   }
   __syncthreads();
-  for (int o = tid; o < B * NC; o += 1024) {  // logits: 16-B row reads, four independent fmaf chains
+  for (int o = tid; o < ((a.diag & 1) ? 0 : B * NC); o += 1024) {  // logits: 16-B row reads, four independent fmaf chains
     const int b = o / NC, c = o - b * NC;
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
     for (int f = 0; f < F; f += 4) {
@@ -301,9 +303,9 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
   __syncthreads();
   // rows: softmax_xent_kernel's expressions (first-max argmax, lse, loss, (p - y) * scale)
   float loss = 0.f, hits = 0.f;
-  for (int b = tid; b < B; b += 1024) {
+  for (int b = tid; b < ((a.diag & 2) ? 0 : B); b += 1024) {
     float* l = sd + b * NC;
-    const float* y = a.y + (long)b * NC;
+    const float* y = a.ylds ? sy + b * NC : a.y + (long)b * NC;
     float mx = -INFINITY, ymax = -1.f;
     int am = 0, yarg = 0;
     for (int c = 0; c < NC; ++c) {
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
   // dW[c][f..f+3] over a batch slice: items (c, f4) x S slices, S = 1024 / (NC * F / 4) (<= 8)
   const int F4 = F / 4, NI = NC * F4, S = a.slices;
   float* part = red + 64;  // [S][NI][4] (S > 1)
-  for (int t = tid; t < NI * S; t += 1024) {
+  for (int t = tid; t < ((a.diag & 4) ? 0 : NI * S); t += 1024) {
     const int s = t / NI, it = t - s * NI, c = it / F4, f = (it - c * F4) * 4;
     const int b0 = s * B / S, b1 = (s + 1) * B / S;
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -360,13 +362,14 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
       }
     }
   }
-  if (tid < NC && a.db) {
+  if (wid < NC && a.db && !(a.diag & 16)) {  // db[c]: wave c, rows strided over the lanes + a butterfly
     float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += sd[b * NC + tid];
-    a.db[tid] = a.store ? acc : a.db[tid] + acc;
+    for (int b = lane; b < B; b += 64) acc += sd[b * NC + wid];
+    acc = wave_sum(acc);
+    if (lane == 0) a.db[wid] = a.store ? acc : a.db[wid] + acc;
   }
   __syncthreads();
-  for (int it = tid; it < (S > 1 ? NI : 0); it += 1024) {
+  for (int it = tid; it < (S > 1 && !(a.diag & 4) ? NI : 0); it += 1024) {
     f32x4_t g = *reinterpret_cast<const f32x4_t*>(part + (long)it * 4);
     for (int s = 1; s < S; ++s) g += *reinterpret_cast<const f32x4_t*>(part + ((long)s * NI + it) * 4);
     const int c = it / F4, f = (it - c * F4) * 4;
@@ -376,7 +379,9 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
       a.dw[o] = a.store ? g[e] : a.dw[o] + g[e];
     }
   }
-  for (int i = tid; i < B * CPR; i += 1024) {  // dfeat = dlogits W, one 16-B store per chunk
+  if (a.dl_out)
+    for (int o = tid; o < B * NC; o += 1024) a.dl_out[o] = sd[o];
+  for (int i = tid; i < ((a.diag & 8) || !a.dfeat ? 0 : B * CPR); i += 1024) {  // dfeat = dlogits W, one 16-B store per chunk
     const int b = i / CPR, f0 = (i - b * CPR) * EPC;
     float acc[EPC] = {};
     for (int c = 0; c < NC; ++c) {
@@ -397,13 +402,17 @@ __global__ __launch_bounds__(1024) void dense_head_kernel(DenseHeadArgs a) {
 
 bool launch_dense_head(const DenseHeadArgs& a, hipStream_t s) {
   // LDS: features + weights [.][F+4], logits [B][NC], 64 reduce floats, dW slice partials (S x NI x 4)
-  const long ni = (long)a.NC * (a.F / 4), base = ((long)(a.B + a.NC) * (a.F + 4) + (long)a.B * a.NC + 64) * 4;
+  const long ni = (long)a.NC * (a.F / 4), base0 = ((long)(a.B + a.NC) * (a.F + 4) + (long)a.B * a.NC + 64) * 4;
+  const bool ylds = base0 + (long)a.B * a.NC * 4 <= 150 * 1024;
+  const long base = base0 + (ylds ? (long)a.B * a.NC * 4 : 0);
   long sl = ni >= 1024 ? 1 : std::min<long>(8, 1024 / ni);
   while (sl > 1 && base + sl * ni * 16 > 150 * 1024) --sl;
   const size_t lds = (size_t)(base + (sl > 1 ? sl * ni * 16 : 0));
-  if (lds > 150 * 1024 || a.NC > DH_NCMAX || a.F % 8 || !a.dw || !a.dfeat) return false;
+  if (lds > 150 * 1024 || a.NC > DH_NCMAX || a.F % 8 || !a.dw || (!a.dfeat && !a.dl_out)) return false;
   DenseHeadArgs ad = a;
   ad.slices = (int)sl;
+  ad.ylds = ylds ? 1 : 0;
+  ad.diag = diag_bits("dh");
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(1), dim3(1024), lds, s, ad);

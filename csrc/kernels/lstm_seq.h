@@ -14,6 +14,9 @@ struct LstmSeqArgs {
   float* c;           // [T][B][H]
   float* hT;          // [B][H] last hidden state
   const float* dhT;   // [B][H] d loss / d h_T (backward in)
+  // optional (backward): dh_T formed in the kernel as dl . W_out^T - dl [B][nc] (the classifier head's
+  // dlogits), W_out [H][nc] - instead of read from dhT (one launch and a [B][H] round trip fewer)
+  const float* dl; const float* wo; int nc;
   float* dg;          // [T][B][4H] gate pre-activation grads (backward out)
 };
 

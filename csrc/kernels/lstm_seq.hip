@@ -30,6 +30,14 @@ namespace dtfe {
 namespace {
 
 constexpr int LR = 16;        // batch rows per workgroup (one MFMA row tile)
+
+// d loss / d h_T of (row, unit): given (dhT), or dl[row] . W_out[unit] (the fused head's dlogits)
+__device__ __forceinline__ float dh_t_of(const LstmSeqArgs& a, int row, int u) {
+  if (!a.dl) return a.dhT[(long)row * a.H + u];
+  float s = 0.f;
+  for (int c = 0; c < a.nc; ++c) s = __builtin_fmaf(a.dl[(long)row * a.nc + c], a.wo[(long)u * a.nc + c], s);
+  return s;
+}
 constexpr int LWAVES = 16;    // 1024 threads
 
 template <int H, int KT4>
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(1024) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
   const int KT = a.I + H;
   // dh_{T-1} comes from the output layer
   for (int e = tid; e < LR * H; e += 1024) {
-    P0[e] = a.dhT[(long)(r0 + e / H) * H + (e % H)];
+    P0[e] = dh_t_of(a, r0 + e / H, e % H);
     P1[e] = 0.f;
   }
   float dcreg[LR * H / 1024];
@@ -444,7 +452,7 @@ __global__ __launch_bounds__(LR * H / NS) void lstm_split_bwd_kernel(LstmSeqArgs
     }
   }
   const int cr = tid / UPW, cu = tid - cr * UPW, u = sp * UPW + cu;
-  float dh = a.dhT[(long)(r0 + cr) * H + u];
+  float dh = dh_t_of(a, r0 + cr, u);
   float dc = 0.f;
   auto fetch = [&](int t, float (&v)[6]) {
     const long ri = (long)t * B + r0 + cr;

@@ -105,8 +105,10 @@ class LstmProgram(StepProgram):
         B = self.batch_size
         if self._persistent() and ops.require().lstm_seq_fwd(self.xh, self.K, self.b, 1.0, self.act, self.c,
                                                                self.hT):
+            # (dfeat = dh_T is formed by the BPTT kernel from these dlogits: lstm_seq_bwd(dl=...))
             if head and ops.dense_head(self.hT, self.Wo, self.bo, self.y, self.logits, self.loss, self.correct,
-                                       self.gWo, self.gbo, self.dh, 1.0 / B, w_fmajor=True, store=True):
+                                       self.gWo, self.gbo, None, 1.0 / B, w_fmajor=True, store=True,
+                                       dl_out=self.dlogits):
                 return True
             ops.gemm(self.hT, self.Wo, self.logits, M=B, N=NC, K=H, bmode=ops.RMAJ, ldb=NC, bias=self.bo)
             return False
@@ -135,7 +137,13 @@ class LstmProgram(StepProgram):
             ops.gemm(self.hT, self.dlogits, self.gWo, M=H + 1, N=NC, K=B, amode=ops.RMAJ, lda=H, bmode=ops.RMAJ,
                      ldb=NC, a_ones_row=H, bias_out=self.gbo)
             ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
-        if self._persistent() and ops.require().lstm_seq_bwd(self.K, self.act, self.c, self.dh, self.dg, I):
+        if fused:
+            # the fused head left dlogits (not dh_T): the persistent BPTT forms dh_T = dlogits . W_out^T
+            if not ops.require().lstm_seq_bwd(self.K, self.act, self.c, self.dh, self.dg, I, dl=self.dlogits,
+                                              wo=self.Wo):
+                ops.gemm(self.dlogits, self.Wo, self.dh, M=B, N=H, K=NC, bmode=ops.KMAJ, ldb=NC)
+                self._bptt_steps()
+        elif self._persistent() and ops.require().lstm_seq_bwd(self.K, self.act, self.c, self.dh, self.dg, I):
             pass  # whole BPTT recurrence in one launch (dc / dh stay on chip)
         else:
             self._bptt_steps()

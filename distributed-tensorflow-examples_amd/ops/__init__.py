@@ -819,16 +819,17 @@ def mse_sigmoid(y, t, loss, dz):
 
 
 def dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale, w_fmajor=False,
-               store=False) -> bool:
+               store=False, dl_out=None) -> bool:
     """A small dense classifier head, forward and backward in one launch (GPU: one workgroup; False when
     it does not fit): logits = feat W^T + b, softmax cross-entropy against one-hot y (loss_sum +=,
     correct +=), dlogits = (p - y) * scale, dw += dlogits^T feat, db += column sums, dfeat16 =
     dlogits W (in feat's dtype: bf16 or fp32).  ``w_fmajor``: W and dw are [F][NC] (a TF Variable of
-    shape (in, out)) instead of [NC][F]; ``store``: dw / db are stored, not accumulated.  The CPU path
-    is the fp32 oracle."""
+    shape (in, out)) instead of [NC][F]; ``store``: dw / db are stored, not accumulated.  ``dl_out``
+    (fp32 [B][NC]): the dlogits rows are written there, and dfeat16 may be None (the consumer forms it:
+    lstm_seq_bwd(dl=...)).  The CPU path is the fp32 oracle."""
     if feat16.is_cuda:
         return bool(require().dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, scale,
-                                         w_fmajor, store))
+                                         w_fmajor, store, dl_out))
     f = feat16.float()
     wf = w.float().t() if w_fmajor else w.float()   # [NC][F]
     lg = f @ wf.t() + (bias.float() if bias is not None else 0.0)
@@ -847,7 +848,10 @@ def dense_head(feat16, w, bias, y, logits, loss_sum, correct, dw, db, dfeat16, s
             db.copy_(dl.sum(0))
         else:
             db += dl.sum(0)
-    dfeat16.copy_((dl @ wf).to(dfeat16.dtype))
+    if dl_out is not None:
+        dl_out.copy_(dl)
+    if dfeat16 is not None:
+        dfeat16.copy_((dl @ wf).to(dfeat16.dtype))
     return True
 
 

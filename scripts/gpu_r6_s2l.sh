@@ -2,9 +2,9 @@
 set -o pipefail
 O=gpurun_out/${1:-r6s2l}
 mkdir -p $O
-timeout -k 10 300 python3 -u -m pytest tests/test_models_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu -k "lstm" > $O/pytest.log 2>&1
+timeout -k 10 300 python3 -u -m pytest tests/test_models_gpu.py tests/test_dense_head.py tests/test_resnet.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu -k "lstm or dense" > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -30; exit $rc; }
-for ns in 8 4 8 4; do
+for ns in 8 8; do
   DTFE_LSTM_SPLIT=$ns timeout -k 10 200 python3 bench/ref_models.py --models lstm > $O/lstm_$ns.log 2>&1 || { tail -5 $O/lstm_$ns.log; exit 1; }
   echo "NS=$ns $(grep ms_per_step $O/lstm_$ns.log)"
 done

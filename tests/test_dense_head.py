@@ -82,3 +82,21 @@ def test_dense_head_fp32_fmajor_store_matches_unfused_gpu(B, F, NC):
     assert torch.allclose(dw, (dl.t() @ feat).t(), atol=1e-5, rtol=1e-4)
     assert torch.allclose(db, dl.sum(0), atol=1e-6, rtol=1e-4)
     assert torch.allclose(dfeat, dl @ w, atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_dense_head_dlogits_out_without_dfeat_gpu():
+    """dl_out (fp32 [B][NC]) instead of dfeat: the dlogits rows the consumer forms dfeat from
+    (lstm_seq_bwd(dl=...)) equal softmax_xent's (p - y) * scale."""
+    torch.manual_seed(4)
+    d, B, F, NC = "cuda", 128, 128, 10
+    feat = torch.randn(B, F, device=d)
+    w_fnc, b = torch.randn(F, NC, device=d) * 0.2, torch.randn(NC, device=d) * 0.1
+    y = torch.nn.functional.one_hot(torch.randint(0, NC, (B,), device=d), NC).float()
+    dw, db, dl = torch.empty(F, NC, device=d), torch.empty(NC, device=d), torch.empty(B, NC, device=d)
+    assert ops.dense_head(feat, w_fnc, b, y, None, None, None, dw, db, None, 1.0 / B, w_fmajor=True, store=True,
+                          dl_out=dl)
+    lg = feat @ w_fnc + b
+    ref = torch.empty_like(lg)
+    ops.softmax_xent(lg, labels_oh=y, scale=1.0 / B, dlogits=ref)
+    assert torch.allclose(dl, ref, atol=1e-6, rtol=1e-4)
