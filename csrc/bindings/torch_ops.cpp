@@ -623,8 +623,8 @@ void wgrad_tallk(const Tensor& A, int64_t lda, const Tensor& B, int64_t ldb, int
   dtfe::launch_wgrad_tallk(a, cur_stream());
 }
 
-void seq_stage(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Tensor& ysrc, const Tensor& ydst,
-               at::TensorList zero) {
+dtfe::SeqStageArgs seq_stage_args(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Tensor& ysrc,
+                                   const Tensor& ydst, at::TensorList zero) {
   check_cuda(x, "x");
   check_cuda(xh, "xh");
   TORCH_CHECK(x.scalar_type() == at::kFloat && xh.scalar_type() == at::kFloat && x.is_contiguous() &&
@@ -633,8 +633,8 @@ void seq_stage(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Te
   const int64_t B = xh.size(1);
   TORCH_CHECK(x.numel() == B * T * I, "seq_stage: x holds B*T*I floats");
   TORCH_CHECK(ysrc.scalar_type() == at::kFloat && ydst.scalar_type() == at::kFloat && ysrc.is_contiguous() &&
-                  ydst.is_contiguous() && ysrc.numel() == ydst.numel(),
-              "seq_stage: label rows f32, same size, contiguous");
+                  ydst.is_contiguous() && ysrc.numel() == ydst.numel() && ysrc.numel() % B == 0,
+              "seq_stage: label rows f32 [B][*], same size, contiguous");
   dtfe::SeqStageArgs a{};
   a.x = x.data_ptr<float>();
   a.xh = xh.data_ptr<float>();
@@ -648,7 +648,12 @@ void seq_stage(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Te
     a.zptr[a.nz] = reinterpret_cast<uint32_t*>(z.data_ptr());
     a.zlen[a.nz++] = z.numel() * z.element_size() / 4;
   }
-  dtfe::launch_seq_stage(a, cur_stream());
+  return a;
+}
+
+void seq_stage(const Tensor& x, const Tensor& xh, int64_t T, int64_t I, const Tensor& ysrc, const Tensor& ydst,
+               at::TensorList zero) {
+  dtfe::launch_seq_stage(seq_stage_args(x, xh, T, I, ysrc, ydst, zero), cur_stream());
 }
 
 void gather_rows(const Tensor& src, const Tensor& dst, const optional<Tensor>& idx, const optional<Tensor>& labels_src,
@@ -832,7 +837,8 @@ void lstm_cell_bwd(const Tensor& act, const optional<Tensor>& c_prev, const Tens
 
 // whole-sequence LSTM (lstm_seq.hip): returns false when the shape needs the per-step path
 bool lstm_seq_fwd(const Tensor& xh, const Tensor& K, const Tensor& bias, double forget_bias, const Tensor& act,
-                  const Tensor& c, const Tensor& hT) {
+                  const Tensor& c, const Tensor& hT, const optional<Tensor>& xsrc, const optional<Tensor>& ysrc,
+                  const optional<Tensor>& ydst, const optional<Tensor>& zero0, const optional<Tensor>& zero1) {
   check_cuda(xh, "xh");
   TORCH_CHECK(xh.dim() == 3 && xh.scalar_type() == at::kFloat && xh.is_contiguous(), "lstm_seq_fwd: xh [T][B][I+H] f32");
   dtfe::LstmSeqArgs a{};
@@ -843,6 +849,13 @@ bool lstm_seq_fwd(const Tensor& xh, const Tensor& K, const Tensor& bias, double 
   a.xh = xh.data_ptr<float>(); a.K = K.data_ptr<float>(); a.bias = bias.data_ptr<float>();
   a.forget_bias = (float)forget_bias; a.act = act.data_ptr<float>(); a.c = c.data_ptr<float>();
   a.hT = hT.data_ptr<float>();
+  if (xsrc.has_value() && xsrc->defined()) {  // seq_stage folded into the forward launch
+    TORCH_CHECK(ysrc.has_value() && ydst.has_value(), "lstm_seq_fwd: xsrc needs ysrc / ydst");
+    std::vector<Tensor> zero;
+    for (const optional<Tensor>* z : {&zero0, &zero1})
+      if (z->has_value() && (*z)->defined()) zero.push_back(**z);
+    a.st = seq_stage_args(*xsrc, xh, a.T, a.I, *ysrc, *ydst, zero);
+  }
   return dtfe::launch_lstm_seq_fwd(a, cur_stream());
 }
 
@@ -1088,7 +1101,8 @@ TORCH_LIBRARY(dtfe, m) {
         " Tensor(c!) labels_dst, Tensor(d!) x, Tensor w, Tensor? bias, Tensor(e!) y, Tensor(f!) argmax,"
         " Tensor(g!)[] zero) -> ()");
   m.def("lstm_seq_fwd(Tensor(a!) xh, Tensor K, Tensor bias, float forget_bias, Tensor(b!) act, Tensor(c!) c,"
-        " Tensor(d!) hT) -> bool");
+        " Tensor(d!) hT, Tensor? xsrc=None, Tensor? ysrc=None, Tensor(e!)? ydst=None, Tensor(f!)? zero0=None,"
+        " Tensor(g!)? zero1=None) -> bool");
   m.def("lstm_seq_bwd(Tensor K, Tensor act, Tensor c, Tensor dhT, Tensor(a!) dg, int I, Tensor? dl=None,"
         " Tensor? wo=None) -> bool");
   m.def("lstm_status(bool reset=False) -> int", &lstm_status);

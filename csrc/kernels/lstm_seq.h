@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "elementwise.h"
+
 namespace dtfe {
 
 struct LstmSeqArgs {
@@ -18,6 +20,10 @@ struct LstmSeqArgs {
   // dlogits), W_out [H][nc] - instead of read from dhT (one launch and a [B][H] round trip fewer)
   const float* dl; const float* wo; int nc;
   float* dg;          // [T][B][4H] gate pre-activation grads (backward out)
+  // optional (forward): st.x != nullptr folds the batch staging (launch_seq_stage: x part of xh, h_{-1} = 0,
+  // label copy, accumulator clears) into the forward launch - the split kernel reads x_t straight from the
+  // images and writes xh for the kernel gradient in its prologue; other paths stage first
+  SeqStageArgs st;
 };
 
 // false when the shape is not supported (H != 128, B % 16, (I+H) % 4): callers fall back

@@ -349,6 +349,23 @@ __global__ __launch_bounds__(LR * H / NS) void lstm_split_fwd_kernel(LstmSeqArgs
 #pragma unroll
   for (int kk = 0; kk < KT4; ++kk) kreg[kk] = a.K[(long)(4 * kk + g) * G4 + col];
   const float bias = a.bias[col] + (gi == 2 ? a.forget_bias : 0.f);
+  // batch staging folded in (a.st.x: the images [B][T*I]): the recurrence reads x_t from the images, and
+  // the NS workgroups of a row group share writing its x rows into xh (read only by the kernel gradient),
+  // the labels and the accumulator clears - one launch and one pass over the batch fewer per step
+  const bool staged = a.st.x != nullptr;
+  const int TI = a.T * I;
+  if (staged) {
+    for (int e = sp * SPT + tid; e < LR * TI; e += NS * SPT) {
+      const int r = e / TI, rem = e - r * TI, t = rem / I;
+      a.xh[((long)t * B + r0 + r) * rowKT + rem - t * I] = a.st.x[(long)(r0 + r) * TI + rem];
+    }
+    const long yrow = a.st.ny / B;
+    if (sp == 0)
+      for (long e = tid; e < LR * yrow; e += SPT) a.st.ydst[r0 * yrow + e] = a.st.ysrc[r0 * yrow + e];
+    if (blockIdx.x == 0)
+      for (int z = 0; z < a.st.nz; ++z)
+        for (long i = tid; i < a.st.zlen[z]; i += SPT) a.st.zptr[z][i] = 0u;
+  }
   // cell update ownership: thread -> (row, unit) of my 16 x 32 slice
   const int cr = tid / UPW, cu = tid - cr * UPW;
   float creg = 0.f;
@@ -358,22 +375,29 @@ __global__ __launch_bounds__(LR * H / NS) void lstm_split_fwd_kernel(LstmSeqArgs
   int xr[XPT], xk[XPT];
   bool xo[XPT];
   float xv[XPT];
+  const float* xp[XPT];
+  const long xstep = staged ? (long)I : (long)B * rowKT;  // x_t -> x_{t+1}
 #pragma unroll
   for (int j = 0; j < XPT; ++j) {
     const int e = tid + j * SPT;
     xo[j] = e < LR * I;
     xr[j] = xo[j] ? e / I : 0;
     xk[j] = xo[j] ? e - xr[j] * I : 0;
-    xv[j] = xo[j] ? a.xh[((long)r0 + xr[j]) * rowKT + xk[j]] : 0.f;
+    xp[j] = staged ? a.st.x + (long)(r0 + xr[j]) * TI + xk[j] : a.xh + ((long)r0 + xr[j]) * rowKT + xk[j];
+    xv[j] = xo[j] ? xp[j][0] : 0.f;
   }
   for (int t = 0; t < a.T; ++t) {
 #pragma unroll
     for (int j = 0; j < XPT; ++j) {
       if (xo[j]) As[xr[j] * AP + xk[j]] = xv[j];
-      if (xo[j] && t + 1 < a.T) xv[j] = a.xh[((long)(t + 1) * B + r0 + xr[j]) * rowKT + xk[j]];
+      if (xo[j] && t + 1 < a.T) xv[j] = xp[j][(t + 1) * xstep];
     }
     if (t == 0) {
-      for (int e = tid; e < LR * H; e += SPT) As[(e / H) * AP + I + e % H] = a.xh[((long)r0 + e / H) * rowKT + I + e % H];
+      for (int e = tid; e < LR * H; e += SPT) {
+        const long o = ((long)r0 + e / H) * rowKT + I + e % H;
+        As[(e / H) * AP + I + e % H] = staged ? 0.f : a.xh[o];  // h_{-1} = 0
+        if (staged && sp == 0) a.xh[o] = 0.f;
+      }
     } else {
       float hv[HW];
       ll_get<HW>(llg + ((t - 1) & 1) * LR * H + tid, SPT, base + t, hv, y.err);
@@ -594,10 +618,15 @@ bool launch_lstm_seq_fwd(const LstmSeqArgs& a, hipStream_t s) {
       if (ns == 8 ? go(std::integral_constant<int, 8>{}) : go(std::integral_constant<int, 4>{})) return true;
     }
   }
+  LstmSeqArgs b = a;
+  if (b.st.x) {  // the single-workgroup-per-group kernel reads xh: stage it first
+    launch_seq_stage(b.st, s);
+    b.st = SeqStageArgs{};
+  }
   const size_t lds = ((size_t)LR * (a.I + a.H + 1) + (size_t)LR * (4 * a.H + 4)) * sizeof(float);
   auto k = lstm_seq_fwd_kernel<128, (28 + 128) / 4>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k, dim3(a.B / LR), dim3(1024), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(a.B / LR), dim3(1024), lds, s, b);
   return true;
 }
 

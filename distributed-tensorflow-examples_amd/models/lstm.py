@@ -80,15 +80,25 @@ class LstmProgram(StepProgram):
         self.ws_k = None
         if self.device.type == "cuda" and os.environ.get("DTFE_LSTM_TALLK", "1") != "0":
             self.ws_k = torch.empty(ops.tallk_ws_floats(I + H, 4 * H, self.k_splits), **f)
+        self._stage = None  # (x, y) of a batch the next forward launch stages (load_batch, GPU)
 
     def load_batch(self, batch):
         x, y = batch
         B = self.batch_size
         # batch_x.reshape((B, timesteps, num_input)) (LSTM:127): row t of the image is step t.
         # One launch stages x, zeroes h_{-1}, copies the labels and clears the step's loss / hit
-        # accumulators (compute_grads then skips its own clearing).
+        # accumulators (compute_grads then skips its own clearing) - on the GPU the forward launch itself
+        # (the split recurrence reads x_t from the images and writes xh in its prologue) when the load is
+        # captured together with the step.
         if x.dtype == torch.float32 and y.dtype == torch.float32 and x.numel() == B * T * I and y.numel() == B * NC:
-            ops.seq_stage(x, self.xh, T, I, y, self.y, zero=(self.loss, self.correct))
+            if (self._persistent() and x.is_contiguous() and y.is_contiguous()
+                    and torch.cuda.is_current_stream_capturing()):
+                # batch load captured with the step (bench/ref_models.py): staged by the forward launch itself
+                # (lstm_seq_fwd xsrc: seq_stage folded in).  An eager load_batch before a graph replay
+                # (train.py) must stage now - the replayed forward would not see a later batch.
+                self._stage = (x, y)
+            else:
+                ops.seq_stage(x, self.xh, T, I, y, self.y, zero=(self.loss, self.correct))
             self._acc_cleared = True
             return
         self.xh[:, :, :I].copy_(x.reshape(B, T, I).transpose(0, 1))
@@ -103,8 +113,13 @@ class LstmProgram(StepProgram):
         launch (ops.dense_head: logits, softmax-xent, dW_out / db_out stored, dh) instead of the head
         GEMM, softmax_xent and two gradient GEMMs; returns whether it ran."""
         B = self.batch_size
+        st, self._stage = self._stage, None
+        if st is not None:  # the batch load_batch left for this launch to stage
+            xs, ys, ydst, z0, z1 = st[0], st[1], self.y, self.loss, self.correct
+        else:
+            xs = ys = ydst = z0 = z1 = None
         if self._persistent() and ops.require().lstm_seq_fwd(self.xh, self.K, self.b, 1.0, self.act, self.c,
-                                                               self.hT):
+                                                               self.hT, xs, ys, ydst, z0, z1):
             # (dfeat = dh_T is formed by the BPTT kernel from these dlogits: lstm_seq_bwd(dl=...))
             if head and ops.dense_head(self.hT, self.Wo, self.bo, self.y, self.logits, self.loss, self.correct,
                                        self.gWo, self.gbo, None, 1.0 / B, w_fmajor=True, store=True,
@@ -112,6 +127,8 @@ class LstmProgram(StepProgram):
                 return True
             ops.gemm(self.hT, self.Wo, self.logits, M=B, N=NC, K=H, bmode=ops.RMAJ, ldb=NC, bias=self.bo)
             return False
+        if st is not None:
+            ops.seq_stage(st[0], self.xh, T, I, st[1], self.y, zero=(self.loss, self.correct))
         for t in range(T):
             ops.gemm(self.xh[t], self.K, self.gates[t], M=B, N=4 * H, K=I + H, bmode=ops.RMAJ, ldb=4 * H,
                      bias=self.b)

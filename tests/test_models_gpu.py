@@ -147,3 +147,45 @@ def test_lstm_split_kernels_replay_in_a_graph(monkeypatch):
     assert torch.equal(prog.P.grad, ref)
     prog.check_health()  # the split kernels' exchange error word stayed clear
     assert int(torch.ops.dtfe.lstm_status(False)) == 0
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_lstm_stage_folded_into_captured_forward(split, monkeypatch):
+    """load_batch captured together with the step (bench/ref_models.py): the forward launch stages the batch
+    itself (lstm_seq_fwd xsrc - x_t read from the images, xh / labels / accumulator clears in its prologue;
+    split=0: the launcher stages first).  Replays over a refilled input buffer give the eager seq_stage
+    path's gradients, xh and hit count bitwise."""
+    from dtfe.utils.graphs import StepGraph
+    monkeypatch.setenv("DTFE_LSTM_SPLIT", split)
+    model = LstmModel()
+    B = 128
+    g = torch.Generator().manual_seed(7)
+    xs = [torch.rand(B, 784, generator=g).cuda() for _ in range(3)]
+    ys = [F.one_hot(torch.randint(0, 10, (B,), generator=g), 10).float().cuda() for _ in range(3)]
+    eager = model.program("cuda", B, seed=4)
+    refs = []
+    for x, y in zip(xs, ys):
+        eager.load_batch((x, y))
+        eager.compute_grads()
+        torch.cuda.synchronize()
+        refs.append((eager.P.grad.clone(), eager.xh.clone(), eager.loss.clone(), eager.correct.clone()))
+    prog = model.program("cuda", B, seed=4)
+    xb, yb = xs[0].clone(), ys[0].clone()
+
+    def step():
+        prog.load_batch((xb, yb))
+        prog.compute_grads()
+
+    run = StepGraph(step, warmup=1)
+    for i in (0, 1, 2, 1, 0):
+        xb.copy_(xs[i])
+        yb.copy_(ys[i])
+        run()
+        torch.cuda.synchronize()
+        for name, got, want in zip(("grad", "xh", "correct"), (prog.P.grad, prog.xh, prog.correct),
+                                   (refs[i][0], refs[i][1], refs[i][3])):
+            assert torch.equal(got, want), (i, name)
+        assert torch.allclose(prog.loss, refs[i][2], rtol=1e-6, atol=0), i  # (loss: an atomic sum)
+    assert run.graph is not None, run.capture_error
+    assert prog._stage is None
+    assert int(torch.ops.dtfe.lstm_status(False)) == 0
