@@ -783,10 +783,50 @@ void gan_loss(const Tensor& d_real, const Tensor& d_fake, const Tensor& gen_loss
   dtfe::launch_gan_loss(a, cur_stream());
 }
 
-void mse_sigmoid(const Tensor& y, const Tensor& t, const Tensor& loss, const Tensor& dz) {
+bool gan_disc_head(const Tensor& d1, const Tensor& w, const optional<Tensor>& b, const optional<Tensor>& p,
+                   const optional<Tensor>& dlog, const optional<Tensor>& dlog_g, const Tensor& gw,
+                   const optional<Tensor>& gb, const Tensor& dd1, const Tensor& ddf, const Tensor& gen_loss,
+                   const Tensor& disc_loss, const Tensor& ws, double clamp_eps) {
+  check_cuda(d1, "d1");
+  TORCH_CHECK(d1.dim() == 2 && d1.size(0) % 2 == 0 && d1.scalar_type() == at::kFloat && d1.is_contiguous(),
+              "gan_disc_head: d1 f32 [2B][DH] contiguous");
+  const int B = (int)(d1.size(0) / 2), DH = (int)d1.size(1);
+  auto f32 = [](const Tensor& t, int64_t n) { return t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n; };
+  TORCH_CHECK(f32(w, DH) && f32(gw, DH) && f32(dd1, 2L * B * DH) && f32(ddf, (int64_t)B * DH) && f32(gen_loss, 1) &&
+                  f32(disc_loss, 1), "gan_disc_head: Wd2 / dWd2 [DH], dd1 [2B][DH], ddf [B][DH], scalar losses (f32)");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= dtfe::gan_head_ws_floats(B, DH),
+              "gan_disc_head: ws needs ", dtfe::gan_head_ws_floats(B, DH), " zeroed floats");
+  auto opt_f32 = [](const optional<Tensor>& t) -> float* {
+    return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+  };
+  dtfe::GanHeadArgs a{};
+  a.B = B; a.DH = DH;
+  a.d1 = d1.data_ptr<float>(); a.w = w.data_ptr<float>(); a.b = opt_f32(b);
+  if (p && p->defined()) { TORCH_CHECK(f32(*p, 2L * B), "gan_disc_head: p [2B]"); a.p = p->data_ptr<float>(); }
+  if (dlog && dlog->defined()) { TORCH_CHECK(f32(*dlog, 2L * B), "gan_disc_head: dlog [2B]"); a.dlog = dlog->data_ptr<float>(); }
+  if (dlog_g && dlog_g->defined()) { TORCH_CHECK(f32(*dlog_g, B), "gan_disc_head: dlog_g [B]"); a.dlog_g = dlog_g->data_ptr<float>(); }
+  a.gw = gw.data_ptr<float>(); a.gb = opt_f32(gb);
+  a.dd1 = dd1.data_ptr<float>(); a.ddf = ddf.data_ptr<float>();
+  a.gen_loss = gen_loss.data_ptr<float>(); a.disc_loss = disc_loss.data_ptr<float>();
+  a.clamp_eps = (float)clamp_eps;
+  a.ws = ws.data_ptr<float>();
+  return dtfe::launch_gan_disc_head(a, cur_stream());
+}
+
+int64_t gan_head_ws_floats(int64_t B, int64_t DH) { return dtfe::gan_head_ws_floats((int)B, (int)DH); }
+
+void mse_sigmoid(const Tensor& y, const Tensor& t, const Tensor& loss, const Tensor& dz, const optional<Tensor>& ws) {
   check_cuda(y, "y");
+  TORCH_CHECK(y.is_contiguous() && t.is_contiguous() && dz.is_contiguous() && t.numel() == y.numel() &&
+                  dz.numel() == y.numel(), "mse_sigmoid: contiguous y / t / dz of one size");
+  float* w = nullptr;
+  if (ws.has_value() && ws->defined()) {
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= dtfe::MSE_WS_FLOATS && ws->is_contiguous(),
+                "mse_sigmoid: ws f32 [>= ", dtfe::MSE_WS_FLOATS, "], zero-initialised");
+    w = ws->data_ptr<float>();
+  }
   dtfe::launch_mse_sigmoid(y.data_ptr<float>(), t.data_ptr<float>(), y.numel(), loss.data_ptr<float>(),
-                           dz.data_ptr<float>(), cur_stream());
+                           dz.data_ptr<float>(), cur_stream(), w);
 }
 
 void colsum(const Tensor& x, int64_t M, int64_t N, int64_t ld, const Tensor& db, double scale) {
@@ -1193,7 +1233,11 @@ TORCH_LIBRARY(dtfe, m) {
   m.def(
       "gan_loss(Tensor d_real, Tensor d_fake, Tensor(a!) gen_loss, Tensor(b!) disc_loss, Tensor(c!) dz_real_disc,"
       " Tensor(d!) dz_fake_disc, Tensor(e!) dz_fake_gen, float clamp_eps) -> ()");
-  m.def("mse_sigmoid(Tensor y, Tensor t, Tensor(a!) loss, Tensor(b!) dz) -> ()");
+  m.def("gan_disc_head(Tensor d1, Tensor w, Tensor? b, Tensor(a!)? p, Tensor(b!)? dlog, Tensor(c!)? dlog_g,"
+        " Tensor(d!) gw, Tensor(e!)? gb, Tensor(f!) dd1, Tensor(g!) ddf, Tensor(h!) gen_loss, Tensor(i!) disc_loss,"
+        " Tensor(j!) ws, float clamp_eps=0.0) -> bool");
+  m.def("gan_head_ws_floats(int B, int DH) -> int");
+  m.def("mse_sigmoid(Tensor y, Tensor t, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? ws=None) -> ()");
   m.def("colsum(Tensor x, int M, int N, int ld, Tensor(a!) db, float scale) -> ()");
   m.def("unpool_f32(Tensor g, Tensor argmax, Tensor(a!) out, int B, int PH, int PW, int C) -> ()");
   m.def("head_xent_f32(Tensor h, Tensor w, Tensor? b, Tensor labels, Tensor(a!) dz, Tensor(b!) dl, Tensor(c!) loss_sum,"
@@ -1237,6 +1281,7 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("softmax_xent", &softmax_xent);
   m.impl("gan_loss", &gan_loss);
   m.impl("mse_sigmoid", &mse_sigmoid);
+  m.impl("gan_disc_head", &gan_disc_head);
   m.impl("colsum", &colsum);
   m.impl("unpool_f32", &unpool_f32);
   m.impl("head_xent_f32", &head_xent_f32);
@@ -1261,4 +1306,5 @@ TORCH_LIBRARY_IMPL(dtfe, CompositeExplicitAutograd, m) {
   m.impl("wgrad_flush", &wgrad_flush);
   m.impl("wgrad_pending", &wgrad_pending);
   m.impl("wgrad_discard", &wgrad_discard);
+  m.impl("gan_head_ws_floats", &gan_head_ws_floats);
 }

@@ -87,8 +87,12 @@ struct GanLossArgs {
 };
 void launch_gan_loss(const GanLossArgs& a, hipStream_t s);
 
-// mean((t - y)^2) with the gradient w.r.t. the pre-sigmoid logit of y
-void launch_mse_sigmoid(const float* y, const float* t, long n, float* loss, float* dz, hipStream_t s);
+// mean((t - y)^2) with the gradient w.r.t. the pre-sigmoid logit of y.  ws (optional,
+// MSE_WS_FLOATS floats, zeroed once): the loss is stored by the last workgroup (no memset, deterministic)
+constexpr int MSE_PARTS = 128;
+constexpr int MSE_WS_FLOATS = MSE_PARTS + 4;
+void launch_mse_sigmoid(const float* y, const float* t, long n, float* loss, float* dz, hipStream_t s,
+                        float* ws = nullptr);
 
 // db[n] += scale * sum_m x[m][n]   (x f32 or bf16)
 void launch_colsum(const void* x, int x_f32, int M, int N, long ld, float* db, float scale, hipStream_t s);

@@ -459,12 +459,29 @@ void launch_gan_loss(const GanLossArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(gan_loss_kernel, dim3(1), dim3(256), 0, s, a);
 }
 
+// ws == nullptr: one float atomic per workgroup into a loss the launcher zeroed (a memset node).  With ws
+// (MSE_WS_FLOATS, zero-initialised): each workgroup leaves its partial in a write-through store and takes a
+// ticket (the split-K hand-off of gemm_dense.h); the last arriver sums the partials in workgroup order and
+// STORES the loss - one launch, no memset, a bitwise-reproducible loss.
+template <bool TICKET>
 __global__ __launch_bounds__(256) void mse_sigmoid_kernel(const float* y, const float* t, long n, float* loss,
-                                                          float* dz) {
+                                                          float* dz, float* ws) {
   __shared__ float part[4];
   float acc = 0.f;
   const float inv = 1.f / (float)n;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+  const long n4 = n / 4, nth = (long)gridDim.x * 256, tid = blockIdx.x * 256L + threadIdx.x;
+  for (long i = tid; i < n4; i += nth) {  // torch allocations: 16-B aligned
+    const f32x4_t yv = reinterpret_cast<const f32x4_t*>(y)[i], tv = reinterpret_cast<const f32x4_t*>(t)[i];
+    f32x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = yv[e] - tv[e];
+      acc += d * d;
+      o[e] = 2.f * d * inv * yv[e] * (1.f - yv[e]);
+    }
+    reinterpret_cast<f32x4_t*>(dz)[i] = o;
+  }
+  for (long i = 4 * n4 + tid; i < n; i += nth) {
     const float d = y[i] - t[i];
     acc += d * d;
     dz[i] = 2.f * d * inv * y[i] * (1.f - y[i]);
@@ -472,13 +489,46 @@ __global__ __launch_bounds__(256) void mse_sigmoid_kernel(const float* y, const 
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(loss, (part[0] + part[1] + part[2] + part[3]) * inv);
+  const float v = ((part[0] + part[1]) + part[2]) + part[3];
+  if constexpr (!TICKET) {
+    if (threadIdx.x == 0) atomicAdd(loss, v * inv);
+  } else {
+    __shared__ int lastf;
+    __shared__ float part2[4];
+    if (threadIdx.x == 0) {
+      const __amdgpu_buffer_rsrc_t slot = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, MSE_PARTS * 4, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), slot, blockIdx.x * 4, 0, 16);  // write-through
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int* ctr = reinterpret_cast<int*>(ws + MSE_PARTS);
+      const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == (int)gridDim.x - 1;
+      if (last) {
+        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lastf = last;
+    }
+    __syncthreads();
+    if (!lastf) return;
+    // the last arriver: one partial per thread (<= MSE_PARTS), a fixed butterfly + wave order
+    float x = (int)threadIdx.x < (int)gridDim.x ? ws[threadIdx.x] : 0.f;
+    x = wave_sum(x);
+    if ((threadIdx.x & 63) == 0) part2[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) *loss = (((part2[0] + part2[1]) + part2[2]) + part2[3]) * inv;
+  }
 }
-void launch_mse_sigmoid(const float* y, const float* t, long n, float* loss, float* dz, hipStream_t s) {
-  long blocks = (n + 255) / 256;
-  if (blocks > 512) blocks = 512;
+void launch_mse_sigmoid(const float* y, const float* t, long n, float* loss, float* dz, hipStream_t s, float* ws) {
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > (ws ? MSE_PARTS : 512)) blocks = ws ? MSE_PARTS : 512;
+  if (blocks < 1) blocks = 1;
+  if (ws) {
+    hipLaunchKernelGGL(mse_sigmoid_kernel<true>, dim3(blocks), dim3(256), 0, s, y, t, n, loss, dz, ws);
+    return;
+  }
   hipMemsetAsync(loss, 0, sizeof(float), s);
-  hipLaunchKernelGGL(mse_sigmoid_kernel, dim3(blocks), dim3(256), 0, s, y, t, n, loss, dz);
+  hipLaunchKernelGGL(mse_sigmoid_kernel<false>, dim3(blocks), dim3(256), 0, s, y, t, n, loss, dz, ws);
 }
 
 // column sums: block = 64 columns x 4 row-groups

@@ -267,6 +267,9 @@ void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, co
 constexpr int GEMM_TILE_SMALL = 13;
 bool gemm_small_eligible(int dtype, const DenseGemmArgs& a);
 void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s);
+// n (<= 2) small GEMMs recorded inside a gemm group: a (RMAJ, RMAJ) + (KMAJ, KMAJ) pair leaves as one
+// launch, anything else launches one by one in recording order
+void launch_gemm_small_group(int n, const int* am, const int* bm, const DenseGemmArgs* g, hipStream_t s);
 // Grouped launch (gemm_dense.hip): between begin and end, launch_gemm_dense calls with glds tile 12
 // or 22 (both pieces the same tile) and one split, and launch_head_wgrad calls, are recorded instead of launched (record functions
 // return false when a call does not fit the group); end launches the recorded pieces as one grid

@@ -105,12 +105,15 @@ static void by_mode(int am, int bm, int tile, int splits, const DenseGemmArgs& a
   else by_tile<T, RMAJ, RMAJ>(tile, splits, a, s);
 }
 
+static bool small_group_record(int amode, int bmode, const DenseGemmArgs& a);
+
 void launch_gemm_dense(int dtype, int amode, int bmode, int tile, int splits, const DenseGemmArgs& args,
                        hipStream_t stream) {
   if (splits < 1) splits = 1;
   if (tile == GEMM_TILE_SMALL) {
     if (!gemm_small_eligible(dtype, args) || splits != 1)
       throw std::runtime_error("gemm_dense: the small-tile kernel takes fp32, one split, no un-pool epilogue");
+    if (small_group_record(amode, bmode, args)) return;  // inside a group
     launch_gemm_small(amode, bmode, args, stream);
     return;
   }
@@ -186,11 +189,25 @@ struct GlGroupRec {
 };
 thread_local GlGroupRec g_group;
 int pad8(int n) { return (n + 7) / 8 * 8; }
+struct SmallGroupRec {  // the fp32 small-tile pieces of the same group (gemm_small.hip)
+  int n = 0, am[2] = {0, 0}, bm[2] = {0, 0};
+  DenseGemmArgs g[2];
+};
+thread_local SmallGroupRec g_small;
 }  // namespace
+
+static bool small_group_record(int amode, int bmode, const DenseGemmArgs& a) {
+  if (!g_group.active || g_small.n == 2) return false;
+  g_small.am[g_small.n] = amode;
+  g_small.bm[g_small.n] = bmode;
+  g_small.g[g_small.n++] = a;
+  return true;
+}
 
 void glds_group_begin() {
   if (g_group.active) throw std::runtime_error("gemm group: already recording");
   g_group = GlGroupRec();
+  g_small = SmallGroupRec();
   g_group.active = true;
 }
 
@@ -216,6 +233,10 @@ void glds_group_end(hipStream_t s) {
   if (!g_group.active) throw std::runtime_error("gemm group: not recording");
   GlGroupRec r = g_group;
   g_group = GlGroupRec();
+  const SmallGroupRec sr = g_small;
+  g_small = SmallGroupRec();
+  if (sr.n) launch_gemm_small_group(sr.n, sr.am, sr.bm, sr.g, s);
+  if (r.ng == 0 && !r.has_h) return;
   const bool fused = r.ng == 2 && r.am[0] == KMAJ && r.bm[0] == RMAJ && r.am[1] == RMAJ && r.bm[1] == RMAJ;
   if (!fused) {  // any other combination: the pieces as separate launches, in recording order
     if (r.has_h) launch_head_wgrad(r.h, s);

@@ -51,10 +51,10 @@ __device__ __forceinline__ f32x4_t load4(const float* p, long ld, int r, int row
 }
 
 template <int AM, int BMD>
-__global__ __launch_bounds__(256) void gemm_small_kernel(DenseGemmArgs a, int a_vec, int b_vec) {
-  __shared__ float red[4][16][17];
+__device__ __forceinline__ void gemm_small_body(const DenseGemmArgs& a, int tile, int a_vec, int b_vec,
+                                                float (*red)[16][17]) {
   const int tiles_n = (a.N + 15) >> 4;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int m = tm * 16 + (lane & 15), n = tn * 16 + (lane & 15);
   // a ones row reads as 1.0 wherever it sits (load4 checks it before the memory read)
@@ -99,6 +99,28 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(DenseGemmArgs a, int a_
   else reinterpret_cast<bf16*>(a.out)[o] = f2bf(x);
 }
 
+template <int AM, int BMD>
+__global__ __launch_bounds__(256) void gemm_small_kernel(DenseGemmArgs a, int a_vec, int b_vec) {
+  __shared__ float red[4][16][17];
+  gemm_small_body<AM, BMD>(a, blockIdx.x, a_vec, b_vec, red);
+}
+
+// Two independent small GEMMs of one backward phase in ONE launch (a layer's weight gradient (RMAJ, RMAJ)
+// beside its data gradient (KMAJ, KMAJ)): workgroups [0, t0) run the first, the rest the second - one
+// dependent launch fewer per layer in the GAN / autoencoder steps, which are chains of ~5 us launches.
+struct SmallPair {
+  DenseGemmArgs g0, g1;
+  int t0, v0a, v0b, v1a, v1b;
+};
+__global__ __launch_bounds__(256) void gemm_small_pair_kernel(SmallPair p) {
+  __shared__ float red[4][16][17];
+  if ((int)blockIdx.x < p.t0) gemm_small_body<RMAJ, RMAJ>(p.g0, blockIdx.x, p.v0a, p.v0b, red);
+  else gemm_small_body<KMAJ, KMAJ>(p.g1, blockIdx.x - p.t0, p.v1a, p.v1b, red);
+}
+
+int small_tiles(const DenseGemmArgs& a) { return ((a.M + 15) / 16) * ((a.N + 15) / 16); }
+int small_vec(int mode, const void* p, int ld) { return mode == KMAJ && ld % 4 == 0 && ((uintptr_t)p & 15) == 0; }
+
 }  // namespace
 
 bool gemm_small_eligible(int dtype, const DenseGemmArgs& a) {
@@ -108,14 +130,34 @@ bool gemm_small_eligible(int dtype, const DenseGemmArgs& a) {
 }
 
 void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s) {
-  const int tiles = ((a.M + 15) / 16) * ((a.N + 15) / 16);
-  const int a_vec = amode == KMAJ && a.lda % 4 == 0 && ((uintptr_t)a.A & 15) == 0;
-  const int b_vec = bmode == KMAJ && a.ldb % 4 == 0 && ((uintptr_t)a.B & 15) == 0;
+  const int tiles = small_tiles(a);
+  const int a_vec = small_vec(amode, a.A, a.lda), b_vec = small_vec(bmode, a.B, a.ldb);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), 0, s, a, a_vec, b_vec); };
   if (amode == KMAJ && bmode == KMAJ) go(gemm_small_kernel<KMAJ, KMAJ>);
   else if (amode == KMAJ && bmode == RMAJ) go(gemm_small_kernel<KMAJ, RMAJ>);
   else if (amode == RMAJ && bmode == KMAJ) go(gemm_small_kernel<RMAJ, KMAJ>);
   else go(gemm_small_kernel<RMAJ, RMAJ>);
+}
+
+void launch_gemm_small_group(int n, const int* am, const int* bm, const DenseGemmArgs* g, hipStream_t s) {
+  int i0 = -1, i1 = -1;  // the (RMAJ, RMAJ) piece and the (KMAJ, KMAJ) piece
+  for (int i = 0; i < n; ++i) {
+    if (am[i] == RMAJ && bm[i] == RMAJ && i0 < 0) i0 = i;
+    else if (am[i] == KMAJ && bm[i] == KMAJ && i1 < 0) i1 = i;
+  }
+  if (n != 2 || i0 < 0 || i1 < 0 || (long)small_tiles(g[0]) + small_tiles(g[1]) > 65535) {
+    for (int i = 0; i < n; ++i) launch_gemm_small(am[i], bm[i], g[i], s);  // separate launches, recording order
+    return;
+  }
+  SmallPair p;
+  p.g0 = g[i0];
+  p.g1 = g[i1];
+  p.t0 = small_tiles(p.g0);
+  p.v0a = small_vec(RMAJ, p.g0.A, p.g0.lda);
+  p.v0b = small_vec(RMAJ, p.g0.B, p.g0.ldb);
+  p.v1a = small_vec(KMAJ, p.g1.A, p.g1.lda);
+  p.v1b = small_vec(KMAJ, p.g1.B, p.g1.ldb);
+  hipLaunchKernelGGL(gemm_small_pair_kernel, dim3(p.t0 + small_tiles(p.g1)), dim3(256), 0, s, p);
 }
 
 }  // namespace dtfe

@@ -218,4 +218,27 @@ __device__ __forceinline__ void head_wgrad4_body(const HeadWgradArgs& a, int bid
   if (bias_blk) head_fold_parts(a);
 }
 
+// The GAN discriminator's output layer with both GAN losses and their gradients down to the hidden
+// layer, one launch (reference gan/distributed_gan.py:128-143): for the B real rows
+// and B fake rows of d1 = relu(.) [2B][DH]: p = sigmoid(d1 . Wd2 + bd2); gen_loss = -mean(log p_fake),
+// disc_loss = -mean(log p_real + log(1 - p_fake)) (no epsilon unless clamp_eps > 0, as gan_loss);
+// dlog = d disc_loss / d logit [2B], dlog_g = d gen_loss / d logit_fake [B]; dWd2 = d1^T dlog, dbd2 =
+// sum dlog (stored); dd1 = dlog Wd2^T * relu'(d1) [2B][DH]; ddf = dlog_g Wd2^T * relu'(d1_fake) [B][DH].
+// Replaces the N = 1 GEMM, gan_loss, the dWd2 GEMM and the two K = 1 GEMMs (5 launches).  One wave per
+// (real, fake) row pair; per-workgroup partials (write-through) + ticket, the last workgroup sums them in
+// workgroup order: every output is bitwise reproducible.
+struct GanHeadArgs {
+  int B, DH;
+  const float* d1; const float* w; const float* b;
+  float* p; float* dlog; float* dlog_g;     // optional outputs ([2B], [2B], [B])
+  float* gw; float* gb;                     // dWd2 [DH], dbd2 [1] (stored)
+  float* dd1; float* ddf;                   // [2B][DH], [B][DH]
+  float* gen_loss; float* disc_loss;        // stored
+  float clamp_eps;
+  float* ws;                                // gan_head_ws_floats(B, DH) floats, zeroed once
+};
+long gan_head_ws_floats(int B, int DH);
+// false: DH > 256 or DH % 4 (the caller runs the unfused chain)
+bool launch_gan_disc_head(const GanHeadArgs& a, hipStream_t s);
+
 }  // namespace dtfe

@@ -17,6 +17,7 @@
 #include "head.h"
 #include "gemm_dense.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace dtfe {
@@ -245,6 +246,120 @@ void launch_head_wgrad(const HeadWgradArgs& a, hipStream_t s) {
   if (a.B <= 256) hipLaunchKernelGGL((head_wgrad_kernel<10, 1>), dim3(blocks), dim3(256), 0, s, a);
   else if (a.B <= 512) hipLaunchKernelGGL((head_wgrad_kernel<10, 2>), dim3(blocks), dim3(256), 0, s, a);
   else hipLaunchKernelGGL((head_wgrad_kernel<10, 4>), dim3(blocks), dim3(256), 0, s, a);
+}
+
+namespace {
+constexpr int GH_SLOT = 256 + 4;  // per-workgroup partial: dWd2[256], dbd2, gen, disc, pad
+int gan_head_grid(int B) { return std::max(1, std::min(256, (B + 3) / 4)); }
+}  // namespace
+
+long gan_head_ws_floats(int B, int DH) { (void)DH; return (long)gan_head_grid(B) * GH_SLOT + 4; }
+
+__global__ __launch_bounds__(256) void gan_disc_head_kernel(GanHeadArgs a) {
+  __shared__ float red[4][GH_SLOT];
+  __shared__ int lastf;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, DH = a.DH, B = a.B;
+  const bool on = 4 * lane < DH;  // this lane's 4 columns
+  const int c0 = on ? 4 * lane : 0;
+  const f32x4_t zero = {0.f, 0.f, 0.f, 0.f};
+  const f32x4_t wv = on ? *reinterpret_cast<const f32x4_t*>(a.w + c0) : zero;
+  const float bias = a.b ? a.b[0] : 0.f, invB = 1.f / (float)B;
+  f32x4_t gw = zero;
+  float gb = 0.f, gl = 0.f, dl = 0.f;  // (lane-uniform)
+  for (int i = blockIdx.x * 4 + wid; i < B; i += gridDim.x * 4) {
+    const f32x4_t xr = on ? *reinterpret_cast<const f32x4_t*>(a.d1 + (long)i * DH + c0) : zero;
+    const f32x4_t xf = on ? *reinterpret_cast<const f32x4_t*>(a.d1 + (long)(B + i) * DH + c0) : zero;
+    float zr = 0.f, zf = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      zr = __builtin_fmaf(xr[e], wv[e], zr);
+      zf = __builtin_fmaf(xf[e], wv[e], zf);
+    }
+    zr = wave_sum(zr) + bias;
+    zf = wave_sum(zf) + bias;
+    const float pr = sigmoidf_(zr), pf = sigmoidf_(zf);
+    float pr_c = pr, pf_c = pf, qf_c = 1.f - pf;
+    if (a.clamp_eps > 0.f) {
+      pr_c = fmaxf(pr, a.clamp_eps);
+      pf_c = fmaxf(pf, a.clamp_eps);
+      qf_c = fmaxf(1.f - pf, a.clamp_eps);
+    }
+    gl += -logf(pf_c);
+    dl += -(logf(pr_c) + logf(qf_c));
+    // d/dz of -log(sigmoid(z)) = -(1 - s);  d/dz of -log(1 - sigmoid(z)) = s
+    const float gr = -(1.f - pr) * invB, gf = pf * invB, gg = -(1.f - pf) * invB;
+    if (lane == 0) {
+      if (a.p) { a.p[i] = pr; a.p[B + i] = pf; }
+      if (a.dlog) { a.dlog[i] = gr; a.dlog[B + i] = gf; }
+      if (a.dlog_g) a.dlog_g[i] = gg;
+    }
+    if (on) {
+      f32x4_t orr, off, ogg;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float mr = xr[e] > 0.f ? wv[e] : 0.f, mf = xf[e] > 0.f ? wv[e] : 0.f;  // Wd2 * relu'(d1)
+        orr[e] = gr * mr;
+        off[e] = gf * mf;
+        ogg[e] = gg * mf;
+        gw[e] = __builtin_fmaf(xf[e], gf, __builtin_fmaf(xr[e], gr, gw[e]));
+      }
+      *reinterpret_cast<f32x4_t*>(a.dd1 + (long)i * DH + c0) = orr;
+      *reinterpret_cast<f32x4_t*>(a.dd1 + (long)(B + i) * DH + c0) = off;
+      *reinterpret_cast<f32x4_t*>(a.ddf + (long)i * DH + c0) = ogg;
+    }
+    gb += gr + gf;
+  }
+  // workgroup partial (waves summed in order) -> write-through slab, ticket; the last arriver sums the
+  // slabs in workgroup order (the split-K hand-off of gemm_dense.h)
+  if (on) *reinterpret_cast<f32x4_t*>(&red[wid][c0]) = gw;
+  if (lane == 0) { red[wid][256] = gb; red[wid][257] = gl; red[wid][258] = dl; }
+  __syncthreads();
+  const int t = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t slab =
+      __builtin_amdgcn_make_buffer_rsrc(a.ws + (long)blockIdx.x * GH_SLOT, (short)0, GH_SLOT * 4, 0x00020000);
+  for (int k = t; k < GH_SLOT; k += 256) {
+    const float v = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), slab, k * 4, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* ctr = reinterpret_cast<int*>(a.ws + (long)gridDim.x * GH_SLOT);
+  if (t == 0) {
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (int)gridDim.x - 1;
+    if (last) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch / replay
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lastf = last;
+  }
+  __syncthreads();
+  if (!lastf) return;
+  const int G = gridDim.x;
+  for (int k = t; k < 259; k += 256) {
+    if (k >= DH && k < 256) continue;
+    // the slabs' column k in workgroup order, 16 loads in flight per chunk (a serial load chain here
+    // cost ~10 us)
+    float sum = 0.f;
+    for (int g0 = 0; g0 < G; g0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = g0 + j < G ? a.ws[(long)(g0 + j) * GH_SLOT + k] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sum += v[j];
+    }
+    if (k < 256) a.gw[k] = sum;
+    else if (k == 256) { if (a.gb) a.gb[0] = sum; }
+    else if (k == 257) *a.gen_loss = sum * invB;
+    else *a.disc_loss = sum * invB;
+  }
+}
+
+bool launch_gan_disc_head(const GanHeadArgs& a, hipStream_t s) {
+  if (a.DH > 256 || a.DH % 4 || a.B < 1 || !a.ws || !a.gw || !a.dd1 || !a.ddf) return false;
+  hipLaunchKernelGGL(gan_disc_head_kernel, dim3(gan_head_grid(a.B)), dim3(256), 0, s, a);
+  return true;
 }
 
 }  // namespace dtfe

@@ -5,9 +5,11 @@ weights AND biases ~ N(0, 1); loss = mean((x - y)^2) (ENC:135);
 TF1 RMSProp(0.01): decay 0.9, momentum 0, eps 1e-10, ms slot initialised to 1.
 
 MI355X step program (fp32, exact-fp32 MFMA): 4 fused GEMM+bias+sigmoid
-forward kernels, a fused MSE+sigmoid-grad kernel, and per layer one wgrad
-GEMM + bias column-sum + one dgrad GEMM whose epilogue applies sigmoid'(a)
-of the layer below (TF's SigmoidGrad fused away).
+forward kernels, a fused MSE+sigmoid-grad kernel (one launch, the last workgroup stores
+the loss), and per layer one wgrad
+GEMM (bias gradient through a ones row) + one dgrad GEMM whose epilogue applies
+sigmoid'(a) of the layer below (TF's SigmoidGrad fused away), the pair as ONE
+launch.
 """
 from __future__ import annotations
 
@@ -57,6 +59,8 @@ class AutoencoderProgram(StepProgram):
         self.a = [torch.empty(B, d, **f) for d in DIMS[1:]]
         self.dz = [torch.empty(B, d, **f) for d in DIMS[1:]]
         self.loss = torch.zeros(1, **f)
+        self.mse_ws = torch.zeros(ops.MSE_WS_FLOATS, **f) if self.device.type == "cuda" else None
+        self.xin = self.x  # the batch the layers read: self.x, or the caller's tensor in a captured step
         n = model.names
         self.W = [self.P.view(n[k]) for k in model.w_keys]
         self.b = [self.P.view(n[k]) for k in model.b_keys]
@@ -65,11 +69,19 @@ class AutoencoderProgram(StepProgram):
 
     def load_batch(self, batch):
         x = batch[0] if isinstance(batch, (tuple, list)) else batch
-        self.x.copy_(x.reshape(self.batch_size, DIMS[0]))
+        x = x.reshape(self.batch_size, DIMS[0])
+        if (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.data_ptr() % 16 == 0
+                and torch.cuda.is_current_stream_capturing()):
+            # batch load captured with the step (bench/ref_models.py): the layers read the caller's tensor
+            # in place - no staging copy node.  An eager load before a graph replay (train.py) must copy.
+            self.xin = x
+            return
+        self.x.copy_(x)
+        self.xin = self.x
 
     def forward(self):
         B = self.batch_size
-        inp = self.x
+        inp = self.xin
         for i in range(4):
             ops.gemm(inp, self.W[i], self.a[i], M=B, N=DIMS[i + 1], K=DIMS[i], bmode=ops.RMAJ, ldb=DIMS[i + 1],
                      bias=self.b[i], act=ops.ACT_SIGMOID)
@@ -80,14 +92,16 @@ class AutoencoderProgram(StepProgram):
         B = self.batch_size
         # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
         y = self.forward()
-        ops.mse_sigmoid(y, self.x, self.loss, self.dz[3])
+        ops.mse_sigmoid(y, self.xin, self.loss, self.dz[3], ws=self.mse_ws)
         for i in range(3, -1, -1):
-            inp = self.x if i == 0 else self.a[i - 1]
-            # dW_i[K][N] = inp^T . dz_i ; db_i = sum_b dz_i through the GEMM's ones row (no colsum launch)
-            ops.gemm(inp, self.dz[i], self.gW[i], M=DIMS[i] + 1, N=DIMS[i + 1], K=B, amode=ops.RMAJ, lda=DIMS[i],
-                     bmode=ops.RMAJ, ldb=DIMS[i + 1], a_ones_row=DIMS[i], bias_out=self.gb[i])
-            if i > 0:
-                # dz_{i-1} = (dz_i . W_i^T) * sigmoid'(a_{i-1})
-                ops.gemm(self.dz[i], self.W[i], self.dz[i - 1], M=B, N=DIMS[i], K=DIMS[i + 1],
-                         bmode=ops.KMAJ, ldb=DIMS[i + 1], aux=self.a[i - 1], aux_act=ops.ACT_SIGMOID)
+            inp = self.xin if i == 0 else self.a[i - 1]
+            # a layer's weight and data gradients are independent: one paired launch (ops.gemm_group)
+            with ops.gemm_group(self.loss):
+                # dW_i[K][N] = inp^T . dz_i ; db_i = sum_b dz_i through the GEMM's ones row (no colsum launch)
+                ops.gemm(inp, self.dz[i], self.gW[i], M=DIMS[i] + 1, N=DIMS[i + 1], K=B, amode=ops.RMAJ,
+                         lda=DIMS[i], bmode=ops.RMAJ, ldb=DIMS[i + 1], a_ones_row=DIMS[i], bias_out=self.gb[i])
+                if i > 0:
+                    # dz_{i-1} = (dz_i . W_i^T) * sigmoid'(a_{i-1})
+                    ops.gemm(self.dz[i], self.W[i], self.dz[i - 1], M=B, N=DIMS[i], K=DIMS[i + 1],
+                             bmode=ops.KMAJ, ldb=DIMS[i + 1], aux=self.a[i - 1], aux_act=ops.ACT_SIGMOID)
         return {"loss": self.loss}

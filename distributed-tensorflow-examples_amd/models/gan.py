@@ -8,8 +8,9 @@ Two TF1 Adams (lr 2e-4) over disjoint var_lists, both advancing global_step
 (so it moves by 2 per iteration, GAN:158-159).
 
 MI355X step program (fp32, exact-fp32 MFMA GEMMs):
-  noise (device hash RNG) -> G (2 fused GEMM+bias+act) -> D on the stacked
-  [real; fake] batch (one 2B-row GEMM pair) -> fused GAN-loss kernel ->
+  noise (device hash RNG) -> G (2 fused GEMM+bias+act) -> D's hidden layer on
+  the stacked [real; fake] batch (one 2B-row GEMM) -> ONE discriminator-head
+  kernel (output layer, both losses, dWd2 and the gradients at d1) ->
   backward of both losses from the SAME parameter snapshot.  The reference
   runs train_gen / train_disc unordered in one sess.run (a race, SURVEY §5.2);
   here both gradients come from one snapshot and the ps applies them in a
@@ -82,6 +83,9 @@ class GanProgram(StepProgram):
         self.noise_ctr = torch.zeros(1, dtype=torch.int64, device=d)
         self.noise_done = torch.zeros(1, dtype=torch.int32, device=d)
         self.seed = seed
+        # the discriminator's output layer, both losses and their gradients down to d1 in one launch
+        # (ops.gan_disc_head: 5 launches -> 1); GPU only
+        self.head_ws = (torch.zeros(ops.gan_head_ws_floats(B, DH), **f) if self.device.type == "cuda" else None)
         n = model.names
         self.W = {k: self.P.view(n[k]) for k in ("Wg1", "Wg2", "Wd1", "Wd2", "bg1", "bg2", "bd1", "bd2")}
         self.G = {k: self.P.gview(n[k]) for k in self.W}
@@ -98,7 +102,8 @@ class GanProgram(StepProgram):
         ops.uniform_fill(self.z, -1.0, 1.0, seed=self.seed, counter=self.noise_ctr, done=self.noise_done,
                          copy=(x, real) if fused else None)
 
-    def forward(self):
+    def forward(self, d2=True):
+        """``d2=False``: stop at d1 (the fused discriminator head forms p itself)."""
         B, W = self.batch_size, self.W
         R = ops.RMAJ
         ops.gemm(self.z, W["Wg1"], self.h1, M=B, N=GH, K=NOISE, bmode=R, ldb=GH, bias=W["bg1"], act=ops.ACT_RELU)
@@ -106,33 +111,46 @@ class GanProgram(StepProgram):
         ops.gemm(self.h1, W["Wg2"], fake, M=B, N=IMG, K=GH, bmode=R, ldb=IMG, bias=W["bg2"], act=ops.ACT_SIGMOID)
         ops.gemm(self.xx, W["Wd1"], self.d1, M=2 * B, N=DH, K=IMG, bmode=R, ldb=DH, bias=W["bd1"],
                  act=ops.ACT_RELU)
-        ops.gemm(self.d1, W["Wd2"], self.p, M=2 * B, N=1, K=DH, bmode=R, ldb=1, bias=W["bd2"],
-                 act=ops.ACT_SIGMOID)
+        if d2:
+            ops.gemm(self.d1, W["Wd2"], self.p, M=2 * B, N=1, K=DH, bmode=R, ldb=1, bias=W["bd2"],
+                     act=ops.ACT_SIGMOID)
 
     def compute_grads(self):
         B, W, G = self.batch_size, self.W, self.G
         R, K = ops.RMAJ, ops.KMAJ
         # no P.grad.zero_(): every gradient element is stored (not accumulated) by this step's kernels
-        self.forward()
-        ops.gan_loss(self.p[:B], self.p[B:], self.gen_loss, self.disc_loss, self.dlog[:B], self.dlog[B:],
-                     self.dlog_g)
-        # ---- discriminator: d disc_loss over the stacked batch
-        # weight grads carry their bias grads in a ones row of A (no separate column-sum launches)
-        ops.gemm(self.d1, self.dlog, G["Wd2"], M=DH + 1, N=1, K=2 * B, amode=R, lda=DH, bmode=R, ldb=1,
-                 a_ones_row=DH, bias_out=G["bd2"])
-        ops.gemm(self.dlog, W["Wd2"], self.dd1, M=2 * B, N=DH, K=1, amode=K, lda=1, bmode=K, ldb=1,
-                 aux=self.d1, aux_act=ops.ACT_RELU)
-        ops.gemm(self.xx, self.dd1, G["Wd1"], M=IMG + 1, N=DH, K=2 * B, amode=R, lda=IMG, bmode=R, ldb=DH,
-                 a_ones_row=IMG, bias_out=G["bd1"])
-        # ---- generator: d gen_loss through D (same parameter snapshot)
-        ops.gemm(self.dlog_g, W["Wd2"], self.ddf, M=B, N=DH, K=1, amode=K, lda=1, bmode=K, ldb=1,
-                 aux=self.d1[B:], aux_act=ops.ACT_RELU)
-        ops.gemm(self.ddf, W["Wd1"], self.dg, M=B, N=IMG, K=DH, amode=K, lda=DH, bmode=K, ldb=DH,
-                 aux=self.xx[B:], aux_act=ops.ACT_SIGMOID)
-        ops.gemm(self.h1, self.dg, G["Wg2"], M=GH + 1, N=IMG, K=B, amode=R, lda=GH, bmode=R, ldb=IMG,
-                 a_ones_row=GH, bias_out=G["bg2"])
-        ops.gemm(self.dg, W["Wg2"], self.dh1, M=B, N=GH, K=IMG, amode=K, lda=IMG, bmode=K, ldb=IMG,
-                 aux=self.h1, aux_act=ops.ACT_RELU)
+        fused = self.head_ws is not None
+        self.forward(d2=not fused)
+        if fused and ops.gan_disc_head(self.d1, W["Wd2"], W["bd2"], self.p, self.dlog, self.dlog_g, G["Wd2"],
+                                       G["bd2"], self.dd1, self.ddf, self.gen_loss, self.disc_loss, self.head_ws):
+            pass  # p, both losses, dWd2 / dbd2, dd1 and ddf from one launch
+        else:
+            if fused:
+                ops.gemm(self.d1, W["Wd2"], self.p, M=2 * B, N=1, K=DH, bmode=R, ldb=1, bias=W["bd2"],
+                         act=ops.ACT_SIGMOID)
+            ops.gan_loss(self.p[:B], self.p[B:], self.gen_loss, self.disc_loss, self.dlog[:B], self.dlog[B:],
+                         self.dlog_g)
+            # ---- discriminator: d disc_loss over the stacked batch
+            # weight grads carry their bias grads in a ones row of A (no separate column-sum launches)
+            ops.gemm(self.d1, self.dlog, G["Wd2"], M=DH + 1, N=1, K=2 * B, amode=R, lda=DH, bmode=R, ldb=1,
+                     a_ones_row=DH, bias_out=G["bd2"])
+            ops.gemm(self.dlog, W["Wd2"], self.dd1, M=2 * B, N=DH, K=1, amode=K, lda=1, bmode=K, ldb=1,
+                     aux=self.d1, aux_act=ops.ACT_RELU)
+            # (generator side: d gen_loss through D, same parameter snapshot)
+            ops.gemm(self.dlog_g, W["Wd2"], self.ddf, M=B, N=DH, K=1, amode=K, lda=1, bmode=K, ldb=1,
+                     aux=self.d1[B:], aux_act=ops.ACT_RELU)
+        # each (weight gradient, data gradient) pair below is independent: one paired launch (ops.gemm_group)
+        with ops.gemm_group(self.d1):
+            ops.gemm(self.xx, self.dd1, G["Wd1"], M=IMG + 1, N=DH, K=2 * B, amode=R, lda=IMG, bmode=R, ldb=DH,
+                     a_ones_row=IMG, bias_out=G["bd1"])
+            # ---- generator: d gen_loss through D (same parameter snapshot)
+            ops.gemm(self.ddf, W["Wd1"], self.dg, M=B, N=IMG, K=DH, amode=K, lda=DH, bmode=K, ldb=DH,
+                     aux=self.xx[B:], aux_act=ops.ACT_SIGMOID)
+        with ops.gemm_group(self.d1):
+            ops.gemm(self.h1, self.dg, G["Wg2"], M=GH + 1, N=IMG, K=B, amode=R, lda=GH, bmode=R, ldb=IMG,
+                     a_ones_row=GH, bias_out=G["bg2"])
+            ops.gemm(self.dg, W["Wg2"], self.dh1, M=B, N=GH, K=IMG, amode=K, lda=IMG, bmode=K, ldb=IMG,
+                     aux=self.h1, aux_act=ops.ACT_RELU)
         ops.gemm(self.z, self.dh1, G["Wg1"], M=NOISE + 1, N=GH, K=B, amode=R, lda=NOISE, bmode=R, ldb=GH,
                  a_ones_row=NOISE, bias_out=G["bg1"])
         return {"gen_loss": self.gen_loss, "disc_loss": self.disc_loss}

@@ -28,7 +28,7 @@ __all__ = [
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
     "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard", "conv1_wgrad_pooled_f32",
-    "head_xent_f32",
+    "head_xent_f32", "gan_disc_head", "gan_head_ws_floats",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -661,6 +661,8 @@ def gemm_group(anchor):
     """Grouped launch: the head_wgrad and glds-tile-12 one-split gemm calls inside the block are
     recorded and leave as ONE kernel launch at its end (head weight gradient, then the
     (KMAJ, RMAJ) and (RMAJ, RMAJ) GEMMs in recording order; any other mix launches one by one).
+    fp32 small-tile GEMMs (the GAN / autoencoder layers): a (RMAJ, RMAJ) weight gradient and a
+    (KMAJ, KMAJ) data gradient recorded in the block leave as one paired launch.
     CPU tensors: a no-op (the ops run eagerly)."""
     if not anchor.is_cuda:
         yield
@@ -808,9 +810,52 @@ def gan_loss(d_real, d_fake, gen_loss, disc_loss, dz_real_disc, dz_fake_disc, dz
     dz_fake_gen.view(-1).copy_(-(1 - pf) / B)
 
 
-def mse_sigmoid(y, t, loss, dz):
+def gan_head_ws_floats(B: int, DH: int) -> int:
+    """Workspace floats of gan_disc_head (mirrors gan_head_ws_floats in csrc/kernels/head.hip)."""
+    return max(1, min(256, (B + 3) // 4)) * 260 + 4
+
+
+def gan_disc_head(d1, w, b, p, dlog, dlog_g, gw, gb, dd1, ddf, gen_loss, disc_loss, ws=None, clamp_eps=0.0) -> bool:
+    """The GAN discriminator's output layer + both GAN losses + their gradients down to the hidden layer
+    (csrc/kernels/head.h GanHeadArgs): d1 [2B][DH] (real rows, then fake rows), w = Wd2 [DH] (, b = bd2):
+    p = sigmoid(d1 w + b) [2B], gen_loss / disc_loss (stored), dlog [2B], dlog_g [B], gw = dWd2 / gb = dbd2
+    (stored), dd1 = dlog w^T relu'(d1) [2B][DH], ddf = dlog_g w^T relu'(d1_fake) [B][DH].  GPU: one launch
+    (``ws``: gan_head_ws_floats zeroed floats, reused), returns False when the shape is not covered.  The CPU
+    path is the fp32 oracle (the gemm + gan_loss chain it replaces)."""
+    if d1.is_cuda:
+        return bool(require().gan_disc_head(d1, w, b, p, dlog, dlog_g, gw, gb, dd1, ddf, gen_loss, disc_loss, ws,
+                                            clamp_eps))
+    B = d1.shape[0] // 2
+    wv = w.reshape(-1)
+    z = d1 @ wv + (b.reshape(()) if b is not None else 0.0)
+    pp = torch.sigmoid(z)
+    dl = torch.empty(2 * B, dtype=d1.dtype)
+    dg = torch.empty(B, dtype=d1.dtype)
+    gan_loss(pp[:B], pp[B:], gen_loss, disc_loss, dl[:B], dl[B:], dg, clamp_eps=clamp_eps)
+    if p is not None:
+        p.view(-1).copy_(pp)
+    if dlog is not None:
+        dlog.view(-1).copy_(dl)
+    if dlog_g is not None:
+        dlog_g.view(-1).copy_(dg)
+    gw.view(-1).copy_(d1.t() @ dl)
+    if gb is not None:
+        gb.view(-1).copy_(dl.sum().reshape(1))
+    mask = (d1 > 0).to(d1.dtype)
+    dd1.copy_(dl[:, None] * wv[None, :] * mask)
+    ddf.copy_(dg[:, None] * wv[None, :] * mask[B:])
+    return True
+
+
+MSE_WS_FLOATS = 132  # csrc/kernels/elementwise.h MSE_WS_FLOATS (128 partials + ticket)
+
+
+def mse_sigmoid(y, t, loss, dz, ws=None):
+    """loss = mean((y - t)^2), dz = d loss / d logit of y = sigmoid(logit).  ``ws`` (GPU, MSE_WS_FLOATS
+    zeroed floats, reused every step): one launch whose last workgroup stores the loss (no memset node,
+    bitwise-reproducible loss) instead of a memset + per-workgroup atomics."""
     if y.is_cuda:
-        require().mse_sigmoid(y, t, loss, dz)
+        require().mse_sigmoid(y, t, loss, dz, ws)
         return
     n = y.numel()
     d = y - t

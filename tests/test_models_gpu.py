@@ -189,3 +189,73 @@ def test_lstm_stage_folded_into_captured_forward(split, monkeypatch):
     assert run.graph is not None, run.capture_error
     assert prog._stage is None
     assert int(torch.ops.dtfe.lstm_status(False)) == 0
+
+
+def test_encoder_captured_load_reads_batch_in_place():
+    """Autoencoder step with load_batch captured in the graph (bench/ref_models.py): the layers read the
+    caller's batch tensor in place (no staging copy) and the MSE loss is stored by the kernel's last
+    workgroup (no memset).  Replays over a refilled input buffer give the eager gradients and loss
+    bitwise (the ticketed loss sum is order-fixed)."""
+    from dtfe.utils.graphs import StepGraph
+    model = AutoencoderModel()
+    B = 256
+    g = torch.Generator().manual_seed(9)
+    xs = [torch.rand(B, 784, generator=g).cuda() for _ in range(3)]
+    eager = model.program("cuda", B, seed=6)
+    refs = []
+    for x in xs:
+        eager.load_batch(x)
+        eager.compute_grads()
+        torch.cuda.synchronize()
+        refs.append((eager.P.grad.clone(), eager.loss.clone()))
+    prog = model.program("cuda", B, seed=6)
+    xb = xs[0].clone()
+
+    def step():
+        prog.load_batch(xb)
+        prog.compute_grads()
+
+    run = StepGraph(step, warmup=1)
+    for i in (0, 1, 2, 1):
+        xb.copy_(xs[i])
+        run()
+        torch.cuda.synchronize()
+        assert torch.equal(prog.P.grad, refs[i][0]), i
+        assert torch.equal(prog.loss, refs[i][1]), i
+    assert run.graph is not None, run.capture_error
+    assert prog.xin.data_ptr() == xb.data_ptr()
+
+
+@pytest.mark.parametrize("B,DH", [(128, 256), (37, 128), (5, 60)])
+def test_gan_disc_head_matches_fp32_chain(B, DH):
+    """ops.gan_disc_head (one launch: output layer, both GAN losses, dWd2 / dbd2, dd1, ddf) vs its CPU fp32
+    oracle (the N = 1 GEMM, gan_loss and the three gradient GEMMs it replaces); two launches bitwise equal
+    (ticketed fixed-order partial sums)."""
+    from dtfe import ops
+    g = torch.Generator().manual_seed(B + DH)
+    d1 = torch.relu(torch.randn(2 * B, DH, generator=g))
+    w = torch.randn(DH, 1, generator=g) / DH ** 0.5
+    b = torch.randn(1, generator=g)
+
+    def outs(dev):
+        z = lambda *s: torch.zeros(*s, device=dev)  # noqa: E731
+        return dict(p=z(2 * B, 1), dlog=z(2 * B, 1), dlog_g=z(B, 1), gw=z(DH, 1), gb=z(1), dd1=z(2 * B, DH),
+                    ddf=z(B, DH), gen=z(1), disc=z(1))
+
+    ref = outs("cpu")
+    assert ops.gan_disc_head(d1, w, b, ref["p"], ref["dlog"], ref["dlog_g"], ref["gw"], ref["gb"], ref["dd1"],
+                             ref["ddf"], ref["gen"], ref["disc"])
+    ws = torch.zeros(ops.gan_head_ws_floats(B, DH), device="cuda")
+    assert ops.gan_head_ws_floats(B, DH) == int(torch.ops.dtfe.gan_head_ws_floats(B, DH))
+    runs = []
+    for _ in range(2):
+        o = outs("cuda")
+        assert ops.gan_disc_head(d1.cuda(), w.cuda(), b.cuda(), o["p"], o["dlog"], o["dlog_g"], o["gw"], o["gb"],
+                                 o["dd1"], o["ddf"], o["gen"], o["disc"], ws)
+        torch.cuda.synchronize()
+        runs.append({k: v.cpu() for k, v in o.items()})
+    for k in ref:
+        assert torch.equal(runs[0][k], runs[1][k]), k
+        r, got = ref[k], runs[0][k]
+        err = ((got - r).norm() / (r.norm() + 1e-12)).item()
+        assert err < 2e-5, (k, err)
