@@ -7,7 +7,7 @@
 // workgroups.  The work itself is < 1 us of v_mfma_f32_16x16x4_f32 per workgroup.  Here:
 //
 //  * one workgroup per 16 x 16 output tile (the tile grid alone reaches 128-833 workgroups for
-//    these layers), its 4 waves splitting K four ways: no cross-workgroup reduction, no fences;
+//    these layers), its 16 waves splitting K sixteen ways: no cross-workgroup reduction, no fences;
 //  * every operand element of a wave's K slice is loaded straight from global memory into
 //    MFMA fragment registers, all loads issued before the first MFMA (one memory latency per
 //    16-group chunk, not one per k-tile), no LDS staging;
@@ -16,16 +16,17 @@
 //    is one 16-byte load per group, a row-contiguous one (RMAJ) four 4-byte loads that 16
 //    lanes read as one 64-byte segment.  A and B use the same k permutation, so the dot
 //    product is unchanged;
-//  * the 4 wave partials meet in LDS and are summed in wave order (bitwise reproducible), then
+//  * the wave partials meet in LDS and are summed in wave order (bitwise reproducible), then
 //    the shared dense epilogue (bias / activation / act' of aux / ones-row bias gradients /
 //    dropout / beta / second output) runs one element per thread.
 #include "gemm_dense.h"
+
+#include <type_traits>
 
 namespace dtfe {
 
 namespace {
 
-constexpr int SG_CHUNK = 16;  // 16-deep k groups per register chunk (16 x 8 = 128 VGPRs of operands)
 
 // 4 consecutive-k operand values of row r (A: m, B: n) at k = kb..kb+3 (zero past K / rows)
 template <int MODE>
@@ -50,7 +51,7 @@ __device__ __forceinline__ f32x4_t load4(const float* p, long ld, int r, int row
   return v;
 }
 
-template <int AM, int BMD>
+template <int AM, int BMD, int NW, int CH>
 __device__ __forceinline__ void gemm_small_body(const DenseGemmArgs& a, int tile, int a_vec, int b_vec,
                                                 float (*red)[16][17]) {
   const int tiles_n = (a.N + 15) >> 4;
@@ -63,13 +64,13 @@ __device__ __forceinline__ void gemm_small_body(const DenseGemmArgs& a, int tile
   const float* B = reinterpret_cast<const float*>(a.B);
   // this wave's share of the 16-deep k groups
   const int G = (a.K + 15) >> 4;
-  const int g0 = (G * w) >> 2, g1 = (G * (w + 1)) >> 2;
+  const int g0 = (G * w) / NW, g1 = (G * (w + 1)) / NW;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  for (int c0 = g0; c0 < g1; c0 += SG_CHUNK) {
-    const int nc = min(SG_CHUNK, g1 - c0);
-    f32x4_t fa[SG_CHUNK], fb[SG_CHUNK];
+  for (int c0 = g0; c0 < g1; c0 += CH) {
+    const int nc = min(CH, g1 - c0);
+    f32x4_t fa[CH], fb[CH];
 #pragma unroll
-    for (int i = 0; i < SG_CHUNK; ++i) {
+    for (int i = 0; i < CH; ++i) {
       if (i < nc) {
         const int kb = (c0 + i) * 16 + 4 * g;
         fa[i] = load4<AM>(A, a.lda, m, a_rows, a.a_ones_row, kb, a.K, a_vec);
@@ -77,7 +78,7 @@ __device__ __forceinline__ void gemm_small_body(const DenseGemmArgs& a, int tile
       }
     }
 #pragma unroll
-    for (int i = 0; i < SG_CHUNK; ++i) {
+    for (int i = 0; i < CH; ++i) {
       if (i < nc) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][j], fb[i][j], acc, 0, 0, 0);
@@ -88,10 +89,13 @@ __device__ __forceinline__ void gemm_small_body(const DenseGemmArgs& a, int tile
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[w][4 * g + j][lane & 15] = acc[j];
   __syncthreads();
+  if (threadIdx.x >= 256) return;
   const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
   const int row = tm * 16 + r, col = tn * 16 + c;
   if (row >= a.M || col >= a.N) return;
-  float x = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
+  float x = red[0][r][c];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) x += red[i][r][c];  // wave order
   const int64_t drop_step = (a.keep < 1.f && a.counter) ? *a.counter : 0;
   if (!dense_epi(a, row, col, x, drop_step, 1.f / a.keep)) return;
   const long o = (long)row * a.ldc + col;
@@ -99,10 +103,10 @@ __device__ __forceinline__ void gemm_small_body(const DenseGemmArgs& a, int tile
   else reinterpret_cast<bf16*>(a.out)[o] = f2bf(x);
 }
 
-template <int AM, int BMD>
-__global__ __launch_bounds__(256) void gemm_small_kernel(DenseGemmArgs a, int a_vec, int b_vec) {
-  __shared__ float red[4][16][17];
-  gemm_small_body<AM, BMD>(a, blockIdx.x, a_vec, b_vec, red);
+template <int AM, int BMD, int NW, int CH>
+__global__ __launch_bounds__(64 * NW) void gemm_small_kernel(DenseGemmArgs a, int a_vec, int b_vec) {
+  __shared__ float red[NW][16][17];
+  gemm_small_body<AM, BMD, NW, CH>(a, blockIdx.x, a_vec, b_vec, red);
 }
 
 // Two independent small GEMMs of one backward phase in ONE launch (a layer's weight gradient (RMAJ, RMAJ)
@@ -112,11 +116,17 @@ struct SmallPair {
   DenseGemmArgs g0, g1;
   int t0, v0a, v0b, v1a, v1b;
 };
-__global__ __launch_bounds__(256) void gemm_small_pair_kernel(SmallPair p) {
-  __shared__ float red[4][16][17];
-  if ((int)blockIdx.x < p.t0) gemm_small_body<RMAJ, RMAJ>(p.g0, blockIdx.x, p.v0a, p.v0b, red);
-  else gemm_small_body<KMAJ, KMAJ>(p.g1, blockIdx.x - p.t0, p.v1a, p.v1b, red);
+template <int NW, int CH>
+__global__ __launch_bounds__(64 * NW) void gemm_small_pair_kernel(SmallPair p) {
+  __shared__ float red[NW][16][17];
+  if ((int)blockIdx.x < p.t0) gemm_small_body<RMAJ, RMAJ, NW, CH>(p.g0, blockIdx.x, p.v0a, p.v0b, red);
+  else gemm_small_body<KMAJ, KMAJ, NW, CH>(p.g1, blockIdx.x - p.t0, p.v1a, p.v1b, red);
 }
+// 16 waves per 16 x 16 tile (K split 16 ways, 8-deep operand chunks: 89-94 VGPRs, 4 waves per SIMD):
+// these GEMMs are latency-bound chains of operand loads; on the GAN / autoencoder steps 16 waves beat 4
+// (the round-6 default until then) by 7-9 % and 8 waves (16-deep chunks, 167 VGPRs) lost 2-3 %
+// (profiles/r6_ref_models_fused.txt)
+constexpr int SW = 16, SCH = 8;
 
 int small_tiles(const DenseGemmArgs& a) { return ((a.M + 15) / 16) * ((a.N + 15) / 16); }
 int small_vec(int mode, const void* p, int ld) { return mode == KMAJ && ld % 4 == 0 && ((uintptr_t)p & 15) == 0; }
@@ -132,11 +142,11 @@ bool gemm_small_eligible(int dtype, const DenseGemmArgs& a) {
 void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s) {
   const int tiles = small_tiles(a);
   const int a_vec = small_vec(amode, a.A, a.lda), b_vec = small_vec(bmode, a.B, a.ldb);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), 0, s, a, a_vec, b_vec); };
-  if (amode == KMAJ && bmode == KMAJ) go(gemm_small_kernel<KMAJ, KMAJ>);
-  else if (amode == KMAJ && bmode == RMAJ) go(gemm_small_kernel<KMAJ, RMAJ>);
-  else if (amode == RMAJ && bmode == KMAJ) go(gemm_small_kernel<RMAJ, KMAJ>);
-  else go(gemm_small_kernel<RMAJ, RMAJ>);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles), dim3(64 * SW), 0, s, a, a_vec, b_vec); };
+  if (amode == KMAJ && bmode == KMAJ) go(gemm_small_kernel<KMAJ, KMAJ, SW, SCH>);
+  else if (amode == KMAJ && bmode == RMAJ) go(gemm_small_kernel<KMAJ, RMAJ, SW, SCH>);
+  else if (amode == RMAJ && bmode == KMAJ) go(gemm_small_kernel<RMAJ, KMAJ, SW, SCH>);
+  else go(gemm_small_kernel<RMAJ, RMAJ, SW, SCH>);
 }
 
 void launch_gemm_small_group(int n, const int* am, const int* bm, const DenseGemmArgs* g, hipStream_t s) {
@@ -157,7 +167,8 @@ void launch_gemm_small_group(int n, const int* am, const int* bm, const DenseGem
   p.v0b = small_vec(RMAJ, p.g0.B, p.g0.ldb);
   p.v1a = small_vec(KMAJ, p.g1.A, p.g1.lda);
   p.v1b = small_vec(KMAJ, p.g1.B, p.g1.ldb);
-  hipLaunchKernelGGL(gemm_small_pair_kernel, dim3(p.t0 + small_tiles(p.g1)), dim3(256), 0, s, p);
+  const int grid = p.t0 + small_tiles(p.g1);
+  hipLaunchKernelGGL((gemm_small_pair_kernel<SW, SCH>), dim3(grid), dim3(64 * SW), 0, s, p);
 }
 
 }  // namespace dtfe
