@@ -199,8 +199,13 @@ class Optimizer:
     # ---- plan of work items for the fused kernel
     def _build_plan(self, chunk: int = 0):
         # flat work items of `chunk` elements (DTFE_OPT_CHUNK; multiple of 1024): one workgroup
-        # each, up to 2048 workgroups per launch
-        chunk = chunk or int(os.environ.get("DTFE_OPT_CHUNK", "8192"))
+        # each, up to 2048 workgroups per launch.  Default 8192; 2048 for var lists under 2 M elements
+        # (the GAN's two Adams over 0.43 M params: 52 workgroups -> 209, 0.0736 -> 0.0702 ms/step; the
+        # autoencoder -1 %, LSTM / ResNet-20 neutral - profiles/r6_ref_models_fused.txt)
+        if not chunk:
+            env = os.environ.get("DTFE_OPT_CHUNK")
+            total = sum(self.P.spec(name).numel for name in self.var_list)
+            chunk = int(env) if env else (2048 if total < 2_000_000 else 8192)
         segs, work = [], []
         for si, name in enumerate(self.var_list):
             s = self.P.spec(name)
