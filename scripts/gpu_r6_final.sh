@@ -20,8 +20,8 @@ row r50 --model resnet50 --steps 20 --warmup 5
 row cnn_x2_ipc --gpus 2 --backend gloo --comm ipc --steps 20 --warmup 5
 row r20_x2_ipc --model resnet20 --gpus 2 --backend gloo --comm ipc --steps 20 --warmup 5
 row ps_1p1w --mode ps --gpus 1 --steps 200 --warmup 20
-row ps_1p8w --mode ps --gpus 8 --steps 50 --warmup 10
-row ps_2p8w --mode ps --gpus 8 --num_ps 2 --ps_partition_mb 4 --steps 50 --warmup 10
+row ps_1p8w --mode ps --gpus 8 --steps 200 --warmup 20
+row ps_2p8w --mode ps --gpus 8 --num_ps 2 --ps_partition_mb 4 --steps 200 --warmup 20
 timeout -k 10 200 python3 bench/ref_models.py > $O/ref.log 2>&1 || { tail -5 $O/ref.log; exit 1; }
 grep ms_per_step $O/ref.log
 echo done
