@@ -148,3 +148,34 @@ def test_glorot_init_is_he_normal_like_reference():
 
     w = glorot_init((784, 256), torch.Generator().manual_seed(0))
     assert abs(w.std().item() - np.sqrt(2 / 784)) < 2e-3
+
+
+def test_gan_disc_head_oracle_matches_autograd():
+    """ops.gan_disc_head's CPU path (the oracle its GPU kernel is checked against) vs torch autograd of the
+    reference losses (GAN:128-143): p = sigmoid(d1 Wd2 + bd2); gen_loss = -mean(log p_fake); disc_loss =
+    -mean(log p_real + log(1 - p_fake)); gradients w.r.t. Wd2, bd2 and d1 (split into the disc / gen parts)."""
+    from dtfe import ops
+    B, DH = 6, 12
+    g = torch.Generator().manual_seed(2)
+    d1 = torch.relu(torch.randn(2 * B, DH, generator=g, dtype=torch.float64))
+    w = torch.randn(DH, 1, generator=g, dtype=torch.float64)
+    b = torch.randn(1, generator=g, dtype=torch.float64)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float64)  # noqa: E731
+    o = dict(p=z(2 * B, 1), dlog=z(2 * B, 1), dlog_g=z(B, 1), gw=z(DH, 1), gb=z(1), dd1=z(2 * B, DH), ddf=z(B, DH),
+             gen=z(1), disc=z(1))
+    assert ops.gan_disc_head(d1, w, b, o["p"], o["dlog"], o["dlog_g"], o["gw"], o["gb"], o["dd1"], o["ddf"], o["gen"],
+                             o["disc"])
+    x, wv, bv = d1.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    p = torch.sigmoid(x @ wv + bv).view(-1)
+    disc = -(torch.log(p[:B]) + torch.log(1 - p[B:])).mean()
+    gw, gb, gx = torch.autograd.grad(disc, (wv, bv, x), retain_graph=True)
+    gen = -torch.log(p[B:]).mean()
+    gxg, = torch.autograd.grad(gen, (x,))
+    mask = (d1 > 0).double()  # relu'(d1) as the backward through the hidden ReLU sees it
+    torch.testing.assert_close(o["p"].view(-1), p.detach())
+    torch.testing.assert_close(o["disc"], disc.detach().view(1))
+    torch.testing.assert_close(o["gen"], gen.detach().view(1))
+    torch.testing.assert_close(o["gw"], gw)
+    torch.testing.assert_close(o["gb"], gb)
+    torch.testing.assert_close(o["dd1"], gx * mask)
+    torch.testing.assert_close(o["ddf"], gxg[B:] * mask[B:])
