@@ -7,7 +7,7 @@
 // workgroups.  The work itself is < 1 us of v_mfma_f32_16x16x4_f32 per workgroup.  Here:
 //
 //  * one workgroup per 16 x 16 output tile (the tile grid alone reaches 128-833 workgroups for
-//    these layers), its 16 waves splitting K sixteen ways: no cross-workgroup reduction, no fences;
+//    these layers), its 4 / 8 / 16 waves splitting K (by grid size): no cross-workgroup reduction, no fences;
 //  * every operand element of a wave's K slice is loaded straight from global memory into
 //    MFMA fragment registers, all loads issued before the first MFMA (one memory latency per
 //    16-group chunk, not one per k-tile), no LDS staging;
@@ -122,11 +122,20 @@ __global__ __launch_bounds__(64 * NW) void gemm_small_pair_kernel(SmallPair p) {
   if ((int)blockIdx.x < p.t0) gemm_small_body<RMAJ, RMAJ, NW, CH>(p.g0, blockIdx.x, p.v0a, p.v0b, red);
   else gemm_small_body<KMAJ, KMAJ, NW, CH>(p.g1, blockIdx.x - p.t0, p.v1a, p.v1b, red);
 }
-// 16 waves per 16 x 16 tile (K split 16 ways, 8-deep operand chunks: 89-94 VGPRs, 4 waves per SIMD):
-// these GEMMs are latency-bound chains of operand loads; on the GAN / autoencoder steps 16 waves beat 4
-// (the round-6 default until then) by 7-9 % and 8 waves (16-deep chunks, 167 VGPRs) lost 2-3 %
-// (profiles/r6_ref_models_fused.txt)
-constexpr int SW = 16, SCH = 8;
+// 8-deep operand chunks (~90 VGPRs: 5 waves per SIMD); the 16-deep chunks of round 2 took 163 VGPRs
+constexpr int SCH = 8;
+// waves per tile by grid size: >= 512 tiles already give >= 2048 waves at a 4-way K split (fewer, longer
+// waves, a 4-partial LDS reduce), >= 256 tiles take an 8-way split, smaller grids 16 ways.  Against 16
+// everywhere: GAN 0.0697 -> 0.0624 ms, autoencoder 0.0806 -> 0.0721 (4 everywhere: 0.0674 / 0.0745; other
+// thresholds in profiles/r6_ref_models_fused.txt)
+int small_waves(long tiles) { return tiles >= 512 ? 4 : tiles >= 256 ? 8 : 16; }
+template <typename F>
+void by_waves(long tiles, F&& f) {
+  const int nw = small_waves(tiles);
+  if (nw == 4) f(std::integral_constant<int, 4>{});
+  else if (nw == 8) f(std::integral_constant<int, 8>{});
+  else f(std::integral_constant<int, 16>{});
+}
 
 int small_tiles(const DenseGemmArgs& a) { return ((a.M + 15) / 16) * ((a.N + 15) / 16); }
 int small_vec(int mode, const void* p, int ld) { return mode == KMAJ && ld % 4 == 0 && ((uintptr_t)p & 15) == 0; }
@@ -142,11 +151,14 @@ bool gemm_small_eligible(int dtype, const DenseGemmArgs& a) {
 void launch_gemm_small(int amode, int bmode, const DenseGemmArgs& a, hipStream_t s) {
   const int tiles = small_tiles(a);
   const int a_vec = small_vec(amode, a.A, a.lda), b_vec = small_vec(bmode, a.B, a.ldb);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles), dim3(64 * SW), 0, s, a, a_vec, b_vec); };
-  if (amode == KMAJ && bmode == KMAJ) go(gemm_small_kernel<KMAJ, KMAJ, SW, SCH>);
-  else if (amode == KMAJ && bmode == RMAJ) go(gemm_small_kernel<KMAJ, RMAJ, SW, SCH>);
-  else if (amode == RMAJ && bmode == KMAJ) go(gemm_small_kernel<RMAJ, KMAJ, SW, SCH>);
-  else go(gemm_small_kernel<RMAJ, RMAJ, SW, SCH>);
+  by_waves(tiles, [&](auto nwc) {
+    constexpr int SW = decltype(nwc)::value;
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(tiles), dim3(64 * SW), 0, s, a, a_vec, b_vec); };
+    if (amode == KMAJ && bmode == KMAJ) go(gemm_small_kernel<KMAJ, KMAJ, SW, SCH>);
+    else if (amode == KMAJ && bmode == RMAJ) go(gemm_small_kernel<KMAJ, RMAJ, SW, SCH>);
+    else if (amode == RMAJ && bmode == KMAJ) go(gemm_small_kernel<RMAJ, KMAJ, SW, SCH>);
+    else go(gemm_small_kernel<RMAJ, RMAJ, SW, SCH>);
+  });
 }
 
 void launch_gemm_small_group(int n, const int* am, const int* bm, const DenseGemmArgs* g, hipStream_t s) {
@@ -168,7 +180,10 @@ void launch_gemm_small_group(int n, const int* am, const int* bm, const DenseGem
   p.v1a = small_vec(KMAJ, p.g1.A, p.g1.lda);
   p.v1b = small_vec(KMAJ, p.g1.B, p.g1.ldb);
   const int grid = p.t0 + small_tiles(p.g1);
-  hipLaunchKernelGGL((gemm_small_pair_kernel<SW, SCH>), dim3(grid), dim3(64 * SW), 0, s, p);
+  by_waves(grid, [&](auto nwc) {
+    constexpr int SW = decltype(nwc)::value;
+    hipLaunchKernelGGL((gemm_small_pair_kernel<SW, SCH>), dim3(grid), dim3(64 * SW), 0, s, p);
+  });
 }
 
 }  // namespace dtfe
