@@ -643,10 +643,13 @@ def test_resnet20_bench_shaped_step_matches_autograd():
     assert abs(float(m["loss"].item()) - loss.item()) < 5e-3 * max(1.0, abs(loss.item()))
     names = [s.name for s in model.specs if not s.name.endswith(("moving_mean", "moving_variance"))]
     last = set(prog.L["blocks"][-1].var_names)
-    rows = []
+    rows, bn_g, bn_r = [], [], []
     for n in names:
         g, r = prog.P.gview(n).detach().float(), ref[n].grad.float()
         rows.append((n, _rel(g, r), _cos(g, r)))
+        if n not in last and n.endswith(("gamma", "beta")):
+            bn_g.append(g.flatten())
+            bn_r.append(r.flatten())
     head = [r for r in rows if r[0].startswith("dense")]
     tail = [r for r in rows if r[0] in last]
     rest = [r for r in rows if r not in head and r not in tail]
@@ -656,8 +659,13 @@ def test_resnet20_bench_shaped_step_matches_autograd():
     # 262k bf16 pixels with heavy cancellation: batch_normalization_3/gamma cos 0.971-0.973 with the
     # fused or the separate statistics pass alike; their betas - sum dy over the same pixels - read
     # 0.9765 in one of two otherwise identical round-6 runs: the bn_stats atomics make the bf16 step
-    # run-to-run different in the last bits, which that cancellation amplifies)
+    # run-to-run different in the last bits, which that cancellation amplifies - four repeats on one box
+    # read bn3 gamma 0.951-0.97, scripts/archive/gpu_r6_r20_cos.sh.  So the BN scale / offset gradients
+    # are pinned as ONE vector (cos >= 0.98: the well-conditioned channels carry it) with a per-variable
+    # floor of 0.93; every other variable at cos >= 0.98)
     assert all(e < 2e-2 for _, e, _ in head), head
     assert all(e < 0.15 and c > 0.99 for _, e, c in tail), tail
-    bad = [r for r in rest if r[2] < (0.96 if r[0].endswith(("gamma", "beta")) else 0.98)]
+    bn_cos = _cos(torch.cat(bn_g), torch.cat(bn_r))
+    assert bn_cos > 0.98, bn_cos
+    bad = [r for r in rest if r[2] < (0.93 if r[0].endswith(("gamma", "beta")) else 0.98)]
     assert not bad, bad
