@@ -21,7 +21,10 @@ sampling, forward, backward, gradient all-reduce, fused Adam), bracketed by
 barrier + device synchronize on both sides; the reported time is the MAX over
 ranks.  The K steps are also cut into up to 5 windows by hipEvents recorded
 between replays (no sync inside the timed region) so the JSON carries its own
-spread.  Rank 0 prints one JSON line.
+spread.  Steps run as hipGraph replays of --steps_per_graph S consecutive steps
+(default 4 on one GPU, 1 with several ranks; K is timed whatever S is, a remainder
+runs as single-step replays, and both graphs are captured before the timed region -
+those capture steps are counted in config.prewarm.steps).  Rank 0 prints one JSON line.
 
 Reference: the reference's only performance output is its per-step wall-clock
 print (gan/distributed_gan.py:195-196, encoder/distributed_encoder.py:166-167).
@@ -65,6 +68,10 @@ def parse_args(argv=None):
                     help="ResNet gradient bucket size, MB of fp32 gradient (default parallel.comm.DEFAULT_BUCKET_MB; "
                          "the CNN keeps its two buckets [head + fc1] / [convs])")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--steps_per_graph", type=int, default=0,
+                    help="training steps captured per hipGraph replay (TF2 steps_per_execution; every step is "
+                         "still a full step, K steps are timed whatever S is).  0: 4 on one GPU, 1 with "
+                         "several ranks")
     ap.add_argument("--model", choices=["mnist_cnn", "resnet20", "resnet50"], default="mnist_cnn")
     ap.add_argument("--mode", choices=["allreduce", "ps"], default="allreduce",
                     help="allreduce: sync data parallel (headline).  ps: async parameter server, "
@@ -190,6 +197,15 @@ def replicas_identical(params, d: Dist):
     return bool(float(diff.item()) == 0.0)
 
 
+def _steps_per_graph(args, d) -> int:
+    """Training steps per hipGraph replay: --steps_per_graph, else 4 on one GPU (the graph-launch gap
+    between replays is ~1.5 % of a CNN step: 0.1923-0.1933 -> 0.1903-0.1904 ms, profiles/r6_steps_per_graph.txt)
+    and 1 with several ranks (their captured collectives are only rehearsed on one GPU here)."""
+    if args.steps_per_graph > 0:
+        return args.steps_per_graph
+    return 4 if d.world == 1 else 1
+
+
 def timed(runner, steps: int, warmup: int, d: Dist, prewarm_ms: float = 0.0):
     """Pre-warm, W untimed steps, then exactly K steps between barrier+sync brackets.  Returns
     (elapsed_s max over ranks, per-window ms/step list measured on this rank, pre-warm steps).
@@ -200,32 +216,34 @@ def timed(runner, steps: int, warmup: int, d: Dist, prewarm_ms: float = 0.0):
     (1 + 4 ms of GPU work) the timed windows fell from 0.212 to 0.204 ms/step, after 100
     untimed steps they sat at 0.195-0.196 (profiles/r4_cnn_clock_ramp.txt).  The pre-warm
     steps are real steps (they train the model) and are reported in the JSON config."""
+    run = runner.run if hasattr(runner, "run") else (lambda n: [runner() for _ in range(n)])
+    S = getattr(runner, "steps", 1)
     pre = 0
     if prewarm_ms > 0:
         t = time.perf_counter()
+        chunk = max(10, S)
         while True:
-            for _ in range(10):
-                runner()
-            pre += 10
+            run(chunk)
+            pre += chunk
             torch.cuda.synchronize()
             if d.max(time.perf_counter() - t) * 1000.0 >= prewarm_ms:
                 break
-    for _ in range(warmup):
-        runner()
+    if hasattr(runner, "prime"):  # graph captures happen here, never inside the timed steps
+        pre += runner.prime()
+    run(warmup)
     torch.cuda.synchronize()
     d.barrier()
     torch.cuda.synchronize()
     nwin = max(1, min(5, steps))
-    cuts = [round(i * steps / nwin) for i in range(nwin + 1)]
+    # window cuts on replay boundaries (multiples of the steps per replay), the last one at K
+    cuts = sorted(set([0] + [min(steps, round(i * steps / nwin / S) * S) for i in range(1, nwin)] + [steps]))
+    nwin = len(cuts) - 1
     evs = [torch.cuda.Event(enable_timing=True) for _ in cuts]
     t0 = time.perf_counter()
     evs[0].record()
-    w = 1
-    for i in range(steps):
-        runner()
-        if i + 1 == cuts[w]:
-            evs[w].record()
-            w += 1
+    for w in range(nwin):
+        run(cuts[w + 1] - cuts[w])
+        evs[w + 1].record()
     torch.cuda.synchronize()
     d.barrier()
     torch.cuda.synchronize()
@@ -308,7 +326,7 @@ def bench_cnn(args, d: Dist):
     import dtfe  # noqa: F401
     from dtfe.models.mnist_cnn import MnistCnnTrainer, num_params
     from dtfe.parallel.allreduce import BucketAllReduce
-    from dtfe.utils.graphs import StepGraph, graphs_enabled
+    from dtfe.utils.graphs import MultiStepGraph, graphs_enabled
 
     B = args.batch_size or MODEL_BATCH["mnist_cnn"]
     if args.dtype == "fp32":
@@ -332,15 +350,17 @@ def bench_cnn(args, d: Dist):
     else:
         step = trainer.step
     # the whole step (with the overlapped all-reduce at world > 1) is one hipGraph replay
-    runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
-                                                and graphs_enabled()), capture_error_mode="thread_local")
+    runner = MultiStepGraph(step, _steps_per_graph(args, d), warmup=2,
+                            enabled=((d.world == 1 or comm is not None) and not args.no_graph and graphs_enabled()),
+                            capture_error_mode="thread_local")
     elapsed, win, pre = timed(runner, args.steps, args.warmup, d, args.prewarm_ms)
     if comm is not None and hasattr(comm, "check_health"):
         comm.check_health()
     loss = float(trainer.loss_sum.item()) / B
     same = replicas_identical(trainer.P.master, d) if d.world > 1 else None
     ndev = d.distinct_devices()
-    extra = {"optimizer": "adam (TF1)", "hip_graph": runner.graph is not None, "last_loss": round(loss, 4),
+    extra = {"optimizer": "adam (TF1)", "hip_graph": runner.graph is not None, "steps_per_graph": runner.steps,
+             "last_loss": round(loss, 4),
              "replicas_identical": same, "distinct_gpus": ndev, "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
     extra.update(_comm_info(args, d, comm))
     _emit(d, args, "images/sec (whole node), MNIST CNN sync all-reduce", B * d.world * args.steps / elapsed,
@@ -360,7 +380,7 @@ def bench_resnet(args, d: Dist):
     from dtfe.optim import Optimizer
     from dtfe.parallel.allreduce import BucketAllReduce
     from dtfe.train import _buckets
-    from dtfe.utils.graphs import StepGraph, graphs_enabled
+    from dtfe.utils.graphs import MultiStepGraph, graphs_enabled
 
     model = ResNetModel(arch=args.model)
     B = args.batch_size or MODEL_BATCH[args.model]
@@ -404,13 +424,13 @@ def bench_resnet(args, d: Dist):
             g16 = ar.grad16
         opt.step(grad16=g16, gscale=1.0 / d.world) if g16 is not None else opt.step(gscale=1.0 / d.world)
 
-    runner = StepGraph(step, warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
+    runner = MultiStepGraph(step, _steps_per_graph(args, d), warmup=2, enabled=((d.world == 1 or comm is not None) and not args.no_graph
                                                 and graphs_enabled()), capture_error_mode="thread_local")
     elapsed, win, pre = timed(runner, args.steps, args.warmup, d, args.prewarm_ms)
     # trainable variables only: BN moving statistics are per-replica (each rank's own batches)
     train_vals = torch.cat([prog.P.view(n).reshape(-1) for n in names])
     same = replicas_identical(train_vals, d) if d.world > 1 else None
-    extra = {"optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None,
+    extra = {"optimizer": "momentum 0.9 (TF1)", "hip_graph": runner.graph is not None, "steps_per_graph": runner.steps,
              "last_loss": round(float(prog.loss.item()) / B, 4), "replicas_identical": same,
              "distinct_gpus": d.distinct_devices(), "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
     extra.update(_comm_info(args, d, comm))

@@ -25,10 +25,10 @@ import torch  # noqa: E402
 import dtfe  # noqa: E402,F401
 from dtfe.optim import Optimizer  # noqa: E402
 from dtfe.train import MODELS  # noqa: E402
-from dtfe.utils.graphs import StepGraph  # noqa: E402
+from dtfe.utils.graphs import MultiStepGraph  # noqa: E402
 
 
-def time_model(name, steps, warmup, graph=True):
+def time_model(name, steps, warmup, graph=True, steps_per_graph=1):
     cls, lr = MODELS[name]
     model = cls(lr=lr)
     dev = torch.device("cuda", 0)
@@ -47,17 +47,15 @@ def time_model(name, steps, warmup, graph=True):
         # all of the step's optimizers in one launch (TF: the minimize ops of one sess.run)
         Optimizer.step_all(opts, [model.gs_increments if i == len(opts) - 1 else 0 for i in range(len(opts))])
 
-    run = StepGraph(step, warmup=2, enabled=graph)
-    for _ in range(warmup):
-        run()
+    run = MultiStepGraph(step, steps_per_graph, warmup=2, enabled=graph)
+    run.run(warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        run()
+    run.run(steps)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     return {"model": name, "batch": B, "ms_per_step": round(ms, 4), "hip_graph": run.graph is not None,
-            "global_step": int(gstep.item())}
+            "steps_per_graph": run.steps, "global_step": int(gstep.item())}
 
 
 def main():
@@ -66,9 +64,11 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--steps_per_graph", type=int, default=1, help="training steps per hipGraph replay")
     a = ap.parse_args()
     for m in a.models.split(","):
-        print(json.dumps(time_model(m, a.steps, a.warmup, graph=not a.no_graph)), flush=True)
+        print(json.dumps(time_model(m, a.steps, a.warmup, graph=not a.no_graph, steps_per_graph=a.steps_per_graph)),
+              flush=True)
 
 
 if __name__ == "__main__":
