@@ -68,6 +68,8 @@ def parse_args(argv=None):
                     help="ResNet gradient bucket size, MB of fp32 gradient (default parallel.comm.DEFAULT_BUCKET_MB; "
                          "the CNN keeps its two buckets [head + fc1] / [convs])")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--no_join_defer", action="store_true",
+                    help="CNN: join the conv2 weight-gradient branch before Adam in every step (A/B hook)")
     ap.add_argument("--steps_per_graph", type=int, default=0,
                     help="training steps captured per hipGraph replay (TF2 steps_per_execution; every step is "
                          "still a full step, K steps are timed whatever S is).  0: 4 on one GPU, 1 with "
@@ -350,9 +352,13 @@ def bench_cnn(args, d: Dist):
     else:
         step = trainer.step
     # the whole step (with the overlapped all-reduce at world > 1) is one hipGraph replay
-    runner = MultiStepGraph(step, _steps_per_graph(args, d), warmup=2,
+    spg = _steps_per_graph(args, d)
+    # one replica, several steps per replay: the conv2 weight-gradient branch rejoins once per replay and
+    # signals Adam on the device instead (MnistCnnTrainer.defer_join; profiles/r6_steps_per_graph.txt)
+    trainer.defer_join = spg > 1 and allreduce is None and args.dtype != "fp32" and not args.no_join_defer
+    runner = MultiStepGraph(step, spg, warmup=2,
                             enabled=((d.world == 1 or comm is not None) and not args.no_graph and graphs_enabled()),
-                            capture_error_mode="thread_local")
+                            capture_error_mode="thread_local", finish=trainer.join_side)
     elapsed, win, pre = timed(runner, args.steps, args.warmup, d, args.prewarm_ms)
     if comm is not None and hasattr(comm, "check_health"):
         comm.check_health()
@@ -360,7 +366,7 @@ def bench_cnn(args, d: Dist):
     same = replicas_identical(trainer.P.master, d) if d.world > 1 else None
     ndev = d.distinct_devices()
     extra = {"optimizer": "adam (TF1)", "hip_graph": runner.graph is not None, "steps_per_graph": runner.steps,
-             "last_loss": round(loss, 4),
+             "join_deferred": bool(getattr(trainer, "defer_join", False)), "last_loss": round(loss, 4),
              "replicas_identical": same, "distinct_gpus": ndev, "prewarm": {"ms": args.prewarm_ms, "steps": pre}}
     extra.update(_comm_info(args, d, comm))
     _emit(d, args, "images/sec (whole node), MNIST CNN sync all-reduce", B * d.world * args.steps / elapsed,

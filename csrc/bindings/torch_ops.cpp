@@ -547,6 +547,23 @@ Tensor opt_pack(const Tensor& segs, const Tensor& work, const Tensor& device_lik
   return host.to(device_like.device());
 }
 
+// apply_wait_next(done, seen, segs): the NEXT apply_gradients call's items of the segments in the bit mask
+// `segs` wait on the device-side counter pair (OptArgs::wait_done / wait_seen) - a gradient produced on
+// another stream with no graph edge to the optimizer launch (the CNN's conv2 weight-gradient branch)
+struct ApplyWait { int* done = nullptr; int* seen = nullptr; uint32_t segs = 0; };
+thread_local ApplyWait g_apply_wait;
+void apply_wait_next(const Tensor& done, const Tensor& seen, int64_t segs) {
+  check_cuda(done, "done");
+  TORCH_CHECK(done.scalar_type() == at::kInt && seen.scalar_type() == at::kInt && done.numel() >= 1 && seen.numel() >= 1,
+              "apply_wait_next: int32 counters");
+  g_apply_wait = ApplyWait{done.data_ptr<int>(), seen.data_ptr<int>(), (uint32_t)segs};
+}
+void epoch_signal(const Tensor& ctr) {
+  check_cuda(ctr, "ctr");
+  TORCH_CHECK(ctr.scalar_type() == at::kInt && ctr.numel() >= 1, "epoch_signal: int32 counter");
+  dtfe::launch_epoch_signal(ctr.data_ptr<int>(), cur_stream());
+}
+
 void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, const optional<Tensor>& g16,
                      double gscale, const optional<Tensor>& s1, const optional<Tensor>& s2, double lr, double beta1,
                      double beta2, double eps, double momentum, double rho, const optional<Tensor>& beta_pow,
@@ -578,6 +595,8 @@ void apply_gradients(int64_t kind, const Tensor& p, const optional<Tensor>& g, c
   if (kind == dtfe::OPT_ADAM) TORCH_CHECK(a.beta_pow && a.s1 && a.s2, "adam needs slots and beta powers");
   if (kind == dtfe::OPT_RMSPROP) TORCH_CHECK(a.s1 && a.s2, "rmsprop needs slots");
   if (kind == dtfe::OPT_MOMENTUM) TORCH_CHECK(a.s1, "momentum needs a slot");
+  a.wait_done = g_apply_wait.done; a.wait_seen = g_apply_wait.seen; a.wait_segs = g_apply_wait.segs;
+  g_apply_wait = ApplyWait{};
   if (group == 0) {
     TORCH_CHECK(pending.empty(), "apply_gradients: a queued group was never launched");
     dtfe::launch_apply_gradients(a, cur_stream());
@@ -1237,6 +1256,8 @@ TORCH_LIBRARY(dtfe, m) {
         " Tensor(d!) gw, Tensor(e!)? gb, Tensor(f!) dd1, Tensor(g!) ddf, Tensor(h!) gen_loss, Tensor(i!) disc_loss,"
         " Tensor(j!) ws, float clamp_eps=0.0) -> bool");
   m.def("gan_head_ws_floats(int B, int DH) -> int");
+  m.def("apply_wait_next(Tensor done, Tensor seen, int segs) -> ()");
+  m.def("epoch_signal(Tensor(a!) ctr) -> ()");
   m.def("mse_sigmoid(Tensor y, Tensor t, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? ws=None) -> ()");
   m.def("colsum(Tensor x, int M, int N, int ld, Tensor(a!) db, float scale) -> ()");
   m.def("unpool_f32(Tensor g, Tensor argmax, Tensor(a!) out, int B, int PH, int PW, int C) -> ()");
@@ -1282,6 +1303,8 @@ TORCH_LIBRARY_IMPL(dtfe, CUDA, m) {
   m.impl("gan_loss", &gan_loss);
   m.impl("mse_sigmoid", &mse_sigmoid);
   m.impl("gan_disc_head", &gan_disc_head);
+  m.impl("apply_wait_next", &apply_wait_next);
+  m.impl("epoch_signal", &epoch_signal);
   m.impl("colsum", &colsum);
   m.impl("unpool_f32", &unpool_f32);
   m.impl("head_xent_f32", &head_xent_f32);

@@ -49,7 +49,13 @@ struct OptArgs {
   const int32_t* rep_gs;
   uint64_t rep_seq, rep_ver;
   int rep_stale;
+  // optional device-side dependency (a gradient produced on another stream with no graph edge to this
+  // launch): the work items of segments in wait_segs wait until *wait_done exceeds *wait_seen (set by
+  // epoch_signal_kernel after the producer); the last workgroup then advances *wait_seen
+  const int* wait_done; int* wait_seen; uint32_t wait_segs;
 };
+// *ctr += 1 (agent-scope release) - launched on the producer's stream right after the producer
+void launch_epoch_signal(int* ctr, hipStream_t s);
 
 void launch_apply_gradients(const OptArgs& a, hipStream_t s);
 // the non-slot scalars of one optimizer step: beta powers (Adam) and global_step += gs_inc

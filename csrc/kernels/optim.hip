@@ -136,9 +136,25 @@ template <int KIND, bool G16>
 __device__ __forceinline__ void apply_items(const OptArgs& a, int bid, int nblk, bf16 (&tile)[64][66]) {
   float lr_t = a.lr;
   if (KIND == OPT_ADAM) lr_t = tf1_adam_lr(a.lr, a.beta_pow);
+  bool waited = false;
   for (int wi = bid; wi < a.nwork; wi += nblk) {
     const OptWork w = a.work[wi];
     const OptSeg sg = a.segs[w.seg];
+    if (a.wait_done && !waited && w.seg < 32 && ((a.wait_segs >> w.seg) & 1u)) {
+      // the producer (another stream, no graph edge) signals through *wait_done; poll with a bounded
+      // wall-clock wait (a producer that never ran: proceed rather than hang the device)
+      if (threadIdx.x == 0) {
+        const int target = __hip_atomic_load(a.wait_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+               wall_clock64() - t0 < 200000000ull)  // 2 s at 100 MHz
+          __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      waited = true;
+    }
     if (w.kind == 0) {
       const long base = sg.off + w.start;
       const long n4 = ((base & 3) == 0) ? (w.count / 4) * 4 : 0;  // segments are 64-aligned; chunks 8192
@@ -242,6 +258,8 @@ __device__ __forceinline__ void apply_body(const OptArgs& a, int bid, int nblk, 
       }
       if (a.global_step && a.gs_inc) atomicAdd(a.global_step, a.gs_inc);
     }
+    if (prev == (uint32_t)nblk - 1 && a.wait_seen)
+      __hip_atomic_fetch_add(a.wait_seen, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (uint32_t)nblk - 1 && a.rep_slot) publish_reply(a);
     if (prev == (uint32_t)nblk - 1) __hip_atomic_store(a.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -286,6 +304,11 @@ __global__ void opt_advance_reply_kernel(OptAdvanceSet g) {
   for (int i = 0; i < g.n; ++i) advance_one(g.o[i]);
   if (g.o[g.n - 1].rep_slot) publish_reply(g.o[g.n - 1]);
 }
+
+__global__ void epoch_signal_kernel(int* ctr) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+void launch_epoch_signal(int* ctr, hipStream_t s) { hipLaunchKernelGGL(epoch_signal_kernel, dim3(1), dim3(64), 0, s, ctr); }
 
 static int apply_blocks(const OptArgs& a) {
   int blocks = a.nwork < 2048 ? a.nwork : 2048;

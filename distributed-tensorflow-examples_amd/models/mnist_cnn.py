@@ -249,6 +249,15 @@ class MnistCnnTrainer:
         if self.par:
             self.s_c2 = torch.cuda.Stream(device=d)
             self.ws_c2 = torch.empty(ops.wgrad_ws_floats(C2, KS * KS * C1), device=d, dtype=torch.float32)
+            # deferred join (opt-in, one replica, no all-reduce: bench.py with several steps per hipGraph
+            # replay): the conv2 weight-gradient branch signals a device counter instead of a stream join
+            # before Adam - Adam's wc2 / bc2 items wait on it (OptArgs::wait_done) - and the branch rejoins
+            # the launch stream only in join_side(), once per replay.  The join is a cross-queue barrier
+            # that idled the GPU ~11 us per step (profiles/r6_steps_per_graph.txt).
+            self.c2_done = torch.zeros(1, device=d, dtype=torch.int32)
+            self.c2_seen = torch.zeros(1, device=d, dtype=torch.int32)
+        self.defer_join = False
+        self._signalled = False
         # (the conv weight-gradient partial reduces stay their own launches: summing the partial slabs
         # inside the Adam launch measured 0.2033-0.2042 vs 0.1989-0.1997 ms/step,
         # profiles/r4_cnn_step_b1024.txt)
@@ -317,13 +326,19 @@ class MnistCnnTrainer:
             self.s_c2.wait_stream(main)
         self._conv2_dgrad()
         self.schedule.append("conv2_dgrad")
+        signal = self.par and self.defer_join and self.allreduce is None
         with torch.cuda.stream(self.s_c2) if self.par else contextlib.nullcontext():
             # conv2 wgrad: dW = sum_p un-pool(dP2)[p] (x) P1[p + tap] ; bias grad alongside
             ops.imgwgrad(self.p1, self.gw["wc2"], self.gw["bc2"], dy_pooled=self.dp2, dy_argmax=self.a2,
                          workspace=self.ws_c2 if self.par else None,
                          max_blocks=self.c2_blocks if self.par else 0, **self.ic2)
+            if signal:
+                ops.epoch_signal(self.c2_done)
         ops.imgwgrad(self.x, self.gw["wc1"], self.gw["bc1"], dy_pooled=self.dp1, dy_argmax=self.a1, **self.ic1)
-        if self.par:
+        self._signalled = signal
+        if signal:
+            self._pending_join = True
+        elif self.par:
             main.wait_stream(self.s_c2)
         if self.allreduce is not None:
             self.allreduce.launch(1)
@@ -388,6 +403,10 @@ class MnistCnnTrainer:
         gscale = 1.0 / self.world if gscale is None else gscale
         if not self.par or not (self.late_split and self.allreduce is not None):
             self.forward_backward()
+            if getattr(self, "_signalled", False):  # Adam's conv2 items wait for the branch's device-side signal
+                vl = self.opt.var_list
+                mask = sum(1 << vl.index(self.names[k]) for k in ("wc2", "bc2"))
+                ops.apply_wait_next(self.c2_done, self.c2_seen, mask)
             self.opt.step(grad16=grad16, gscale=gscale)
             return
         self._ensure_split()
@@ -396,6 +415,13 @@ class MnistCnnTrainer:
             self.forward_backward()
         finally:
             self._late = None
+
+    def join_side(self):
+        """Rejoin the conv2 weight-gradient branch to the launch stream (after the last step of a replay when
+        ``defer_join`` is on; a no-op otherwise)."""
+        if getattr(self, "_pending_join", False):
+            torch.cuda.current_stream(self.device).wait_stream(self.s_c2)
+            self._pending_join = False
 
     def flops_per_image(self) -> float:
         """Training FLOPs per image (fwd + dgrad + wgrad of every GEMM-shaped op)."""

@@ -28,7 +28,7 @@ __all__ = [
     "bn_bwd_apply", "relu_bits", "shortcut_grad_add",
     "gap_fwd", "gap_bwd", "gemm_group", "seq_stage", "wgrad_tallk", "tallk_ws_floats", "maxpool3_fwd", "maxpool3_bwd", "bn_relu_pool3", "pool3_bn_bwd", "imgconv", "imgwgrad", "hash_uniform",
     "imgconv_shortcut", "dense_head", "wgrad_flush", "wgrad_pending", "wgrad_discard", "conv1_wgrad_pooled_f32",
-    "head_xent_f32", "gan_disc_head", "gan_head_ws_floats",
+    "head_xent_f32", "gan_disc_head", "gan_head_ws_floats", "apply_wait_next", "epoch_signal",
 ]
 
 _TILES = [(1, 128, 128), (2, 128, 64), (3, 64, 128), (0, 64, 64)]
@@ -808,6 +808,18 @@ def gan_loss(d_real, d_fake, gen_loss, disc_loss, dz_real_disc, dz_fake_disc, dz
     dz_real_disc.view(-1).copy_(-(1 - pr) / B)
     dz_fake_disc.view(-1).copy_(pf / B)
     dz_fake_gen.view(-1).copy_(-(1 - pf) / B)
+
+
+def apply_wait_next(done, seen, segs: int):
+    """The next apply_gradients launch's items of the var-list segments in bit mask ``segs`` wait (on the
+    device) until ``done`` exceeds ``seen`` - a gradient produced on another stream that signals with
+    epoch_signal(done) instead of a stream join; the launch's last workgroup advances ``seen``."""
+    require().apply_wait_next(done, seen, int(segs))
+
+
+def epoch_signal(ctr):
+    """ctr += 1 on the current stream (after the producer a later apply_wait_next consumer waits for)."""
+    require().epoch_signal(ctr)
 
 
 def gan_head_ws_floats(B: int, DH: int) -> int:

@@ -75,13 +75,22 @@ class MultiStepGraph:
     exactly n of them: whole S-step replays, then single-step replays for the remainder."""
 
     def __init__(self, fn, steps: int = 1, warmup: int = 2, enabled: bool = True,
-                 capture_error_mode: str = "global"):
+                 capture_error_mode: str = "global", finish=None):
+        """``finish``: called after the last step of every replay (and of every eager block) - e.g. the
+        CNN trainer's join_side(), which rejoins a side stream once per replay instead of once per step."""
         self.steps = max(1, int(steps))
-        self.one = StepGraph(fn, warmup=warmup, enabled=enabled, capture_error_mode=capture_error_mode)
+
+        def one():
+            fn()
+            if finish is not None:
+                finish()
+        self.one = StepGraph(one, warmup=warmup, enabled=enabled, capture_error_mode=capture_error_mode)
 
         def many():
             for _ in range(self.steps):
                 fn()
+            if finish is not None:
+                finish()
         self.many = (StepGraph(many, warmup=1, enabled=enabled, capture_error_mode=capture_error_mode)
                      if self.steps > 1 else None)
 

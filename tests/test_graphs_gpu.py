@@ -43,3 +43,23 @@ def test_multistep_cnn_steps_match_single_step_replays():
         out.append((tr.P.master.clone(), int(tr.global_step.item())))
     assert out[0][1] == out[1][1] == 8
     assert torch.equal(out[0][0], out[1][0])
+
+
+def test_deferred_join_cnn_matches_joined_steps():
+    """MnistCnnTrainer.defer_join (bench.py, several steps per replay): the conv2 weight-gradient branch
+    signals Adam through a device counter and rejoins once per replay - 8 steps as two 4-step replays give
+    the joined-every-step parameters bitwise, eagerly and replayed."""
+    from dtfe.models.mnist_cnn import MnistCnnTrainer
+    out = []
+    for defer, graph in ((False, True), (True, True), (True, False)):
+        tr = MnistCnnTrainer(256, "cuda:0", seed=0)
+        tr.defer_join = defer
+        g = MultiStepGraph(tr.step, 4, warmup=2, enabled=graph, finish=tr.join_side)
+        g.run(8)  # (graph: the first 4-step block eager, the second captured and replayed)
+        torch.cuda.synchronize()
+        out.append((tr.P.master.clone(), int(tr.global_step.item()), int(tr.c2_done.item()), int(tr.c2_seen.item())))
+    ref = out[0]
+    for m, gs, done, seen in out[1:]:
+        assert torch.equal(m, ref[0])
+        assert done == seen == gs  # one signal and one consume per step
+    assert ref[2] == ref[3] == 0
